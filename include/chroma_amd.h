@@ -1,0 +1,219 @@
+/* chroma_amd.h -- C ABI of the MI355X-native Chroma propagator (libchroma_amd.so).
+ *
+ * Every entry point replaces one thing the reference binds through PyCUDA
+ * (a JIT-compiled `extern "C" __global__` kernel launched from Python, or a
+ * make_gpu_struct() upload).  The "replaces" line on each declaration cites the
+ * reference interface (paths relative to youngsm/chroma-lite).
+ *
+ * Conventions
+ *  - plain C types only; no torch / HIP types in the signatures.  `stream` is a
+ *    hipStream_t passed as void* (NULL = default stream).
+ *  - pointers named d_* are DEVICE pointers (e.g. torch.Tensor.data_ptr()),
+ *    pointers named h_* are host pointers.
+ *  - photon vectors (pos/dir/pol) are float3-packed: 3 floats per photon,
+ *    exactly the reference's ga.vec.float3 arrays (chroma/gpu/photon.py:46-48).
+ *  - every function returns 0 on success or a nonzero chr_status; the message
+ *    of the last failure on the calling thread is chr_last_error().
+ *  - all launches are asynchronous on `stream` unless documented otherwise;
+ *    functions that return a count to the host synchronise the stream.
+ */
+#ifndef CHROMA_AMD_H
+#define CHROMA_AMD_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum chr_status {
+    CHR_OK = 0,
+    CHR_ERR_INVALID = 1,     /* bad argument (reference: ValueError / assert) */
+    CHR_ERR_HIP = 2,         /* HIP runtime error (reference: pycuda LogicError/LaunchError) */
+    CHR_ERR_NOMEM = 3,
+    CHR_ERR_STACK = 4        /* BVH stack overflow (reference: printf in mesh.h:111-114) */
+};
+
+/* photon history bits as stored on the device (reference photon.h:53-68).
+ * NOTE the reference keeps history in an unsigned short on the device, so
+ * NAN_ABORT is bit 15 there (and any propagate clears bits 16..31). */
+enum chr_history {
+    CHR_NO_HIT = 1u << 0, CHR_BULK_ABSORB = 1u << 1, CHR_SURFACE_DETECT = 1u << 2,
+    CHR_SURFACE_ABSORB = 1u << 3, CHR_RAYLEIGH_SCATTER = 1u << 4, CHR_REFLECT_DIFFUSE = 1u << 5,
+    CHR_REFLECT_SPECULAR = 1u << 6, CHR_SURFACE_REEMIT = 1u << 7, CHR_SURFACE_TRANSMIT = 1u << 8,
+    CHR_BULK_REEMIT = 1u << 9, CHR_CHERENKOV = 1u << 10, CHR_SCINTILLATION = 1u << 11,
+    CHR_NAN_ABORT = 1u << 15
+};
+
+/* surface models (reference geometry_types.h:22) */
+enum chr_surface_model { CHR_SURFACE_DEFAULT = 0, CHR_SURFACE_COMPLEX = 1, CHR_SURFACE_WLS = 2,
+                         CHR_SURFACE_DICHROIC = 3, CHR_SURFACE_ANGULAR = 4 };
+
+/* ---------------------------------------------------------------- geometry
+ * Host-side description of a flattened, BVH-indexed geometry.  All tables are
+ * sampled on one wavelength grid (wavelength_start + i*wavelength_step,
+ * i < wavelength_n) and one time grid, as GPUGeometry does
+ * (chroma/gpu/geometry.py:44-107).  EVERY table pointer must address n+1
+ * floats: the last element duplicates element n-1 (the reference's
+ * interp_property reads fp[n] at x == last grid point, geometry.h:61-74).
+ */
+typedef struct chr_material_desc {         /* reference struct Material, geometry_types.h:4-20 */
+    uint32_t num_comp;
+    const float *refractive_index;          /* [wavelength_n+1] */
+    const float *absorption_length;
+    const float *scattering_length;
+    const float *comp_reemission_prob;      /* [num_comp][wavelength_n+1] */
+    const float *comp_reemission_wvl_cdf;   /* [num_comp][wavelength_n+1] */
+    const float *comp_reemission_time_cdf;  /* [num_comp][time_n+1] */
+    const float *comp_absorption_length;    /* [num_comp][wavelength_n+1] */
+} chr_material_desc;
+
+typedef struct chr_surface_desc {          /* reference struct Surface, geometry_types.h:60-79 */
+    int32_t present;                        /* 0: NULL slot (the `None` surface) */
+    uint32_t model;                         /* chr_surface_model */
+    uint32_t transmissive;
+    float thickness;
+    const float *detect, *absorb, *reemit, *reflect_diffuse, *reflect_specular,
+                *eta, *k, *reemission_cdf;  /* [wavelength_n+1] each */
+    uint32_t dichroic_nangles;              /* 0: no DichroicProps */
+    const float *dichroic_angles;           /* [nangles] */
+    const float *dichroic_reflect;          /* [nangles][wavelength_n+1] */
+    const float *dichroic_transmit;         /* [nangles][wavelength_n+1] */
+    uint32_t angular_nangles;               /* 0: no AngularProps */
+    const float *angular_angles, *angular_transmit, *angular_reflect_specular,
+                *angular_reflect_diffuse;   /* [nangles] */
+} chr_surface_desc;
+
+typedef struct chr_wireplane_desc {        /* reference struct WirePlane, geometry_types.h:42-58 */
+    float origin[3], u[3], v[3];
+    float pitch, radius, umin, umax, vmin, vmax, v0;
+    int32_t surface_index, material_outer_index, material_inner_index;
+    uint32_t color;
+} chr_wireplane_desc;
+
+typedef struct chr_geometry_desc {         /* reference struct Geometry, geometry_types.h:124-139 */
+    uint32_t nvertices, ntriangles, nnodes;
+    uint32_t nmaterials, nsurfaces, nwireplanes;
+    const float *h_vertices;                /* [nvertices*3] */
+    const uint32_t *h_triangles;            /* [ntriangles*3] */
+    const uint32_t *h_material_codes;       /* [ntriangles]: m1<<24 | m2<<16 | surf<<8 (gpu/geometry.py:401-404) */
+    const uint32_t *h_nodes;                /* [nnodes*4] packed uint4 BVH nodes (bvh/bvh.py:106-195) */
+    float world_origin[3];
+    float world_scale;
+    uint32_t wavelength_n; float wavelength_start, wavelength_step;
+    uint32_t time_n; float time_start, time_step;
+    const chr_material_desc *materials;
+    const chr_surface_desc *surfaces;
+    const chr_wireplane_desc *wireplanes;
+} chr_geometry_desc;
+
+typedef struct chr_geometry chr_geometry;  /* opaque device-resident geometry */
+
+/* replaces: GPUGeometry.__init__ device uploads (chroma/gpu/geometry.py:14-526).
+ * Copies everything to HBM of the current device, builds the traversal layout.
+ * Synchronous. */
+int chr_geometry_create(const chr_geometry_desc *desc, chr_geometry **out);
+int chr_geometry_destroy(chr_geometry *g);
+/* bytes of HBM held by the geometry (reference: GPUGeometry.device_usage_str) */
+int chr_geometry_device_bytes(const chr_geometry *g, uint64_t *bytes);
+
+/* ----------------------------------------------------------------- photons */
+typedef struct chr_photons {               /* reference GPUPhotons arrays, photon.py:46-62 */
+    float *d_pos, *d_dir, *d_pol;          /* float3-packed [n*3] */
+    float *d_wavelengths, *d_t, *d_weights;
+    uint32_t *d_flags;
+    int32_t *d_last_hit_triangles;
+    uint32_t *d_evidx;
+} chr_photons;
+
+/* ---------------------------------------------------------------- random */
+/* RNG slot states: 6 x u32 per slot, SoA (word k of slot s at d_states[k*nslots+s]).
+ * replaces: get_rng_states / init_rng (chroma/gpu/tools.py:117-145):
+ * curand_init(seed, subsequence = slot, offset) for every slot. */
+int chr_init_rng(uint32_t *d_states, uint32_t nslots, uint64_t seed, uint64_t offset, void *stream);
+/* copy slot states to the host (tests; 6*nslots words, SoA) */
+int chr_rng_download(const uint32_t *d_states, uint32_t nslots, uint32_t *h_out, void *stream);
+
+/* -------------------------------------------------------------- propagate */
+/* replaces: the `propagate` kernel (chroma/cuda/propagate.cu:254-366), one
+ * chunk launch: slots [0, nthreads), photon = d_input_queue[first_photon + slot].
+ * Survivors are appended to d_output_queue in input order (stable; the
+ * reference's warp-atomic order is nondeterministic) and d_output_queue[0]
+ * counts them (+1, photon.py:248-250).  d_scratch must hold
+ * chr_propagate_scratch_words(nthreads) u32 words. */
+uint64_t chr_propagate_scratch_words(uint32_t nthreads);
+int chr_propagate_chunk(const chr_geometry *g, const chr_photons *ph, uint32_t *d_rng_states,
+                        uint32_t rng_nslots, int32_t first_photon, int32_t nthreads,
+                        const uint32_t *d_input_queue, uint32_t *d_output_queue,
+                        int32_t max_steps, int32_t use_weights, int32_t scatter_first,
+                        uint32_t *d_scratch, void *stream);
+
+typedef struct chr_propagate_stats {
+    uint32_t steps_run;         /* host-loop steps executed */
+    uint32_t launches;          /* chunk launches */
+    uint32_t final_alive;       /* photons still in the queue at exit */
+    uint32_t stack_overflows;   /* traversals that exceeded the 1000-entry stack */
+} chr_propagate_stats;
+
+/* replaces: GPUPhotons.propagate host loop (chroma/gpu/photon.py:226-293) for
+ * track=False: queue setup (clones interleaved, 242-250), the nsteps policy
+ * (261-264), chunk_iterator chunking (tools.py:159-180), queue swap and the
+ * per-step survivor count (277-286).  Synchronous. */
+int chr_propagate(const chr_geometry *g, const chr_photons *ph, uint32_t nphotons,
+                  uint32_t true_nphotons, uint32_t ncopies,
+                  uint32_t *d_rng_states, uint32_t rng_nslots,
+                  int32_t nthreads_per_block, int32_t max_blocks, int32_t max_steps,
+                  int32_t use_weights, int32_t scatter_first,
+                  chr_propagate_stats *stats, void *stream);
+
+/* ------------------------------------------------------------ selection */
+/* replaces: count_photon_hits + copy_photon_hits (propagate.cu:172-251),
+ * driven by GPUPhotons.get_flat_hits (photon.py:141-209).  Hits are compacted
+ * in ascending photon order.  Pass d_out.* = NULL to only count.  *nhits is
+ * written on the host (synchronises). */
+int chr_photon_hits(const chr_photons *ph, int32_t start_photon, int32_t nphotons,
+                    uint32_t detection_state, const uint32_t *d_solid_map,
+                    const int32_t *d_solid_id_to_channel_index,
+                    const chr_photons *d_out, int32_t *d_out_channels,
+                    uint32_t *nhits, void *stream);
+/* replaces: count_photons + copy_photons (propagate.cu:70-139) = GPUPhotons.select */
+int chr_select_photons(const chr_photons *ph, int32_t start_photon, int32_t nphotons,
+                       uint32_t target_flag, const chr_photons *d_out, uint32_t *nselected,
+                       void *stream);
+/* replaces: copy_photon_queue (propagate.cu:141-169): out[i] = in[queue[i]], i in [first, first+n) */
+int chr_copy_photon_queue(const chr_photons *ph, int32_t first_photon, int32_t nphotons,
+                          const uint32_t *d_queue, const chr_photons *d_out, void *stream);
+/* replaces: photon_duplicate (propagate.cu:29-68): copy photon i to i + stride*c, c=1..copies.
+ * evidx must be allocated nphotons*(copies+1) (the reference allocates only n: photon.py:62). */
+int chr_photon_duplicate(const chr_photons *ph, int32_t first_photon, int32_t nphotons,
+                         int32_t copies, int32_t stride, void *stream);
+
+/* replaces: distance_to_mesh test kernel (chroma/cuda/mesh.h:131-159).
+ * d_distance[i] is written only when ray i hits (reference semantics). */
+int chr_distance_to_mesh(const chr_geometry *g, uint32_t n, const float *d_origin,
+                         const float *d_direction, float *d_distance, void *stream);
+
+/* ------------------------------------------------------------- BVH build */
+/* replaces: make_recursive_grid_bvh (chroma/bvh/grid.py:11-95) with its GPU
+ * helpers create_leaf_nodes/make_leaves, merge_nodes_detailed/make_parents_detailed,
+ * concatenate_layers/copy_and_offset and collapse_chains/collapse_child
+ * (chroma/gpu/bvh.py:18-130, chroma/cuda/bvh.cu:148-384,530-543), on the host.
+ * Leaves with equal Morton codes keep triangle order (stable sort; the
+ * reference's numpy quicksort is unstable).  Two-phase: call with h_nodes=NULL
+ * to get *nnodes and *nlayers, then again with buffers of that size. */
+int chr_bvh_build_grid(const float *h_vertices, uint32_t nvertices,
+                       const uint32_t *h_triangles, uint32_t ntriangles,
+                       int32_t target_degree, float *world_origin /*[3] out*/,
+                       float *world_scale /*out*/, uint32_t *h_nodes /*[nnodes*4] out*/,
+                       uint32_t *h_layer_offsets /*[nlayers] out*/,
+                       uint32_t *nnodes, uint32_t *nlayers);
+
+/* ------------------------------------------------------------- misc */
+const char *chr_last_error(void);
+int chr_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CHROMA_AMD_H */

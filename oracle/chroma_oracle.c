@@ -1,0 +1,1126 @@
+/* chroma_oracle.c -- TEST INFRASTRUCTURE ONLY.
+ *
+ * CPU restatement of the reference photon propagator (youngsm/chroma-lite),
+ * used as the parity checker for the HIP path.  Only tests/, the
+ * __graft_entry__.smoke() check and bench.py's cpu_baseline leg may load it.
+ * The product (chroma-lite_amd/) never links or calls it.
+ *
+ * It follows the reference sources function by function (file:line on each),
+ * written as plain sequential C: the BVH walk keeps the reference's DFS order
+ * and 1000-entry stack, the photon loop keeps the exact random-number draw
+ * order, and the host queue loop is chroma/gpu/photon.py:226-293 with a STABLE
+ * survivor compaction (the reference's warp-atomic enqueue order is
+ * nondeterministic; input order is one of its possible outcomes).
+ *
+ * Floating point: the reference is compiled with --use_fast_math, so its
+ * transcendental bits are not reproducible; this oracle and the HIP kernels
+ * share the portable math of include/chroma_fmath.h and the cuRAND-XORWOW
+ * restatement of include/chroma_rng.h (the two "platform" substitutes), and
+ * spell every multiply-add that nvcc would contract as an explicit fmaf.
+ * Compiled with -ffp-contract=off.
+ *
+ * Parity status: pinned against the reference's own fixtures where they exist
+ * (test/data/ray_intersection.npy for intersect_mesh, the test_bvh.py packing
+ * KAT for the node layout, the statistical tests of test_rayleigh.py /
+ * test_sample_cdf.py); per-photon propagate outputs of the CUDA reference
+ * cannot be produced here (no GPU/nvcc/pycuda), so per-photon parity vs the
+ * reference binary is unpinned (DESIGN.md section "Oracle").
+ */
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#include <math.h>
+
+#include "../include/chroma_amd.h"
+#include "../include/chroma_fmath.h"
+#include "../include/chroma_rng.h"
+
+#define EXPORT __attribute__((visibility("default")))
+
+/* ------------------------------------------------ linalg.h:4-174 */
+typedef struct { float x, y, z; } f3;
+static inline f3 mk(float x, float y, float z) { f3 r = {x, y, z}; return r; }
+static inline f3 add(f3 a, f3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
+static inline f3 sub(f3 a, f3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
+static inline f3 neg(f3 a) { return mk(-a.x, -a.y, -a.z); }
+static inline f3 mulf(f3 a, float c) { return mk(a.x * c, a.y * c, a.z * c); }
+static inline f3 divf(f3 a, float c) { return mk(a.x / c, a.y / c, a.z / c); }
+/* a.x*b.x + a.y*b.y + a.z*b.z, contracted left to right */
+static inline float dot(f3 a, f3 b) { return fmaf(a.z, b.z, fmaf(a.y, b.y, a.x * b.x)); }
+static inline f3 cross(f3 a, f3 b) {
+    return mk(fmaf(a.y, b.z, -(a.z * b.y)), fmaf(a.z, b.x, -(a.x * b.z)), fmaf(a.x, b.y, -(a.y * b.x)));
+}
+static inline float norm(f3 a) { return chr_sqrtf(dot(a, a)); }
+static inline f3 normalize(f3 a) { return divf(a, norm(a)); }
+/* p + d*v */
+static inline f3 axpy(float d, f3 v, f3 p) { return mk(fmaf(d, v.x, p.x), fmaf(d, v.y, p.y), fmaf(d, v.z, p.z)); }
+static inline float fmin_(float a, float b) { if (chr_isnan(a)) return b; if (chr_isnan(b)) return a; return a < b ? a : b; }
+static inline float fmax_(float a, float b) { if (chr_isnan(a)) return b; if (chr_isnan(b)) return a; return a > b ? a : b; }
+
+/* rotate.h:21-28 */
+static f3 rotate(f3 a, float phi, f3 n) {
+    float s, c;
+    chr_sincosf(phi, &s, &c);
+    float d = dot(a, n);
+    float omc = 1.0f - c;
+    f3 cr = cross(a, n);
+    return mk(fmaf(cr.x, s, fmaf(n.x * d, omc, a.x * c)),
+              fmaf(cr.y, s, fmaf(n.y * d, omc, a.y * c)),
+              fmaf(cr.z, s, fmaf(n.z * d, omc, a.z * c)));
+}
+
+/* ------------------------------------------------ photon / state (photon.h:19-51) */
+typedef struct {
+    f3 pos, dir, pol;
+    float wavelength, time, weight;
+    uint16_t history;            /* unsigned short on the device, photon.h:29 */
+    int32_t last_hit_triangle;
+    uint32_t evidx;
+} Photon;
+
+typedef struct {
+    int inside_to_outside;
+    f3 surface_normal;
+    float n1, n2, absorption_length, scattering_length;
+    int material1;
+    int surface_index;
+    float distance_to_boundary;
+} State;
+
+enum { BREAK = 0, CONTINUE = 1, PASS = 2 };
+#define DEAD_MASK (CHR_NO_HIT | CHR_BULK_ABSORB | CHR_SURFACE_DETECT | CHR_SURFACE_ABSORB | CHR_NAN_ABORT)
+#define WEIGHT_LOWER_THRESHOLD 0.0001f
+#define SPEED_OF_LIGHT 299.792458f
+#define PI_F 3.141592653589793f
+
+/* oracle-side geometry view */
+typedef struct {
+    const chr_geometry_desc *d;
+    uint64_t nodes_visited, tris_tested;   /* instrumentation (bytes/photon) */
+    uint32_t max_depth, overflows;
+} Geo;
+
+/* ------------------------------------------------ geometry.h:30-74 */
+typedef struct { f3 lower, upper; uint32_t child, nchild; } Node;
+
+static Node get_node(const Geo *g, uint32_t i) {
+    const uint32_t *n = g->d->h_nodes + 4u * (size_t)i;
+    Node r;
+    f3 o = mk(g->d->world_origin[0], g->d->world_origin[1], g->d->world_origin[2]);
+    float s = g->d->world_scale;
+    /* world_origin + to_float3(q) * world_scale, contracted */
+    r.lower = mk(fmaf((float)(n[0] & 0xFFFFu), s, o.x), fmaf((float)(n[1] & 0xFFFFu), s, o.y),
+                 fmaf((float)(n[2] & 0xFFFFu), s, o.z));
+    r.upper = mk(fmaf((float)(n[0] >> 16), s, o.x), fmaf((float)(n[1] >> 16), s, o.y),
+                 fmaf((float)(n[2] >> 16), s, o.z));
+    r.child = n[3] & ~(0xFFFFu << 28);
+    r.nchild = n[3] >> 28;
+    return r;
+}
+
+static void get_triangle(const Geo *g, uint32_t i, f3 *v0, f3 *v1, f3 *v2) {
+    const uint32_t *t = g->d->h_triangles + 3u * (size_t)i;
+    const float *v = g->d->h_vertices;
+    *v0 = mk(v[3 * t[0]], v[3 * t[0] + 1], v[3 * t[0] + 2]);
+    *v1 = mk(v[3 * t[1]], v[3 * t[1] + 1], v[3 * t[1] + 2]);
+    *v2 = mk(v[3 * t[2]], v[3 * t[2] + 1], v[3 * t[2] + 2]);
+}
+
+static float interp_property(const Geo *g, float x, const float *fp) {
+    const chr_geometry_desc *d = g->d;
+    float start = d->wavelength_start, step = d->wavelength_step;
+    int n = (int)d->wavelength_n;
+    if (x < start) return fp[0];
+    if (x > fmaf((float)(n - 1), step, start)) return fp[n - 1];
+    int jl = (int)((x - start) / step);
+    float base = fmaf((float)jl, step, start);
+    return fp[jl] + ((x - base) * (fp[jl + 1] - fp[jl])) / step;
+}
+
+/* interpolate.h:4-29 (computed in double as the reference's 1.0* literal does) */
+static float interp_idx(float x, int n, const float *xp) {
+    int lower = 0, upper = n - 1;
+    if (x <= xp[lower]) return (float)lower;
+    if (x >= xp[upper]) return (float)upper;
+    while (lower < upper - 1) {
+        int half = (lower + upper) / 2;
+        if (x < xp[half]) upper = half; else lower = half;
+    }
+    float dx = xp[upper] - xp[lower];
+    return (float)((double)lower + (double)(x - xp[lower]) / (double)dx);
+}
+
+/* random.h:15-23 */
+static f3 uniform_sphere(chr_xorwow *s) {
+    float theta = chr_uniform(s, 0.0f, 2 * PI_F);
+    float u = chr_uniform(s, -1.0f, 1.0f);
+    float c = chr_sqrtf(fmaf(-u, u, 1.0f));
+    float st, ct;
+    chr_sincosf(theta, &st, &ct);
+    return mk(c * ct, c * st, u);
+}
+
+/* random.h:27-55 (uniformly sampled CDF) */
+static float sample_cdf(chr_xorwow *rng, int ncdf, float x0, float delta, const float *cdf_y) {
+    float u = chr_uniform01(rng);
+    int lower = 0, upper = ncdf - 1;
+    while (lower < upper - 1) {
+        int half = (lower + upper) / 2;
+        if (u < cdf_y[half]) upper = half; else lower = half;
+    }
+    float dcy = cdf_y[upper] - cdf_y[lower];
+    return fmaf(delta, (float)lower, x0) + (delta * (u - cdf_y[lower])) / dcy;
+}
+
+/* ------------------------------------------------ intersect.h:26-157 */
+/* thresholds equivalent to the reference's float-vs-double comparisons:
+ *   (double)u < -1e-6   <=>  u < -9.99999997e-07f (float nearest above -1e-6)
+ *   (double)u > 1+1e-6  <=>  u > 1.00000095f, etc.; computed at init */
+static float T_NEG_EPS, T_ONE_EPS, T_POS_EPS;
+
+static void init_thresholds(void) {
+    /* smallest float >= -1e-6 */
+    float a = (float)-1e-6; if ((double)a < -1e-6) a = nextafterf(a, 1.0f); T_NEG_EPS = a;
+    /* largest float <= 1+1e-6 */
+    float b = (float)(1.0 + 1e-6); if ((double)b > 1.0 + 1e-6) b = nextafterf(b, 0.0f); T_ONE_EPS = b;
+    /* largest float <= 1e-6 */
+    float c = (float)1e-6; if ((double)c > 1e-6) c = nextafterf(c, 0.0f); T_POS_EPS = c;
+}
+
+static int intersect_triangle(f3 origin, f3 direction, f3 v0, f3 v1, f3 v2, float *distance) {
+    f3 edge1 = sub(v1, v0), edge2 = sub(v2, v0);
+    f3 h = cross(direction, edge2);
+    float a = dot(edge1, h);
+    if (a > -1.19209290e-7f && a < 1.19209290e-7f) return 0;   /* FLT_EPSILON */
+    float f = 1.0f / a;          /* == (float)(1.0/(double)a): double rounding is innocuous */
+    f3 s = sub(origin, v0);
+    float u = f * dot(s, h);
+    if (u < T_NEG_EPS || u > T_ONE_EPS) return 0;
+    f3 q = cross(s, edge1);
+    float v = f * dot(direction, q);
+    if (v < T_NEG_EPS || u + v > T_ONE_EPS) return 0;
+    float t = f * dot(edge2, q);
+    if (t > T_POS_EPS && t < INFINITY) { *distance = t; return 1; }
+    return 0;
+}
+
+static int intersect_box(f3 noid, f3 inv, f3 lo, f3 hi, float *dist) {
+    float tmin = 0.0f, tmax = INFINITY, t0, t1;
+    if (chr_isfinite(inv.x)) {
+        t0 = fmaf(lo.x, inv.x, noid.x); t1 = fmaf(hi.x, inv.x, noid.x);
+        tmin = fmax_(tmin, fmin_(t0, t1)); tmax = fmin_(tmax, fmax_(t0, t1));
+    }
+    if (chr_isfinite(inv.y)) {
+        t0 = fmaf(lo.y, inv.y, noid.y); t1 = fmaf(hi.y, inv.y, noid.y);
+        tmin = fmax_(tmin, fmin_(t0, t1)); tmax = fmin_(tmax, fmax_(t0, t1));
+    }
+    if (chr_isfinite(inv.z)) {
+        t0 = fmaf(lo.z, inv.z, noid.z); t1 = fmaf(hi.z, inv.z, noid.z);
+        tmin = fmax_(tmin, fmin_(t0, t1)); tmax = fmin_(tmax, fmax_(t0, t1));
+    }
+    if (tmin > tmax) return 0;
+    *dist = tmin;
+    return 1;
+}
+
+/* mesh.h:16-38 */
+static int intersect_node(f3 noid, f3 inv, const Node *node, float min_distance) {
+    float d;
+    if (!intersect_box(noid, inv, node->lower, node->upper, &d)) return 0;
+    if (min_distance < 0.0f) return 1;
+    if (d > min_distance) return 0;
+    return 1;
+}
+
+#define STACK_SIZE 1000
+/* mesh.h:45-126: DFS over groups; within a group ascending child index; an
+ * internal child's group is pushed, the last pushed group is popped first;
+ * nearest hit by strict '<'.  On stack overflow the reference writes past its
+ * 1000-entry array (UB); here the walk stops and reports it. */
+static int intersect_mesh(Geo *g, f3 origin, f3 direction, float *min_distance, int last_hit_triangle) {
+    int triangle_index = -1;
+    float distance;
+    *min_distance = -1.0f;
+    Node root = get_node(g, 0);
+    f3 noid = mk(-origin.x / direction.x, -origin.y / direction.y, -origin.z / direction.z);
+    f3 inv = mk(1.0f / direction.x, 1.0f / direction.y, 1.0f / direction.z);
+    g->nodes_visited++;
+    if (!intersect_node(noid, inv, &root, *min_distance)) return -1;
+    uint32_t child_stack[STACK_SIZE], nchild_stack[STACK_SIZE];
+    child_stack[0] = root.child; nchild_stack[0] = root.nchild;
+    int curr = 0;
+    uint32_t depth_max = 1;
+    while (curr >= 0) {
+        uint32_t first_child = child_stack[curr], nchild = nchild_stack[curr];
+        curr--;
+        for (uint32_t i = first_child; i < first_child + nchild; i++) {
+            Node node = get_node(g, i);
+            g->nodes_visited++;
+            if (intersect_node(noid, inv, &node, *min_distance)) {
+                if (node.nchild == 0) {
+                    if (node.child != (uint32_t)last_hit_triangle) {
+                        f3 v0, v1, v2;
+                        g->tris_tested++;
+                        get_triangle(g, node.child, &v0, &v1, &v2);
+                        if (intersect_triangle(origin, direction, v0, v1, v2, &distance)) {
+                            if (triangle_index == -1 || distance < *min_distance) {
+                                triangle_index = (int)node.child;
+                                *min_distance = distance;
+                            }
+                        }
+                    }
+                } else {
+                    if (curr + 1 >= STACK_SIZE) { g->overflows++; goto done; }
+                    curr++;
+                    child_stack[curr] = node.child;
+                    nchild_stack[curr] = node.nchild;
+                    if ((uint32_t)curr + 1 > depth_max) depth_max = (uint32_t)curr + 1;
+                }
+            }
+        }
+    }
+done:
+    if (depth_max > g->max_depth) g->max_depth = depth_max;
+    return triangle_index;
+}
+
+/* ------------------------------------------------ photon.h:72-397 */
+static int convert(int c) { return (c & 0x80) ? (int)(0xFFFFFF00u | (uint32_t)c) : c; }
+
+static float get_theta(f3 a, f3 b) { return chr_acosf(fmax_(-1.0f, fmin_(1.0f, dot(a, b)))); }
+
+static const chr_material_desc *MAT(const Geo *g, int i) { return &g->d->materials[i]; }
+
+/* analytic wire planes, photon.h:108-270 (FP64) */
+static void wireplanes(const Geo *g, const Photon *p, float best_distance, int *a_surface, int *a_inner,
+                       int *a_outer, f3 *a_normal_raw, float *a_dot_raw, int *a_plane, float *a_distance) {
+    const chr_geometry_desc *d = g->d;
+    for (int ip = 0; ip < (int)d->nwireplanes; ++ip) {
+        const chr_wireplane_desc *wp = &d->wireplanes[ip];
+        const double ux = wp->u[0], uy = wp->u[1], uz = wp->u[2];
+        const double vx0 = wp->v[0], vy0 = wp->v[1], vz0 = wp->v[2];
+        const double un = 1.0 / sqrt(ux * ux + uy * uy + uz * uz);
+        const double ux1 = ux * un, uy1 = uy * un, uz1 = uz * un;
+        const double vdotu = vx0 * ux1 + vy0 * uy1 + vz0 * uz1;
+        const double vx1 = vx0 - vdotu * ux1, vy1 = vy0 - vdotu * uy1, vz1 = vz0 - vdotu * uz1;
+        const double vn = 1.0 / sqrt(vx1 * vx1 + vy1 * vy1 + vz1 * vz1);
+        const double vx = vx1 * vn, vy = vy1 * vn, vz = vz1 * vn;
+        const double nx = uy1 * vz - uz1 * vy, ny = uz1 * vx - ux1 * vz, nz = ux1 * vy - uy1 * vx;
+        f3 w = sub(p->pos, mk(wp->origin[0], wp->origin[1], wp->origin[2]));
+        double du = (double)p->dir.x * ux1 + (double)p->dir.y * uy1 + (double)p->dir.z * uz1;
+        double dv = (double)p->dir.x * vx + (double)p->dir.y * vy + (double)p->dir.z * vz;
+        double dn = (double)p->dir.x * nx + (double)p->dir.y * ny + (double)p->dir.z * nz;
+        double wu = (double)w.x * ux1 + (double)w.y * uy1 + (double)w.z * uz1;
+        double wv0 = (double)w.x * vx + (double)w.y * vy + (double)w.z * vz - (double)wp->v0;
+        double wn0 = (double)w.x * nx + (double)w.y * ny + (double)w.z * nz;
+        double t_in = -1.0e300, t_out = 1.0e300;
+        if (fabs(du) < 1e-15) {
+            if (wu < (double)wp->umin || wu > (double)wp->umax) continue;
+        } else {
+            double t1 = ((double)wp->umin - wu) / du, t2 = ((double)wp->umax - wu) / du;
+            if (t1 > t2) { double tmp = t1; t1 = t2; t2 = tmp; }
+            if (t1 > t_in) t_in = t1;
+            if (t2 < t_out) t_out = t2;
+            if (t_in > t_out) continue;
+        }
+        const double pitch = (double)wp->pitch;
+        const double inv_pitch = (pitch != 0.0) ? (1.0 / pitch) : 0.0;
+        const double wire_radius = (double)wp->radius;
+        const double wire_thickness = 2.0 * wire_radius;
+        const double pad_v = 0.5 * wire_thickness + 1e-6, pad_n = 0.5 * wire_thickness + 1e-6;
+        int kmin = (int)ceil(((double)wp->vmin - (double)wp->v0) / pitch);
+        int kmax = (int)floor(((double)wp->vmax - (double)wp->v0) / pitch);
+        double A = dv * dv + dn * dn;
+        int k_start = kmin, k_stop = kmax;
+        if (kmin <= kmax) {
+            const double t_eps = 1.0e-4;
+            double t_lo = fmax(t_in, t_eps), t_hi = t_out;
+            double best_cap = (double)best_distance;
+            if (best_cap < t_hi) t_hi = best_cap;
+            if (fabs(dn) > 1e-12) {
+                double tn1 = (-pad_n - wn0) / dn, tn2 = (pad_n - wn0) / dn;
+                if (tn1 > tn2) { double tmp = tn1; tn1 = tn2; tn2 = tmp; }
+                t_lo = fmax(t_lo, tn1); t_hi = fmin(t_hi, tn2);
+            } else if (fabs(wn0) > pad_n) continue;
+            if (t_hi < t_lo) continue;
+            if (fabs(dn) <= 1e-12 && fabs(dv) > 1e-12) {
+                double t_span = (pitch + wire_thickness) / fabs(dv);
+                t_hi = fmin(t_hi, t_lo + t_span);
+            }
+            double v_entry = wv0 + dv * t_lo, v_exit = wv0 + dv * t_hi;
+            double v_lo = fmin(v_entry, v_exit) - pad_v, v_hi = fmax(v_entry, v_exit) + pad_v;
+            if (wv0 - pad_v < v_lo) v_lo = wv0 - pad_v;
+            if (wv0 + pad_v > v_hi) v_hi = wv0 + pad_v;
+            long long k_lo = (long long)floor(v_lo * inv_pitch), k_hi = (long long)ceil(v_hi * inv_pitch);
+            if (k_lo < kmin) k_lo = kmin;
+            if (k_hi > kmax) k_hi = kmax;
+            if (k_lo > k_hi) continue;
+            k_start = (int)k_lo; k_stop = (int)k_hi;
+        }
+        for (int k = k_start; k <= k_stop; ++k) {
+            double wv = wv0 - (double)k * pitch;
+            double B = wv * dv + wn0 * dn;
+            double C = wv * wv + wn0 * wn0 - wire_radius * wire_radius;
+            double disc = B * B - A * C;
+            if (disc < 0.0) continue;
+            double sq = sqrt(disc);
+            double t_small = (-B - sq) / A, t_large = (-B + sq) / A;
+            const double t_min = 1.0e-4;
+            const double r2_wire = wire_radius * wire_radius;
+            const double r2_0 = wv * wv + wn0 * wn0;
+            const double eps0 = fmax(1e-18, 1e-12 * r2_wire);
+            double t;
+            if (r2_0 > r2_wire + eps0) { if (t_small <= t_min) continue; t = t_small; }
+            else if (r2_0 < r2_wire - eps0) { if (t_large <= t_min) continue; t = t_large; }
+            else t = t_min;
+            double uc = wu + du * t;
+            if (uc < wp->umin || uc > wp->umax) continue;
+            if ((float)t >= *a_distance) continue;
+            if (t < t_in || t > t_out) continue;
+            double vn_hit = wv + dv * t, nn_hit = wn0 + dn * t;
+            double len = sqrt(vn_hit * vn_hit + nn_hit * nn_hit);
+            if (len <= 0.0) continue;
+            f3 nl = mk((float)((vn_hit / len) * vx + (nn_hit / len) * nx),
+                       (float)((vn_hit / len) * vy + (nn_hit / len) * ny),
+                       (float)((vn_hit / len) * vz + (nn_hit / len) * nz));
+            *a_distance = (float)t;
+            *a_surface = wp->surface_index;
+            *a_inner = wp->material_inner_index;
+            *a_outer = wp->material_outer_index;
+            *a_normal_raw = nl;
+            *a_dot_raw = dot(nl, neg(p->dir));
+            *a_plane = ip;
+        }
+    }
+}
+
+static void fill_state(Geo *g, State *s, Photon *p) {
+    int mesh_triangle = intersect_mesh(g, p->pos, p->dir, &s->distance_to_boundary, p->last_hit_triangle);
+    float best_distance = (mesh_triangle == -1) ? 1e30f : s->distance_to_boundary;
+    int a_surface = -1, a_inner = -1, a_outer = -1, a_plane = -1;
+    f3 a_normal_raw = mk(0, 0, 0);
+    float a_dot_raw = 0.0f, a_distance = 1e30f;
+    if (g->d->nwireplanes > 0 && g->d->wireplanes)
+        wireplanes(g, p, best_distance, &a_surface, &a_inner, &a_outer, &a_normal_raw, &a_dot_raw, &a_plane, &a_distance);
+    int use_analytic = 0;
+    if (a_surface >= 0) use_analytic = ((double)a_distance + 1e-12 < (double)best_distance);
+    int m1, m2;
+    if (use_analytic) {
+        s->distance_to_boundary = a_distance;
+        s->surface_index = a_surface;
+        p->last_hit_triangle = -2;
+        if (a_dot_raw > 0.0f) {
+            m1 = a_outer; m2 = a_inner; s->surface_normal = a_normal_raw; s->inside_to_outside = 0;
+        } else {
+            m1 = a_inner; m2 = a_outer; s->surface_normal = neg(a_normal_raw); s->inside_to_outside = 1;
+        }
+    } else if (mesh_triangle != -1) {
+        p->last_hit_triangle = mesh_triangle;
+        f3 v0, v1, v2;
+        get_triangle(g, (uint32_t)mesh_triangle, &v0, &v1, &v2);
+        uint32_t code = g->d->h_material_codes[mesh_triangle];
+        int inner = convert(0xFF & (int)(code >> 24));
+        int outer = convert(0xFF & (int)(code >> 16));
+        s->surface_index = convert(0xFF & (int)(code >> 8));
+        s->surface_normal = normalize(cross(sub(v1, v0), sub(v2, v1)));
+        if (dot(s->surface_normal, neg(p->dir)) > 0.0f) {
+            m1 = outer; m2 = inner; s->inside_to_outside = 0;
+        } else {
+            m1 = inner; m2 = outer; s->surface_normal = neg(s->surface_normal); s->inside_to_outside = 1;
+        }
+    } else {
+        p->last_hit_triangle = -1;
+        p->history |= CHR_NO_HIT;
+        return;
+    }
+    s->n1 = interp_property(g, p->wavelength, MAT(g, m1)->refractive_index);
+    s->n2 = interp_property(g, p->wavelength, MAT(g, m2)->refractive_index);
+    s->absorption_length = interp_property(g, p->wavelength, MAT(g, m1)->absorption_length);
+    s->scattering_length = interp_property(g, p->wavelength, MAT(g, m1)->scattering_length);
+    s->material1 = m1;
+}
+
+/* photon.h:399-427 */
+static f3 pick_new_direction(f3 axis, float theta, float phi) {
+    float st, ct, sp, cp;
+    chr_sincosf(theta, &st, &ct);
+    chr_sincosf(phi, &sp, &cp);
+    float sat = chr_sqrtf(fmaf(-axis.z, axis.z, 1.0f));
+    float cap, sap;
+    if (chr_isnan(sat) || sat < 0.00001f) { cap = 1.0f; sap = 0.0f; }
+    else { cap = axis.x / sat; sap = axis.y / sat; }
+    float dx = fmaf(st, fmaf(axis.z * cp, cap, -(sp * sap)), ct * axis.x);
+    float dy = fmaf(st, fmaf(cp * axis.z, sap, sp * cap), ct * axis.y);
+    float dz = fmaf(-(st * cp), sat, ct * axis.z);
+    return mk(dx, dy, dz);
+}
+
+/* photon.h:429-453 */
+static void rayleigh_scatter(Photon *p, chr_xorwow *rng) {
+    float u = chr_uniform01(rng);
+    float cos_theta = 2.0f * chr_cosf((chr_acosf(fmaf(-2.0f, u, 1.0f)) - 2 * PI_F) / 3.0f);
+    if (cos_theta > 1.0f) cos_theta = 1.0f;
+    else if (cos_theta < -1.0f) cos_theta = -1.0f;
+    float theta = chr_acosf(cos_theta);
+    float phi = chr_uniform(rng, 0.0f, 2.0f * PI_F);
+    p->dir = pick_new_direction(p->pol, theta, phi);
+    if (1.0f - chr_fabsf(cos_theta) < 1e-6f)
+        p->pol = pick_new_direction(p->pol, PI_F / 2.0f, phi);
+    else
+        p->pol = mk(fmaf(-cos_theta, p->dir.x, p->pol.x), fmaf(-cos_theta, p->dir.y, p->pol.y),
+                    fmaf(-cos_theta, p->dir.z, p->pol.z));
+    p->dir = divf(p->dir, norm(p->dir));
+    p->pol = divf(p->pol, norm(p->pol));
+}
+
+/* photon.h:455-570 */
+static int propagate_to_boundary(Geo *g, Photon *p, State *s, chr_xorwow *rng, int use_weights, int scatter_first) {
+    float absorption_distance = -s->absorption_length * chr_logf(chr_uniform01(rng));
+    float scattering_distance = -s->scattering_length * chr_logf(chr_uniform01(rng));
+    if (use_weights && p->weight > WEIGHT_LOWER_THRESHOLD) absorption_distance = 1e30f;
+    else use_weights = 0;
+    if (scatter_first == 1) {
+        float scatter_prob = 1.0f - chr_expf(-s->distance_to_boundary / s->scattering_length);
+        if (scatter_prob > WEIGHT_LOWER_THRESHOLD) {
+            int i = 0;
+            while (i < 1000 && scattering_distance > s->distance_to_boundary) {
+                scattering_distance = -s->scattering_length * chr_logf(chr_uniform01(rng));
+                i++;
+            }
+            p->weight *= scatter_prob;
+        }
+    } else if (scatter_first == -1) {
+        float no_scatter_prob = chr_expf(-s->distance_to_boundary / s->scattering_length);
+        if (no_scatter_prob > WEIGHT_LOWER_THRESHOLD) {
+            int i = 0;
+            while (i < 1000 && scattering_distance <= s->distance_to_boundary) {
+                scattering_distance = -s->scattering_length * chr_logf(chr_uniform01(rng));
+                i++;
+            }
+            p->weight *= no_scatter_prob;
+        }
+    }
+    if (absorption_distance <= scattering_distance) {
+        if (absorption_distance <= s->distance_to_boundary) {
+            p->time = p->time + absorption_distance / (SPEED_OF_LIGHT / s->n1);
+            p->pos = axpy(absorption_distance, p->dir, p->pos);
+            const chr_material_desc *m = MAT(g, s->material1);
+            if (m->num_comp == 0) {
+                p->last_hit_triangle = -1;
+                p->history |= CHR_BULK_ABSORB;
+                return BREAK;
+            }
+            int W1 = (int)g->d->wavelength_n + 1, T1 = (int)g->d->time_n + 1;
+            float usc = chr_uniform01(rng);
+            float prob = 0.0f;
+            uint32_t comp;
+            for (comp = 0;; comp++) {
+                float comp_abs = interp_property(g, p->wavelength, m->comp_absorption_length + comp * W1);
+                prob += s->absorption_length / comp_abs;
+                if (usc < prob || comp + 1 == m->num_comp) break;
+            }
+            float usr = chr_uniform01(rng);
+            float crp = interp_property(g, p->wavelength, m->comp_reemission_prob + comp * W1);
+            if (usr < crp) {
+                p->wavelength = sample_cdf(rng, (int)g->d->wavelength_n, g->d->wavelength_start,
+                                           g->d->wavelength_step, m->comp_reemission_wvl_cdf + comp * W1);
+                p->time += sample_cdf(rng, (int)g->d->time_n, g->d->time_start, g->d->time_step,
+                                      m->comp_reemission_time_cdf + comp * T1);
+                p->dir = uniform_sphere(rng);
+                p->pol = cross(uniform_sphere(rng), p->dir);
+                p->pol = divf(p->pol, norm(p->pol));
+                p->last_hit_triangle = -1;
+                p->history |= CHR_BULK_REEMIT;
+                return CONTINUE;
+            }
+            p->last_hit_triangle = -1;
+            p->history |= CHR_BULK_ABSORB;
+            return BREAK;
+        }
+    } else {
+        if (scattering_distance <= s->distance_to_boundary) {
+            if (use_weights) p->weight *= chr_expf(-scattering_distance / s->absorption_length);
+            p->time = p->time + scattering_distance / (SPEED_OF_LIGHT / s->n1);
+            p->pos = axpy(scattering_distance, p->dir, p->pos);
+            rayleigh_scatter(p, rng);
+            p->history |= CHR_RAYLEIGH_SCATTER;
+            p->last_hit_triangle = -1;
+            return CONTINUE;
+        }
+    }
+    if (use_weights) p->weight *= chr_expf(-s->distance_to_boundary / s->absorption_length);
+    p->pos = axpy(s->distance_to_boundary, p->dir, p->pos);
+    p->time = p->time + s->distance_to_boundary / (SPEED_OF_LIGHT / s->n1);
+    return PASS;
+}
+
+/* photon.h:572-632 */
+static void propagate_at_boundary(Photon *p, State *s, chr_xorwow *rng) {
+    float incident_angle = get_theta(s->surface_normal, neg(p->dir));
+    float refracted_angle = chr_asinf((chr_sinf(incident_angle) * s->n1) / s->n2);
+    f3 ipn = cross(p->dir, s->surface_normal);
+    float ipn_len = norm(ipn);
+    if (ipn_len < 1e-6f) ipn = p->pol; else ipn = divf(ipn, ipn_len);
+    float nc = dot(p->pol, ipn);
+    float normal_probability = nc * nc;
+    float rc;
+    if (chr_uniform01(rng) < normal_probability) {
+        rc = -chr_sinf(incident_angle - refracted_angle) / chr_sinf(incident_angle + refracted_angle);
+        if ((chr_uniform01(rng) < rc * rc) || chr_isnan(refracted_angle)) {
+            p->dir = rotate(s->surface_normal, incident_angle, ipn);
+            p->history |= CHR_REFLECT_SPECULAR;
+        } else {
+            p->dir = rotate(s->surface_normal, PI_F - refracted_angle, ipn);
+        }
+        p->pol = ipn;
+    } else {
+        rc = chr_tanf(incident_angle - refracted_angle) / chr_tanf(incident_angle + refracted_angle);
+        if ((chr_uniform01(rng) < rc * rc) || chr_isnan(refracted_angle)) {
+            p->dir = rotate(s->surface_normal, incident_angle, ipn);
+            p->history |= CHR_REFLECT_SPECULAR;
+        } else {
+            p->dir = rotate(s->surface_normal, PI_F - refracted_angle, ipn);
+        }
+        p->pol = cross(ipn, p->dir);
+        p->pol = divf(p->pol, norm(p->pol));
+    }
+}
+
+/* photon.h:634-667 */
+static int specular_reflector(Photon *p, State *s) {
+    float incident_angle = get_theta(s->surface_normal, neg(p->dir));
+    f3 ipn = cross(p->dir, s->surface_normal);
+    ipn = divf(ipn, norm(ipn));
+    p->dir = rotate(s->surface_normal, incident_angle, ipn);
+    p->history |= CHR_REFLECT_SPECULAR;
+    return CONTINUE;
+}
+
+static int diffuse_reflector(Photon *p, State *s, chr_xorwow *rng) {
+    float ndotv;
+    do {
+        p->dir = uniform_sphere(rng);
+        ndotv = dot(p->dir, s->surface_normal);
+        if (ndotv < 0.0f) { p->dir = neg(p->dir); ndotv = -ndotv; }
+    } while (!(chr_uniform01(rng) < ndotv));
+    p->pol = cross(uniform_sphere(rng), p->dir);
+    p->pol = divf(p->pol, norm(p->pol));
+    p->history |= CHR_REFLECT_DIFFUSE;
+    return CONTINUE;
+}
+
+/* ---- cuComplex.h (CUDA toolkit header; restated from its published code) + cx.h:1-35 */
+typedef struct { float r, i; } cx;
+static inline cx cxm(float r, float i) { cx c = {r, i}; return c; }
+static inline cx cadd(cx a, cx b) { return cxm(a.r + b.r, a.i + b.i); }
+static inline cx csub(cx a, cx b) { return cxm(a.r - b.r, a.i - b.i); }
+static inline cx cmul(cx a, cx b) { return cxm(fmaf(a.r, b.r, -(a.i * b.i)), fmaf(a.r, b.i, a.i * b.r)); }
+static cx cdiv(cx x, cx y) {
+    float s = chr_fabsf(y.r) + chr_fabsf(y.i);
+    float oos = 1.0f / s;
+    float ars = x.r * oos, ais = x.i * oos, brs = y.r * oos, bis = y.i * oos;
+    s = fmaf(bis, bis, brs * brs);
+    oos = 1.0f / s;
+    return cxm(fmaf(ais, bis, ars * brs) * oos, fmaf(ais, brs, -(ars * bis)) * oos);
+}
+static float cabs_(cx x) {
+    float a = chr_fabsf(x.r), b = chr_fabsf(x.i), v, w, t;
+    if (a > b) { v = a; w = b; } else { v = b; w = a; }
+    t = w / v;
+    t = fmaf(t, t, 1.0f);
+    t = v * chr_sqrtf(t);
+    if ((v == 0.0f) || (v > 3.402823466e38f) || (w > 3.402823466e38f)) t = v + w;
+    return t;
+}
+static float carg_(cx x) { return chr_atan2f(x.i, x.r); }
+static cx csqrt_(cx x) {
+    float r = chr_sqrtf(cabs_(x));
+    float t = carg_(x) / 2.0f;
+    float st, ct;
+    chr_sincosf(t, &st, &ct);
+    return cxm(r * ct, r * st);
+}
+
+/* photon.h:669-827 (thin-film model) */
+static int propagate_complex(Geo *g, Photon *p, State *s, chr_xorwow *rng, const chr_surface_desc *sf, int use_weights) {
+    float detect = interp_property(g, p->wavelength, sf->detect);
+    float reflect_specular = interp_property(g, p->wavelength, sf->reflect_specular);
+    float reflect_diffuse = interp_property(g, p->wavelength, sf->reflect_diffuse);
+    float n2_eta = interp_property(g, p->wavelength, sf->eta);
+    float n2_k = interp_property(g, p->wavelength, sf->k);
+    (void)reflect_specular;
+    cx n1 = cxm(s->n1, 0.0f), n2 = cxm(n2_eta, n2_k), n3 = cxm(s->n2, 0.0f);
+    float cos_t1 = dot(p->dir, s->surface_normal);
+    if (cos_t1 < 0.0f) cos_t1 = -cos_t1;
+    float theta = chr_acosf(cos_t1);
+    float sth, cth;
+    chr_sincosf(theta, &sth, &cth);
+    cx cos1 = cxm(cth, 0.0f), sin1 = cxm(sth, 0.0f);
+    float e = ((2.0f * PI_F) * sf->thickness) / p->wavelength;
+    cx r13 = cdiv(n1, n3), r12 = cdiv(n1, n2);
+    cx ratio13sin = cmul(cmul(r13, r13), cmul(sin1, sin1));
+    cx cos3 = csqrt_(csub(cxm(1.0f, 0.0f), ratio13sin));
+    cx ratio12sin = cmul(cmul(r12, r12), cmul(sin1, sin1));
+    cx cos2 = csqrt_(csub(cxm(1.0f, 0.0f), ratio12sin));
+    cx n2c2 = cmul(n2, cos2);
+    float u = n2c2.r, v = n2c2.i;
+    cx two = cxm(2.0f, 0.0f);
+    /* s polarization */
+    cx s_n1c1 = cmul(n1, cos1), s_n2c2 = cmul(n2, cos2), s_n3c3 = cmul(n3, cos3);
+    cx s_r12 = cdiv(csub(s_n1c1, s_n2c2), cadd(s_n1c1, s_n2c2));
+    cx s_r23 = cdiv(csub(s_n2c2, s_n3c3), cadd(s_n2c2, s_n3c3));
+    cx s_t12 = cdiv(cmul(two, s_n1c1), cadd(s_n1c1, s_n2c2));
+    cx s_t23 = cdiv(cmul(two, s_n2c2), cadd(s_n2c2, s_n3c3));
+    cx s_g = cdiv(s_n3c3, s_n1c1);
+    float s_abs_r12 = cabs_(s_r12), s_abs_r23 = cabs_(s_r23), s_abs_t12 = cabs_(s_t12), s_abs_t23 = cabs_(s_t23);
+    float s_arg_r12 = carg_(s_r12), s_arg_r23 = carg_(s_r23);
+    float s_exp1 = chr_expf((2.0f * v) * e);
+    float s_exp2 = 1.0f / s_exp1;
+    float two_ue = (2.0f * u) * e;
+    float s_denom = s_exp1 + ((s_abs_r12 * s_abs_r12) * (s_abs_r23 * s_abs_r23)) * s_exp2
+                    + ((2.0f * s_abs_r12) * s_abs_r23) * chr_cosf(s_arg_r23 + s_arg_r12 + two_ue);
+    float s_r = (s_abs_r12 * s_abs_r12) * s_exp1 + (s_abs_r23 * s_abs_r23) * s_exp2
+                + ((2.0f * s_abs_r12) * s_abs_r23) * chr_cosf(s_arg_r23 - s_arg_r12 + two_ue);
+    s_r /= s_denom;
+    float s_t = ((s_g.r * (s_abs_t12 * s_abs_t12)) * s_abs_t23) * s_abs_t23;
+    s_t /= s_denom;
+    /* p polarization */
+    cx p_n2c1 = cmul(n2, cos1), p_n3c2 = cmul(n3, cos2), p_n2c3 = cmul(n2, cos3), p_n1c2 = cmul(n1, cos2);
+    cx p_r12 = cdiv(csub(p_n2c1, p_n1c2), cadd(p_n2c1, p_n1c2));
+    cx p_r23 = cdiv(csub(p_n3c2, p_n2c3), cadd(p_n3c2, p_n2c3));
+    cx p_t12 = cdiv(cmul(cmul(two, n1), cos1), cadd(p_n2c1, p_n1c2));
+    cx p_t23 = cdiv(cmul(cmul(two, n2), cos2), cadd(p_n3c2, p_n2c3));
+    cx p_g = cdiv(cmul(n3, cos3), cmul(n1, cos1));
+    float p_abs_r12 = cabs_(p_r12), p_abs_r23 = cabs_(p_r23), p_abs_t12 = cabs_(p_t12), p_abs_t23 = cabs_(p_t23);
+    float p_arg_r12 = carg_(p_r12), p_arg_r23 = carg_(p_r23);
+    float p_exp1 = chr_expf((2.0f * v) * e);
+    float p_exp2 = 1.0f / p_exp1;
+    float p_denom = p_exp1 + ((p_abs_r12 * p_abs_r12) * (p_abs_r23 * p_abs_r23)) * p_exp2
+                    + ((2.0f * p_abs_r12) * p_abs_r23) * chr_cosf(p_arg_r23 + p_arg_r12 + two_ue);
+    float p_r = (p_abs_r12 * p_abs_r12) * p_exp1 + (p_abs_r23 * p_abs_r23) * p_exp2
+                + ((2.0f * p_abs_r12) * p_abs_r23) * chr_cosf(p_arg_r23 - p_arg_r12 + two_ue);
+    p_r /= p_denom;
+    float p_t = ((p_g.r * (p_abs_t12 * p_abs_t12)) * p_abs_t23) * p_abs_t23;
+    p_t /= p_denom;
+    /* s fraction, identical to propagate_at_boundary */
+    float incident_angle = get_theta(s->surface_normal, neg(p->dir));
+    float refracted_angle = chr_asinf((chr_sinf(incident_angle) * s->n1) / s->n2);
+    f3 ipn = cross(p->dir, s->surface_normal);
+    float ipn_len = norm(ipn);
+    if (ipn_len < 1e-6f) ipn = p->pol; else ipn = divf(ipn, ipn_len);
+    float nc = dot(p->pol, ipn);
+    float normal_probability = nc * nc;
+    float transmit = fmaf(normal_probability, s_t, (1.0f - normal_probability) * p_t);
+    if (!sf->transmissive) transmit = 0.0f;
+    float reflect = fmaf(normal_probability, s_r, (1.0f - normal_probability) * p_r);
+    float absorb = 1.0f - transmit - reflect;
+    if (use_weights && p->weight > WEIGHT_LOWER_THRESHOLD && absorb < (1.0f - WEIGHT_LOWER_THRESHOLD)) {
+        float survive = 1.0f - absorb;
+        absorb = 0.0f;
+        p->weight *= survive;
+        detect /= survive; reflect /= survive; transmit /= survive;
+    }
+    if (use_weights && detect > 0.0f) {
+        p->history |= CHR_SURFACE_DETECT;
+        p->weight *= detect;
+        return BREAK;
+    }
+    float us = chr_uniform01(rng);
+    if (us < absorb) {
+        float usd = chr_uniform01(rng);
+        if (usd < detect) p->history |= CHR_SURFACE_DETECT;
+        else p->history |= CHR_SURFACE_ABSORB;
+        return BREAK;
+    } else if (us < absorb + reflect || !sf->transmissive) {
+        float usr = chr_uniform01(rng);
+        if (usr < reflect_diffuse) return diffuse_reflector(p, s, rng);
+        return specular_reflector(p, s);
+    }
+    p->dir = rotate(s->surface_normal, PI_F - refracted_angle, ipn);
+    p->pol = cross(ipn, p->dir);
+    p->pol = divf(p->pol, norm(p->pol));
+    p->history |= CHR_SURFACE_TRANSMIT;
+    return CONTINUE;
+}
+
+/* photon.h:829-874 */
+static int propagate_at_wls(Geo *g, Photon *p, State *s, chr_xorwow *rng, const chr_surface_desc *sf, int use_weights) {
+    float absorb = interp_property(g, p->wavelength, sf->absorb);
+    float reflect_specular = interp_property(g, p->wavelength, sf->reflect_specular);
+    float reflect_diffuse = interp_property(g, p->wavelength, sf->reflect_diffuse);
+    float reemit = interp_property(g, p->wavelength, sf->reemit);
+    float us = chr_uniform01(rng);
+    if (use_weights && p->weight > WEIGHT_LOWER_THRESHOLD && absorb < (1.0f - WEIGHT_LOWER_THRESHOLD)) {
+        float survive = 1.0f - absorb;
+        absorb = 0.0f;
+        p->weight *= survive;
+        reflect_diffuse /= survive;
+        reflect_specular /= survive;
+    }
+    if (us < absorb) {
+        float usr = chr_uniform01(rng);
+        if (usr < reemit) {
+            p->history |= CHR_SURFACE_REEMIT;
+            p->wavelength = sample_cdf(rng, (int)g->d->wavelength_n, g->d->wavelength_start,
+                                       g->d->wavelength_step, sf->reemission_cdf);
+            p->dir = uniform_sphere(rng);
+            p->pol = cross(uniform_sphere(rng), p->dir);
+            p->pol = divf(p->pol, norm(p->pol));
+            return CONTINUE;
+        }
+        p->history |= CHR_SURFACE_ABSORB;
+        return BREAK;
+    } else if (us < absorb + reflect_specular + reflect_diffuse) {
+        float usr = chr_uniform01(rng) * (reflect_specular + reflect_diffuse);
+        if (usr < reflect_specular) return specular_reflector(p, s);
+        return diffuse_reflector(p, s, rng);
+    }
+    p->history |= CHR_SURFACE_TRANSMIT;
+    return PASS;
+}
+
+/* photon.h:877-907; the reference reads dichroic_reflect[iidx+1] past the last
+ * angle (UB) where the weight of that term is 0: clamped here. */
+static int propagate_at_dichroic(Geo *g, Photon *p, State *s, chr_xorwow *rng, const chr_surface_desc *sf) {
+    float incident_angle = get_theta(s->surface_normal, neg(p->dir));
+    int na = (int)sf->dichroic_nangles;
+    float idx = interp_idx(incident_angle, na, sf->dichroic_angles);
+    uint32_t iidx = (uint32_t)(int)idx;
+    uint32_t ihi = (iidx + 1 < (uint32_t)na) ? iidx + 1 : (uint32_t)na - 1;
+    int W1 = (int)g->d->wavelength_n + 1;
+    float rlo = interp_property(g, p->wavelength, sf->dichroic_reflect + iidx * W1);
+    float rhi = interp_property(g, p->wavelength, sf->dichroic_reflect + ihi * W1);
+    float tlo = interp_property(g, p->wavelength, sf->dichroic_transmit + iidx * W1);
+    float thi = interp_property(g, p->wavelength, sf->dichroic_transmit + ihi * W1);
+    float fr = idx - (float)iidx;
+    float reflect_prob = fmaf(rhi - rlo, fr, rlo);
+    float transmit_prob = fmaf(thi - tlo, fr, tlo);
+    float us = chr_uniform01(rng);
+    if (us < reflect_prob) return specular_reflector(p, s);
+    if (us < transmit_prob + reflect_prob) { p->history |= CHR_SURFACE_TRANSMIT; return PASS; }
+    p->history |= CHR_SURFACE_ABSORB;
+    return BREAK;
+}
+
+/* photon.h:909-951 (same clamp of iidx+1) */
+static int propagate_at_angular(Geo *g, Photon *p, State *s, chr_xorwow *rng, const chr_surface_desc *sf, int use_weights) {
+    (void)g;
+    float incident_angle = get_theta(s->surface_normal, neg(p->dir));
+    int na = (int)sf->angular_nangles;
+    float idx = interp_idx(incident_angle, na, sf->angular_angles);
+    uint32_t iidx = (uint32_t)(int)idx;
+    uint32_t ihi = (iidx + 1 < (uint32_t)na) ? iidx + 1 : (uint32_t)na - 1;
+    float t = idx - (float)iidx;
+    float tp = fmaf(t, sf->angular_transmit[ihi] - sf->angular_transmit[iidx], sf->angular_transmit[iidx]);
+    float rs = fmaf(t, sf->angular_reflect_specular[ihi] - sf->angular_reflect_specular[iidx], sf->angular_reflect_specular[iidx]);
+    float rd = fmaf(t, sf->angular_reflect_diffuse[ihi] - sf->angular_reflect_diffuse[iidx], sf->angular_reflect_diffuse[iidx]);
+    float ap = 1.0f - tp - rs - rd;
+    if (use_weights && p->weight > WEIGHT_LOWER_THRESHOLD && ap < (1.0f - WEIGHT_LOWER_THRESHOLD)) {
+        float survive = 1.0f - ap;
+        ap = 0.0f;
+        p->weight *= survive;
+        tp /= survive; rs /= survive; rd /= survive;
+    }
+    float us = chr_uniform01(rng);
+    if (us < ap) { p->history |= CHR_SURFACE_ABSORB; return BREAK; }
+    if (us < ap + tp) { p->history |= CHR_SURFACE_TRANSMIT; return PASS; }
+    if (us < ap + tp + rs) return specular_reflector(p, s);
+    return diffuse_reflector(p, s, rng);
+}
+
+/* photon.h:953-1037 (CHROMA_FORCE_SCATTER_AT_PASS is effectively 0) */
+static int propagate_at_surface(Geo *g, Photon *p, State *s, chr_xorwow *rng, int use_weights) {
+    const chr_surface_desc *sf = &g->d->surfaces[s->surface_index];
+    if (sf->model == CHR_SURFACE_COMPLEX) return propagate_complex(g, p, s, rng, sf, use_weights);
+    if (sf->model == CHR_SURFACE_WLS) return propagate_at_wls(g, p, s, rng, sf, use_weights);
+    if (sf->model == CHR_SURFACE_DICHROIC) return propagate_at_dichroic(g, p, s, rng, sf);
+    if (sf->model == CHR_SURFACE_ANGULAR) return propagate_at_angular(g, p, s, rng, sf, use_weights);
+    float detect = interp_property(g, p->wavelength, sf->detect);
+    float absorb = interp_property(g, p->wavelength, sf->absorb);
+    float reflect_diffuse = interp_property(g, p->wavelength, sf->reflect_diffuse);
+    float reflect_specular = interp_property(g, p->wavelength, sf->reflect_specular);
+    float us = chr_uniform01(rng);
+    if (use_weights && p->weight > WEIGHT_LOWER_THRESHOLD && absorb < (1.0f - WEIGHT_LOWER_THRESHOLD)) {
+        float survive = 1.0f - absorb;
+        absorb = 0.0f;
+        p->weight *= survive;
+        detect /= survive; reflect_diffuse /= survive; reflect_specular /= survive;
+    }
+    if (use_weights && detect > 0.0f) {
+        p->history |= CHR_SURFACE_DETECT;
+        p->weight *= detect;
+        return BREAK;
+    }
+    if (us < absorb) { p->history |= CHR_SURFACE_ABSORB; return BREAK; }
+    if (us < absorb + detect) { p->history |= CHR_SURFACE_DETECT; return BREAK; }
+    if (us < absorb + detect + reflect_diffuse) return diffuse_reflector(p, s, rng);
+    if (us < absorb + detect + reflect_diffuse + reflect_specular) return specular_reflector(p, s);
+    return PASS;
+}
+
+/* ------------------------------------------------ host-side photon view */
+typedef struct {
+    float *pos, *dir, *pol, *wavelengths, *t, *weights;
+    uint32_t *flags; int32_t *last_hit; uint32_t *evidx;
+} Photons;
+
+/* propagate.cu:254-366 for one slot; returns 1 if the photon is still alive.
+ * *processed is 0 when the photon was dead on entry (no write-back). */
+static int propagate_one(Geo *g, Photons *ph, uint32_t photon_id, chr_xorwow *rng, int max_steps,
+                         int use_weights, int scatter_first, int *processed) {
+    Photon p;
+    uint32_t i = photon_id;
+    p.pos = mk(ph->pos[3 * i], ph->pos[3 * i + 1], ph->pos[3 * i + 2]);
+    p.dir = mk(ph->dir[3 * i], ph->dir[3 * i + 1], ph->dir[3 * i + 2]);
+    p.dir = divf(p.dir, norm(p.dir));
+    p.pol = mk(ph->pol[3 * i], ph->pol[3 * i + 1], ph->pol[3 * i + 2]);
+    p.pol = divf(p.pol, norm(p.pol));
+    p.wavelength = ph->wavelengths[i];
+    p.time = ph->t[i];
+    p.last_hit_triangle = ph->last_hit[i];
+    p.history = (uint16_t)ph->flags[i];
+    p.weight = ph->weights[i];
+    p.evidx = ph->evidx[i];
+    *processed = 0;
+    if (p.history & DEAD_MASK) return 0;
+    *processed = 1;
+    State s;
+    int steps = 0;
+    while (steps < max_steps) {
+        steps++;
+        float prod = ((((p.dir.x * p.dir.y) * p.dir.z) * p.pos.x) * p.pos.y) * p.pos.z;
+        if (chr_isnan(prod)) { p.history |= CHR_NO_HIT | CHR_NAN_ABORT; break; }
+        fill_state(g, &s, &p);
+        if (p.last_hit_triangle == -1) break;
+        int command = propagate_to_boundary(g, &p, &s, rng, use_weights, scatter_first);
+        scatter_first = 0;
+        if (command == BREAK) break;
+        if (command == CONTINUE) continue;
+        if (s.surface_index != -1) {
+            command = propagate_at_surface(g, &p, &s, rng, use_weights);
+            if (command == BREAK) break;
+            if (command == CONTINUE) continue;
+        }
+        propagate_at_boundary(&p, &s, rng);
+    }
+    ph->pos[3 * i] = p.pos.x; ph->pos[3 * i + 1] = p.pos.y; ph->pos[3 * i + 2] = p.pos.z;
+    ph->dir[3 * i] = p.dir.x; ph->dir[3 * i + 1] = p.dir.y; ph->dir[3 * i + 2] = p.dir.z;
+    ph->pol[3 * i] = p.pol.x; ph->pol[3 * i + 1] = p.pol.y; ph->pol[3 * i + 2] = p.pol.z;
+    ph->wavelengths[i] = p.wavelength;
+    ph->t[i] = p.time;
+    ph->flags[i] = p.history;
+    ph->last_hit[i] = p.last_hit_triangle;
+    ph->weights[i] = p.weight;
+    ph->evidx[i] = p.evidx;
+    return (p.history & DEAD_MASK) == 0;
+}
+
+typedef struct {
+    uint64_t nodes_visited, tris_tested, steps_traversed;
+    uint32_t max_depth, overflows, host_steps, launches;
+} orc_stats;
+
+static inline void rng_load(const uint32_t *st, uint32_t nslots, uint32_t s, chr_xorwow *r) {
+    r->d = st[s]; r->v0 = st[nslots + s]; r->v1 = st[2 * nslots + s];
+    r->v2 = st[3 * nslots + s]; r->v3 = st[4 * nslots + s]; r->v4 = st[5 * nslots + s];
+}
+static inline void rng_store(uint32_t *st, uint32_t nslots, uint32_t s, const chr_xorwow *r) {
+    st[s] = r->d; st[nslots + s] = r->v0; st[2 * nslots + s] = r->v1;
+    st[3 * nslots + s] = r->v2; st[4 * nslots + s] = r->v3; st[5 * nslots + s] = r->v4;
+}
+
+/* one kernel launch (propagate.cu:254): slots [0,nthreads) in parallel */
+static void launch_chunk(const chr_geometry_desc *d, Photons *ph, uint32_t *rng, uint32_t nslots,
+                         const uint32_t *input_queue, int first, int nthreads, uint8_t *alive,
+                         int max_steps, int use_weights, int scatter_first, orc_stats *st, int nthreads_omp) {
+    uint64_t nv = 0, nt = 0;
+    uint32_t md = 0, ov = 0;
+#pragma omp parallel for schedule(dynamic, 64) num_threads(nthreads_omp) reduction(+:nv,nt,ov) reduction(max:md)
+    for (int id = 0; id < nthreads; ++id) {
+        Geo g = {d, 0, 0, 0, 0};
+        chr_xorwow r;
+        rng_load(rng, nslots, (uint32_t)id, &r);
+        uint32_t photon_id = input_queue[first + id];
+        int processed;
+        alive[id] = (uint8_t)propagate_one(&g, ph, photon_id, &r, max_steps, use_weights, scatter_first, &processed);
+        if (processed) rng_store(rng, nslots, (uint32_t)id, &r);
+        nv += g.nodes_visited; nt += g.tris_tested; ov += g.overflows;
+        if (g.max_depth > md) md = g.max_depth;
+    }
+    st->nodes_visited += nv; st->tris_tested += nt; st->overflows += ov;
+    if (md > st->max_depth) st->max_depth = md;
+    st->launches++;
+}
+
+static int g_init = 0;
+static void init_once(void) { if (!g_init) { init_thresholds(); g_init = 1; } }
+
+/* ---------------------------------------------------------------- exports */
+
+EXPORT void orc_rng_init(uint32_t *states, uint32_t nslots, unsigned long long seed, unsigned long long offset) {
+    static uint32_t *seq = NULL, *off = NULL;
+    if (!seq) {
+        seq = (uint32_t *)malloc(sizeof(uint32_t) * CHR_XW_MATWORDS * 40);
+        off = (uint32_t *)malloc(sizeof(uint32_t) * CHR_XW_MATWORDS * 64);
+        chr_xw_sequence_matrices(seq, 40);
+        chr_xw_offset_matrices(off, 64);
+    }
+#pragma omp parallel for
+    for (int64_t s = 0; s < (int64_t)nslots; ++s) {
+        chr_xorwow r;
+        chr_xorwow_init(&r, seed, (unsigned long long)s, offset, seq, 40, off, 64);
+        rng_store(states, nslots, (uint32_t)s, &r);
+    }
+}
+
+/* A^(2^(67+i)) for the rocRAND cross-check */
+EXPORT void orc_sequence_matrices(uint32_t *out, int nlevels) { chr_xw_sequence_matrices(out, nlevels); }
+
+/* draw n uniforms from slot states (tests of the generator) */
+EXPORT void orc_rng_uniforms(uint32_t *states, uint32_t nslots, uint32_t slot, int n, float *out) {
+    chr_xorwow r;
+    rng_load(states, nslots, slot, &r);
+    for (int i = 0; i < n; ++i) out[i] = chr_uniform01(&r);
+    rng_store(states, nslots, slot, &r);
+}
+
+/* distance_to_mesh (mesh.h:131-159) */
+EXPORT int orc_distance_to_mesh(const chr_geometry_desc *d, int n, const float *origin, const float *direction,
+                                float *distance, int32_t *triangle, uint64_t *nodes_tris) {
+    init_once();
+    uint64_t nv = 0, nt = 0;
+#pragma omp parallel for reduction(+:nv,nt)
+    for (int i = 0; i < n; ++i) {
+        Geo g = {d, 0, 0, 0, 0};
+        f3 o = mk(origin[3 * i], origin[3 * i + 1], origin[3 * i + 2]);
+        f3 dir = mk(direction[3 * i], direction[3 * i + 1], direction[3 * i + 2]);
+        dir = divf(dir, norm(dir));
+        float dist;
+        int tri = intersect_mesh(&g, o, dir, &dist, -1);
+        if (tri != -1) distance[i] = dist;
+        if (triangle) triangle[i] = tri;
+        nv += g.nodes_visited; nt += g.tris_tested;
+    }
+    if (nodes_tris) { nodes_tris[0] = nv; nodes_tris[1] = nt; }
+    return 0;
+}
+
+static void chunk_iter(int nelements, int ntpb, int maxb, int first, int *count) {
+    (void)first;
+    int left = nelements;
+    int blocks = left / ntpb + (left % ntpb != 0);
+    if (blocks > maxb) blocks = maxb;
+    *count = left < blocks * ntpb ? left : blocks * ntpb;
+}
+
+/* GPUPhotons.propagate (photon.py:226-293), track=False, stable compaction.
+ * Photon arrays are host arrays updated in place; rng states SoA. */
+EXPORT int orc_propagate(const chr_geometry_desc *d, float *pos, float *dir, float *pol, float *wavelengths,
+                         float *t, uint32_t *flags, int32_t *last_hit, float *weights, uint32_t *evidx,
+                         uint32_t nphotons_total, uint32_t true_nphotons, uint32_t ncopies,
+                         uint32_t *rng, uint32_t nslots, int ntpb, int max_blocks, int max_steps,
+                         int use_weights, int scatter_first, int omp_threads, uint64_t *stats_out) {
+    init_once();
+    Photons ph = {pos, dir, pol, wavelengths, t, weights, flags, last_hit, evidx};
+    if ((uint64_t)ntpb * (uint64_t)max_blocks > nslots) return CHR_ERR_INVALID;
+    uint32_t *qin = (uint32_t *)malloc(sizeof(uint32_t) * (nphotons_total + 1));
+    uint32_t *qout = (uint32_t *)malloc(sizeof(uint32_t) * (nphotons_total + 1));
+    uint8_t *alive = (uint8_t *)malloc((size_t)ntpb * max_blocks + 1);
+    if (!qin || !qout || !alive) return CHR_ERR_NOMEM;
+    qin[0] = 0;
+    for (uint32_t c = 0; c < ncopies; ++c)
+        for (uint32_t k = 0; k < true_nphotons; ++k) qin[1 + c + k * ncopies] = k + c * true_nphotons;
+    for (uint32_t k = 0; k <= nphotons_total; ++k) qout[k] = 0;
+    qout[0] = 1;
+    orc_stats st;
+    memset(&st, 0, sizeof(st));
+    int nphotons = (int)nphotons_total;
+    int step = 0;
+    while (step < max_steps) {
+        int nsteps = (nphotons < ntpb * 16 * 8 || use_weights) ? max_steps - step : 1;
+        int first = 0;
+        while (first < nphotons) {
+            int count;
+            chunk_iter(nphotons - first, ntpb, max_blocks, first, &count);
+            launch_chunk(d, &ph, rng, nslots, qin + 1, first, count, alive, nsteps, use_weights, scatter_first,
+                         &st, omp_threads);
+            /* stable enqueue of survivors (input order) */
+            for (int id = 0; id < count; ++id)
+                if (alive[id]) qout[qout[0]++] = qin[1 + first + id];
+            first += count;
+        }
+        st.host_steps++;
+        step += nsteps;
+        scatter_first = 0;
+        if (step < max_steps) {
+            uint32_t *tmp = qin; qin = qout; qout = tmp;
+            qout[0] = 1;
+            nphotons = (int)qin[0] - 1;
+            if (nphotons == 0) break;
+        }
+    }
+    if (stats_out) {
+        stats_out[0] = st.nodes_visited; stats_out[1] = st.tris_tested; stats_out[2] = st.max_depth;
+        stats_out[3] = st.overflows; stats_out[4] = st.host_steps; stats_out[5] = st.launches;
+        stats_out[6] = (step < max_steps) ? (uint64_t)(qin[0] - 1) : 0;
+    }
+    free(qin); free(qout); free(alive);
+    return 0;
+}
+
+/* single-photon single-step probes for unit tests of the physics pieces */
+EXPORT int orc_fill_state(const chr_geometry_desc *d, const float *posdir, int32_t last_hit, float wavelength,
+                          float *out /*[8]: dist, nx,ny,nz, n1,n2,abs,scat*/, int32_t *iout /*[4]*/) {
+    init_once();
+    Geo g = {d, 0, 0, 0, 0};
+    Photon p;
+    memset(&p, 0, sizeof(p));
+    p.pos = mk(posdir[0], posdir[1], posdir[2]);
+    p.dir = mk(posdir[3], posdir[4], posdir[5]);
+    p.last_hit_triangle = last_hit;
+    p.wavelength = wavelength;
+    State s;
+    memset(&s, 0, sizeof(s));
+    fill_state(&g, &s, &p);
+    out[0] = s.distance_to_boundary; out[1] = s.surface_normal.x; out[2] = s.surface_normal.y;
+    out[3] = s.surface_normal.z; out[4] = s.n1; out[5] = s.n2; out[6] = s.absorption_length;
+    out[7] = s.scattering_length;
+    iout[0] = p.last_hit_triangle; iout[1] = s.surface_index; iout[2] = s.material1; iout[3] = p.history;
+    return 0;
+}
+
+/* math probes (tests/test_fmath.py) */
+EXPORT void orc_math(int which, int n, const float *x, const float *y, float *out) {
+    for (int i = 0; i < n; ++i) {
+        switch (which) {
+        case 0: out[i] = chr_logf(x[i]); break;
+        case 1: out[i] = chr_expf(x[i]); break;
+        case 2: out[i] = chr_sinf(x[i]); break;
+        case 3: out[i] = chr_cosf(x[i]); break;
+        case 4: out[i] = chr_tanf(x[i]); break;
+        case 5: out[i] = chr_asinf(x[i]); break;
+        case 6: out[i] = chr_acosf(x[i]); break;
+        case 7: out[i] = chr_atan2f(y[i], x[i]); break;
+        default: out[i] = 0.0f;
+        }
+    }
+}
+
+/* rayleigh scatter probe: n photons with the given pol/dir, one scatter each from slot 0 */
+EXPORT void orc_rayleigh(int n, float *dir, float *pol, uint32_t *states, uint32_t nslots) {
+    init_once();
+    chr_xorwow r;
+    rng_load(states, nslots, 0, &r);
+    for (int i = 0; i < n; ++i) {
+        Photon p;
+        memset(&p, 0, sizeof(p));
+        p.dir = mk(dir[3 * i], dir[3 * i + 1], dir[3 * i + 2]);
+        p.pol = mk(pol[3 * i], pol[3 * i + 1], pol[3 * i + 2]);
+        rayleigh_scatter(&p, &r);
+        dir[3 * i] = p.dir.x; dir[3 * i + 1] = p.dir.y; dir[3 * i + 2] = p.dir.z;
+        pol[3 * i] = p.pol.x; pol[3 * i + 1] = p.pol.y; pol[3 * i + 2] = p.pol.z;
+    }
+    rng_store(states, nslots, 0, &r);
+}
+
+EXPORT int orc_version(void) { return 1; }
