@@ -1,0 +1,253 @@
+#!/usr/bin/env python
+"""Benchmark: propagated photons/s of GPUPhotons.propagate (the reference's
+hot path, chroma/gpu/photon.py:226-293) on a demo PMT detector.
+
+One "step" = one propagate of a fresh batch of isotropic photons (BASELINE.md
+section 3 source: centre point source, seed 20260102) to termination or
+max_steps (default 1000, the Simulation.simulate default), launch shape of
+Simulation (nthreads_per_block=512, max_blocks=1024 -> 524,288 RNG slots).
+Photon inputs are resident in HBM before the timed region; each step restores
+them from a device-resident copy (D2D, inside the timed region).
+
+Multi-GPU: one process per GPU (torchrun), geometry replicated, photons
+sharded (each rank propagates its own batch: weak scaling), no collective in
+the data path; the timed region is bracketed by barriers and the max over
+ranks is reported.
+
+Roofline: the propagate kernel is bound by HBM/L2 latency-bandwidth on the
+BVH + triangle gathers.  achieved = algorithmic bytes per step / summed
+propagate-kernel time (HIP events around every launch, on its stream), with
+algorithmic bytes per photon B_alg = 120 + sum over traversals of
+(16 * nodes tested + 48 * triangles tested + 4), counted by the CPU oracle on
+the cpu_baseline sample of the same workload.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, 'chroma-lite_amd'))
+
+import numpy as np  # noqa: E402
+
+METRIC = 'propagated photons/sec, 29k-PMT detector, 10M isotropic photons, 1/2/4/8 GPUs'
+HBM_PEAK_GBS = 8000.0
+DETECTORS = {
+    # name: (description, kwargs of chroma.demo.detector)
+    '29k': ('demo.detector(pmt_radius=23780, sphere_radius=24280): 29,007 PMTs, ~170M triangles',
+            dict(pmt_radius=23780.0, sphere_radius=24280.0)),
+    'demo': ('demo.detector(): 10,055 PMTs, 58.96M triangles', dict()),
+    'tiny': ('demo.tiny(): 53 PMTs, 389,568 triangles', dict(pmt_radius=2000.0, sphere_radius=2500.0,
+                                                             spiral_step=700.0)),
+    'small': ('demo.detector(600, 900, 1500): 2 PMTs, 90,912 triangles',
+              dict(pmt_radius=600.0, sphere_radius=900.0, spiral_step=1500.0)),
+}
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def build_geometry(name, cache_dir):
+    """Flattened demo detector + BVH, cached on local disk (same box reuse)."""
+    from chroma import demo
+    from chroma.bvh import make_recursive_grid_bvh, BVH, WorldCoords
+    t0 = time.time()
+    det = demo.detector(**DETECTORS[name][1])
+    path = os.path.join(cache_dir, 'geometry_%s.npz' % name) if cache_dir else None
+    if path and os.path.exists(path):
+        z = np.load(path)
+        from chroma.geometry import Mesh
+        det.solid_id_to_channel_index = np.asarray(det.solid_id_to_channel_index, dtype=np.int32)
+        det.channel_index_to_solid_id = np.asarray(det.channel_index_to_solid_id, dtype=np.int32)
+        mesh = Mesh.__new__(Mesh)
+        mesh.vertices, mesh.triangles = z['vertices'], z['triangles']
+        det.mesh = mesh
+        det.solid_id, det.colors = z['solid_id'], z['colors']
+        det.material1_index, det.material2_index, det.surface_index = \
+            z['material1_index'], z['material2_index'], z['surface_index']
+        det.unique_materials = [m for m in _unique_materials(det)]
+        det.unique_surfaces = [s for s in _unique_surfaces(det)]
+        det.bvh = BVH(WorldCoords(z['world_origin'], z['world_scale']), z['nodes'], z['layer_offsets'])
+        log('geometry %s loaded from cache in %.1fs' % (name, time.time() - t0))
+        return det
+    det.flatten()
+    t1 = time.time()
+    det.bvh = make_recursive_grid_bvh(det.mesh, target_degree=3)
+    log('geometry %s: %d triangles, flatten %.1fs, BVH %.1fs (%d nodes)' % (
+        name, len(det.mesh.triangles), t1 - t0, time.time() - t1, len(det.bvh.nodes)))
+    if path:
+        try:
+            os.makedirs(cache_dir, exist_ok=True)
+            np.savez(path + '.tmp.npz', vertices=det.mesh.vertices, triangles=det.mesh.triangles,
+                     solid_id=det.solid_id, colors=det.colors, material1_index=det.material1_index,
+                     material2_index=det.material2_index, surface_index=det.surface_index,
+                     nodes=det.bvh.nodes, layer_offsets=np.asarray(det.bvh.layer_offsets),
+                     world_origin=det.bvh.world_coords.world_origin,
+                     world_scale=det.bvh.world_coords.world_scale)
+            os.replace(path + '.tmp.npz', path)
+        except OSError as e:
+            log('geometry cache not written: %s' % e)
+    return det
+
+
+def _unique_materials(det):
+    from chroma.geometry import _first_seen
+    return _first_seen([m for s in det.solids for m in s.unique_materials])
+
+
+def _unique_surfaces(det):
+    from chroma.geometry import _first_seen
+    return _first_seen([x for s in det.solids for x in s.unique_surfaces])
+
+
+def cpu_baseline(packed, photons, nslots, ntpb, max_blocks, max_steps, seed, budget_s, threads):
+    """Oracle (plain C port of the reference kernel, OpenMP) on a bounded
+    sample of the same workload; also returns the per-photon algorithmic
+    byte count for the roofline."""
+    sys.path.insert(0, os.path.join(ROOT, 'oracle'))
+    import oracle
+    from chroma.event import Photons
+    n = 2000
+    total_t = 0.0
+    agg = None
+    while True:
+        sample = Photons(photons.pos[:n], photons.dir[:n], photons.pol[:n], photons.wavelengths[:n])
+        host = oracle.HostPhotons(sample)
+        st = oracle.rng_init(nslots, seed=seed)
+        t0 = time.time()
+        stats = oracle.propagate(packed, host, st, nslots, ntpb, max_blocks, max_steps, threads=threads)
+        dt = time.time() - t0
+        total_t, agg = dt, (n, stats)
+        if dt > budget_s / 4 or n * 4 > len(photons.pos):
+            break
+        n = int(min(len(photons.pos), n * max(2.0, min(8.0, (budget_s / 2) / max(dt, 1e-3)))))
+    n, stats = agg
+    b_alg = 120.0 + (16.0 * stats['nodes_visited'] + 48.0 * stats['tris_tested'] + 4.0 * stats['traversals']) / n
+    return dict(value=n / total_t, unit='photons/s', cores=threads, kind='port',
+                sample='%d of the same isotropic photons, same geometry and launch shape, max_steps=%d; %.1fs on %d '
+                       'threads' % (n, max_steps, total_t, threads)), b_alg, stats, n
+
+
+def main():
+    ap = argparse.ArgumentParser(description=__doc__)
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=3)
+    ap.add_argument('--warmup', type=int, default=1)
+    ap.add_argument('--photons', type=int, default=10_000_000, help='photons per GPU per step')
+    ap.add_argument('--detector', default='29k', choices=sorted(DETECTORS))
+    ap.add_argument('--max-steps', type=int, default=1000)
+    ap.add_argument('--nthreads-per-block', type=int, default=512)
+    ap.add_argument('--max-blocks', type=int, default=1024)
+    ap.add_argument('--seed', type=int, default=1)
+    ap.add_argument('--cpu-budget', type=float, default=20.0, help='seconds of CPU-baseline work')
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--cache-dir', default=os.environ.get('CHROMA_BENCH_CACHE', '/tmp/chroma_bench_cache'))
+    args = ap.parse_args()
+
+    import torch
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+
+    from chroma import gpu
+    from chroma.gpu import gpuarray as ga
+    from chroma.gpu.packing import PackedGeometry
+    from chroma.photon_source import isotropic
+    from types import SimpleNamespace
+
+    det = build_geometry(args.detector, args.cache_dir)
+    t0 = time.time()
+    gdet = gpu.GPUDetector(det)
+    log('rank %d: geometry on device in %.1fs (%.2f GB)' % (rank, time.time() - t0, gdet.device_bytes() / 1e9))
+    nslots = args.nthreads_per_block * args.max_blocks
+    rng = gpu.get_rng_states(nslots, seed=args.seed + 7919 * rank)
+
+    photons = isotropic(args.photons, seed=20260102 + rank)
+    pristine = SimpleNamespace(
+        pos=ga.to_gpu(gpu.to_float3(photons.pos)), dir=ga.to_gpu(gpu.to_float3(photons.dir)),
+        pol=ga.to_gpu(gpu.to_float3(photons.pol)), wavelengths=ga.to_gpu(photons.wavelengths),
+        t=ga.to_gpu(photons.t), flags=ga.to_gpu(photons.flags), evidx=ga.to_gpu(photons.evidx),
+        true_nphotons=args.photons)
+    torch.cuda.synchronize()
+
+    def step():
+        gp = gpu.GPUPhotons(pristine, copy_flags=True, copy_triangles=False, copy_weights=False)
+        gp.propagate(gdet, rng, nthreads_per_block=args.nthreads_per_block, max_blocks=args.max_blocks,
+                     max_steps=args.max_steps)
+        return gp
+
+    for _ in range(args.warmup):
+        gp = step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    kernel_ms = 0.0
+    launches = 0
+    host_steps = 0
+    for _ in range(args.steps):
+        gp = step()
+        kernel_ms += gp.last_stats.kernel_ms
+        launches += gp.last_stats.launches
+        host_steps += gp.last_stats.steps_run
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device='cuda')
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    detected = int(((gp.flags.get() & 4) != 0).sum())
+
+    if rank == 0:
+        total = args.photons * world * args.steps
+        value = total / elapsed
+        result = {
+            'metric': METRIC, 'value': value, 'unit': 'photons/s', 'n_gpus': world, 'steps': args.steps,
+            'warmup': args.warmup, 'ms_per_step': 1e3 * elapsed / args.steps, 'higher_is_better': True,
+            'scaling': 'weak', 'vs_baseline': (value / 2.5e6) if args.detector == '29k' else None,
+            'dtype': 'f32', 'data': 'synthetic isotropic point source (BASELINE.md section 3), seed 20260102+rank',
+            'config': {'workload': 'GPUPhotons.propagate of %d isotropic photons per GPU per step on %s, '
+                                   'max_steps=%d, launch shape %dx%d (524,288 RNG slots)' % (
+                                       args.photons, DETECTORS[args.detector][0], args.max_steps,
+                                       args.nthreads_per_block, args.max_blocks),
+                       'detector': args.detector, 'photons_per_gpu': args.photons, 'triangles': len(det.mesh.triangles),
+                       'bvh_nodes': len(det.bvh.nodes), 'channels': det.num_channels(),
+                       'parallelism': 'photon-sharded x%d, geometry replicated' % world},
+            'detail': {'kernel_ms_per_step': kernel_ms / args.steps, 'launches_per_step': launches / args.steps,
+                       'host_steps_per_propagate': host_steps / args.steps,
+                       'detected_fraction': detected / args.photons},
+            'roofline': None, 'cpu_baseline': None,
+        }
+        if not args.no_cpu_baseline and world == 1:
+            threads = min(16, len(os.sched_getaffinity(0)))
+            cpu, b_alg, ostats, nsample = cpu_baseline(PackedGeometry(det), photons, nslots, args.nthreads_per_block,
+                                                       args.max_blocks, args.max_steps, args.seed, args.cpu_budget,
+                                                       threads)
+            result['cpu_baseline'] = cpu
+            per_step_s = kernel_ms / args.steps / 1e3
+            achieved = args.photons * b_alg / per_step_s / 1e9
+            result['roofline'] = {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                                  'frac': achieved / HBM_PEAK_GBS, 'traffic': None,
+                                  'bytes_per_photon_alg': b_alg,
+                                  'nodes_per_photon': ostats['nodes_visited'] / nsample,
+                                  'triangles_per_photon': ostats['tris_tested'] / nsample,
+                                  'traversals_per_photon': ostats['traversals'] / nsample,
+                                  'kernel': 'chr::propagate_kernel'}
+        print(json.dumps(result), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

@@ -1,0 +1,8 @@
+"""Device layer (drop-in for reference chroma/gpu/): GPUPhotons, GPUGeometry,
+GPUDetector, RNG states, context helpers.  Everything launches hand-written
+gfx950 HIP kernels through libchroma_amd.so (chroma.gpu._native)."""
+from chroma.gpu.tools import (chunk_iterator, to_float3, to_uint3, create_cuda_context, get_rng_states,  # noqa
+                              RNGStates, current_stream)
+from chroma.gpu.geometry import GPUGeometry  # noqa: F401
+from chroma.gpu.detector import GPUDetector  # noqa: F401
+from chroma.gpu.photon import GPUPhotons, GPUPhotonsSlice  # noqa: F401

@@ -1,0 +1,132 @@
+"""ctypes binding of the C ABI in include/chroma_amd.h (libchroma_amd.so).
+
+This is the only place Python touches native code.  The library is built
+in-tree (chroma-lite_amd/csrc/Makefile -> chroma/_lib/libchroma_amd.so) and is
+REQUIRED: there is no Python or CPU fallback for the GPU path, so a missing
+library raises immediately.
+"""
+import ctypes
+import os
+
+_LIBPATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), '_lib',
+                        'libchroma_amd.so')
+
+c_u32 = ctypes.c_uint32
+c_i32 = ctypes.c_int32
+c_u64 = ctypes.c_uint64
+c_f32 = ctypes.c_float
+c_vp = ctypes.c_void_p
+P_f32 = ctypes.POINTER(ctypes.c_float)
+P_u32 = ctypes.POINTER(ctypes.c_uint32)
+
+
+class MaterialDesc(ctypes.Structure):
+    _fields_ = [('num_comp', c_u32), ('refractive_index', c_vp), ('absorption_length', c_vp),
+                ('scattering_length', c_vp), ('comp_reemission_prob', c_vp),
+                ('comp_reemission_wvl_cdf', c_vp), ('comp_reemission_time_cdf', c_vp),
+                ('comp_absorption_length', c_vp)]
+
+
+class SurfaceDesc(ctypes.Structure):
+    _fields_ = [('present', c_i32), ('model', c_u32), ('transmissive', c_u32), ('thickness', c_f32),
+                ('detect', c_vp), ('absorb', c_vp), ('reemit', c_vp), ('reflect_diffuse', c_vp),
+                ('reflect_specular', c_vp), ('eta', c_vp), ('k', c_vp), ('reemission_cdf', c_vp),
+                ('dichroic_nangles', c_u32), ('dichroic_angles', c_vp), ('dichroic_reflect', c_vp),
+                ('dichroic_transmit', c_vp), ('angular_nangles', c_u32), ('angular_angles', c_vp),
+                ('angular_transmit', c_vp), ('angular_reflect_specular', c_vp),
+                ('angular_reflect_diffuse', c_vp)]
+
+
+class WirePlaneDesc(ctypes.Structure):
+    _fields_ = [('origin', c_f32 * 3), ('u', c_f32 * 3), ('v', c_f32 * 3), ('pitch', c_f32),
+                ('radius', c_f32), ('umin', c_f32), ('umax', c_f32), ('vmin', c_f32), ('vmax', c_f32),
+                ('v0', c_f32), ('surface_index', c_i32), ('material_outer_index', c_i32),
+                ('material_inner_index', c_i32), ('color', c_u32)]
+
+
+class GeometryDesc(ctypes.Structure):
+    _fields_ = [('nvertices', c_u32), ('ntriangles', c_u32), ('nnodes', c_u32), ('nmaterials', c_u32),
+                ('nsurfaces', c_u32), ('nwireplanes', c_u32), ('h_vertices', c_vp), ('h_triangles', c_vp),
+                ('h_material_codes', c_vp), ('h_nodes', c_vp), ('world_origin', c_f32 * 3),
+                ('world_scale', c_f32), ('wavelength_n', c_u32), ('wavelength_start', c_f32),
+                ('wavelength_step', c_f32), ('time_n', c_u32), ('time_start', c_f32), ('time_step', c_f32),
+                ('materials', ctypes.POINTER(MaterialDesc)), ('surfaces', ctypes.POINTER(SurfaceDesc)),
+                ('wireplanes', ctypes.POINTER(WirePlaneDesc))]
+
+
+class PhotonsDesc(ctypes.Structure):
+    _fields_ = [('d_pos', c_vp), ('d_dir', c_vp), ('d_pol', c_vp), ('d_wavelengths', c_vp), ('d_t', c_vp),
+                ('d_weights', c_vp), ('d_flags', c_vp), ('d_last_hit_triangles', c_vp), ('d_evidx', c_vp)]
+
+
+class PropagateStats(ctypes.Structure):
+    _fields_ = [('steps_run', c_u32), ('launches', c_u32), ('final_alive', c_u32), ('stack_overflows', c_u32),
+                ('kernel_ms', ctypes.c_double)]
+
+
+_SIGNATURES = {
+    'chr_geometry_create': (c_i32, [ctypes.POINTER(GeometryDesc), ctypes.POINTER(c_vp)]),
+    'chr_geometry_destroy': (c_i32, [c_vp]),
+    'chr_geometry_device_bytes': (c_i32, [c_vp, ctypes.POINTER(c_u64)]),
+    'chr_init_rng': (c_i32, [c_vp, c_u32, c_u64, c_u64, c_vp]),
+    'chr_rng_download': (c_i32, [c_vp, c_u32, c_vp, c_vp]),
+    'chr_propagate_scratch_words': (c_u64, [c_u32]),
+    'chr_propagate_chunk': (c_i32, [c_vp, ctypes.POINTER(PhotonsDesc), c_vp, c_u32, c_i32, c_i32, c_vp, c_vp,
+                                    c_i32, c_i32, c_i32, c_vp, c_vp]),
+    'chr_propagate': (c_i32, [c_vp, ctypes.POINTER(PhotonsDesc), c_u32, c_u32, c_u32, c_vp, c_u32, c_i32, c_i32,
+                              c_i32, c_i32, c_i32, ctypes.POINTER(PropagateStats), c_vp]),
+    'chr_photon_hits': (c_i32, [ctypes.POINTER(PhotonsDesc), c_i32, c_i32, c_u32, c_vp, c_vp,
+                                ctypes.POINTER(PhotonsDesc), c_vp, ctypes.POINTER(c_u32), c_vp]),
+    'chr_select_photons': (c_i32, [ctypes.POINTER(PhotonsDesc), c_i32, c_i32, c_u32, ctypes.POINTER(PhotonsDesc),
+                                   ctypes.POINTER(c_u32), c_vp]),
+    'chr_copy_photon_queue': (c_i32, [ctypes.POINTER(PhotonsDesc), c_i32, c_i32, c_vp, ctypes.POINTER(PhotonsDesc),
+                                      c_vp]),
+    'chr_photon_duplicate': (c_i32, [ctypes.POINTER(PhotonsDesc), c_i32, c_i32, c_i32, c_i32, c_vp]),
+    'chr_distance_to_mesh': (c_i32, [c_vp, c_u32, c_vp, c_vp, c_vp, c_vp]),
+    'chr_bvh_build_grid': (c_i32, [c_vp, c_u32, c_vp, c_u32, c_i32, ctypes.POINTER(c_vp)]),
+    'chr_bvh_result_info': (c_i32, [c_vp, ctypes.POINTER(c_u32), ctypes.POINTER(c_u32), c_vp,
+                                    ctypes.POINTER(c_f32)]),
+    'chr_bvh_result_copy': (c_i32, [c_vp, c_vp, c_vp]),
+    'chr_bvh_result_free': (c_i32, [c_vp]),
+    'chr_last_error': (ctypes.c_char_p, []),
+    'chr_version': (c_i32, []),
+}
+
+EXPORTED = tuple(_SIGNATURES)
+
+_lib = None
+
+
+class NativeError(RuntimeError):
+    """A nonzero chr_status from libchroma_amd (message = chr_last_error())."""
+
+
+def library_path():
+    return _LIBPATH
+
+
+def lib():
+    """Load libchroma_amd.so (once).  Raises if it has not been built."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIBPATH):
+            raise ImportError('libchroma_amd.so not found at %s: build it with '
+                              '`make -C chroma-lite_amd/csrc` (or __graft_entry__.build())' % _LIBPATH)
+        l = ctypes.CDLL(_LIBPATH)
+        for name, (res, args) in _SIGNATURES.items():
+            fn = getattr(l, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = l
+    return _lib
+
+
+def check(rc, what=''):
+    if rc != 0:
+        msg = lib().chr_last_error().decode(errors='replace')
+        raise NativeError('%s failed (status %d): %s' % (what, rc, msg))
+    return rc
+
+
+def call(name, *args):
+    return check(getattr(lib(), name)(*args), name)

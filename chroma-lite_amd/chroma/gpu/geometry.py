@@ -1,0 +1,61 @@
+"""GPUGeometry (drop-in for reference chroma/gpu/geometry.py:13-565).
+
+Packs the geometry (chroma.gpu.packing) and uploads it with
+chr_geometry_create, which lays it out for the gfx950 traversal kernel
+(csrc/device_geometry.h).  `gpudata` is the opaque device-geometry handle the
+kernels take.  There is no host-mapped split of the BVH (the reference's
+min_free_gpu_mem path, geometry.py:409-439): 288 GB of HBM holds even the
+~170 M-triangle 29k-PMT detector many times over.
+"""
+import ctypes
+
+import numpy as np
+
+from chroma.gpu import _native
+from chroma.gpu import gpuarray as ga
+from chroma.gpu.packing import PackedGeometry
+from chroma.gpu.tools import format_size
+from chroma.log import logger
+
+
+class GPUGeometry(object):
+    def __init__(self, geometry, wavelengths=None, times=None, print_usage=False, min_free_gpu_mem=300e6):
+        if getattr(geometry, 'bvh', None) is None:
+            from chroma.loader import load_bvh
+            geometry.bvh = load_bvh(geometry)
+        self.packed = PackedGeometry(geometry, wavelengths=wavelengths, times=times)
+        handle = ctypes.c_void_p()
+        _native.call('chr_geometry_create', ctypes.byref(self.packed.desc()), ctypes.byref(handle))
+        self._handle = handle
+        self.geometry = geometry
+        self.solid_id_map = ga.to_gpu(np.asarray(geometry.solid_id, dtype=np.uint32))
+        self.world_origin = self.packed.world_origin
+        self.world_scale = self.packed.world_scale
+        if print_usage:
+            self.print_device_usage()
+        logger.info(self.device_usage_str())
+
+    @property
+    def gpudata(self):
+        return self._handle.value
+
+    def device_bytes(self):
+        b = ctypes.c_uint64()
+        _native.call('chr_geometry_device_bytes', self._handle, ctypes.byref(b))
+        return b.value
+
+    def device_usage_str(self):
+        return 'device usage: geometry %s (%d triangles, %d BVH nodes)' % (
+            format_size(self.device_bytes()), len(self.packed.triangles), len(self.packed.nodes))
+
+    def print_device_usage(self):
+        print(self.device_usage_str())
+
+    def __del__(self):
+        h = getattr(self, '_handle', None)
+        if h is not None and h.value:
+            try:
+                _native.lib().chr_geometry_destroy(h)
+            except Exception:
+                pass
+            self._handle = ctypes.c_void_p()

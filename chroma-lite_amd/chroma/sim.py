@@ -1,0 +1,151 @@
+"""Simulation driver (drop-in for reference chroma/sim.py:22-282).
+
+Batches events (never splitting one), uploads photons, propagates them on the
+device with the reference's launch shape (nthreads_per_block=512,
+max_blocks=1024 -> 524,288 RNG slots) and splits the detected hits back into
+events.  Photon tracking and GPU-resident inputs are supported as in the
+reference.  run_daq needs the DAQ stage, which is not part of this build yet.
+"""
+import os
+import time
+from types import SimpleNamespace
+
+import numpy as np
+
+from chroma import event
+from chroma import gpu
+from chroma.gpu import gpuarray as ga
+from chroma.itertoolset import peek
+
+
+def pick_seed():
+    """A seed from the current time and process id."""
+    return int(time.time()) ^ (os.getpid() << 16) & 2 ** 32 - 1
+
+
+class Simulation(object):
+    def __init__(self, detector, seed=None, cuda_device=None, photon_tracking=False, nthreads_per_block=512,
+                 max_blocks=1024):
+        self.detector = detector
+        self.nthreads_per_block = nthreads_per_block
+        self.max_blocks = max_blocks
+        self.photon_tracking = photon_tracking
+        self.seed = pick_seed() if seed is None else seed
+        np.random.seed(self.seed & 0xFFFFFFFF)
+        self.context = gpu.create_cuda_context(cuda_device)
+        if hasattr(detector, 'num_channels'):
+            self.gpu_geometry = gpu.GPUDetector(detector)
+        else:
+            self.gpu_geometry = gpu.GPUGeometry(detector)
+        self.rng_states = gpu.get_rng_states(self.nthreads_per_block * self.max_blocks, seed=self.seed)
+        self.pdf_config = None
+
+    def _simulate_batch(self, batch_events, keep_photons_beg=False, keep_photons_end=False, keep_hits=True,
+                        keep_flat_hits=True, run_daq=False, max_steps=100, verbose=False):
+        t0 = time.time()
+        sources = [ev.photons_beg for ev in batch_events]
+        bounds = np.cumsum(np.concatenate([[0], [len(s) for s in sources]]))
+        src = self._stack_gpu_photon_sources(sources)
+        if src is None:
+            src = event.Photons.join(sources)
+        gpu_photons = gpu.GPUPhotons(src, copy_flags=True, copy_triangles=False, copy_weights=False)
+        tracking = gpu_photons.propagate(self.gpu_geometry, self.rng_states, nthreads_per_block=self.nthreads_per_block,
+                                         max_blocks=self.max_blocks, max_steps=max_steps, track=self.photon_tracking)
+        if verbose:
+            print('Batch took %0.2f s' % (time.time() - t0))
+        if keep_photons_end:
+            photons_end = gpu_photons.get()
+        has_channels = hasattr(self.detector, 'num_channels')
+        if has_channels and (keep_hits or keep_flat_hits):
+            batch_hits = gpu_photons.get_flat_hits(self.gpu_geometry)
+        if run_daq:
+            raise NotImplementedError('run_daq: the DAQ stage (reference chroma/gpu/daq.py) is not built yet')
+        for i, (ev, (start, end)) in enumerate(zip(batch_events, zip(bounds[:-1], bounds[1:]))):
+            if not keep_photons_beg:
+                ev.photons_beg = None
+            if self.photon_tracking:
+                step_ids, step_photons = tracking
+                tracks = [[] for _ in range(end - start)]
+                for ids, photons in zip(step_ids, step_photons):
+                    mask = (ids >= start) & (ids < end)
+                    if not mask.any():
+                        break
+                    sel = photons[mask]
+                    for k, pid in enumerate(ids[mask] - start):
+                        tracks[pid].append(sel[k])
+                ev.photon_tracks = [event.Photons.join(t, concatenate=False) if t else event.Photons()
+                                    for t in tracks]
+            if keep_photons_end:
+                ev.photons_end = photons_end[start:end]
+            if has_channels and (keep_hits or keep_flat_hits):
+                ev_hits = batch_hits[batch_hits.evidx == i]
+                if keep_hits:
+                    ev.hits = {int(ch): ev_hits[ev_hits.channel == ch] for ch in np.unique(ev_hits.channel)}
+                if keep_flat_hits:
+                    ev.flat_hits = ev_hits
+            yield ev
+
+    @staticmethod
+    def _is_gpu_photon_source(photons):
+        return all(isinstance(getattr(photons, f, None), ga.GPUArray)
+                   for f in ('pos', 'dir', 'pol', 'wavelengths', 't', 'evidx', 'flags'))
+
+    @classmethod
+    def _stack_gpu_photon_sources(cls, sources):
+        """Join GPU-resident inputs on the device (sim.py:171-223)."""
+        if not sources or not all(cls._is_gpu_photon_source(s) for s in sources):
+            return None
+        total = sum(len(s) for s in sources)
+        fields = ('pos', 'dir', 'pol', 'wavelengths', 't', 'evidx', 'flags')
+        out = {}
+        for f in fields:
+            dest = ga.empty(total, getattr(sources[0], f).dtype)
+            off = 0
+            for s in sources:
+                n = len(s)
+                if n:
+                    dest[off:off + n].tensor.copy_(getattr(s, f)[:n].tensor)
+                    off += n
+            out[f] = dest
+        out['true_nphotons'] = total
+        return SimpleNamespace(**out)
+
+    def simulate(self, iterable, keep_photons_beg=False, keep_photons_end=False, keep_hits=True,
+                 keep_flat_hits=True, run_daq=False, max_steps=1000, photons_per_batch=1000000):
+        if isinstance(iterable, event.Photons):
+            first, iterable = iterable, [iterable]
+        else:
+            first, iterable = peek(iterable)
+        if isinstance(first, event.Photons):
+            iterable = (event.Event(photons_beg=x) for x in iterable)
+        elif isinstance(first, event.Vertex):
+            raise NotImplementedError('Vertex input not supported in Chroma')
+        nphotons = 0
+        batch = []
+        kw = dict(keep_photons_beg=keep_photons_beg, keep_photons_end=keep_photons_end, keep_hits=keep_hits,
+                  keep_flat_hits=keep_flat_hits, run_daq=run_daq, max_steps=max_steps)
+        for ev in iterable:
+            ev.nphotons = len(ev.photons_beg)
+            idx = len(batch)
+            evidx = getattr(ev.photons_beg, 'evidx', None)
+            if evidx is not None:
+                if isinstance(evidx, ga.GPUArray):
+                    if ev.nphotons > 0:
+                        evidx[:ev.nphotons].fill(np.uint32(idx))
+                else:
+                    evidx[:ev.nphotons] = np.uint32(idx)
+            nphotons += ev.nphotons
+            batch.append(ev)
+            if nphotons >= photons_per_batch:
+                yield from self._simulate_batch(batch, **kw)
+                nphotons, batch = 0, []
+        if batch:
+            yield from self._simulate_batch(batch, **kw)
+
+    def __del__(self):
+        ctx = getattr(self, 'context', None)
+        if ctx is not None:
+            try:
+                ctx.pop()
+            except Exception:
+                pass

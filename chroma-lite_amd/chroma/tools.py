@@ -55,7 +55,8 @@ def offset(points, x, tol=1e-9):
                    + [points[-1] - (points[-2] - points[-1])])
 
     def shifted(p, q):
-        n = np.cross(q - p, (0, 0, 1))[:2]
+        d = q - p
+        n = np.array([d[1], -d[0]])         # (d, 0) x z-hat, exactly
         n /= np.linalg.norm(n)
         n *= x
         return p + n, q + n

@@ -1,0 +1,70 @@
+// device_geometry.h -- HBM layout of a geometry on gfx950.
+//
+// Reference layout (chroma/cuda/geometry_types.h:124-139, gpu/geometry.py:389-520):
+// a Geometry struct of pointers, copied into __shared__ by every block,
+// double pointer chase (materials[i]->refractive_index[j]) per table lookup,
+// triangles as index triples into a vertex array (4 dependent loads/triangle).
+//
+// Here:
+//  * DevGeom is passed BY VALUE as a kernel argument (lands in SGPRs, no
+//    per-block copy);
+//  * BVH nodes stay the reference's 16-byte quantised uint4 (so the traversal
+//    order, and therefore nearest-hit tie-breaking, is the reference's);
+//  * triangles are de-indexed into 48-byte records of three float4:
+//        (v0.x v0.y v0.z e1.x) (e1.y e1.z e2.x e2.y) (e2.z e3.x e3.y e3.z)
+//    with e1 = v1-v0, e2 = v2-v0 (the Moller-Trumbore edges, intersect.h:26-101)
+//    and e3 = v2-v1 (the normal edge of fill_state, photon.h:365-367), all
+//    computed on the host in float32 exactly as the kernel would: one
+//    16-byte-aligned 48-byte gather per tested triangle instead of 12+3x12;
+//  * every wavelength / time table lives in one float blob (each table padded
+//    by one element, see chr_geometry_desc), addressed by 32-bit offsets held
+//    in small DevMaterial / DevSurface records.
+#pragma once
+
+#include <cstdint>
+
+#include "../../include/chroma_amd.h"
+
+namespace chr {
+
+struct DevMaterial {
+    uint32_t num_comp;
+    uint32_t refractive_index, absorption_length, scattering_length;       // blob offsets
+    uint32_t comp_reemission_prob, comp_reemission_wvl_cdf, comp_reemission_time_cdf,
+        comp_absorption_length;                                            // first component
+};
+
+struct DevSurface {
+    uint32_t present, model, transmissive;
+    float thickness;
+    uint32_t detect, absorb, reemit, reflect_diffuse, reflect_specular, eta, k, reemission_cdf;
+    uint32_t dichroic_nangles, dichroic_angles, dichroic_reflect, dichroic_transmit;
+    uint32_t angular_nangles, angular_angles, angular_transmit, angular_reflect_specular,
+        angular_reflect_diffuse;
+};
+
+struct DevGeom {
+    const uint4 *nodes;
+    const float4 *tri;               // 3 float4 per triangle
+    const uint32_t *material_codes;
+    const float *tables;
+    const DevMaterial *materials;
+    const DevSurface *surfaces;
+    const chr_wireplane_desc *wireplanes;
+    float ox, oy, oz, scale;         // world_origin, world_scale
+    uint32_t nnodes, ntriangles, nwireplanes;
+    uint32_t wl_n;
+    float wl_start, wl_step;
+    uint32_t t_n;
+    float t_start, t_step;
+};
+
+}  // namespace chr
+
+struct chr_geometry {
+    chr::DevGeom dev;
+    int device;
+    uint64_t bytes;
+    void *allocs[8];
+    int nallocs;
+};

@@ -1,0 +1,220 @@
+// geometry.cpp -- chr_geometry_create: upload a flattened, BVH-indexed
+// geometry into HBM in the gfx950 traversal layout (device_geometry.h).
+// Replaces GPUGeometry.__init__'s device uploads (chroma/gpu/geometry.py:14-526)
+// and the Material/Surface/WirePlane make_gpu_struct packing.
+#include <hip/hip_runtime_api.h>
+
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/chroma_amd.h"
+#include "common.h"
+#include "device_geometry.h"
+
+namespace chr {
+std::string &last_error() {
+    static thread_local std::string msg;
+    return msg;
+}
+}  // namespace chr
+
+extern "C" const char *chr_last_error(void) { return chr::last_error().c_str(); }
+extern "C" int chr_version(void) { return 1; }
+
+namespace {
+
+struct Blob {
+    std::vector<float> data;
+    // append n+1 floats (table + its pad element) and return the offset
+    uint32_t add(const float *p, uint32_t n_with_pad) {
+        uint32_t off = (uint32_t)data.size();
+        if (p) data.insert(data.end(), p, p + n_with_pad);
+        else data.insert(data.end(), n_with_pad, 0.0f);
+        return off;
+    }
+};
+
+int dev_upload(chr_geometry *g, const void *host, size_t bytes, void **dptr) {
+    void *p = nullptr;
+    if (bytes == 0) bytes = 16;
+    hipError_t e = hipMalloc(&p, bytes);
+    if (e != hipSuccess) return chr::fail(CHR_ERR_NOMEM, "hipMalloc(%zu) failed: %s", bytes, hipGetErrorString(e));
+    g->allocs[g->nallocs++] = p;
+    g->bytes += bytes;
+    if (host) {
+        e = hipMemcpy(p, host, bytes, hipMemcpyHostToDevice);
+        if (e != hipSuccess) return chr::fail(CHR_ERR_HIP, "hipMemcpy H2D failed: %s", hipGetErrorString(e));
+    }
+    *dptr = p;
+    return CHR_OK;
+}
+
+}  // namespace
+
+extern "C" int chr_geometry_destroy(chr_geometry *g) {
+    if (!g) return CHR_OK;
+    int prev = 0;
+    hipGetDevice(&prev);
+    hipSetDevice(g->device);
+    for (int i = 0; i < g->nallocs; ++i) hipFree(g->allocs[i]);
+    hipSetDevice(prev);
+    delete g;
+    return CHR_OK;
+}
+
+extern "C" int chr_geometry_device_bytes(const chr_geometry *g, uint64_t *bytes) {
+    if (!g || !bytes) return chr::fail(CHR_ERR_INVALID, "chr_geometry_device_bytes: null argument");
+    *bytes = g->bytes;
+    return CHR_OK;
+}
+
+extern "C" int chr_geometry_create(const chr_geometry_desc *d, chr_geometry **out) {
+    if (!d || !out) return chr::fail(CHR_ERR_INVALID, "chr_geometry_create: null argument");
+    if (d->ntriangles == 0 || d->nnodes == 0 || !d->h_vertices || !d->h_triangles || !d->h_nodes ||
+        !d->h_material_codes)
+        return chr::fail(CHR_ERR_INVALID, "chr_geometry_create: empty mesh or BVH");
+    if (d->nmaterials == 0 || !d->materials) return chr::fail(CHR_ERR_INVALID, "chr_geometry_create: no materials");
+    if (d->nwireplanes && !d->wireplanes) return chr::fail(CHR_ERR_INVALID, "chr_geometry_create: wireplanes NULL");
+    if (d->wavelength_n < 2 || d->time_n < 2) return chr::fail(CHR_ERR_INVALID, "chr_geometry_create: grids need >= 2 points");
+    // validate triangle indices / BVH child ranges up front: an out-of-range
+    // index would otherwise become an out-of-bounds read inside the kernel.
+    for (size_t i = 0; i < (size_t)d->ntriangles * 3; ++i)
+        if (d->h_triangles[i] >= d->nvertices)
+            return chr::fail(CHR_ERR_INVALID, "triangle %zu references vertex %u >= %u", i / 3, d->h_triangles[i], d->nvertices);
+    for (size_t i = 0; i < d->nnodes; ++i) {
+        const uint32_t w = d->h_nodes[4 * i + 3];
+        const uint32_t nc = w >> 28, child = w & 0x0FFFFFFFu;
+        if (nc == 0 ? child >= d->ntriangles : (uint64_t)child + nc > d->nnodes)
+            return chr::fail(CHR_ERR_INVALID, "BVH node %zu has child %u nchild %u out of range", i, child, nc);
+    }
+    for (size_t t = 0; t < d->ntriangles; ++t) {
+        const uint32_t c = d->h_material_codes[t];
+        int m1 = (c >> 24) & 0xFF, m2 = (c >> 16) & 0xFF, s = (c >> 8) & 0xFF;
+        if (m1 >= (int)d->nmaterials || m2 >= (int)d->nmaterials)
+            return chr::fail(CHR_ERR_INVALID, "triangle %zu: material index out of range", t);
+        if (s != 0xFF && (s >= (int)d->nsurfaces || !d->surfaces || !d->surfaces[s].present))
+            return chr::fail(CHR_ERR_INVALID, "triangle %zu: surface %d missing", t, s);
+    }
+
+    chr_geometry *g = new (std::nothrow) chr_geometry();
+    if (!g) return chr::fail(CHR_ERR_NOMEM, "chr_geometry_create: host allocation failed");
+    std::memset(g, 0, sizeof(*g));
+    hipGetDevice(&g->device);
+    int rc = CHR_OK;
+    try {
+        chr::DevGeom &dg = g->dev;
+        dg.ox = d->world_origin[0]; dg.oy = d->world_origin[1]; dg.oz = d->world_origin[2];
+        dg.scale = d->world_scale;
+        dg.nnodes = d->nnodes; dg.ntriangles = d->ntriangles; dg.nwireplanes = d->nwireplanes;
+        dg.wl_n = d->wavelength_n; dg.wl_start = d->wavelength_start; dg.wl_step = d->wavelength_step;
+        dg.t_n = d->time_n; dg.t_start = d->time_start; dg.t_step = d->time_step;
+
+        void *p;
+        if ((rc = dev_upload(g, d->h_nodes, (size_t)d->nnodes * 16, &p))) throw rc;
+        dg.nodes = (const uint4 *)p;
+
+        // de-indexed triangle records: v0, e1 = v1-v0, e2 = v2-v0, e3 = v2-v1
+        std::vector<float> tri((size_t)d->ntriangles * 12);
+        const float *v = d->h_vertices;
+#pragma omp parallel for schedule(static)
+        for (int64_t t = 0; t < (int64_t)d->ntriangles; ++t) {
+            const uint32_t *ix = d->h_triangles + 3 * t;
+            const float *a = v + 3 * (size_t)ix[0], *b = v + 3 * (size_t)ix[1], *c = v + 3 * (size_t)ix[2];
+            float *r = tri.data() + 12 * t;
+            r[0] = a[0]; r[1] = a[1]; r[2] = a[2];
+            r[3] = b[0] - a[0]; r[4] = b[1] - a[1]; r[5] = b[2] - a[2];
+            r[6] = c[0] - a[0]; r[7] = c[1] - a[1]; r[8] = c[2] - a[2];
+            r[9] = c[0] - b[0]; r[10] = c[1] - b[1]; r[11] = c[2] - b[2];
+        }
+        if ((rc = dev_upload(g, tri.data(), tri.size() * sizeof(float), &p))) throw rc;
+        dg.tri = (const float4 *)p;
+        std::vector<float>().swap(tri);
+
+        if ((rc = dev_upload(g, d->h_material_codes, (size_t)d->ntriangles * 4, &p))) throw rc;
+        dg.material_codes = (const uint32_t *)p;
+
+        Blob blob;
+        const uint32_t W1 = d->wavelength_n + 1, T1 = d->time_n + 1;
+        std::vector<chr::DevMaterial> mats(d->nmaterials);
+        for (uint32_t i = 0; i < d->nmaterials; ++i) {
+            const chr_material_desc &m = d->materials[i];
+            chr::DevMaterial &o = mats[i];
+            if (!m.refractive_index || !m.absorption_length || !m.scattering_length) {
+                rc = chr::fail(CHR_ERR_INVALID, "material %u: missing table", i);
+                throw rc;
+            }
+            o.num_comp = m.num_comp;
+            o.refractive_index = blob.add(m.refractive_index, W1);
+            o.absorption_length = blob.add(m.absorption_length, W1);
+            o.scattering_length = blob.add(m.scattering_length, W1);
+            o.comp_reemission_prob = (uint32_t)blob.data.size();
+            for (uint32_t c = 0; c < m.num_comp; ++c) blob.add(m.comp_reemission_prob + c * W1, W1);
+            o.comp_reemission_wvl_cdf = (uint32_t)blob.data.size();
+            for (uint32_t c = 0; c < m.num_comp; ++c) blob.add(m.comp_reemission_wvl_cdf + c * W1, W1);
+            o.comp_reemission_time_cdf = (uint32_t)blob.data.size();
+            for (uint32_t c = 0; c < m.num_comp; ++c) blob.add(m.comp_reemission_time_cdf + c * T1, T1);
+            o.comp_absorption_length = (uint32_t)blob.data.size();
+            for (uint32_t c = 0; c < m.num_comp; ++c) blob.add(m.comp_absorption_length + c * W1, W1);
+        }
+        std::vector<chr::DevSurface> surfs(d->nsurfaces > 0 ? d->nsurfaces : 1);
+        std::memset(surfs.data(), 0, surfs.size() * sizeof(chr::DevSurface));
+        for (uint32_t i = 0; i < d->nsurfaces; ++i) {
+            const chr_surface_desc &s = d->surfaces[i];
+            chr::DevSurface &o = surfs[i];
+            o.present = s.present ? 1u : 0u;
+            if (!s.present) continue;
+            o.model = s.model; o.transmissive = s.transmissive; o.thickness = s.thickness;
+            o.detect = blob.add(s.detect, W1);
+            o.absorb = blob.add(s.absorb, W1);
+            o.reemit = blob.add(s.reemit, W1);
+            o.reflect_diffuse = blob.add(s.reflect_diffuse, W1);
+            o.reflect_specular = blob.add(s.reflect_specular, W1);
+            o.eta = blob.add(s.eta, W1);
+            o.k = blob.add(s.k, W1);
+            o.reemission_cdf = blob.add(s.reemission_cdf, W1);
+            if (s.model == CHR_SURFACE_DICHROIC && s.dichroic_nangles == 0) {
+                rc = chr::fail(CHR_ERR_INVALID, "surface %u: dichroic model without DichroicProps", i);
+                throw rc;
+            }
+            if (s.model == CHR_SURFACE_ANGULAR && s.angular_nangles == 0) {
+                rc = chr::fail(CHR_ERR_INVALID, "surface %u: angular model without AngularProps", i);
+                throw rc;
+            }
+            o.dichroic_nangles = s.dichroic_nangles;
+            if (s.dichroic_nangles) {
+                o.dichroic_angles = blob.add(s.dichroic_angles, s.dichroic_nangles);
+                o.dichroic_reflect = (uint32_t)blob.data.size();
+                blob.data.insert(blob.data.end(), s.dichroic_reflect, s.dichroic_reflect + (size_t)s.dichroic_nangles * W1);
+                o.dichroic_transmit = (uint32_t)blob.data.size();
+                blob.data.insert(blob.data.end(), s.dichroic_transmit, s.dichroic_transmit + (size_t)s.dichroic_nangles * W1);
+            }
+            o.angular_nangles = s.angular_nangles;
+            if (s.angular_nangles) {
+                o.angular_angles = blob.add(s.angular_angles, s.angular_nangles);
+                o.angular_transmit = blob.add(s.angular_transmit, s.angular_nangles);
+                o.angular_reflect_specular = blob.add(s.angular_reflect_specular, s.angular_nangles);
+                o.angular_reflect_diffuse = blob.add(s.angular_reflect_diffuse, s.angular_nangles);
+            }
+        }
+        if ((rc = dev_upload(g, blob.data.data(), blob.data.size() * 4, &p))) throw rc;
+        dg.tables = (const float *)p;
+        if ((rc = dev_upload(g, mats.data(), mats.size() * sizeof(chr::DevMaterial), &p))) throw rc;
+        dg.materials = (const chr::DevMaterial *)p;
+        if ((rc = dev_upload(g, surfs.data(), surfs.size() * sizeof(chr::DevSurface), &p))) throw rc;
+        dg.surfaces = (const chr::DevSurface *)p;
+        if (d->nwireplanes) {
+            if ((rc = dev_upload(g, d->wireplanes, (size_t)d->nwireplanes * sizeof(chr_wireplane_desc), &p))) throw rc;
+            dg.wireplanes = (const chr_wireplane_desc *)p;
+        }
+    } catch (int code) {
+        chr_geometry_destroy(g);
+        return code;
+    } catch (const std::bad_alloc &) {
+        chr_geometry_destroy(g);
+        return chr::fail(CHR_ERR_NOMEM, "chr_geometry_create: host allocation failed");
+    }
+    *out = g;
+    return CHR_OK;
+}

@@ -1,0 +1,1340 @@
+// propagate.hip -- gfx950 photon propagation kernels + their C ABI.
+//
+// Hot path: the `propagate` kernel of the reference (chroma/cuda/propagate.cu:
+// 254-366) with everything it inlines from photon.h (fill_state, propagate_to_
+// boundary, propagate_at_surface, propagate_at_boundary), mesh.h
+// (intersect_mesh) and intersect.h.  Restructured for CDNA4:
+//   * one work-item per queue slot, 256-thread workgroups (4 waves of 64);
+//   * the BVH walk keeps the reference's DFS order and 1000-entry stack
+//     semantics, but the top STACK_LDS entries live in LDS (lane-strided, bank
+//     conflict free) and only deeper entries spill to private scratch;
+//   * triangles are fetched as one 48-byte de-indexed record (device_geometry.h);
+//   * the RNG state (cuRAND-compatible XORWOW) sits in VGPRs for the whole
+//     launch; slot states are stored SoA so the six words load/store coalesced;
+//   * survivors are compacted with a wave64 ballot mask per 64 slots, an
+//     exclusive scan of the mask popcounts and an order-preserving scatter
+//     (the reference's warp-atomic enqueue is nondeterministic);
+//   * all transcendental math is include/chroma_fmath.h, bit-identical to the
+//     CPU oracle.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <vector>
+
+#include "../../include/chroma_amd.h"
+#include "../../include/chroma_fmath.h"
+#include "../../include/chroma_rng.h"
+#include "common.h"
+#include "device_geometry.h"
+#include "device_math.h"
+
+namespace chr {
+
+constexpr int BLOCK = 256;
+constexpr int STACK_SIZE = 1000;   // mesh.h:10
+constexpr int STACK_LDS = 24;      // entries kept in LDS per work-item
+constexpr uint32_t DEAD_MASK = CHR_NO_HIT | CHR_BULK_ABSORB | CHR_SURFACE_DETECT | CHR_SURFACE_ABSORB | CHR_NAN_ABORT;
+constexpr float WEIGHT_LOWER_THRESHOLD = 0.0001f;
+constexpr float SPEED_OF_LIGHT = 299.792458f;
+constexpr float PI_F = 3.141592653589793f;
+// float thresholds equivalent to the reference's float-vs-double compares
+// (intersect.h:259-267): (double)u < -1e-6, (double)u > 1+1e-6, (double)t > 1e-6
+constexpr float T_NEG_EPS = -9.99999997e-07f;
+constexpr float T_ONE_EPS = 1.00000095367431640625f;
+constexpr float T_POS_EPS = 9.99999997e-07f;
+
+enum { BREAK = 0, CONTINUE = 1, PASS = 2 };
+
+struct Photon {
+    V3 pos, dir, pol;
+    float wavelength, time, weight;
+    uint32_t history;   // holds a 16-bit value (photon.h:29)
+    int last_hit;
+};
+
+struct State {
+    V3 normal;
+    float n1, n2, absorption_length, scattering_length, distance;
+    int material1, surface_index;
+};
+
+struct Stack {
+    uint32_t *lds;      // this work-item's column: entry i at lds[i * BLOCK]
+    uint32_t spill[STACK_SIZE - STACK_LDS];
+};
+
+__device__ __forceinline__ void stack_put(Stack &s, int i, uint32_t v) {
+    if (i < STACK_LDS) s.lds[i * BLOCK] = v;
+    else s.spill[i - STACK_LDS] = v;
+}
+__device__ __forceinline__ uint32_t stack_get(const Stack &s, int i) {
+    return (i < STACK_LDS) ? s.lds[i * BLOCK] : s.spill[i - STACK_LDS];
+}
+
+// ---------------------------------------------------------------- geometry.h
+__device__ __forceinline__ void node_bounds(const DevGeom &g, uint4 n, V3 &lo, V3 &hi) {
+    lo = v3(__builtin_fmaf((float)(n.x & 0xFFFFu), g.scale, g.ox), __builtin_fmaf((float)(n.y & 0xFFFFu), g.scale, g.oy),
+            __builtin_fmaf((float)(n.z & 0xFFFFu), g.scale, g.oz));
+    hi = v3(__builtin_fmaf((float)(n.x >> 16), g.scale, g.ox), __builtin_fmaf((float)(n.y >> 16), g.scale, g.oy),
+            __builtin_fmaf((float)(n.z >> 16), g.scale, g.oz));
+}
+
+__device__ __forceinline__ float interp_property(const DevGeom &g, float x, const float *fp) {
+    const float start = g.wl_start, step = g.wl_step;
+    const int n = (int)g.wl_n;
+    if (x < start) return fp[0];
+    if (x > __builtin_fmaf((float)(n - 1), step, start)) return fp[n - 1];
+    const int jl = (int)((x - start) / step);
+    const float base = __builtin_fmaf((float)jl, step, start);
+    return fp[jl] + ((x - base) * (fp[jl + 1] - fp[jl])) / step;
+}
+
+__device__ float interp_idx(float x, int n, const float *xp) {
+    int lower = 0, upper = n - 1;
+    if (x <= xp[lower]) return (float)lower;
+    if (x >= xp[upper]) return (float)upper;
+    while (lower < upper - 1) {
+        int half = (lower + upper) / 2;
+        if (x < xp[half]) upper = half; else lower = half;
+    }
+    float dx = xp[upper] - xp[lower];
+    return (float)((double)lower + (double)(x - xp[lower]) / (double)dx);
+}
+
+// ---------------------------------------------------------------- random.h
+__device__ __forceinline__ V3 uniform_sphere(chr_xorwow &s) {
+    const float theta = chr_uniform(&s, 0.0f, 2 * PI_F);
+    const float u = chr_uniform(&s, -1.0f, 1.0f);
+    const float c = chr_sqrtf(__builtin_fmaf(-u, u, 1.0f));
+    float st, ct;
+    chr_sincosf(theta, &st, &ct);
+    return v3(c * ct, c * st, u);
+}
+
+__device__ float sample_cdf(chr_xorwow &rng, int ncdf, float x0, float delta, const float *cdf_y) {
+    const float u = chr_uniform01(&rng);
+    int lower = 0, upper = ncdf - 1;
+    while (lower < upper - 1) {
+        int half = (lower + upper) / 2;
+        if (u < cdf_y[half]) upper = half; else lower = half;
+    }
+    const float dcy = cdf_y[upper] - cdf_y[lower];
+    return __builtin_fmaf(delta, (float)lower, x0) + (delta * (u - cdf_y[lower])) / dcy;
+}
+
+// ---------------------------------------------------------------- intersect.h / mesh.h
+__device__ __forceinline__ bool intersect_box(V3 noid, V3 inv, V3 lo, V3 hi, float &dist) {
+    float tmin = 0.0f, tmax = __builtin_inff();
+    if (chr_isfinite(inv.x)) {
+        const float t0 = __builtin_fmaf(lo.x, inv.x, noid.x), t1 = __builtin_fmaf(hi.x, inv.x, noid.x);
+        tmin = fmax_(tmin, fmin_(t0, t1)); tmax = fmin_(tmax, fmax_(t0, t1));
+    }
+    if (chr_isfinite(inv.y)) {
+        const float t0 = __builtin_fmaf(lo.y, inv.y, noid.y), t1 = __builtin_fmaf(hi.y, inv.y, noid.y);
+        tmin = fmax_(tmin, fmin_(t0, t1)); tmax = fmin_(tmax, fmax_(t0, t1));
+    }
+    if (chr_isfinite(inv.z)) {
+        const float t0 = __builtin_fmaf(lo.z, inv.z, noid.z), t1 = __builtin_fmaf(hi.z, inv.z, noid.z);
+        tmin = fmax_(tmin, fmin_(t0, t1)); tmax = fmin_(tmax, fmax_(t0, t1));
+    }
+    if (tmin > tmax) return false;
+    dist = tmin;
+    return true;
+}
+
+// Moller-Trumbore on a de-indexed record (v0, e1, e2)
+__device__ __forceinline__ bool intersect_triangle(V3 o, V3 d, V3 v0, V3 e1, V3 e2, float &distance) {
+    const V3 h = cross(d, e2);
+    const float a = dot(e1, h);
+    if (a > -1.19209290e-7f && a < 1.19209290e-7f) return false;
+    const float f = 1.0f / a;
+    const V3 s = o - v0;
+    const float u = f * dot(s, h);
+    if (u < T_NEG_EPS || u > T_ONE_EPS) return false;
+    const V3 q = cross(s, e1);
+    const float v = f * dot(d, q);
+    if (v < T_NEG_EPS || u + v > T_ONE_EPS) return false;
+    const float t = f * dot(e2, q);
+    if (t > T_POS_EPS && t < __builtin_inff()) {
+        distance = t;
+        return true;
+    }
+    return false;
+}
+
+// mesh.h:45-126 -- nearest triangle != last_hit; reference DFS order.
+__device__ int intersect_mesh(const DevGeom &g, V3 o, V3 d, float &min_distance, int last_hit, Stack &st,
+                              uint32_t &overflow) {
+    int triangle_index = -1;
+    min_distance = -1.0f;
+    const V3 noid = v3(-o.x / d.x, -o.y / d.y, -o.z / d.z);
+    const V3 inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    const uint4 root = g.nodes[0];
+    {
+        V3 lo, hi;
+        float bd;
+        node_bounds(g, root, lo, hi);
+        if (!intersect_box(noid, inv, lo, hi, bd)) return -1;
+    }
+    stack_put(st, 0, root.w);
+    int curr = 0;
+    const uint32_t last = (uint32_t)last_hit;
+    while (curr >= 0) {
+        const uint32_t w = stack_get(st, curr);
+        curr--;
+        const uint32_t first = w & 0x0FFFFFFFu;
+        const uint32_t end = first + (w >> 28);
+        for (uint32_t i = first; i < end; ++i) {
+            const uint4 node = g.nodes[i];
+            V3 lo, hi;
+            node_bounds(g, node, lo, hi);
+            float bd;
+            if (!intersect_box(noid, inv, lo, hi, bd)) continue;
+            if (min_distance >= 0.0f && bd > min_distance) continue;
+            const uint32_t child = node.w & 0x0FFFFFFFu;
+            if ((node.w >> 28) == 0) {
+                if (child != last) {
+                    const float4 r0 = g.tri[3 * (size_t)child], r1 = g.tri[3 * (size_t)child + 1],
+                                 r2 = g.tri[3 * (size_t)child + 2];
+                    float dist;
+                    if (intersect_triangle(o, d, v3(r0.x, r0.y, r0.z), v3(r0.w, r1.x, r1.y), v3(r1.z, r1.w, r2.x), dist)) {
+                        if (triangle_index == -1 || dist < min_distance) {
+                            triangle_index = (int)child;
+                            min_distance = dist;
+                        }
+                    }
+                }
+            } else {
+                if (curr + 1 >= STACK_SIZE) {
+                    overflow++;
+                    return triangle_index;
+                }
+                curr++;
+                stack_put(st, curr, node.w);
+            }
+        }
+    }
+    return triangle_index;
+}
+
+// ---------------------------------------------------------------- photon.h
+__device__ __forceinline__ int convert(int c) { return (c & 0x80) ? (int)(0xFFFFFF00u | (uint32_t)c) : c; }
+__device__ __forceinline__ float get_theta(V3 a, V3 b) { return chr_acosf(fmax_(-1.0f, fmin_(1.0f, dot(a, b)))); }
+
+// analytic wire planes (photon.h:108-270), FP64, rare path
+__device__ __noinline__ void wireplanes(const DevGeom &g, const Photon &p, float best_distance, int &a_surface,
+                                        int &a_inner, int &a_outer, V3 &a_normal_raw, float &a_dot_raw,
+                                        float &a_distance) {
+    for (int ip = 0; ip < (int)g.nwireplanes; ++ip) {
+        const chr_wireplane_desc &wp = g.wireplanes[ip];
+        const double ux = wp.u[0], uy = wp.u[1], uz = wp.u[2];
+        const double vx0 = wp.v[0], vy0 = wp.v[1], vz0 = wp.v[2];
+        const double un = 1.0 / sqrt(ux * ux + uy * uy + uz * uz);
+        const double ux1 = ux * un, uy1 = uy * un, uz1 = uz * un;
+        const double vdotu = vx0 * ux1 + vy0 * uy1 + vz0 * uz1;
+        const double vx1 = vx0 - vdotu * ux1, vy1 = vy0 - vdotu * uy1, vz1 = vz0 - vdotu * uz1;
+        const double vn = 1.0 / sqrt(vx1 * vx1 + vy1 * vy1 + vz1 * vz1);
+        const double vx = vx1 * vn, vy = vy1 * vn, vz = vz1 * vn;
+        const double nx = uy1 * vz - uz1 * vy, ny = uz1 * vx - ux1 * vz, nz = ux1 * vy - uy1 * vx;
+        const V3 w = p.pos - v3(wp.origin[0], wp.origin[1], wp.origin[2]);
+        const double du = (double)p.dir.x * ux1 + (double)p.dir.y * uy1 + (double)p.dir.z * uz1;
+        const double dv = (double)p.dir.x * vx + (double)p.dir.y * vy + (double)p.dir.z * vz;
+        const double dn = (double)p.dir.x * nx + (double)p.dir.y * ny + (double)p.dir.z * nz;
+        const double wu = (double)w.x * ux1 + (double)w.y * uy1 + (double)w.z * uz1;
+        const double wv0 = (double)w.x * vx + (double)w.y * vy + (double)w.z * vz - (double)wp.v0;
+        const double wn0 = (double)w.x * nx + (double)w.y * ny + (double)w.z * nz;
+        double t_in = -1.0e300, t_out = 1.0e300;
+        if (fabs(du) < 1e-15) {
+            if (wu < (double)wp.umin || wu > (double)wp.umax) continue;
+        } else {
+            double t1 = ((double)wp.umin - wu) / du, t2 = ((double)wp.umax - wu) / du;
+            if (t1 > t2) { double tmp = t1; t1 = t2; t2 = tmp; }
+            if (t1 > t_in) t_in = t1;
+            if (t2 < t_out) t_out = t2;
+            if (t_in > t_out) continue;
+        }
+        const double pitch = (double)wp.pitch;
+        const double inv_pitch = (pitch != 0.0) ? (1.0 / pitch) : 0.0;
+        const double wire_radius = (double)wp.radius;
+        const double wire_thickness = 2.0 * wire_radius;
+        const double pad_v = 0.5 * wire_thickness + 1e-6, pad_n = 0.5 * wire_thickness + 1e-6;
+        const int kmin = (int)ceil(((double)wp.vmin - (double)wp.v0) / pitch);
+        const int kmax = (int)floor(((double)wp.vmax - (double)wp.v0) / pitch);
+        const double A = dv * dv + dn * dn;
+        int k_start = kmin, k_stop = kmax;
+        if (kmin <= kmax) {
+            const double t_eps = 1.0e-4;
+            double t_lo = fmax(t_in, t_eps), t_hi = t_out;
+            const double best_cap = (double)best_distance;
+            if (best_cap < t_hi) t_hi = best_cap;
+            if (fabs(dn) > 1e-12) {
+                double tn1 = (-pad_n - wn0) / dn, tn2 = (pad_n - wn0) / dn;
+                if (tn1 > tn2) { double tmp = tn1; tn1 = tn2; tn2 = tmp; }
+                t_lo = fmax(t_lo, tn1); t_hi = fmin(t_hi, tn2);
+            } else if (fabs(wn0) > pad_n) continue;
+            if (t_hi < t_lo) continue;
+            if (fabs(dn) <= 1e-12 && fabs(dv) > 1e-12) {
+                const double t_span = (pitch + wire_thickness) / fabs(dv);
+                t_hi = fmin(t_hi, t_lo + t_span);
+            }
+            const double v_entry = wv0 + dv * t_lo, v_exit = wv0 + dv * t_hi;
+            double v_lo = fmin(v_entry, v_exit) - pad_v, v_hi = fmax(v_entry, v_exit) + pad_v;
+            if (wv0 - pad_v < v_lo) v_lo = wv0 - pad_v;
+            if (wv0 + pad_v > v_hi) v_hi = wv0 + pad_v;
+            long long k_lo = (long long)floor(v_lo * inv_pitch), k_hi = (long long)ceil(v_hi * inv_pitch);
+            if (k_lo < kmin) k_lo = kmin;
+            if (k_hi > kmax) k_hi = kmax;
+            if (k_lo > k_hi) continue;
+            k_start = (int)k_lo; k_stop = (int)k_hi;
+        }
+        for (int k = k_start; k <= k_stop; ++k) {
+            const double wv = wv0 - (double)k * pitch;
+            const double B = wv * dv + wn0 * dn;
+            const double C = wv * wv + wn0 * wn0 - wire_radius * wire_radius;
+            const double disc = B * B - A * C;
+            if (disc < 0.0) continue;
+            const double sq = sqrt(disc);
+            const double t_small = (-B - sq) / A, t_large = (-B + sq) / A;
+            const double t_min = 1.0e-4;
+            const double r2_wire = wire_radius * wire_radius;
+            const double r2_0 = wv * wv + wn0 * wn0;
+            const double eps0 = fmax(1e-18, 1e-12 * r2_wire);
+            double t;
+            if (r2_0 > r2_wire + eps0) { if (t_small <= t_min) continue; t = t_small; }
+            else if (r2_0 < r2_wire - eps0) { if (t_large <= t_min) continue; t = t_large; }
+            else t = t_min;
+            const double uc = wu + du * t;
+            if (uc < wp.umin || uc > wp.umax) continue;
+            if ((float)t >= a_distance) continue;
+            if (t < t_in || t > t_out) continue;
+            const double vn_hit = wv + dv * t, nn_hit = wn0 + dn * t;
+            const double len = sqrt(vn_hit * vn_hit + nn_hit * nn_hit);
+            if (len <= 0.0) continue;
+            const V3 nl = v3((float)((vn_hit / len) * vx + (nn_hit / len) * nx),
+                             (float)((vn_hit / len) * vy + (nn_hit / len) * ny),
+                             (float)((vn_hit / len) * vz + (nn_hit / len) * nz));
+            a_distance = (float)t;
+            a_surface = wp.surface_index;
+            a_inner = wp.material_inner_index;
+            a_outer = wp.material_outer_index;
+            a_normal_raw = nl;
+            a_dot_raw = dot(nl, -p.dir);
+        }
+    }
+}
+
+// photon.h:87-397
+__device__ __forceinline__ void fill_state(const DevGeom &g, State &s, Photon &p, Stack &st, uint32_t &overflow) {
+    const int mesh_triangle = intersect_mesh(g, p.pos, p.dir, s.distance, p.last_hit, st, overflow);
+    int m1, m2;
+    bool use_analytic = false;
+    int a_surface = -1, a_inner = -1, a_outer = -1;
+    V3 a_normal_raw = v3(0.0f, 0.0f, 0.0f);
+    float a_dot_raw = 0.0f, a_distance = 1e30f;
+    if (g.nwireplanes > 0) {
+        const float best_distance = (mesh_triangle == -1) ? 1e30f : s.distance;
+        wireplanes(g, p, best_distance, a_surface, a_inner, a_outer, a_normal_raw, a_dot_raw, a_distance);
+        if (a_surface >= 0) use_analytic = ((double)a_distance + 1e-12 < (double)best_distance);
+    }
+    if (use_analytic) {
+        s.distance = a_distance;
+        s.surface_index = a_surface;
+        p.last_hit = -2;
+        if (a_dot_raw > 0.0f) { m1 = a_outer; m2 = a_inner; s.normal = a_normal_raw; }
+        else { m1 = a_inner; m2 = a_outer; s.normal = -a_normal_raw; }
+    } else if (mesh_triangle != -1) {
+        p.last_hit = mesh_triangle;
+        const float4 r0 = g.tri[3 * (size_t)mesh_triangle], r1 = g.tri[3 * (size_t)mesh_triangle + 1],
+                     r2 = g.tri[3 * (size_t)mesh_triangle + 2];
+        const uint32_t code = g.material_codes[mesh_triangle];
+        const int inner = convert(0xFF & (int)(code >> 24));
+        const int outer = convert(0xFF & (int)(code >> 16));
+        s.surface_index = convert(0xFF & (int)(code >> 8));
+        s.normal = normalize(cross(v3(r0.w, r1.x, r1.y), v3(r2.y, r2.z, r2.w)));
+        if (dot(s.normal, -p.dir) > 0.0f) { m1 = outer; m2 = inner; }
+        else { m1 = inner; m2 = outer; s.normal = -s.normal; }
+    } else {
+        p.last_hit = -1;
+        p.history |= CHR_NO_HIT;
+        return;
+    }
+    const DevMaterial &mat1 = g.materials[m1];
+    const DevMaterial &mat2 = g.materials[m2];
+    s.n1 = interp_property(g, p.wavelength, g.tables + mat1.refractive_index);
+    s.n2 = interp_property(g, p.wavelength, g.tables + mat2.refractive_index);
+    s.absorption_length = interp_property(g, p.wavelength, g.tables + mat1.absorption_length);
+    s.scattering_length = interp_property(g, p.wavelength, g.tables + mat1.scattering_length);
+    s.material1 = m1;
+}
+
+// photon.h:399-427
+__device__ V3 pick_new_direction(V3 axis, float theta, float phi) {
+    float st, ct, sp, cp;
+    chr_sincosf(theta, &st, &ct);
+    chr_sincosf(phi, &sp, &cp);
+    const float sat = chr_sqrtf(__builtin_fmaf(-axis.z, axis.z, 1.0f));
+    float cap, sap;
+    if (chr_isnan(sat) || sat < 0.00001f) { cap = 1.0f; sap = 0.0f; }
+    else { cap = axis.x / sat; sap = axis.y / sat; }
+    const float dx = __builtin_fmaf(st, __builtin_fmaf(axis.z * cp, cap, -(sp * sap)), ct * axis.x);
+    const float dy = __builtin_fmaf(st, __builtin_fmaf(cp * axis.z, sap, sp * cap), ct * axis.y);
+    const float dz = __builtin_fmaf(-(st * cp), sat, ct * axis.z);
+    return v3(dx, dy, dz);
+}
+
+// photon.h:429-453
+__device__ void rayleigh_scatter(Photon &p, chr_xorwow &rng) {
+    const float u = chr_uniform01(&rng);
+    float cos_theta = 2.0f * chr_cosf((chr_acosf(__builtin_fmaf(-2.0f, u, 1.0f)) - 2 * PI_F) / 3.0f);
+    if (cos_theta > 1.0f) cos_theta = 1.0f;
+    else if (cos_theta < -1.0f) cos_theta = -1.0f;
+    const float theta = chr_acosf(cos_theta);
+    const float phi = chr_uniform(&rng, 0.0f, 2.0f * PI_F);
+    p.dir = pick_new_direction(p.pol, theta, phi);
+    if (1.0f - chr_fabsf(cos_theta) < 1e-6f)
+        p.pol = pick_new_direction(p.pol, PI_F / 2.0f, phi);
+    else
+        p.pol = v3(__builtin_fmaf(-cos_theta, p.dir.x, p.pol.x), __builtin_fmaf(-cos_theta, p.dir.y, p.pol.y),
+                   __builtin_fmaf(-cos_theta, p.dir.z, p.pol.z));
+    p.dir = p.dir / norm(p.dir);
+    p.pol = p.pol / norm(p.pol);
+}
+
+// photon.h:455-570
+__device__ int propagate_to_boundary(const DevGeom &g, Photon &p, State &s, chr_xorwow &rng, int use_weights,
+                                     int scatter_first) {
+    float absorption_distance = -s.absorption_length * chr_logf(chr_uniform01(&rng));
+    float scattering_distance = -s.scattering_length * chr_logf(chr_uniform01(&rng));
+    if (use_weights && p.weight > WEIGHT_LOWER_THRESHOLD) absorption_distance = 1e30f;
+    else use_weights = 0;
+    if (scatter_first == 1) {
+        const float scatter_prob = 1.0f - chr_expf(-s.distance / s.scattering_length);
+        if (scatter_prob > WEIGHT_LOWER_THRESHOLD) {
+            int i = 0;
+            while (i < 1000 && scattering_distance > s.distance) {
+                scattering_distance = -s.scattering_length * chr_logf(chr_uniform01(&rng));
+                i++;
+            }
+            p.weight *= scatter_prob;
+        }
+    } else if (scatter_first == -1) {
+        const float no_scatter_prob = chr_expf(-s.distance / s.scattering_length);
+        if (no_scatter_prob > WEIGHT_LOWER_THRESHOLD) {
+            int i = 0;
+            while (i < 1000 && scattering_distance <= s.distance) {
+                scattering_distance = -s.scattering_length * chr_logf(chr_uniform01(&rng));
+                i++;
+            }
+            p.weight *= no_scatter_prob;
+        }
+    }
+    if (absorption_distance <= scattering_distance) {
+        if (absorption_distance <= s.distance) {
+            p.time = p.time + absorption_distance / (SPEED_OF_LIGHT / s.n1);
+            p.pos = axpy(absorption_distance, p.dir, p.pos);
+            const DevMaterial &m = g.materials[s.material1];
+            if (m.num_comp == 0) {
+                p.last_hit = -1;
+                p.history |= CHR_BULK_ABSORB;
+                return BREAK;
+            }
+            const uint32_t W1 = g.wl_n + 1, T1 = g.t_n + 1;
+            const float usc = chr_uniform01(&rng);
+            float prob = 0.0f;
+            uint32_t comp;
+            for (comp = 0;; comp++) {
+                const float comp_abs = interp_property(g, p.wavelength, g.tables + m.comp_absorption_length + comp * W1);
+                prob += s.absorption_length / comp_abs;
+                if (usc < prob || comp + 1 == m.num_comp) break;
+            }
+            const float usr = chr_uniform01(&rng);
+            const float crp = interp_property(g, p.wavelength, g.tables + m.comp_reemission_prob + comp * W1);
+            if (usr < crp) {
+                p.wavelength = sample_cdf(rng, (int)g.wl_n, g.wl_start, g.wl_step,
+                                          g.tables + m.comp_reemission_wvl_cdf + comp * W1);
+                p.time += sample_cdf(rng, (int)g.t_n, g.t_start, g.t_step, g.tables + m.comp_reemission_time_cdf + comp * T1);
+                p.dir = uniform_sphere(rng);
+                p.pol = cross(uniform_sphere(rng), p.dir);
+                p.pol = p.pol / norm(p.pol);
+                p.last_hit = -1;
+                p.history |= CHR_BULK_REEMIT;
+                return CONTINUE;
+            }
+            p.last_hit = -1;
+            p.history |= CHR_BULK_ABSORB;
+            return BREAK;
+        }
+    } else {
+        if (scattering_distance <= s.distance) {
+            if (use_weights) p.weight *= chr_expf(-scattering_distance / s.absorption_length);
+            p.time = p.time + scattering_distance / (SPEED_OF_LIGHT / s.n1);
+            p.pos = axpy(scattering_distance, p.dir, p.pos);
+            rayleigh_scatter(p, rng);
+            p.history |= CHR_RAYLEIGH_SCATTER;
+            p.last_hit = -1;
+            return CONTINUE;
+        }
+    }
+    if (use_weights) p.weight *= chr_expf(-s.distance / s.absorption_length);
+    p.pos = axpy(s.distance, p.dir, p.pos);
+    p.time = p.time + s.distance / (SPEED_OF_LIGHT / s.n1);
+    return PASS;
+}
+
+// photon.h:572-632 (Fresnel)
+__device__ void propagate_at_boundary(Photon &p, const State &s, chr_xorwow &rng) {
+    const float incident_angle = get_theta(s.normal, -p.dir);
+    const float refracted_angle = chr_asinf((chr_sinf(incident_angle) * s.n1) / s.n2);
+    V3 ipn = cross(p.dir, s.normal);
+    const float ipn_len = norm(ipn);
+    if (ipn_len < 1e-6f) ipn = p.pol; else ipn = ipn / ipn_len;
+    const float nc = dot(p.pol, ipn);
+    const float normal_probability = nc * nc;
+    float rc;
+    if (chr_uniform01(&rng) < normal_probability) {
+        rc = -chr_sinf(incident_angle - refracted_angle) / chr_sinf(incident_angle + refracted_angle);
+        if ((chr_uniform01(&rng) < rc * rc) || chr_isnan(refracted_angle)) {
+            p.dir = rotate(s.normal, incident_angle, ipn);
+            p.history |= CHR_REFLECT_SPECULAR;
+        } else {
+            p.dir = rotate(s.normal, PI_F - refracted_angle, ipn);
+        }
+        p.pol = ipn;
+    } else {
+        rc = chr_tanf(incident_angle - refracted_angle) / chr_tanf(incident_angle + refracted_angle);
+        if ((chr_uniform01(&rng) < rc * rc) || chr_isnan(refracted_angle)) {
+            p.dir = rotate(s.normal, incident_angle, ipn);
+            p.history |= CHR_REFLECT_SPECULAR;
+        } else {
+            p.dir = rotate(s.normal, PI_F - refracted_angle, ipn);
+        }
+        p.pol = cross(ipn, p.dir);
+        p.pol = p.pol / norm(p.pol);
+    }
+}
+
+// photon.h:634-667
+__device__ int specular_reflector(Photon &p, const State &s) {
+    const float incident_angle = get_theta(s.normal, -p.dir);
+    V3 ipn = cross(p.dir, s.normal);
+    ipn = ipn / norm(ipn);
+    p.dir = rotate(s.normal, incident_angle, ipn);
+    p.history |= CHR_REFLECT_SPECULAR;
+    return CONTINUE;
+}
+
+__device__ int diffuse_reflector(Photon &p, const State &s, chr_xorwow &rng) {
+    float ndotv;
+    do {
+        p.dir = uniform_sphere(rng);
+        ndotv = dot(p.dir, s.normal);
+        if (ndotv < 0.0f) { p.dir = -p.dir; ndotv = -ndotv; }
+    } while (!(chr_uniform01(&rng) < ndotv));
+    p.pol = cross(uniform_sphere(rng), p.dir);
+    p.pol = p.pol / norm(p.pol);
+    p.history |= CHR_REFLECT_DIFFUSE;
+    return CONTINUE;
+}
+
+// cuComplex semantics (CUDA toolkit cuComplex.h) + cx.h:1-35
+struct Cx { float r, i; };
+__device__ __forceinline__ Cx cxm(float r, float i) { return Cx{r, i}; }
+__device__ __forceinline__ Cx cadd(Cx a, Cx b) { return cxm(a.r + b.r, a.i + b.i); }
+__device__ __forceinline__ Cx csub(Cx a, Cx b) { return cxm(a.r - b.r, a.i - b.i); }
+__device__ __forceinline__ Cx cmul(Cx a, Cx b) {
+    return cxm(__builtin_fmaf(a.r, b.r, -(a.i * b.i)), __builtin_fmaf(a.r, b.i, a.i * b.r));
+}
+__device__ Cx cdiv(Cx x, Cx y) {
+    float s = chr_fabsf(y.r) + chr_fabsf(y.i);
+    float oos = 1.0f / s;
+    const float ars = x.r * oos, ais = x.i * oos, brs = y.r * oos, bis = y.i * oos;
+    s = __builtin_fmaf(bis, bis, brs * brs);
+    oos = 1.0f / s;
+    return cxm(__builtin_fmaf(ais, bis, ars * brs) * oos, __builtin_fmaf(ais, brs, -(ars * bis)) * oos);
+}
+__device__ float cabs_(Cx x) {
+    const float a = chr_fabsf(x.r), b = chr_fabsf(x.i);
+    float v, w, t;
+    if (a > b) { v = a; w = b; } else { v = b; w = a; }
+    t = w / v;
+    t = __builtin_fmaf(t, t, 1.0f);
+    t = v * chr_sqrtf(t);
+    if ((v == 0.0f) || (v > 3.402823466e38f) || (w > 3.402823466e38f)) t = v + w;
+    return t;
+}
+__device__ __forceinline__ float carg_(Cx x) { return chr_atan2f(x.i, x.r); }
+__device__ Cx csqrt_(Cx x) {
+    const float r = chr_sqrtf(cabs_(x));
+    const float t = carg_(x) / 2.0f;
+    float st, ct;
+    chr_sincosf(t, &st, &ct);
+    return cxm(r * ct, r * st);
+}
+
+// photon.h:669-827 (thin film); rare path, kept out of line
+__device__ __noinline__ int propagate_complex(const DevGeom &g, Photon &p, const State &s, chr_xorwow &rng,
+                                              const DevSurface &sf, int use_weights) {
+    const float *T = g.tables;
+    float detect = interp_property(g, p.wavelength, T + sf.detect);
+    const float reflect_diffuse = interp_property(g, p.wavelength, T + sf.reflect_diffuse);
+    const float n2_eta = interp_property(g, p.wavelength, T + sf.eta);
+    const float n2_k = interp_property(g, p.wavelength, T + sf.k);
+    const Cx n1 = cxm(s.n1, 0.0f), n2 = cxm(n2_eta, n2_k), n3 = cxm(s.n2, 0.0f);
+    float cos_t1 = dot(p.dir, s.normal);
+    if (cos_t1 < 0.0f) cos_t1 = -cos_t1;
+    const float theta = chr_acosf(cos_t1);
+    float sth, cth;
+    chr_sincosf(theta, &sth, &cth);
+    const Cx cos1 = cxm(cth, 0.0f), sin1 = cxm(sth, 0.0f);
+    const float e = ((2.0f * PI_F) * sf.thickness) / p.wavelength;
+    const Cx r13 = cdiv(n1, n3), r12 = cdiv(n1, n2);
+    const Cx ratio13sin = cmul(cmul(r13, r13), cmul(sin1, sin1));
+    const Cx cos3 = csqrt_(csub(cxm(1.0f, 0.0f), ratio13sin));
+    const Cx ratio12sin = cmul(cmul(r12, r12), cmul(sin1, sin1));
+    const Cx cos2 = csqrt_(csub(cxm(1.0f, 0.0f), ratio12sin));
+    const Cx n2c2 = cmul(n2, cos2);
+    const float u = n2c2.r, v = n2c2.i;
+    const Cx two = cxm(2.0f, 0.0f);
+    const Cx s_n1c1 = cmul(n1, cos1), s_n2c2 = cmul(n2, cos2), s_n3c3 = cmul(n3, cos3);
+    const Cx s_r12 = cdiv(csub(s_n1c1, s_n2c2), cadd(s_n1c1, s_n2c2));
+    const Cx s_r23 = cdiv(csub(s_n2c2, s_n3c3), cadd(s_n2c2, s_n3c3));
+    const Cx s_t12 = cdiv(cmul(two, s_n1c1), cadd(s_n1c1, s_n2c2));
+    const Cx s_t23 = cdiv(cmul(two, s_n2c2), cadd(s_n2c2, s_n3c3));
+    const Cx s_g = cdiv(s_n3c3, s_n1c1);
+    const float s_abs_r12 = cabs_(s_r12), s_abs_r23 = cabs_(s_r23), s_abs_t12 = cabs_(s_t12), s_abs_t23 = cabs_(s_t23);
+    const float s_arg_r12 = carg_(s_r12), s_arg_r23 = carg_(s_r23);
+    const float s_exp1 = chr_expf((2.0f * v) * e);
+    const float s_exp2 = 1.0f / s_exp1;
+    const float two_ue = (2.0f * u) * e;
+    const float s_denom = s_exp1 + ((s_abs_r12 * s_abs_r12) * (s_abs_r23 * s_abs_r23)) * s_exp2 +
+                          ((2.0f * s_abs_r12) * s_abs_r23) * chr_cosf(s_arg_r23 + s_arg_r12 + two_ue);
+    float s_r = (s_abs_r12 * s_abs_r12) * s_exp1 + (s_abs_r23 * s_abs_r23) * s_exp2 +
+                ((2.0f * s_abs_r12) * s_abs_r23) * chr_cosf(s_arg_r23 - s_arg_r12 + two_ue);
+    s_r /= s_denom;
+    float s_t = ((s_g.r * (s_abs_t12 * s_abs_t12)) * s_abs_t23) * s_abs_t23;
+    s_t /= s_denom;
+    const Cx p_n2c1 = cmul(n2, cos1), p_n3c2 = cmul(n3, cos2), p_n2c3 = cmul(n2, cos3), p_n1c2 = cmul(n1, cos2);
+    const Cx p_r12 = cdiv(csub(p_n2c1, p_n1c2), cadd(p_n2c1, p_n1c2));
+    const Cx p_r23 = cdiv(csub(p_n3c2, p_n2c3), cadd(p_n3c2, p_n2c3));
+    const Cx p_t12 = cdiv(cmul(cmul(two, n1), cos1), cadd(p_n2c1, p_n1c2));
+    const Cx p_t23 = cdiv(cmul(cmul(two, n2), cos2), cadd(p_n3c2, p_n2c3));
+    const Cx p_g = cdiv(cmul(n3, cos3), cmul(n1, cos1));
+    const float p_abs_r12 = cabs_(p_r12), p_abs_r23 = cabs_(p_r23), p_abs_t12 = cabs_(p_t12), p_abs_t23 = cabs_(p_t23);
+    const float p_arg_r12 = carg_(p_r12), p_arg_r23 = carg_(p_r23);
+    const float p_exp1 = chr_expf((2.0f * v) * e);
+    const float p_exp2 = 1.0f / p_exp1;
+    const float p_denom = p_exp1 + ((p_abs_r12 * p_abs_r12) * (p_abs_r23 * p_abs_r23)) * p_exp2 +
+                          ((2.0f * p_abs_r12) * p_abs_r23) * chr_cosf(p_arg_r23 + p_arg_r12 + two_ue);
+    float p_r = (p_abs_r12 * p_abs_r12) * p_exp1 + (p_abs_r23 * p_abs_r23) * p_exp2 +
+                ((2.0f * p_abs_r12) * p_abs_r23) * chr_cosf(p_arg_r23 - p_arg_r12 + two_ue);
+    p_r /= p_denom;
+    float p_t = ((p_g.r * (p_abs_t12 * p_abs_t12)) * p_abs_t23) * p_abs_t23;
+    p_t /= p_denom;
+    const float incident_angle = get_theta(s.normal, -p.dir);
+    const float refracted_angle = chr_asinf((chr_sinf(incident_angle) * s.n1) / s.n2);
+    V3 ipn = cross(p.dir, s.normal);
+    const float ipn_len = norm(ipn);
+    if (ipn_len < 1e-6f) ipn = p.pol; else ipn = ipn / ipn_len;
+    const float nc = dot(p.pol, ipn);
+    const float normal_probability = nc * nc;
+    float transmit = __builtin_fmaf(normal_probability, s_t, (1.0f - normal_probability) * p_t);
+    if (!sf.transmissive) transmit = 0.0f;
+    float reflect = __builtin_fmaf(normal_probability, s_r, (1.0f - normal_probability) * p_r);
+    float absorb = 1.0f - transmit - reflect;
+    if (use_weights && p.weight > WEIGHT_LOWER_THRESHOLD && absorb < (1.0f - WEIGHT_LOWER_THRESHOLD)) {
+        const float survive = 1.0f - absorb;
+        absorb = 0.0f;
+        p.weight *= survive;
+        detect /= survive; reflect /= survive; transmit /= survive;
+    }
+    if (use_weights && detect > 0.0f) {
+        p.history |= CHR_SURFACE_DETECT;
+        p.weight *= detect;
+        return BREAK;
+    }
+    const float us = chr_uniform01(&rng);
+    if (us < absorb) {
+        const float usd = chr_uniform01(&rng);
+        if (usd < detect) p.history |= CHR_SURFACE_DETECT;
+        else p.history |= CHR_SURFACE_ABSORB;
+        return BREAK;
+    } else if (us < absorb + reflect || !sf.transmissive) {
+        const float usr = chr_uniform01(&rng);
+        if (usr < reflect_diffuse) return diffuse_reflector(p, s, rng);
+        return specular_reflector(p, s);
+    }
+    p.dir = rotate(s.normal, PI_F - refracted_angle, ipn);
+    p.pol = cross(ipn, p.dir);
+    p.pol = p.pol / norm(p.pol);
+    p.history |= CHR_SURFACE_TRANSMIT;
+    return CONTINUE;
+}
+
+// photon.h:829-874
+__device__ __noinline__ int propagate_at_wls(const DevGeom &g, Photon &p, const State &s, chr_xorwow &rng,
+                                             const DevSurface &sf, int use_weights) {
+    const float *T = g.tables;
+    float absorb = interp_property(g, p.wavelength, T + sf.absorb);
+    float reflect_specular = interp_property(g, p.wavelength, T + sf.reflect_specular);
+    float reflect_diffuse = interp_property(g, p.wavelength, T + sf.reflect_diffuse);
+    const float reemit = interp_property(g, p.wavelength, T + sf.reemit);
+    const float us = chr_uniform01(&rng);
+    if (use_weights && p.weight > WEIGHT_LOWER_THRESHOLD && absorb < (1.0f - WEIGHT_LOWER_THRESHOLD)) {
+        const float survive = 1.0f - absorb;
+        absorb = 0.0f;
+        p.weight *= survive;
+        reflect_diffuse /= survive;
+        reflect_specular /= survive;
+    }
+    if (us < absorb) {
+        const float usr = chr_uniform01(&rng);
+        if (usr < reemit) {
+            p.history |= CHR_SURFACE_REEMIT;
+            p.wavelength = sample_cdf(rng, (int)g.wl_n, g.wl_start, g.wl_step, T + sf.reemission_cdf);
+            p.dir = uniform_sphere(rng);
+            p.pol = cross(uniform_sphere(rng), p.dir);
+            p.pol = p.pol / norm(p.pol);
+            return CONTINUE;
+        }
+        p.history |= CHR_SURFACE_ABSORB;
+        return BREAK;
+    } else if (us < absorb + reflect_specular + reflect_diffuse) {
+        const float usr = chr_uniform01(&rng) * (reflect_specular + reflect_diffuse);
+        if (usr < reflect_specular) return specular_reflector(p, s);
+        return diffuse_reflector(p, s, rng);
+    }
+    p.history |= CHR_SURFACE_TRANSMIT;
+    return PASS;
+}
+
+// photon.h:877-907 (iidx+1 clamped at the last angle, see oracle)
+__device__ __noinline__ int propagate_at_dichroic(const DevGeom &g, Photon &p, const State &s, chr_xorwow &rng,
+                                                  const DevSurface &sf) {
+    const float *T = g.tables;
+    const float incident_angle = get_theta(s.normal, -p.dir);
+    const int na = (int)sf.dichroic_nangles;
+    const float idx = interp_idx(incident_angle, na, T + sf.dichroic_angles);
+    const uint32_t iidx = (uint32_t)(int)idx;
+    const uint32_t ihi = (iidx + 1 < (uint32_t)na) ? iidx + 1 : (uint32_t)na - 1;
+    const uint32_t W1 = g.wl_n + 1;
+    const float rlo = interp_property(g, p.wavelength, T + sf.dichroic_reflect + iidx * W1);
+    const float rhi = interp_property(g, p.wavelength, T + sf.dichroic_reflect + ihi * W1);
+    const float tlo = interp_property(g, p.wavelength, T + sf.dichroic_transmit + iidx * W1);
+    const float thi = interp_property(g, p.wavelength, T + sf.dichroic_transmit + ihi * W1);
+    const float fr = idx - (float)iidx;
+    const float reflect_prob = __builtin_fmaf(rhi - rlo, fr, rlo);
+    const float transmit_prob = __builtin_fmaf(thi - tlo, fr, tlo);
+    const float us = chr_uniform01(&rng);
+    if (us < reflect_prob) return specular_reflector(p, s);
+    if (us < transmit_prob + reflect_prob) { p.history |= CHR_SURFACE_TRANSMIT; return PASS; }
+    p.history |= CHR_SURFACE_ABSORB;
+    return BREAK;
+}
+
+// photon.h:909-951
+__device__ __noinline__ int propagate_at_angular(const DevGeom &g, Photon &p, const State &s, chr_xorwow &rng,
+                                                 const DevSurface &sf, int use_weights) {
+    const float *T = g.tables;
+    const float incident_angle = get_theta(s.normal, -p.dir);
+    const int na = (int)sf.angular_nangles;
+    const float idx = interp_idx(incident_angle, na, T + sf.angular_angles);
+    const uint32_t iidx = (uint32_t)(int)idx;
+    const uint32_t ihi = (iidx + 1 < (uint32_t)na) ? iidx + 1 : (uint32_t)na - 1;
+    const float t = idx - (float)iidx;
+    const float *tr = T + sf.angular_transmit, *rsp = T + sf.angular_reflect_specular, *rdf = T + sf.angular_reflect_diffuse;
+    float tp = __builtin_fmaf(t, tr[ihi] - tr[iidx], tr[iidx]);
+    float rs = __builtin_fmaf(t, rsp[ihi] - rsp[iidx], rsp[iidx]);
+    float rd = __builtin_fmaf(t, rdf[ihi] - rdf[iidx], rdf[iidx]);
+    float ap = 1.0f - tp - rs - rd;
+    if (use_weights && p.weight > WEIGHT_LOWER_THRESHOLD && ap < (1.0f - WEIGHT_LOWER_THRESHOLD)) {
+        const float survive = 1.0f - ap;
+        ap = 0.0f;
+        p.weight *= survive;
+        tp /= survive; rs /= survive; rd /= survive;
+    }
+    const float us = chr_uniform01(&rng);
+    if (us < ap) { p.history |= CHR_SURFACE_ABSORB; return BREAK; }
+    if (us < ap + tp) { p.history |= CHR_SURFACE_TRANSMIT; return PASS; }
+    if (us < ap + tp + rs) return specular_reflector(p, s);
+    return diffuse_reflector(p, s, rng);
+}
+
+// photon.h:953-1037
+__device__ __forceinline__ int propagate_at_surface(const DevGeom &g, Photon &p, const State &s, chr_xorwow &rng,
+                                                    int use_weights) {
+    const DevSurface &sf = g.surfaces[s.surface_index];
+    if (sf.model == CHR_SURFACE_COMPLEX) return propagate_complex(g, p, s, rng, sf, use_weights);
+    if (sf.model == CHR_SURFACE_WLS) return propagate_at_wls(g, p, s, rng, sf, use_weights);
+    if (sf.model == CHR_SURFACE_DICHROIC) return propagate_at_dichroic(g, p, s, rng, sf);
+    if (sf.model == CHR_SURFACE_ANGULAR) return propagate_at_angular(g, p, s, rng, sf, use_weights);
+    const float *T = g.tables;
+    float detect = interp_property(g, p.wavelength, T + sf.detect);
+    float absorb = interp_property(g, p.wavelength, T + sf.absorb);
+    float reflect_diffuse = interp_property(g, p.wavelength, T + sf.reflect_diffuse);
+    float reflect_specular = interp_property(g, p.wavelength, T + sf.reflect_specular);
+    const float us = chr_uniform01(&rng);
+    if (use_weights && p.weight > WEIGHT_LOWER_THRESHOLD && absorb < (1.0f - WEIGHT_LOWER_THRESHOLD)) {
+        const float survive = 1.0f - absorb;
+        absorb = 0.0f;
+        p.weight *= survive;
+        detect /= survive; reflect_diffuse /= survive; reflect_specular /= survive;
+    }
+    if (use_weights && detect > 0.0f) {
+        p.history |= CHR_SURFACE_DETECT;
+        p.weight *= detect;
+        return BREAK;
+    }
+    if (us < absorb) { p.history |= CHR_SURFACE_ABSORB; return BREAK; }
+    if (us < absorb + detect) { p.history |= CHR_SURFACE_DETECT; return BREAK; }
+    if (us < absorb + detect + reflect_diffuse) return diffuse_reflector(p, s, rng);
+    if (us < absorb + detect + reflect_diffuse + reflect_specular) return specular_reflector(p, s);
+    return PASS;
+}
+
+// ---------------------------------------------------------------- kernels
+struct PropagateArgs {
+    DevGeom g;
+    float *pos, *dir, *pol, *wl, *t, *weights;
+    uint32_t *flags;
+    int32_t *last_hit;
+    uint32_t *evidx;
+    uint32_t *rng;
+    uint32_t nslots;
+    const uint32_t *input_queue;
+    int32_t first, nthreads, max_steps, use_weights, scatter_first;
+    unsigned long long *alive_masks;   // one word per 64 slots
+    uint32_t *counters;                // [0]: stack overflows
+};
+
+__device__ __forceinline__ V3 load3(const float *p, uint32_t i) { return v3(p[3 * i], p[3 * i + 1], p[3 * i + 2]); }
+__device__ __forceinline__ void store3(float *p, uint32_t i, V3 v) { p[3 * i] = v.x; p[3 * i + 1] = v.y; p[3 * i + 2] = v.z; }
+
+// propagate.cu:254-366
+__global__ __launch_bounds__(BLOCK) void propagate_kernel(PropagateArgs a) {
+    __shared__ uint32_t lds_stack[STACK_LDS * BLOCK];
+    const int id = blockIdx.x * BLOCK + threadIdx.x;
+    unsigned alive = 0;
+    if (id < a.nthreads) {
+        const uint32_t photon_id = a.input_queue[a.first + id];
+        Photon p;
+        p.history = a.flags[photon_id] & 0xFFFFu;   // unsigned short on the device (photon.h:29)
+        if (!(p.history & DEAD_MASK)) {
+            chr_xorwow rng;
+            const uint32_t ns = a.nslots;
+            rng.d = a.rng[id]; rng.v0 = a.rng[ns + id]; rng.v1 = a.rng[2 * ns + id];
+            rng.v2 = a.rng[3 * ns + id]; rng.v3 = a.rng[4 * ns + id]; rng.v4 = a.rng[5 * ns + id];
+            p.pos = load3(a.pos, photon_id);
+            p.dir = load3(a.dir, photon_id);
+            p.dir = p.dir / norm(p.dir);
+            p.pol = load3(a.pol, photon_id);
+            p.pol = p.pol / norm(p.pol);
+            p.wavelength = a.wl[photon_id];
+            p.time = a.t[photon_id];
+            p.last_hit = a.last_hit[photon_id];
+            p.weight = a.weights[photon_id];
+            Stack st;
+            st.lds = lds_stack + threadIdx.x;
+            uint32_t overflow = 0;
+            State s;
+            int scatter_first = a.scatter_first;
+            const DevGeom &g = a.g;
+            int steps = 0;
+            while (steps < a.max_steps) {
+                steps++;
+                const float prod = ((((p.dir.x * p.dir.y) * p.dir.z) * p.pos.x) * p.pos.y) * p.pos.z;
+                if (chr_isnan(prod)) { p.history |= CHR_NO_HIT | CHR_NAN_ABORT; break; }
+                fill_state(g, s, p, st, overflow);
+                if (p.last_hit == -1) break;
+                int command = propagate_to_boundary(g, p, s, rng, a.use_weights, scatter_first);
+                scatter_first = 0;
+                if (command == BREAK) break;
+                if (command == CONTINUE) continue;
+                if (s.surface_index != -1) {
+                    command = propagate_at_surface(g, p, s, rng, a.use_weights);
+                    if (command == BREAK) break;
+                    if (command == CONTINUE) continue;
+                }
+                propagate_at_boundary(p, s, rng);
+            }
+            a.rng[id] = rng.d; a.rng[ns + id] = rng.v0; a.rng[2 * ns + id] = rng.v1;
+            a.rng[3 * ns + id] = rng.v2; a.rng[4 * ns + id] = rng.v3; a.rng[5 * ns + id] = rng.v4;
+            store3(a.pos, photon_id, p.pos);
+            store3(a.dir, photon_id, p.dir);
+            store3(a.pol, photon_id, p.pol);
+            a.wl[photon_id] = p.wavelength;
+            a.t[photon_id] = p.time;
+            a.flags[photon_id] = p.history;
+            a.last_hit[photon_id] = p.last_hit;
+            a.weights[photon_id] = p.weight;
+            alive = (p.history & DEAD_MASK) == 0;
+            if (overflow) atomicAdd(a.counters, overflow);
+        }
+    }
+    const unsigned long long mask = __ballot(alive);
+    if ((threadIdx.x & 63) == 0 && id < a.nthreads) a.alive_masks[id >> 6] = mask;
+}
+
+// exclusive scan of the popcounts of nwords masks (single workgroup);
+// word_offsets[i] = survivors before word i; base[0] = out_counter[0] on entry;
+// out_counter[0] += total.
+__global__ __launch_bounds__(1024) void scan_masks_kernel(const unsigned long long *masks, uint32_t nwords,
+                                                          uint32_t *word_offsets, uint32_t *out_counter,
+                                                          uint32_t *base, uint32_t *total_out) {
+    __shared__ uint32_t partial[1024];
+    const uint32_t tid = threadIdx.x;
+    const uint32_t per = (nwords + 1023) / 1024;
+    const uint32_t w0 = tid * per;
+    uint32_t sum = 0;
+    for (uint32_t k = 0; k < per && w0 + k < nwords; ++k) sum += __popcll(masks[w0 + k]);
+    partial[tid] = sum;
+    __syncthreads();
+    for (uint32_t off = 1; off < 1024; off <<= 1) {
+        const uint32_t v = (tid >= off) ? partial[tid - off] : 0;
+        __syncthreads();
+        partial[tid] += v;
+        __syncthreads();
+    }
+    uint32_t run = partial[tid] - sum;
+    for (uint32_t k = 0; k < per && w0 + k < nwords; ++k) {
+        word_offsets[w0 + k] = run;
+        run += __popcll(masks[w0 + k]);
+    }
+    if (tid == 1023) {
+        const uint32_t total = partial[1023];
+        if (base) base[0] = out_counter ? out_counter[0] : 0u;
+        if (out_counter) out_counter[0] += total;
+        if (total_out) total_out[0] = total;
+    }
+}
+
+__global__ __launch_bounds__(BLOCK) void scatter_queue_kernel(const unsigned long long *masks, const uint32_t *word_offsets,
+                                                               const uint32_t *base, const uint32_t *in_queue,
+                                                               int32_t first, int32_t n, uint32_t *out_queue) {
+    const int id = blockIdx.x * BLOCK + threadIdx.x;
+    if (id >= n) return;
+    const unsigned long long m = masks[id >> 6];
+    const int lane = id & 63;
+    if ((m >> lane) & 1ull) {
+        const uint32_t rank = __popcll(m & ((1ull << lane) - 1ull));
+        out_queue[base[0] + word_offsets[id >> 6] + rank] = in_queue[first + id];
+    }
+}
+
+// ---------------------------------------------------------------- RNG init
+__global__ __launch_bounds__(BLOCK) void init_rng_kernel(uint32_t *states, uint32_t nslots, unsigned long long seed,
+                                                          unsigned long long offset, const uint32_t *seq, int nseq,
+                                                          const uint32_t *off, int noff) {
+    const uint32_t s = blockIdx.x * BLOCK + threadIdx.x;
+    if (s >= nslots) return;
+    chr_xorwow r;
+    chr_xorwow_init(&r, seed, s, offset, seq, nseq, off, noff);
+    states[s] = r.d; states[nslots + s] = r.v0; states[2 * nslots + s] = r.v1;
+    states[3 * nslots + s] = r.v2; states[4 * nslots + s] = r.v3; states[5 * nslots + s] = r.v4;
+}
+
+// ---------------------------------------------------------------- selection kernels
+struct PhotonPtrs {
+    float *pos, *dir, *pol, *wl, *t, *weights;
+    uint32_t *flags;
+    int32_t *last_hit;
+    uint32_t *evidx;
+};
+
+__device__ __forceinline__ void copy_photon(const PhotonPtrs &src, uint32_t i, const PhotonPtrs &dst, uint32_t o) {
+    store3(dst.pos, o, load3(src.pos, i));
+    store3(dst.dir, o, load3(src.dir, i));
+    store3(dst.pol, o, load3(src.pol, i));
+    dst.wl[o] = src.wl[i];
+    dst.t[o] = src.t[i];
+    dst.flags[o] = src.flags[i];
+    dst.last_hit[o] = src.last_hit[i];
+    dst.weights[o] = src.weights[i];
+    dst.evidx[o] = src.evidx[i];
+}
+
+// mode 0: hits (count_photon_hits, propagate.cu:172-199); mode 1: flag select (count_photons, 70-95)
+__global__ __launch_bounds__(BLOCK) void flag_kernel(PhotonPtrs ph, int32_t start, int32_t n, uint32_t state,
+                                                      const uint32_t *solid_map, const int32_t *solid_to_channel,
+                                                      int mode, unsigned long long *masks) {
+    const int id = blockIdx.x * BLOCK + threadIdx.x;
+    unsigned hit = 0;
+    if (id < n) {
+        const uint32_t i = (uint32_t)(start + id);
+        if (ph.flags[i] & state) {
+            if (mode == 1) hit = 1;
+            else {
+                const int tri = ph.last_hit[i];
+                if (tri > -1) hit = solid_to_channel[solid_map[tri]] >= 0;
+            }
+        }
+    }
+    const unsigned long long m = __ballot(hit);
+    if ((threadIdx.x & 63) == 0 && id < n) masks[id >> 6] = m;
+}
+
+__global__ __launch_bounds__(BLOCK) void copy_selected_kernel(PhotonPtrs ph, int32_t start, int32_t n,
+                                                               const unsigned long long *masks,
+                                                               const uint32_t *word_offsets, PhotonPtrs out,
+                                                               int32_t *channels, const uint32_t *solid_map,
+                                                               const int32_t *solid_to_channel) {
+    const int id = blockIdx.x * BLOCK + threadIdx.x;
+    if (id >= n) return;
+    const unsigned long long m = masks[id >> 6];
+    const int lane = id & 63;
+    if (!((m >> lane) & 1ull)) return;
+    const uint32_t o = word_offsets[id >> 6] + __popcll(m & ((1ull << lane) - 1ull));
+    const uint32_t i = (uint32_t)(start + id);
+    copy_photon(ph, i, out, o);
+    if (channels) channels[o] = solid_to_channel[solid_map[ph.last_hit[i]]];
+}
+
+// propagate.cu:141-169
+__global__ __launch_bounds__(BLOCK) void copy_queue_kernel(PhotonPtrs ph, int32_t first, int32_t n, const uint32_t *queue,
+                                                            PhotonPtrs out) {
+    const int id = blockIdx.x * BLOCK + threadIdx.x;
+    if (id >= n) return;
+    const uint32_t o = (uint32_t)(first + id);
+    copy_photon(ph, queue[o], out, o);
+}
+
+// propagate.cu:29-68
+__global__ __launch_bounds__(BLOCK) void duplicate_kernel(PhotonPtrs ph, int32_t first, int32_t n, int32_t copies,
+                                                           int32_t stride) {
+    const int id = blockIdx.x * BLOCK + threadIdx.x;
+    if (id >= n) return;
+    const uint32_t i = (uint32_t)(first + id);
+    for (int c = 1; c <= copies; ++c) copy_photon(ph, i, ph, i + (uint32_t)(stride * c));
+}
+
+// mesh.h:131-159
+__global__ __launch_bounds__(BLOCK) void distance_kernel(DevGeom g, uint32_t n, const float *origin, const float *dir,
+                                                          float *distance, uint32_t *counters) {
+    __shared__ uint32_t lds_stack[STACK_LDS * BLOCK];
+    const uint32_t id = blockIdx.x * BLOCK + threadIdx.x;
+    if (id >= n) return;
+    V3 o = load3(origin, id), d = load3(dir, id);
+    d = d / norm(d);
+    Stack st;
+    st.lds = lds_stack + threadIdx.x;
+    uint32_t overflow = 0;
+    float dist;
+    const int tri = intersect_mesh(g, o, d, dist, -1, st, overflow);
+    if (tri != -1) distance[id] = dist;
+    if (overflow && counters) atomicAdd(counters, overflow);
+}
+
+}  // namespace chr
+
+// ====================================================================== C ABI
+using namespace chr;
+
+namespace {
+
+inline unsigned grid_for(uint64_t n) { return (unsigned)((n + BLOCK - 1) / BLOCK); }
+
+PhotonPtrs to_ptrs(const chr_photons *p) {
+    return PhotonPtrs{p->d_pos, p->d_dir, p->d_pol, p->d_wavelengths, p->d_t, p->d_weights, p->d_flags,
+                      p->d_last_hit_triangles, p->d_evidx};
+}
+
+bool photons_ok(const chr_photons *p) {
+    return p && p->d_pos && p->d_dir && p->d_pol && p->d_wavelengths && p->d_t && p->d_weights && p->d_flags &&
+           p->d_last_hit_triangles && p->d_evidx;
+}
+
+struct JumpTables {
+    uint32_t *seq = nullptr, *off = nullptr;
+    int device = -1;
+};
+
+int get_jump_tables(JumpTables &jt) {
+    static thread_local JumpTables cache[16];
+    int dev = 0;
+    CHR_HIP_CHECK(hipGetDevice(&dev));
+    if (dev < 0 || dev >= 16) return chr::fail(CHR_ERR_INVALID, "device id %d unsupported", dev);
+    if (!cache[dev].seq) {
+        static std::vector<uint32_t> hseq, hoff;
+        if (hseq.empty()) {
+            hseq.resize((size_t)CHR_XW_MATWORDS * 32);
+            hoff.resize((size_t)CHR_XW_MATWORDS * 64);
+            chr_xw_sequence_matrices(hseq.data(), 32);
+            chr_xw_offset_matrices(hoff.data(), 64);
+        }
+        CHR_HIP_CHECK(hipMalloc(&cache[dev].seq, hseq.size() * 4));
+        CHR_HIP_CHECK(hipMalloc(&cache[dev].off, hoff.size() * 4));
+        CHR_HIP_CHECK(hipMemcpy(cache[dev].seq, hseq.data(), hseq.size() * 4, hipMemcpyHostToDevice));
+        CHR_HIP_CHECK(hipMemcpy(cache[dev].off, hoff.data(), hoff.size() * 4, hipMemcpyHostToDevice));
+    }
+    jt = cache[dev];
+    return CHR_OK;
+}
+
+// device scratch reused by the selection helpers (per thread, grown on demand)
+struct Scratch {
+    void *ptr = nullptr;
+    size_t bytes = 0;
+    int device = -1;
+};
+
+int scratch_get(size_t bytes, void **out) {
+    static thread_local Scratch s[16];
+    int dev = 0;
+    CHR_HIP_CHECK(hipGetDevice(&dev));
+    Scratch &x = s[dev & 15];
+    if (x.bytes < bytes) {
+        if (x.ptr) CHR_HIP_CHECK(hipFree(x.ptr));
+        x.ptr = nullptr;
+        CHR_HIP_CHECK(hipMalloc(&x.ptr, bytes));
+        x.bytes = bytes;
+    }
+    *out = x.ptr;
+    return CHR_OK;
+}
+
+}  // namespace
+
+extern "C" int chr_init_rng(uint32_t *d_states, uint32_t nslots, uint64_t seed, uint64_t offset, void *stream) {
+    if (!d_states || nslots == 0) return chr::fail(CHR_ERR_INVALID, "chr_init_rng: empty state buffer");
+    JumpTables jt;
+    int rc = get_jump_tables(jt);
+    if (rc) return rc;
+    hipLaunchKernelGGL(init_rng_kernel, dim3(grid_for(nslots)), dim3(BLOCK), 0, (hipStream_t)stream, d_states, nslots,
+                       (unsigned long long)seed, (unsigned long long)offset, jt.seq, 32, jt.off, 64);
+    CHR_HIP_CHECK(hipGetLastError());
+    return CHR_OK;
+}
+
+extern "C" int chr_rng_download(const uint32_t *d_states, uint32_t nslots, uint32_t *h_out, void *stream) {
+    CHR_HIP_CHECK(hipMemcpyAsync(h_out, d_states, (size_t)nslots * 24, hipMemcpyDeviceToHost, (hipStream_t)stream));
+    CHR_HIP_CHECK(hipStreamSynchronize((hipStream_t)stream));
+    return CHR_OK;
+}
+
+extern "C" uint64_t chr_propagate_scratch_words(uint32_t nthreads) {
+    const uint64_t nwords = (nthreads + 63) / 64;
+    return 2 * nwords /*masks*/ + nwords /*offsets*/ + 8;
+}
+
+// scratch layout (u32 words): [0..7] counters/base; masks (u64, 8-aligned); offsets
+static int launch_chunk(const chr_geometry *g, const chr_photons *ph, uint32_t *rng, uint32_t nslots, int32_t first,
+                        int32_t nthreads, const uint32_t *in_queue, uint32_t *out_queue, int32_t max_steps,
+                        int32_t use_weights, int32_t scatter_first, uint32_t *scratch, hipStream_t stream,
+                        hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr) {
+    const uint32_t nwords = (uint32_t)((nthreads + 63) / 64);
+    uint32_t *counters = scratch;               // [0] overflows, [1] base
+    unsigned long long *masks = (unsigned long long *)(scratch + 8);
+    uint32_t *offsets = scratch + 8 + 2 * (size_t)nwords;
+    PropagateArgs a;
+    a.g = g->dev;
+    a.pos = ph->d_pos; a.dir = ph->d_dir; a.pol = ph->d_pol; a.wl = ph->d_wavelengths; a.t = ph->d_t;
+    a.weights = ph->d_weights; a.flags = ph->d_flags; a.last_hit = ph->d_last_hit_triangles; a.evidx = ph->d_evidx;
+    a.rng = rng; a.nslots = nslots; a.input_queue = in_queue; a.first = first; a.nthreads = nthreads;
+    a.max_steps = max_steps; a.use_weights = use_weights; a.scatter_first = scatter_first;
+    a.alive_masks = masks; a.counters = counters;
+    if (ev0) CHR_HIP_CHECK(hipEventRecord(ev0, stream));
+    hipLaunchKernelGGL(propagate_kernel, dim3(grid_for(nthreads)), dim3(BLOCK), 0, stream, a);
+    if (ev1) CHR_HIP_CHECK(hipEventRecord(ev1, stream));
+    hipLaunchKernelGGL(scan_masks_kernel, dim3(1), dim3(1024), 0, stream, masks, nwords, offsets, out_queue,
+                       counters + 1, (uint32_t *)nullptr);
+    hipLaunchKernelGGL(scatter_queue_kernel, dim3(grid_for(nthreads)), dim3(BLOCK), 0, stream, masks, offsets,
+                       counters + 1, in_queue, first, nthreads, out_queue);
+    CHR_HIP_CHECK(hipGetLastError());
+    return CHR_OK;
+}
+
+extern "C" int chr_propagate_chunk(const chr_geometry *g, const chr_photons *ph, uint32_t *d_rng_states,
+                                   uint32_t rng_nslots, int32_t first_photon, int32_t nthreads,
+                                   const uint32_t *d_input_queue, uint32_t *d_output_queue, int32_t max_steps,
+                                   int32_t use_weights, int32_t scatter_first, uint32_t *d_scratch, void *stream) {
+    if (!g || !photons_ok(ph) || !d_rng_states || !d_input_queue || !d_output_queue || !d_scratch)
+        return chr::fail(CHR_ERR_INVALID, "chr_propagate_chunk: null argument");
+    if (nthreads <= 0) return CHR_OK;
+    if ((uint32_t)nthreads > rng_nslots)
+        return chr::fail(CHR_ERR_INVALID, "chr_propagate_chunk: %d threads but only %u rng states", nthreads, rng_nslots);
+    return launch_chunk(g, ph, d_rng_states, rng_nslots, first_photon, nthreads, d_input_queue, d_output_queue,
+                        max_steps, use_weights, scatter_first, d_scratch, (hipStream_t)stream);
+}
+
+extern "C" int chr_propagate(const chr_geometry *g, const chr_photons *ph, uint32_t nphotons, uint32_t true_nphotons,
+                             uint32_t ncopies, uint32_t *d_rng_states, uint32_t rng_nslots, int32_t ntpb,
+                             int32_t max_blocks, int32_t max_steps, int32_t use_weights, int32_t scatter_first,
+                             chr_propagate_stats *stats, void *vstream) {
+    if (!g || !photons_ok(ph) || !d_rng_states) return chr::fail(CHR_ERR_INVALID, "chr_propagate: null argument");
+    if (ntpb <= 0 || max_blocks <= 0) return chr::fail(CHR_ERR_INVALID, "chr_propagate: bad launch shape");
+    if ((uint64_t)ntpb * (uint64_t)max_blocks > rng_nslots)
+        return chr::fail(CHR_ERR_INVALID, "chr_propagate: rng_states must hold nthreads_per_block*max_blocks=%lld states (have %u)",
+                         (long long)ntpb * max_blocks, rng_nslots);
+    if (ncopies == 0 || (uint64_t)true_nphotons * ncopies != nphotons)
+        return chr::fail(CHR_ERR_INVALID, "chr_propagate: nphotons != true_nphotons*ncopies");
+    hipStream_t stream = (hipStream_t)vstream;
+    chr_propagate_stats st{};
+    if (nphotons == 0) { if (stats) *stats = st; return CHR_OK; }
+    const uint32_t chunk_cap = (uint32_t)std::min<uint64_t>((uint64_t)ntpb * max_blocks, nphotons);
+    // queues (photon.py:242-250): [0] = count+1 header, entries from [1]
+    std::vector<uint32_t> hq(nphotons + 1);
+    hq[0] = 0;
+    for (uint32_t c = 0; c < ncopies; ++c)
+        for (uint32_t k = 0; k < true_nphotons; ++k) hq[1 + c + (size_t)k * ncopies] = k + c * true_nphotons;
+    uint32_t *q[2] = {nullptr, nullptr};
+    uint32_t *scratch = nullptr;
+    uint32_t *pinned = nullptr;
+    int rc = CHR_OK;
+    const size_t qbytes = ((size_t)nphotons + 1) * 4;
+    const size_t sbytes = chr_propagate_scratch_words(chunk_cap) * 4;
+    void *buf = nullptr;
+    rc = scratch_get(2 * qbytes + sbytes + 64, &buf);
+    if (rc) return rc;
+    q[0] = (uint32_t *)buf;
+    q[1] = q[0] + (nphotons + 1);
+    scratch = (uint32_t *)(((uintptr_t)(q[1] + nphotons + 1) + 15) & ~(uintptr_t)15);
+    CHR_HIP_CHECK(hipHostMalloc((void **)&pinned, 16, hipHostMallocDefault));
+    const size_t max_chunks = (nphotons + chunk_cap - 1) / chunk_cap;
+    std::vector<hipEvent_t> events(2 * max_chunks, nullptr);
+    for (auto &ev : events) CHR_HIP_CHECK(hipEventCreate(&ev));
+    double kernel_ms = 0.0;
+    auto cleanup = [&]() {
+        if (pinned) hipHostFree(pinned);
+        for (auto &ev : events) if (ev) (void)hipEventDestroy(ev);
+    };
+    auto collect = [&](size_t nchunks) -> hipError_t {
+        for (size_t c = 0; c < nchunks; ++c) {
+            float ms = 0.0f;
+            hipError_t err = hipEventElapsedTime(&ms, events[2 * c], events[2 * c + 1]);
+            if (err != hipSuccess) return err;
+            kernel_ms += ms;
+        }
+        return hipSuccess;
+    };
+    hipError_t e;
+    if ((e = hipMemcpyAsync(q[0], hq.data(), qbytes, hipMemcpyHostToDevice, stream)) != hipSuccess) { cleanup(); CHR_HIP_CHECK(e); }
+    pinned[0] = 1;
+    if ((e = hipMemcpyAsync(q[1], pinned, 4, hipMemcpyHostToDevice, stream)) != hipSuccess) { cleanup(); CHR_HIP_CHECK(e); }
+    if ((e = hipMemsetAsync(scratch, 0, 32, stream)) != hipSuccess) { cleanup(); CHR_HIP_CHECK(e); }
+    int cur = 0;
+    int64_t n = nphotons;
+    int step = 0;
+    while (step < max_steps) {
+        const int nsteps = (n < (int64_t)ntpb * 16 * 8 || use_weights) ? max_steps - step : 1;
+        int64_t first = 0;
+        size_t nchunks = 0;
+        while (first < n) {
+            // chunk_iterator (tools.py:159-180)
+            const int64_t left = n - first;
+            int64_t blocks = left / ntpb + (left % ntpb != 0);
+            if (blocks > max_blocks) blocks = max_blocks;
+            const int64_t count = std::min<int64_t>(left, blocks * ntpb);
+            rc = launch_chunk(g, ph, d_rng_states, rng_nslots, (int32_t)first, (int32_t)count, q[cur] + 1, q[cur ^ 1],
+                              nsteps, use_weights, scatter_first, scratch, stream, events[2 * nchunks],
+                              events[2 * nchunks + 1]);
+            if (rc) { cleanup(); return rc; }
+            st.launches++;
+            nchunks++;
+            first += count;
+        }
+        st.steps_run++;
+        step += nsteps;
+        scatter_first = 0;
+        if (step < max_steps) {
+            cur ^= 1;
+            // read the survivor count (photon.py:284) and reset the other header
+            if ((e = hipMemcpyAsync(pinned, q[cur], 4, hipMemcpyDeviceToHost, stream)) != hipSuccess) { cleanup(); CHR_HIP_CHECK(e); }
+            if ((e = hipStreamSynchronize(stream)) != hipSuccess) { cleanup(); CHR_HIP_CHECK(e); }
+            if ((e = collect(nchunks)) != hipSuccess) { cleanup(); CHR_HIP_CHECK(e); }
+            nchunks = 0;
+            n = (int64_t)pinned[0] - 1;
+            pinned[1] = 1;
+            if ((e = hipMemcpyAsync(q[cur ^ 1], pinned + 1, 4, hipMemcpyHostToDevice, stream)) != hipSuccess) { cleanup(); CHR_HIP_CHECK(e); }
+            if (n == 0) break;
+        }
+        if (nchunks) {   // last step (no survivor read-back): drain before collecting
+            if ((e = hipStreamSynchronize(stream)) != hipSuccess) { cleanup(); CHR_HIP_CHECK(e); }
+            if ((e = collect(nchunks)) != hipSuccess) { cleanup(); CHR_HIP_CHECK(e); }
+        }
+    }
+    if ((e = hipMemcpyAsync(pinned + 2, scratch, 4, hipMemcpyDeviceToHost, stream)) != hipSuccess) { cleanup(); CHR_HIP_CHECK(e); }
+    if ((e = hipStreamSynchronize(stream)) != hipSuccess) { cleanup(); CHR_HIP_CHECK(e); }
+    st.stack_overflows = pinned[2];
+    st.kernel_ms = kernel_ms;
+    st.final_alive = (step < max_steps) ? (uint32_t)n : 0u;
+    cleanup();
+    if (stats) *stats = st;
+    return CHR_OK;
+}
+
+static int select_common(const chr_photons *ph, int32_t start, int32_t n, uint32_t state, const uint32_t *solid_map,
+                         const int32_t *s2c, int mode, const chr_photons *out, int32_t *channels, uint32_t *count,
+                         hipStream_t stream) {
+    if (!photons_ok(ph) || !count) return chr::fail(CHR_ERR_INVALID, "selection: null argument");
+    if (mode == 0 && (!solid_map || !s2c)) return chr::fail(CHR_ERR_INVALID, "hits: solid map / channel map missing");
+    *count = 0;
+    if (n <= 0) return CHR_OK;
+    const uint32_t nwords = (uint32_t)((n + 63) / 64);
+    void *buf;
+    int rc = scratch_get((size_t)nwords * 12 + 64, &buf);
+    if (rc) return rc;
+    uint32_t *cnt = (uint32_t *)buf;
+    unsigned long long *masks = (unsigned long long *)((uint32_t *)buf + 8);
+    uint32_t *offsets = (uint32_t *)buf + 8 + 2 * (size_t)nwords;
+    const PhotonPtrs p = to_ptrs(ph);
+    hipLaunchKernelGGL(flag_kernel, dim3(grid_for(n)), dim3(BLOCK), 0, stream, p, start, n, state, solid_map, s2c, mode,
+                       masks);
+    hipLaunchKernelGGL(scan_masks_kernel, dim3(1), dim3(1024), 0, stream, masks, nwords, offsets, (uint32_t *)nullptr,
+                       (uint32_t *)nullptr, cnt);
+    CHR_HIP_CHECK(hipGetLastError());
+    uint32_t total = 0;
+    CHR_HIP_CHECK(hipMemcpyAsync(&total, cnt, 4, hipMemcpyDeviceToHost, stream));
+    CHR_HIP_CHECK(hipStreamSynchronize(stream));
+    *count = total;
+    if (out && total > 0) {
+        if (!photons_ok(out)) return chr::fail(CHR_ERR_INVALID, "selection: output buffers missing");
+        hipLaunchKernelGGL(copy_selected_kernel, dim3(grid_for(n)), dim3(BLOCK), 0, stream, p, start, n, masks, offsets,
+                           to_ptrs(out), channels, solid_map, s2c);
+        CHR_HIP_CHECK(hipGetLastError());
+        CHR_HIP_CHECK(hipStreamSynchronize(stream));
+    }
+    return CHR_OK;
+}
+
+extern "C" int chr_photon_hits(const chr_photons *ph, int32_t start_photon, int32_t nphotons, uint32_t detection_state,
+                               const uint32_t *d_solid_map, const int32_t *d_solid_id_to_channel_index,
+                               const chr_photons *d_out, int32_t *d_out_channels, uint32_t *nhits, void *stream) {
+    return select_common(ph, start_photon, nphotons, detection_state, d_solid_map, d_solid_id_to_channel_index, 0, d_out,
+                         d_out_channels, nhits, (hipStream_t)stream);
+}
+
+extern "C" int chr_select_photons(const chr_photons *ph, int32_t start_photon, int32_t nphotons, uint32_t target_flag,
+                                  const chr_photons *d_out, uint32_t *nselected, void *stream) {
+    return select_common(ph, start_photon, nphotons, target_flag, nullptr, nullptr, 1, d_out, nullptr, nselected,
+                         (hipStream_t)stream);
+}
+
+extern "C" int chr_copy_photon_queue(const chr_photons *ph, int32_t first_photon, int32_t nphotons,
+                                     const uint32_t *d_queue, const chr_photons *d_out, void *stream) {
+    if (!photons_ok(ph) || !photons_ok(d_out) || !d_queue) return chr::fail(CHR_ERR_INVALID, "copy_queue: null argument");
+    if (nphotons <= 0) return CHR_OK;
+    hipLaunchKernelGGL(copy_queue_kernel, dim3(grid_for(nphotons)), dim3(BLOCK), 0, (hipStream_t)stream, to_ptrs(ph),
+                       first_photon, nphotons, d_queue, to_ptrs(d_out));
+    CHR_HIP_CHECK(hipGetLastError());
+    return CHR_OK;
+}
+
+extern "C" int chr_photon_duplicate(const chr_photons *ph, int32_t first_photon, int32_t nphotons, int32_t copies,
+                                    int32_t stride, void *stream) {
+    if (!photons_ok(ph)) return chr::fail(CHR_ERR_INVALID, "duplicate: null argument");
+    if (nphotons <= 0 || copies <= 0) return CHR_OK;
+    hipLaunchKernelGGL(duplicate_kernel, dim3(grid_for(nphotons)), dim3(BLOCK), 0, (hipStream_t)stream, to_ptrs(ph),
+                       first_photon, nphotons, copies, stride);
+    CHR_HIP_CHECK(hipGetLastError());
+    return CHR_OK;
+}
+
+extern "C" int chr_distance_to_mesh(const chr_geometry *g, uint32_t n, const float *d_origin, const float *d_direction,
+                                    float *d_distance, void *stream) {
+    if (!g || !d_origin || !d_direction || !d_distance) return chr::fail(CHR_ERR_INVALID, "distance_to_mesh: null argument");
+    if (n == 0) return CHR_OK;
+    hipLaunchKernelGGL(distance_kernel, dim3(grid_for(n)), dim3(BLOCK), 0, (hipStream_t)stream, g->dev, n, d_origin,
+                       d_direction, d_distance, (uint32_t *)nullptr);
+    CHR_HIP_CHECK(hipGetLastError());
+    return CHR_OK;
+}

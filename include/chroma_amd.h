@@ -154,6 +154,7 @@ typedef struct chr_propagate_stats {
     uint32_t launches;          /* chunk launches */
     uint32_t final_alive;       /* photons still in the queue at exit */
     uint32_t stack_overflows;   /* traversals that exceeded the 1000-entry stack */
+    double kernel_ms;           /* summed device time of the propagate kernels (HIP events) */
 } chr_propagate_stats;
 
 /* replaces: GPUPhotons.propagate host loop (chroma/gpu/photon.py:226-293) for
@@ -200,14 +201,17 @@ int chr_distance_to_mesh(const chr_geometry *g, uint32_t n, const float *d_origi
  * concatenate_layers/copy_and_offset and collapse_chains/collapse_child
  * (chroma/gpu/bvh.py:18-130, chroma/cuda/bvh.cu:148-384,530-543), on the host.
  * Leaves with equal Morton codes keep triangle order (stable sort; the
- * reference's numpy quicksort is unstable).  Two-phase: call with h_nodes=NULL
- * to get *nnodes and *nlayers, then again with buffers of that size. */
+ * reference's numpy quicksort is unstable).  The result is an opaque handle:
+ * query sizes with chr_bvh_result_info, copy out with chr_bvh_result_copy. */
+typedef struct chr_bvh_result chr_bvh_result;
 int chr_bvh_build_grid(const float *h_vertices, uint32_t nvertices,
                        const uint32_t *h_triangles, uint32_t ntriangles,
-                       int32_t target_degree, float *world_origin /*[3] out*/,
-                       float *world_scale /*out*/, uint32_t *h_nodes /*[nnodes*4] out*/,
-                       uint32_t *h_layer_offsets /*[nlayers] out*/,
-                       uint32_t *nnodes, uint32_t *nlayers);
+                       int32_t target_degree, chr_bvh_result **out);
+int chr_bvh_result_info(const chr_bvh_result *r, uint32_t *nnodes, uint32_t *nlayers,
+                        float *world_origin /*[3]*/, float *world_scale);
+int chr_bvh_result_copy(const chr_bvh_result *r, uint32_t *h_nodes /*[nnodes*4]*/,
+                        uint32_t *h_layer_offsets /*[nlayers]*/);
+int chr_bvh_result_free(chr_bvh_result *r);
 
 /* ------------------------------------------------------------- misc */
 const char *chr_last_error(void);

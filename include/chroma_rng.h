@@ -30,6 +30,12 @@
 
 #include "chroma_fmath.h"
 
+#if defined(__HIPCC__)
+#define CHR_HOST_FN __host__ static inline
+#else
+#define CHR_HOST_FN static inline
+#endif
+
 typedef struct { uint32_t d, v0, v1, v2, v3, v4; } chr_xorwow;
 
 CHR_FN uint32_t chr_xorwow_next(chr_xorwow *s) {
@@ -82,9 +88,8 @@ CHR_FN void chr_xw_matvec(const uint32_t *m, uint32_t v[5]) {
     v[0] = r0; v[1] = r1; v[2] = r2; v[3] = r3; v[4] = r4;
 }
 
-#if !defined(__HIP_DEVICE_COMPILE__)
 /* out = a o b (apply b first).  out must not alias a or b. */
-static inline void chr_xw_matmul(const uint32_t *a, const uint32_t *b, uint32_t *out) {
+CHR_HOST_FN void chr_xw_matmul(const uint32_t *a, const uint32_t *b, uint32_t *out) {
     for (int col = 0; col < 160; ++col) {
         uint32_t v[5];
         for (int k = 0; k < 5; ++k) v[k] = b[col * 5 + k];
@@ -94,7 +99,7 @@ static inline void chr_xw_matmul(const uint32_t *a, const uint32_t *b, uint32_t 
 }
 
 /* one-step transition matrix of the xorshift part */
-static inline void chr_xw_step_matrix(uint32_t *m) {
+CHR_HOST_FN void chr_xw_step_matrix(uint32_t *m) {
     for (int col = 0; col < 160; ++col) {
         uint32_t x[5] = {0, 0, 0, 0, 0};
         x[col / 32] = 1u << (col % 32);
@@ -105,7 +110,7 @@ static inline void chr_xw_step_matrix(uint32_t *m) {
 }
 
 /* seq[i] = A^(2^(67+i)), i = 0..nlevels-1; caller provides nlevels*800 words. */
-static inline void chr_xw_sequence_matrices(uint32_t *seq, int nlevels) {
+CHR_HOST_FN void chr_xw_sequence_matrices(uint32_t *seq, int nlevels) {
     uint32_t cur[CHR_XW_MATWORDS], tmp[CHR_XW_MATWORDS];
     chr_xw_step_matrix(cur);
     for (int i = 0; i < 67; ++i) { chr_xw_matmul(cur, cur, tmp); for (int k = 0; k < CHR_XW_MATWORDS; ++k) cur[k] = tmp[k]; }
@@ -117,7 +122,7 @@ static inline void chr_xw_sequence_matrices(uint32_t *seq, int nlevels) {
 }
 
 /* off[i] = A^(2^i), i = 0..nlevels-1 */
-static inline void chr_xw_offset_matrices(uint32_t *off, int nlevels) {
+CHR_HOST_FN void chr_xw_offset_matrices(uint32_t *off, int nlevels) {
     uint32_t cur[CHR_XW_MATWORDS], tmp[CHR_XW_MATWORDS];
     chr_xw_step_matrix(cur);
     for (int l = 0; l < nlevels; ++l) {
@@ -126,7 +131,6 @@ static inline void chr_xw_offset_matrices(uint32_t *off, int nlevels) {
         for (int k = 0; k < CHR_XW_MATWORDS; ++k) cur[k] = tmp[k];
     }
 }
-#endif
 
 /* curand_init(seed, subseq, offset) given precomputed jump tables
  * (seq: A^(2^(67+i)) for i < nseq; off: A^(2^i) for i < noff). */

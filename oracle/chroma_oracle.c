@@ -98,6 +98,7 @@ typedef struct {
     const chr_geometry_desc *d;
     uint64_t nodes_visited, tris_tested;   /* instrumentation (bytes/photon) */
     uint32_t max_depth, overflows;
+    uint64_t traversals;
 } Geo;
 
 /* ------------------------------------------------ geometry.h:30-74 */
@@ -245,6 +246,7 @@ static int intersect_mesh(Geo *g, f3 origin, f3 direction, float *min_distance, 
     f3 noid = mk(-origin.x / direction.x, -origin.y / direction.y, -origin.z / direction.z);
     f3 inv = mk(1.0f / direction.x, 1.0f / direction.y, 1.0f / direction.z);
     g->nodes_visited++;
+    g->traversals++;
     if (!intersect_node(noid, inv, &root, *min_distance)) return -1;
     uint32_t child_stack[STACK_SIZE], nchild_stack[STACK_SIZE];
     child_stack[0] = root.child; nchild_stack[0] = root.nchild;
@@ -916,7 +918,7 @@ static int propagate_one(Geo *g, Photons *ph, uint32_t photon_id, chr_xorwow *rn
 }
 
 typedef struct {
-    uint64_t nodes_visited, tris_tested, steps_traversed;
+    uint64_t nodes_visited, tris_tested, traversals;
     uint32_t max_depth, overflows, host_steps, launches;
 } orc_stats;
 
@@ -933,21 +935,21 @@ static inline void rng_store(uint32_t *st, uint32_t nslots, uint32_t s, const ch
 static void launch_chunk(const chr_geometry_desc *d, Photons *ph, uint32_t *rng, uint32_t nslots,
                          const uint32_t *input_queue, int first, int nthreads, uint8_t *alive,
                          int max_steps, int use_weights, int scatter_first, orc_stats *st, int nthreads_omp) {
-    uint64_t nv = 0, nt = 0;
+    uint64_t nv = 0, nt = 0, tv = 0;
     uint32_t md = 0, ov = 0;
-#pragma omp parallel for schedule(dynamic, 64) num_threads(nthreads_omp) reduction(+:nv,nt,ov) reduction(max:md)
+#pragma omp parallel for schedule(dynamic, 64) num_threads(nthreads_omp) reduction(+:nv,nt,ov,tv) reduction(max:md)
     for (int id = 0; id < nthreads; ++id) {
-        Geo g = {d, 0, 0, 0, 0};
+        Geo g = {d, 0, 0, 0, 0, 0};
         chr_xorwow r;
         rng_load(rng, nslots, (uint32_t)id, &r);
         uint32_t photon_id = input_queue[first + id];
         int processed;
         alive[id] = (uint8_t)propagate_one(&g, ph, photon_id, &r, max_steps, use_weights, scatter_first, &processed);
         if (processed) rng_store(rng, nslots, (uint32_t)id, &r);
-        nv += g.nodes_visited; nt += g.tris_tested; ov += g.overflows;
+        nv += g.nodes_visited; nt += g.tris_tested; ov += g.overflows; tv += g.traversals;
         if (g.max_depth > md) md = g.max_depth;
     }
-    st->nodes_visited += nv; st->tris_tested += nt; st->overflows += ov;
+    st->nodes_visited += nv; st->tris_tested += nt; st->overflows += ov; st->traversals += tv;
     if (md > st->max_depth) st->max_depth = md;
     st->launches++;
 }
@@ -991,7 +993,7 @@ EXPORT int orc_distance_to_mesh(const chr_geometry_desc *d, int n, const float *
     uint64_t nv = 0, nt = 0;
 #pragma omp parallel for reduction(+:nv,nt)
     for (int i = 0; i < n; ++i) {
-        Geo g = {d, 0, 0, 0, 0};
+        Geo g = {d, 0, 0, 0, 0, 0};
         f3 o = mk(origin[3 * i], origin[3 * i + 1], origin[3 * i + 2]);
         f3 dir = mk(direction[3 * i], direction[3 * i + 1], direction[3 * i + 2]);
         dir = divf(dir, norm(dir));
@@ -1063,6 +1065,7 @@ EXPORT int orc_propagate(const chr_geometry_desc *d, float *pos, float *dir, flo
         stats_out[0] = st.nodes_visited; stats_out[1] = st.tris_tested; stats_out[2] = st.max_depth;
         stats_out[3] = st.overflows; stats_out[4] = st.host_steps; stats_out[5] = st.launches;
         stats_out[6] = (step < max_steps) ? (uint64_t)(qin[0] - 1) : 0;
+        stats_out[7] = st.traversals;
     }
     free(qin); free(qout); free(alive);
     return 0;
@@ -1072,7 +1075,7 @@ EXPORT int orc_propagate(const chr_geometry_desc *d, float *pos, float *dir, flo
 EXPORT int orc_fill_state(const chr_geometry_desc *d, const float *posdir, int32_t last_hit, float wavelength,
                           float *out /*[8]: dist, nx,ny,nz, n1,n2,abs,scat*/, int32_t *iout /*[4]*/) {
     init_once();
-    Geo g = {d, 0, 0, 0, 0};
+    Geo g = {d, 0, 0, 0, 0, 0};
     Photon p;
     memset(&p, 0, sizeof(p));
     p.pos = mk(posdir[0], posdir[1], posdir[2]);

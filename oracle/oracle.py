@@ -1,0 +1,151 @@
+"""TEST INFRASTRUCTURE ONLY: ctypes front-end of the CPU oracle (liboracle.so).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg use this.
+The product never imports it.  See chroma_oracle.c for what is restated from
+the reference and how parity is pinned.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIBPATH = os.path.join(HERE, '_build', 'liboracle.so')
+_lib = None
+
+
+def build():
+    subprocess.check_call(['make', '-s', '-C', HERE])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIBPATH):
+            build()
+        l = ctypes.CDLL(LIBPATH)
+        vp, u32, i32, u64 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int, ctypes.c_ulonglong
+        l.orc_rng_init.argtypes = [vp, u32, u64, u64]
+        l.orc_sequence_matrices.argtypes = [vp, i32]
+        l.orc_rng_uniforms.argtypes = [vp, u32, u32, i32, vp]
+        l.orc_distance_to_mesh.argtypes = [vp, i32, vp, vp, vp, vp, vp]
+        l.orc_propagate.argtypes = [vp] + [vp] * 9 + [u32, u32, u32, vp, u32, i32, i32, i32, i32, i32, i32, vp]
+        l.orc_fill_state.argtypes = [vp, vp, ctypes.c_int32, ctypes.c_float, vp, vp]
+        l.orc_math.argtypes = [i32, i32, vp, vp, vp]
+        l.orc_rayleigh.argtypes = [i32, vp, vp, vp, u32]
+        _lib = l
+    return _lib
+
+
+def _p(a):
+    return a.ctypes.data if a is not None else None
+
+
+def rng_init(nslots, seed=1, offset=0):
+    st = np.zeros(6 * nslots, dtype=np.uint32)
+    lib().orc_rng_init(_p(st), nslots, seed, offset)
+    return st
+
+
+def sequence_matrices(nlevels):
+    out = np.zeros(nlevels * 800, dtype=np.uint32)
+    lib().orc_sequence_matrices(_p(out), nlevels)
+    return out.reshape(nlevels, 800)
+
+
+def uniforms(states, nslots, slot, n):
+    out = np.zeros(n, dtype=np.float32)
+    lib().orc_rng_uniforms(_p(states), nslots, slot, n, _p(out))
+    return out
+
+
+MATH = {'log': 0, 'exp': 1, 'sin': 2, 'cos': 3, 'tan': 4, 'asin': 5, 'acos': 6, 'atan2': 7}
+
+
+def math(name, x, y=None):
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    y = np.ascontiguousarray(y if y is not None else np.zeros_like(x), dtype=np.float32)
+    out = np.zeros_like(x)
+    lib().orc_math(MATH[name], len(x), _p(x), _p(y), _p(out))
+    return out
+
+
+def distance_to_mesh(packed, origins, directions):
+    o = np.ascontiguousarray(origins, dtype=np.float32).reshape(-1, 3)
+    d = np.ascontiguousarray(directions, dtype=np.float32).reshape(-1, 3)
+    dist = np.zeros(len(o), dtype=np.float32)
+    tri = np.zeros(len(o), dtype=np.int32)
+    counts = np.zeros(2, dtype=np.uint64)
+    desc = packed.desc()
+    lib().orc_distance_to_mesh(ctypes.addressof(desc), len(o), _p(o), _p(d), _p(dist), _p(tri), _p(counts))
+    return dist, tri, counts
+
+
+class HostPhotons(object):
+    """Writable host copies of the nine photon arrays (float3 as (n,3))."""
+    FIELDS = ('pos', 'dir', 'pol', 'wavelengths', 't', 'flags', 'last_hit_triangles', 'weights', 'evidx')
+    DTYPES = (np.float32, np.float32, np.float32, np.float32, np.float32, np.uint32, np.int32, np.float32, np.uint32)
+
+    def __init__(self, photons):
+        for f, dt in zip(self.FIELDS, self.DTYPES):
+            setattr(self, f, np.array(getattr(photons, f), dtype=dt, copy=True, order='C'))
+
+    def __len__(self):
+        return len(self.pos)
+
+
+def propagate(packed, photons, rng_states, nslots, nthreads_per_block=256, max_blocks=1024, max_steps=10,
+              use_weights=False, scatter_first=0, ncopies=1, true_nphotons=None, threads=None):
+    """GPUPhotons.propagate semantics on the host; photons (HostPhotons) and
+    rng_states are updated in place.  Returns the oracle's stats dict."""
+    n = len(photons)
+    true_n = n // ncopies if true_nphotons is None else true_nphotons
+    stats = np.zeros(8, dtype=np.uint64)
+    threads = threads or os.cpu_count() or 1
+    desc = packed.desc()
+    rc = lib().orc_propagate(ctypes.addressof(desc), _p(photons.pos), _p(photons.dir), _p(photons.pol),
+                             _p(photons.wavelengths), _p(photons.t), _p(photons.flags),
+                             _p(photons.last_hit_triangles), _p(photons.weights), _p(photons.evidx),
+                             n, true_n, ncopies, _p(rng_states), nslots, nthreads_per_block, max_blocks,
+                             max_steps, int(bool(use_weights)), int(scatter_first), threads, _p(stats))
+    if rc != 0:
+        raise RuntimeError('orc_propagate failed with status %d' % rc)
+    keys = ('nodes_visited', 'tris_tested', 'max_depth', 'overflows', 'host_steps', 'launches', 'final_alive',
+            'traversals')
+    return dict(zip(keys, (int(x) for x in stats[:8])))
+
+
+def fill_state(packed, pos, dir, last_hit=-1, wavelength=400.0):
+    pd = np.ascontiguousarray(np.concatenate([pos, dir]), dtype=np.float32)
+    out = np.zeros(8, dtype=np.float32)
+    iout = np.zeros(4, dtype=np.int32)
+    desc = packed.desc()
+    lib().orc_fill_state(ctypes.addressof(desc), _p(pd), int(last_hit), float(wavelength), _p(out), _p(iout))
+    return out, iout
+
+
+def rayleigh(dir, pol, states, nslots):
+    d = np.ascontiguousarray(dir, dtype=np.float32).copy()
+    p = np.ascontiguousarray(pol, dtype=np.float32).copy()
+    lib().orc_rayleigh(len(d), _p(d), _p(p), _p(states), nslots)
+    return d, p
+
+
+# ---- numpy restatements of the selection kernels (propagate.cu:29-251),
+# ascending photon order (the reference's warp-atomic order is arbitrary)
+def hits(photons, solid_id, solid_id_to_channel_index, detection_state=0x4, start=0, n=None):
+    n = len(photons) - start if n is None else n
+    sl = slice(start, start + n)
+    tri = np.asarray(photons.last_hit_triangles[sl])
+    flagged = (np.asarray(photons.flags[sl]) & detection_state) != 0
+    ok = flagged & (tri > -1)
+    channel = np.full(n, -1, dtype=np.int32)
+    channel[ok] = np.asarray(solid_id_to_channel_index)[np.asarray(solid_id)[tri[ok]]]
+    sel = ok & (channel >= 0)
+    return np.flatnonzero(sel) + start, channel[sel]
+
+
+def select(photons, target_flag, start=0, n=None):
+    n = len(photons) - start if n is None else n
+    return np.flatnonzero((np.asarray(photons.flags[start:start + n]) & target_flag) != 0) + start

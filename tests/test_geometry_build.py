@@ -1,0 +1,85 @@
+"""The host geometry layer reproduces the reference's meshes bit for bit
+(fixtures exported by tests/golden/make_golden.py)."""
+import hashlib
+import json
+import os
+
+import numpy as np
+
+from conftest import GOLDEN
+
+
+def _names(objs):
+    return np.array([('' if o is None else o.name) for o in objs])
+
+
+def test_pmt_solid_matches_reference():
+    from chroma.demo.pmt import build_8inch_pmt_with_lc
+    p = build_8inch_pmt_with_lc()
+    g = np.load(os.path.join(GOLDEN, 'pmt_lc_solid.npz'))
+    assert np.array_equal(p.mesh.vertices, g['vertices'])
+    assert np.array_equal(p.mesh.triangles, g['triangles'])
+    for k in ('material1', 'material2', 'surface'):
+        assert np.array_equal(_names(getattr(p, k)), g[k])
+    assert np.array_equal(p.color, g['color'])
+
+
+def test_cube_matches_reference():
+    from chroma import make
+    c = make.cube(1000.0)
+    g = np.load(os.path.join(GOLDEN, 'cube_1000.npz'))
+    assert np.array_equal(c.vertices, g['vertices']) and np.array_equal(c.triangles, g['triangles'])
+
+
+def test_small_detector_flatten_matches_reference(small_detector):
+    d = small_detector
+    g = np.load(os.path.join(GOLDEN, 'detector_small.npz'))
+    assert np.array_equal(d.mesh.vertices, g['vertices'])
+    assert np.array_equal(d.mesh.triangles, g['triangles'])
+    assert np.array_equal(d.solid_id, g['solid_id'])
+    assert np.array_equal(d.colors, g['colors'])
+    mn = _names(d.unique_materials)
+    sn = _names(d.unique_surfaces)
+    # index order may differ (the reference orders by set() hash), names must not
+    assert np.array_equal(mn[d.material1_index], g['material_names'][g['material1_index']])
+    assert np.array_equal(mn[d.material2_index], g['material_names'][g['material2_index']])
+    s, gs = d.surface_index, g['surface_index']
+    assert np.array_equal(s < 0, gs < 0)
+    assert np.array_equal(sn[s[s >= 0]], g['surface_names'][gs[gs >= 0]])
+    assert np.array_equal(d.solid_id_to_channel_index, g['solid_id_to_channel_index'])
+    assert np.array_equal(d.time_cdf[1], g['time_cdf_y']) and np.array_equal(d.charge_cdf[0], g['charge_cdf_x'])
+
+
+def test_tiny_detector_hashes():
+    from chroma import demo
+    h = json.load(open(os.path.join(GOLDEN, 'reference_hashes.json')))['tiny']
+    t = demo.tiny()
+    t.flatten()
+    md5 = lambda a: hashlib.md5(np.ascontiguousarray(a).tobytes()).hexdigest()   # noqa: E731
+    assert len(t.mesh.triangles) == h['triangles'] and len(t.mesh.vertices) == h['vertices']
+    assert t.num_channels() == h['channels']
+    assert md5(t.mesh.triangles.astype(np.int64)) == h['md5_triangles']
+    assert md5(t.solid_id.astype(np.int64)) == h['md5_solid_id']
+    assert float(t.mesh.vertices.astype(np.float64).sum()) == h['vertex_sum']
+
+
+def test_from_film_matches_reference():
+    from chroma import tools
+    h = json.load(open(os.path.join(GOLDEN, 'reference_hashes.json')))
+    pos, d = tools.from_film()
+    m = hashlib.md5(np.asarray(pos, np.float64).tobytes())
+    m.update(np.asarray(d, np.float64).tobytes())
+    assert m.hexdigest() == h['from_film_md5']
+
+
+def test_packing_tables(small_detector, small_packed):
+    """Tables are np.interp onto 60..995 nm, float32, padded by one element."""
+    from chroma.geometry import standard_wavelengths
+    pk = small_packed
+    assert len(pk.wavelengths) == 188 and pk.wavelength_step == 5.0
+    for m, mp in zip(small_detector.unique_materials, pk.materials):
+        ri = np.interp(standard_wavelengths, m.refractive_index[:, 0], m.refractive_index[:, 1]).astype(np.float32)
+        assert np.array_equal(mp['refractive_index'][:-1], ri) and mp['refractive_index'][-1] == ri[-1]
+    codes = pk.material_codes
+    assert np.array_equal((codes >> 24) & 0xFF, small_detector.material1_index & 0xFF)
+    assert np.array_equal((codes >> 8) & 0xFF, small_detector.surface_index & 0xFF)

@@ -1,0 +1,37 @@
+"""The C-ABI library loads and exports every symbol include/chroma_amd.h declares
+(no device calls: runs without a GPU)."""
+import ctypes
+import os
+import re
+
+from conftest import ROOT
+
+
+def declared_symbols():
+    text = open(os.path.join(ROOT, 'include', 'chroma_amd.h')).read()
+    text = re.sub(r'/\*.*?\*/', '', text, flags=re.S)
+    return sorted(set(re.findall(r'\b(chr_[a-z0-9_]+)\s*\(', text)))
+
+
+def test_library_exports_all_declared_symbols():
+    from chroma.gpu import _native
+    lib = ctypes.CDLL(_native.library_path())
+    names = declared_symbols()
+    assert len(names) >= 15
+    missing = [n for n in names if not hasattr(lib, n)]
+    assert not missing, missing
+    assert set(names) == set(_native.EXPORTED)
+
+
+def test_version_and_error_string():
+    from chroma.gpu import _native
+    l = _native.lib()
+    assert l.chr_version() == 1
+    assert isinstance(l.chr_last_error(), bytes)
+
+
+def test_invalid_arguments_fail_loudly():
+    import pytest
+    from chroma.gpu import _native
+    with pytest.raises(_native.NativeError):
+        _native.call('chr_bvh_build_grid', None, 0, None, 0, 3, ctypes.byref(ctypes.c_void_p()))
