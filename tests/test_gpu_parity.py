@@ -102,7 +102,7 @@ def test_propagate_multi_launch_parity(cuda, small_detector, small_packed):
     """Per-step relaunch + survivor compaction + chunks sharing RNG slots."""
     from chroma.photon_source import isotropic
     photons = isotropic(30000, seed=12)
-    gp, host, rng, st, stats = _run_both(small_detector, small_packed, photons, 64, 64, 64, 1000)
+    gp, host, rng, st, stats = _run_both(small_detector, small_packed, photons, 64 * 64, 64, 64, 1000)
     _compare(host, gp, 'multi-launch')
     assert np.array_equal(rng.get().reshape(-1), st)
     assert stats['host_steps'] > 1 and stats['launches'] > stats['host_steps']
@@ -121,9 +121,11 @@ def test_physics_scene_parity(cuda, use_weights, scatter_first):
                                          use_weights=use_weights, scatter_first=scatter_first)
     _compare(host, gp, 'scene w=%s sf=%s' % (use_weights, scatter_first))
     assert np.array_equal(rng.get().reshape(-1), st)
-    fl = host.flags
-    for bit in (1 << 1, 1 << 3, 1 << 4, 1 << 5, 1 << 6, 1 << 7, 1 << 8, 1 << 9):
-        assert ((fl & bit) != 0).any(), 'branch bit %d never exercised' % bit
+    if not use_weights and scatter_first == 0:     # use_weights disables bulk absorption
+        fl = host.flags
+        for bit in (1 << 1, 1 << 3, 1 << 4, 1 << 5, 1 << 6, 1 << 7, 1 << 8, 1 << 9):
+            assert ((fl & bit) != 0).any(), 'branch bit %d never exercised' % bit
+        assert (host.last_hit_triangles == -2).any(), 'wire planes never hit'
 
 
 def test_ncopies_and_selection_parity(cuda, small_detector, small_packed):
