@@ -20,6 +20,7 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <cstdlib>
 #include <vector>
 
 #include "../../include/chroma_amd.h"
@@ -164,6 +165,11 @@ __device__ __forceinline__ bool intersect_triangle(V3 o, V3 d, V3 v0, V3 e1, V3 
 }
 
 // mesh.h:45-126 -- nearest triangle != last_hit; reference DFS order.
+// The children of a popped group are fetched BATCH at a time (independent
+// 16-byte loads in flight together), their slab tests computed up front, and
+// then walked strictly in index order with the reference's prune / accept /
+// push decisions, so the result (including tie-breaking) is unchanged.
+template <int BATCH>
 __device__ int intersect_mesh(const DevGeom &g, V3 o, V3 d, float &min_distance, int last_hit, Stack &st,
                               uint32_t &overflow) {
     int triangle_index = -1;
@@ -183,40 +189,52 @@ __device__ int intersect_mesh(const DevGeom &g, V3 o, V3 d, float &min_distance,
     while (curr >= 0) {
         const uint32_t w = stack_get(st, curr);
         curr--;
-        const uint32_t first = w & 0x0FFFFFFFu;
-        const uint32_t end = first + (w >> 28);
-        for (uint32_t i = first; i < end; ++i) {
-            const uint4 node = g.nodes[i];
-            V3 lo, hi;
-            node_bounds(g, node, lo, hi);
-            float bd;
-            if (!intersect_box(noid, inv, lo, hi, bd)) continue;
-            if (min_distance >= 0.0f && bd > min_distance) continue;
-            const uint32_t child = node.w & 0x0FFFFFFFu;
-            if ((node.w >> 28) == 0) {
-                if (child != last) {
-                    const float4 r0 = g.tri[3 * (size_t)child], r1 = g.tri[3 * (size_t)child + 1],
-                                 r2 = g.tri[3 * (size_t)child + 2];
-                    float dist;
-                    if (intersect_triangle(o, d, v3(r0.x, r0.y, r0.z), v3(r0.w, r1.x, r1.y), v3(r1.z, r1.w, r2.x), dist)) {
-                        if (triangle_index == -1 || dist < min_distance) {
-                            triangle_index = (int)child;
-                            min_distance = dist;
+        const uint32_t end = (w & 0x0FFFFFFFu) + (w >> 28);
+        for (uint32_t i = w & 0x0FFFFFFFu; i < end; i += BATCH) {
+            uint4 nd[BATCH];
+#pragma unroll
+            for (int k = 0; k < BATCH; ++k)
+                if (i + k < end) nd[k] = g.nodes[i + k];
+            float bd[BATCH];
+            bool hit[BATCH];
+#pragma unroll
+            for (int k = 0; k < BATCH; ++k) {
+                V3 lo, hi;
+                node_bounds(g, nd[k], lo, hi);
+                hit[k] = (i + k < end) && intersect_box(noid, inv, lo, hi, bd[k]);
+            }
+#pragma unroll
+            for (int k = 0; k < BATCH; ++k) {
+                if (!hit[k]) continue;
+                if (min_distance >= 0.0f && bd[k] > min_distance) continue;
+                const uint32_t child = nd[k].w & 0x0FFFFFFFu;
+                if ((nd[k].w >> 28) == 0) {
+                    if (child != last) {
+                        const float4 *r = g.tri + 3 * (size_t)child;
+                        const float4 r0 = r[0], r1 = r[1], r2 = r[2];
+                        float dist;
+                        if (intersect_triangle(o, d, v3(r0.x, r0.y, r0.z), v3(r0.w, r1.x, r1.y), v3(r1.z, r1.w, r2.x),
+                                               dist)) {
+                            if (triangle_index == -1 || dist < min_distance) {
+                                triangle_index = (int)child;
+                                min_distance = dist;
+                            }
                         }
                     }
+                } else {
+                    if (curr + 1 >= STACK_SIZE) {
+                        overflow++;
+                        return triangle_index;
+                    }
+                    curr++;
+                    stack_put(st, curr, nd[k].w);
                 }
-            } else {
-                if (curr + 1 >= STACK_SIZE) {
-                    overflow++;
-                    return triangle_index;
-                }
-                curr++;
-                stack_put(st, curr, node.w);
             }
         }
     }
     return triangle_index;
 }
+
 
 // ---------------------------------------------------------------- photon.h
 __device__ __forceinline__ int convert(int c) { return (c & 0x80) ? (int)(0xFFFFFF00u | (uint32_t)c) : c; }
@@ -325,8 +343,9 @@ __device__ __noinline__ void wireplanes(const DevGeom &g, const Photon &p, float
 }
 
 // photon.h:87-397
+template <int BATCH>
 __device__ __forceinline__ void fill_state(const DevGeom &g, State &s, Photon &p, Stack &st, uint32_t &overflow) {
-    const int mesh_triangle = intersect_mesh(g, p.pos, p.dir, s.distance, p.last_hit, st, overflow);
+    const int mesh_triangle = intersect_mesh<BATCH>(g, p.pos, p.dir, s.distance, p.last_hit, st, overflow);
     int m1, m2;
     bool use_analytic = false;
     int a_surface = -1, a_inner = -1, a_outer = -1;
@@ -810,8 +829,10 @@ struct PropagateArgs {
 __device__ __forceinline__ V3 load3(const float *p, uint32_t i) { return v3(p[3 * i], p[3 * i + 1], p[3 * i + 2]); }
 __device__ __forceinline__ void store3(float *p, uint32_t i, V3 v) { p[3 * i] = v.x; p[3 * i + 1] = v.y; p[3 * i + 2] = v.z; }
 
-// propagate.cu:254-366
-__global__ __launch_bounds__(BLOCK) void propagate_kernel(PropagateArgs a) {
+// propagate.cu:254-366.  BATCH: children fetched together per group;
+// MINW: minimum waves per SIMD requested from the register allocator.
+template <int BATCH, int MINW>
+__global__ __launch_bounds__(BLOCK, MINW) void propagate_kernel(PropagateArgs a) {
     __shared__ uint32_t lds_stack[STACK_LDS * BLOCK];
     const int id = blockIdx.x * BLOCK + threadIdx.x;
     unsigned alive = 0;
@@ -844,7 +865,7 @@ __global__ __launch_bounds__(BLOCK) void propagate_kernel(PropagateArgs a) {
                 steps++;
                 const float prod = ((((p.dir.x * p.dir.y) * p.dir.z) * p.pos.x) * p.pos.y) * p.pos.z;
                 if (chr_isnan(prod)) { p.history |= CHR_NO_HIT | CHR_NAN_ABORT; break; }
-                fill_state(g, s, p, st, overflow);
+                fill_state<BATCH>(g, s, p, st, overflow);
                 if (p.last_hit == -1) break;
                 int command = propagate_to_boundary(g, p, s, rng, a.use_weights, scatter_first);
                 scatter_first = 0;
@@ -1019,7 +1040,7 @@ __global__ __launch_bounds__(BLOCK) void distance_kernel(DevGeom g, uint32_t n, 
     st.lds = lds_stack + threadIdx.x;
     uint32_t overflow = 0;
     float dist;
-    const int tri = intersect_mesh(g, o, d, dist, -1, st, overflow);
+    const int tri = intersect_mesh<4>(g, o, d, dist, -1, st, overflow);
     if (tri != -1) distance[id] = dist;
     if (overflow && counters) atomicAdd(counters, overflow);
 }
@@ -1116,6 +1137,26 @@ extern "C" uint64_t chr_propagate_scratch_words(uint32_t nthreads) {
     return 2 * nwords /*masks*/ + nwords /*offsets*/ + 8;
 }
 
+// Kernel variants (A/B-able at run time with CHR_PROPAGATE_VARIANT=<n>;
+// all produce identical results, they differ only in schedule/occupancy).
+typedef void (*propagate_fn)(PropagateArgs);
+// measured on demo.detector(), 4M photons (profiles/r01/ab_variants.log):
+// <1,3> 89.2 ms, <4,3> 74.9, <4,4> 66.8, <4,5> 66.5, <8,4> 64.3, <8,3> 74.1, <2,3> 76.5
+static const propagate_fn kVariants[] = {
+    propagate_kernel<8, 4>,   // 0: default
+    propagate_kernel<1, 3>,   // 1: reference-shaped one-node-at-a-time walk
+    propagate_kernel<4, 4>,   // 2
+    propagate_kernel<8, 5>,   // 3
+    propagate_kernel<8, 6>,   // 4
+    propagate_kernel<16, 4>,  // 5
+};
+static propagate_fn select_variant() {
+    const char *e = getenv("CHR_PROPAGATE_VARIANT");   // read per launch: A/B in one process
+    int v = e ? atoi(e) : 0;
+    if (v < 0 || v >= (int)(sizeof(kVariants) / sizeof(kVariants[0]))) v = 0;
+    return kVariants[v];
+}
+
 // scratch layout (u32 words): [0..7] counters/base; masks (u64, 8-aligned); offsets
 static int launch_chunk(const chr_geometry *g, const chr_photons *ph, uint32_t *rng, uint32_t nslots, int32_t first,
                         int32_t nthreads, const uint32_t *in_queue, uint32_t *out_queue, int32_t max_steps,
@@ -1133,7 +1174,7 @@ static int launch_chunk(const chr_geometry *g, const chr_photons *ph, uint32_t *
     a.max_steps = max_steps; a.use_weights = use_weights; a.scatter_first = scatter_first;
     a.alive_masks = masks; a.counters = counters;
     if (ev0) CHR_HIP_CHECK(hipEventRecord(ev0, stream));
-    hipLaunchKernelGGL(propagate_kernel, dim3(grid_for(nthreads)), dim3(BLOCK), 0, stream, a);
+    hipLaunchKernelGGL(select_variant(), dim3(grid_for(nthreads)), dim3(BLOCK), 0, stream, a);
     if (ev1) CHR_HIP_CHECK(hipEventRecord(ev1, stream));
     hipLaunchKernelGGL(scan_masks_kernel, dim3(1), dim3(1024), 0, stream, masks, nwords, offsets, out_queue,
                        counters + 1, (uint32_t *)nullptr);

@@ -1,0 +1,68 @@
+#!/usr/bin/env python
+"""A/B the propagate-kernel variants (CHR_PROPAGATE_VARIANT) in ONE process,
+interleaved rounds (cdna_hip_programming.md 5.4 rule 24).  Checks that every
+variant gives identical photon histories.  Dev tool, not part of the product."""
+import argparse
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, 'chroma-lite_amd'))
+
+import numpy as np  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--detector', default='demo')
+    ap.add_argument('--photons', type=int, default=4_000_000)
+    ap.add_argument('--variants', default='0,1,2,3,4,5,6')
+    ap.add_argument('--rounds', type=int, default=3)
+    ap.add_argument('--max-steps', type=int, default=1000)
+    args = ap.parse_args()
+    import torch
+    import bench
+    from chroma import gpu
+    from chroma.gpu import gpuarray as ga
+    from chroma.photon_source import isotropic
+    from types import SimpleNamespace
+    torch.cuda.set_device(0)
+    det = bench.build_geometry(args.detector, '/tmp/chroma_bench_cache')
+    gdet = gpu.GPUDetector(det)
+    photons = isotropic(args.photons, seed=20260102)
+    pristine = SimpleNamespace(pos=ga.to_gpu(gpu.to_float3(photons.pos)), dir=ga.to_gpu(gpu.to_float3(photons.dir)),
+                               pol=ga.to_gpu(gpu.to_float3(photons.pol)), wavelengths=ga.to_gpu(photons.wavelengths),
+                               t=ga.to_gpu(photons.t), flags=ga.to_gpu(photons.flags), evidx=ga.to_gpu(photons.evidx),
+                               true_nphotons=args.photons)
+    variants = [int(v) for v in args.variants.split(',')]
+    times = {v: [] for v in variants}
+    kms = {v: [] for v in variants}
+    ref_flags = None
+    for r in range(args.rounds + 1):
+        for v in variants:
+            os.environ['CHR_PROPAGATE_VARIANT'] = str(v)
+            rng = gpu.get_rng_states(512 * 1024, seed=1)
+            gp = gpu.GPUPhotons(pristine, copy_flags=True, copy_triangles=False, copy_weights=False)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            gp.propagate(gdet, rng, nthreads_per_block=512, max_blocks=1024, max_steps=args.max_steps)
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - t0
+            fl = gp.flags.get()
+            if ref_flags is None:
+                ref_flags = fl
+            elif not np.array_equal(fl, ref_flags):
+                print('VARIANT %d DIFFERS' % v, flush=True)
+            if r > 0:
+                times[v].append(dt)
+                kms[v].append(gp.last_stats.kernel_ms)
+    for v in variants:
+        print('variant %d: wall %.1f ms (min %.1f)  kernel %.1f ms  -> %.1f Mphotons/s' % (
+            v, 1e3 * np.median(times[v]), 1e3 * min(times[v]), np.median(kms[v]),
+            args.photons / np.median(times[v]) / 1e6), flush=True)
+
+
+if __name__ == '__main__':
+    main()
