@@ -88,6 +88,11 @@ _SIGNATURES = {
                                     ctypes.POINTER(c_f32)]),
     'chr_bvh_result_copy': (c_i32, [c_vp, c_vp, c_vp]),
     'chr_bvh_result_free': (c_i32, [c_vp]),
+    'chr_wide_bvh_build': (c_i32, [ctypes.POINTER(GeometryDesc), ctypes.POINTER(c_vp)]),
+    'chr_wide_bvh_info': (c_i32, [c_vp, ctypes.POINTER(c_u32), ctypes.POINTER(c_u32), ctypes.POINTER(c_u32),
+                                  ctypes.POINTER(ctypes.c_int32)]),
+    'chr_wide_bvh_copy': (c_i32, [c_vp, c_vp, c_vp]),
+    'chr_wide_bvh_free': (c_i32, [c_vp]),
     'chr_last_error': (ctypes.c_char_p, []),
     'chr_version': (c_i32, []),
 }

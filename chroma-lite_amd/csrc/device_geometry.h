@@ -8,8 +8,10 @@
 // Here:
 //  * DevGeom is passed BY VALUE as a kernel argument (lands in SGPRs, no
 //    per-block copy);
-//  * BVH nodes stay the reference's 16-byte quantised uint4 (so the traversal
-//    order, and therefore nearest-hit tie-breaking, is the reference's);
+//  * BVH nodes stay the reference's 16-byte quantised uint4 (the exact-order
+//    traversal variant walks them); the default traversal walks an 8-wide SAH
+//    BVH built over the same leaf boxes with the reference DFS rank as the
+//    nearest-hit tie-break (wide_bvh.h) -- same answers, far fewer nodes;
 //  * triangles are de-indexed into 48-byte records of three float4:
 //        (v0.x v0.y v0.z e1.x) (e1.y e1.z e2.x e2.y) (e2.z e3.x e3.y e3.z)
 //    with e1 = v1-v0, e2 = v2-v0 (the Moller-Trumbore edges, intersect.h:26-101)
@@ -51,6 +53,9 @@ struct DevGeom {
     const DevMaterial *materials;
     const DevSurface *surfaces;
     const chr_wireplane_desc *wireplanes;
+    const uint4 *wnodes;             // 8-wide SAH BVH, 6 uint4 per node (wide_bvh.h)
+    const float4 *wtri;              // 3 float4 per leaf triangle record (wide_bvh.h)
+    uint32_t nwnodes, nwtri;
     float ox, oy, oz, scale;         // world_origin, world_scale
     uint32_t nnodes, ntriangles, nwireplanes;
     uint32_t wl_n;
@@ -65,6 +70,6 @@ struct chr_geometry {
     chr::DevGeom dev;
     int device;
     uint64_t bytes;
-    void *allocs[8];
+    void *allocs[12];
     int nallocs;
 };

@@ -4,6 +4,8 @@
 // and the Material/Surface/WirePlane make_gpu_struct packing.
 #include <hip/hip_runtime_api.h>
 
+#include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -11,6 +13,7 @@
 
 #include "../../include/chroma_amd.h"
 #include "common.h"
+#include "wide_bvh.h"
 #include "device_geometry.h"
 
 namespace chr {
@@ -131,6 +134,20 @@ extern "C" int chr_geometry_create(const chr_geometry_desc *d, chr_geometry **ou
         if ((rc = dev_upload(g, tri.data(), tri.size() * sizeof(float), &p))) throw rc;
         dg.tri = (const float4 *)p;
         std::vector<float>().swap(tri);
+
+        {
+            chr::WideBVH wb;
+            if ((rc = chr::build_wide_bvh(d, wb))) throw rc;
+            if (wb.usable && !std::getenv("CHR_EXACT_ORDER_ONLY")) {
+                if ((rc = dev_upload(g, wb.nodes.data(), wb.nodes.size() * sizeof(chr::WideNode), &p))) throw rc;
+                dg.wnodes = (const uint4 *)p;
+                if ((rc = dev_upload(g, wb.tri.data(), std::max<size_t>(1, wb.tri.size()) * sizeof(chr::WideTri), &p)))
+                    throw rc;
+                dg.wtri = (const float4 *)p;
+                dg.nwnodes = (uint32_t)wb.nodes.size();
+                dg.nwtri = (uint32_t)wb.tri.size();
+            }
+        }
 
         if ((rc = dev_upload(g, d->h_material_codes, (size_t)d->ntriangles * 4, &p))) throw rc;
         dg.material_codes = (const uint32_t *)p;

@@ -29,6 +29,7 @@
 #include "common.h"
 #include "device_geometry.h"
 #include "device_math.h"
+#include "wide_bvh.h"
 
 namespace chr {
 
@@ -235,6 +236,122 @@ __device__ int intersect_mesh(const DevGeom &g, V3 o, V3 d, float &min_distance,
     return triangle_index;
 }
 
+// ---------------------------------------------------------------- wide traversal
+// The same nearest-hit query over the 8-wide SAH BVH (wide_bvh.h).  Each
+// triangle is still admitted by the reference's own leaf test (slab test of
+// its reference leaf box + prune `box distance > best`), then Moller-Trumbore,
+// and the winner is the minimum of (distance, reference DFS rank) -- exactly
+// the triangle the reference's strict-'<' DFS keeps (wide_bvh.cpp explains
+// why the tested set covers the reference's).  Stack: top WIDE_LDS entries
+// (node, entry distance) in LDS, the rest in scratch; nearest inner child
+// first, the others pushed and culled at pop against the running best.
+constexpr int WIDE_LDS = 16;
+
+struct WStack {
+    uint32_t *node;     // this work-item's LDS column: entry i at node[i * BLOCK]
+    float *dist;
+    uint2 spill[WIDE_STACK - WIDE_LDS];
+};
+
+__device__ __forceinline__ void wpush(WStack &s, int i, uint32_t n, float t) {
+    if (i < WIDE_LDS) { s.node[i * BLOCK] = n; s.dist[i * BLOCK] = t; }
+    else s.spill[i - WIDE_LDS] = make_uint2(n, __float_as_uint(t));
+}
+__device__ __forceinline__ void wpop(const WStack &s, int i, uint32_t &n, float &t) {
+    if (i < WIDE_LDS) { n = s.node[i * BLOCK]; t = s.dist[i * BLOCK]; }
+    else { const uint2 e = s.spill[i - WIDE_LDS]; n = e.x; t = __uint_as_float(e.y); }
+}
+
+__device__ __forceinline__ float byte_f(uint32_t lo4, uint32_t hi4, int k) {   // byte k of (hi4:lo4) as float
+    const uint32_t w = k < 4 ? lo4 : hi4;
+    return (float)((w >> (8 * (k & 3))) & 0xFFu);
+}
+__device__ __forceinline__ float exp_scale(uint32_t e) { return __uint_as_float((e & 0xFFu) << 23); }
+
+__device__ int intersect_wide(const DevGeom &g, V3 o, V3 d, float &min_distance, int last_hit, WStack &st,
+                              uint32_t &overflow) {
+    const V3 noid = v3(-o.x / d.x, -o.y / d.y, -o.z / d.z);
+    const V3 inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    float best = __builtin_inff();
+    uint32_t best_rank = 0xFFFFFFFFu;
+    int best_id = -1;
+    const uint32_t last = (uint32_t)last_hit;
+    int sp = 0;
+    uint32_t node = 0;
+    while (true) {
+        const uint4 *np = g.wnodes + 6 * (size_t)node;
+        const uint4 h = np[0], a1 = np[1], a2 = np[2], a3 = np[3], a4 = np[4], a5 = np[5];
+        const V3 org = v3(__uint_as_float(h.x), __uint_as_float(h.y), __uint_as_float(h.z));
+        const float sx = exp_scale(h.w), sy = exp_scale(h.w >> 8), sz = exp_scale(h.w >> 16);
+        uint32_t leaf_mask = 0;
+        uint32_t near_node = 0xFFFFFFFFu;
+        float near_t = 0.0f;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const uint32_t kind = ((k < 4 ? a4.z : a4.w) >> (8 * (k & 3))) & 0xFFu;
+            if (kind == 0) continue;
+            const V3 lo = v3(__builtin_fmaf(byte_f(a1.x, a1.y, k), sx, org.x), __builtin_fmaf(byte_f(a1.z, a1.w, k), sy, org.y),
+                             __builtin_fmaf(byte_f(a2.x, a2.y, k), sz, org.z));
+            const V3 hi = v3(__builtin_fmaf(byte_f(a2.z, a2.w, k), sx, org.x), __builtin_fmaf(byte_f(a3.x, a3.y, k), sy, org.y),
+                             __builtin_fmaf(byte_f(a3.z, a3.w, k), sz, org.z));
+            float bd;
+            if (!intersect_box(noid, inv, lo, hi, bd) || bd > best) continue;
+            if (kind != WIDE_INNER) { leaf_mask |= 1u << k; continue; }
+            const uint32_t child = a4.x + (((k < 4 ? a5.x : a5.y) >> (8 * (k & 3))) & 0xFFu);
+            if (near_node == 0xFFFFFFFFu) { near_node = child; near_t = bd; continue; }
+            // keep the nearer one in hand, push the other
+            uint32_t pn = child;
+            float pt = bd;
+            if (bd < near_t) { pn = near_node; pt = near_t; near_node = child; near_t = bd; }
+            if (sp >= WIDE_STACK) { overflow++; break; }
+            wpush(st, sp, pn, pt);
+            sp++;
+        }
+        const unsigned long long kinds = ((unsigned long long)a4.w << 32) | a4.z;
+        const unsigned long long offs = ((unsigned long long)a5.y << 32) | a5.x;
+        while (leaf_mask) {
+            const int k = __builtin_ctz(leaf_mask);
+            leaf_mask &= leaf_mask - 1;
+            const uint32_t cnt = (uint32_t)(kinds >> (8 * k)) & 0xFFu;
+            const uint32_t first = a4.y + ((uint32_t)(offs >> (8 * k)) & 0xFFu);
+            for (uint32_t j = 0; j < cnt; ++j) {
+                const float4 *r = g.wtri + 4 * (size_t)(first + j);
+                const float4 r0 = r[0], r1 = r[1], r2 = r[2], r3 = r[3];
+                const uint32_t id = __float_as_uint(r2.y);
+                if (id == last) continue;
+                V3 lo, hi;
+                node_bounds(g, make_uint4(__float_as_uint(r2.w), __float_as_uint(r3.x), __float_as_uint(r3.y), 0u), lo, hi);
+                float bd;
+                if (!intersect_box(noid, inv, lo, hi, bd) || bd > best) continue;   // mesh.h:94-96
+                float dist;
+                if (!intersect_triangle(o, d, v3(r0.x, r0.y, r0.z), v3(r0.w, r1.x, r1.y), v3(r1.z, r1.w, r2.x), dist))
+                    continue;
+                const uint32_t rank = __float_as_uint(r2.z);
+                if (dist < best || (dist == best && rank < best_rank)) {
+                    best = dist;
+                    best_rank = rank;
+                    best_id = (int)id;
+                }
+            }
+        }
+        if (near_node != 0xFFFFFFFFu && !(near_t > best)) {
+            node = near_node;
+            continue;
+        }
+        // pop, culling entries whose box starts beyond the best hit
+        bool found = false;
+        while (sp > 0) {
+            sp--;
+            float t;
+            wpop(st, sp, node, t);
+            if (!(t > best)) { found = true; break; }
+        }
+        if (!found) break;
+    }
+    min_distance = best_id == -1 ? -1.0f : best;
+    return best_id;
+}
+
 
 // ---------------------------------------------------------------- photon.h
 __device__ __forceinline__ int convert(int c) { return (c & 0x80) ? (int)(0xFFFFFF00u | (uint32_t)c) : c; }
@@ -343,9 +460,12 @@ __device__ __noinline__ void wireplanes(const DevGeom &g, const Photon &p, float
 }
 
 // photon.h:87-397
-template <int BATCH>
-__device__ __forceinline__ void fill_state(const DevGeom &g, State &s, Photon &p, Stack &st, uint32_t &overflow) {
-    const int mesh_triangle = intersect_mesh<BATCH>(g, p.pos, p.dir, s.distance, p.last_hit, st, overflow);
+template <int BATCH, bool WIDE>
+__device__ __forceinline__ void fill_state(const DevGeom &g, State &s, Photon &p, Stack &st, WStack &wst,
+                                           uint32_t &overflow) {
+    int mesh_triangle;
+    if constexpr (WIDE) mesh_triangle = intersect_wide(g, p.pos, p.dir, s.distance, p.last_hit, wst, overflow);
+    else mesh_triangle = intersect_mesh<BATCH>(g, p.pos, p.dir, s.distance, p.last_hit, st, overflow);
     int m1, m2;
     bool use_analytic = false;
     int a_surface = -1, a_inner = -1, a_outer = -1;
@@ -831,9 +951,9 @@ __device__ __forceinline__ void store3(float *p, uint32_t i, V3 v) { p[3 * i] = 
 
 // propagate.cu:254-366.  BATCH: children fetched together per group;
 // MINW: minimum waves per SIMD requested from the register allocator.
-template <int BATCH, int MINW>
+template <int BATCH, int MINW, bool WIDE>
 __global__ __launch_bounds__(BLOCK, MINW) void propagate_kernel(PropagateArgs a) {
-    __shared__ uint32_t lds_stack[STACK_LDS * BLOCK];
+    __shared__ uint32_t lds_stack[WIDE ? 2 * WIDE_LDS * BLOCK : STACK_LDS * BLOCK];
     const int id = blockIdx.x * BLOCK + threadIdx.x;
     unsigned alive = 0;
     if (id < a.nthreads) {
@@ -855,7 +975,10 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_kernel(PropagateArgs a)
             p.last_hit = a.last_hit[photon_id];
             p.weight = a.weights[photon_id];
             Stack st;
+            WStack wst;
             st.lds = lds_stack + threadIdx.x;
+            wst.node = lds_stack + threadIdx.x;
+            wst.dist = reinterpret_cast<float *>(lds_stack) + WIDE_LDS * BLOCK + threadIdx.x;
             uint32_t overflow = 0;
             State s;
             int scatter_first = a.scatter_first;
@@ -865,7 +988,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_kernel(PropagateArgs a)
                 steps++;
                 const float prod = ((((p.dir.x * p.dir.y) * p.dir.z) * p.pos.x) * p.pos.y) * p.pos.z;
                 if (chr_isnan(prod)) { p.history |= CHR_NO_HIT | CHR_NAN_ABORT; break; }
-                fill_state<BATCH>(g, s, p, st, overflow);
+                fill_state<BATCH, WIDE>(g, s, p, st, wst, overflow);
                 if (p.last_hit == -1) break;
                 int command = propagate_to_boundary(g, p, s, rng, a.use_weights, scatter_first);
                 scatter_first = 0;
@@ -1029,18 +1152,27 @@ __global__ __launch_bounds__(BLOCK) void duplicate_kernel(PhotonPtrs ph, int32_t
 }
 
 // mesh.h:131-159
+template <bool WIDE>
 __global__ __launch_bounds__(BLOCK) void distance_kernel(DevGeom g, uint32_t n, const float *origin, const float *dir,
                                                           float *distance, uint32_t *counters) {
-    __shared__ uint32_t lds_stack[STACK_LDS * BLOCK];
+    __shared__ uint32_t lds_stack[WIDE ? 2 * WIDE_LDS * BLOCK : STACK_LDS * BLOCK];
     const uint32_t id = blockIdx.x * BLOCK + threadIdx.x;
     if (id >= n) return;
     V3 o = load3(origin, id), d = load3(dir, id);
     d = d / norm(d);
-    Stack st;
-    st.lds = lds_stack + threadIdx.x;
     uint32_t overflow = 0;
     float dist;
-    const int tri = intersect_mesh<4>(g, o, d, dist, -1, st, overflow);
+    int tri;
+    if constexpr (WIDE) {
+        WStack st;
+        st.node = lds_stack + threadIdx.x;
+        st.dist = reinterpret_cast<float *>(lds_stack) + WIDE_LDS * BLOCK + threadIdx.x;
+        tri = intersect_wide(g, o, d, dist, -1, st, overflow);
+    } else {
+        Stack st;
+        st.lds = lds_stack + threadIdx.x;
+        tri = intersect_mesh<4>(g, o, d, dist, -1, st, overflow);
+    }
     if (tri != -1) distance[id] = dist;
     if (overflow && counters) atomicAdd(counters, overflow);
 }
@@ -1143,17 +1275,18 @@ typedef void (*propagate_fn)(PropagateArgs);
 // measured on demo.detector(), 4M photons (profiles/r01/ab_variants.log):
 // <1,3> 89.2 ms, <4,3> 74.9, <4,4> 66.8, <4,5> 66.5, <8,4> 64.3, <8,3> 74.1, <2,3> 76.5
 static const propagate_fn kVariants[] = {
-    propagate_kernel<8, 4>,   // 0: default
-    propagate_kernel<1, 3>,   // 1: reference-shaped one-node-at-a-time walk
-    propagate_kernel<4, 4>,   // 2
-    propagate_kernel<8, 5>,   // 3
-    propagate_kernel<8, 6>,   // 4
-    propagate_kernel<16, 4>,  // 5
+    propagate_kernel<8, 4, true>,    // 0: default -- 8-wide SAH BVH, rank tie-break
+    propagate_kernel<8, 4, false>,   // 1: exact-order walk of the reference BVH, 8 children in flight
+    propagate_kernel<8, 3, true>,    // 2
+    propagate_kernel<8, 5, true>,    // 3
+    propagate_kernel<1, 3, false>,   // 4: reference-shaped one-node-at-a-time walk
 };
-static propagate_fn select_variant() {
+static constexpr int kExactVariant = 1;
+static propagate_fn select_variant(const chr_geometry *g) {
     const char *e = getenv("CHR_PROPAGATE_VARIANT");   // read per launch: A/B in one process
     int v = e ? atoi(e) : 0;
     if (v < 0 || v >= (int)(sizeof(kVariants) / sizeof(kVariants[0]))) v = 0;
+    if (g->dev.nwnodes == 0 && (v == 0 || v == 2 || v == 3)) v = kExactVariant;   // no wide BVH for this geometry
     return kVariants[v];
 }
 
@@ -1174,7 +1307,7 @@ static int launch_chunk(const chr_geometry *g, const chr_photons *ph, uint32_t *
     a.max_steps = max_steps; a.use_weights = use_weights; a.scatter_first = scatter_first;
     a.alive_masks = masks; a.counters = counters;
     if (ev0) CHR_HIP_CHECK(hipEventRecord(ev0, stream));
-    hipLaunchKernelGGL(select_variant(), dim3(grid_for(nthreads)), dim3(BLOCK), 0, stream, a);
+    hipLaunchKernelGGL(select_variant(g), dim3(grid_for(nthreads)), dim3(BLOCK), 0, stream, a);
     if (ev1) CHR_HIP_CHECK(hipEventRecord(ev1, stream));
     hipLaunchKernelGGL(scan_masks_kernel, dim3(1), dim3(1024), 0, stream, masks, nwords, offsets, out_queue,
                        counters + 1, (uint32_t *)nullptr);
@@ -1374,8 +1507,10 @@ extern "C" int chr_distance_to_mesh(const chr_geometry *g, uint32_t n, const flo
                                     float *d_distance, void *stream) {
     if (!g || !d_origin || !d_direction || !d_distance) return chr::fail(CHR_ERR_INVALID, "distance_to_mesh: null argument");
     if (n == 0) return CHR_OK;
-    hipLaunchKernelGGL(distance_kernel, dim3(grid_for(n)), dim3(BLOCK), 0, (hipStream_t)stream, g->dev, n, d_origin,
-                       d_direction, d_distance, (uint32_t *)nullptr);
+    const char *e = getenv("CHR_PROPAGATE_VARIANT");
+    const bool wide = g->dev.nwnodes != 0 && !(e && (atoi(e) == 1 || atoi(e) == 4));
+    hipLaunchKernelGGL(wide ? distance_kernel<true> : distance_kernel<false>, dim3(grid_for(n)), dim3(BLOCK), 0,
+                       (hipStream_t)stream, g->dev, n, d_origin, d_direction, d_distance, (uint32_t *)nullptr);
     CHR_HIP_CHECK(hipGetLastError());
     return CHR_OK;
 }

@@ -1,0 +1,414 @@
+// wide_bvh.cpp -- the gfx950 traversal layout: an 8-wide, SAH-built BVH with
+// 8-bit parent-relative child boxes (96-byte nodes), built on the host from
+// the reference BVH's own leaf boxes.
+//
+// Why it exists.  The reference BVH (chroma/bvh/grid.py: Morton-grid groups of
+// up to 15 children, one triangle per leaf) makes every ray test ~140-180
+// 16-byte nodes in ~30 dependent groups.  A surface-area-heuristic 8-wide tree
+// over the SAME leaf boxes tests far fewer nodes, each one 96-byte record.
+//
+// Why results do not change.  The nearest hit the reference reports is
+//   argmin over triangles it TESTS of (distance, position in its DFS order)
+// (strict '<', mesh.h:95).  Here:
+//   * every triangle's box is the reference leaf box decoded exactly as the
+//     reference decodes it (world_origin + q * world_scale, fmaf), and every
+//     wide child box contains its triangles' boxes after the kernel's own float
+//     decode (checked below), so a ray that passes the reference's slab test on a
+//     leaf passes all of ours (the slab test is monotone in the box bounds);
+//   * pruning uses the same strict '>' against a running best that is never
+//     below the final answer, so the triangles we test include the ones the
+//     reference tests;
+//   * ties are broken by the reference DFS rank of each triangle (computed
+//     here from the reference node array: leaves of a group in index order,
+//     then the group's inner children's subtrees in reverse index order).
+// Only triangles reachable in the reference BVH are included.
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "../../include/chroma_amd.h"
+#include "common.h"
+#include "wide_bvh.h"
+
+namespace chr {
+namespace {
+
+constexpr int LEAF_MAX = 4;
+constexpr int NBINS = 32;
+
+struct Box {
+    float lo[3], hi[3];
+    void empty() { for (int a = 0; a < 3; ++a) { lo[a] = INFINITY; hi[a] = -INFINITY; } }
+    void grow(const Box &b) {
+        for (int a = 0; a < 3; ++a) { lo[a] = std::min(lo[a], b.lo[a]); hi[a] = std::max(hi[a], b.hi[a]); }
+    }
+    void grow(const float *p) {
+        for (int a = 0; a < 3; ++a) { lo[a] = std::min(lo[a], p[a]); hi[a] = std::max(hi[a], p[a]); }
+    }
+    double area() const {
+        double d[3];
+        for (int a = 0; a < 3; ++a) d[a] = std::max(0.0, (double)hi[a] - (double)lo[a]);
+        return 2.0 * (d[0] * d[1] + d[1] * d[2] + d[2] * d[0]);
+    }
+};
+
+struct Cluster {
+    uint32_t begin, end;
+    Box box;
+    uint32_t count() const { return end - begin; }
+};
+
+struct Builder {
+    const std::vector<Box> &tri_box;
+    const std::vector<float> &centroid;   // 3 per triangle
+    std::vector<uint32_t> &idx;
+
+    Box range_box(uint32_t b, uint32_t e, bool par) const {
+        Box r;
+        r.empty();
+        if (!par) {
+            for (uint32_t i = b; i < e; ++i) r.grow(tri_box[idx[i]]);
+            return r;
+        }
+#pragma omp parallel
+        {
+            Box l;
+            l.empty();
+#pragma omp for schedule(static) nowait
+            for (int64_t i = b; i < (int64_t)e; ++i) l.grow(tri_box[idx[i]]);
+#pragma omp critical
+            r.grow(l);
+        }
+        return r;
+    }
+
+    // binned SAH split of [b,e); returns split point (b < m < e)
+    uint32_t split(uint32_t b, uint32_t e, bool par) {
+        Box cb;
+        cb.empty();
+        for (uint32_t i = b; i < e; ++i) cb.grow(&centroid[3 * (size_t)idx[i]]);   // cheap relative to binning
+        int best_axis = -1, best_bin = -1;
+        double best_cost = INFINITY;
+        for (int a = 0; a < 3; ++a) {
+            const double ext = (double)cb.hi[a] - (double)cb.lo[a];
+            if (!(ext > 0.0)) continue;
+            const double k = NBINS / ext * (1.0 - 1e-9);
+            Box bins[NBINS];
+            uint32_t cnt[NBINS];
+            for (int j = 0; j < NBINS; ++j) { bins[j].empty(); cnt[j] = 0; }
+            const float lo = cb.lo[a];
+            auto bin_of = [&](uint32_t t) {
+                int j = (int)(((double)centroid[3 * (size_t)t + a] - lo) * k);
+                return std::min(NBINS - 1, std::max(0, j));
+            };
+            if (par) {
+#pragma omp parallel
+                {
+                    Box lb[NBINS];
+                    uint32_t lc[NBINS];
+                    for (int j = 0; j < NBINS; ++j) { lb[j].empty(); lc[j] = 0; }
+#pragma omp for schedule(static) nowait
+                    for (int64_t i = b; i < (int64_t)e; ++i) {
+                        const uint32_t t = idx[i];
+                        const int j = bin_of(t);
+                        lb[j].grow(tri_box[t]);
+                        lc[j]++;
+                    }
+#pragma omp critical
+                    for (int j = 0; j < NBINS; ++j) { bins[j].grow(lb[j]); cnt[j] += lc[j]; }
+                }
+            } else {
+                for (uint32_t i = b; i < e; ++i) {
+                    const uint32_t t = idx[i];
+                    const int j = bin_of(t);
+                    bins[j].grow(tri_box[t]);
+                    cnt[j]++;
+                }
+            }
+            double right_area[NBINS];
+            uint32_t right_cnt[NBINS];
+            Box acc;
+            acc.empty();
+            uint32_t c = 0;
+            for (int j = NBINS - 1; j > 0; --j) {
+                acc.grow(bins[j]);
+                c += cnt[j];
+                right_area[j] = acc.area();
+                right_cnt[j] = c;
+            }
+            acc.empty();
+            c = 0;
+            for (int j = 0; j < NBINS - 1; ++j) {
+                acc.grow(bins[j]);
+                c += cnt[j];
+                if (c == 0 || right_cnt[j + 1] == 0) continue;
+                const double cost = acc.area() * c + right_area[j + 1] * right_cnt[j + 1];
+                if (cost < best_cost) { best_cost = cost; best_axis = a; best_bin = j + 1; }
+            }
+        }
+        if (best_axis < 0) return b + (e - b) / 2;   // all centroids coincide: split by count
+        const int a = best_axis;
+        const double k = NBINS / ((double)cb.hi[a] - (double)cb.lo[a]) * (1.0 - 1e-9);
+        const float lo = cb.lo[a];
+        auto mid = std::partition(idx.begin() + b, idx.begin() + e, [&](uint32_t t) {
+            int j = (int)(((double)centroid[3 * (size_t)t + a] - lo) * k);
+            return std::min(NBINS - 1, std::max(0, j)) < best_bin;
+        });
+        uint32_t m = (uint32_t)(mid - idx.begin());
+        if (m == b || m == e) m = b + (e - b) / 2;
+        return m;
+    }
+
+    // cut [b,e) into <= 8 clusters: repeatedly split the largest-area cluster
+    // that holds more than LEAF_MAX triangles
+    int clusters(uint32_t b, uint32_t e, bool par, Cluster out[8]) {
+        int n = 1;
+        out[0] = Cluster{b, e, range_box(b, e, par)};
+        while (n < 8) {
+            int pick = -1;
+            double best = -1.0;
+            for (int i = 0; i < n; ++i)
+                if (out[i].count() > LEAF_MAX && out[i].box.area() > best) { best = out[i].box.area(); pick = i; }
+            if (pick < 0) break;
+            const Cluster c = out[pick];
+            const bool p = par && c.count() > (1u << 18);
+            const uint32_t m = split(c.begin, c.end, p);
+            out[pick] = Cluster{c.begin, m, range_box(c.begin, m, p)};
+            out[n++] = Cluster{m, c.end, range_box(m, c.end, p)};
+        }
+        return n;
+    }
+};
+
+inline float pow2f(int e) {     // 2^e as float, e in [-126, 127]
+    uint32_t u = (uint32_t)(e + 127) << 23;
+    float f;
+    std::memcpy(&f, &u, 4);
+    return f;
+}
+
+// quantise one axis of up to 8 child boxes against origin o; returns exponent
+// (biased) so that every decoded box contains its child
+int quantize_axis(float o, float node_hi, const float *clo, const float *chi, int n, uint8_t *qlo, uint8_t *qhi) {
+    const double ext = (double)node_hi - (double)o;
+    int e = ext > 0 ? (int)std::ceil(std::log2(ext / 255.0)) : -126;
+    e = std::max(-126, std::min(127, e));
+    for (;; ++e) {
+        const float s = pow2f(e);
+        bool ok = true;
+        for (int k = 0; k < n && ok; ++k) {
+            double fl = std::floor(((double)clo[k] - o) / s), fh = std::ceil(((double)chi[k] - o) / s);
+            int l = (int)std::max(0.0, std::min(255.0, fl));
+            int h = (int)std::max(0.0, std::min(255.0, fh));
+            while (l > 0 && std::fmaf((float)l, s, o) > clo[k]) --l;
+            while (h < 255 && std::fmaf((float)h, s, o) < chi[k]) ++h;
+            if (std::fmaf((float)l, s, o) > clo[k] || std::fmaf((float)h, s, o) < chi[k]) ok = false;
+            qlo[k] = (uint8_t)l;
+            qhi[k] = (uint8_t)h;
+        }
+        if (ok) return e + 127;
+        if (e >= 127) return -1;
+    }
+}
+
+}  // namespace
+
+int build_wide_bvh(const chr_geometry_desc *d, WideBVH &out) {
+    const uint32_t ntri = d->ntriangles;
+    const float wo[3] = {d->world_origin[0], d->world_origin[1], d->world_origin[2]};
+    const float ws = d->world_scale;
+    // 1. reference DFS: rank + leaf box per reachable triangle (mesh.h:75-117 order)
+    std::vector<uint32_t> rank(ntri, 0xFFFFFFFFu);
+    std::vector<Box> tri_box(ntri);
+    std::vector<uint32_t> leafq((size_t)ntri * 3);
+    out.usable = true;
+    {
+        auto decode = [&](const uint32_t *n, Box &b) {
+            for (int a = 0; a < 3; ++a) {
+                b.lo[a] = std::fmaf((float)(n[a] & 0xFFFFu), ws, wo[a]);
+                b.hi[a] = std::fmaf((float)(n[a] >> 16), ws, wo[a]);
+            }
+        };
+        const uint32_t *N = d->h_nodes;
+        uint32_t next_rank = 0;
+        std::vector<uint32_t> stack;
+        const uint32_t root_w = N[3];
+        if ((root_w >> 28) == 0) {   // a one-triangle mesh: the root is the leaf
+            const uint32_t t = root_w & 0x0FFFFFFFu;
+            rank[t] = next_rank++;
+            decode(N, tri_box[t]);
+            std::memcpy(&leafq[3 * (size_t)t], N, 12);
+        } else {
+            stack.push_back(root_w);
+        }
+        while (!stack.empty()) {
+            const uint32_t w = stack.back();
+            stack.pop_back();
+            const uint32_t first = w & 0x0FFFFFFFu, end = first + (w >> 28);
+            for (uint32_t i = first; i < end; ++i) {
+                const uint32_t *n = N + 4 * (size_t)i;
+                if ((n[3] >> 28) == 0) {
+                    const uint32_t t = n[3] & 0x0FFFFFFFu;
+                    if (rank[t] == 0xFFFFFFFFu) {   // first visit defines the tie rank
+                        rank[t] = next_rank++;
+                        decode(n, tri_box[t]);
+                        std::memcpy(&leafq[3 * (size_t)t], n, 12);
+                    } else if (std::memcmp(&leafq[3 * (size_t)t], n, 12) != 0) {
+                        // a triangle under two different leaf boxes (no builder we
+                        // know of makes this): keep the exact-order traversal
+                        out.usable = false;
+                    }
+                } else {
+                    stack.push_back(n[3]);
+                }
+            }
+        }
+    }
+    std::vector<uint32_t> idx;
+    idx.reserve(ntri);
+    for (uint32_t t = 0; t < ntri; ++t)
+        if (rank[t] != 0xFFFFFFFFu) idx.push_back(t);
+    const uint32_t nreach = (uint32_t)idx.size();
+    std::vector<float> centroid((size_t)ntri * 3);
+#pragma omp parallel for schedule(static)
+    for (int64_t t = 0; t < (int64_t)ntri; ++t)
+        for (int a = 0; a < 3; ++a) centroid[3 * t + a] = 0.5f * (tri_box[t].lo[a] + tri_box[t].hi[a]);
+
+    Builder B{tri_box, centroid, idx};
+    out.nodes.clear();
+    out.tri.clear();
+    out.nodes.resize(1);
+    out.tri.resize((size_t)nreach * 3);
+    if (nreach == 0) {
+        std::memset(&out.nodes[0], 0, sizeof(WideNode));
+        return CHR_OK;
+    }
+    struct Task { uint32_t begin, end, node; };
+    std::vector<Task> level{Task{0, nreach, 0}};
+    uint32_t tri_next = 0;
+    while (!level.empty()) {
+        const size_t nt = level.size();
+        std::vector<Cluster> cl(nt * 8);
+        std::vector<int> ncl(nt);
+        if (nt < 16) {
+            for (size_t i = 0; i < nt; ++i) ncl[i] = B.clusters(level[i].begin, level[i].end, true, &cl[8 * i]);
+        } else {
+#pragma omp parallel for schedule(dynamic, 1)
+            for (int64_t i = 0; i < (int64_t)nt; ++i) ncl[i] = B.clusters(level[i].begin, level[i].end, false, &cl[8 * i]);
+        }
+        // deterministic allocation of child nodes / triangle slots
+        std::vector<uint32_t> child_base(nt), tri_base(nt);
+        std::vector<Task> next;
+        for (size_t i = 0; i < nt; ++i) {
+            child_base[i] = (uint32_t)out.nodes.size();
+            tri_base[i] = tri_next;
+            uint32_t ninner = 0;
+            for (int k = 0; k < ncl[i]; ++k) {
+                const Cluster &c = cl[8 * i + k];
+                if (c.count() > (uint32_t)LEAF_MAX) {
+                    next.push_back(Task{c.begin, c.end, child_base[i] + ninner});
+                    ninner++;
+                } else {
+                    tri_next += c.count();
+                }
+            }
+            out.nodes.resize(out.nodes.size() + ninner);
+        }
+        int bad = 0;
+#pragma omp parallel for schedule(static) reduction(+:bad)
+        for (int64_t i = 0; i < (int64_t)nt; ++i) {
+            WideNode &W = out.nodes[level[i].node];
+            std::memset(&W, 0, sizeof(W));
+            const int n = ncl[i];
+            Box nb;
+            nb.empty();
+            for (int k = 0; k < n; ++k) nb.grow(cl[8 * i + k].box);
+            W.origin[0] = nb.lo[0]; W.origin[1] = nb.lo[1]; W.origin[2] = nb.lo[2];
+            W.nchild = (uint8_t)n;
+            for (int a = 0; a < 3; ++a) {
+                float clo[8], chi[8];
+                for (int k = 0; k < n; ++k) { clo[k] = cl[8 * i + k].box.lo[a]; chi[k] = cl[8 * i + k].box.hi[a]; }
+                const int e = quantize_axis(nb.lo[a], nb.hi[a], clo, chi, n, W.qlo[a], W.qhi[a]);
+                if (e < 0) { bad++; continue; }
+                W.exp[a] = (uint8_t)e;
+            }
+            W.child_base = child_base[i];
+            W.tri_base = tri_base[i];
+            uint32_t ninner = 0, toff = 0;
+            for (int k = 0; k < n; ++k) {
+                const Cluster &c = cl[8 * i + k];
+                if (c.count() > (uint32_t)LEAF_MAX) {
+                    W.kind[k] = WIDE_INNER;
+                    W.off[k] = (uint8_t)ninner++;
+                } else {
+                    W.kind[k] = (uint8_t)c.count();
+                    W.off[k] = (uint8_t)toff;
+                    for (uint32_t j = c.begin; j < c.end; ++j) {
+                        const uint32_t t = idx[j];
+                        const size_t slot = (size_t)W.tri_base + toff++;
+                        const uint32_t *ix = d->h_triangles + 3 * (size_t)t;
+                        const float *v0 = d->h_vertices + 3 * (size_t)ix[0];
+                        const float *v1 = d->h_vertices + 3 * (size_t)ix[1];
+                        const float *v2 = d->h_vertices + 3 * (size_t)ix[2];
+                        WideTri &R = out.tri[slot];
+                        R.v0[0] = v0[0]; R.v0[1] = v0[1]; R.v0[2] = v0[2];
+                        for (int a = 0; a < 3; ++a) { R.e1[a] = v1[a] - v0[a]; R.e2[a] = v2[a] - v0[a]; }
+                        R.id = t;
+                        R.rank = rank[t];
+                        std::memcpy(R.leaf, &leafq[3 * (size_t)t], 12);
+                        R.pad[0] = R.pad[1] = 0;
+                    }
+                }
+            }
+        }
+        if (bad) return chr::fail(CHR_ERR_INVALID, "wide BVH: a node could not be quantised");
+        level.swap(next);
+        if (!level.empty()) out.max_depth++;
+    }
+    out.tri.resize(tri_next);
+    if (7 * (out.max_depth + 1) + 1 > (uint32_t)WIDE_STACK) out.usable = false;
+    return CHR_OK;
+}
+
+}  // namespace chr
+
+struct chr_wide_result {
+    chr::WideBVH b;
+};
+
+extern "C" int chr_wide_bvh_build(const chr_geometry_desc *d, chr_wide_result **out) {
+    if (!d || !out || !d->h_nodes || !d->h_vertices || !d->h_triangles || d->nnodes == 0)
+        return chr::fail(CHR_ERR_INVALID, "chr_wide_bvh_build: null argument or empty BVH");
+    chr_wide_result *r = new (std::nothrow) chr_wide_result();
+    if (!r) return chr::fail(CHR_ERR_NOMEM, "chr_wide_bvh_build: host allocation failed");
+    const int rc = chr::build_wide_bvh(d, r->b);
+    if (rc) { delete r; return rc; }
+    *out = r;
+    return CHR_OK;
+}
+
+extern "C" int chr_wide_bvh_info(const chr_wide_result *r, uint32_t *nnodes, uint32_t *ntri, uint32_t *max_depth,
+                                 int32_t *usable) {
+    if (!r) return chr::fail(CHR_ERR_INVALID, "chr_wide_bvh_info: null handle");
+    if (nnodes) *nnodes = (uint32_t)r->b.nodes.size();
+    if (ntri) *ntri = (uint32_t)r->b.tri.size();
+    if (max_depth) *max_depth = r->b.max_depth;
+    if (usable) *usable = r->b.usable ? 1 : 0;
+    return CHR_OK;
+}
+
+extern "C" int chr_wide_bvh_copy(const chr_wide_result *r, void *h_nodes, void *h_tri) {
+    if (!r) return chr::fail(CHR_ERR_INVALID, "chr_wide_bvh_copy: null handle");
+    if (h_nodes) std::memcpy(h_nodes, r->b.nodes.data(), r->b.nodes.size() * sizeof(chr::WideNode));
+    if (h_tri) std::memcpy(h_tri, r->b.tri.data(), r->b.tri.size() * sizeof(chr::WideTri));
+    return CHR_OK;
+}
+
+extern "C" int chr_wide_bvh_free(chr_wide_result *r) {
+    delete r;
+    return CHR_OK;
+}

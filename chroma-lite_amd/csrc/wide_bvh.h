@@ -1,0 +1,65 @@
+// wide_bvh.h -- 8-wide quantised BVH used by the gfx950 traversal (see wide_bvh.cpp).
+//
+// WideNode, 96 bytes = six 16-byte loads:
+//   [ 0,16)  origin xyz (f32), biased power-of-two exponent per axis, nchild
+//   [16,64)  per-child 8-bit boxes: qlo[x][8] qlo[y][8] qlo[z][8] qhi[x][8] qhi[y][8] qhi[z][8]
+//            decoded as fmaf(q, 2^(exp-127), origin) -- always contains the child
+//   [64,72)  child_base (first inner child node), tri_base (first triangle record)
+//   [72,88)  kind[8]: 0 empty, 1..4 leaf with that many triangles, WIDE_INNER;
+//            off[8]:  inner -> node child_base+off, leaf -> records tri_base+off..
+// WideTri, 64 bytes = four 16-byte loads (half a 128-byte line): v0, e1 = v1-v0,
+// e2 = v2-v0 (float32, the Moller-Trumbore operands of intersect.h:26-101), the
+// original triangle id, its rank in the reference BVH's DFS order (the
+// nearest-hit tie-break) and the x/y/z words of its reference leaf node, so the
+// kernel applies the reference's own leaf slab test + prune before Moller-Trumbore.
+#pragma once
+
+#include <cstdint>
+#include <vector>
+
+struct chr_geometry_desc;
+
+namespace chr {
+
+constexpr uint8_t WIDE_INNER = 0x80;
+
+struct alignas(16) WideNode {
+    float origin[3];
+    uint8_t exp[3];
+    uint8_t nchild;
+    uint8_t qlo[3][8];
+    uint8_t qhi[3][8];
+    uint32_t child_base;
+    uint32_t tri_base;
+    uint8_t kind[8];
+    uint8_t off[8];
+    uint32_t pad[2];
+};
+static_assert(sizeof(WideNode) == 96, "WideNode must be 96 bytes");
+
+struct alignas(16) WideTri {
+    float v0[3];
+    float e1[3];
+    float e2[3];
+    uint32_t id;
+    uint32_t rank;
+    uint32_t leaf[3];      // reference leaf node words x, y, z (lo | hi << 16)
+    uint32_t pad[2];
+};
+static_assert(sizeof(WideTri) == 64, "WideTri must be 64 bytes");
+
+struct WideBVH {
+    std::vector<WideNode> nodes;   // node 0 is the root
+    std::vector<WideTri> tri;      // leaf order
+    uint32_t max_depth = 0;        // levels below the root
+    bool usable = true;            // false: the exact-order traversal must be used
+};
+
+// stack capacity of the wide traversal (entries); the builder marks a tree
+// whose worst-case stack (7 pushes per level) would not fit as unusable
+constexpr int WIDE_STACK = 128;
+
+// Build from the descriptor's mesh and reference BVH (h_nodes).  Returns a chr_status.
+int build_wide_bvh(const chr_geometry_desc *d, WideBVH &out);
+
+}  // namespace chr

@@ -213,6 +213,21 @@ int chr_bvh_result_copy(const chr_bvh_result *r, uint32_t *h_nodes /*[nnodes*4]*
                         uint32_t *h_layer_offsets /*[nlayers]*/);
 int chr_bvh_result_free(chr_bvh_result *r);
 
+/* ------------------------------------------------------------- traversal BVH
+ * The layout the gfx950 walk uses (csrc/wide_bvh.h): an 8-wide SAH tree over
+ * the reference BVH's own leaf boxes, each triangle carrying its reference DFS
+ * rank.  chr_geometry_create builds it internally; these entries expose the
+ * same host build for inspection and tests (no reference counterpart: it is
+ * a derived acceleration structure, not part of the reference's data).
+ * Nodes are 96 bytes, triangle records 64 bytes (see wide_bvh.h). */
+typedef struct chr_wide_result chr_wide_result;
+int chr_wide_bvh_build(const chr_geometry_desc *desc, chr_wide_result **out);
+int chr_wide_bvh_info(const chr_wide_result *r, uint32_t *nnodes, uint32_t *ntri,
+                      uint32_t *max_depth, int32_t *usable);
+int chr_wide_bvh_copy(const chr_wide_result *r, void *h_nodes /*[nnodes*96 B]*/,
+                      void *h_tri /*[ntri*64 B]*/);
+int chr_wide_bvh_free(chr_wide_result *r);
+
 /* ------------------------------------------------------------- misc */
 const char *chr_last_error(void);
 int chr_version(void);

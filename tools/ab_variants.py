@@ -1,7 +1,7 @@
 #!/usr/bin/env python
 """A/B the propagate-kernel variants (CHR_PROPAGATE_VARIANT) in ONE process,
 interleaved rounds (cdna_hip_programming.md 5.4 rule 24).  Checks that every
-variant gives identical photon histories.  Dev tool, not part of the product."""
+variant gives identical photon histories, last-hit triangles and positions.  Dev tool, not part of the product."""
 import argparse
 import os
 import sys
@@ -50,11 +50,14 @@ def main():
             gp.propagate(gdet, rng, nthreads_per_block=512, max_blocks=1024, max_steps=args.max_steps)
             torch.cuda.synchronize()
             dt = time.perf_counter() - t0
-            fl = gp.flags.get()
+            fl = (gp.flags.get(), gp.last_hit_triangles.get(), gp.pos.get().view(np.uint32).reshape(len(fl0 := gp.flags.get()), -1))
             if ref_flags is None:
                 ref_flags = fl
-            elif not np.array_equal(fl, ref_flags):
-                print('VARIANT %d DIFFERS' % v, flush=True)
+            else:
+                bad = (fl[0] != ref_flags[0]) | (fl[1] != ref_flags[1]) | (fl[2] != ref_flags[2]).any(axis=1)
+                if bad.any():
+                    print('VARIANT %d DIFFERS from variant %d on %d photons (first %s)' % (
+                        v, variants[0], int(bad.sum()), np.flatnonzero(bad)[:8]), flush=True)
             if r > 0:
                 times[v].append(dt)
                 kms[v].append(gp.last_stats.kernel_ms)
