@@ -17,9 +17,13 @@ ranks is reported.
 Roofline: the propagate kernel is bound by HBM/L2 latency-bandwidth on the
 BVH + triangle gathers.  achieved = algorithmic bytes per step / summed
 propagate-kernel time (HIP events around every launch, on its stream), with
-algorithmic bytes per photon B_alg = 120 + sum over traversals of
-(16 * nodes tested + 48 * triangles tested + 4), counted by the CPU oracle on
-the cpu_baseline sample of the same workload.
+algorithmic bytes per photon
+    B_alg = 120 + (96 * wide nodes visited + 64 * triangle records tested
+                   + 52 * traversals) / photons
+(photon record in+out; 96-byte BVH nodes; 64-byte triangle records; the hit
+triangle's 48-byte normal record + 4-byte material code per traversal),
+counted on ALL photons of the step by one extra, untimed propagate with the
+counting kernel variant (CHR_PROPAGATE_VARIANT=5: same walk + counters).
 """
 import argparse
 import json
@@ -208,6 +212,15 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     detected = int(((gp.flags.get() & 4) != 0).sum())
+    # untimed: same propagate with the counting kernel variant -> algorithmic bytes
+    prev = os.environ.get('CHR_PROPAGATE_VARIANT')
+    os.environ['CHR_PROPAGATE_VARIANT'] = '5'
+    cst = step().last_stats
+    if prev is None:
+        del os.environ['CHR_PROPAGATE_VARIANT']
+    else:
+        os.environ['CHR_PROPAGATE_VARIANT'] = prev
+    torch.cuda.synchronize()
 
     if rank == 0:
         total = args.photons * world * args.steps
@@ -229,21 +242,26 @@ def main():
                        'detected_fraction': detected / args.photons},
             'roofline': None, 'cpu_baseline': None,
         }
+        n = float(args.photons)
+        b_alg = 120.0 + (96.0 * cst.nodes_visited + 64.0 * cst.triangles_tested + 52.0 * cst.traversals) / n
+        per_step_s = kernel_ms / args.steps / 1e3
+        achieved = n * b_alg / per_step_s / 1e9
+        result['roofline'] = {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                              'frac': achieved / HBM_PEAK_GBS, 'traffic': None,
+                              'bytes_per_photon_alg': b_alg,
+                              'nodes_per_photon': cst.nodes_visited / n,
+                              'triangles_per_photon': cst.triangles_tested / n,
+                              'traversals_per_photon': cst.traversals / n,
+                              'kernel': 'chr::propagate_kernel<8,4,true>',
+                              'avg_launch_ms': kernel_ms / max(1, launches)}
         if not args.no_cpu_baseline and world == 1:
             threads = min(16, len(os.sched_getaffinity(0)))
-            cpu, b_alg, ostats, nsample = cpu_baseline(PackedGeometry(det), photons, nslots, args.nthreads_per_block,
-                                                       args.max_blocks, args.max_steps, args.seed, args.cpu_budget,
-                                                       threads)
+            cpu, _, ostats, nsample = cpu_baseline(PackedGeometry(det), photons, nslots, args.nthreads_per_block,
+                                                   args.max_blocks, args.max_steps, args.seed, args.cpu_budget,
+                                                   threads)
             result['cpu_baseline'] = cpu
-            per_step_s = kernel_ms / args.steps / 1e3
-            achieved = args.photons * b_alg / per_step_s / 1e9
-            result['roofline'] = {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
-                                  'frac': achieved / HBM_PEAK_GBS, 'traffic': None,
-                                  'bytes_per_photon_alg': b_alg,
-                                  'nodes_per_photon': ostats['nodes_visited'] / nsample,
-                                  'triangles_per_photon': ostats['tris_tested'] / nsample,
-                                  'traversals_per_photon': ostats['traversals'] / nsample,
-                                  'kernel': 'chr::propagate_kernel'}
+            result['detail']['reference_bvh_nodes_per_photon'] = ostats['nodes_visited'] / nsample
+            result['detail']['reference_bvh_triangles_per_photon'] = ostats['tris_tested'] / nsample
         print(json.dumps(result), flush=True)
     if dist:
         dist.destroy_process_group()

@@ -21,6 +21,7 @@
 #include <algorithm>
 #include <cstdint>
 #include <cstdlib>
+#include <cstring>
 #include <vector>
 
 #include "../../include/chroma_amd.h"
@@ -268,8 +269,14 @@ __device__ __forceinline__ float byte_f(uint32_t lo4, uint32_t hi4, int k) {   /
 }
 __device__ __forceinline__ float exp_scale(uint32_t e) { return __uint_as_float((e & 0xFFu) << 23); }
 
+struct WalkCounts {   // filled only by the counting variant (bench: algorithmic bytes per photon)
+    uint32_t nodes, tris, walks;
+};
+
+template <bool COUNT>
 __device__ int intersect_wide(const DevGeom &g, V3 o, V3 d, float &min_distance, int last_hit, WStack &st,
-                              uint32_t &overflow) {
+                              uint32_t &overflow, WalkCounts &cnt) {
+    if constexpr (COUNT) cnt.walks++;
     const V3 noid = v3(-o.x / d.x, -o.y / d.y, -o.z / d.z);
     const V3 inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
     float best = __builtin_inff();
@@ -279,6 +286,7 @@ __device__ int intersect_wide(const DevGeom &g, V3 o, V3 d, float &min_distance,
     int sp = 0;
     uint32_t node = 0;
     while (true) {
+        if constexpr (COUNT) cnt.nodes++;
         const uint4 *np = g.wnodes + 6 * (size_t)node;
         const uint4 h = np[0], a1 = np[1], a2 = np[2], a3 = np[3], a4 = np[4], a5 = np[5];
         const V3 org = v3(__uint_as_float(h.x), __uint_as_float(h.y), __uint_as_float(h.z));
@@ -312,9 +320,10 @@ __device__ int intersect_wide(const DevGeom &g, V3 o, V3 d, float &min_distance,
         while (leaf_mask) {
             const int k = __builtin_ctz(leaf_mask);
             leaf_mask &= leaf_mask - 1;
-            const uint32_t cnt = (uint32_t)(kinds >> (8 * k)) & 0xFFu;
+            const uint32_t ntri = (uint32_t)(kinds >> (8 * k)) & 0xFFu;
             const uint32_t first = a4.y + ((uint32_t)(offs >> (8 * k)) & 0xFFu);
-            for (uint32_t j = 0; j < cnt; ++j) {
+            for (uint32_t j = 0; j < ntri; ++j) {
+                if constexpr (COUNT) cnt.tris++;
                 const float4 *r = g.wtri + 4 * (size_t)(first + j);
                 const float4 r0 = r[0], r1 = r[1], r2 = r[2], r3 = r[3];
                 const uint32_t id = __float_as_uint(r2.y);
@@ -460,11 +469,12 @@ __device__ __noinline__ void wireplanes(const DevGeom &g, const Photon &p, float
 }
 
 // photon.h:87-397
-template <int BATCH, bool WIDE>
+template <int BATCH, bool WIDE, bool COUNT>
 __device__ __forceinline__ void fill_state(const DevGeom &g, State &s, Photon &p, Stack &st, WStack &wst,
-                                           uint32_t &overflow) {
+                                           uint32_t &overflow, WalkCounts &cnt) {
     int mesh_triangle;
-    if constexpr (WIDE) mesh_triangle = intersect_wide(g, p.pos, p.dir, s.distance, p.last_hit, wst, overflow);
+    if constexpr (WIDE)
+        mesh_triangle = intersect_wide<COUNT>(g, p.pos, p.dir, s.distance, p.last_hit, wst, overflow, cnt);
     else mesh_triangle = intersect_mesh<BATCH>(g, p.pos, p.dir, s.distance, p.last_hit, st, overflow);
     int m1, m2;
     bool use_analytic = false;
@@ -951,7 +961,7 @@ __device__ __forceinline__ void store3(float *p, uint32_t i, V3 v) { p[3 * i] = 
 
 // propagate.cu:254-366.  BATCH: children fetched together per group;
 // MINW: minimum waves per SIMD requested from the register allocator.
-template <int BATCH, int MINW, bool WIDE>
+template <int BATCH, int MINW, bool WIDE, bool COUNT = false>
 __global__ __launch_bounds__(BLOCK, MINW) void propagate_kernel(PropagateArgs a) {
     __shared__ uint32_t lds_stack[WIDE ? 2 * WIDE_LDS * BLOCK : STACK_LDS * BLOCK];
     const int id = blockIdx.x * BLOCK + threadIdx.x;
@@ -980,6 +990,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_kernel(PropagateArgs a)
             wst.node = lds_stack + threadIdx.x;
             wst.dist = reinterpret_cast<float *>(lds_stack) + WIDE_LDS * BLOCK + threadIdx.x;
             uint32_t overflow = 0;
+            WalkCounts cnt{0u, 0u, 0u};
             State s;
             int scatter_first = a.scatter_first;
             const DevGeom &g = a.g;
@@ -988,7 +999,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_kernel(PropagateArgs a)
                 steps++;
                 const float prod = ((((p.dir.x * p.dir.y) * p.dir.z) * p.pos.x) * p.pos.y) * p.pos.z;
                 if (chr_isnan(prod)) { p.history |= CHR_NO_HIT | CHR_NAN_ABORT; break; }
-                fill_state<BATCH, WIDE>(g, s, p, st, wst, overflow);
+                fill_state<BATCH, WIDE, COUNT>(g, s, p, st, wst, overflow, cnt);
                 if (p.last_hit == -1) break;
                 int command = propagate_to_boundary(g, p, s, rng, a.use_weights, scatter_first);
                 scatter_first = 0;
@@ -1013,6 +1024,12 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_kernel(PropagateArgs a)
             a.weights[photon_id] = p.weight;
             alive = (p.history & DEAD_MASK) == 0;
             if (overflow) atomicAdd(a.counters, overflow);
+            if constexpr (COUNT) {
+                unsigned long long *c64 = reinterpret_cast<unsigned long long *>(a.counters + 2);
+                atomicAdd(c64, (unsigned long long)cnt.nodes);
+                atomicAdd(c64 + 1, (unsigned long long)cnt.tris);
+                atomicAdd(c64 + 2, (unsigned long long)cnt.walks);
+            }
         }
     }
     const unsigned long long mask = __ballot(alive);
@@ -1167,7 +1184,8 @@ __global__ __launch_bounds__(BLOCK) void distance_kernel(DevGeom g, uint32_t n, 
         WStack st;
         st.node = lds_stack + threadIdx.x;
         st.dist = reinterpret_cast<float *>(lds_stack) + WIDE_LDS * BLOCK + threadIdx.x;
-        tri = intersect_wide(g, o, d, dist, -1, st, overflow);
+        WalkCounts cnt;
+        tri = intersect_wide<false>(g, o, d, dist, -1, st, overflow, cnt);
     } else {
         Stack st;
         st.lds = lds_stack + threadIdx.x;
@@ -1280,17 +1298,18 @@ static const propagate_fn kVariants[] = {
     propagate_kernel<8, 3, true>,    // 2
     propagate_kernel<8, 5, true>,    // 3
     propagate_kernel<1, 3, false>,   // 4: reference-shaped one-node-at-a-time walk
+    propagate_kernel<8, 4, true, true>,   // 5: default + node/triangle counters (bench's byte count)
 };
 static constexpr int kExactVariant = 1;
 static propagate_fn select_variant(const chr_geometry *g) {
     const char *e = getenv("CHR_PROPAGATE_VARIANT");   // read per launch: A/B in one process
     int v = e ? atoi(e) : 0;
     if (v < 0 || v >= (int)(sizeof(kVariants) / sizeof(kVariants[0]))) v = 0;
-    if (g->dev.nwnodes == 0 && (v == 0 || v == 2 || v == 3)) v = kExactVariant;   // no wide BVH for this geometry
+    if (g->dev.nwnodes == 0 && (v == 0 || v == 2 || v == 3 || v == 5)) v = kExactVariant;   // no wide BVH for this geometry
     return kVariants[v];
 }
 
-// scratch layout (u32 words): [0..7] counters/base; masks (u64, 8-aligned); offsets
+// scratch layout (u32 words): [0] overflows [1] queue base [2..7] u64 walk counters; masks (u64, 8-aligned); offsets
 static int launch_chunk(const chr_geometry *g, const chr_photons *ph, uint32_t *rng, uint32_t nslots, int32_t first,
                         int32_t nthreads, const uint32_t *in_queue, uint32_t *out_queue, int32_t max_steps,
                         int32_t use_weights, int32_t scatter_first, uint32_t *scratch, hipStream_t stream,
@@ -1362,7 +1381,7 @@ extern "C" int chr_propagate(const chr_geometry *g, const chr_photons *ph, uint3
     q[0] = (uint32_t *)buf;
     q[1] = q[0] + (nphotons + 1);
     scratch = (uint32_t *)(((uintptr_t)(q[1] + nphotons + 1) + 15) & ~(uintptr_t)15);
-    CHR_HIP_CHECK(hipHostMalloc((void **)&pinned, 16, hipHostMallocDefault));
+    CHR_HIP_CHECK(hipHostMalloc((void **)&pinned, 64, hipHostMallocDefault));
     const size_t max_chunks = (nphotons + chunk_cap - 1) / chunk_cap;
     std::vector<hipEvent_t> events(2 * max_chunks, nullptr);
     for (auto &ev : events) CHR_HIP_CHECK(hipEventCreate(&ev));
@@ -1427,8 +1446,16 @@ extern "C" int chr_propagate(const chr_geometry *g, const chr_photons *ph, uint3
         }
     }
     if ((e = hipMemcpyAsync(pinned + 2, scratch, 4, hipMemcpyDeviceToHost, stream)) != hipSuccess) { cleanup(); CHR_HIP_CHECK(e); }
+    if ((e = hipMemcpyAsync(pinned + 4, scratch + 2, 24, hipMemcpyDeviceToHost, stream)) != hipSuccess) { cleanup(); CHR_HIP_CHECK(e); }
     if ((e = hipStreamSynchronize(stream)) != hipSuccess) { cleanup(); CHR_HIP_CHECK(e); }
     st.stack_overflows = pinned[2];
+    {
+        uint64_t c[3];
+        std::memcpy(c, pinned + 4, 24);
+        st.nodes_visited = c[0];
+        st.triangles_tested = c[1];
+        st.traversals = c[2];
+    }
     st.kernel_ms = kernel_ms;
     st.final_alive = (step < max_steps) ? (uint32_t)n : 0u;
     cleanup();

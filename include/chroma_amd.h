@@ -155,6 +155,9 @@ typedef struct chr_propagate_stats {
     uint32_t final_alive;       /* photons still in the queue at exit */
     uint32_t stack_overflows;   /* traversals that exceeded the 1000-entry stack */
     double kernel_ms;           /* summed device time of the propagate kernels (HIP events) */
+    uint64_t nodes_visited;     /* BVH nodes / triangles / walks: filled only by the counting */
+    uint64_t triangles_tested;  /* kernel variant (CHR_PROPAGATE_VARIANT=5), zero otherwise */
+    uint64_t traversals;
 } chr_propagate_stats;
 
 /* replaces: GPUPhotons.propagate host loop (chroma/gpu/photon.py:226-293) for
