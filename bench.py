@@ -135,6 +135,36 @@ def cpu_baseline(packed, photons, nslots, ntpb, max_blocks, max_steps, seed, bud
                        'threads' % (n, max_steps, total_t, threads)), b_alg, stats, n
 
 
+def roofline(args, cst, n, kernel_ms, launches):
+    """roofline object of the bench line for the dominant kernel (propagate_kernel)."""
+    b_alg = 120.0 + (96.0 * cst.nodes_visited + 64.0 * cst.triangles_tested + 52.0 * cst.traversals) / n
+    launches_per_step = launches / args.steps
+    alg_per_launch = n * b_alg / launches_per_step
+    avg_launch_s = kernel_ms / max(1, launches) / 1e3
+    achieved = alg_per_launch / avg_launch_s / 1e9
+    rl = {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+          'frac': achieved / HBM_PEAK_GBS, 'traffic': None,
+          'alg_bytes_per_launch': alg_per_launch,
+          'bytes_per_photon_alg': b_alg,
+          'nodes_per_photon': cst.nodes_visited / n,
+          'triangles_per_photon': cst.triangles_tested / n,
+          'traversals_per_photon': cst.traversals / n,
+          'kernel': 'chr::propagate_kernel<8,4,true>',
+          'avg_launch_ms': 1e3 * avg_launch_s}
+    # HBM bytes per launch from the PMC passes (tools/rocprof_bench.sh) of this same workload
+    pmc_path = os.path.join(ROOT, 'profiles', 'latest_pmc.json')
+    if os.path.exists(pmc_path):
+        with open(pmc_path) as f:
+            pmc = json.load(f)
+        w = pmc.get('workload', {})
+        if (w.get('detector'), w.get('photons'), w.get('max_steps')) == (args.detector, args.photons, args.max_steps) \
+                and 'hbm_bytes_per_launch' in pmc:
+            rl['traffic'] = pmc['hbm_bytes_per_launch']
+            rl['traffic_unit'] = 'bytes/launch (FETCH_SIZE x2 + WRITE_SIZE)'
+            rl['traffic_source'] = pmc.get('source')
+    return rl
+
+
 def main():
     ap = argparse.ArgumentParser(description=__doc__)
     ap.add_argument('--gpus', type=int, default=1)
@@ -148,6 +178,8 @@ def main():
     ap.add_argument('--seed', type=int, default=1)
     ap.add_argument('--cpu-budget', type=float, default=20.0, help='seconds of CPU-baseline work')
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--no-count', action='store_true',
+                    help='skip the untimed counting pass (profiling runs: keeps rocprof averages to one variant)')
     ap.add_argument('--cache-dir', default=os.environ.get('CHROMA_BENCH_CACHE', '/tmp/chroma_bench_cache'))
     args = ap.parse_args()
 
@@ -213,14 +245,16 @@ def main():
         elapsed = float(tt.item())
     detected = int(((gp.flags.get() & 4) != 0).sum())
     # untimed: same propagate with the counting kernel variant -> algorithmic bytes
-    prev = os.environ.get('CHR_PROPAGATE_VARIANT')
-    os.environ['CHR_PROPAGATE_VARIANT'] = '5'
-    cst = step().last_stats
-    if prev is None:
-        del os.environ['CHR_PROPAGATE_VARIANT']
-    else:
-        os.environ['CHR_PROPAGATE_VARIANT'] = prev
-    torch.cuda.synchronize()
+    cst = None
+    if not args.no_count:
+        prev = os.environ.get('CHR_PROPAGATE_VARIANT')
+        os.environ['CHR_PROPAGATE_VARIANT'] = '5'
+        cst = step().last_stats
+        if prev is None:
+            del os.environ['CHR_PROPAGATE_VARIANT']
+        else:
+            os.environ['CHR_PROPAGATE_VARIANT'] = prev
+        torch.cuda.synchronize()
 
     if rank == 0:
         total = args.photons * world * args.steps
@@ -243,17 +277,8 @@ def main():
             'roofline': None, 'cpu_baseline': None,
         }
         n = float(args.photons)
-        b_alg = 120.0 + (96.0 * cst.nodes_visited + 64.0 * cst.triangles_tested + 52.0 * cst.traversals) / n
-        per_step_s = kernel_ms / args.steps / 1e3
-        achieved = n * b_alg / per_step_s / 1e9
-        result['roofline'] = {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
-                              'frac': achieved / HBM_PEAK_GBS, 'traffic': None,
-                              'bytes_per_photon_alg': b_alg,
-                              'nodes_per_photon': cst.nodes_visited / n,
-                              'triangles_per_photon': cst.triangles_tested / n,
-                              'traversals_per_photon': cst.traversals / n,
-                              'kernel': 'chr::propagate_kernel<8,4,true>',
-                              'avg_launch_ms': kernel_ms / max(1, launches)}
+        if cst is not None:
+            result['roofline'] = roofline(args, cst, n, kernel_ms, launches)
         if not args.no_cpu_baseline and world == 1:
             threads = min(16, len(os.sched_getaffinity(0)))
             cpu, _, ostats, nsample = cpu_baseline(PackedGeometry(det), photons, nslots, args.nthreads_per_block,

@@ -1,0 +1,54 @@
+#!/usr/bin/env python
+"""Summarise the FETCH_SIZE / WRITE_SIZE passes of tools/rocprof_bench.sh into
+HBM bytes per propagate-kernel launch (MI355X_MICROARCH.md "HBM": FETCH_SIZE and
+WRITE_SIZE are rocprofv3 derived counters in KiB; on gfx950 FETCH_SIZE reports
+half the bytes of wide coalesced reads, so it is doubled here -- an upper-bound
+correction for the narrower gathers of the BVH walk, whose calibration is
+unknown).  Prints one JSON object."""
+import csv
+import glob
+import json
+import os
+import sys
+
+
+def per_kernel(d, counter):
+    files = glob.glob(os.path.join(d, '**', '*counter_collection.csv'), recursive=True)
+    vals = {}
+    for f in files:
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                if row.get('Counter_Name') != counter:
+                    continue
+                name = row.get('Kernel_Name', '')
+                key = (row.get('Dispatch_Id'), name)
+                vals[key] = vals.get(key, 0.0) + float(row['Counter_Value'])
+    out = {}
+    for (_, name), v in vals.items():
+        short = name.split('(')[0]
+        out.setdefault(short, []).append(v)
+    return out
+
+
+def main():
+    d = sys.argv[1]
+    fetch = per_kernel(os.path.join(d, 'fetch'), 'FETCH_SIZE')
+    write = per_kernel(os.path.join(d, 'write'), 'WRITE_SIZE')
+    k = 'chr::propagate_kernel'
+    res = {'kernel': k}
+    if k in fetch:
+        f = fetch[k]
+        res['launches_fetch_pass'] = len(f)
+        res['fetch_kib_per_launch_raw'] = sum(f) / len(f)
+        res['read_bytes_per_launch'] = 2.0 * 1024.0 * sum(f) / len(f)
+    if k in write:
+        w = write[k]
+        res['launches_write_pass'] = len(w)
+        res['write_bytes_per_launch'] = 1024.0 * sum(w) / len(w)
+    if 'read_bytes_per_launch' in res and 'write_bytes_per_launch' in res:
+        res['hbm_bytes_per_launch'] = res['read_bytes_per_launch'] + res['write_bytes_per_launch']
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == '__main__':
+    main()
