@@ -149,6 +149,8 @@ def roofline(args, cst, n, kernel_ms, launches):
           'nodes_per_photon': cst.nodes_visited / n,
           'triangles_per_photon': cst.triangles_tested / n,
           'traversals_per_photon': cst.traversals / n,
+          'simd_efficiency_nodes': cst.nodes_visited / max(1.0, 64.0 * cst.wave_node_steps),
+          'simd_efficiency_triangles': cst.triangles_tested / max(1.0, 64.0 * cst.wave_triangle_steps),
           'kernel': 'chr::propagate_kernel<8,4,true>',
           'avg_launch_ms': 1e3 * avg_launch_s}
     # HBM bytes per launch from the PMC passes (tools/rocprof_bench.sh) of this same workload

@@ -10,6 +10,8 @@ import os
 
 _LIBPATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), '_lib',
                         'libchroma_amd.so')
+# dev A/B of alternative builds (still in-tree): CHROMA_AMD_LIB=/path/to/libchroma_amd*.so
+_LIBPATH = os.environ.get('CHROMA_AMD_LIB', _LIBPATH)
 
 c_u32 = ctypes.c_uint32
 c_i32 = ctypes.c_int32
@@ -62,7 +64,7 @@ class PhotonsDesc(ctypes.Structure):
 class PropagateStats(ctypes.Structure):
     _fields_ = [('steps_run', c_u32), ('launches', c_u32), ('final_alive', c_u32), ('stack_overflows', c_u32),
                 ('kernel_ms', ctypes.c_double), ('nodes_visited', c_u64), ('triangles_tested', c_u64),
-                ('traversals', c_u64)]
+                ('traversals', c_u64), ('wave_node_steps', c_u64), ('wave_triangle_steps', c_u64)]
 
 
 _SIGNATURES = {
@@ -120,6 +122,8 @@ def lib():
                               '`make -C chroma-lite_amd/csrc` (or __graft_entry__.build())' % _LIBPATH)
         l = ctypes.CDLL(_LIBPATH)
         for name, (res, args) in _SIGNATURES.items():
+            if 'CHROMA_AMD_LIB' in os.environ and not hasattr(l, name):
+                continue     # dev A/B against an older build
             fn = getattr(l, name)
             fn.restype = res
             fn.argtypes = args

@@ -6,8 +6,10 @@
 // triangles as index triples into a vertex array (4 dependent loads/triangle).
 //
 // Here:
-//  * DevGeom is passed BY VALUE as a kernel argument (lands in SGPRs, no
-//    per-block copy);
+//  * DevGeom lives in device memory and kernels take a `const DevGeom *__restrict__`:
+//    its fields are uniform scalar loads, and passing it to out-of-line helpers
+//    passes a pointer (a by-value kernel argument whose address escapes gets
+//    copied into every work-item's scratch);
 //  * BVH nodes stay the reference's 16-byte quantised uint4 (the exact-order
 //    traversal variant walks them); the default traversal walks an 8-wide SAH
 //    BVH built over the same leaf boxes with the reference DFS rank as the
@@ -68,6 +70,7 @@ struct DevGeom {
 
 struct chr_geometry {
     chr::DevGeom dev;
+    void *d_dev;          // a device copy of dev: kernels take `const DevGeom *` (uniform scalar loads)
     int device;
     uint64_t bytes;
     void *allocs[12];

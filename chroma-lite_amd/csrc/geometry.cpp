@@ -225,6 +225,8 @@ extern "C" int chr_geometry_create(const chr_geometry_desc *d, chr_geometry **ou
             if ((rc = dev_upload(g, d->wireplanes, (size_t)d->nwireplanes * sizeof(chr_wireplane_desc), &p))) throw rc;
             dg.wireplanes = (const chr_wireplane_desc *)p;
         }
+        if ((rc = dev_upload(g, &dg, sizeof(dg), &p))) throw rc;
+        g->d_dev = p;
     } catch (int code) {
         chr_geometry_destroy(g);
         return code;

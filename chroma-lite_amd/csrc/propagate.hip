@@ -17,6 +17,7 @@
 //   * all transcendental math is include/chroma_fmath.h, bit-identical to the
 //     CPU oracle.
 #include <hip/hip_runtime.h>
+#include <rocprim/device/device_radix_sort.hpp>
 
 #include <algorithm>
 #include <cstdint>
@@ -62,17 +63,40 @@ struct State {
     int material1, surface_index;
 };
 
+#define CHR_LDS __attribute__((address_space(3)))
+#ifndef CHR_COLD
+#define CHR_COLD __forceinline__
+#endif
+// The LDS column pointer travels as a plain value (never inside an object that
+// also holds the scratch spill array: such an object lives in scratch and its
+// LDS pointer degrades to flat loads/stores).
 struct Stack {
-    uint32_t *lds;      // this work-item's column: entry i at lds[i * BLOCK]
-    uint32_t spill[STACK_SIZE - STACK_LDS];
+    CHR_LDS uint32_t *lds;   // this work-item's column: entry i at lds[i * BLOCK]
 };
 
-__device__ __forceinline__ void stack_put(Stack &s, int i, uint32_t v) {
+__device__ __forceinline__ void stack_put(const Stack &s, uint32_t *spill, int i, uint32_t v) {
     if (i < STACK_LDS) s.lds[i * BLOCK] = v;
-    else s.spill[i - STACK_LDS] = v;
+    else spill[i - STACK_LDS] = v;
 }
-__device__ __forceinline__ uint32_t stack_get(const Stack &s, int i) {
-    return (i < STACK_LDS) ? s.lds[i * BLOCK] : s.spill[i - STACK_LDS];
+__device__ __forceinline__ uint32_t stack_get(const Stack &s, const uint32_t *spill, int i) {
+    return (i < STACK_LDS) ? s.lds[i * BLOCK] : spill[i - STACK_LDS];
+}
+
+// Loads through pointers fetched from the device-resident DevGeom are flat
+// (generic) loads unless the address space is stated; flat loads also count in
+// lgkmcnt and so serialise against the LDS stack.  gld() = global_load.
+#define CHR_GLOBAL __attribute__((address_space(1)))
+template <typename T>
+__device__ __forceinline__ T gld(const T *p) { return *(const CHR_GLOBAL T *)p; }
+typedef uint32_t chr_u32x4 __attribute__((ext_vector_type(4)));
+typedef float chr_f32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 gld(const uint4 *p) {
+    const chr_u32x4 v = *(const CHR_GLOBAL chr_u32x4 *)p;
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ float4 gld(const float4 *p) {
+    const chr_f32x4 v = *(const CHR_GLOBAL chr_f32x4 *)p;
+    return make_float4(v.x, v.y, v.z, v.w);
 }
 
 // ---------------------------------------------------------------- geometry.h
@@ -86,11 +110,12 @@ __device__ __forceinline__ void node_bounds(const DevGeom &g, uint4 n, V3 &lo, V
 __device__ __forceinline__ float interp_property(const DevGeom &g, float x, const float *fp) {
     const float start = g.wl_start, step = g.wl_step;
     const int n = (int)g.wl_n;
-    if (x < start) return fp[0];
-    if (x > __builtin_fmaf((float)(n - 1), step, start)) return fp[n - 1];
+    if (x < start) return gld(fp);
+    if (x > __builtin_fmaf((float)(n - 1), step, start)) return gld(fp + n - 1);
     const int jl = (int)((x - start) / step);
     const float base = __builtin_fmaf((float)jl, step, start);
-    return fp[jl] + ((x - base) * (fp[jl + 1] - fp[jl])) / step;
+    const float f0 = gld(fp + jl), f1 = gld(fp + jl + 1);
+    return f0 + ((x - base) * (f1 - f0)) / step;
 }
 
 __device__ float interp_idx(float x, int n, const float *xp) {
@@ -172,31 +197,32 @@ __device__ __forceinline__ bool intersect_triangle(V3 o, V3 d, V3 v0, V3 e1, V3 
 // then walked strictly in index order with the reference's prune / accept /
 // push decisions, so the result (including tie-breaking) is unchanged.
 template <int BATCH>
-__device__ int intersect_mesh(const DevGeom &g, V3 o, V3 d, float &min_distance, int last_hit, Stack &st,
-                              uint32_t &overflow) {
+__device__ __forceinline__ int intersect_mesh(const DevGeom &g, V3 o, V3 d, float &min_distance, int last_hit,
+                                              Stack st, uint32_t &overflow) {
+    uint32_t spill[STACK_SIZE - STACK_LDS];
     int triangle_index = -1;
     min_distance = -1.0f;
     const V3 noid = v3(-o.x / d.x, -o.y / d.y, -o.z / d.z);
     const V3 inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
-    const uint4 root = g.nodes[0];
+    const uint4 root = gld(g.nodes);
     {
         V3 lo, hi;
         float bd;
         node_bounds(g, root, lo, hi);
         if (!intersect_box(noid, inv, lo, hi, bd)) return -1;
     }
-    stack_put(st, 0, root.w);
+    stack_put(st, spill, 0, root.w);
     int curr = 0;
     const uint32_t last = (uint32_t)last_hit;
     while (curr >= 0) {
-        const uint32_t w = stack_get(st, curr);
+        const uint32_t w = stack_get(st, spill, curr);
         curr--;
         const uint32_t end = (w & 0x0FFFFFFFu) + (w >> 28);
         for (uint32_t i = w & 0x0FFFFFFFu; i < end; i += BATCH) {
             uint4 nd[BATCH];
 #pragma unroll
             for (int k = 0; k < BATCH; ++k)
-                if (i + k < end) nd[k] = g.nodes[i + k];
+                if (i + k < end) nd[k] = gld(g.nodes + i + k);
             float bd[BATCH];
             bool hit[BATCH];
 #pragma unroll
@@ -213,7 +239,7 @@ __device__ int intersect_mesh(const DevGeom &g, V3 o, V3 d, float &min_distance,
                 if ((nd[k].w >> 28) == 0) {
                     if (child != last) {
                         const float4 *r = g.tri + 3 * (size_t)child;
-                        const float4 r0 = r[0], r1 = r[1], r2 = r[2];
+                        const float4 r0 = gld(r), r1 = gld(r + 1), r2 = gld(r + 2);
                         float dist;
                         if (intersect_triangle(o, d, v3(r0.x, r0.y, r0.z), v3(r0.w, r1.x, r1.y), v3(r1.z, r1.w, r2.x),
                                                dist)) {
@@ -229,7 +255,7 @@ __device__ int intersect_mesh(const DevGeom &g, V3 o, V3 d, float &min_distance,
                         return triangle_index;
                     }
                     curr++;
-                    stack_put(st, curr, nd[k].w);
+                    stack_put(st, spill, curr, nd[k].w);
                 }
             }
         }
@@ -248,6 +274,11 @@ __device__ int intersect_mesh(const DevGeom &g, V3 o, V3 d, float &min_distance,
 // first, the others pushed and culled at pop against the running best.
 constexpr int WIDE_LDS = 16;
 
+// NB: measured (profiles/r01/ab_stack_layout.log): keeping the LDS column
+// pointers generic and the spill array in the same object (flat stack ops)
+// runs the walk 1.4x faster than typed LDS pointers with ds_* ops -- the
+// typed form changes how the walk's control flow is structurised and the
+// wave executes ~1.8x more VALU instructions for the same per-lane work.
 struct WStack {
     uint32_t *node;     // this work-item's LDS column: entry i at node[i * BLOCK]
     float *dist;
@@ -271,7 +302,12 @@ __device__ __forceinline__ float exp_scale(uint32_t e) { return __uint_as_float(
 
 struct WalkCounts {   // filled only by the counting variant (bench: algorithmic bytes per photon)
     uint32_t nodes, tris, walks;
+    uint32_t wave_nodes, wave_tris;   // steps the whole wave executed (counted by its first active lane)
 };
+__device__ __forceinline__ bool wave_leader() {
+    const unsigned long long m = __ballot(1);
+    return (unsigned)__lane_id() == (unsigned)(__ffsll((long long)m) - 1);
+}
 
 template <bool COUNT>
 __device__ int intersect_wide(const DevGeom &g, V3 o, V3 d, float &min_distance, int last_hit, WStack &st,
@@ -286,9 +322,10 @@ __device__ int intersect_wide(const DevGeom &g, V3 o, V3 d, float &min_distance,
     int sp = 0;
     uint32_t node = 0;
     while (true) {
-        if constexpr (COUNT) cnt.nodes++;
+        if constexpr (COUNT) { cnt.nodes++; if (wave_leader()) cnt.wave_nodes++; }
         const uint4 *np = g.wnodes + 6 * (size_t)node;
-        const uint4 h = np[0], a1 = np[1], a2 = np[2], a3 = np[3], a4 = np[4], a5 = np[5];
+        const uint4 h = gld(np), a1 = gld(np + 1), a2 = gld(np + 2), a3 = gld(np + 3), a4 = gld(np + 4),
+                    a5 = gld(np + 5);
         const V3 org = v3(__uint_as_float(h.x), __uint_as_float(h.y), __uint_as_float(h.z));
         const float sx = exp_scale(h.w), sy = exp_scale(h.w >> 8), sz = exp_scale(h.w >> 16);
         uint32_t leaf_mask = 0;
@@ -323,9 +360,9 @@ __device__ int intersect_wide(const DevGeom &g, V3 o, V3 d, float &min_distance,
             const uint32_t ntri = (uint32_t)(kinds >> (8 * k)) & 0xFFu;
             const uint32_t first = a4.y + ((uint32_t)(offs >> (8 * k)) & 0xFFu);
             for (uint32_t j = 0; j < ntri; ++j) {
-                if constexpr (COUNT) cnt.tris++;
+                if constexpr (COUNT) { cnt.tris++; if (wave_leader()) cnt.wave_tris++; }
                 const float4 *r = g.wtri + 4 * (size_t)(first + j);
-                const float4 r0 = r[0], r1 = r[1], r2 = r[2], r3 = r[3];
+                const float4 r0 = gld(r), r1 = gld(r + 1), r2 = gld(r + 2), r3 = gld(r + 3);
                 const uint32_t id = __float_as_uint(r2.y);
                 if (id == last) continue;
                 V3 lo, hi;
@@ -362,12 +399,134 @@ __device__ int intersect_wide(const DevGeom &g, V3 o, V3 d, float &min_distance,
 }
 
 
+// The same query, scheduled for 64-wide SIMT (default).  Leaf triangles are
+// not tested inside the node step of the lane that reached them: a lane that
+// hits leaves parks them (one node's worth) and the WAVE decides each
+// iteration, by ballot, between a node step (lanes without parked work) and
+// a triangle step (every lane with parked work tests one triangle) -- the
+// triangle step runs when >= TRI_BATCH lanes have work or no lane can
+// traverse.  This keeps most lanes busy in both kinds of step (measured
+// SIMD efficiency of the per-node loop above: 6% for triangles).
+// Moller-Trumbore runs first; the reference leaf slab test + prune
+// (mesh.h:94-96) is evaluated only for a hit that would become the best,
+// with the same `best`, so the accept decision is unchanged.
+template <bool COUNT, int TRI_BATCH>
+__device__ int intersect_wide_sched(const DevGeom &g, V3 o, V3 d, float &min_distance, int last_hit, WStack &st,
+                                    uint32_t &overflow, WalkCounts &cnt) {
+    if constexpr (COUNT) cnt.walks++;
+    const V3 noid = v3(-o.x / d.x, -o.y / d.y, -o.z / d.z);
+    const V3 inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    float best = __builtin_inff();
+    uint32_t best_rank = 0xFFFFFFFFu;
+    int best_id = -1;
+    const uint32_t last = (uint32_t)last_hit;
+    int sp = 0;
+    uint32_t node = 0;              // node to expand next (INVALID: pop)
+    bool done = false;
+    // parked leaf work of one node: current leaf [pcur, pcur+pleft), further hit leaves in pmask
+    uint32_t pcur = 0, pleft = 0, pmask = 0, pbase = 0;
+    unsigned long long pkinds = 0, poffs = 0;
+    constexpr uint32_t INVALID = 0xFFFFFFFFu;
+    while (true) {
+        const bool has_work = pleft != 0;
+        const bool can_walk = !done && !has_work;
+        const unsigned long long mw = __ballot(can_walk);
+        const unsigned long long mt = __ballot(has_work);
+        if ((mw | mt) == 0) break;
+        if (mw != 0 && __popcll(mt) < TRI_BATCH) {
+            // ------------------------------------------------ node step
+            if (!can_walk) continue;
+            if (node == INVALID) {
+                bool found = false;
+                while (sp > 0) {
+                    sp--;
+                    float t;
+                    wpop(st, sp, node, t);
+                    if (!(t > best)) { found = true; break; }
+                }
+                if (!found) { done = true; continue; }
+            }
+            if constexpr (COUNT) { cnt.nodes++; if (wave_leader()) cnt.wave_nodes++; }
+            const uint4 *np = g.wnodes + 6 * (size_t)node;
+            const uint4 h = gld(np), a1 = gld(np + 1), a2 = gld(np + 2), a3 = gld(np + 3), a4 = gld(np + 4),
+                        a5 = gld(np + 5);
+            const V3 org = v3(__uint_as_float(h.x), __uint_as_float(h.y), __uint_as_float(h.z));
+            const float sx = exp_scale(h.w), sy = exp_scale(h.w >> 8), sz = exp_scale(h.w >> 16);
+            uint32_t leaf_mask = 0;
+            uint32_t near_node = INVALID;
+            float near_t = 0.0f;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const uint32_t kind = ((k < 4 ? a4.z : a4.w) >> (8 * (k & 3))) & 0xFFu;
+                if (kind == 0) continue;
+                const V3 lo = v3(__builtin_fmaf(byte_f(a1.x, a1.y, k), sx, org.x),
+                                 __builtin_fmaf(byte_f(a1.z, a1.w, k), sy, org.y),
+                                 __builtin_fmaf(byte_f(a2.x, a2.y, k), sz, org.z));
+                const V3 hi = v3(__builtin_fmaf(byte_f(a2.z, a2.w, k), sx, org.x),
+                                 __builtin_fmaf(byte_f(a3.x, a3.y, k), sy, org.y),
+                                 __builtin_fmaf(byte_f(a3.z, a3.w, k), sz, org.z));
+                float bd;
+                if (!intersect_box(noid, inv, lo, hi, bd) || bd > best) continue;
+                if (kind != WIDE_INNER) { leaf_mask |= 1u << k; continue; }
+                const uint32_t child = a4.x + (((k < 4 ? a5.x : a5.y) >> (8 * (k & 3))) & 0xFFu);
+                if (near_node == INVALID) { near_node = child; near_t = bd; continue; }
+                uint32_t pn = child;
+                float pt = bd;
+                if (bd < near_t) { pn = near_node; pt = near_t; near_node = child; near_t = bd; }
+                if (sp >= WIDE_STACK) { overflow++; break; }
+                wpush(st, sp, pn, pt);
+                sp++;
+            }
+            node = near_node;
+            if (leaf_mask) {
+                pkinds = ((unsigned long long)a4.w << 32) | a4.z;
+                poffs = ((unsigned long long)a5.y << 32) | a5.x;
+                pbase = a4.y;
+                const int k = __builtin_ctz(leaf_mask);
+                pmask = leaf_mask & (leaf_mask - 1);
+                pleft = (uint32_t)(pkinds >> (8 * k)) & 0xFFu;
+                pcur = pbase + ((uint32_t)(poffs >> (8 * k)) & 0xFFu);
+            }
+        } else {
+            // ------------------------------------------------ triangle step
+            if (!has_work) continue;
+            if constexpr (COUNT) { cnt.tris++; if (wave_leader()) cnt.wave_tris++; }
+            const float4 *r = g.wtri + 4 * (size_t)pcur;
+            const float4 r0 = gld(r), r1 = gld(r + 1), r2 = gld(r + 2);
+            pcur++;
+            if (--pleft == 0 && pmask) {
+                const int k = __builtin_ctz(pmask);
+                pmask &= pmask - 1;
+                pleft = (uint32_t)(pkinds >> (8 * k)) & 0xFFu;
+                pcur = pbase + ((uint32_t)(poffs >> (8 * k)) & 0xFFu);
+            }
+            const uint32_t id = __float_as_uint(r2.y);
+            float dist;
+            if (id == last ||
+                !intersect_triangle(o, d, v3(r0.x, r0.y, r0.z), v3(r0.w, r1.x, r1.y), v3(r1.z, r1.w, r2.x), dist))
+                continue;
+            const uint32_t rank = __float_as_uint(r2.z);
+            if (!(dist < best || (dist == best && rank < best_rank))) continue;
+            const float4 r3 = gld(r + 3);
+            V3 lo, hi;
+            node_bounds(g, make_uint4(__float_as_uint(r2.w), __float_as_uint(r3.x), __float_as_uint(r3.y), 0u), lo, hi);
+            float bd;
+            if (!intersect_box(noid, inv, lo, hi, bd) || bd > best) continue;   // mesh.h:94-96
+            best = dist;
+            best_rank = rank;
+            best_id = (int)id;
+        }
+    }
+    min_distance = best_id == -1 ? -1.0f : best;
+    return best_id;
+}
+
 // ---------------------------------------------------------------- photon.h
 __device__ __forceinline__ int convert(int c) { return (c & 0x80) ? (int)(0xFFFFFF00u | (uint32_t)c) : c; }
 __device__ __forceinline__ float get_theta(V3 a, V3 b) { return chr_acosf(fmax_(-1.0f, fmin_(1.0f, dot(a, b)))); }
 
 // analytic wire planes (photon.h:108-270), FP64, rare path
-__device__ __noinline__ void wireplanes(const DevGeom &g, const Photon &p, float best_distance, int &a_surface,
+__device__ CHR_COLD void wireplanes(const DevGeom &g, const Photon &p, float best_distance, int &a_surface,
                                         int &a_inner, int &a_outer, V3 &a_normal_raw, float &a_dot_raw,
                                         float &a_distance) {
     for (int ip = 0; ip < (int)g.nwireplanes; ++ip) {
@@ -469,12 +628,14 @@ __device__ __noinline__ void wireplanes(const DevGeom &g, const Photon &p, float
 }
 
 // photon.h:87-397
-template <int BATCH, bool WIDE, bool COUNT>
-__device__ __forceinline__ void fill_state(const DevGeom &g, State &s, Photon &p, Stack &st, WStack &wst,
+template <int BATCH, int WIDE, bool COUNT>
+__device__ __forceinline__ void fill_state(const DevGeom &g, State &s, Photon &p, Stack st, WStack &wst,
                                            uint32_t &overflow, WalkCounts &cnt) {
     int mesh_triangle;
-    if constexpr (WIDE)
+    if constexpr (WIDE == 1)
         mesh_triangle = intersect_wide<COUNT>(g, p.pos, p.dir, s.distance, p.last_hit, wst, overflow, cnt);
+    else if constexpr (WIDE >= 2)   // scheduled walk, WIDE = triangle batch threshold
+        mesh_triangle = intersect_wide_sched<COUNT, WIDE>(g, p.pos, p.dir, s.distance, p.last_hit, wst, overflow, cnt);
     else mesh_triangle = intersect_mesh<BATCH>(g, p.pos, p.dir, s.distance, p.last_hit, st, overflow);
     int m1, m2;
     bool use_analytic = false;
@@ -494,9 +655,9 @@ __device__ __forceinline__ void fill_state(const DevGeom &g, State &s, Photon &p
         else { m1 = a_inner; m2 = a_outer; s.normal = -a_normal_raw; }
     } else if (mesh_triangle != -1) {
         p.last_hit = mesh_triangle;
-        const float4 r0 = g.tri[3 * (size_t)mesh_triangle], r1 = g.tri[3 * (size_t)mesh_triangle + 1],
-                     r2 = g.tri[3 * (size_t)mesh_triangle + 2];
-        const uint32_t code = g.material_codes[mesh_triangle];
+        const float4 *r = g.tri + 3 * (size_t)mesh_triangle;
+        const float4 r0 = gld(r), r1 = gld(r + 1), r2 = gld(r + 2);
+        const uint32_t code = gld(g.material_codes + mesh_triangle);
         const int inner = convert(0xFF & (int)(code >> 24));
         const int outer = convert(0xFF & (int)(code >> 16));
         s.surface_index = convert(0xFF & (int)(code >> 8));
@@ -722,7 +883,7 @@ __device__ Cx csqrt_(Cx x) {
 }
 
 // photon.h:669-827 (thin film); rare path, kept out of line
-__device__ __noinline__ int propagate_complex(const DevGeom &g, Photon &p, const State &s, chr_xorwow &rng,
+__device__ CHR_COLD int propagate_complex(const DevGeom &g, Photon &p, const State &s, chr_xorwow &rng,
                                               const DevSurface &sf, int use_weights) {
     const float *T = g.tables;
     float detect = interp_property(g, p.wavelength, T + sf.detect);
@@ -821,7 +982,7 @@ __device__ __noinline__ int propagate_complex(const DevGeom &g, Photon &p, const
 }
 
 // photon.h:829-874
-__device__ __noinline__ int propagate_at_wls(const DevGeom &g, Photon &p, const State &s, chr_xorwow &rng,
+__device__ CHR_COLD int propagate_at_wls(const DevGeom &g, Photon &p, const State &s, chr_xorwow &rng,
                                              const DevSurface &sf, int use_weights) {
     const float *T = g.tables;
     float absorb = interp_property(g, p.wavelength, T + sf.absorb);
@@ -858,7 +1019,7 @@ __device__ __noinline__ int propagate_at_wls(const DevGeom &g, Photon &p, const 
 }
 
 // photon.h:877-907 (iidx+1 clamped at the last angle, see oracle)
-__device__ __noinline__ int propagate_at_dichroic(const DevGeom &g, Photon &p, const State &s, chr_xorwow &rng,
+__device__ CHR_COLD int propagate_at_dichroic(const DevGeom &g, Photon &p, const State &s, chr_xorwow &rng,
                                                   const DevSurface &sf) {
     const float *T = g.tables;
     const float incident_angle = get_theta(s.normal, -p.dir);
@@ -882,7 +1043,7 @@ __device__ __noinline__ int propagate_at_dichroic(const DevGeom &g, Photon &p, c
 }
 
 // photon.h:909-951
-__device__ __noinline__ int propagate_at_angular(const DevGeom &g, Photon &p, const State &s, chr_xorwow &rng,
+__device__ CHR_COLD int propagate_at_angular(const DevGeom &g, Photon &p, const State &s, chr_xorwow &rng,
                                                  const DevSurface &sf, int use_weights) {
     const float *T = g.tables;
     const float incident_angle = get_theta(s.normal, -p.dir);
@@ -943,7 +1104,6 @@ __device__ __forceinline__ int propagate_at_surface(const DevGeom &g, Photon &p,
 
 // ---------------------------------------------------------------- kernels
 struct PropagateArgs {
-    DevGeom g;
     float *pos, *dir, *pol, *wl, *t, *weights;
     uint32_t *flags;
     int32_t *last_hit;
@@ -954,6 +1114,7 @@ struct PropagateArgs {
     int32_t first, nthreads, max_steps, use_weights, scatter_first;
     unsigned long long *alive_masks;   // one word per 64 slots
     uint32_t *counters;                // [0]: stack overflows
+    const uint32_t *order;             // coherence order: work-item t runs slot order[t] (nullptr: t)
 };
 
 __device__ __forceinline__ V3 load3(const float *p, uint32_t i) { return v3(p[3 * i], p[3 * i + 1], p[3 * i + 2]); }
@@ -961,12 +1122,18 @@ __device__ __forceinline__ void store3(float *p, uint32_t i, V3 v) { p[3 * i] = 
 
 // propagate.cu:254-366.  BATCH: children fetched together per group;
 // MINW: minimum waves per SIMD requested from the register allocator.
-template <int BATCH, int MINW, bool WIDE, bool COUNT = false>
-__global__ __launch_bounds__(BLOCK, MINW) void propagate_kernel(PropagateArgs a) {
+// WIDE: 0 exact-order walk of the reference BVH, 1 wide BVH node loop,
+// >= 2 wide BVH scheduled walk with that triangle batch threshold.
+template <int BATCH, int MINW, int WIDE, bool COUNT = false>
+__global__ __launch_bounds__(BLOCK, MINW) void propagate_kernel(const DevGeom *__restrict__ gdev, PropagateArgs a) {
     __shared__ uint32_t lds_stack[WIDE ? 2 * WIDE_LDS * BLOCK : STACK_LDS * BLOCK];
-    const int id = blockIdx.x * BLOCK + threadIdx.x;
+    const int tid = blockIdx.x * BLOCK + threadIdx.x;
     unsigned alive = 0;
-    if (id < a.nthreads) {
+    // A photon's RNG slot and queue position are its slot id, whichever
+    // work-item runs it: the coherence order only changes which rays share a
+    // wave, never what any photon computes.
+    const int id = (a.order && tid < a.nthreads) ? (int)a.order[tid] : tid;
+    if (tid < a.nthreads) {
         const uint32_t photon_id = a.input_queue[a.first + id];
         Photon p;
         p.history = a.flags[photon_id] & 0xFFFFu;   // unsigned short on the device (photon.h:29)
@@ -986,14 +1153,14 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_kernel(PropagateArgs a)
             p.weight = a.weights[photon_id];
             Stack st;
             WStack wst;
-            st.lds = lds_stack + threadIdx.x;
+            st.lds = (CHR_LDS uint32_t *)(lds_stack + threadIdx.x);
             wst.node = lds_stack + threadIdx.x;
             wst.dist = reinterpret_cast<float *>(lds_stack) + WIDE_LDS * BLOCK + threadIdx.x;
             uint32_t overflow = 0;
-            WalkCounts cnt{0u, 0u, 0u};
+            WalkCounts cnt{0u, 0u, 0u, 0u, 0u};
             State s;
             int scatter_first = a.scatter_first;
-            const DevGeom &g = a.g;
+            const DevGeom &g = *gdev;   // device-resident: uniform s_loads, no private copy
             int steps = 0;
             while (steps < a.max_steps) {
                 steps++;
@@ -1029,11 +1196,59 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_kernel(PropagateArgs a)
                 atomicAdd(c64, (unsigned long long)cnt.nodes);
                 atomicAdd(c64 + 1, (unsigned long long)cnt.tris);
                 atomicAdd(c64 + 2, (unsigned long long)cnt.walks);
+                atomicAdd(c64 + 3, (unsigned long long)cnt.wave_nodes);
+                atomicAdd(c64 + 4, (unsigned long long)cnt.wave_tris);
             }
         }
     }
+    if (a.order) {   // masks zeroed by the host; bit per slot
+        if (alive) atomicOr(a.alive_masks + (id >> 6), 1ull << (id & 63));
+        return;
+    }
     const unsigned long long mask = __ballot(alive);
     if ((threadIdx.x & 63) == 0 && id < a.nthreads) a.alive_masks[id >> 6] = mask;
+}
+
+// Coherence key of a queued photon: 18-bit Morton code of its position in the
+// world box (6 bits/axis) above a 12-bit octahedral direction cell.  Photons
+// already dead sort last (their work-items exit at once).
+__device__ __forceinline__ uint32_t spread3_6(uint32_t x) {   // 6 bits -> every third bit
+    x &= 0x3Fu;
+    x = (x | (x << 8)) & 0x0000F00Fu;
+    x = (x | (x << 4)) & 0x000C30C3u;
+    x = (x | (x << 2)) & 0x00249249u;
+    return x;
+}
+
+__global__ __launch_bounds__(BLOCK) void sort_key_kernel(const float *pos, const float *dir, const uint32_t *flags,
+                                                         const uint32_t *queue, int32_t first, int32_t n,
+                                                         float ox, float oy, float oz, float inv_extent,
+                                                         uint32_t *keys, uint32_t *vals) {
+    const int t = blockIdx.x * BLOCK + threadIdx.x;
+    if (t >= n) return;
+    const uint32_t ph = queue[first + t];
+    uint32_t key = 0xFFFFFFFFu;
+    if (!((flags[ph] & 0xFFFFu) & DEAD_MASK)) {
+        const V3 p = load3(pos, ph), d = load3(dir, ph);
+        auto cell = [&](float x, float o) {
+            const float u = (x - o) * inv_extent * 64.0f;
+            return (uint32_t)fminf(63.0f, fmaxf(0.0f, u));
+        };
+        const uint32_t m = spread3_6(cell(p.x, ox)) | (spread3_6(cell(p.y, oy)) << 1) | (spread3_6(cell(p.z, oz)) << 2);
+        // octahedral map of the direction to [0,1]^2, 6 bits each
+        const float l1 = fabsf(d.x) + fabsf(d.y) + fabsf(d.z);
+        float u = d.x / l1, v = d.y / l1;
+        if (d.z < 0.0f) {
+            const float uu = (1.0f - fabsf(v)) * (u >= 0.0f ? 1.0f : -1.0f);
+            const float vv = (1.0f - fabsf(u)) * (v >= 0.0f ? 1.0f : -1.0f);
+            u = uu; v = vv;
+        }
+        const uint32_t du = (uint32_t)fminf(63.0f, fmaxf(0.0f, (u * 0.5f + 0.5f) * 64.0f));
+        const uint32_t dv = (uint32_t)fminf(63.0f, fmaxf(0.0f, (v * 0.5f + 0.5f) * 64.0f));
+        key = (m << 12) | (du << 6) | dv;   // < 2^30 (NaN inputs land in some cell: harmless)
+    }
+    keys[t] = key;
+    vals[t] = (uint32_t)t;
 }
 
 // exclusive scan of the popcounts of nwords masks (single workgroup);
@@ -1170,11 +1385,12 @@ __global__ __launch_bounds__(BLOCK) void duplicate_kernel(PhotonPtrs ph, int32_t
 
 // mesh.h:131-159
 template <bool WIDE>
-__global__ __launch_bounds__(BLOCK) void distance_kernel(DevGeom g, uint32_t n, const float *origin, const float *dir,
+__global__ __launch_bounds__(BLOCK) void distance_kernel(const DevGeom *__restrict__ gdev, uint32_t n, const float *origin, const float *dir,
                                                           float *distance, uint32_t *counters) {
     __shared__ uint32_t lds_stack[WIDE ? 2 * WIDE_LDS * BLOCK : STACK_LDS * BLOCK];
     const uint32_t id = blockIdx.x * BLOCK + threadIdx.x;
     if (id >= n) return;
+    const DevGeom &g = *gdev;
     V3 o = load3(origin, id), d = load3(dir, id);
     d = d / norm(d);
     uint32_t overflow = 0;
@@ -1185,10 +1401,10 @@ __global__ __launch_bounds__(BLOCK) void distance_kernel(DevGeom g, uint32_t n, 
         st.node = lds_stack + threadIdx.x;
         st.dist = reinterpret_cast<float *>(lds_stack) + WIDE_LDS * BLOCK + threadIdx.x;
         WalkCounts cnt;
-        tri = intersect_wide<false>(g, o, d, dist, -1, st, overflow, cnt);
+        tri = intersect_wide_sched<false, 32>(g, o, d, dist, -1, st, overflow, cnt);
     } else {
         Stack st;
-        st.lds = lds_stack + threadIdx.x;
+        st.lds = (CHR_LDS uint32_t *)(lds_stack + threadIdx.x);
         tri = intersect_mesh<4>(g, o, d, dist, -1, st, overflow);
     }
     if (tri != -1) distance[id] = dist;
@@ -1282,51 +1498,86 @@ extern "C" int chr_rng_download(const uint32_t *d_states, uint32_t nslots, uint3
     return CHR_OK;
 }
 
+static size_t sort_temp_bytes(uint32_t n) {
+    size_t bytes = 0;
+    rocprim::radix_sort_pairs((void *)nullptr, bytes, (const uint32_t *)nullptr, (uint32_t *)nullptr,
+                              (const uint32_t *)nullptr, (uint32_t *)nullptr, n, 0, 30);
+    return bytes;
+}
+
+// u32 words: [0..7] counters | masks (2 per 64 slots) | offsets (1 per 64) |
+// sort keys in/out + order in/out (n each) | rocprim sort temporary storage
 extern "C" uint64_t chr_propagate_scratch_words(uint32_t nthreads) {
     const uint64_t nwords = (nthreads + 63) / 64;
-    return 2 * nwords /*masks*/ + nwords /*offsets*/ + 8;
+    return 16 + 2 * nwords /*masks*/ + nwords /*offsets*/ + 4 * (uint64_t)nthreads + 64 +
+           (sort_temp_bytes(nthreads) + 3) / 4;
 }
 
 // Kernel variants (A/B-able at run time with CHR_PROPAGATE_VARIANT=<n>;
 // all produce identical results, they differ only in schedule/occupancy).
-typedef void (*propagate_fn)(PropagateArgs);
+typedef void (*propagate_fn)(const DevGeom *, PropagateArgs);
 // measured on demo.detector(), 4M photons (profiles/r01/ab_variants.log):
 // <1,3> 89.2 ms, <4,3> 74.9, <4,4> 66.8, <4,5> 66.5, <8,4> 64.3, <8,3> 74.1, <2,3> 76.5
 static const propagate_fn kVariants[] = {
-    propagate_kernel<8, 4, true>,    // 0: default -- 8-wide SAH BVH, rank tie-break
-    propagate_kernel<8, 4, false>,   // 1: exact-order walk of the reference BVH, 8 children in flight
-    propagate_kernel<8, 3, true>,    // 2
-    propagate_kernel<8, 5, true>,    // 3
-    propagate_kernel<1, 3, false>,   // 4: reference-shaped one-node-at-a-time walk
-    propagate_kernel<8, 4, true, true>,   // 5: default + node/triangle counters (bench's byte count)
+    propagate_kernel<8, 4, 32>,          // 0: default -- 8-wide SAH BVH, wave-scheduled node/triangle steps
+    propagate_kernel<8, 4, 0>,           // 1: exact-order walk of the reference BVH, 8 children in flight
+    propagate_kernel<8, 4, 1>,           // 2: 8-wide BVH, triangles tested inside the node step
+    propagate_kernel<8, 4, 16>,          // 3: scheduled, triangle batch 16
+    propagate_kernel<8, 4, 48>,          // 4: scheduled, triangle batch 48
+    propagate_kernel<8, 4, 32, true>,    // 5: default + node/triangle counters (bench's byte count)
+    propagate_kernel<8, 3, 32>,          // 6: default at 3 waves/SIMD
+    propagate_kernel<8, 4, 1, true>,     // 7: variant 2 + counters
 };
 static constexpr int kExactVariant = 1;
 static propagate_fn select_variant(const chr_geometry *g) {
     const char *e = getenv("CHR_PROPAGATE_VARIANT");   // read per launch: A/B in one process
     int v = e ? atoi(e) : 0;
     if (v < 0 || v >= (int)(sizeof(kVariants) / sizeof(kVariants[0]))) v = 0;
-    if (g->dev.nwnodes == 0 && (v == 0 || v == 2 || v == 3 || v == 5)) v = kExactVariant;   // no wide BVH for this geometry
+    if (g->dev.nwnodes == 0 && v != 1) v = kExactVariant;   // no wide BVH for this geometry
     return kVariants[v];
 }
 
-// scratch layout (u32 words): [0] overflows [1] queue base [2..7] u64 walk counters; masks (u64, 8-aligned); offsets
+static constexpr int32_t kSortMin = 16384;   // below this a launch is a few waves: no reordering
+static bool sort_enabled() {
+    const char *e = getenv("CHR_SORT");   // read per launch (A/B); default on
+    return !(e && e[0] == '0');
+}
+
+// scratch layout (u32 words): [0] overflows [1] queue base [2..11] u64 walk counters [12..15] pad; masks (u64, 8-aligned); offsets
 static int launch_chunk(const chr_geometry *g, const chr_photons *ph, uint32_t *rng, uint32_t nslots, int32_t first,
                         int32_t nthreads, const uint32_t *in_queue, uint32_t *out_queue, int32_t max_steps,
                         int32_t use_weights, int32_t scatter_first, uint32_t *scratch, hipStream_t stream,
                         hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr) {
     const uint32_t nwords = (uint32_t)((nthreads + 63) / 64);
     uint32_t *counters = scratch;               // [0] overflows, [1] base
-    unsigned long long *masks = (unsigned long long *)(scratch + 8);
-    uint32_t *offsets = scratch + 8 + 2 * (size_t)nwords;
+    unsigned long long *masks = (unsigned long long *)(scratch + 16);
+    uint32_t *offsets = scratch + 16 + 2 * (size_t)nwords;
     PropagateArgs a;
-    a.g = g->dev;
     a.pos = ph->d_pos; a.dir = ph->d_dir; a.pol = ph->d_pol; a.wl = ph->d_wavelengths; a.t = ph->d_t;
     a.weights = ph->d_weights; a.flags = ph->d_flags; a.last_hit = ph->d_last_hit_triangles; a.evidx = ph->d_evidx;
     a.rng = rng; a.nslots = nslots; a.input_queue = in_queue; a.first = first; a.nthreads = nthreads;
     a.max_steps = max_steps; a.use_weights = use_weights; a.scatter_first = scatter_first;
     a.alive_masks = masks; a.counters = counters;
+    a.order = nullptr;
+    if (sort_enabled() && nthreads >= kSortMin) {
+        // coherence order (sort_key_kernel): rays that start close together in
+        // similar directions share a wave
+        uint32_t *keys = offsets + nwords;
+        uint32_t *keys_out = keys + nthreads, *vals = keys_out + nthreads, *vals_out = vals + nthreads;
+        void *temp = (void *)(((uintptr_t)(vals_out + nthreads) + 255) & ~(uintptr_t)255);
+        size_t temp_bytes = sort_temp_bytes((uint32_t)nthreads);
+        const float inv_extent = 1.0f / (g->dev.scale * 65536.0f);
+        hipLaunchKernelGGL(sort_key_kernel, dim3(grid_for(nthreads)), dim3(BLOCK), 0, stream, ph->d_pos, ph->d_dir,
+                           ph->d_flags, in_queue, first, nthreads, g->dev.ox, g->dev.oy, g->dev.oz, inv_extent, keys,
+                           vals);
+        CHR_HIP_CHECK(rocprim::radix_sort_pairs(temp, temp_bytes, keys, keys_out, vals, vals_out, (uint32_t)nthreads,
+                                                0, 30, stream));
+        CHR_HIP_CHECK(hipMemsetAsync(masks, 0, (size_t)nwords * 8, stream));
+        a.order = vals_out;
+    }
     if (ev0) CHR_HIP_CHECK(hipEventRecord(ev0, stream));
-    hipLaunchKernelGGL(select_variant(g), dim3(grid_for(nthreads)), dim3(BLOCK), 0, stream, a);
+    hipLaunchKernelGGL(select_variant(g), dim3(grid_for(nthreads)), dim3(BLOCK), 0, stream,
+                       (const DevGeom *)g->d_dev, a);
     if (ev1) CHR_HIP_CHECK(hipEventRecord(ev1, stream));
     hipLaunchKernelGGL(scan_masks_kernel, dim3(1), dim3(1024), 0, stream, masks, nwords, offsets, out_queue,
                        counters + 1, (uint32_t *)nullptr);
@@ -1381,7 +1632,7 @@ extern "C" int chr_propagate(const chr_geometry *g, const chr_photons *ph, uint3
     q[0] = (uint32_t *)buf;
     q[1] = q[0] + (nphotons + 1);
     scratch = (uint32_t *)(((uintptr_t)(q[1] + nphotons + 1) + 15) & ~(uintptr_t)15);
-    CHR_HIP_CHECK(hipHostMalloc((void **)&pinned, 64, hipHostMallocDefault));
+    CHR_HIP_CHECK(hipHostMalloc((void **)&pinned, 128, hipHostMallocDefault));
     const size_t max_chunks = (nphotons + chunk_cap - 1) / chunk_cap;
     std::vector<hipEvent_t> events(2 * max_chunks, nullptr);
     for (auto &ev : events) CHR_HIP_CHECK(hipEventCreate(&ev));
@@ -1403,7 +1654,7 @@ extern "C" int chr_propagate(const chr_geometry *g, const chr_photons *ph, uint3
     if ((e = hipMemcpyAsync(q[0], hq.data(), qbytes, hipMemcpyHostToDevice, stream)) != hipSuccess) { cleanup(); CHR_HIP_CHECK(e); }
     pinned[0] = 1;
     if ((e = hipMemcpyAsync(q[1], pinned, 4, hipMemcpyHostToDevice, stream)) != hipSuccess) { cleanup(); CHR_HIP_CHECK(e); }
-    if ((e = hipMemsetAsync(scratch, 0, 32, stream)) != hipSuccess) { cleanup(); CHR_HIP_CHECK(e); }
+    if ((e = hipMemsetAsync(scratch, 0, 64, stream)) != hipSuccess) { cleanup(); CHR_HIP_CHECK(e); }
     int cur = 0;
     int64_t n = nphotons;
     int step = 0;
@@ -1446,15 +1697,17 @@ extern "C" int chr_propagate(const chr_geometry *g, const chr_photons *ph, uint3
         }
     }
     if ((e = hipMemcpyAsync(pinned + 2, scratch, 4, hipMemcpyDeviceToHost, stream)) != hipSuccess) { cleanup(); CHR_HIP_CHECK(e); }
-    if ((e = hipMemcpyAsync(pinned + 4, scratch + 2, 24, hipMemcpyDeviceToHost, stream)) != hipSuccess) { cleanup(); CHR_HIP_CHECK(e); }
+    if ((e = hipMemcpyAsync(pinned + 4, scratch + 2, 40, hipMemcpyDeviceToHost, stream)) != hipSuccess) { cleanup(); CHR_HIP_CHECK(e); }
     if ((e = hipStreamSynchronize(stream)) != hipSuccess) { cleanup(); CHR_HIP_CHECK(e); }
     st.stack_overflows = pinned[2];
     {
-        uint64_t c[3];
-        std::memcpy(c, pinned + 4, 24);
+        uint64_t c[5];
+        std::memcpy(c, pinned + 4, 40);
         st.nodes_visited = c[0];
         st.triangles_tested = c[1];
         st.traversals = c[2];
+        st.wave_node_steps = c[3];
+        st.wave_triangle_steps = c[4];
     }
     st.kernel_ms = kernel_ms;
     st.final_alive = (step < max_steps) ? (uint32_t)n : 0u;
@@ -1535,9 +1788,10 @@ extern "C" int chr_distance_to_mesh(const chr_geometry *g, uint32_t n, const flo
     if (!g || !d_origin || !d_direction || !d_distance) return chr::fail(CHR_ERR_INVALID, "distance_to_mesh: null argument");
     if (n == 0) return CHR_OK;
     const char *e = getenv("CHR_PROPAGATE_VARIANT");
-    const bool wide = g->dev.nwnodes != 0 && !(e && (atoi(e) == 1 || atoi(e) == 4));
+    const bool wide = g->dev.nwnodes != 0 && !(e && atoi(e) == 1);
     hipLaunchKernelGGL(wide ? distance_kernel<true> : distance_kernel<false>, dim3(grid_for(n)), dim3(BLOCK), 0,
-                       (hipStream_t)stream, g->dev, n, d_origin, d_direction, d_distance, (uint32_t *)nullptr);
+                       (hipStream_t)stream, (const DevGeom *)g->d_dev, n, d_origin, d_direction, d_distance,
+                       (uint32_t *)nullptr);
     CHR_HIP_CHECK(hipGetLastError());
     return CHR_OK;
 }

@@ -26,6 +26,7 @@
 #include <atomic>
 #include <cmath>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <vector>
@@ -63,6 +64,7 @@ struct Cluster {
 };
 
 struct Builder {
+    bool fill_leaves;
     const std::vector<Box> &tri_box;
     const std::vector<float> &centroid;   // 3 per triangle
     std::vector<uint32_t> &idx;
@@ -164,7 +166,10 @@ struct Builder {
     }
 
     // cut [b,e) into <= 8 clusters: repeatedly split the largest-area cluster
-    // that holds more than LEAF_MAX triangles
+    // that holds more than LEAF_MAX triangles; with slots left over, keep
+    // splitting multi-triangle leaves (largest area first).  A node costs the
+    // same eight slab tests whatever its fill, while leaf triangles are the
+    // poorly-converged part of a wave's walk: full nodes, small leaves.
     int clusters(uint32_t b, uint32_t e, bool par, Cluster out[8]) {
         int n = 1;
         out[0] = Cluster{b, e, range_box(b, e, par)};
@@ -173,6 +178,9 @@ struct Builder {
             double best = -1.0;
             for (int i = 0; i < n; ++i)
                 if (out[i].count() > LEAF_MAX && out[i].box.area() > best) { best = out[i].box.area(); pick = i; }
+            if (pick < 0 && fill_leaves)
+                for (int i = 0; i < n; ++i)
+                    if (out[i].count() > 1 && out[i].box.area() > best) { best = out[i].box.area(); pick = i; }
             if (pick < 0) break;
             const Cluster c = out[pick];
             const bool p = par && c.count() > (1u << 18);
@@ -278,7 +286,7 @@ int build_wide_bvh(const chr_geometry_desc *d, WideBVH &out) {
     for (int64_t t = 0; t < (int64_t)ntri; ++t)
         for (int a = 0; a < 3; ++a) centroid[3 * t + a] = 0.5f * (tri_box[t].lo[a] + tri_box[t].hi[a]);
 
-    Builder B{tri_box, centroid, idx};
+    Builder B{!std::getenv("CHR_WIDE_NO_FILL"), tri_box, centroid, idx};
     out.nodes.clear();
     out.tri.clear();
     out.nodes.resize(1);

@@ -158,6 +158,8 @@ typedef struct chr_propagate_stats {
     uint64_t nodes_visited;     /* BVH nodes / triangles / walks: filled only by the counting */
     uint64_t triangles_tested;  /* kernel variant (CHR_PROPAGATE_VARIANT=5), zero otherwise */
     uint64_t traversals;
+    uint64_t wave_node_steps;     /* node / triangle steps executed per wave (SIMD efficiency = */
+    uint64_t wave_triangle_steps; /* nodes_visited / (64 * wave_node_steps)); counting variant only */
 } chr_propagate_stats;
 
 /* replaces: GPUPhotons.propagate host loop (chroma/gpu/photon.py:226-293) for

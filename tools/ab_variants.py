@@ -36,13 +36,14 @@ def main():
                                pol=ga.to_gpu(gpu.to_float3(photons.pol)), wavelengths=ga.to_gpu(photons.wavelengths),
                                t=ga.to_gpu(photons.t), flags=ga.to_gpu(photons.flags), evidx=ga.to_gpu(photons.evidx),
                                true_nphotons=args.photons)
-    variants = [int(v) for v in args.variants.split(',')]
+    variants = args.variants.split(',')   # "<n>" or "<n>:nosort" (CHR_SORT=0)
     times = {v: [] for v in variants}
     kms = {v: [] for v in variants}
     ref_flags = None
     for r in range(args.rounds + 1):
         for v in variants:
-            os.environ['CHR_PROPAGATE_VARIANT'] = str(v)
+            os.environ['CHR_PROPAGATE_VARIANT'] = v.split(':')[0]
+            os.environ['CHR_SORT'] = '0' if v.endswith(':nosort') else '1'
             rng = gpu.get_rng_states(512 * 1024, seed=1)
             gp = gpu.GPUPhotons(pristine, copy_flags=True, copy_triangles=False, copy_weights=False)
             torch.cuda.synchronize()
@@ -56,13 +57,24 @@ def main():
             else:
                 bad = (fl[0] != ref_flags[0]) | (fl[1] != ref_flags[1]) | (fl[2] != ref_flags[2]).any(axis=1)
                 if bad.any():
-                    print('VARIANT %d DIFFERS from variant %d on %d photons (first %s)' % (
+                    print('VARIANT %s DIFFERS from variant %s on %d photons (first %s)' % (
                         v, variants[0], int(bad.sum()), np.flatnonzero(bad)[:8]), flush=True)
+            st = gp.last_stats
+            if r == 0 and st.nodes_visited:
+                n = float(args.photons)
+                print('variant %s counters: nodes/photon %.2f tris/photon %.2f walks/photon %.3f  SIMD efficiency '
+                      'nodes %.3f tris %.3f  (wave node steps %d, wave tri steps %d)' % (
+                          v, st.nodes_visited / n, st.triangles_tested / n, st.traversals / n,
+                          st.nodes_visited / (64.0 * max(1, st.wave_node_steps)),
+                          st.triangles_tested / (64.0 * max(1, st.wave_triangle_steps)),
+                          st.wave_node_steps, st.wave_triangle_steps), flush=True)
             if r > 0:
                 times[v].append(dt)
                 kms[v].append(gp.last_stats.kernel_ms)
     for v in variants:
-        print('variant %d: wall %.1f ms (min %.1f)  kernel %.1f ms  -> %.1f Mphotons/s' % (
+        if not times[v]:
+            continue
+        print('variant %s: wall %.1f ms (min %.1f)  kernel %.1f ms  -> %.1f Mphotons/s' % (
             v, 1e3 * np.median(times[v]), 1e3 * min(times[v]), np.median(kms[v]),
             args.photons / np.median(times[v]) / 1e6), flush=True)
 

@@ -25,7 +25,7 @@ def per_kernel(d, counter):
                 vals[key] = vals.get(key, 0.0) + float(row['Counter_Value'])
     out = {}
     for (_, name), v in vals.items():
-        short = name.split('(')[0]
+        short = 'chr::propagate_kernel' if 'propagate_kernel' in name else name.split('(')[0]
         out.setdefault(short, []).append(v)
     return out
 
