@@ -274,17 +274,15 @@ __device__ __forceinline__ int intersect_mesh(const DevGeom &g, V3 o, V3 d, floa
 // first, the others pushed and culled at pop against the running best.
 constexpr int WIDE_LDS = 16;
 
-// NB: measured (profiles/r01/ab_stack_layout.log): keeping the LDS column
-// pointers generic and the spill array in the same object (flat stack ops)
-// runs the walk 1.4x faster than typed LDS pointers with ds_* ops -- the
-// typed form changes how the walk's control flow is structurised and the
-// wave executes ~1.8x more VALU instructions for the same per-lane work.
+// The LDS column pointers are typed (ds_* ops) and the scratch spill array is
+// a separate object: an object holding both lives in scratch and its LDS
+// pointers degrade to flat ops behind a scratch load (measured r01: the
+// scheduled walk runs 1.14x faster this way).
 struct WStack {
-    uint32_t *node;     // this work-item's LDS column: entry i at node[i * BLOCK]
-    float *dist;
-    uint2 spill[WIDE_STACK - WIDE_LDS];
+    CHR_LDS uint32_t *node;   // this work-item's LDS column: entry i at node[i * BLOCK]
+    CHR_LDS float *dist;
+    uint2 *spill;             // entries >= WIDE_LDS (scratch)
 };
-
 __device__ __forceinline__ void wpush(WStack &s, int i, uint32_t n, float t) {
     if (i < WIDE_LDS) { s.node[i * BLOCK] = n; s.dist[i * BLOCK] = t; }
     else s.spill[i - WIDE_LDS] = make_uint2(n, __float_as_uint(t));
@@ -299,6 +297,76 @@ __device__ __forceinline__ float byte_f(uint32_t lo4, uint32_t hi4, int k) {   /
     return (float)((w >> (8 * (k & 3))) & 0xFFu);
 }
 __device__ __forceinline__ float exp_scale(uint32_t e) { return __uint_as_float((e & 0xFFu) << 23); }
+
+// Per-ray constants of the branch-free slab test used on wide nodes.  For an
+// axis with finite 1/d the near/far plane distances are fmaf(x, inv, noid) --
+// the reference's own expression (intersect_box, intersect.h:113-157), and
+// since fmaf is monotone in x, selecting the near/far bound by the sign of
+// inv gives exactly the min/max the reference takes.  An axis with
+// non-finite 1/d is skipped by the reference; here it yields [-inf, +inf]
+// (inv 0, offsets -inf/+inf), which leaves tmin/tmax unchanged the same way.
+struct RaySlab {
+    float inx, iny, inz;        // multipliers (inv or 0)
+    float onx, ony, onz;        // near offsets (noid or -inf)
+    float ofx, ofy, ofz;        // far offsets (noid or +inf)
+    bool negx, negy, negz;      // inv < 0: the near plane is the box's hi face
+};
+__device__ __forceinline__ RaySlab make_slab(V3 noid, V3 inv) {
+    RaySlab r;
+    const float inf = __builtin_inff();
+    const bool fx = chr_isfinite(inv.x), fy = chr_isfinite(inv.y), fz = chr_isfinite(inv.z);
+    r.inx = fx ? inv.x : 0.0f; r.onx = fx ? noid.x : -inf; r.ofx = fx ? noid.x : inf;
+    r.iny = fy ? inv.y : 0.0f; r.ony = fy ? noid.y : -inf; r.ofy = fy ? noid.y : inf;
+    r.inz = fz ? inv.z : 0.0f; r.onz = fz ? noid.z : -inf; r.ofz = fz ? noid.z : inf;
+    r.negx = inv.x < 0.0f; r.negy = inv.y < 0.0f; r.negz = inv.z < 0.0f;
+    return r;
+}
+
+// Slab-test the up-to-8 children of one wide node.  Returns the leaf children
+// hit (bit mask), leaves the nearest hit inner child in near_node/near_t and
+// pushes the other hit inner children.  Boxes entered beyond `best` are culled
+// (strict '>', mesh.h:94-96).
+__device__ __forceinline__ uint32_t expand_node(const uint4 h, const uint4 a1, const uint4 a2, const uint4 a3,
+                                                const uint4 a4, const uint4 a5, const RaySlab &r, float best,
+                                                uint32_t &near_node, float &near_t, WStack &st, int &sp,
+                                                uint32_t &overflow) {
+    const V3 org = v3(__uint_as_float(h.x), __uint_as_float(h.y), __uint_as_float(h.z));
+    const float sx = exp_scale(h.w), sy = exp_scale(h.w >> 8), sz = exp_scale(h.w >> 16);
+    // byte arrays: x lo = a1.xy, y lo = a1.zw, z lo = a2.xy, x hi = a2.zw, y hi = a3.xy, z hi = a3.zw
+    const uint32_t nx0 = r.negx ? a2.z : a1.x, nx1 = r.negx ? a2.w : a1.y;
+    const uint32_t fx0 = r.negx ? a1.x : a2.z, fx1 = r.negx ? a1.y : a2.w;
+    const uint32_t ny0 = r.negy ? a3.x : a1.z, ny1 = r.negy ? a3.y : a1.w;
+    const uint32_t fy0 = r.negy ? a1.z : a3.x, fy1 = r.negy ? a1.w : a3.y;
+    const uint32_t nz0 = r.negz ? a3.z : a2.x, nz1 = r.negz ? a3.w : a2.y;
+    const uint32_t fz0 = r.negz ? a2.x : a3.z, fz1 = r.negz ? a2.y : a3.w;
+    uint32_t leaf_mask = 0;
+    near_node = 0xFFFFFFFFu;
+    near_t = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const uint32_t kind = ((k < 4 ? a4.z : a4.w) >> (8 * (k & 3))) & 0xFFu;
+        if (kind == 0) continue;
+        const float tnx = __builtin_fmaf(__builtin_fmaf(byte_f(nx0, nx1, k), sx, org.x), r.inx, r.onx);
+        const float tfx = __builtin_fmaf(__builtin_fmaf(byte_f(fx0, fx1, k), sx, org.x), r.inx, r.ofx);
+        const float tny = __builtin_fmaf(__builtin_fmaf(byte_f(ny0, ny1, k), sy, org.y), r.iny, r.ony);
+        const float tfy = __builtin_fmaf(__builtin_fmaf(byte_f(fy0, fy1, k), sy, org.y), r.iny, r.ofy);
+        const float tnz = __builtin_fmaf(__builtin_fmaf(byte_f(nz0, nz1, k), sz, org.z), r.inz, r.onz);
+        const float tfz = __builtin_fmaf(__builtin_fmaf(byte_f(fz0, fz1, k), sz, org.z), r.inz, r.ofz);
+        const float tmin = __builtin_fmaxf(__builtin_fmaxf(__builtin_fmaxf(tnx, tny), tnz), 0.0f);
+        const float tmax = __builtin_fminf(__builtin_fminf(tfx, tfy), tfz);
+        if (tmin > tmax || tmin > best) continue;
+        if (kind != WIDE_INNER) { leaf_mask |= 1u << k; continue; }
+        const uint32_t child = a4.x + (((k < 4 ? a5.x : a5.y) >> (8 * (k & 3))) & 0xFFu);
+        if (near_node == 0xFFFFFFFFu) { near_node = child; near_t = tmin; continue; }
+        uint32_t pn = child;
+        float pt = tmin;
+        if (tmin < near_t) { pn = near_node; pt = near_t; near_node = child; near_t = tmin; }
+        if (sp >= WIDE_STACK) { overflow++; break; }
+        wpush(st, sp, pn, pt);
+        sp++;
+    }
+    return leaf_mask;
+}
 
 struct WalkCounts {   // filled only by the counting variant (bench: algorithmic bytes per photon)
     uint32_t nodes, tris, walks;
@@ -315,6 +383,7 @@ __device__ int intersect_wide(const DevGeom &g, V3 o, V3 d, float &min_distance,
     if constexpr (COUNT) cnt.walks++;
     const V3 noid = v3(-o.x / d.x, -o.y / d.y, -o.z / d.z);
     const V3 inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    const RaySlab slab = make_slab(noid, inv);
     float best = __builtin_inff();
     uint32_t best_rank = 0xFFFFFFFFu;
     int best_id = -1;
@@ -326,32 +395,9 @@ __device__ int intersect_wide(const DevGeom &g, V3 o, V3 d, float &min_distance,
         const uint4 *np = g.wnodes + 6 * (size_t)node;
         const uint4 h = gld(np), a1 = gld(np + 1), a2 = gld(np + 2), a3 = gld(np + 3), a4 = gld(np + 4),
                     a5 = gld(np + 5);
-        const V3 org = v3(__uint_as_float(h.x), __uint_as_float(h.y), __uint_as_float(h.z));
-        const float sx = exp_scale(h.w), sy = exp_scale(h.w >> 8), sz = exp_scale(h.w >> 16);
-        uint32_t leaf_mask = 0;
-        uint32_t near_node = 0xFFFFFFFFu;
-        float near_t = 0.0f;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const uint32_t kind = ((k < 4 ? a4.z : a4.w) >> (8 * (k & 3))) & 0xFFu;
-            if (kind == 0) continue;
-            const V3 lo = v3(__builtin_fmaf(byte_f(a1.x, a1.y, k), sx, org.x), __builtin_fmaf(byte_f(a1.z, a1.w, k), sy, org.y),
-                             __builtin_fmaf(byte_f(a2.x, a2.y, k), sz, org.z));
-            const V3 hi = v3(__builtin_fmaf(byte_f(a2.z, a2.w, k), sx, org.x), __builtin_fmaf(byte_f(a3.x, a3.y, k), sy, org.y),
-                             __builtin_fmaf(byte_f(a3.z, a3.w, k), sz, org.z));
-            float bd;
-            if (!intersect_box(noid, inv, lo, hi, bd) || bd > best) continue;
-            if (kind != WIDE_INNER) { leaf_mask |= 1u << k; continue; }
-            const uint32_t child = a4.x + (((k < 4 ? a5.x : a5.y) >> (8 * (k & 3))) & 0xFFu);
-            if (near_node == 0xFFFFFFFFu) { near_node = child; near_t = bd; continue; }
-            // keep the nearer one in hand, push the other
-            uint32_t pn = child;
-            float pt = bd;
-            if (bd < near_t) { pn = near_node; pt = near_t; near_node = child; near_t = bd; }
-            if (sp >= WIDE_STACK) { overflow++; break; }
-            wpush(st, sp, pn, pt);
-            sp++;
-        }
+        uint32_t near_node;
+        float near_t;
+        uint32_t leaf_mask = expand_node(h, a1, a2, a3, a4, a5, slab, best, near_node, near_t, st, sp, overflow);
         const unsigned long long kinds = ((unsigned long long)a4.w << 32) | a4.z;
         const unsigned long long offs = ((unsigned long long)a5.y << 32) | a5.x;
         while (leaf_mask) {
@@ -416,6 +462,7 @@ __device__ int intersect_wide_sched(const DevGeom &g, V3 o, V3 d, float &min_dis
     if constexpr (COUNT) cnt.walks++;
     const V3 noid = v3(-o.x / d.x, -o.y / d.y, -o.z / d.z);
     const V3 inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    const RaySlab slab = make_slab(noid, inv);
     float best = __builtin_inff();
     uint32_t best_rank = 0xFFFFFFFFu;
     int best_id = -1;
@@ -433,7 +480,9 @@ __device__ int intersect_wide_sched(const DevGeom &g, V3 o, V3 d, float &min_dis
         const unsigned long long mw = __ballot(can_walk);
         const unsigned long long mt = __ballot(has_work);
         if ((mw | mt) == 0) break;
-        if (mw != 0 && __popcll(mt) < TRI_BATCH) {
+        // TRI_BATCH == 0: no wave-level choice -- every iteration each lane
+        // does whichever step it has (parked triangle first)
+        if (TRI_BATCH == 0 ? can_walk : (mw != 0 && __popcll(mt) < TRI_BATCH)) {
             // ------------------------------------------------ node step
             if (!can_walk) continue;
             if (node == INVALID) {
@@ -450,33 +499,10 @@ __device__ int intersect_wide_sched(const DevGeom &g, V3 o, V3 d, float &min_dis
             const uint4 *np = g.wnodes + 6 * (size_t)node;
             const uint4 h = gld(np), a1 = gld(np + 1), a2 = gld(np + 2), a3 = gld(np + 3), a4 = gld(np + 4),
                         a5 = gld(np + 5);
-            const V3 org = v3(__uint_as_float(h.x), __uint_as_float(h.y), __uint_as_float(h.z));
-            const float sx = exp_scale(h.w), sy = exp_scale(h.w >> 8), sz = exp_scale(h.w >> 16);
-            uint32_t leaf_mask = 0;
-            uint32_t near_node = INVALID;
-            float near_t = 0.0f;
-#pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                const uint32_t kind = ((k < 4 ? a4.z : a4.w) >> (8 * (k & 3))) & 0xFFu;
-                if (kind == 0) continue;
-                const V3 lo = v3(__builtin_fmaf(byte_f(a1.x, a1.y, k), sx, org.x),
-                                 __builtin_fmaf(byte_f(a1.z, a1.w, k), sy, org.y),
-                                 __builtin_fmaf(byte_f(a2.x, a2.y, k), sz, org.z));
-                const V3 hi = v3(__builtin_fmaf(byte_f(a2.z, a2.w, k), sx, org.x),
-                                 __builtin_fmaf(byte_f(a3.x, a3.y, k), sy, org.y),
-                                 __builtin_fmaf(byte_f(a3.z, a3.w, k), sz, org.z));
-                float bd;
-                if (!intersect_box(noid, inv, lo, hi, bd) || bd > best) continue;
-                if (kind != WIDE_INNER) { leaf_mask |= 1u << k; continue; }
-                const uint32_t child = a4.x + (((k < 4 ? a5.x : a5.y) >> (8 * (k & 3))) & 0xFFu);
-                if (near_node == INVALID) { near_node = child; near_t = bd; continue; }
-                uint32_t pn = child;
-                float pt = bd;
-                if (bd < near_t) { pn = near_node; pt = near_t; near_node = child; near_t = bd; }
-                if (sp >= WIDE_STACK) { overflow++; break; }
-                wpush(st, sp, pn, pt);
-                sp++;
-            }
+            uint32_t near_node;
+            float near_t;
+            const uint32_t leaf_mask =
+                expand_node(h, a1, a2, a3, a4, a5, slab, best, near_node, near_t, st, sp, overflow);
             node = near_node;
             if (leaf_mask) {
                 pkinds = ((unsigned long long)a4.w << 32) | a4.z;
@@ -634,8 +660,9 @@ __device__ __forceinline__ void fill_state(const DevGeom &g, State &s, Photon &p
     int mesh_triangle;
     if constexpr (WIDE == 1)
         mesh_triangle = intersect_wide<COUNT>(g, p.pos, p.dir, s.distance, p.last_hit, wst, overflow, cnt);
-    else if constexpr (WIDE >= 2)   // scheduled walk, WIDE = triangle batch threshold
-        mesh_triangle = intersect_wide_sched<COUNT, WIDE>(g, p.pos, p.dir, s.distance, p.last_hit, wst, overflow, cnt);
+    else if constexpr (WIDE >= 1000)   // scheduled walk, triangle batch threshold WIDE - 1000
+        mesh_triangle =
+            intersect_wide_sched<COUNT, WIDE - 1000>(g, p.pos, p.dir, s.distance, p.last_hit, wst, overflow, cnt);
     else mesh_triangle = intersect_mesh<BATCH>(g, p.pos, p.dir, s.distance, p.last_hit, st, overflow);
     int m1, m2;
     bool use_analytic = false;
@@ -1123,7 +1150,7 @@ __device__ __forceinline__ void store3(float *p, uint32_t i, V3 v) { p[3 * i] = 
 // propagate.cu:254-366.  BATCH: children fetched together per group;
 // MINW: minimum waves per SIMD requested from the register allocator.
 // WIDE: 0 exact-order walk of the reference BVH, 1 wide BVH node loop,
-// >= 2 wide BVH scheduled walk with that triangle batch threshold.
+// 1000 + b: wide BVH scheduled walk, triangle batch threshold b (0: per-lane choice).
 template <int BATCH, int MINW, int WIDE, bool COUNT = false>
 __global__ __launch_bounds__(BLOCK, MINW) void propagate_kernel(const DevGeom *__restrict__ gdev, PropagateArgs a) {
     __shared__ uint32_t lds_stack[WIDE ? 2 * WIDE_LDS * BLOCK : STACK_LDS * BLOCK];
@@ -1154,8 +1181,10 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_kernel(const DevGeom *_
             Stack st;
             WStack wst;
             st.lds = (CHR_LDS uint32_t *)(lds_stack + threadIdx.x);
-            wst.node = lds_stack + threadIdx.x;
-            wst.dist = reinterpret_cast<float *>(lds_stack) + WIDE_LDS * BLOCK + threadIdx.x;
+            uint2 wspill[WIDE_STACK - WIDE_LDS];
+            wst.spill = wspill;
+            wst.node = (CHR_LDS uint32_t *)(lds_stack + threadIdx.x);
+            wst.dist = (CHR_LDS float *)(lds_stack + WIDE_LDS * BLOCK + threadIdx.x);
             uint32_t overflow = 0;
             WalkCounts cnt{0u, 0u, 0u, 0u, 0u};
             State s;
@@ -1398,10 +1427,12 @@ __global__ __launch_bounds__(BLOCK) void distance_kernel(const DevGeom *__restri
     int tri;
     if constexpr (WIDE) {
         WStack st;
-        st.node = lds_stack + threadIdx.x;
-        st.dist = reinterpret_cast<float *>(lds_stack) + WIDE_LDS * BLOCK + threadIdx.x;
+        uint2 wspill[WIDE_STACK - WIDE_LDS];
+        st.spill = wspill;
+        st.node = (CHR_LDS uint32_t *)(lds_stack + threadIdx.x);
+        st.dist = (CHR_LDS float *)(lds_stack + WIDE_LDS * BLOCK + threadIdx.x);
         WalkCounts cnt;
-        tri = intersect_wide_sched<false, 32>(g, o, d, dist, -1, st, overflow, cnt);
+        tri = intersect_wide_sched<false, 2>(g, o, d, dist, -1, st, overflow, cnt);
     } else {
         Stack st;
         st.lds = (CHR_LDS uint32_t *)(lds_stack + threadIdx.x);
@@ -1519,14 +1550,16 @@ typedef void (*propagate_fn)(const DevGeom *, PropagateArgs);
 // measured on demo.detector(), 4M photons (profiles/r01/ab_variants.log):
 // <1,3> 89.2 ms, <4,3> 74.9, <4,4> 66.8, <4,5> 66.5, <8,4> 64.3, <8,3> 74.1, <2,3> 76.5
 static const propagate_fn kVariants[] = {
-    propagate_kernel<8, 4, 32>,          // 0: default -- 8-wide SAH BVH, wave-scheduled node/triangle steps
+    propagate_kernel<8, 4, 1002>,        // 0: default -- 8-wide SAH BVH, wave-scheduled steps, triangle batch 2
     propagate_kernel<8, 4, 0>,           // 1: exact-order walk of the reference BVH, 8 children in flight
-    propagate_kernel<8, 4, 1>,           // 2: 8-wide BVH, triangles tested inside the node step
-    propagate_kernel<8, 4, 16>,          // 3: scheduled, triangle batch 16
-    propagate_kernel<8, 4, 48>,          // 4: scheduled, triangle batch 48
-    propagate_kernel<8, 4, 32, true>,    // 5: default + node/triangle counters (bench's byte count)
-    propagate_kernel<8, 3, 32>,          // 6: default at 3 waves/SIMD
-    propagate_kernel<8, 4, 1, true>,     // 7: variant 2 + counters
+    propagate_kernel<8, 4, 1>,           // 2: 8-wide BVH, leaf triangles tested inside the node step
+    propagate_kernel<8, 4, 1001>,        // 3: scheduled, triangle batch 1
+    propagate_kernel<8, 4, 1004>,        // 4: scheduled, triangle batch 4
+    propagate_kernel<8, 4, 1002, true>,  // 5: default + node/triangle counters (bench's byte count)
+    propagate_kernel<8, 4, 1008>,        // 6: scheduled, triangle batch 8
+    propagate_kernel<8, 4, 1000>,        // 7: scheduled, per-lane choice
+    propagate_kernel<8, 3, 1002>,        // 8: default at 3 waves/SIMD
+    propagate_kernel<8, 5, 1002>,        // 9: default at 5 waves/SIMD
 };
 static constexpr int kExactVariant = 1;
 static propagate_fn select_variant(const chr_geometry *g) {
@@ -1539,8 +1572,10 @@ static propagate_fn select_variant(const chr_geometry *g) {
 
 static constexpr int32_t kSortMin = 16384;   // below this a launch is a few waves: no reordering
 static bool sort_enabled() {
-    const char *e = getenv("CHR_SORT");   // read per launch (A/B); default on
-    return !(e && e[0] == '0');
+    // read per launch (A/B).  Default off: on demo.detector() the reordered
+    // walk was not faster and the sort costs ~3 ms per 4M photons (r01 A/B).
+    const char *e = getenv("CHR_SORT");
+    return e && e[0] == '1';
 }
 
 // scratch layout (u32 words): [0] overflows [1] queue base [2..11] u64 walk counters [12..15] pad; masks (u64, 8-aligned); offsets

@@ -36,14 +36,14 @@ def main():
                                pol=ga.to_gpu(gpu.to_float3(photons.pol)), wavelengths=ga.to_gpu(photons.wavelengths),
                                t=ga.to_gpu(photons.t), flags=ga.to_gpu(photons.flags), evidx=ga.to_gpu(photons.evidx),
                                true_nphotons=args.photons)
-    variants = args.variants.split(',')   # "<n>" or "<n>:nosort" (CHR_SORT=0)
+    variants = args.variants.split(',')   # "<n>" or "<n>:sort" (CHR_SORT=1)
     times = {v: [] for v in variants}
     kms = {v: [] for v in variants}
     ref_flags = None
     for r in range(args.rounds + 1):
         for v in variants:
             os.environ['CHR_PROPAGATE_VARIANT'] = v.split(':')[0]
-            os.environ['CHR_SORT'] = '0' if v.endswith(':nosort') else '1'
+            os.environ['CHR_SORT'] = '1' if v.endswith(':sort') else '0'
             rng = gpu.get_rng_states(512 * 1024, seed=1)
             gp = gpu.GPUPhotons(pristine, copy_flags=True, copy_triangles=False, copy_weights=False)
             torch.cuda.synchronize()
