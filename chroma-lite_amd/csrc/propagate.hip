@@ -1147,7 +1147,82 @@ struct PropagateArgs {
 __device__ __forceinline__ V3 load3(const float *p, uint32_t i) { return v3(p[3 * i], p[3 * i + 1], p[3 * i + 2]); }
 __device__ __forceinline__ void store3(float *p, uint32_t i, V3 v) { p[3 * i] = v.x; p[3 * i + 1] = v.y; p[3 * i + 2] = v.z; }
 
-// propagate.cu:254-366.  BATCH: children fetched together per group;
+// One live photon through the step loop of propagate.cu:279-341 (the caller
+// has checked the entry history against DEAD_MASK, propagate.cu:283-284) and
+// its write-back (propagate.cu:343-353).  Returns whether it is still alive.
+template <int BATCH, int WIDE, bool COUNT>
+__device__ __forceinline__ bool run_photon(const DevGeom &g, const PropagateArgs &a, uint32_t photon_id,
+                                           uint32_t history, chr_xorwow &rng, Stack st, WStack &wst,
+                                           uint32_t &overflow, WalkCounts &cnt) {
+    Photon p;
+    p.history = history;
+    p.pos = load3(a.pos, photon_id);
+    p.dir = load3(a.dir, photon_id);
+    p.dir = p.dir / norm(p.dir);
+    p.pol = load3(a.pol, photon_id);
+    p.pol = p.pol / norm(p.pol);
+    p.wavelength = a.wl[photon_id];
+    p.time = a.t[photon_id];
+    p.last_hit = a.last_hit[photon_id];
+    p.weight = a.weights[photon_id];
+    State s;
+    int scatter_first = a.scatter_first;
+    int steps = 0;
+    while (steps < a.max_steps) {
+        steps++;
+        const float prod = ((((p.dir.x * p.dir.y) * p.dir.z) * p.pos.x) * p.pos.y) * p.pos.z;
+        if (chr_isnan(prod)) { p.history |= CHR_NO_HIT | CHR_NAN_ABORT; break; }
+        fill_state<BATCH, WIDE, COUNT>(g, s, p, st, wst, overflow, cnt);
+        if (p.last_hit == -1) break;
+        int command = propagate_to_boundary(g, p, s, rng, a.use_weights, scatter_first);
+        scatter_first = 0;
+        if (command == BREAK) break;
+        if (command == CONTINUE) continue;
+        if (s.surface_index != -1) {
+            command = propagate_at_surface(g, p, s, rng, a.use_weights);
+            if (command == BREAK) break;
+            if (command == CONTINUE) continue;
+        }
+        propagate_at_boundary(p, s, rng);
+    }
+    store3(a.pos, photon_id, p.pos);
+    store3(a.dir, photon_id, p.dir);
+    store3(a.pol, photon_id, p.pol);
+    a.wl[photon_id] = p.wavelength;
+    a.t[photon_id] = p.time;
+    a.flags[photon_id] = p.history;
+    a.last_hit[photon_id] = p.last_hit;
+    a.weights[photon_id] = p.weight;
+    return (p.history & DEAD_MASK) == 0;
+}
+
+__device__ __forceinline__ void load_rng(const PropagateArgs &a, uint32_t slot, chr_xorwow &rng) {
+    const uint32_t ns = a.nslots;
+    rng.d = a.rng[slot]; rng.v0 = a.rng[ns + slot]; rng.v1 = a.rng[2 * ns + slot];
+    rng.v2 = a.rng[3 * ns + slot]; rng.v3 = a.rng[4 * ns + slot]; rng.v4 = a.rng[5 * ns + slot];
+}
+__device__ __forceinline__ void store_rng(const PropagateArgs &a, uint32_t slot, const chr_xorwow &rng) {
+    const uint32_t ns = a.nslots;
+    a.rng[slot] = rng.d; a.rng[ns + slot] = rng.v0; a.rng[2 * ns + slot] = rng.v1;
+    a.rng[3 * ns + slot] = rng.v2; a.rng[4 * ns + slot] = rng.v3; a.rng[5 * ns + slot] = rng.v4;
+}
+
+template <bool COUNT>
+__device__ __forceinline__ void flush_counters(const PropagateArgs &a, uint32_t overflow, const WalkCounts &cnt) {
+    if (overflow) atomicAdd(a.counters, overflow);
+    if constexpr (COUNT) {
+        unsigned long long *c64 = reinterpret_cast<unsigned long long *>(a.counters + 2);
+        atomicAdd(c64, (unsigned long long)cnt.nodes);
+        atomicAdd(c64 + 1, (unsigned long long)cnt.tris);
+        atomicAdd(c64 + 2, (unsigned long long)cnt.walks);
+        atomicAdd(c64 + 3, (unsigned long long)cnt.wave_nodes);
+        atomicAdd(c64 + 4, (unsigned long long)cnt.wave_tris);
+    }
+}
+
+// propagate.cu:254-366, one chunk per launch (the reference's launch
+// structure; used when the slot count is not a multiple of 64).
+// BATCH: children fetched together per group (exact-order walk);
 // MINW: minimum waves per SIMD requested from the register allocator.
 // WIDE: 0 exact-order walk of the reference BVH, 1 wide BVH node loop,
 // 1000 + b: wide BVH scheduled walk, triangle batch threshold b (0: per-lane choice).
@@ -1162,22 +1237,10 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_kernel(const DevGeom *_
     const int id = (a.order && tid < a.nthreads) ? (int)a.order[tid] : tid;
     if (tid < a.nthreads) {
         const uint32_t photon_id = a.input_queue[a.first + id];
-        Photon p;
-        p.history = a.flags[photon_id] & 0xFFFFu;   // unsigned short on the device (photon.h:29)
-        if (!(p.history & DEAD_MASK)) {
+        const uint32_t history = a.flags[photon_id] & 0xFFFFu;   // unsigned short on the device (photon.h:29)
+        if (!(history & DEAD_MASK)) {
             chr_xorwow rng;
-            const uint32_t ns = a.nslots;
-            rng.d = a.rng[id]; rng.v0 = a.rng[ns + id]; rng.v1 = a.rng[2 * ns + id];
-            rng.v2 = a.rng[3 * ns + id]; rng.v3 = a.rng[4 * ns + id]; rng.v4 = a.rng[5 * ns + id];
-            p.pos = load3(a.pos, photon_id);
-            p.dir = load3(a.dir, photon_id);
-            p.dir = p.dir / norm(p.dir);
-            p.pol = load3(a.pol, photon_id);
-            p.pol = p.pol / norm(p.pol);
-            p.wavelength = a.wl[photon_id];
-            p.time = a.t[photon_id];
-            p.last_hit = a.last_hit[photon_id];
-            p.weight = a.weights[photon_id];
+            load_rng(a, (uint32_t)id, rng);
             Stack st;
             WStack wst;
             st.lds = (CHR_LDS uint32_t *)(lds_stack + threadIdx.x);
@@ -1187,47 +1250,10 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_kernel(const DevGeom *_
             wst.dist = (CHR_LDS float *)(lds_stack + WIDE_LDS * BLOCK + threadIdx.x);
             uint32_t overflow = 0;
             WalkCounts cnt{0u, 0u, 0u, 0u, 0u};
-            State s;
-            int scatter_first = a.scatter_first;
             const DevGeom &g = *gdev;   // device-resident: uniform s_loads, no private copy
-            int steps = 0;
-            while (steps < a.max_steps) {
-                steps++;
-                const float prod = ((((p.dir.x * p.dir.y) * p.dir.z) * p.pos.x) * p.pos.y) * p.pos.z;
-                if (chr_isnan(prod)) { p.history |= CHR_NO_HIT | CHR_NAN_ABORT; break; }
-                fill_state<BATCH, WIDE, COUNT>(g, s, p, st, wst, overflow, cnt);
-                if (p.last_hit == -1) break;
-                int command = propagate_to_boundary(g, p, s, rng, a.use_weights, scatter_first);
-                scatter_first = 0;
-                if (command == BREAK) break;
-                if (command == CONTINUE) continue;
-                if (s.surface_index != -1) {
-                    command = propagate_at_surface(g, p, s, rng, a.use_weights);
-                    if (command == BREAK) break;
-                    if (command == CONTINUE) continue;
-                }
-                propagate_at_boundary(p, s, rng);
-            }
-            a.rng[id] = rng.d; a.rng[ns + id] = rng.v0; a.rng[2 * ns + id] = rng.v1;
-            a.rng[3 * ns + id] = rng.v2; a.rng[4 * ns + id] = rng.v3; a.rng[5 * ns + id] = rng.v4;
-            store3(a.pos, photon_id, p.pos);
-            store3(a.dir, photon_id, p.dir);
-            store3(a.pol, photon_id, p.pol);
-            a.wl[photon_id] = p.wavelength;
-            a.t[photon_id] = p.time;
-            a.flags[photon_id] = p.history;
-            a.last_hit[photon_id] = p.last_hit;
-            a.weights[photon_id] = p.weight;
-            alive = (p.history & DEAD_MASK) == 0;
-            if (overflow) atomicAdd(a.counters, overflow);
-            if constexpr (COUNT) {
-                unsigned long long *c64 = reinterpret_cast<unsigned long long *>(a.counters + 2);
-                atomicAdd(c64, (unsigned long long)cnt.nodes);
-                atomicAdd(c64 + 1, (unsigned long long)cnt.tris);
-                atomicAdd(c64 + 2, (unsigned long long)cnt.walks);
-                atomicAdd(c64 + 3, (unsigned long long)cnt.wave_nodes);
-                atomicAdd(c64 + 4, (unsigned long long)cnt.wave_tris);
-            }
+            alive = run_photon<BATCH, WIDE, COUNT>(g, a, photon_id, history, rng, st, wst, overflow, cnt);
+            store_rng(a, (uint32_t)id, rng);
+            flush_counters<COUNT>(a, overflow, cnt);
         }
     }
     if (a.order) {   // masks zeroed by the host; bit per slot
@@ -1236,6 +1262,56 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_kernel(const DevGeom *_
     }
     const unsigned long long mask = __ballot(alive);
     if ((threadIdx.x & 63) == 0 && id < a.nthreads) a.alive_masks[id >> 6] = mask;
+}
+
+// One whole host step in ONE launch (default).  The reference launches the
+// queue in chunks of cap = nthreads_per_block*max_blocks photons, one after
+// the other, and the photon at queue position q uses RNG slot q mod cap
+// (photon.py:266-276, chunk_iterator).  Here work-item `slot` runs queue
+// positions slot, slot+cap, slot+2cap, ... in that order with the slot's RNG
+// state held in registers: the same photons meet the same states in the same
+// order as in the chunked launches, so every result is identical -- but there
+// is one launch (and one grid drain) per step instead of ceil(n/cap), and each
+// lane's work is a sum over ~n/cap photons, which evens out the lanes of a wave.
+// Alive bits are per queue position (a.alive_masks[q >> 6]); requires
+// cap % 64 == 0 so that a wave's 64 positions share one mask word.
+template <int BATCH, int MINW, int WIDE, bool COUNT = false>
+__global__ __launch_bounds__(BLOCK, MINW) void propagate_step_kernel(const DevGeom *__restrict__ gdev,
+                                                                     PropagateArgs a, uint32_t cap) {
+    __shared__ uint32_t lds_stack[WIDE ? 2 * WIDE_LDS * BLOCK : STACK_LDS * BLOCK];
+    const uint32_t slot = blockIdx.x * BLOCK + threadIdx.x;
+    const uint32_t n = (uint32_t)a.nthreads;   // queue length of this step
+    // whole waves only (cap % 64 == 0); the partial last wave of a short queue
+    // stays to write its mask word
+    if (slot >= cap || (slot & ~63u) >= n) return;
+    Stack st;
+    WStack wst;
+    st.lds = (CHR_LDS uint32_t *)(lds_stack + threadIdx.x);
+    uint2 wspill[WIDE_STACK - WIDE_LDS];
+    wst.spill = wspill;
+    wst.node = (CHR_LDS uint32_t *)(lds_stack + threadIdx.x);
+    wst.dist = (CHR_LDS float *)(lds_stack + WIDE_LDS * BLOCK + threadIdx.x);
+    uint32_t overflow = 0;
+    WalkCounts cnt{0u, 0u, 0u, 0u, 0u};
+    const DevGeom &g = *gdev;
+    chr_xorwow rng;
+    bool have_rng = false;
+    for (uint32_t q = slot & ~63u; q < n; q += cap) {   // wave-uniform trip count
+        const uint32_t pos = q + (slot & 63u);
+        bool alive = false;
+        if (pos < n) {
+            const uint32_t photon_id = a.input_queue[pos];
+            const uint32_t history = a.flags[photon_id] & 0xFFFFu;   // photon.h:29
+            if (!(history & DEAD_MASK)) {
+                if (!have_rng) { load_rng(a, slot, rng); have_rng = true; }
+                alive = run_photon<BATCH, WIDE, COUNT>(g, a, photon_id, history, rng, st, wst, overflow, cnt);
+            }
+        }
+        const unsigned long long mask = __ballot(alive);
+        if ((slot & 63u) == 0) a.alive_masks[q >> 6] = mask;
+    }
+    if (have_rng) store_rng(a, slot, rng);
+    flush_counters<COUNT>(a, overflow, cnt);
 }
 
 // Coherence key of a queued photon: 18-bit Morton code of its position in the
@@ -1324,6 +1400,16 @@ __global__ __launch_bounds__(BLOCK) void scatter_queue_kernel(const unsigned lon
         const uint32_t rank = __popcll(m & ((1ull << lane) - 1ull));
         out_queue[base[0] + word_offsets[id >> 6] + rank] = in_queue[first + id];
     }
+}
+
+// photon.py:242-250: input queue entries (from q0[1]) = photon ids with the
+// ncopies clones of a photon interleaved; q0[0] = 0, q1[0] = 1 (count + 1)
+__global__ __launch_bounds__(BLOCK) void init_queue_kernel(uint32_t *q0, uint32_t *q1, uint32_t n, uint32_t true_n,
+                                                           uint32_t ncopies) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n) return;
+    q0[1 + i] = i / ncopies + (i % ncopies) * true_n;
+    if (i == 0) { q0[0] = 0u; q1[0] = 1u; }
 }
 
 // ---------------------------------------------------------------- RNG init
@@ -1570,6 +1656,20 @@ static propagate_fn select_variant(const chr_geometry *g) {
     return kVariants[v];
 }
 
+typedef void (*propagate_step_fn)(const DevGeom *, PropagateArgs, uint32_t);
+static propagate_step_fn select_step_variant(const chr_geometry *g) {
+    const char *e = getenv("CHR_PROPAGATE_VARIANT");
+    int v = e ? atoi(e) : 0;
+    if (g->dev.nwnodes == 0) v = kExactVariant;
+    switch (v) {
+        case 1: return propagate_step_kernel<8, 4, 0>;
+        case 5: return propagate_step_kernel<8, 4, 1002, true>;
+        case 8: return propagate_step_kernel<8, 3, 1002>;
+        case 9: return propagate_step_kernel<8, 5, 1002>;
+        default: return propagate_step_kernel<8, 4, 1002>;
+    }
+}
+
 static constexpr int32_t kSortMin = 16384;   // below this a launch is a few waves: no reordering
 static bool sort_enabled() {
     // read per launch (A/B).  Default off: on demo.detector() the reordered
@@ -1622,6 +1722,37 @@ static int launch_chunk(const chr_geometry *g, const chr_photons *ph, uint32_t *
     return CHR_OK;
 }
 
+// one host step as one launch of propagate_step_kernel over the n queued
+// photons (slot = queue position mod cap); same scratch layout as launch_chunk
+// with mask words per queue position.
+static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *rng, uint32_t nslots, uint32_t cap,
+                       uint32_t n, const uint32_t *in_queue, uint32_t *out_queue, int32_t max_steps,
+                       int32_t use_weights, int32_t scatter_first, uint32_t *scratch, hipStream_t stream,
+                       hipEvent_t ev0, hipEvent_t ev1) {
+    const uint32_t nwords = (n + 63) / 64;
+    uint32_t *counters = scratch;
+    unsigned long long *masks = (unsigned long long *)(scratch + 16);
+    uint32_t *offsets = scratch + 16 + 2 * (size_t)nwords;
+    PropagateArgs a;
+    a.pos = ph->d_pos; a.dir = ph->d_dir; a.pol = ph->d_pol; a.wl = ph->d_wavelengths; a.t = ph->d_t;
+    a.weights = ph->d_weights; a.flags = ph->d_flags; a.last_hit = ph->d_last_hit_triangles; a.evidx = ph->d_evidx;
+    a.rng = rng; a.nslots = nslots; a.input_queue = in_queue; a.first = 0; a.nthreads = (int32_t)n;
+    a.max_steps = max_steps; a.use_weights = use_weights; a.scatter_first = scatter_first;
+    a.alive_masks = masks; a.counters = counters;
+    a.order = nullptr;
+    const uint32_t threads = std::min(cap, (n + 63u) & ~63u);
+    if (ev0) CHR_HIP_CHECK(hipEventRecord(ev0, stream));
+    hipLaunchKernelGGL(select_step_variant(g), dim3(grid_for(threads)), dim3(BLOCK), 0, stream,
+                       (const DevGeom *)g->d_dev, a, cap);
+    if (ev1) CHR_HIP_CHECK(hipEventRecord(ev1, stream));
+    hipLaunchKernelGGL(scan_masks_kernel, dim3(1), dim3(1024), 0, stream, masks, nwords, offsets, out_queue,
+                       counters + 1, (uint32_t *)nullptr);
+    hipLaunchKernelGGL(scatter_queue_kernel, dim3(grid_for(n)), dim3(BLOCK), 0, stream, masks, offsets,
+                       counters + 1, in_queue, 0, (int32_t)n, out_queue);
+    CHR_HIP_CHECK(hipGetLastError());
+    return CHR_OK;
+}
+
 extern "C" int chr_propagate_chunk(const chr_geometry *g, const chr_photons *ph, uint32_t *d_rng_states,
                                    uint32_t rng_nslots, int32_t first_photon, int32_t nthreads,
                                    const uint32_t *d_input_queue, uint32_t *d_output_queue, int32_t max_steps,
@@ -1635,6 +1766,36 @@ extern "C" int chr_propagate_chunk(const chr_geometry *g, const chr_photons *ph,
                         max_steps, use_weights, scatter_first, d_scratch, (hipStream_t)stream);
 }
 
+// pinned host words for survivor counts / counters (per thread and device, reused)
+static int pinned_words(uint32_t **out) {
+    static thread_local uint32_t *p[16] = {};
+    int dev = 0;
+    CHR_HIP_CHECK(hipGetDevice(&dev));
+    if (!p[dev & 15]) CHR_HIP_CHECK(hipHostMalloc((void **)&p[dev & 15], 128, hipHostMallocDefault));
+    *out = p[dev & 15];
+    return CHR_OK;
+}
+
+// timing events, reused across calls (per thread)
+static int timing_events(size_t n, std::vector<hipEvent_t> **out) {
+    static thread_local std::vector<hipEvent_t> ev[16];
+    int dev = 0;
+    CHR_HIP_CHECK(hipGetDevice(&dev));
+    std::vector<hipEvent_t> &v = ev[dev & 15];
+    while (v.size() < n) {
+        hipEvent_t e;
+        CHR_HIP_CHECK(hipEventCreate(&e));
+        v.push_back(e);
+    }
+    *out = &v;
+    return CHR_OK;
+}
+
+static bool step_launch_enabled() {   // CHR_STEP_LAUNCH=0: the reference's one-launch-per-chunk structure (A/B)
+    const char *e = getenv("CHR_STEP_LAUNCH");
+    return !(e && e[0] == '0');
+}
+
 extern "C" int chr_propagate(const chr_geometry *g, const chr_photons *ph, uint32_t nphotons, uint32_t true_nphotons,
                              uint32_t ncopies, uint32_t *d_rng_states, uint32_t rng_nslots, int32_t ntpb,
                              int32_t max_blocks, int32_t max_steps, int32_t use_weights, int32_t scatter_first,
@@ -1646,70 +1807,73 @@ extern "C" int chr_propagate(const chr_geometry *g, const chr_photons *ph, uint3
                          (long long)ntpb * max_blocks, rng_nslots);
     if (ncopies == 0 || (uint64_t)true_nphotons * ncopies != nphotons)
         return chr::fail(CHR_ERR_INVALID, "chr_propagate: nphotons != true_nphotons*ncopies");
+    if (nphotons > 0x7FFFFFFFu) return chr::fail(CHR_ERR_INVALID, "chr_propagate: more than 2^31-1 photons");
     hipStream_t stream = (hipStream_t)vstream;
     chr_propagate_stats st{};
     if (nphotons == 0) { if (stats) *stats = st; return CHR_OK; }
-    const uint32_t chunk_cap = (uint32_t)std::min<uint64_t>((uint64_t)ntpb * max_blocks, nphotons);
-    // queues (photon.py:242-250): [0] = count+1 header, entries from [1]
-    std::vector<uint32_t> hq(nphotons + 1);
-    hq[0] = 0;
-    for (uint32_t c = 0; c < ncopies; ++c)
-        for (uint32_t k = 0; k < true_nphotons; ++k) hq[1 + c + (size_t)k * ncopies] = k + c * true_nphotons;
-    uint32_t *q[2] = {nullptr, nullptr};
-    uint32_t *scratch = nullptr;
-    uint32_t *pinned = nullptr;
-    int rc = CHR_OK;
+    const uint64_t cap = (uint64_t)ntpb * max_blocks;   // slots of one chunk (chunk_iterator)
+    const uint32_t chunk_cap = (uint32_t)std::min<uint64_t>(cap, nphotons);
+    // one launch per step when a wave's 64 slots map to whole mask words
+    const bool fused = (cap % 64 == 0) && cap <= 0x7FFFFFFFull && step_launch_enabled() && !sort_enabled();
+    const uint64_t nwords_all = (nphotons + 63) / 64;
+    uint64_t swords = chr_propagate_scratch_words(chunk_cap);
+    if (fused) swords = std::max<uint64_t>(swords, 16 + 3 * nwords_all + 16);
     const size_t qbytes = ((size_t)nphotons + 1) * 4;
-    const size_t sbytes = chr_propagate_scratch_words(chunk_cap) * 4;
     void *buf = nullptr;
-    rc = scratch_get(2 * qbytes + sbytes + 64, &buf);
+    int rc = scratch_get(2 * qbytes + swords * 4 + 64, &buf);
     if (rc) return rc;
+    uint32_t *q[2];
     q[0] = (uint32_t *)buf;
     q[1] = q[0] + (nphotons + 1);
-    scratch = (uint32_t *)(((uintptr_t)(q[1] + nphotons + 1) + 15) & ~(uintptr_t)15);
-    CHR_HIP_CHECK(hipHostMalloc((void **)&pinned, 128, hipHostMallocDefault));
-    const size_t max_chunks = (nphotons + chunk_cap - 1) / chunk_cap;
-    std::vector<hipEvent_t> events(2 * max_chunks, nullptr);
-    for (auto &ev : events) CHR_HIP_CHECK(hipEventCreate(&ev));
+    uint32_t *scratch = (uint32_t *)(((uintptr_t)(q[1] + nphotons + 1) + 15) & ~(uintptr_t)15);
+    uint32_t *pinned = nullptr;
+    if ((rc = pinned_words(&pinned))) return rc;
+    const size_t max_chunks = fused ? 1 : (nphotons + chunk_cap - 1) / chunk_cap;
+    std::vector<hipEvent_t> *evp = nullptr;
+    if ((rc = timing_events(2 * max_chunks, &evp))) return rc;
+    std::vector<hipEvent_t> &events = *evp;
     double kernel_ms = 0.0;
-    auto cleanup = [&]() {
-        if (pinned) hipHostFree(pinned);
-        for (auto &ev : events) if (ev) (void)hipEventDestroy(ev);
-    };
-    auto collect = [&](size_t nchunks) -> hipError_t {
+    auto collect = [&](size_t nchunks) -> int {
         for (size_t c = 0; c < nchunks; ++c) {
             float ms = 0.0f;
-            hipError_t err = hipEventElapsedTime(&ms, events[2 * c], events[2 * c + 1]);
-            if (err != hipSuccess) return err;
+            CHR_HIP_CHECK(hipEventElapsedTime(&ms, events[2 * c], events[2 * c + 1]));
             kernel_ms += ms;
         }
-        return hipSuccess;
+        return CHR_OK;
     };
-    hipError_t e;
-    if ((e = hipMemcpyAsync(q[0], hq.data(), qbytes, hipMemcpyHostToDevice, stream)) != hipSuccess) { cleanup(); CHR_HIP_CHECK(e); }
-    pinned[0] = 1;
-    if ((e = hipMemcpyAsync(q[1], pinned, 4, hipMemcpyHostToDevice, stream)) != hipSuccess) { cleanup(); CHR_HIP_CHECK(e); }
-    if ((e = hipMemsetAsync(scratch, 0, 64, stream)) != hipSuccess) { cleanup(); CHR_HIP_CHECK(e); }
+    // queues (photon.py:242-250): clones interleaved, q[1] header = 1 (count + 1)
+    hipLaunchKernelGGL(init_queue_kernel, dim3(grid_for(nphotons)), dim3(BLOCK), 0, stream, q[0], q[1], nphotons,
+                       true_nphotons, ncopies);
+    CHR_HIP_CHECK(hipGetLastError());
+    CHR_HIP_CHECK(hipMemsetAsync(scratch, 0, 64, stream));
     int cur = 0;
     int64_t n = nphotons;
     int step = 0;
     while (step < max_steps) {
-        const int nsteps = (n < (int64_t)ntpb * 16 * 8 || use_weights) ? max_steps - step : 1;
-        int64_t first = 0;
+        const int nsteps = (n < (int64_t)ntpb * 16 * 8 || use_weights) ? max_steps - step : 1;   // photon.py:261-264
         size_t nchunks = 0;
-        while (first < n) {
-            // chunk_iterator (tools.py:159-180)
-            const int64_t left = n - first;
-            int64_t blocks = left / ntpb + (left % ntpb != 0);
-            if (blocks > max_blocks) blocks = max_blocks;
-            const int64_t count = std::min<int64_t>(left, blocks * ntpb);
-            rc = launch_chunk(g, ph, d_rng_states, rng_nslots, (int32_t)first, (int32_t)count, q[cur] + 1, q[cur ^ 1],
-                              nsteps, use_weights, scatter_first, scratch, stream, events[2 * nchunks],
-                              events[2 * nchunks + 1]);
-            if (rc) { cleanup(); return rc; }
+        if (fused) {
+            rc = launch_step(g, ph, d_rng_states, rng_nslots, (uint32_t)cap, (uint32_t)n, q[cur] + 1, q[cur ^ 1],
+                             nsteps, use_weights, scatter_first, scratch, stream, events[0], events[1]);
+            if (rc) return rc;
             st.launches++;
-            nchunks++;
-            first += count;
+            nchunks = 1;
+        } else {
+            int64_t first = 0;
+            while (first < n) {
+                // chunk_iterator (tools.py:159-180)
+                const int64_t left = n - first;
+                int64_t blocks = left / ntpb + (left % ntpb != 0);
+                if (blocks > max_blocks) blocks = max_blocks;
+                const int64_t count = std::min<int64_t>(left, blocks * ntpb);
+                rc = launch_chunk(g, ph, d_rng_states, rng_nslots, (int32_t)first, (int32_t)count, q[cur] + 1,
+                                  q[cur ^ 1], nsteps, use_weights, scatter_first, scratch, stream, events[2 * nchunks],
+                                  events[2 * nchunks + 1]);
+                if (rc) return rc;
+                st.launches++;
+                nchunks++;
+                first += count;
+            }
         }
         st.steps_run++;
         step += nsteps;
@@ -1717,23 +1881,23 @@ extern "C" int chr_propagate(const chr_geometry *g, const chr_photons *ph, uint3
         if (step < max_steps) {
             cur ^= 1;
             // read the survivor count (photon.py:284) and reset the other header
-            if ((e = hipMemcpyAsync(pinned, q[cur], 4, hipMemcpyDeviceToHost, stream)) != hipSuccess) { cleanup(); CHR_HIP_CHECK(e); }
-            if ((e = hipStreamSynchronize(stream)) != hipSuccess) { cleanup(); CHR_HIP_CHECK(e); }
-            if ((e = collect(nchunks)) != hipSuccess) { cleanup(); CHR_HIP_CHECK(e); }
+            CHR_HIP_CHECK(hipMemcpyAsync(pinned, q[cur], 4, hipMemcpyDeviceToHost, stream));
+            CHR_HIP_CHECK(hipStreamSynchronize(stream));
+            if ((rc = collect(nchunks))) return rc;
             nchunks = 0;
             n = (int64_t)pinned[0] - 1;
             pinned[1] = 1;
-            if ((e = hipMemcpyAsync(q[cur ^ 1], pinned + 1, 4, hipMemcpyHostToDevice, stream)) != hipSuccess) { cleanup(); CHR_HIP_CHECK(e); }
+            CHR_HIP_CHECK(hipMemcpyAsync(q[cur ^ 1], pinned + 1, 4, hipMemcpyHostToDevice, stream));
             if (n == 0) break;
         }
         if (nchunks) {   // last step (no survivor read-back): drain before collecting
-            if ((e = hipStreamSynchronize(stream)) != hipSuccess) { cleanup(); CHR_HIP_CHECK(e); }
-            if ((e = collect(nchunks)) != hipSuccess) { cleanup(); CHR_HIP_CHECK(e); }
+            CHR_HIP_CHECK(hipStreamSynchronize(stream));
+            if ((rc = collect(nchunks))) return rc;
         }
     }
-    if ((e = hipMemcpyAsync(pinned + 2, scratch, 4, hipMemcpyDeviceToHost, stream)) != hipSuccess) { cleanup(); CHR_HIP_CHECK(e); }
-    if ((e = hipMemcpyAsync(pinned + 4, scratch + 2, 40, hipMemcpyDeviceToHost, stream)) != hipSuccess) { cleanup(); CHR_HIP_CHECK(e); }
-    if ((e = hipStreamSynchronize(stream)) != hipSuccess) { cleanup(); CHR_HIP_CHECK(e); }
+    CHR_HIP_CHECK(hipMemcpyAsync(pinned + 2, scratch, 4, hipMemcpyDeviceToHost, stream));
+    CHR_HIP_CHECK(hipMemcpyAsync(pinned + 4, scratch + 2, 40, hipMemcpyDeviceToHost, stream));
+    CHR_HIP_CHECK(hipStreamSynchronize(stream));
     st.stack_overflows = pinned[2];
     {
         uint64_t c[5];
@@ -1746,7 +1910,6 @@ extern "C" int chr_propagate(const chr_geometry *g, const chr_photons *ph, uint3
     }
     st.kernel_ms = kernel_ms;
     st.final_alive = (step < max_steps) ? (uint32_t)n : 0u;
-    cleanup();
     if (stats) *stats = st;
     return CHR_OK;
 }

@@ -98,14 +98,23 @@ def test_propagate_single_launch_parity(cuda, small_detector, small_packed):
     assert stats['launches'] == 1
 
 
-def test_propagate_multi_launch_parity(cuda, small_detector, small_packed):
-    """Per-step relaunch + survivor compaction + chunks sharing RNG slots."""
+@pytest.mark.parametrize('ntpb,max_blocks,step_launch', [(64, 64, '1'), (64, 64, '0'), (100, 41, '1')])
+def test_propagate_multi_launch_parity(cuda, small_detector, small_packed, monkeypatch, ntpb, max_blocks,
+                                       step_launch):
+    """Per-step relaunch + survivor compaction + chunks sharing RNG slots.
+    (64, 64, '1'): one launch per step, work-item = slot looping over the
+    step's chunks; '0': the reference's one launch per chunk; (100, 41): a
+    slot count that is not a multiple of 64 (per-chunk launches)."""
     from chroma.photon_source import isotropic
+    monkeypatch.setenv('CHR_STEP_LAUNCH', step_launch)
     photons = isotropic(30000, seed=12)
-    gp, host, rng, st, stats = _run_both(small_detector, small_packed, photons, 64 * 64, 64, 64, 1000)
-    _compare(host, gp, 'multi-launch')
+    gp, host, rng, st, stats = _run_both(small_detector, small_packed, photons, ntpb * max_blocks, ntpb, max_blocks,
+                                         1000)
+    _compare(host, gp, 'multi-launch %s' % ((ntpb, max_blocks, step_launch),))
     assert np.array_equal(rng.get().reshape(-1), st)
     assert stats['host_steps'] > 1 and stats['launches'] > stats['host_steps']
+    fused = step_launch == '1' and (ntpb * max_blocks) % 64 == 0
+    assert (gp.last_stats.launches == gp.last_stats.steps_run) == fused
 
 
 @pytest.mark.parametrize('use_weights,scatter_first', [(False, 0), (True, 0), (False, 1), (False, -1)])
