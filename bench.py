@@ -10,9 +10,11 @@ Photon inputs are resident in HBM before the timed region; each step restores
 them from a device-resident copy (D2D, inside the timed region).
 
 Multi-GPU: one process per GPU (torchrun), geometry replicated, photons
-sharded (each rank propagates its own batch: weak scaling), no collective in
-the data path; the timed region is bracketed by barriers and the max over
-ranks is reported.
+sharded (each rank propagates its own batch: weak scaling, RNG subsequences
+disjoint per rank).  Each step ends with the hit-channel reduce: detected
+photons are histogrammed per PMT channel on the device and SUM-reduced over
+the ranks (RCCL, chroma.gpu.shard) -- the only exchange the path has.  The
+timed region is bracketed by barriers and the max over ranks is reported.
 
 Roofline: the propagate kernel is bound by HBM/L2 latency-bandwidth on the
 BVH + triangle gathers.  achieved = algorithmic bytes per step / summed
@@ -151,7 +153,7 @@ def roofline(args, cst, n, kernel_ms, launches):
           'traversals_per_photon': cst.traversals / n,
           'simd_efficiency_nodes': cst.nodes_visited / max(1.0, 64.0 * cst.wave_node_steps),
           'simd_efficiency_triangles': cst.triangles_tested / max(1.0, 64.0 * cst.wave_triangle_steps),
-          'kernel': 'chr::propagate_kernel<8,4,true>',
+          'kernel': 'chr::propagate_step_kernel<8,4,1002>',
           'avg_launch_ms': 1e3 * avg_launch_s}
     # HBM bytes per launch from the PMC passes (tools/rocprof_bench.sh) of this same workload
     pmc_path = os.path.join(ROOT, 'profiles', 'latest_pmc.json')
@@ -206,7 +208,7 @@ def main():
     gdet = gpu.GPUDetector(det)
     log('rank %d: geometry on device in %.1fs (%.2f GB)' % (rank, time.time() - t0, gdet.device_bytes() / 1e9))
     nslots = args.nthreads_per_block * args.max_blocks
-    rng = gpu.get_rng_states(nslots, seed=args.seed + 7919 * rank)
+    rng = gpu.get_rng_states(nslots, seed=args.seed, first_subsequence=rank * nslots)
 
     photons = isotropic(args.photons, seed=20260102 + rank)
     pristine = SimpleNamespace(
@@ -216,10 +218,23 @@ def main():
         true_nphotons=args.photons)
     torch.cuda.synchronize()
 
+    import ctypes
+    from chroma.gpu import _native, shard
+    from chroma.gpu.tools import current_stream
+    counts = ga.zeros(gdet.nchannels, np.uint32)
+    reduced = {}
+
     def step():
         gp = gpu.GPUPhotons(pristine, copy_flags=True, copy_triangles=False, copy_weights=False)
         gp.propagate(gdet, rng, nthreads_per_block=args.nthreads_per_block, max_blocks=args.max_blocks,
                      max_steps=args.max_steps)
+        # hit-channel reduce: detected photons per PMT channel on each rank,
+        # SUM-reduced over ranks (RCCL for N > 1)
+        counts.fill(0)
+        _native.call('chr_channel_hit_counts', ctypes.byref(gp._desc()), 0, args.photons, 0x4,
+                     gdet.solid_id_map.gpudata, gdet.solid_id_to_channel_index_gpu.gpudata, counts.gpudata,
+                     gdet.nchannels, current_stream())
+        reduced['counts'] = shard.allreduce_channel_counts(counts.tensor)
         return gp
 
     for _ in range(args.warmup):
@@ -246,6 +261,7 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     detected = int(((gp.flags.get() & 4) != 0).sum())
+    channel_hits = int(reduced['counts'].sum().item())     # all ranks, detected with a channel
     # untimed: same propagate with the counting kernel variant -> algorithmic bytes
     cst = None
     if not args.no_count:
@@ -275,7 +291,8 @@ def main():
                        'parallelism': 'photon-sharded x%d, geometry replicated' % world},
             'detail': {'kernel_ms_per_step': kernel_ms / args.steps, 'launches_per_step': launches / args.steps,
                        'host_steps_per_propagate': host_steps / args.steps,
-                       'detected_fraction': detected / args.photons},
+                       'detected_fraction': detected / args.photons,
+                       'channel_hits_all_ranks': channel_hits},
             'roofline': None, 'cpu_baseline': None,
         }
         n = float(args.photons)

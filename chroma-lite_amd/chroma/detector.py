@@ -66,5 +66,9 @@ class Detector(Geometry):
         self.solid_id_to_channel_index = np.asarray(self.solid_id_to_channel_index, dtype=np.int32)
         self.channel_index_to_solid_id = np.asarray(self.channel_index_to_solid_id, dtype=np.int32)
         self.channel_index_to_channel_type = np.asarray(self.channel_index_to_channel_type, dtype=np.int32)
-        self.channel_index_to_position = np.asarray(self.channel_index_to_position, dtype=np.int32)
+        # a PMT added without a displacement sits at the origin (add_pmt's documented
+        # default, reference detector.py:60-62); the reference's asarray would raise on None
+        self.channel_index_to_position = np.asarray([np.zeros(3) if p is None else p
+                                                     for p in self.channel_index_to_position],
+                                                    dtype=np.int32).reshape(-1, 3)
         Geometry.flatten(self)

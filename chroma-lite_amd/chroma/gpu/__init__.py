@@ -6,3 +6,4 @@ from chroma.gpu.tools import (chunk_iterator, to_float3, to_uint3, create_cuda_c
 from chroma.gpu.geometry import GPUGeometry  # noqa: F401
 from chroma.gpu.detector import GPUDetector  # noqa: F401
 from chroma.gpu.photon import GPUPhotons, GPUPhotonsSlice  # noqa: F401
+from chroma.gpu.daq import GPUDaq, GPUChannels  # noqa: F401

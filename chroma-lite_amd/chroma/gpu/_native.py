@@ -96,6 +96,13 @@ _SIGNATURES = {
                                   ctypes.POINTER(ctypes.c_int32)]),
     'chr_wide_bvh_copy': (c_i32, [c_vp, c_vp, c_vp]),
     'chr_wide_bvh_free': (c_i32, [c_vp]),
+    'chr_daq_begin': (c_i32, [c_vp, c_vp, c_vp, c_u32, c_f32, c_vp]),
+    'chr_daq_acquire': (c_i32, [ctypes.POINTER(PhotonsDesc), c_vp, c_u32, c_vp, c_u32, c_i32, c_i32, c_vp, c_vp,
+                                c_vp, c_vp, c_vp, c_i32, c_i32, c_f32, c_i32, c_i32, c_vp]),
+    'chr_daq_end': (c_i32, [c_vp, c_vp, c_vp, c_vp, c_u32, c_i32, c_f32, c_vp]),
+    'chr_init_rng_subseq': (c_i32, [c_vp, c_u32, c_u64, c_u64, c_u64, c_vp]),
+    'chr_channel_hit_counts': (c_i32, [ctypes.POINTER(PhotonsDesc), c_i32, c_i32, c_u32, c_vp, c_vp, c_vp, c_i32,
+                                       c_vp]),
     'chr_last_error': (ctypes.c_char_p, []),
     'chr_version': (c_i32, []),
 }

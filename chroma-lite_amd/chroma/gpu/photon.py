@@ -117,10 +117,10 @@ class GPUPhotons(object):
         flat = self.get_flat_hits(*args, **kwargs)
         return {int(ch): flat[flat.channel == ch] for ch in np.unique(flat.channel)}
 
-    def get_flat_hits(self, gpu_detector, target_flag=(0x1 << 2), nthreads_per_block=256, max_blocks=1024,
-                      start_photon=None, nphotons=None, no_map=False):
-        """Detected photons: flags & target_flag, last_hit_triangle > -1 and
-        a channel behind the hit solid; returns event.Photons with .channel."""
+    def flat_hits_device(self, gpu_detector, target_flag=(0x1 << 2), start_photon=None, nphotons=None):
+        """Device-resident compacted hits: (dict of the nine photon GPUArrays,
+        channel GPUArray i32), ascending photon order.  get_flat_hits() is this
+        plus the download; the photon-sharded path gathers these over RCCL."""
         start = 0 if start_photon is None else start_photon
         n = self.pos.size - start if nphotons is None else nphotons
         desc = self._desc()
@@ -138,6 +138,13 @@ class GPUPhotons(object):
                          gpu_detector.solid_id_map.gpudata, gpu_detector.solid_id_to_channel_index_gpu.gpudata,
                          ctypes.byref(odesc), channels.gpudata, ctypes.byref(count), current_stream())
             assert count.value == k
+        return out, channels
+
+    def get_flat_hits(self, gpu_detector, target_flag=(0x1 << 2), nthreads_per_block=256, max_blocks=1024,
+                      start_photon=None, nphotons=None, no_map=False):
+        """Detected photons: flags & target_flag, last_hit_triangle > -1 and
+        a channel behind the hit solid; returns event.Photons with .channel."""
+        out, channels = self.flat_hits_device(gpu_detector, target_flag, start_photon, nphotons)
 
         def vec3(a):
             return a.get().view(np.float32).reshape((len(a), 3))

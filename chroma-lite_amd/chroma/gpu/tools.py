@@ -89,12 +89,27 @@ class RNGStates(object):
         """Host copy, shape (6, size): rows d, v0..v4."""
         return self.array.get().reshape(6, self.size)
 
+    @property
+    def normal_cache(self):
+        """curand_normal's cached second value per slot ({flag, bits}, 2 x u32
+        SoA; zero = empty, as curand_init leaves it).  Allocated on first use
+        (only the ndaq > 1 DAQ draws normals)."""
+        if getattr(self, '_normal', None) is None:
+            self._normal = ga.zeros(2 * self.size, np.uint32)
+        return self._normal
 
-def get_rng_states(size, seed=1, offset=0):
+
+def get_rng_states(size, seed=1, offset=0, first_subsequence=0):
     """Return `size` random-number-generator states, slot s initialised as
-    curand_init(seed, s, offset)."""
+    curand_init(seed, first_subsequence + s, offset).  first_subsequence is an
+    extension for photon-sharded runs (rank r of a job takes subsequences
+    [r*size, (r+1)*size) so no two ranks share a stream); 0 is the reference."""
     st = RNGStates(size)
-    _native.call('chr_init_rng', st.gpudata, st.size, int(seed) & (2 ** 64 - 1), int(offset), current_stream())
+    if first_subsequence:
+        _native.call('chr_init_rng_subseq', st.gpudata, st.size, int(seed) & (2 ** 64 - 1), int(first_subsequence),
+                     int(offset), current_stream())
+    else:
+        _native.call('chr_init_rng', st.gpudata, st.size, int(seed) & (2 ** 64 - 1), int(offset), current_stream())
     return st
 
 

@@ -3,8 +3,8 @@
 Batches events (never splitting one), uploads photons, propagates them on the
 device with the reference's launch shape (nthreads_per_block=512,
 max_blocks=1024 -> 524,288 RNG slots) and splits the detected hits back into
-events.  Photon tracking and GPU-resident inputs are supported as in the
-reference.  run_daq needs the DAQ stage, which is not part of this build yet.
+events.  Photon tracking, GPU-resident inputs and the per-event DAQ
+(run_daq=True, chroma.gpu.daq) are supported as in the reference.
 """
 import os
 import time
@@ -35,6 +35,7 @@ class Simulation(object):
         self.context = gpu.create_cuda_context(cuda_device)
         if hasattr(detector, 'num_channels'):
             self.gpu_geometry = gpu.GPUDetector(detector)
+            self.gpu_daq = gpu.GPUDaq(self.gpu_geometry) if self.gpu_geometry.nchannels > 0 else None
         else:
             self.gpu_geometry = gpu.GPUGeometry(detector)
         self.rng_states = gpu.get_rng_states(self.nthreads_per_block * self.max_blocks, seed=self.seed)
@@ -58,8 +59,6 @@ class Simulation(object):
         has_channels = hasattr(self.detector, 'num_channels')
         if has_channels and (keep_hits or keep_flat_hits):
             batch_hits = gpu_photons.get_flat_hits(self.gpu_geometry)
-        if run_daq:
-            raise NotImplementedError('run_daq: the DAQ stage (reference chroma/gpu/daq.py) is not built yet')
         for i, (ev, (start, end)) in enumerate(zip(batch_events, zip(bounds[:-1], bounds[1:]))):
             if not keep_photons_beg:
                 ev.photons_beg = None
@@ -83,6 +82,12 @@ class Simulation(object):
                     ev.hits = {int(ch): ev_hits[ev_hits.channel == ch] for ch in np.unique(ev_hits.channel)}
                 if keep_flat_hits:
                     ev.flat_hits = ev_hits
+            if run_daq and getattr(self, 'gpu_daq', None) is not None:
+                # per event, as the reference does (sim.py:143-152)
+                self.gpu_daq.begin_acquire()
+                self.gpu_daq.acquire(gpu_photons, self.rng_states, start_photon=int(start), nphotons=int(end - start),
+                                     nthreads_per_block=self.nthreads_per_block, max_blocks=self.max_blocks)
+                ev.channels = self.gpu_daq.end_acquire().get()
             yield ev
 
     @staticmethod
@@ -149,3 +154,83 @@ class Simulation(object):
                 ctx.pop()
             except Exception:
                 pass
+
+
+class ShardedSimulation(Simulation):
+    """Simulation across the ranks of a torch.distributed job, one process per
+    GPU (launch with torchrun; backend "nccl" = RCCL).  Every rank must call
+    simulate() with the same events; each propagates its contiguous share of
+    every batch on its own GPU (geometry replicated), then the detected hits
+    are gathered in global photon order and the per-event DAQ channels are
+    reduced (chroma.gpu.shard).  Every rank yields the same, complete events,
+    equal to a single-GPU run's except for the RNG streams of ranks > 0
+    (rank r draws from curand subsequences r*S .. r*S+S-1).
+    photon_tracking and keep_photons_end are not sharded (use Simulation)."""
+
+    def __init__(self, detector, seed=None, group=None, nthreads_per_block=512, max_blocks=1024):
+        import torch
+        import torch.distributed as dist
+        from chroma.gpu import shard
+        self.group = group
+        self.rank, self.world = shard.dist_info(group)
+        if seed is None:
+            seed = pick_seed()
+            if self.world > 1:      # one seed for the job
+                box = [seed]
+                dist.broadcast_object_list(box, src=0, group=group)
+                seed = box[0]
+        Simulation.__init__(self, detector, seed=seed, cuda_device=shard.local_device(),
+                            nthreads_per_block=nthreads_per_block, max_blocks=max_blocks)
+        nslots = self.nthreads_per_block * self.max_blocks
+        if self.rank:
+            self.rng_states = gpu.get_rng_states(nslots, seed=self.seed, first_subsequence=self.rank * nslots)
+        self._torch = torch
+
+    def _simulate_batch(self, batch_events, keep_photons_beg=False, keep_photons_end=False, keep_hits=True,
+                        keep_flat_hits=True, run_daq=False, max_steps=100, verbose=False):
+        from chroma.gpu import shard
+        if keep_photons_end:
+            raise NotImplementedError('ShardedSimulation: keep_photons_end is not gathered; use Simulation')
+        torch = self._torch
+        sources = [ev.photons_beg for ev in batch_events]
+        bounds = np.cumsum(np.concatenate([[0], [len(s) for s in sources]])).astype(np.int64)
+        total = int(bounds[-1])
+        lo, hi = shard.shard_range(total, self.rank, self.world)
+        src = self._stack_gpu_photon_sources(sources)
+        if src is None:
+            local = event.Photons.join(sources)[lo:hi]
+        else:
+            local = SimpleNamespace(**{f: getattr(src, f)[lo:hi] for f in
+                                       ('pos', 'dir', 'pol', 'wavelengths', 't', 'evidx', 'flags')})
+            local.true_nphotons = hi - lo
+        gpu_photons = gpu.GPUPhotons(local, copy_flags=True, copy_triangles=False, copy_weights=False)
+        if hi > lo:
+            gpu_photons.propagate(self.gpu_geometry, self.rng_states, nthreads_per_block=self.nthreads_per_block,
+                                  max_blocks=self.max_blocks, max_steps=max_steps)
+        has_channels = hasattr(self.detector, 'num_channels')
+        if has_channels and (keep_hits or keep_flat_hits):
+            fields, channels = gpu_photons.flat_hits_device(self.gpu_geometry)
+            batch_hits = shard.unpack_hits(shard.allgather_rows(shard.pack_hits(fields, channels), self.group))
+        for i, (ev, (start, end)) in enumerate(zip(batch_events, zip(bounds[:-1], bounds[1:]))):
+            if not keep_photons_beg:
+                ev.photons_beg = None
+            if has_channels and (keep_hits or keep_flat_hits):
+                ev_hits = batch_hits[batch_hits.evidx == i]
+                if keep_hits:
+                    ev.hits = {int(ch): ev_hits[ev_hits.channel == ch] for ch in np.unique(ev_hits.channel)}
+                if keep_flat_hits:
+                    ev.flat_hits = ev_hits
+            if run_daq and getattr(self, 'gpu_daq', None) is not None:
+                daq = self.gpu_daq
+                daq.begin_acquire()
+                a, b = max(int(start), lo), min(int(end), hi)     # this rank's part of the event
+                if b > a:
+                    daq.acquire(gpu_photons, self.rng_states, start_photon=a - lo, nphotons=b - a,
+                                nthreads_per_block=self.nthreads_per_block, max_blocks=self.max_blocks)
+                t, q, h = shard.reduce_channels(daq.earliest_time_int_gpu.tensor, daq.channel_q_int_gpu.tensor,
+                                                daq.channel_history_gpu.tensor, self.group)
+                daq.earliest_time_int_gpu.tensor.copy_(t)
+                daq.channel_q_int_gpu.tensor.copy_(q)
+                daq.channel_history_gpu.tensor.copy_(h)
+                ev.channels = daq.end_acquire().get()
+            yield ev

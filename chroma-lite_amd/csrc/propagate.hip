@@ -1414,12 +1414,12 @@ __global__ __launch_bounds__(BLOCK) void init_queue_kernel(uint32_t *q0, uint32_
 
 // ---------------------------------------------------------------- RNG init
 __global__ __launch_bounds__(BLOCK) void init_rng_kernel(uint32_t *states, uint32_t nslots, unsigned long long seed,
-                                                          unsigned long long offset, const uint32_t *seq, int nseq,
-                                                          const uint32_t *off, int noff) {
+                                                          unsigned long long subseq0, unsigned long long offset,
+                                                          const uint32_t *seq, int nseq, const uint32_t *off, int noff) {
     const uint32_t s = blockIdx.x * BLOCK + threadIdx.x;
     if (s >= nslots) return;
     chr_xorwow r;
-    chr_xorwow_init(&r, seed, s, offset, seq, nseq, off, noff);
+    chr_xorwow_init(&r, seed, subseq0 + s, offset, seq, nseq, off, noff);
     states[s] = r.d; states[nslots + s] = r.v0; states[2 * nslots + s] = r.v1;
     states[3 * nslots + s] = r.v2; states[4 * nslots + s] = r.v3; states[5 * nslots + s] = r.v4;
 }
@@ -1598,15 +1598,23 @@ int scratch_get(size_t bytes, void **out) {
 
 }  // namespace
 
-extern "C" int chr_init_rng(uint32_t *d_states, uint32_t nslots, uint64_t seed, uint64_t offset, void *stream) {
+extern "C" int chr_init_rng_subseq(uint32_t *d_states, uint32_t nslots, uint64_t seed, uint64_t first_subsequence,
+                                   uint64_t offset, void *stream) {
     if (!d_states || nslots == 0) return chr::fail(CHR_ERR_INVALID, "chr_init_rng: empty state buffer");
+    if (first_subsequence + nslots > (1ull << 32))
+        return chr::fail(CHR_ERR_INVALID, "chr_init_rng: subsequences beyond 2^32 are not supported");
     JumpTables jt;
     int rc = get_jump_tables(jt);
     if (rc) return rc;
     hipLaunchKernelGGL(init_rng_kernel, dim3(grid_for(nslots)), dim3(BLOCK), 0, (hipStream_t)stream, d_states, nslots,
-                       (unsigned long long)seed, (unsigned long long)offset, jt.seq, 32, jt.off, 64);
+                       (unsigned long long)seed, (unsigned long long)first_subsequence, (unsigned long long)offset,
+                       jt.seq, 32, jt.off, 64);
     CHR_HIP_CHECK(hipGetLastError());
     return CHR_OK;
+}
+
+extern "C" int chr_init_rng(uint32_t *d_states, uint32_t nslots, uint64_t seed, uint64_t offset, void *stream) {
+    return chr_init_rng_subseq(d_states, nslots, seed, 0, offset, stream);
 }
 
 extern "C" int chr_rng_download(const uint32_t *d_states, uint32_t nslots, uint32_t *h_out, void *stream) {

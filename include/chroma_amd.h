@@ -132,6 +132,10 @@ typedef struct chr_photons {               /* reference GPUPhotons arrays, photo
  * replaces: get_rng_states / init_rng (chroma/gpu/tools.py:117-145):
  * curand_init(seed, subsequence = slot, offset) for every slot. */
 int chr_init_rng(uint32_t *d_states, uint32_t nslots, uint64_t seed, uint64_t offset, void *stream);
+/* extension for photon-sharded runs: slot s = curand_init(seed, first_subsequence + s, offset)
+ * (first_subsequence + nslots <= 2^32); chr_init_rng is first_subsequence = 0. */
+int chr_init_rng_subseq(uint32_t *d_states, uint32_t nslots, uint64_t seed, uint64_t first_subsequence,
+                        uint64_t offset, void *stream);
 /* copy slot states to the host (tests; 6*nslots words, SoA) */
 int chr_rng_download(const uint32_t *d_states, uint32_t nslots, uint32_t *h_out, void *stream);
 
@@ -232,6 +236,53 @@ int chr_wide_bvh_info(const chr_wide_result *r, uint32_t *nnodes, uint32_t *ntri
 int chr_wide_bvh_copy(const chr_wide_result *r, void *h_nodes /*[nnodes*96 B]*/,
                       void *h_tri /*[ntri*64 B]*/);
 int chr_wide_bvh_free(chr_wide_result *r);
+
+/* ------------------------------------------------------------------- DAQ
+ * replaces: chroma/cuda/daq.cu + GPUDaq (chroma/gpu/daq.py:37-101) and the
+ * Detector struct (chroma/cuda/detector.h:4-22, uploaded by
+ * chroma/gpu/detector.py:21-40).  Per-channel accumulators are u32 arrays of
+ * ndaq*nchannels (copy i of channel c at i*stride + c): earliest time as the
+ * float's bit pattern under unsigned atomicMin (daq.cu:5-10 keeps
+ * float_to_sortable_int as a plain bit cast), charge as round(q/charge_unit)
+ * under atomicAdd, history under atomicOr -- all order-independent, so the
+ * result does not depend on the schedule. */
+typedef struct chr_daq_detector {
+    const int32_t *d_solid_id_to_channel_index;   /* [nsolids] */
+    const float *d_time_cdf_x, *d_time_cdf_y;     /* [time_cdf_len] */
+    const float *d_charge_cdf_x, *d_charge_cdf_y; /* [charge_cdf_len] */
+    int32_t nchannels, time_cdf_len, charge_cdf_len;
+    float charge_unit;                            /* charge_cdf_x[-1] / 2^16 (gpu/detector.py:39) */
+} chr_daq_detector;
+
+/* replaces: GPUDaq.begin_acquire (daq.py:56-60): time words = bits(maxtime), q and history = 0 */
+int chr_daq_begin(uint32_t *d_time_int, uint32_t *d_q_int, uint32_t *d_history, uint32_t n, float maxtime,
+                  void *stream);
+/* replaces: GPUDaq.acquire (daq.py:62-91): run_daq (ndaq == 1, daq.cu:35-83) or
+ * run_daq_many (ndaq > 1, daq.cu:85-145) over photons [start, start+n) with the
+ * reference's chunking (slot = position in chunk; nthreads_per_block*max_blocks
+ * slots for ndaq == 1, one photon per block of nthreads_per_block slots for
+ * ndaq > 1).  d_normal_cache (2 words per slot, zero after chr_init_rng) holds
+ * curand_normal's cached value; required only for ndaq > 1.  Synchronous. */
+int chr_daq_acquire(const chr_photons *ph, uint32_t *d_rng_states, uint32_t rng_nslots, uint32_t *d_normal_cache,
+                    uint32_t detection_state, int32_t start_photon, int32_t nphotons,
+                    const uint32_t *d_solid_map, const chr_daq_detector *det,
+                    uint32_t *d_time_int, uint32_t *d_q_int, uint32_t *d_history,
+                    int32_t ndaq, int32_t stride, float global_weight,
+                    int32_t nthreads_per_block, int32_t max_blocks, void *stream);
+/* replaces: GPUDaq.end_acquire (daq.py:93-101): convert_sortable_int_to_float
+ * over all n words, convert_charge_int_to_float over the first nchannels words
+ * only (daq.cu:158-172; later DAQ copies keep charge 0, as in the reference). */
+int chr_daq_end(const uint32_t *d_time_int, float *d_time, const uint32_t *d_q_int, float *d_q, uint32_t n,
+                int32_t nchannels, float charge_unit, void *stream);
+
+/* Detected photons per channel, ACCUMULATED into d_counts[nchannels] (u32; the
+ * caller zeroes it): the selection of count_photon_hits (propagate.cu:172-199)
+ * histogrammed by channel.  No reference counterpart -- it is the per-rank
+ * array a photon-sharded run reduces over RCCL (chroma/gpu/shard.py). Async. */
+int chr_channel_hit_counts(const chr_photons *ph, int32_t start_photon, int32_t nphotons,
+                           uint32_t detection_state, const uint32_t *d_solid_map,
+                           const int32_t *d_solid_id_to_channel_index, uint32_t *d_counts,
+                           int32_t nchannels, void *stream);
 
 /* ------------------------------------------------------------- misc */
 const char *chr_last_error(void);

@@ -148,4 +148,28 @@ CHR_FN void chr_xorwow_init(chr_xorwow *s, unsigned long long seed, unsigned lon
     s->d += (uint32_t)offset * 362437u;
 }
 
+/* curand_normal (Box-Muller with one cached value), used by the reference's
+ * run_daq_many (daq.cu:131).  cuRAND keeps the cache in the state
+ * (boxmuller_flag / boxmuller_extra, zeroed by curand_init); here it is a
+ * separate 2-word record per slot {flag, extra bits}.  Box-Muller as cuRAND
+ * states it: u = x*2^-32 + 2^-33, v = y*(2pi*2^-32) + pi*2^-32,
+ * s = sqrt(-2 log u), return s*sin(v), cache s*cos(v).  "Parity unpinned"
+ * like the seed salts (no cuRAND in this image). */
+CHR_FN float chr_normal(chr_xorwow *s, uint32_t *flag, uint32_t *extra) {
+    if (*flag != 1u) {
+        const uint32_t x = chr_xorwow_next(s);
+        const uint32_t y = chr_xorwow_next(s);
+        const float u = (float)x * 2.3283064365386963e-10f + 1.1641532182693481e-10f;
+        const float v = (float)y * 1.4629180792671596e-09f + 7.3145903963357980e-10f;
+        const float r = chr_sqrtf(-2.0f * chr_logf(u));
+        float sv, cv;
+        chr_sincosf(v, &sv, &cv);
+        *extra = chr_f2u(cv * r);
+        *flag = 1u;
+        return sv * r;
+    }
+    *flag = 0u;
+    return chr_u2f(*extra);
+}
+
 #endif /* CHROMA_RNG_H */

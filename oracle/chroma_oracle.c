@@ -959,7 +959,8 @@ static void init_once(void) { if (!g_init) { init_thresholds(); g_init = 1; } }
 
 /* ---------------------------------------------------------------- exports */
 
-EXPORT void orc_rng_init(uint32_t *states, uint32_t nslots, unsigned long long seed, unsigned long long offset) {
+EXPORT void orc_rng_init_subseq(uint32_t *states, uint32_t nslots, unsigned long long seed,
+                                unsigned long long subseq0, unsigned long long offset) {
     static uint32_t *seq = NULL, *off = NULL;
     if (!seq) {
         seq = (uint32_t *)malloc(sizeof(uint32_t) * CHR_XW_MATWORDS * 40);
@@ -970,9 +971,14 @@ EXPORT void orc_rng_init(uint32_t *states, uint32_t nslots, unsigned long long s
 #pragma omp parallel for
     for (int64_t s = 0; s < (int64_t)nslots; ++s) {
         chr_xorwow r;
-        chr_xorwow_init(&r, seed, (unsigned long long)s, offset, seq, 40, off, 64);
+        chr_xorwow_init(&r, seed, subseq0 + (unsigned long long)s, offset, seq, 40, off, 64);
         rng_store(states, nslots, (uint32_t)s, &r);
     }
+}
+
+/* init_rng (gpu/tools.py:117-145): curand_init(seed, slot, offset) */
+EXPORT void orc_rng_init(uint32_t *states, uint32_t nslots, unsigned long long seed, unsigned long long offset) {
+    orc_rng_init_subseq(states, nslots, seed, 0, offset);
 }
 
 /* A^(2^(67+i)) for the rocRAND cross-check */
@@ -1127,3 +1133,113 @@ EXPORT void orc_rayleigh(int n, float *dir, float *pol, uint32_t *states, uint32
 }
 
 EXPORT int orc_version(void) { return 1; }
+
+/* ------------------------------------------------ DAQ (chroma/cuda/daq.cu, gpu/daq.py)
+ * Sequential restatement with the reference's own launch structure: ndaq == 1
+ * is run_daq (daq.cu:35-83) over chunk_iterator(n, ntpb, max_blocks) chunks,
+ * slot = position in chunk; ndaq > 1 is run_daq_many (daq.cu:85-145) over
+ * chunk_iterator(n, 1, max_blocks), one photon per block of ntpb slots.
+ * The curand_normal cache lives in normal_cache[slot], [nslots + slot]. */
+
+/* interpolate.h:32-58 */
+static float interp_xy(float x, int n, const float *xp, const float *fp) {
+    int lower = 0, upper = n - 1;
+    if (x <= xp[lower]) return fp[lower];
+    if (x >= xp[upper]) return fp[upper];
+    while (lower < upper - 1) {
+        int half = (lower + upper) / 2;
+        if (x < xp[half]) upper = half; else lower = half;
+    }
+    float df = fp[upper] - fp[lower];
+    float dx = xp[upper] - xp[lower];
+    return fp[lower] + (df * (x - xp[lower])) / dx;
+}
+
+/* random.h:26-30 */
+static float sample_cdf_xy(chr_xorwow *rng, int ncdf, const float *cdf_x, const float *cdf_y) {
+    return interp_xy(chr_uniform01(rng), ncdf, cdf_y, cdf_x);
+}
+
+static void daq_record(uint32_t *time_int, uint32_t *q_int, uint32_t *hist, int c, float time, float charge,
+                       float charge_unit, uint32_t history) {
+    uint32_t ti = chr_f2u(time);                             /* float_to_sortable_int: bit cast (daq.cu:5-10) */
+    uint32_t qi = (uint32_t)roundf(charge / charge_unit);    /* daq.cu:72 */
+    if (ti < time_int[c]) time_int[c] = ti;                  /* atomicMin (unsigned) */
+    q_int[c] += qi;                                          /* atomicAdd */
+    hist[c] |= history;                                      /* atomicOr */
+}
+
+EXPORT int orc_daq(const float *t, const uint32_t *flags, const int32_t *last_hit, const float *weights,
+                   const uint32_t *solid_map, const int32_t *s2c,
+                   const float *tcx, const float *tcy, int tlen, const float *qcx, const float *qcy, int qlen,
+                   float charge_unit, uint32_t *rng, uint32_t nslots, uint32_t *normal_cache,
+                   uint32_t detection_state, int start, int nphotons,
+                   uint32_t *time_int, uint32_t *q_int, uint32_t *hist,
+                   int ndaq, int stride, float global_weight, int ntpb, int max_blocks) {
+    int first = 0;
+    if (ndaq == 1) {
+        while (first < nphotons) {
+            int count;
+            chunk_iter(nphotons - first, ntpb, max_blocks, first, &count);
+            if ((uint32_t)count > nslots) return CHR_ERR_INVALID;
+            for (int id = 0; id < count; ++id) {                 /* run_daq, one work-item */
+                chr_xorwow r;
+                rng_load(rng, nslots, (uint32_t)id, &r);
+                int photon_id = start + first + id;
+                int tri = last_hit[photon_id];
+                if (tri > -1) {
+                    int solid_id = (int)solid_map[tri];
+                    uint32_t history = flags[photon_id];
+                    int c = s2c[solid_id];
+                    if (c >= 0 && (history & detection_state)) {
+                        float w = weights[photon_id] * global_weight;
+                        if (chr_uniform01(&r) < w) {
+                            float time = t[photon_id] + sample_cdf_xy(&r, tlen, tcx, tcy);
+                            float charge = sample_cdf_xy(&r, qlen, qcx, qcy);
+                            daq_record(time_int, q_int, hist, c, time, charge, charge_unit, history);
+                        }
+                    }
+                }
+                rng_store(rng, nslots, (uint32_t)id, &r);
+            }
+            first += count;
+        }
+        return 0;
+    }
+    while (first < nphotons) {
+        int count;
+        chunk_iter(nphotons - first, 1, max_blocks, first, &count);
+        if ((uint64_t)count * ntpb > nslots) return CHR_ERR_INVALID;
+        for (int b = 0; b < count; ++b) {                         /* run_daq_many, one block */
+            int photon_id = start + first + b;
+            int tri = last_hit[photon_id];
+            if (tri <= -1) continue;                              /* daq.cu:120-122 (wire-plane -2: not detected) */
+            int solid_id = (int)solid_map[tri];
+            uint32_t history = flags[photon_id];
+            int c = s2c[solid_id];
+            if (c < 0 || !(history & detection_state)) continue;
+            float photon_time = t[photon_id];
+            float w = weights[photon_id] * global_weight;
+            for (int tx = 0; tx < ntpb; ++tx) {
+                uint32_t slot = (uint32_t)(tx + ntpb * b);
+                chr_xorwow r;
+                rng_load(rng, nslots, slot, &r);
+                uint32_t nflag = normal_cache[slot], nextra = normal_cache[nslots + slot];
+                for (int i = tx; i < ndaq; i += ntpb) {
+                    int off = c + i * stride;
+                    if (chr_uniform01(&r) < w) {
+                        float time = photon_time + chr_normal(&r, &nflag, &nextra);
+                        time = time + sample_cdf_xy(&r, tlen, tcx, tcy);
+                        float charge = sample_cdf_xy(&r, qlen, qcx, qcy);
+                        daq_record(time_int, q_int, hist, off, time, charge, charge_unit, history);
+                    }
+                }
+                rng_store(rng, nslots, slot, &r);
+                normal_cache[slot] = nflag;
+                normal_cache[nslots + slot] = nextra;
+            }
+        }
+        first += count;
+    }
+    return 0;
+}

@@ -27,6 +27,9 @@ def lib():
         l = ctypes.CDLL(LIBPATH)
         vp, u32, i32, u64 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int, ctypes.c_ulonglong
         l.orc_rng_init.argtypes = [vp, u32, u64, u64]
+        l.orc_rng_init_subseq.argtypes = [vp, u32, u64, u64, u64]
+        l.orc_daq.argtypes = [vp] * 8 + [i32, vp, vp, i32, ctypes.c_float, vp, u32, vp, u32, i32, i32,
+                                         vp, vp, vp, i32, i32, ctypes.c_float, i32, i32]
         l.orc_sequence_matrices.argtypes = [vp, i32]
         l.orc_rng_uniforms.argtypes = [vp, u32, u32, i32, vp]
         l.orc_distance_to_mesh.argtypes = [vp, i32, vp, vp, vp, vp, vp]
@@ -42,9 +45,9 @@ def _p(a):
     return a.ctypes.data if a is not None else None
 
 
-def rng_init(nslots, seed=1, offset=0):
+def rng_init(nslots, seed=1, offset=0, first_subsequence=0):
     st = np.zeros(6 * nslots, dtype=np.uint32)
-    lib().orc_rng_init(_p(st), nslots, seed, offset)
+    lib().orc_rng_init_subseq(_p(st), nslots, seed, first_subsequence, offset)
     return st
 
 
@@ -149,3 +152,36 @@ def hits(photons, solid_id, solid_id_to_channel_index, detection_state=0x4, star
 def select(photons, target_flag, start=0, n=None):
     n = len(photons) - start if n is None else n
     return np.flatnonzero((np.asarray(photons.flags[start:start + n]) & target_flag) != 0) + start
+
+
+def daq(photons, solid_id, solid_id_to_channel_index, time_cdf, charge_cdf, charge_unit, rng_states, nslots,
+        normal_cache=None, start=0, n=None, ndaq=1, nchannels=None, global_weight=1.0, nthreads_per_block=64,
+        max_blocks=1024, detection_state=0x4, maxtime=1e9, raw=False):
+    """GPUDaq begin/acquire/end (daq.py:56-101) on the host.  time_cdf /
+    charge_cdf are the (x, y) arrays as the device holds them (equal lengths).
+    rng_states / normal_cache are updated in place.  Returns (t, q, flags),
+    each of ndaq*nchannels entries (raw=True: the u32 words before end_acquire)."""
+    n = len(photons) - start if n is None else n
+    nchannels = int(nchannels)
+    total = nchannels * ndaq
+    time_int = np.full(total, np.float32(maxtime).view(np.uint32), dtype=np.uint32)
+    q_int = np.zeros(total, dtype=np.uint32)
+    hist = np.zeros(total, dtype=np.uint32)
+    if normal_cache is None:
+        normal_cache = np.zeros(2 * nslots, dtype=np.uint32)
+    a = [np.ascontiguousarray(x, dtype=np.float32) for x in (time_cdf[0], time_cdf[1], charge_cdf[0], charge_cdf[1])]
+    sm = np.ascontiguousarray(solid_id, dtype=np.uint32)
+    s2c = np.ascontiguousarray(solid_id_to_channel_index, dtype=np.int32)
+    rc = lib().orc_daq(_p(photons.t), _p(photons.flags), _p(photons.last_hit_triangles), _p(photons.weights),
+                       _p(sm), _p(s2c), _p(a[0]), _p(a[1]), len(a[0]), _p(a[2]), _p(a[3]), len(a[2]),
+                       float(charge_unit), _p(rng_states), nslots, _p(normal_cache), detection_state, start, n,
+                       _p(time_int), _p(q_int), _p(hist), ndaq, nchannels, float(global_weight),
+                       nthreads_per_block, max_blocks)
+    if rc != 0:
+        raise RuntimeError('orc_daq failed with status %d' % rc)
+    if raw:          # the u32 accumulator words (time bits, quantised charge, history)
+        return time_int, q_int, hist
+    t = time_int.view(np.float32).copy()
+    q = np.zeros(total, dtype=np.float32)
+    q[:nchannels] = q_int[:nchannels].astype(np.float32) * np.float32(charge_unit)
+    return t, q, hist

@@ -6,6 +6,7 @@ half the bytes of wide coalesced reads, so it is doubled here -- an upper-bound
 correction for the narrower gathers of the BVH walk, whose calibration is
 unknown).  Prints one JSON object."""
 import csv
+import re
 import glob
 import json
 import os
@@ -25,7 +26,12 @@ def per_kernel(d, counter):
                 vals[key] = vals.get(key, 0.0) + float(row['Counter_Value'])
     out = {}
     for (_, name), v in vals.items():
-        short = 'chr::propagate_kernel' if 'propagate_kernel' in name else name.split('(')[0]
+        if re.search(r'propagate_(step_)?kernel<[^>]*, false>', name):
+            short = 'chr::propagate_kernel'
+        elif 'propagate' in name and 'kernel' in name and ', true>' in name:
+            short = 'counting_variant'
+        else:
+            short = name.split('(')[0]
         out.setdefault(short, []).append(v)
     return out
 

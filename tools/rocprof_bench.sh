@@ -14,9 +14,9 @@ mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 export CHROMA_BENCH_CACHE=/tmp/chroma_bench_cache
 timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- \
-    python3 "$R/bench.py" --no-cpu-baseline "$@" > "$OUT/bench_trace.json" 2> "$OUT/bench_trace.log" || exit $?
+    python3 "$R/bench.py" --no-cpu-baseline --no-count "$@" > "$OUT/bench_trace.json" 2> "$OUT/bench_trace.log" || exit $?
 timeout -k 10 900 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch" -o run -- \
-    python3 "$R/bench.py" --no-cpu-baseline "$@" > "$OUT/bench_fetch.json" 2> "$OUT/bench_fetch.log" || exit $?
+    python3 "$R/bench.py" --no-cpu-baseline --no-count "$@" > "$OUT/bench_fetch.json" 2> "$OUT/bench_fetch.log" || exit $?
 timeout -k 10 900 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write" -o run -- \
-    python3 "$R/bench.py" --no-cpu-baseline "$@" > "$OUT/bench_write.json" 2> "$OUT/bench_write.log" || exit $?
+    python3 "$R/bench.py" --no-cpu-baseline --no-count "$@" > "$OUT/bench_write.json" 2> "$OUT/bench_write.log" || exit $?
 python3 "$R/tools/pmc_traffic.py" "$OUT" > "$OUT/pmc_traffic.json"
