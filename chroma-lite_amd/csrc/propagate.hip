@@ -272,7 +272,10 @@ __device__ __forceinline__ int intersect_mesh(const DevGeom &g, V3 o, V3 d, floa
 // why the tested set covers the reference's).  Stack: top WIDE_LDS entries
 // (node, entry distance) in LDS, the rest in scratch; nearest inner child
 // first, the others pushed and culled at pop against the running best.
-constexpr int WIDE_LDS = 16;
+constexpr int WIDE_LDS = 12;
+constexpr int LEAFQ = 16;          // per-lane parked-leaf queue (speculative walk), LDS
+// LDS words per work-item: traversal stack (node + entry distance) [+ leaf queue]
+constexpr int lds_words(int wide) { return wide >= 2000 ? 2 * WIDE_LDS + LEAFQ : (wide ? 2 * WIDE_LDS : 0); }
 
 // The LDS column pointers are typed (ds_* ops) and the scratch spill array is
 // a separate object: an object holding both lives in scratch and its LDS
@@ -282,6 +285,7 @@ struct WStack {
     CHR_LDS uint32_t *node;   // this work-item's LDS column: entry i at node[i * BLOCK]
     CHR_LDS float *dist;
     uint2 *spill;             // entries >= WIDE_LDS (scratch)
+    CHR_LDS uint32_t *leafq;  // parked leaves (speculative walk): entry i at leafq[i * BLOCK]
 };
 __device__ __forceinline__ void wpush(WStack &s, int i, uint32_t n, float t) {
     if (i < WIDE_LDS) { s.node[i * BLOCK] = n; s.dist[i * BLOCK] = t; }
@@ -547,6 +551,105 @@ __device__ int intersect_wide_sched(const DevGeom &g, V3 o, V3 d, float &min_dis
     return best_id;
 }
 
+// Speculative variant of the scheduled walk (Aila & Laine 2009, "speculative
+// traversal"): a lane that reaches leaves parks them in a small LDS queue and
+// keeps walking (with the best it has so far) while the queue has room for a
+// node's worth of leaves; the WAVE runs a triangle step only once at least
+// F/8 of its live lanes have parked triangles (or no lane can walk), so the
+// triangle steps run with most lanes busy instead of a handful.  Each lane
+// still tests its own triangles in the order it found them, with the accept
+// rule and reference leaf check of intersect_wide_sched; walking ahead with a
+// best that is not yet updated only adds nodes/triangles to what is tested
+// (a superset: culling uses a best that never drops below the final one), so
+// the nearest hit is unchanged.
+// Leaf queue entry: first triangle record (bits 0-29) | (count-1) << 30.
+template <bool COUNT, int F>
+__device__ int intersect_wide_spec(const DevGeom &g, V3 o, V3 d, float &min_distance, int last_hit, WStack &st,
+                                   uint32_t &overflow, WalkCounts &cnt) {
+    if constexpr (COUNT) cnt.walks++;
+    const V3 noid = v3(-o.x / d.x, -o.y / d.y, -o.z / d.z);
+    const V3 inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    const RaySlab slab = make_slab(noid, inv);
+    float best = __builtin_inff();
+    uint32_t best_rank = 0xFFFFFFFFu;
+    int best_id = -1;
+    const uint32_t last = (uint32_t)last_hit;
+    int sp = 0;
+    uint32_t node = 0;
+    bool done = false;
+    uint32_t qh = 0, qt = 0;        // queue head / tail (free-running; slot = x % LEAFQ)
+    uint32_t pcur = 0, pleft = 0;   // leaf being tested
+    constexpr uint32_t INVALID = 0xFFFFFFFFu;
+    while (true) {
+        const bool has_work = pleft != 0 || qh != qt;
+        const bool can_walk = !done && (qt - qh) <= (uint32_t)(LEAFQ - 8);
+        const unsigned long long mw = __ballot(can_walk);
+        const unsigned long long mt = __ballot(has_work);
+        if ((mw | mt) == 0) break;
+        if (mw != 0 && 8 * __popcll(mt) < F * __popcll(mw | mt)) {
+            // ------------------------------------------------ node step
+            if (!can_walk) continue;
+            if (node == INVALID) {
+                bool found = false;
+                while (sp > 0) {
+                    sp--;
+                    float t;
+                    wpop(st, sp, node, t);
+                    if (!(t > best)) { found = true; break; }
+                }
+                if (!found) { done = true; continue; }
+            }
+            if constexpr (COUNT) { cnt.nodes++; if (wave_leader()) cnt.wave_nodes++; }
+            const uint4 *np = g.wnodes + 6 * (size_t)node;
+            const uint4 h = gld(np), a1 = gld(np + 1), a2 = gld(np + 2), a3 = gld(np + 3), a4 = gld(np + 4),
+                        a5 = gld(np + 5);
+            uint32_t near_node;
+            float near_t;
+            uint32_t leaf_mask = expand_node(h, a1, a2, a3, a4, a5, slab, best, near_node, near_t, st, sp, overflow);
+            node = near_node;
+            while (leaf_mask) {
+                const int k = __builtin_ctz(leaf_mask);
+                leaf_mask &= leaf_mask - 1;
+                const uint32_t kind = ((k < 4 ? a4.z : a4.w) >> (8 * (k & 3))) & 0xFFu;
+                const uint32_t first = a4.y + (((k < 4 ? a5.x : a5.y) >> (8 * (k & 3))) & 0xFFu);
+                st.leafq[(qt % LEAFQ) * BLOCK] = first | ((kind - 1u) << 30);
+                qt++;
+            }
+        } else {
+            // ------------------------------------------------ triangle step
+            if (!has_work) continue;
+            if (pleft == 0) {
+                const uint32_t e = st.leafq[(qh % LEAFQ) * BLOCK];
+                qh++;
+                pcur = e & 0x3FFFFFFFu;
+                pleft = (e >> 30) + 1u;
+            }
+            if constexpr (COUNT) { cnt.tris++; if (wave_leader()) cnt.wave_tris++; }
+            const float4 *r = g.wtri + 4 * (size_t)pcur;
+            const float4 r0 = gld(r), r1 = gld(r + 1), r2 = gld(r + 2);
+            pcur++;
+            pleft--;
+            const uint32_t id = __float_as_uint(r2.y);
+            float dist;
+            if (id == last ||
+                !intersect_triangle(o, d, v3(r0.x, r0.y, r0.z), v3(r0.w, r1.x, r1.y), v3(r1.z, r1.w, r2.x), dist))
+                continue;
+            const uint32_t rank = __float_as_uint(r2.z);
+            if (!(dist < best || (dist == best && rank < best_rank))) continue;
+            const float4 r3 = gld(r + 3);
+            V3 lo, hi;
+            node_bounds(g, make_uint4(__float_as_uint(r2.w), __float_as_uint(r3.x), __float_as_uint(r3.y), 0u), lo, hi);
+            float bd;
+            if (!intersect_box(noid, inv, lo, hi, bd) || bd > best) continue;   // mesh.h:94-96
+            best = dist;
+            best_rank = rank;
+            best_id = (int)id;
+        }
+    }
+    min_distance = best_id == -1 ? -1.0f : best;
+    return best_id;
+}
+
 // ---------------------------------------------------------------- photon.h
 __device__ __forceinline__ int convert(int c) { return (c & 0x80) ? (int)(0xFFFFFF00u | (uint32_t)c) : c; }
 __device__ __forceinline__ float get_theta(V3 a, V3 b) { return chr_acosf(fmax_(-1.0f, fmin_(1.0f, dot(a, b)))); }
@@ -660,6 +763,9 @@ __device__ __forceinline__ void fill_state(const DevGeom &g, State &s, Photon &p
     int mesh_triangle;
     if constexpr (WIDE == 1)
         mesh_triangle = intersect_wide<COUNT>(g, p.pos, p.dir, s.distance, p.last_hit, wst, overflow, cnt);
+    else if constexpr (WIDE >= 2000)   // speculative walk, triangle-step threshold (WIDE - 2000)/8 of live lanes
+        mesh_triangle =
+            intersect_wide_spec<COUNT, WIDE - 2000>(g, p.pos, p.dir, s.distance, p.last_hit, wst, overflow, cnt);
     else if constexpr (WIDE >= 1000)   // scheduled walk, triangle batch threshold WIDE - 1000
         mesh_triangle =
             intersect_wide_sched<COUNT, WIDE - 1000>(g, p.pos, p.dir, s.distance, p.last_hit, wst, overflow, cnt);
@@ -1228,7 +1334,7 @@ __device__ __forceinline__ void flush_counters(const PropagateArgs &a, uint32_t 
 // 1000 + b: wide BVH scheduled walk, triangle batch threshold b (0: per-lane choice).
 template <int BATCH, int MINW, int WIDE, bool COUNT = false>
 __global__ __launch_bounds__(BLOCK, MINW) void propagate_kernel(const DevGeom *__restrict__ gdev, PropagateArgs a) {
-    __shared__ uint32_t lds_stack[WIDE ? 2 * WIDE_LDS * BLOCK : STACK_LDS * BLOCK];
+    __shared__ uint32_t lds_stack[WIDE ? lds_words(WIDE) * BLOCK : STACK_LDS * BLOCK];
     const int tid = blockIdx.x * BLOCK + threadIdx.x;
     unsigned alive = 0;
     // A photon's RNG slot and queue position are its slot id, whichever
@@ -1248,6 +1354,8 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_kernel(const DevGeom *_
             wst.spill = wspill;
             wst.node = (CHR_LDS uint32_t *)(lds_stack + threadIdx.x);
             wst.dist = (CHR_LDS float *)(lds_stack + WIDE_LDS * BLOCK + threadIdx.x);
+    wst.leafq = (CHR_LDS uint32_t *)(lds_stack + 2 * WIDE_LDS * BLOCK + threadIdx.x);
+            wst.leafq = (CHR_LDS uint32_t *)(lds_stack + 2 * WIDE_LDS * BLOCK + threadIdx.x);
             uint32_t overflow = 0;
             WalkCounts cnt{0u, 0u, 0u, 0u, 0u};
             const DevGeom &g = *gdev;   // device-resident: uniform s_loads, no private copy
@@ -1278,7 +1386,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_kernel(const DevGeom *_
 template <int BATCH, int MINW, int WIDE, bool COUNT = false>
 __global__ __launch_bounds__(BLOCK, MINW) void propagate_step_kernel(const DevGeom *__restrict__ gdev,
                                                                      PropagateArgs a, uint32_t cap) {
-    __shared__ uint32_t lds_stack[WIDE ? 2 * WIDE_LDS * BLOCK : STACK_LDS * BLOCK];
+    __shared__ uint32_t lds_stack[WIDE ? lds_words(WIDE) * BLOCK : STACK_LDS * BLOCK];
     const uint32_t slot = blockIdx.x * BLOCK + threadIdx.x;
     const uint32_t n = (uint32_t)a.nthreads;   // queue length of this step
     // whole waves only (cap % 64 == 0); the partial last wave of a short queue
@@ -1291,6 +1399,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_step_kernel(const DevGe
     wst.spill = wspill;
     wst.node = (CHR_LDS uint32_t *)(lds_stack + threadIdx.x);
     wst.dist = (CHR_LDS float *)(lds_stack + WIDE_LDS * BLOCK + threadIdx.x);
+    wst.leafq = (CHR_LDS uint32_t *)(lds_stack + 2 * WIDE_LDS * BLOCK + threadIdx.x);
     uint32_t overflow = 0;
     WalkCounts cnt{0u, 0u, 0u, 0u, 0u};
     const DevGeom &g = *gdev;
@@ -1502,7 +1611,7 @@ __global__ __launch_bounds__(BLOCK) void duplicate_kernel(PhotonPtrs ph, int32_t
 template <bool WIDE>
 __global__ __launch_bounds__(BLOCK) void distance_kernel(const DevGeom *__restrict__ gdev, uint32_t n, const float *origin, const float *dir,
                                                           float *distance, uint32_t *counters) {
-    __shared__ uint32_t lds_stack[WIDE ? 2 * WIDE_LDS * BLOCK : STACK_LDS * BLOCK];
+    __shared__ uint32_t lds_stack[WIDE ? lds_words(WIDE) * BLOCK : STACK_LDS * BLOCK];
     const uint32_t id = blockIdx.x * BLOCK + threadIdx.x;
     if (id >= n) return;
     const DevGeom &g = *gdev;
@@ -1517,6 +1626,7 @@ __global__ __launch_bounds__(BLOCK) void distance_kernel(const DevGeom *__restri
         st.spill = wspill;
         st.node = (CHR_LDS uint32_t *)(lds_stack + threadIdx.x);
         st.dist = (CHR_LDS float *)(lds_stack + WIDE_LDS * BLOCK + threadIdx.x);
+        st.leafq = nullptr;
         WalkCounts cnt;
         tri = intersect_wide_sched<false, 2>(g, o, d, dist, -1, st, overflow, cnt);
     } else {
@@ -1669,11 +1779,17 @@ static propagate_step_fn select_step_variant(const chr_geometry *g) {
     const char *e = getenv("CHR_PROPAGATE_VARIANT");
     int v = e ? atoi(e) : 0;
     if (g->dev.nwnodes == 0) v = kExactVariant;
+    if (v >= 12 && g->dev.nwtri >= (1u << 30)) v = 0;   // leaf-queue entries hold 30-bit record indices
     switch (v) {
         case 1: return propagate_step_kernel<8, 4, 0>;
         case 5: return propagate_step_kernel<8, 4, 1002, true>;
         case 8: return propagate_step_kernel<8, 3, 1002>;
         case 9: return propagate_step_kernel<8, 5, 1002>;
+        case 12: return propagate_step_kernel<8, 4, 2002>;
+        case 14: return propagate_step_kernel<8, 4, 2004>;
+        case 15: return propagate_step_kernel<8, 4, 2004, true>;
+        case 16: return propagate_step_kernel<8, 4, 2006>;
+        case 18: return propagate_step_kernel<8, 4, 2008>;
         default: return propagate_step_kernel<8, 4, 1002>;
     }
 }
