@@ -55,9 +55,10 @@ struct DevGeom {
     const DevMaterial *materials;
     const DevSurface *surfaces;
     const chr_wireplane_desc *wireplanes;
-    const uint4 *wnodes;             // 8-wide SAH BVH, 6 uint4 per node (wide_bvh.h)
+    const uint4 *wnodes;             // 8-wide SAH BVH, node i at wnodes[wstride * i] (wide_bvh.h)
     const float4 *wtri;              // 3 float4 per leaf triangle record (wide_bvh.h)
     uint32_t nwnodes, nwtri;
+    uint32_t wstride;                // uint4 per node slot: 8 (96-byte node padded to one 128-byte line) or 6
     float ox, oy, oz, scale;         // world_origin, world_scale
     uint32_t nnodes, ntriangles, nwireplanes;
     uint32_t wl_n;
@@ -75,4 +76,6 @@ struct chr_geometry {
     uint64_t bytes;
     void *allocs[12];
     int nallocs;
+    const uint4 *wnodes_alt;   // the other node layout (only with CHR_NODE_LAYOUT_AB set at creation; A/B tooling)
+    uint32_t wstride_alt;
 };

@@ -396,7 +396,7 @@ __device__ int intersect_wide(const DevGeom &g, V3 o, V3 d, float &min_distance,
     uint32_t node = 0;
     while (true) {
         if constexpr (COUNT) { cnt.nodes++; if (wave_leader()) cnt.wave_nodes++; }
-        const uint4 *np = g.wnodes + 6 * (size_t)node;
+        const uint4 *np = g.wnodes + (size_t)g.wstride * node;
         const uint4 h = gld(np), a1 = gld(np + 1), a2 = gld(np + 2), a3 = gld(np + 3), a4 = gld(np + 4),
                     a5 = gld(np + 5);
         uint32_t near_node;
@@ -500,7 +500,7 @@ __device__ int intersect_wide_sched(const DevGeom &g, V3 o, V3 d, float &min_dis
                 if (!found) { done = true; continue; }
             }
             if constexpr (COUNT) { cnt.nodes++; if (wave_leader()) cnt.wave_nodes++; }
-            const uint4 *np = g.wnodes + 6 * (size_t)node;
+            const uint4 *np = g.wnodes + (size_t)g.wstride * node;
             const uint4 h = gld(np), a1 = gld(np + 1), a2 = gld(np + 2), a3 = gld(np + 3), a4 = gld(np + 4),
                         a5 = gld(np + 5);
             uint32_t near_node;
@@ -600,7 +600,7 @@ __device__ int intersect_wide_spec(const DevGeom &g, V3 o, V3 d, float &min_dist
                 if (!found) { done = true; continue; }
             }
             if constexpr (COUNT) { cnt.nodes++; if (wave_leader()) cnt.wave_nodes++; }
-            const uint4 *np = g.wnodes + 6 * (size_t)node;
+            const uint4 *np = g.wnodes + (size_t)g.wstride * node;
             const uint4 h = gld(np), a1 = gld(np + 1), a2 = gld(np + 2), a3 = gld(np + 3), a4 = gld(np + 4),
                         a5 = gld(np + 5);
             uint32_t near_node;
@@ -1465,18 +1465,44 @@ __global__ __launch_bounds__(BLOCK) void sort_key_kernel(const float *pos, const
     vals[t] = (uint32_t)t;
 }
 
-// exclusive scan of the popcounts of nwords masks (single workgroup);
-// word_offsets[i] = survivors before word i; base[0] = out_counter[0] on entry;
-// out_counter[0] += total.
-__global__ __launch_bounds__(1024) void scan_masks_kernel(const unsigned long long *masks, uint32_t nwords,
-                                                          uint32_t *word_offsets, uint32_t *out_counter,
-                                                          uint32_t *base, uint32_t *total_out) {
+// Two-level exclusive scan of the popcounts of nwords alive/selection masks.
+// mask_block_scan_kernel: workgroup b scans words [256b, 256b+256) -> word_offsets
+// (exclusive within the workgroup) and block_sums[b]; scan_block_sums_kernel
+// (one workgroup) turns block_sums into exclusive block prefixes, records
+// base[0] = out_counter[0] on entry, out_counter[0] += total, total_out = total.
+// Consumers add block_prefix[w >> 8] to word_offsets[w].
+constexpr int SCAN_WORDS = 256;
+__global__ __launch_bounds__(SCAN_WORDS) void mask_block_scan_kernel(const unsigned long long *masks, uint32_t nwords,
+                                                                     uint32_t *word_offsets, uint32_t *block_sums) {
+    __shared__ uint32_t wave_tot[SCAN_WORDS / 64];
+    const uint32_t w = blockIdx.x * SCAN_WORDS + threadIdx.x;
+    const uint32_t c = w < nwords ? (uint32_t)__popcll(masks[w]) : 0u;
+    // inclusive scan within the wave (shuffles), then across the 4 waves
+    uint32_t x = c;
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(x, off, 64);
+        if (lane >= off) x += y;
+    }
+    const int wid = threadIdx.x >> 6;
+    if (lane == 63) wave_tot[wid] = x;
+    __syncthreads();
+    uint32_t before = 0;
+    for (int k = 0; k < wid; ++k) before += wave_tot[k];
+    if (w < nwords) word_offsets[w] = before + x - c;
+    if (threadIdx.x == SCAN_WORDS - 1) block_sums[blockIdx.x] = before + x;
+}
+
+__global__ __launch_bounds__(1024) void scan_block_sums_kernel(uint32_t *block_sums, uint32_t nblocks,
+                                                               uint32_t *out_counter, uint32_t *base,
+                                                               uint32_t *total_out) {
     __shared__ uint32_t partial[1024];
     const uint32_t tid = threadIdx.x;
-    const uint32_t per = (nwords + 1023) / 1024;
-    const uint32_t w0 = tid * per;
+    const uint32_t per = (nblocks + 1023) / 1024;
+    const uint32_t b0 = tid * per;
     uint32_t sum = 0;
-    for (uint32_t k = 0; k < per && w0 + k < nwords; ++k) sum += __popcll(masks[w0 + k]);
+    for (uint32_t k = 0; k < per && b0 + k < nblocks; ++k) sum += block_sums[b0 + k];
     partial[tid] = sum;
     __syncthreads();
     for (uint32_t off = 1; off < 1024; off <<= 1) {
@@ -1486,9 +1512,10 @@ __global__ __launch_bounds__(1024) void scan_masks_kernel(const unsigned long lo
         __syncthreads();
     }
     uint32_t run = partial[tid] - sum;
-    for (uint32_t k = 0; k < per && w0 + k < nwords; ++k) {
-        word_offsets[w0 + k] = run;
-        run += __popcll(masks[w0 + k]);
+    for (uint32_t k = 0; k < per && b0 + k < nblocks; ++k) {
+        const uint32_t v = block_sums[b0 + k];
+        block_sums[b0 + k] = run;
+        run += v;
     }
     if (tid == 1023) {
         const uint32_t total = partial[1023];
@@ -1498,16 +1525,21 @@ __global__ __launch_bounds__(1024) void scan_masks_kernel(const unsigned long lo
     }
 }
 
+__device__ __forceinline__ uint32_t word_offset(const uint32_t *word_offsets, const uint32_t *block_prefix, uint32_t w) {
+    return word_offsets[w] + block_prefix[w / SCAN_WORDS];
+}
+
 __global__ __launch_bounds__(BLOCK) void scatter_queue_kernel(const unsigned long long *masks, const uint32_t *word_offsets,
-                                                               const uint32_t *base, const uint32_t *in_queue,
-                                                               int32_t first, int32_t n, uint32_t *out_queue) {
+                                                               const uint32_t *block_prefix, const uint32_t *base,
+                                                               const uint32_t *in_queue, int32_t first, int32_t n,
+                                                               uint32_t *out_queue) {
     const int id = blockIdx.x * BLOCK + threadIdx.x;
     if (id >= n) return;
     const unsigned long long m = masks[id >> 6];
     const int lane = id & 63;
     if ((m >> lane) & 1ull) {
         const uint32_t rank = __popcll(m & ((1ull << lane) - 1ull));
-        out_queue[base[0] + word_offsets[id >> 6] + rank] = in_queue[first + id];
+        out_queue[base[0] + word_offset(word_offsets, block_prefix, (uint32_t)id >> 6) + rank] = in_queue[first + id];
     }
 }
 
@@ -1575,7 +1607,8 @@ __global__ __launch_bounds__(BLOCK) void flag_kernel(PhotonPtrs ph, int32_t star
 
 __global__ __launch_bounds__(BLOCK) void copy_selected_kernel(PhotonPtrs ph, int32_t start, int32_t n,
                                                                const unsigned long long *masks,
-                                                               const uint32_t *word_offsets, PhotonPtrs out,
+                                                               const uint32_t *word_offsets,
+                                                               const uint32_t *block_prefix, PhotonPtrs out,
                                                                int32_t *channels, const uint32_t *solid_map,
                                                                const int32_t *solid_to_channel) {
     const int id = blockIdx.x * BLOCK + threadIdx.x;
@@ -1583,7 +1616,7 @@ __global__ __launch_bounds__(BLOCK) void copy_selected_kernel(PhotonPtrs ph, int
     const unsigned long long m = masks[id >> 6];
     const int lane = id & 63;
     if (!((m >> lane) & 1ull)) return;
-    const uint32_t o = word_offsets[id >> 6] + __popcll(m & ((1ull << lane) - 1ull));
+    const uint32_t o = word_offset(word_offsets, block_prefix, (uint32_t)id >> 6) + __popcll(m & ((1ull << lane) - 1ull));
     const uint32_t i = (uint32_t)(start + id);
     copy_photon(ph, i, out, o);
     if (channels) channels[o] = solid_to_channel[solid_map[ph.last_hit[i]]];
@@ -1646,6 +1679,18 @@ using namespace chr;
 namespace {
 
 inline unsigned grid_for(uint64_t n) { return (unsigned)((n + BLOCK - 1) / BLOCK); }
+
+inline uint32_t scan_blocks(uint32_t nwords) { return (nwords + SCAN_WORDS - 1) / SCAN_WORDS; }
+
+// word_offsets (nwords) + block prefixes (scan_blocks(nwords)) of the masks
+void launch_mask_scan(const unsigned long long *masks, uint32_t nwords, uint32_t *word_offsets, uint32_t *block_sums,
+                      uint32_t *out_counter, uint32_t *base, uint32_t *total_out, hipStream_t stream) {
+    const uint32_t nb = scan_blocks(nwords);
+    if (nb) hipLaunchKernelGGL(mask_block_scan_kernel, dim3(nb), dim3(SCAN_WORDS), 0, stream, masks, nwords, word_offsets,
+                               block_sums);
+    hipLaunchKernelGGL(scan_block_sums_kernel, dim3(1), dim3(1024), 0, stream, block_sums, nb, out_counter, base,
+                       total_out);
+}
 
 PhotonPtrs to_ptrs(const chr_photons *p) {
     return PhotonPtrs{p->d_pos, p->d_dir, p->d_pol, p->d_wavelengths, p->d_t, p->d_weights, p->d_flags,
@@ -1740,12 +1785,15 @@ static size_t sort_temp_bytes(uint32_t n) {
     return bytes;
 }
 
-// u32 words: [0..7] counters | masks (2 per 64 slots) | offsets (1 per 64) |
-// sort keys in/out + order in/out (n each) | rocprim sort temporary storage
+// u32 words: [0..15] counters | masks (2 per 64 slots) | offsets (1 per 64) |
+// block prefixes (1 per 256 words, +2) | sort keys in/out + order in/out (n each) |
+// rocprim sort temporary storage
+static uint64_t mask_scan_words(uint64_t n) {   // masks + offsets + block prefixes for n positions
+    const uint64_t nwords = (n + 63) / 64;
+    return 2 * nwords + nwords + scan_blocks((uint32_t)nwords) + 2;
+}
 extern "C" uint64_t chr_propagate_scratch_words(uint32_t nthreads) {
-    const uint64_t nwords = (nthreads + 63) / 64;
-    return 16 + 2 * nwords /*masks*/ + nwords /*offsets*/ + 4 * (uint64_t)nthreads + 64 +
-           (sort_temp_bytes(nthreads) + 3) / 4;
+    return 16 + mask_scan_words(nthreads) + 4 * (uint64_t)nthreads + 64 + (sort_temp_bytes(nthreads) + 3) / 4;
 }
 
 // Kernel variants (A/B-able at run time with CHR_PROPAGATE_VARIANT=<n>;
@@ -1811,6 +1859,7 @@ static int launch_chunk(const chr_geometry *g, const chr_photons *ph, uint32_t *
     uint32_t *counters = scratch;               // [0] overflows, [1] base
     unsigned long long *masks = (unsigned long long *)(scratch + 16);
     uint32_t *offsets = scratch + 16 + 2 * (size_t)nwords;
+    uint32_t *bsums = offsets + nwords;
     PropagateArgs a;
     a.pos = ph->d_pos; a.dir = ph->d_dir; a.pol = ph->d_pol; a.wl = ph->d_wavelengths; a.t = ph->d_t;
     a.weights = ph->d_weights; a.flags = ph->d_flags; a.last_hit = ph->d_last_hit_triangles; a.evidx = ph->d_evidx;
@@ -1821,7 +1870,7 @@ static int launch_chunk(const chr_geometry *g, const chr_photons *ph, uint32_t *
     if (sort_enabled() && nthreads >= kSortMin) {
         // coherence order (sort_key_kernel): rays that start close together in
         // similar directions share a wave
-        uint32_t *keys = offsets + nwords;
+        uint32_t *keys = bsums + scan_blocks(nwords) + 2;
         uint32_t *keys_out = keys + nthreads, *vals = keys_out + nthreads, *vals_out = vals + nthreads;
         void *temp = (void *)(((uintptr_t)(vals_out + nthreads) + 255) & ~(uintptr_t)255);
         size_t temp_bytes = sort_temp_bytes((uint32_t)nthreads);
@@ -1838,9 +1887,8 @@ static int launch_chunk(const chr_geometry *g, const chr_photons *ph, uint32_t *
     hipLaunchKernelGGL(select_variant(g), dim3(grid_for(nthreads)), dim3(BLOCK), 0, stream,
                        (const DevGeom *)g->d_dev, a);
     if (ev1) CHR_HIP_CHECK(hipEventRecord(ev1, stream));
-    hipLaunchKernelGGL(scan_masks_kernel, dim3(1), dim3(1024), 0, stream, masks, nwords, offsets, out_queue,
-                       counters + 1, (uint32_t *)nullptr);
-    hipLaunchKernelGGL(scatter_queue_kernel, dim3(grid_for(nthreads)), dim3(BLOCK), 0, stream, masks, offsets,
+    launch_mask_scan(masks, nwords, offsets, bsums, out_queue, counters + 1, nullptr, stream);
+    hipLaunchKernelGGL(scatter_queue_kernel, dim3(grid_for(nthreads)), dim3(BLOCK), 0, stream, masks, offsets, bsums,
                        counters + 1, in_queue, first, nthreads, out_queue);
     CHR_HIP_CHECK(hipGetLastError());
     return CHR_OK;
@@ -1857,6 +1905,7 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
     uint32_t *counters = scratch;
     unsigned long long *masks = (unsigned long long *)(scratch + 16);
     uint32_t *offsets = scratch + 16 + 2 * (size_t)nwords;
+    uint32_t *bsums = offsets + nwords;
     PropagateArgs a;
     a.pos = ph->d_pos; a.dir = ph->d_dir; a.pol = ph->d_pol; a.wl = ph->d_wavelengths; a.t = ph->d_t;
     a.weights = ph->d_weights; a.flags = ph->d_flags; a.last_hit = ph->d_last_hit_triangles; a.evidx = ph->d_evidx;
@@ -1869,9 +1918,8 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
     hipLaunchKernelGGL(select_step_variant(g), dim3(grid_for(threads)), dim3(BLOCK), 0, stream,
                        (const DevGeom *)g->d_dev, a, cap);
     if (ev1) CHR_HIP_CHECK(hipEventRecord(ev1, stream));
-    hipLaunchKernelGGL(scan_masks_kernel, dim3(1), dim3(1024), 0, stream, masks, nwords, offsets, out_queue,
-                       counters + 1, (uint32_t *)nullptr);
-    hipLaunchKernelGGL(scatter_queue_kernel, dim3(grid_for(n)), dim3(BLOCK), 0, stream, masks, offsets,
+    launch_mask_scan(masks, nwords, offsets, bsums, out_queue, counters + 1, nullptr, stream);
+    hipLaunchKernelGGL(scatter_queue_kernel, dim3(grid_for(n)), dim3(BLOCK), 0, stream, masks, offsets, bsums,
                        counters + 1, in_queue, 0, (int32_t)n, out_queue);
     CHR_HIP_CHECK(hipGetLastError());
     return CHR_OK;
@@ -1915,6 +1963,21 @@ static int timing_events(size_t n, std::vector<hipEvent_t> **out) {
     return CHR_OK;
 }
 
+// A/B of the node layouts (CHR_NODE_LAYOUT=96|128, read per launch; only when
+// the geometry was created with CHR_NODE_LAYOUT_AB set): swap the live layout
+static int apply_node_layout(const chr_geometry *cg, hipStream_t stream) {
+    chr_geometry *g = const_cast<chr_geometry *>(cg);
+    if (!g->wnodes_alt) return CHR_OK;
+    const char *e = getenv("CHR_NODE_LAYOUT");
+    const uint32_t want = (e && atoi(e) == 96) ? 6u : 8u;
+    if (g->dev.wstride == want) return CHR_OK;
+    std::swap(g->dev.wnodes, g->wnodes_alt);
+    std::swap(g->dev.wstride, g->wstride_alt);
+    CHR_HIP_CHECK(hipMemcpyAsync(g->d_dev, &g->dev, sizeof(g->dev), hipMemcpyHostToDevice, stream));
+    CHR_HIP_CHECK(hipStreamSynchronize(stream));
+    return CHR_OK;
+}
+
 static bool step_launch_enabled() {   // CHR_STEP_LAUNCH=0: the reference's one-launch-per-chunk structure (A/B)
     const char *e = getenv("CHR_STEP_LAUNCH");
     return !(e && e[0] == '0');
@@ -1935,13 +1998,13 @@ extern "C" int chr_propagate(const chr_geometry *g, const chr_photons *ph, uint3
     hipStream_t stream = (hipStream_t)vstream;
     chr_propagate_stats st{};
     if (nphotons == 0) { if (stats) *stats = st; return CHR_OK; }
+    if (int lrc = apply_node_layout(g, stream)) return lrc;
     const uint64_t cap = (uint64_t)ntpb * max_blocks;   // slots of one chunk (chunk_iterator)
     const uint32_t chunk_cap = (uint32_t)std::min<uint64_t>(cap, nphotons);
     // one launch per step when a wave's 64 slots map to whole mask words
     const bool fused = (cap % 64 == 0) && cap <= 0x7FFFFFFFull && step_launch_enabled() && !sort_enabled();
-    const uint64_t nwords_all = (nphotons + 63) / 64;
     uint64_t swords = chr_propagate_scratch_words(chunk_cap);
-    if (fused) swords = std::max<uint64_t>(swords, 16 + 3 * nwords_all + 16);
+    if (fused) swords = std::max<uint64_t>(swords, 16 + mask_scan_words(nphotons) + 16);
     const size_t qbytes = ((size_t)nphotons + 1) * 4;
     void *buf = nullptr;
     int rc = scratch_get(2 * qbytes + swords * 4 + 64, &buf);
@@ -2047,16 +2110,16 @@ static int select_common(const chr_photons *ph, int32_t start, int32_t n, uint32
     if (n <= 0) return CHR_OK;
     const uint32_t nwords = (uint32_t)((n + 63) / 64);
     void *buf;
-    int rc = scratch_get((size_t)nwords * 12 + 64, &buf);
+    int rc = scratch_get((mask_scan_words((uint64_t)n) + 8) * 4 + 64, &buf);
     if (rc) return rc;
     uint32_t *cnt = (uint32_t *)buf;
     unsigned long long *masks = (unsigned long long *)((uint32_t *)buf + 8);
     uint32_t *offsets = (uint32_t *)buf + 8 + 2 * (size_t)nwords;
+    uint32_t *bsums = offsets + nwords;
     const PhotonPtrs p = to_ptrs(ph);
     hipLaunchKernelGGL(flag_kernel, dim3(grid_for(n)), dim3(BLOCK), 0, stream, p, start, n, state, solid_map, s2c, mode,
                        masks);
-    hipLaunchKernelGGL(scan_masks_kernel, dim3(1), dim3(1024), 0, stream, masks, nwords, offsets, (uint32_t *)nullptr,
-                       (uint32_t *)nullptr, cnt);
+    launch_mask_scan(masks, nwords, offsets, bsums, nullptr, nullptr, cnt, stream);
     CHR_HIP_CHECK(hipGetLastError());
     uint32_t total = 0;
     CHR_HIP_CHECK(hipMemcpyAsync(&total, cnt, 4, hipMemcpyDeviceToHost, stream));
@@ -2065,7 +2128,7 @@ static int select_common(const chr_photons *ph, int32_t start, int32_t n, uint32
     if (out && total > 0) {
         if (!photons_ok(out)) return chr::fail(CHR_ERR_INVALID, "selection: output buffers missing");
         hipLaunchKernelGGL(copy_selected_kernel, dim3(grid_for(n)), dim3(BLOCK), 0, stream, p, start, n, masks, offsets,
-                           to_ptrs(out), channels, solid_map, s2c);
+                           bsums, to_ptrs(out), channels, solid_map, s2c);
         CHR_HIP_CHECK(hipGetLastError());
         CHR_HIP_CHECK(hipStreamSynchronize(stream));
     }
