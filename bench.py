@@ -153,7 +153,7 @@ def roofline(args, cst, n, kernel_ms, launches):
           'traversals_per_photon': cst.traversals / n,
           'simd_efficiency_nodes': cst.nodes_visited / max(1.0, 64.0 * cst.wave_node_steps),
           'simd_efficiency_triangles': cst.triangles_tested / max(1.0, 64.0 * cst.wave_triangle_steps),
-          'kernel': 'chr::propagate_step_kernel<8,4,1002>',
+          'kernel': 'chr::propagate_step_kernel<8,4,2006> (speculative walk)',
           'avg_launch_ms': 1e3 * avg_launch_s}
     # HBM bytes per launch from the PMC passes (tools/rocprof_bench.sh) of this same workload
     pmc_path = os.path.join(ROOT, 'profiles', 'latest_pmc.json')
@@ -286,7 +286,7 @@ def main():
                                    'max_steps=%d, launch shape %dx%d (524,288 RNG slots)' % (
                                        args.photons, DETECTORS[args.detector][0], args.max_steps,
                                        args.nthreads_per_block, args.max_blocks),
-                       'detector': args.detector, 'photons_per_gpu': args.photons, 'triangles': len(det.mesh.triangles),
+                       'detector': args.detector, 'photons_per_gpu': args.photons, 'max_steps': args.max_steps, 'triangles': len(det.mesh.triangles),
                        'bvh_nodes': len(det.bvh.nodes), 'channels': det.num_channels(),
                        'parallelism': 'photon-sharded x%d, geometry replicated' % world},
             'detail': {'kernel_ms_per_step': kernel_ms / args.steps, 'launches_per_step': launches / args.steps,

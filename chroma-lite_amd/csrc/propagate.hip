@@ -372,9 +372,72 @@ __device__ __forceinline__ uint32_t expand_node(const uint4 h, const uint4 a1, c
     return leaf_mask;
 }
 
+// Branch-light form of expand_node for a lane whose LDS stack has room for a
+// whole node (sp + 7 <= WIDE_LDS): all eight slab tests first (no control
+// flow), the nearest hit inner child chosen with selects (first of the
+// smallest entry distance, as expand_node), then the other hit inner children
+// pushed in child order with predicated LDS stores.  The pushed set and the
+// near child are expand_node's; only the push order can differ (which changes
+// the walk's order, not what it finds: the nearest hit is argmin(distance,
+// reference rank) over a superset of the reference's tested triangles).
+__device__ __forceinline__ uint32_t expand_node_fast(const uint4 h, const uint4 a1, const uint4 a2, const uint4 a3,
+                                                     const uint4 a4, const uint4 a5, const RaySlab &r, float best,
+                                                     uint32_t &near_node, float &near_t, WStack &st, int &sp) {
+    const V3 org = v3(__uint_as_float(h.x), __uint_as_float(h.y), __uint_as_float(h.z));
+    const float sx = exp_scale(h.w), sy = exp_scale(h.w >> 8), sz = exp_scale(h.w >> 16);
+    const uint32_t nx0 = r.negx ? a2.z : a1.x, nx1 = r.negx ? a2.w : a1.y;
+    const uint32_t fx0 = r.negx ? a1.x : a2.z, fx1 = r.negx ? a1.y : a2.w;
+    const uint32_t ny0 = r.negy ? a3.x : a1.z, ny1 = r.negy ? a3.y : a1.w;
+    const uint32_t fy0 = r.negy ? a1.z : a3.x, fy1 = r.negy ? a1.w : a3.y;
+    const uint32_t nz0 = r.negz ? a3.z : a2.x, nz1 = r.negz ? a3.w : a2.y;
+    const uint32_t fz0 = r.negz ? a2.x : a3.z, fz1 = r.negz ? a2.y : a3.w;
+    uint32_t leaf_mask = 0, inner_mask = 0;
+    float tk[8];
+    float nt = __builtin_inff();
+    int nk = -1;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const uint32_t kind = ((k < 4 ? a4.z : a4.w) >> (8 * (k & 3))) & 0xFFu;
+        const float tnx = __builtin_fmaf(__builtin_fmaf(byte_f(nx0, nx1, k), sx, org.x), r.inx, r.onx);
+        const float tfx = __builtin_fmaf(__builtin_fmaf(byte_f(fx0, fx1, k), sx, org.x), r.inx, r.ofx);
+        const float tny = __builtin_fmaf(__builtin_fmaf(byte_f(ny0, ny1, k), sy, org.y), r.iny, r.ony);
+        const float tfy = __builtin_fmaf(__builtin_fmaf(byte_f(fy0, fy1, k), sy, org.y), r.iny, r.ofy);
+        const float tnz = __builtin_fmaf(__builtin_fmaf(byte_f(nz0, nz1, k), sz, org.z), r.inz, r.onz);
+        const float tfz = __builtin_fmaf(__builtin_fmaf(byte_f(fz0, fz1, k), sz, org.z), r.inz, r.ofz);
+        const float tmin = __builtin_fmaxf(__builtin_fmaxf(__builtin_fmaxf(tnx, tny), tnz), 0.0f);
+        const float tmax = __builtin_fminf(__builtin_fminf(tfx, tfy), tfz);
+        const bool hit = (kind != 0u) & !(tmin > tmax) & !(tmin > best);
+        const bool inner = hit & (kind == WIDE_INNER);
+        leaf_mask |= (hit & !inner) ? (1u << k) : 0u;
+        inner_mask |= inner ? (1u << k) : 0u;
+        tk[k] = tmin;
+        const bool take = inner & ((nk < 0) | (tmin < nt));
+        nt = take ? tmin : nt;
+        nk = take ? k : nk;
+    }
+    near_node = 0xFFFFFFFFu;
+    near_t = 0.0f;
+    if (nk >= 0) {
+        near_t = nt;
+        near_node = a4.x + ((((nk < 4 ? a5.x : a5.y) >> (8 * (nk & 3))) & 0xFFu));
+        inner_mask &= ~(1u << nk);
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        if ((inner_mask >> k) & 1u) {
+            const uint32_t child = a4.x + (((k < 4 ? a5.x : a5.y) >> (8 * (k & 3))) & 0xFFu);
+            st.node[sp * BLOCK] = child;
+            st.dist[sp * BLOCK] = tk[k];
+            sp++;
+        }
+    }
+    return leaf_mask;
+}
+
 struct WalkCounts {   // filled only by the counting variant (bench: algorithmic bytes per photon)
     uint32_t nodes, tris, walks;
     uint32_t wave_nodes, wave_tris;   // steps the whole wave executed (counted by its first active lane)
+    unsigned long long wave_fill_cycles, wave_other_cycles;   // s_memtime spent in fill_state / rest of the step loop
 };
 __device__ __forceinline__ bool wave_leader() {
     const unsigned long long m = __ballot(1);
@@ -563,7 +626,7 @@ __device__ int intersect_wide_sched(const DevGeom &g, V3 o, V3 d, float &min_dis
 // (a superset: culling uses a best that never drops below the final one), so
 // the nearest hit is unchanged.
 // Leaf queue entry: first triangle record (bits 0-29) | (count-1) << 30.
-template <bool COUNT, int F>
+template <bool COUNT, int F, bool FASTX>
 __device__ int intersect_wide_spec(const DevGeom &g, V3 o, V3 d, float &min_distance, int last_hit, WStack &st,
                                    uint32_t &overflow, WalkCounts &cnt) {
     if constexpr (COUNT) cnt.walks++;
@@ -605,7 +668,11 @@ __device__ int intersect_wide_spec(const DevGeom &g, V3 o, V3 d, float &min_dist
                         a5 = gld(np + 5);
             uint32_t near_node;
             float near_t;
-            uint32_t leaf_mask = expand_node(h, a1, a2, a3, a4, a5, slab, best, near_node, near_t, st, sp, overflow);
+            uint32_t leaf_mask;
+            if (FASTX && sp + 7 <= WIDE_LDS)
+                leaf_mask = expand_node_fast(h, a1, a2, a3, a4, a5, slab, best, near_node, near_t, st, sp);
+            else
+                leaf_mask = expand_node(h, a1, a2, a3, a4, a5, slab, best, near_node, near_t, st, sp, overflow);
             node = near_node;
             while (leaf_mask) {
                 const int k = __builtin_ctz(leaf_mask);
@@ -763,9 +830,12 @@ __device__ __forceinline__ void fill_state(const DevGeom &g, State &s, Photon &p
     int mesh_triangle;
     if constexpr (WIDE == 1)
         mesh_triangle = intersect_wide<COUNT>(g, p.pos, p.dir, s.distance, p.last_hit, wst, overflow, cnt);
+    else if constexpr (WIDE >= 3000)   // speculative walk + branch-light node expansion
+        mesh_triangle =
+            intersect_wide_spec<COUNT, WIDE - 3000, true>(g, p.pos, p.dir, s.distance, p.last_hit, wst, overflow, cnt);
     else if constexpr (WIDE >= 2000)   // speculative walk, triangle-step threshold (WIDE - 2000)/8 of live lanes
         mesh_triangle =
-            intersect_wide_spec<COUNT, WIDE - 2000>(g, p.pos, p.dir, s.distance, p.last_hit, wst, overflow, cnt);
+            intersect_wide_spec<COUNT, WIDE - 2000, false>(g, p.pos, p.dir, s.distance, p.last_hit, wst, overflow, cnt);
     else if constexpr (WIDE >= 1000)   // scheduled walk, triangle batch threshold WIDE - 1000
         mesh_triangle =
             intersect_wide_sched<COUNT, WIDE - 1000>(g, p.pos, p.dir, s.distance, p.last_hit, wst, overflow, cnt);
@@ -1274,11 +1344,19 @@ __device__ __forceinline__ bool run_photon(const DevGeom &g, const PropagateArgs
     State s;
     int scatter_first = a.scatter_first;
     int steps = 0;
+    unsigned long long tstart = 0;
+    if constexpr (COUNT) tstart = __builtin_amdgcn_s_memtime();
     while (steps < a.max_steps) {
         steps++;
         const float prod = ((((p.dir.x * p.dir.y) * p.dir.z) * p.pos.x) * p.pos.y) * p.pos.z;
         if (chr_isnan(prod)) { p.history |= CHR_NO_HIT | CHR_NAN_ABORT; break; }
+        unsigned long long t0 = 0;
+        if constexpr (COUNT) t0 = __builtin_amdgcn_s_memtime();
         fill_state<BATCH, WIDE, COUNT>(g, s, p, st, wst, overflow, cnt);
+        if constexpr (COUNT) {
+            const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+            if (wave_leader()) cnt.wave_fill_cycles += t1 - t0;
+        }
         if (p.last_hit == -1) break;
         int command = propagate_to_boundary(g, p, s, rng, a.use_weights, scatter_first);
         scatter_first = 0;
@@ -1290,6 +1368,10 @@ __device__ __forceinline__ bool run_photon(const DevGeom &g, const PropagateArgs
             if (command == CONTINUE) continue;
         }
         propagate_at_boundary(p, s, rng);
+    }
+    if constexpr (COUNT) {
+        const unsigned long long tend = __builtin_amdgcn_s_memtime();
+        if (wave_leader()) cnt.wave_other_cycles += tend - tstart;   // includes fill; split on the host
     }
     store3(a.pos, photon_id, p.pos);
     store3(a.dir, photon_id, p.dir);
@@ -1323,6 +1405,8 @@ __device__ __forceinline__ void flush_counters(const PropagateArgs &a, uint32_t 
         atomicAdd(c64 + 2, (unsigned long long)cnt.walks);
         atomicAdd(c64 + 3, (unsigned long long)cnt.wave_nodes);
         atomicAdd(c64 + 4, (unsigned long long)cnt.wave_tris);
+        atomicAdd(c64 + 5, cnt.wave_fill_cycles);
+        atomicAdd(c64 + 6, cnt.wave_other_cycles);
     }
 }
 
@@ -1357,7 +1441,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_kernel(const DevGeom *_
     wst.leafq = (CHR_LDS uint32_t *)(lds_stack + 2 * WIDE_LDS * BLOCK + threadIdx.x);
             wst.leafq = (CHR_LDS uint32_t *)(lds_stack + 2 * WIDE_LDS * BLOCK + threadIdx.x);
             uint32_t overflow = 0;
-            WalkCounts cnt{0u, 0u, 0u, 0u, 0u};
+            WalkCounts cnt{0u, 0u, 0u, 0u, 0u, 0ull, 0ull};
             const DevGeom &g = *gdev;   // device-resident: uniform s_loads, no private copy
             alive = run_photon<BATCH, WIDE, COUNT>(g, a, photon_id, history, rng, st, wst, overflow, cnt);
             store_rng(a, (uint32_t)id, rng);
@@ -1401,7 +1485,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_step_kernel(const DevGe
     wst.dist = (CHR_LDS float *)(lds_stack + WIDE_LDS * BLOCK + threadIdx.x);
     wst.leafq = (CHR_LDS uint32_t *)(lds_stack + 2 * WIDE_LDS * BLOCK + threadIdx.x);
     uint32_t overflow = 0;
-    WalkCounts cnt{0u, 0u, 0u, 0u, 0u};
+    WalkCounts cnt{0u, 0u, 0u, 0u, 0u, 0ull, 0ull};
     const DevGeom &g = *gdev;
     chr_xorwow rng;
     bool have_rng = false;
@@ -1801,17 +1885,24 @@ extern "C" uint64_t chr_propagate_scratch_words(uint32_t nthreads) {
 typedef void (*propagate_fn)(const DevGeom *, PropagateArgs);
 // measured on demo.detector(), 4M photons (profiles/r01/ab_variants.log):
 // <1,3> 89.2 ms, <4,3> 74.9, <4,4> 66.8, <4,5> 66.5, <8,4> 64.3, <8,3> 74.1, <2,3> 76.5
+// Walk schedules, demo.detector() 4M photons, one launch per step (gpurun_out r1h-r1j):
+// scheduled (1002) 13.2 ms, speculative 2004 13.1, 2006 11.8, 2008 ~12.0, 3006 (branch-light
+// node expansion) 12.8 -> the speculative walk with threshold 6/8 is the default.
+static constexpr int kWalk = 2006;        // default walk (wide BVH)
+static constexpr int kWalkSched = 1002;   // scheduled walk; also used when the leaf queue cannot index the triangles
 static const propagate_fn kVariants[] = {
-    propagate_kernel<8, 4, 1002>,        // 0: default -- 8-wide SAH BVH, wave-scheduled steps, triangle batch 2
+    propagate_kernel<8, 4, kWalk>,       // 0: default -- 8-wide SAH BVH, speculative walk (parked-leaf queue)
     propagate_kernel<8, 4, 0>,           // 1: exact-order walk of the reference BVH, 8 children in flight
     propagate_kernel<8, 4, 1>,           // 2: 8-wide BVH, leaf triangles tested inside the node step
     propagate_kernel<8, 4, 1001>,        // 3: scheduled, triangle batch 1
     propagate_kernel<8, 4, 1004>,        // 4: scheduled, triangle batch 4
-    propagate_kernel<8, 4, 1002, true>,  // 5: default + node/triangle counters (bench's byte count)
+    propagate_kernel<8, 4, kWalk, true>, // 5: default + node/triangle counters (bench's byte count)
     propagate_kernel<8, 4, 1008>,        // 6: scheduled, triangle batch 8
     propagate_kernel<8, 4, 1000>,        // 7: scheduled, per-lane choice
-    propagate_kernel<8, 3, 1002>,        // 8: default at 3 waves/SIMD
-    propagate_kernel<8, 5, 1002>,        // 9: default at 5 waves/SIMD
+    propagate_kernel<8, 3, kWalk>,       // 8: default at 3 waves/SIMD
+    propagate_kernel<8, 5, kWalk>,       // 9: default at 5 waves/SIMD
+    propagate_kernel<8, 4, kWalkSched>,  // 10: scheduled walk, triangle batch 2 (the previous default)
+    propagate_kernel<8, 4, kWalkSched, true>,   // 11: scheduled walk + counters
 };
 static constexpr int kExactVariant = 1;
 static propagate_fn select_variant(const chr_geometry *g) {
@@ -1819,6 +1910,7 @@ static propagate_fn select_variant(const chr_geometry *g) {
     int v = e ? atoi(e) : 0;
     if (v < 0 || v >= (int)(sizeof(kVariants) / sizeof(kVariants[0]))) v = 0;
     if (g->dev.nwnodes == 0 && v != 1) v = kExactVariant;   // no wide BVH for this geometry
+    if (g->dev.nwtri >= (1u << 30) && (v == 0 || v == 5 || v == 8 || v == 9)) v = (v == 5) ? 11 : 10;
     return kVariants[v];
 }
 
@@ -1827,18 +1919,22 @@ static propagate_step_fn select_step_variant(const chr_geometry *g) {
     const char *e = getenv("CHR_PROPAGATE_VARIANT");
     int v = e ? atoi(e) : 0;
     if (g->dev.nwnodes == 0) v = kExactVariant;
-    if (v >= 12 && g->dev.nwtri >= (1u << 30)) v = 0;   // leaf-queue entries hold 30-bit record indices
+    const bool queue_ok = g->dev.nwtri < (1u << 30);   // leaf-queue entries hold 30-bit record indices
+    if (!queue_ok && (v == 0 || v == 5 || v >= 12)) v = (v == 5) ? 11 : 10;
     switch (v) {
         case 1: return propagate_step_kernel<8, 4, 0>;
-        case 5: return propagate_step_kernel<8, 4, 1002, true>;
-        case 8: return propagate_step_kernel<8, 3, 1002>;
-        case 9: return propagate_step_kernel<8, 5, 1002>;
+        case 5: return propagate_step_kernel<8, 4, kWalk, true>;
+        case 8: return propagate_step_kernel<8, 3, kWalk>;
+        case 9: return propagate_step_kernel<8, 5, kWalk>;
+        case 10: return propagate_step_kernel<8, 4, kWalkSched>;
+        case 11: return propagate_step_kernel<8, 4, kWalkSched, true>;
         case 12: return propagate_step_kernel<8, 4, 2002>;
         case 14: return propagate_step_kernel<8, 4, 2004>;
         case 15: return propagate_step_kernel<8, 4, 2004, true>;
-        case 16: return propagate_step_kernel<8, 4, 2006>;
         case 18: return propagate_step_kernel<8, 4, 2008>;
-        default: return propagate_step_kernel<8, 4, 1002>;
+        case 26: return propagate_step_kernel<8, 4, 3006>;
+        case 27: return propagate_step_kernel<8, 4, 3006, true>;
+        default: return propagate_step_kernel<8, 4, kWalk>;
     }
 }
 
@@ -1969,7 +2065,7 @@ static int apply_node_layout(const chr_geometry *cg, hipStream_t stream) {
     chr_geometry *g = const_cast<chr_geometry *>(cg);
     if (!g->wnodes_alt) return CHR_OK;
     const char *e = getenv("CHR_NODE_LAYOUT");
-    const uint32_t want = (e && atoi(e) == 96) ? 6u : 8u;
+    const uint32_t want = (e && atoi(e) == 128) ? 8u : 6u;
     if (g->dev.wstride == want) return CHR_OK;
     std::swap(g->dev.wnodes, g->wnodes_alt);
     std::swap(g->dev.wstride, g->wstride_alt);
@@ -2083,12 +2179,14 @@ extern "C" int chr_propagate(const chr_geometry *g, const chr_photons *ph, uint3
         }
     }
     CHR_HIP_CHECK(hipMemcpyAsync(pinned + 2, scratch, 4, hipMemcpyDeviceToHost, stream));
-    CHR_HIP_CHECK(hipMemcpyAsync(pinned + 4, scratch + 2, 40, hipMemcpyDeviceToHost, stream));
+    CHR_HIP_CHECK(hipMemcpyAsync(pinned + 4, scratch + 2, 56, hipMemcpyDeviceToHost, stream));
     CHR_HIP_CHECK(hipStreamSynchronize(stream));
     st.stack_overflows = pinned[2];
     {
-        uint64_t c[5];
-        std::memcpy(c, pinned + 4, 40);
+        uint64_t c[7];
+        std::memcpy(c, pinned + 4, 56);
+        st.wave_fill_cycles = c[5];
+        st.wave_step_cycles = c[6];
         st.nodes_visited = c[0];
         st.triangles_tested = c[1];
         st.traversals = c[2];

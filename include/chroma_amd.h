@@ -164,6 +164,8 @@ typedef struct chr_propagate_stats {
     uint64_t traversals;
     uint64_t wave_node_steps;     /* node / triangle steps executed per wave (SIMD efficiency = */
     uint64_t wave_triangle_steps; /* nodes_visited / (64 * wave_node_steps)); counting variant only */
+    uint64_t wave_fill_cycles;    /* s_memtime cycles waves spent in fill_state (traversal) and in */
+    uint64_t wave_step_cycles;    /* whole photon step loops; counting variant only */
 } chr_propagate_stats;
 
 /* replaces: GPUPhotons.propagate host loop (chroma/gpu/photon.py:226-293) for

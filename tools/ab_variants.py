@@ -29,7 +29,7 @@ def main():
     from chroma.photon_source import isotropic
     from types import SimpleNamespace
     torch.cuda.set_device(0)
-    os.environ['CHR_NODE_LAYOUT_AB'] = '1'      # keep both node layouts on the device (":n96" variants)
+    os.environ['CHR_NODE_LAYOUT_AB'] = '1'      # keep both node layouts on the device (":n128" variants)
     det = bench.build_geometry(args.detector, '/tmp/chroma_bench_cache')
     gdet = gpu.GPUDetector(det)
     photons = isotropic(args.photons, seed=20260102)
@@ -37,7 +37,7 @@ def main():
                                pol=ga.to_gpu(gpu.to_float3(photons.pol)), wavelengths=ga.to_gpu(photons.wavelengths),
                                t=ga.to_gpu(photons.t), flags=ga.to_gpu(photons.flags), evidx=ga.to_gpu(photons.evidx),
                                true_nphotons=args.photons)
-    variants = args.variants.split(',')   # "<n>[:sort][:n96][:chunked]"
+    variants = args.variants.split(',')   # "<n>[:sort][:n128][:chunked]"
     times = {v: [] for v in variants}
     kms = {v: [] for v in variants}
     ref_flags = None
@@ -46,7 +46,7 @@ def main():
             opts = v.split(':')
             os.environ['CHR_PROPAGATE_VARIANT'] = opts[0]
             os.environ['CHR_SORT'] = '1' if 'sort' in opts[1:] else '0'
-            os.environ['CHR_NODE_LAYOUT'] = '96' if 'n96' in opts[1:] else '128'
+            os.environ['CHR_NODE_LAYOUT'] = '128' if 'n128' in opts[1:] else '96'
             os.environ['CHR_STEP_LAUNCH'] = '0' if 'chunked' in opts[1:] else '1'
             rng = gpu.get_rng_states(512 * 1024, seed=1)
             gp = gpu.GPUPhotons(pristine, copy_flags=True, copy_triangles=False, copy_weights=False)
@@ -72,6 +72,8 @@ def main():
                           st.nodes_visited / (64.0 * max(1, st.wave_node_steps)),
                           st.triangles_tested / (64.0 * max(1, st.wave_triangle_steps)),
                           st.wave_node_steps, st.wave_triangle_steps), flush=True)
+                print('variant %s time split: fill_state (traversal) %.1f%% of photon-loop wave cycles' % (
+                    v, 100.0 * st.wave_fill_cycles / max(1, st.wave_step_cycles)), flush=True)
             if r > 0:
                 times[v].append(dt)
                 kms[v].append(gp.last_stats.kernel_ms)

@@ -53,6 +53,16 @@ def main():
         res['write_bytes_per_launch'] = 1024.0 * sum(w) / len(w)
     if 'read_bytes_per_launch' in res and 'write_bytes_per_launch' in res:
         res['hbm_bytes_per_launch'] = res['read_bytes_per_launch'] + res['write_bytes_per_launch']
+    # the workload the passes ran (bench.py only uses a summary of its own workload)
+    try:
+        with open(os.path.join(d, 'bench_fetch.json')) as f:
+            cfg = json.loads(f.read().strip().splitlines()[-1])['config']
+        res['workload'] = {'detector': cfg['detector'], 'photons': cfg['photons_per_gpu'],
+                           'max_steps': cfg.get('max_steps')}
+    except (OSError, ValueError, KeyError, IndexError):
+        pass
+    res['source'] = 'rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE passes of bench.py (tools/rocprof_bench.sh), ' + \
+        os.path.basename(os.path.normpath(d))
     print(json.dumps(res, indent=1))
 
 
