@@ -40,15 +40,28 @@ import numpy as np  # noqa: E402
 
 METRIC = 'propagated photons/sec, 29k-PMT detector, 10M isotropic photons, 1/2/4/8 GPUs'
 HBM_PEAK_GBS = 8000.0
+def _demo_detector(**kw):
+    from chroma import demo
+    return demo.detector(**kw)
+
+
+def _scint_detector(**kw):
+    from chroma.demo import scint
+    return scint.detector(**kw)
+
+
 DETECTORS = {
-    # name: (description, kwargs of chroma.demo.detector)
+    # name: (description, kwargs, builder)
     '29k': ('demo.detector(pmt_radius=23780, sphere_radius=24280): 29,007 PMTs, ~170M triangles',
-            dict(pmt_radius=23780.0, sphere_radius=24280.0)),
-    'demo': ('demo.detector(): 10,055 PMTs, 58.96M triangles', dict()),
+            dict(pmt_radius=23780.0, sphere_radius=24280.0), _demo_detector),
+    'demo': ('demo.detector(): 10,055 PMTs, 58.96M triangles', dict(), _demo_detector),
     'tiny': ('demo.tiny(): 53 PMTs, 389,568 triangles', dict(pmt_radius=2000.0, sphere_radius=2500.0,
-                                                             spiral_step=700.0)),
+                                                             spiral_step=700.0), _demo_detector),
     'small': ('demo.detector(600, 900, 1500): 2 PMTs, 90,912 triangles',
-              dict(pmt_radius=600.0, sphere_radius=900.0, spiral_step=1500.0)),
+              dict(pmt_radius=600.0, sphere_radius=900.0, spiral_step=1500.0), _demo_detector),
+    # BASELINE config 5: scintillator + WLS + dichroic surfaces (chroma.demo.scint)
+    'scint': ('demo.scint.detector(): 10,055 PMTs in liquid scintillator (2-component bulk re-emission), '
+              'light cones cycling shiny / dichroic / WLS, 58.96M triangles', dict(), _scint_detector),
 }
 
 
@@ -58,55 +71,35 @@ def log(*a):
 
 def build_geometry(name, cache_dir):
     """Flattened demo detector + BVH, cached on local disk (same box reuse)."""
-    from chroma import demo
-    from chroma.bvh import make_recursive_grid_bvh, BVH, WorldCoords
+    from chroma.bvh import make_recursive_grid_bvh
+    from chroma.cache import Cache
     t0 = time.time()
-    det = demo.detector(**DETECTORS[name][1])
-    path = os.path.join(cache_dir, 'geometry_%s.npz' % name) if cache_dir else None
-    if path and os.path.exists(path):
-        z = np.load(path)
-        from chroma.geometry import Mesh
-        det.solid_id_to_channel_index = np.asarray(det.solid_id_to_channel_index, dtype=np.int32)
-        det.channel_index_to_solid_id = np.asarray(det.channel_index_to_solid_id, dtype=np.int32)
-        mesh = Mesh.__new__(Mesh)
-        mesh.vertices, mesh.triangles = z['vertices'], z['triangles']
-        det.mesh = mesh
-        det.solid_id, det.colors = z['solid_id'], z['colors']
-        det.material1_index, det.material2_index, det.surface_index = \
-            z['material1_index'], z['material2_index'], z['surface_index']
-        det.unique_materials = [m for m in _unique_materials(det)]
-        det.unique_surfaces = [s for s in _unique_surfaces(det)]
-        det.bvh = BVH(WorldCoords(z['world_origin'], z['world_scale']), z['nodes'], z['layer_offsets'])
+    cache = None
+    if cache_dir:
+        try:
+            os.makedirs(cache_dir, exist_ok=True)
+            cache = Cache(cache_dir)
+        except OSError as e:
+            log('geometry cache unavailable: %s' % e)
+    key = 'bench_%s' % name
+    if cache is not None and key in cache.list_geometry():
+        det = cache.load_geometry(key)
+        det.bvh = cache.load_bvh(cache.get_geometry_hash(key))
         log('geometry %s loaded from cache in %.1fs' % (name, time.time() - t0))
         return det
+    det = DETECTORS[name][2](**DETECTORS[name][1])
     det.flatten()
     t1 = time.time()
     det.bvh = make_recursive_grid_bvh(det.mesh, target_degree=3)
     log('geometry %s: %d triangles, flatten %.1fs, BVH %.1fs (%d nodes)' % (
         name, len(det.mesh.triangles), t1 - t0, time.time() - t1, len(det.bvh.nodes)))
-    if path:
+    if cache is not None:
         try:
-            os.makedirs(cache_dir, exist_ok=True)
-            np.savez(path + '.tmp.npz', vertices=det.mesh.vertices, triangles=det.mesh.triangles,
-                     solid_id=det.solid_id, colors=det.colors, material1_index=det.material1_index,
-                     material2_index=det.material2_index, surface_index=det.surface_index,
-                     nodes=det.bvh.nodes, layer_offsets=np.asarray(det.bvh.layer_offsets),
-                     world_origin=det.bvh.world_coords.world_origin,
-                     world_scale=det.bvh.world_coords.world_scale)
-            os.replace(path + '.tmp.npz', path)
+            cache.save_bvh(det.bvh, det.mesh.md5())
+            cache.save_geometry(key, det)
         except OSError as e:
             log('geometry cache not written: %s' % e)
     return det
-
-
-def _unique_materials(det):
-    from chroma.geometry import _first_seen
-    return _first_seen([m for s in det.solids for m in s.unique_materials])
-
-
-def _unique_surfaces(det):
-    from chroma.geometry import _first_seen
-    return _first_seen([x for s in det.solids for x in s.unique_surfaces])
 
 
 def cpu_baseline(packed, photons, nslots, ntpb, max_blocks, max_steps, seed, budget_s, threads):

@@ -1,9 +1,12 @@
 import os
 import sys
+import tempfile
 
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+# the loader's BVH cache (chroma.cache, default ~/.chroma) goes to a per-session temp dir
+os.environ['CHROMA_CACHE_DIR'] = tempfile.mkdtemp(prefix='chroma_cache_test_')
 for p in (os.path.join(ROOT, 'chroma-lite_amd'), os.path.join(ROOT, 'oracle')):
     if p not in sys.path:
         sys.path.insert(0, p)
