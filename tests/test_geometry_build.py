@@ -83,3 +83,23 @@ def test_packing_tables(small_detector, small_packed):
     codes = pk.material_codes
     assert np.array_equal((codes >> 24) & 0xFF, small_detector.material1_index & 0xFF)
     assert np.array_equal((codes >> 8) & 0xFF, small_detector.surface_index & 0xFF)
+
+
+def test_scintillator_detector_build():
+    """chroma.demo.scint (BASELINE config 5): same PMT layout and mesh size as
+    demo.tiny(), three light-cone surface models, a 2-component scintillator
+    whose re-emission CDFs are proper CDFs."""
+    from chroma.demo import scint
+    det = scint.tiny()
+    det.flatten()
+    assert len(det.mesh.triangles) == 389568 and det.num_channels() == 53
+    models = sorted({s.model for s in det.unique_surfaces if s is not None})
+    assert models == [0, 2, 3]
+    ls = det.detector_material
+    assert len(ls.comp_reemission_prob) == 2
+    for cdf in ls.comp_reemission_wvl_cdf + ls.comp_reemission_time_cdf:
+        assert cdf[0, 1] == 0.0 and cdf[-1, 1] == 1.0 and (np.diff(cdf[:, 1]) >= 0).all()
+    dp = [s for s in det.unique_surfaces if s is not None and s.model == 3][0].dichroic_props
+    assert len(dp.angles) == len(dp.dichroic_reflect) == len(dp.dichroic_transmit)
+    for r, t in zip(dp.dichroic_reflect, dp.dichroic_transmit):
+        assert (r[:, 1] + t[:, 1] <= 1.0 + 1e-6).all()

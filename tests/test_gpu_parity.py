@@ -181,3 +181,25 @@ def test_simulation_end_to_end(cuda, small_detector, small_packed):
         mine = idx[(idx >= 3000 * i) & (idx < 3000 * (i + 1))]
         assert len(ev.flat_hits) == len(mine)
         assert sum(len(v) for v in ev.hits.values()) == len(mine)
+
+
+def test_scintillator_detector_parity(cuda):
+    """BASELINE config 5 geometry (chroma.demo.scint.tiny(): liquid scintillator
+    with 2-component bulk re-emission, light cones cycling shiny / dichroic /
+    WLS): HIP == oracle, hits included, with the re-emission branches taken."""
+    from chroma import gpu, loader
+    from chroma.demo import scint
+    from chroma.gpu.packing import PackedGeometry
+    from chroma.photon_source import isotropic
+    geo = loader.create_geometry_from_obj(scint.tiny())
+    packed = PackedGeometry(geo)
+    photons = isotropic(30000, seed=5)
+    gp, host, rng, st, _ = _run_both(geo, packed, photons, 128 * 256, 128, 256, 1000, seed=9)
+    _compare(host, gp, 'scint')
+    assert np.array_equal(rng.get().reshape(-1), st)
+    fl = host.flags
+    for bit in (1 << 7, 1 << 9, 1 << 2):            # SURFACE_REEMIT, BULK_REEMIT, SURFACE_DETECT
+        assert ((fl & bit) != 0).any(), 'branch bit %d never exercised' % bit
+    hits = gp.get_flat_hits(gpu.GPUDetector(geo))
+    idx, ch = oracle.hits(host, geo.solid_id, geo.solid_id_to_channel_index)
+    assert np.array_equal(hits.channel.astype(np.int64), ch.astype(np.int64))
