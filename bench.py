@@ -16,16 +16,21 @@ photons are histogrammed per PMT channel on the device and SUM-reduced over
 the ranks (RCCL, chroma.gpu.shard) -- the only exchange the path has.  The
 timed region is bracketed by barriers and the max over ranks is reported.
 
-Roofline: the propagate kernel is bound by HBM/L2 latency-bandwidth on the
-BVH + triangle gathers.  achieved = algorithmic bytes per step / summed
-propagate-kernel time (HIP events around every launch, on its stream), with
-algorithmic bytes per photon
-    B_alg = 120 + (96 * wide nodes visited + 64 * triangle records tested
-                   + 52 * traversals) / photons
-(photon record in+out; 96-byte BVH nodes; 64-byte triangle records; the hit
-triangle's 48-byte normal record + 4-byte material code per traversal),
-counted on ALL photons of the step by one extra, untimed propagate with the
-counting kernel variant (CHR_PROPAGATE_VARIANT=5: same walk + counters).
+Roofline: the dominant kernel is trace_kernel, the
+BVH walk of every one-step launch (the last, multi-step launch of the
+reference's nsteps policy runs the fused step kernel).  It is bound by HBM/L2
+latency-bandwidth on dependent node/triangle gathers.
+    achieved = algorithmic bytes per trace launch / average trace launch time
+with the average from HIP events around each trace launch on its stream, and
+the algorithmic bytes of section 8(d): per walk 16 * reference-BVH nodes +
+48 * reference triangles + 4, counted by the CPU oracle walking the REFERENCE
+BVH in the reference's DFS order on the cpu_baseline sample of the same
+workload (layout-independent, comparable across builds), times the rays of
+the launch.  The bytes of this build's own layout (96-byte wide nodes, 64-byte
+triangle records) are counted on every photon by one extra, untimed propagate
+with the counting variant (CHR_PROPAGATE_VARIANT=5) and reported beside it;
+traffic = HBM bytes per trace launch from the rocprofv3 FETCH_SIZE/WRITE_SIZE
+passes of this workload (profiles/latest_pmc.json).
 """
 import argparse
 import json
@@ -130,24 +135,43 @@ def cpu_baseline(packed, photons, nslots, ntpb, max_blocks, max_steps, seed, bud
                        'threads' % (n, max_steps, total_t, threads)), b_alg, stats, n
 
 
-def roofline(args, cst, n, kernel_ms, launches):
-    """roofline object of the bench line for the dominant kernel (propagate_kernel)."""
-    b_alg = 120.0 + (96.0 * cst.nodes_visited + 64.0 * cst.triangles_tested + 52.0 * cst.traversals) / n
-    launches_per_step = launches / args.steps
-    alg_per_launch = n * b_alg / launches_per_step
-    avg_launch_s = kernel_ms / max(1, launches) / 1e3
-    achieved = alg_per_launch / avg_launch_s / 1e9
+def roofline(args, live, cst, ref, n):
+    """roofline object of the bench line for the dominant kernel (trace_kernel).
+    live: timed-region sums of the propagate stats; cst: counting pass (own
+    layout); ref: oracle counts on the reference BVH (None without cpu_baseline)."""
+    launches = max(1, live['trace_launches'])
+    rays_per_launch = live['trace_rays'] / launches
+    avg_launch_s = live['trace_ms'] / launches / 1e3
+    own = None
+    if cst is not None and cst.traversals:
+        own = (96.0 * cst.nodes_visited + 64.0 * cst.triangles_tested + 52.0 * cst.traversals) / cst.traversals
+    if ref is not None:
+        per_walk, basis = (16.0 * ref['nodes_visited'] + 48.0 * ref['tris_tested']) / ref['traversals'] + 4.0, \
+            'SURVEY 8(d): 16 B x reference-BVH nodes + 48 B x triangles + 4 B per walk (oracle, reference DFS order)'
+    else:
+        per_walk, basis = own, 'own layout: 96 B x wide nodes + 64 B x triangle records + 52 B per walk'
+    alg_per_launch = rays_per_launch * per_walk if per_walk else 0.0
+    achieved = alg_per_launch / avg_launch_s / 1e9 if avg_launch_s > 0 else 0.0
     rl = {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
           'frac': achieved / HBM_PEAK_GBS, 'traffic': None,
+          'kernel': 'chr::trace_kernel (BVH walk of the one-step launches)',
+          'basis': basis,
           'alg_bytes_per_launch': alg_per_launch,
-          'bytes_per_photon_alg': b_alg,
-          'nodes_per_photon': cst.nodes_visited / n,
-          'triangles_per_photon': cst.triangles_tested / n,
-          'traversals_per_photon': cst.traversals / n,
-          'simd_efficiency_nodes': cst.nodes_visited / max(1.0, 64.0 * cst.wave_node_steps),
-          'simd_efficiency_triangles': cst.triangles_tested / max(1.0, 64.0 * cst.wave_triangle_steps),
-          'kernel': 'chr::propagate_step_kernel<8,4,2006> (speculative walk)',
-          'avg_launch_ms': 1e3 * avg_launch_s}
+          'alg_bytes_per_walk': per_walk,
+          'rays_per_launch': rays_per_launch,
+          'avg_launch_ms': 1e3 * avg_launch_s,
+          'launches_timed': live['trace_launches']}
+    if own is not None:
+        rl['own_layout_bytes_per_walk'] = own
+        rl['own_layout_achieved'] = rays_per_launch * own / avg_launch_s / 1e9 if avg_launch_s > 0 else 0.0
+        rl['nodes_per_photon'] = cst.nodes_visited / n
+        rl['triangles_per_photon'] = cst.triangles_tested / n
+        rl['traversals_per_photon'] = cst.traversals / n
+        rl['simd_efficiency_nodes'] = cst.nodes_visited / max(1.0, 64.0 * cst.wave_node_steps)
+        rl['simd_efficiency_triangles'] = cst.triangles_tested / max(1.0, 64.0 * cst.wave_triangle_steps)
+    if ref is not None:
+        rl['reference_bvh_nodes_per_walk'] = ref['nodes_visited'] / ref['traversals']
+        rl['reference_bvh_triangles_per_walk'] = ref['tris_tested'] / ref['traversals']
     # HBM bytes per launch from the PMC passes (tools/rocprof_bench.sh) of this same workload
     pmc_path = os.path.join(ROOT, 'profiles', 'latest_pmc.json')
     if os.path.exists(pmc_path):
@@ -155,7 +179,7 @@ def roofline(args, cst, n, kernel_ms, launches):
             pmc = json.load(f)
         w = pmc.get('workload', {})
         if (w.get('detector'), w.get('photons'), w.get('max_steps')) == (args.detector, args.photons, args.max_steps) \
-                and 'hbm_bytes_per_launch' in pmc:
+                and pmc.get('kernel') == 'chr::trace_kernel' and 'hbm_bytes_per_launch' in pmc:
             rl['traffic'] = pmc['hbm_bytes_per_launch']
             rl['traffic_unit'] = 'bytes/launch (FETCH_SIZE x2 + WRITE_SIZE)'
             rl['traffic_source'] = pmc.get('source')
@@ -237,14 +261,16 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    kernel_ms = 0.0
-    launches = 0
-    host_steps = 0
+    live = dict(kernel_ms=0.0, launches=0, host_steps=0, trace_ms=0.0, trace_launches=0, trace_rays=0)
     for _ in range(args.steps):
         gp = step()
-        kernel_ms += gp.last_stats.kernel_ms
-        launches += gp.last_stats.launches
-        host_steps += gp.last_stats.steps_run
+        ls = gp.last_stats
+        live['kernel_ms'] += ls.kernel_ms
+        live['launches'] += ls.launches
+        live['host_steps'] += ls.steps_run
+        live['trace_ms'] += ls.trace_ms
+        live['trace_launches'] += ls.trace_launches
+        live['trace_rays'] += ls.trace_rays
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -282,23 +308,27 @@ def main():
                        'detector': args.detector, 'photons_per_gpu': args.photons, 'max_steps': args.max_steps, 'triangles': len(det.mesh.triangles),
                        'bvh_nodes': len(det.bvh.nodes), 'channels': det.num_channels(),
                        'parallelism': 'photon-sharded x%d, geometry replicated' % world},
-            'detail': {'kernel_ms_per_step': kernel_ms / args.steps, 'launches_per_step': launches / args.steps,
-                       'host_steps_per_propagate': host_steps / args.steps,
+            'detail': {'kernel_ms_per_step': live['kernel_ms'] / args.steps,
+                       'trace_ms_per_step': live['trace_ms'] / args.steps,
+                       'launches_per_step': live['launches'] / args.steps,
+                       'host_steps_per_propagate': live['host_steps'] / args.steps,
                        'detected_fraction': detected / args.photons,
                        'channel_hits_all_ranks': channel_hits},
             'roofline': None, 'cpu_baseline': None,
         }
         n = float(args.photons)
-        if cst is not None:
-            result['roofline'] = roofline(args, cst, n, kernel_ms, launches)
+        ostats = None
         if not args.no_cpu_baseline and world == 1:
             threads = min(16, len(os.sched_getaffinity(0)))
-            cpu, _, ostats, nsample = cpu_baseline(PackedGeometry(det), photons, nslots, args.nthreads_per_block,
+            cpu, b_ref, ostats, nsample = cpu_baseline(PackedGeometry(det), photons, nslots, args.nthreads_per_block,
                                                    args.max_blocks, args.max_steps, args.seed, args.cpu_budget,
                                                    threads)
             result['cpu_baseline'] = cpu
             result['detail']['reference_bvh_nodes_per_photon'] = ostats['nodes_visited'] / nsample
             result['detail']['reference_bvh_triangles_per_photon'] = ostats['tris_tested'] / nsample
+            result['detail']['bytes_per_photon_alg_8d'] = b_ref
+        if live['trace_launches']:
+            result['roofline'] = roofline(args, live, cst, ostats, n)
         print(json.dumps(result), flush=True)
     if dist:
         dist.destroy_process_group()

@@ -65,7 +65,8 @@ class PropagateStats(ctypes.Structure):
     _fields_ = [('steps_run', c_u32), ('launches', c_u32), ('final_alive', c_u32), ('stack_overflows', c_u32),
                 ('kernel_ms', ctypes.c_double), ('nodes_visited', c_u64), ('triangles_tested', c_u64),
                 ('traversals', c_u64), ('wave_node_steps', c_u64), ('wave_triangle_steps', c_u64),
-                ('wave_fill_cycles', c_u64), ('wave_step_cycles', c_u64)]
+                ('wave_fill_cycles', c_u64), ('wave_step_cycles', c_u64), ('trace_ms', ctypes.c_double),
+                ('trace_launches', c_u32), ('reserved', c_u32), ('trace_rays', c_u64)]
 
 
 _SIGNATURES = {

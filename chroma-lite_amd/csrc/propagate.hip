@@ -21,6 +21,7 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <vector>
@@ -275,7 +276,10 @@ __device__ __forceinline__ int intersect_mesh(const DevGeom &g, V3 o, V3 d, floa
 constexpr int WIDE_LDS = 12;
 constexpr int LEAFQ = 16;          // per-lane parked-leaf queue (speculative walk), LDS
 // LDS words per work-item: traversal stack (node + entry distance) [+ leaf queue]
-constexpr int lds_words(int wide) { return wide >= 2000 ? 2 * WIDE_LDS + LEAFQ : (wide ? 2 * WIDE_LDS : 0); }
+constexpr int HITS_MODE = 9000;    // shade-only step kernel: the walk's result comes from trace_kernel
+constexpr int lds_words(int wide) {
+    return wide == HITS_MODE ? 1 : (wide >= 2000 ? 2 * WIDE_LDS + LEAFQ : (wide ? 2 * WIDE_LDS : 0));
+}
 
 // The LDS column pointers are typed (ds_* ops) and the scratch spill array is
 // a separate object: an object holding both lives in scratch and its LDS
@@ -287,13 +291,16 @@ struct WStack {
     uint2 *spill;             // entries >= WIDE_LDS (scratch)
     CHR_LDS uint32_t *leafq;  // parked leaves (speculative walk): entry i at leafq[i * BLOCK]
 };
+// SL: stack entries kept in LDS (the rest spill to scratch)
+template <int SL = WIDE_LDS>
 __device__ __forceinline__ void wpush(WStack &s, int i, uint32_t n, float t) {
-    if (i < WIDE_LDS) { s.node[i * BLOCK] = n; s.dist[i * BLOCK] = t; }
-    else s.spill[i - WIDE_LDS] = make_uint2(n, __float_as_uint(t));
+    if (i < SL) { s.node[i * BLOCK] = n; s.dist[i * BLOCK] = t; }
+    else s.spill[i - SL] = make_uint2(n, __float_as_uint(t));
 }
+template <int SL = WIDE_LDS>
 __device__ __forceinline__ void wpop(const WStack &s, int i, uint32_t &n, float &t) {
-    if (i < WIDE_LDS) { n = s.node[i * BLOCK]; t = s.dist[i * BLOCK]; }
-    else { const uint2 e = s.spill[i - WIDE_LDS]; n = e.x; t = __uint_as_float(e.y); }
+    if (i < SL) { n = s.node[i * BLOCK]; t = s.dist[i * BLOCK]; }
+    else { const uint2 e = s.spill[i - SL]; n = e.x; t = __uint_as_float(e.y); }
 }
 
 __device__ __forceinline__ float byte_f(uint32_t lo4, uint32_t hi4, int k) {   // byte k of (hi4:lo4) as float
@@ -330,6 +337,7 @@ __device__ __forceinline__ RaySlab make_slab(V3 noid, V3 inv) {
 // hit (bit mask), leaves the nearest hit inner child in near_node/near_t and
 // pushes the other hit inner children.  Boxes entered beyond `best` are culled
 // (strict '>', mesh.h:94-96).
+template <int SL = WIDE_LDS>
 __device__ __forceinline__ uint32_t expand_node(const uint4 h, const uint4 a1, const uint4 a2, const uint4 a3,
                                                 const uint4 a4, const uint4 a5, const RaySlab &r, float best,
                                                 uint32_t &near_node, float &near_t, WStack &st, int &sp,
@@ -366,7 +374,7 @@ __device__ __forceinline__ uint32_t expand_node(const uint4 h, const uint4 a1, c
         float pt = tmin;
         if (tmin < near_t) { pn = near_node; pt = near_t; near_node = child; near_t = tmin; }
         if (sp >= WIDE_STACK) { overflow++; break; }
-        wpush(st, sp, pn, pt);
+        wpush<SL>(st, sp, pn, pt);
         sp++;
     }
     return leaf_mask;
@@ -823,23 +831,11 @@ __device__ CHR_COLD void wireplanes(const DevGeom &g, const Photon &p, float bes
     }
 }
 
-// photon.h:87-397
-template <int BATCH, int WIDE, bool COUNT>
-__device__ __forceinline__ void fill_state(const DevGeom &g, State &s, Photon &p, Stack st, WStack &wst,
-                                           uint32_t &overflow, WalkCounts &cnt) {
-    int mesh_triangle;
-    if constexpr (WIDE == 1)
-        mesh_triangle = intersect_wide<COUNT>(g, p.pos, p.dir, s.distance, p.last_hit, wst, overflow, cnt);
-    else if constexpr (WIDE >= 3000)   // speculative walk + branch-light node expansion
-        mesh_triangle =
-            intersect_wide_spec<COUNT, WIDE - 3000, true>(g, p.pos, p.dir, s.distance, p.last_hit, wst, overflow, cnt);
-    else if constexpr (WIDE >= 2000)   // speculative walk, triangle-step threshold (WIDE - 2000)/8 of live lanes
-        mesh_triangle =
-            intersect_wide_spec<COUNT, WIDE - 2000, false>(g, p.pos, p.dir, s.distance, p.last_hit, wst, overflow, cnt);
-    else if constexpr (WIDE >= 1000)   // scheduled walk, triangle batch threshold WIDE - 1000
-        mesh_triangle =
-            intersect_wide_sched<COUNT, WIDE - 1000>(g, p.pos, p.dir, s.distance, p.last_hit, wst, overflow, cnt);
-    else mesh_triangle = intersect_mesh<BATCH>(g, p.pos, p.dir, s.distance, p.last_hit, st, overflow);
+// Second half of fill_state (photon.h:272-397): the mesh hit (or an analytic
+// wire plane, FP64) -> material pair, surface, oriented normal and the four
+// interpolated bulk properties; no hit -> NO_HIT.  s.distance holds the mesh
+// hit distance on entry.
+__device__ __forceinline__ void finish_fill(const DevGeom &g, State &s, Photon &p, int mesh_triangle) {
     int m1, m2;
     bool use_analytic = false;
     int a_surface = -1, a_inner = -1, a_outer = -1;
@@ -879,6 +875,30 @@ __device__ __forceinline__ void fill_state(const DevGeom &g, State &s, Photon &p
     s.absorption_length = interp_property(g, p.wavelength, g.tables + mat1.absorption_length);
     s.scattering_length = interp_property(g, p.wavelength, g.tables + mat1.scattering_length);
     s.material1 = m1;
+}
+
+// photon.h:87-397
+template <int BATCH, int WIDE, bool COUNT>
+__device__ __forceinline__ void fill_state(const DevGeom &g, State &s, Photon &p, Stack st, WStack &wst,
+                                           uint32_t &overflow, WalkCounts &cnt, const int2 *hit) {
+    int mesh_triangle;
+    if constexpr (WIDE == HITS_MODE) {   // walked by trace_kernel: (triangle, distance)
+        const int2 h = *hit;
+        mesh_triangle = h.x;
+        s.distance = __int_as_float(h.y);
+    } else if constexpr (WIDE == 1)
+        mesh_triangle = intersect_wide<COUNT>(g, p.pos, p.dir, s.distance, p.last_hit, wst, overflow, cnt);
+    else if constexpr (WIDE >= 3000)   // speculative walk + branch-light node expansion
+        mesh_triangle =
+            intersect_wide_spec<COUNT, WIDE - 3000, true>(g, p.pos, p.dir, s.distance, p.last_hit, wst, overflow, cnt);
+    else if constexpr (WIDE >= 2000)   // speculative walk, triangle-step threshold (WIDE - 2000)/8 of live lanes
+        mesh_triangle =
+            intersect_wide_spec<COUNT, WIDE - 2000, false>(g, p.pos, p.dir, s.distance, p.last_hit, wst, overflow, cnt);
+    else if constexpr (WIDE >= 1000)   // scheduled walk, triangle batch threshold WIDE - 1000
+        mesh_triangle =
+            intersect_wide_sched<COUNT, WIDE - 1000>(g, p.pos, p.dir, s.distance, p.last_hit, wst, overflow, cnt);
+    else mesh_triangle = intersect_mesh<BATCH>(g, p.pos, p.dir, s.distance, p.last_hit, st, overflow);
+    finish_fill(g, s, p, mesh_triangle);
 }
 
 // photon.h:399-427
@@ -1318,6 +1338,7 @@ struct PropagateArgs {
     unsigned long long *alive_masks;   // one word per 64 slots
     uint32_t *counters;                // [0]: stack overflows
     const uint32_t *order;             // coherence order: work-item t runs slot order[t] (nullptr: t)
+    const int2 *hits;                  // HITS_MODE: walk result per queue position (trace_kernel)
 };
 
 __device__ __forceinline__ V3 load3(const float *p, uint32_t i) { return v3(p[3 * i], p[3 * i + 1], p[3 * i + 2]); }
@@ -1328,7 +1349,7 @@ __device__ __forceinline__ void store3(float *p, uint32_t i, V3 v) { p[3 * i] = 
 // its write-back (propagate.cu:343-353).  Returns whether it is still alive.
 template <int BATCH, int WIDE, bool COUNT>
 __device__ __forceinline__ bool run_photon(const DevGeom &g, const PropagateArgs &a, uint32_t photon_id,
-                                           uint32_t history, chr_xorwow &rng, Stack st, WStack &wst,
+                                           uint32_t qpos, uint32_t history, chr_xorwow &rng, Stack st, WStack &wst,
                                            uint32_t &overflow, WalkCounts &cnt) {
     Photon p;
     p.history = history;
@@ -1352,7 +1373,7 @@ __device__ __forceinline__ bool run_photon(const DevGeom &g, const PropagateArgs
         if (chr_isnan(prod)) { p.history |= CHR_NO_HIT | CHR_NAN_ABORT; break; }
         unsigned long long t0 = 0;
         if constexpr (COUNT) t0 = __builtin_amdgcn_s_memtime();
-        fill_state<BATCH, WIDE, COUNT>(g, s, p, st, wst, overflow, cnt);
+        fill_state<BATCH, WIDE, COUNT>(g, s, p, st, wst, overflow, cnt, a.hits + qpos);
         if constexpr (COUNT) {
             const unsigned long long t1 = __builtin_amdgcn_s_memtime();
             if (wave_leader()) cnt.wave_fill_cycles += t1 - t0;
@@ -1443,7 +1464,8 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_kernel(const DevGeom *_
             uint32_t overflow = 0;
             WalkCounts cnt{0u, 0u, 0u, 0u, 0u, 0ull, 0ull};
             const DevGeom &g = *gdev;   // device-resident: uniform s_loads, no private copy
-            alive = run_photon<BATCH, WIDE, COUNT>(g, a, photon_id, history, rng, st, wst, overflow, cnt);
+            alive = run_photon<BATCH, WIDE, COUNT>(g, a, photon_id, a.first + id, history, rng, st, wst, overflow,
+                                                   cnt);
             store_rng(a, (uint32_t)id, rng);
             flush_counters<COUNT>(a, overflow, cnt);
         }
@@ -1497,7 +1519,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_step_kernel(const DevGe
             const uint32_t history = a.flags[photon_id] & 0xFFFFu;   // photon.h:29
             if (!(history & DEAD_MASK)) {
                 if (!have_rng) { load_rng(a, slot, rng); have_rng = true; }
-                alive = run_photon<BATCH, WIDE, COUNT>(g, a, photon_id, history, rng, st, wst, overflow, cnt);
+                alive = run_photon<BATCH, WIDE, COUNT>(g, a, photon_id, pos, history, rng, st, wst, overflow, cnt);
             }
         }
         const unsigned long long mask = __ballot(alive);
@@ -1505,6 +1527,260 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_step_kernel(const DevGe
     }
     if (have_rng) store_rng(a, slot, rng);
     flush_counters<COUNT>(a, overflow, cnt);
+}
+
+// ---------------------------------------------------------------- ray binning (trace order)
+// The order in which trace_kernel walks the queued rays does not change any
+// result (each walk's result is stored at its queue position), so rays are
+// binned by direction cell (counting sort, 65,536 octahedral cells) to make the
+// 64 rays of a wave walk the same subtrees: better L1/L2 reuse of nodes.
+constexpr uint32_t NBINS = 65536;
+__device__ __forceinline__ uint32_t octa_cell(V3 d) {   // octahedral map of a unit vector, 8 bits per axis
+    const float s = fabsf(d.x) + fabsf(d.y) + fabsf(d.z);
+    float u = d.x / s, v = d.y / s;
+    if (d.z < 0.0f) {
+        const float uu = (1.0f - fabsf(v)) * (u < 0.0f ? -1.0f : 1.0f);
+        const float vv = (1.0f - fabsf(u)) * (v < 0.0f ? -1.0f : 1.0f);
+        u = uu; v = vv;
+    }
+    const uint32_t iu = (uint32_t)fminf(fmaxf((u + 1.0f) * 128.0f, 0.0f), 255.0f);
+    const uint32_t iv = (uint32_t)fminf(fmaxf((v + 1.0f) * 128.0f, 0.0f), 255.0f);
+    return (iv << 8) | iu;
+}
+__global__ __launch_bounds__(BLOCK) void bin_count_kernel(const float *dir, const uint32_t *queue, uint32_t n,
+                                                          uint32_t *keys, uint32_t *hist) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t pid = queue[i];
+    V3 d = v3(dir[3 * pid], dir[3 * pid + 1], dir[3 * pid + 2]);
+    const float l = sqrtf(d.x * d.x + d.y * d.y + d.z * d.z);
+    const uint32_t key = (l > 0.0f && l < __builtin_inff()) ? octa_cell(v3(d.x / l, d.y / l, d.z / l)) : 0u;
+    keys[i] = key;
+    atomicAdd(hist + key, 1u);
+}
+__global__ __launch_bounds__(BLOCK) void bin_key_kernel(const float *dir, const uint32_t *queue, uint32_t n,
+                                                        uint32_t *keys, uint32_t *vals) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t pid = queue[i];
+    V3 d = v3(dir[3 * pid], dir[3 * pid + 1], dir[3 * pid + 2]);
+    const float l = sqrtf(d.x * d.x + d.y * d.y + d.z * d.z);
+    keys[i] = (l > 0.0f && l < __builtin_inff()) ? octa_cell(v3(d.x / l, d.y / l, d.z / l)) : 0u;
+    vals[i] = i;
+}
+// exclusive scan of NBINS counts in place (one workgroup of 1024, 64 bins each)
+__global__ __launch_bounds__(1024) void bin_scan_kernel(uint32_t *hist) {
+    __shared__ uint32_t part[1024];
+    const uint32_t t = threadIdx.x;
+    uint32_t sum = 0;
+    for (uint32_t k = 0; k < NBINS / 1024; ++k) sum += hist[t * (NBINS / 1024) + k];
+    part[t] = sum;
+    __syncthreads();
+    for (uint32_t off = 1; off < 1024; off <<= 1) {
+        const uint32_t v = t >= off ? part[t - off] : 0u;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    uint32_t run = part[t] - sum;
+    for (uint32_t k = 0; k < NBINS / 1024; ++k) {
+        const uint32_t c = hist[t * (NBINS / 1024) + k];
+        hist[t * (NBINS / 1024) + k] = run;
+        run += c;
+    }
+}
+__global__ __launch_bounds__(BLOCK) void bin_scatter_kernel(const uint32_t *keys, uint32_t n, uint32_t *cursor,
+                                                            uint32_t *order) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n) return;
+    order[atomicAdd(cursor + keys[i], 1u)] = i;
+}
+
+// ---------------------------------------------------------------- wavefront split
+// A one-step launch (max_steps == 1, every host step above the tail) is split
+// in two kernels:
+//   trace_kernel  -- the BVH walk of fill_state (mesh.h:45-126) for every live
+//                    queued photon, written as (triangle, distance) per queue
+//                    position;
+//   propagate_step_kernel<..., HITS_MODE> -- the rest of the step, unchanged,
+//                    reading that walk result instead of walking.
+// A photon's walk depends only on its position, direction and last hit, which
+// the step does not change before fill_state, so every result is identical.
+// The trace kernel holds only the walk state (no photon physics, no RNG): it
+// needs fewer registers and less LDS than the fused step kernel, so more waves
+// fit per SIMD to hide the dependent node/triangle fetch latency, and it is
+// persistent: a lane whose walk ends fetches the next queued photon (wave-batched
+// atomic ray counter) instead of idling until the slowest lane of its wave ends.
+struct TraceArgs {
+    const float *pos, *dir;
+    const uint32_t *flags;
+    const int32_t *last_hit;
+    const uint32_t *queue;       // this step's queue
+    uint32_t n;                  // queue length
+    int2 *hits;                  // per queue position: (triangle or -1, distance bits)
+    uint32_t *next;              // ray counter (zeroed by the host)
+    uint32_t *counters;          // [0] overflows, [2..] u64 walk counters (COUNT)
+    const uint32_t *order;       // fetch order: the j-th ray walked is queue position order[j] (nullptr: j)
+    uint32_t *walk_hist;         // COUNT: [0..31] walks by log2(nodes + triangles), [32..33] u64 max (cost << 32 | photon)
+};
+
+// COUNT: walk counters; F: triangle step once F/8 of the walking lanes have
+// parked leaves (intersect_wide_spec); SL: stack entries in LDS; MINW: waves
+// per SIMD; R: refill once R of the 64 lanes are without a ray.
+template <bool COUNT, int F, int SL, int MINW, int R>
+__global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__restrict__ gdev, TraceArgs a) {
+    __shared__ uint32_t lds[(2 * SL + LEAFQ) * BLOCK];
+    WStack st;
+    uint2 spill[WIDE_STACK - SL];
+    st.spill = spill;
+    st.node = (CHR_LDS uint32_t *)(lds + threadIdx.x);
+    st.dist = (CHR_LDS float *)(lds + SL * BLOCK + threadIdx.x);
+    st.leafq = (CHR_LDS uint32_t *)(lds + 2 * SL * BLOCK + threadIdx.x);
+    const DevGeom &g = *gdev;
+    const uint32_t lane = __lane_id();
+    uint32_t overflow = 0;
+    WalkCounts cnt{0u, 0u, 0u, 0u, 0u, 0ull, 0ull};
+    bool has_ray = false, exhausted = false;
+    uint32_t q = 0, pid = 0, walk_cost = 0;
+    V3 o = v3(0.0f, 0.0f, 0.0f), d = v3(0.0f, 0.0f, 1.0f);
+    RaySlab slab = make_slab(o, d);
+    float best = 0.0f;
+    uint32_t best_rank = 0, last = 0, node = 0;
+    int best_id = -1, sp = 0;
+    bool walk_done = true;
+    uint32_t qh = 0, qt = 0, pcur = 0, pleft = 0;
+    constexpr uint32_t INVALID = 0xFFFFFFFFu;
+    while (true) {
+        if (has_ray && walk_done && pleft == 0 && qh == qt) {   // walk over: publish (mesh.h:123-125)
+            a.hits[q] = make_int2(best_id, __float_as_int(best_id == -1 ? -1.0f : best));
+            has_ray = false;
+            if constexpr (COUNT) {
+                if (a.walk_hist) {
+                    atomicAdd(a.walk_hist + (31 - __builtin_clz(walk_cost + 1)), 1u);
+                    atomicMax(reinterpret_cast<unsigned long long *>(a.walk_hist + 32),
+                              ((unsigned long long)walk_cost << 32) | pid);
+                }
+            }
+        }
+        if (!exhausted) {
+            const unsigned long long need = __ballot(!has_ray);
+            if (need != 0 && (__popcll(need) >= R || need == __ballot(1))) {
+                const int leader = __ffsll((long long)need) - 1;
+                uint32_t base = 0;
+                if ((int)lane == leader) base = atomicAdd(a.next, (uint32_t)__popcll(need));
+                base = __shfl(base, leader);
+                if (base + (uint32_t)__popcll(need) >= a.n) exhausted = true;
+                if (!has_ray) {
+                    q = base + (uint32_t)__popcll(need & ((1ull << lane) - 1ull));
+                    if (q < a.n) {
+                        if (a.order) q = a.order[q];
+                        pid = a.queue[q];
+                        // dead on entry / NaN: no walk (the step kernel skips / aborts them)
+                        if (!((a.flags[pid] & 0xFFFFu) & DEAD_MASK)) {
+                            o = load3(a.pos, pid);
+                            d = load3(a.dir, pid);
+                            d = d / norm(d);                        // propagate.cu:280-281
+                            const float prod = ((((d.x * d.y) * d.z) * o.x) * o.y) * o.z;
+                            if (!chr_isnan(prod)) {
+                                slab = make_slab(v3(-o.x / d.x, -o.y / d.y, -o.z / d.z),
+                                                 v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z));
+                                best = __builtin_inff();
+                                best_rank = 0xFFFFFFFFu;
+                                best_id = -1;
+                                last = (uint32_t)a.last_hit[pid];
+                                sp = 0;
+                                node = 0;
+                                walk_done = false;
+                                has_ray = true;
+                                walk_cost = 0;
+                                if constexpr (COUNT) cnt.walks++;
+                            }
+                        }
+                    }
+                }
+            }
+        }
+        const bool has_work = has_ray && (pleft != 0 || qh != qt);
+        const bool can_walk = has_ray && !walk_done && (qt - qh) <= (uint32_t)(LEAFQ - 8);
+        const unsigned long long mw = __ballot(can_walk);
+        const unsigned long long mt = __ballot(has_work);
+        if ((mw | mt) == 0) {
+            if (exhausted && __ballot(has_ray) == 0) break;
+            continue;                                    // walks ended: publish + refill
+        }
+        if (mw != 0 && 8 * __popcll(mt) < F * __popcll(mw | mt)) {
+            // ------------------------------------------------ node step
+            if (!can_walk) continue;
+            if (node == INVALID) {
+                bool found = false;
+                while (sp > 0) {
+                    sp--;
+                    float t;
+                    wpop<SL>(st, sp, node, t);
+                    if (!(t > best)) { found = true; break; }
+                }
+                if (!found) { walk_done = true; continue; }
+            }
+            if constexpr (COUNT) { cnt.nodes++; walk_cost++; if (wave_leader()) cnt.wave_nodes++; }
+            const uint4 *np = g.wnodes + (size_t)g.wstride * node;
+            const uint4 h = gld(np), a1 = gld(np + 1), a2 = gld(np + 2), a3 = gld(np + 3), a4 = gld(np + 4),
+                        a5 = gld(np + 5);
+            uint32_t near_node;
+            float near_t;
+            uint32_t leaf_mask =
+                expand_node<SL>(h, a1, a2, a3, a4, a5, slab, best, near_node, near_t, st, sp, overflow);
+            node = near_node;
+            while (leaf_mask) {
+                const int k = __builtin_ctz(leaf_mask);
+                leaf_mask &= leaf_mask - 1;
+                const uint32_t kind = ((k < 4 ? a4.z : a4.w) >> (8 * (k & 3))) & 0xFFu;
+                const uint32_t first = a4.y + (((k < 4 ? a5.x : a5.y) >> (8 * (k & 3))) & 0xFFu);
+                st.leafq[(qt % LEAFQ) * BLOCK] = first | ((kind - 1u) << 30);
+                qt++;
+            }
+        } else {
+            // ------------------------------------------------ triangle step
+            if (!has_work) continue;
+            if (pleft == 0) {
+                const uint32_t e = st.leafq[(qh % LEAFQ) * BLOCK];
+                qh++;
+                pcur = e & 0x3FFFFFFFu;
+                pleft = (e >> 30) + 1u;
+            }
+            if constexpr (COUNT) { cnt.tris++; walk_cost++; if (wave_leader()) cnt.wave_tris++; }
+            const float4 *r = g.wtri + 4 * (size_t)pcur;
+            const float4 r0 = gld(r), r1 = gld(r + 1), r2 = gld(r + 2);
+            pcur++;
+            pleft--;
+            const uint32_t id = __float_as_uint(r2.y);
+            float dist;
+            if (id == last ||
+                !intersect_triangle(o, d, v3(r0.x, r0.y, r0.z), v3(r0.w, r1.x, r1.y), v3(r1.z, r1.w, r2.x), dist))
+                continue;
+            const uint32_t rank = __float_as_uint(r2.z);
+            if (!(dist < best || (dist == best && rank < best_rank))) continue;
+            const float4 r3 = gld(r + 3);
+            V3 lo, hi;
+            node_bounds(g, make_uint4(__float_as_uint(r2.w), __float_as_uint(r3.x), __float_as_uint(r3.y), 0u), lo, hi);
+            float bd;
+            if (!intersect_box(v3(-o.x / d.x, -o.y / d.y, -o.z / d.z), v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z), lo, hi,
+                               bd) ||
+                bd > best)
+                continue;                                // mesh.h:94-96
+            best = dist;
+            best_rank = rank;
+            best_id = (int)id;
+        }
+    }
+    if (overflow) atomicAdd(a.counters, overflow);
+    if constexpr (COUNT) {
+        unsigned long long *c64 = reinterpret_cast<unsigned long long *>(a.counters + 2);
+        atomicAdd(c64, (unsigned long long)cnt.nodes);
+        atomicAdd(c64 + 1, (unsigned long long)cnt.tris);
+        atomicAdd(c64 + 2, (unsigned long long)cnt.walks);
+        atomicAdd(c64 + 3, (unsigned long long)cnt.wave_nodes);
+        atomicAdd(c64 + 4, (unsigned long long)cnt.wave_tris);
+    }
 }
 
 // Coherence key of a queued photon: 18-bit Morton code of its position in the
@@ -1862,9 +2138,15 @@ extern "C" int chr_rng_download(const uint32_t *d_states, uint32_t nslots, uint3
     return CHR_OK;
 }
 
+static size_t sort_temp_bytes16(uint32_t n) {
+    size_t bytes = 0;
+    (void)rocprim::radix_sort_pairs((void *)nullptr, bytes, (const uint32_t *)nullptr, (uint32_t *)nullptr,
+                                    (const uint32_t *)nullptr, (uint32_t *)nullptr, n, 0, 16);
+    return bytes;
+}
 static size_t sort_temp_bytes(uint32_t n) {
     size_t bytes = 0;
-    rocprim::radix_sort_pairs((void *)nullptr, bytes, (const uint32_t *)nullptr, (uint32_t *)nullptr,
+    (void)rocprim::radix_sort_pairs((void *)nullptr, bytes, (const uint32_t *)nullptr, (uint32_t *)nullptr,
                               (const uint32_t *)nullptr, (uint32_t *)nullptr, n, 0, 30);
     return bytes;
 }
@@ -1915,12 +2197,65 @@ static propagate_fn select_variant(const chr_geometry *g) {
 }
 
 typedef void (*propagate_step_fn)(const DevGeom *, PropagateArgs, uint32_t);
-static propagate_step_fn select_step_variant(const chr_geometry *g) {
+typedef void (*trace_fn)(const DevGeom *, TraceArgs);
+static propagate_step_fn select_step_fn(int v);
+struct StepVariant {
+    propagate_step_fn fn;     // fused step kernel (any max_steps)
+    trace_fn trace;           // one-step launches: trace_kernel + shade kernel (nullptr: fused)
+    propagate_step_fn shade;
+    int trace_waves;          // waves per SIMD of the trace kernel (persistent grid size)
+    int binned;               // trace rays in direction-binned order: 1 atomic counting sort, 2 radix sort,
+                              // 3 radix sort on the first host step of a propagate only (n >= kBinFirstMin)
+};
+// Direction binning pays where the rays of a step share an origin -- the
+// first step of a point or track source -- and not after the first bounce
+// (demo.detector(), 4M photons: first-step walk 2.65 -> 2.21 ms for 0.11 ms of
+// sorting; second step unchanged).
+static constexpr uint32_t kBinFirstMin = 1u << 20;
+static StepVariant select_step_variant(const chr_geometry *g) {
     const char *e = getenv("CHR_PROPAGATE_VARIANT");
     int v = e ? atoi(e) : 0;
     if (g->dev.nwnodes == 0) v = kExactVariant;
     const bool queue_ok = g->dev.nwtri < (1u << 30);   // leaf-queue entries hold 30-bit record indices
     if (!queue_ok && (v == 0 || v == 5 || v >= 12)) v = (v == 5) ? 11 : 10;
+    // 0 (default) = 64, 5 (counting form of the default) = 65; 66 / 67: the fused
+    // step kernel alone (previous default) and its counting form
+    if (v == 0) v = 64;
+    else if (v == 5) v = 65;
+    else if (v == 66) v = 0;
+    else if (v == 67) v = 5;
+    StepVariant sv{select_step_fn(v), nullptr, nullptr, 0, 0};
+    propagate_step_fn shade = propagate_step_kernel<8, 4, HITS_MODE>;
+    switch (v) {   // wavefront split: trace_kernel<COUNT, F, SL, MINW, R>
+        case 50: sv.trace = trace_kernel<false, 6, 12, 4, 16>; sv.trace_waves = 4; break;
+        case 51: sv.trace = trace_kernel<true, 6, 12, 4, 16>; sv.trace_waves = 4;
+                 sv.fn = select_step_fn(5); break;
+        case 52: sv.trace = trace_kernel<false, 6, 8, 5, 16>; sv.trace_waves = 5; break;
+        case 53: sv.trace = trace_kernel<false, 6, 4, 6, 16>; sv.trace_waves = 6; break;
+        case 54: sv.trace = trace_kernel<false, 6, 12, 4, 32>; sv.trace_waves = 4; break;
+        case 55: sv.trace = trace_kernel<false, 6, 12, 4, 8>; sv.trace_waves = 4; break;
+        case 56: sv.trace = trace_kernel<false, 4, 12, 4, 16>; sv.trace_waves = 4; break;
+        case 57: sv.trace = trace_kernel<false, 6, 12, 4, 32>; sv.trace_waves = 4; sv.binned = 1; break;
+        case 58: sv.trace = trace_kernel<true, 6, 12, 4, 32>; sv.trace_waves = 4; sv.binned = 1;
+                 sv.fn = select_step_fn(5); break;
+        case 59: sv.trace = trace_kernel<false, 6, 4, 6, 32>; sv.trace_waves = 6; sv.binned = 1; break;
+        case 60: sv.trace = trace_kernel<false, 6, 12, 4, 32>; sv.trace_waves = 4; sv.binned = 2; break;
+        case 61: sv.trace = trace_kernel<false, 6, 12, 4, 32>; sv.trace_waves = 4; sv.binned = 2;
+                 shade = propagate_step_kernel<8, 2, HITS_MODE>; break;
+        case 62: sv.trace = trace_kernel<false, 6, 12, 4, 32>; sv.trace_waves = 4; sv.binned = 2;
+                 shade = propagate_step_kernel<8, 3, HITS_MODE>; break;
+        case 63: sv.trace = trace_kernel<false, 6, 12, 4, 32>; sv.trace_waves = 4;
+                 shade = propagate_step_kernel<8, 2, HITS_MODE>; break;
+        case 64: sv.trace = trace_kernel<false, 6, 12, 4, 32>; sv.trace_waves = 4; sv.binned = 3;
+                 shade = propagate_step_kernel<8, 2, HITS_MODE>; break;
+        case 65: sv.trace = trace_kernel<true, 6, 12, 4, 32>; sv.trace_waves = 4; sv.binned = 3;
+                 shade = propagate_step_kernel<8, 2, HITS_MODE>; sv.fn = select_step_fn(5); break;
+        default: break;
+    }
+    if (sv.trace) sv.shade = shade;
+    return sv;
+}
+static propagate_step_fn select_step_fn(int v) {
     switch (v) {
         case 1: return propagate_step_kernel<8, 4, 0>;
         case 5: return propagate_step_kernel<8, 4, kWalk, true>;
@@ -1963,6 +2298,7 @@ static int launch_chunk(const chr_geometry *g, const chr_photons *ph, uint32_t *
     a.max_steps = max_steps; a.use_weights = use_weights; a.scatter_first = scatter_first;
     a.alive_masks = masks; a.counters = counters;
     a.order = nullptr;
+    a.hits = nullptr;
     if (sort_enabled() && nthreads >= kSortMin) {
         // coherence order (sort_key_kernel): rays that start close together in
         // similar directions share a wave
@@ -1993,10 +2329,21 @@ static int launch_chunk(const chr_geometry *g, const chr_photons *ph, uint32_t *
 // one host step as one launch of propagate_step_kernel over the n queued
 // photons (slot = queue position mod cap); same scratch layout as launch_chunk
 // with mask words per queue position.
+static int device_cus() {
+    static int cus[16] = {};
+    int dev = 0;
+    CHR_HIP_CHECK(hipGetDevice(&dev));
+    if (!cus[dev & 15]) CHR_HIP_CHECK(hipDeviceGetAttribute(&cus[dev & 15], hipDeviceAttributeMultiprocessorCount, dev));
+    return cus[dev & 15];
+}
+
+static bool trace_steps();
+// hits: n (triangle, distance) slots + a ray counter word, for the split path
 static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *rng, uint32_t nslots, uint32_t cap,
                        uint32_t n, const uint32_t *in_queue, uint32_t *out_queue, int32_t max_steps,
                        int32_t use_weights, int32_t scatter_first, uint32_t *scratch, hipStream_t stream,
-                       hipEvent_t ev0, hipEvent_t ev1) {
+                       hipEvent_t ev0, hipEvent_t ev1, int2 *hits, uint32_t *sort_space, bool first_step,
+                       hipEvent_t evt0, hipEvent_t evt1, bool *split_out) {
     const uint32_t nwords = (n + 63) / 64;
     uint32_t *counters = scratch;
     unsigned long long *masks = (unsigned long long *)(scratch + 16);
@@ -2009,9 +2356,54 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
     a.max_steps = max_steps; a.use_weights = use_weights; a.scatter_first = scatter_first;
     a.alive_masks = masks; a.counters = counters;
     a.order = nullptr;
+    a.hits = nullptr;
     const uint32_t threads = std::min(cap, (n + 63u) & ~63u);
-    if (ev0) CHR_HIP_CHECK(hipEventRecord(ev0, stream));
-    hipLaunchKernelGGL(select_step_variant(g), dim3(grid_for(threads)), dim3(BLOCK), 0, stream,
+    const StepVariant sv = select_step_variant(g);
+    const bool split = sv.trace && hits && max_steps == 1;
+    if (split) {
+        uint32_t *next = (uint32_t *)(hits + n);
+        CHR_HIP_CHECK(hipMemsetAsync(next, 0, 4, stream));
+        TraceArgs ta;
+        ta.pos = ph->d_pos; ta.dir = ph->d_dir; ta.flags = ph->d_flags; ta.last_hit = ph->d_last_hit_triangles;
+        ta.queue = in_queue; ta.n = n; ta.hits = hits; ta.next = next; ta.counters = counters; ta.order = nullptr;
+        ta.walk_hist = nullptr;
+        if (trace_steps()) {   // debugging: per-walk cost histogram (counting variants), printed per step
+            ta.walk_hist = next + 16 + 2 * (size_t)n + NBINS;
+            CHR_HIP_CHECK(hipMemsetAsync(ta.walk_hist, 0, 34 * 4, stream));
+        }
+        if (ev0) CHR_HIP_CHECK(hipEventRecord(ev0, stream));
+        if (sv.binned == 1) {   // hits region: [hits n x int2][next][pad] [keys n][order n][hist NBINS]
+            uint32_t *keys = next + 16, *order = keys + n, *hist = order + n;
+            CHR_HIP_CHECK(hipMemsetAsync(hist, 0, NBINS * 4, stream));
+            hipLaunchKernelGGL(bin_count_kernel, dim3(grid_for(n)), dim3(BLOCK), 0, stream, ph->d_dir, in_queue, n,
+                               keys, hist);
+            hipLaunchKernelGGL(bin_scan_kernel, dim3(1), dim3(1024), 0, stream, hist);
+            hipLaunchKernelGGL(bin_scatter_kernel, dim3(grid_for(n)), dim3(BLOCK), 0, stream, keys, n, hist, order);
+            ta.order = order;
+        } else if (sv.binned == 2 || (sv.binned == 3 && first_step && n >= kBinFirstMin)) {   // 16-bit radix sort of (cell, queue position); temp space after the hits region
+            uint32_t *keys = next + 16, *order = keys + n;
+            hipLaunchKernelGGL(bin_key_kernel, dim3(grid_for(n)), dim3(BLOCK), 0, stream, ph->d_dir, in_queue, n, keys,
+                               order);
+            uint32_t *keys_out = sort_space, *vals_out = keys_out + n;
+            void *temp = (void *)(((uintptr_t)(vals_out + n) + 255) & ~(uintptr_t)255);
+            size_t temp_bytes = sort_temp_bytes16(n);
+            CHR_HIP_CHECK(rocprim::radix_sort_pairs(temp, temp_bytes, keys, keys_out, order, vals_out, n, 0, 16,
+                                                    stream));
+            ta.order = vals_out;
+        }
+        const int cus = device_cus();
+        if (cus <= 0) return chr::fail(CHR_ERR_HIP, "launch_step: no compute units");
+        const uint64_t resident = (uint64_t)cus * 4 * sv.trace_waves * 64 / BLOCK;   // persistent grid
+        const uint32_t blocks = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(resident, grid_for(n)));
+        if (evt0) CHR_HIP_CHECK(hipEventRecord(evt0, stream));
+        hipLaunchKernelGGL(sv.trace, dim3(blocks), dim3(BLOCK), 0, stream, (const DevGeom *)g->d_dev, ta);
+        if (evt1) CHR_HIP_CHECK(hipEventRecord(evt1, stream));
+        a.hits = hits;
+    } else if (ev0) {
+        CHR_HIP_CHECK(hipEventRecord(ev0, stream));
+    }
+    if (split_out) *split_out = split;
+    hipLaunchKernelGGL(split ? sv.shade : sv.fn, dim3(grid_for(threads)), dim3(BLOCK), 0, stream,
                        (const DevGeom *)g->d_dev, a, cap);
     if (ev1) CHR_HIP_CHECK(hipEventRecord(ev1, stream));
     launch_mask_scan(masks, nwords, offsets, bsums, out_queue, counters + 1, nullptr, stream);
@@ -2074,6 +2466,11 @@ static int apply_node_layout(const chr_geometry *cg, hipStream_t stream) {
     return CHR_OK;
 }
 
+static bool trace_steps() {   // CHR_TRACE_STEPS=1: one stderr line per host step (debugging)
+    const char *e = getenv("CHR_TRACE_STEPS");
+    return e && e[0] == '1';
+}
+
 static bool step_launch_enabled() {   // CHR_STEP_LAUNCH=0: the reference's one-launch-per-chunk structure (A/B)
     const char *e = getenv("CHR_STEP_LAUNCH");
     return !(e && e[0] == '0');
@@ -2102,25 +2499,37 @@ extern "C" int chr_propagate(const chr_geometry *g, const chr_photons *ph, uint3
     uint64_t swords = chr_propagate_scratch_words(chunk_cap);
     if (fused) swords = std::max<uint64_t>(swords, 16 + mask_scan_words(nphotons) + 16);
     const size_t qbytes = ((size_t)nphotons + 1) * 4;
+    // split path: hits, ray counter, binning keys/order/histogram
+    const size_t hbytes = fused ? (size_t)nphotons * 24 + 128 + NBINS * 4 + 256 + 512 + sort_temp_bytes16(nphotons) : 0;
     void *buf = nullptr;
-    int rc = scratch_get(2 * qbytes + swords * 4 + 64, &buf);
+    int rc = scratch_get(2 * qbytes + swords * 4 + 64 + hbytes, &buf);
     if (rc) return rc;
     uint32_t *q[2];
     q[0] = (uint32_t *)buf;
     q[1] = q[0] + (nphotons + 1);
     uint32_t *scratch = (uint32_t *)(((uintptr_t)(q[1] + nphotons + 1) + 15) & ~(uintptr_t)15);
+    int2 *hits = fused ? (int2 *)(((uintptr_t)(scratch + swords) + 15) & ~(uintptr_t)15) : nullptr;
+    // radix-sort space after [hits][next+pad][keys][order][hist][walk hist]
+    uint32_t *sort_space = fused ? (uint32_t *)(((uintptr_t)((uint32_t *)(hits + nphotons) + 16 + 2 * (size_t)nphotons +
+                                                            NBINS + 64) + 255) & ~(uintptr_t)255) : nullptr;
     uint32_t *pinned = nullptr;
     if ((rc = pinned_words(&pinned))) return rc;
-    const size_t max_chunks = fused ? 1 : (nphotons + chunk_cap - 1) / chunk_cap;
+    const size_t max_chunks = fused ? 2 : (nphotons + chunk_cap - 1) / chunk_cap;   // fused: step + its walk
     std::vector<hipEvent_t> *evp = nullptr;
     if ((rc = timing_events(2 * max_chunks, &evp))) return rc;
     std::vector<hipEvent_t> &events = *evp;
-    double kernel_ms = 0.0;
+    double kernel_ms = 0.0, trace_ms = 0.0;
+    bool split_step = false;
     auto collect = [&](size_t nchunks) -> int {
         for (size_t c = 0; c < nchunks; ++c) {
             float ms = 0.0f;
             CHR_HIP_CHECK(hipEventElapsedTime(&ms, events[2 * c], events[2 * c + 1]));
             kernel_ms += ms;
+        }
+        if (fused && split_step) {
+            float ms = 0.0f;
+            CHR_HIP_CHECK(hipEventElapsedTime(&ms, events[2], events[3]));
+            trace_ms += ms;
         }
         return CHR_OK;
     };
@@ -2134,13 +2543,19 @@ extern "C" int chr_propagate(const chr_geometry *g, const chr_photons *ph, uint3
     int step = 0;
     while (step < max_steps) {
         const int nsteps = (n < (int64_t)ntpb * 16 * 8 || use_weights) ? max_steps - step : 1;   // photon.py:261-264
+        const int64_t n_prev = n;
         size_t nchunks = 0;
         if (fused) {
             rc = launch_step(g, ph, d_rng_states, rng_nslots, (uint32_t)cap, (uint32_t)n, q[cur] + 1, q[cur ^ 1],
-                             nsteps, use_weights, scatter_first, scratch, stream, events[0], events[1]);
+                             nsteps, use_weights, scatter_first, scratch, stream, events[0], events[1], hits,
+                             sort_space, step == 0, events[2], events[3], &split_step);
             if (rc) return rc;
             st.launches++;
             nchunks = 1;
+            if (split_step) {
+                st.trace_launches++;
+                st.trace_rays += (uint64_t)n;
+            }
         } else {
             int64_t first = 0;
             while (first < n) {
@@ -2169,6 +2584,17 @@ extern "C" int chr_propagate(const chr_geometry *g, const chr_photons *ph, uint3
             if ((rc = collect(nchunks))) return rc;
             nchunks = 0;
             n = (int64_t)pinned[0] - 1;
+            if (trace_steps()) {
+                fprintf(stderr, "chr_propagate: step %d nsteps %d -> %lld alive\n", step, nsteps, (long long)n);
+                if (nsteps == 1 && hits) {   // walk-cost histogram of a counting trace variant (zeros otherwise)
+                    uint32_t wh[34];
+                    CHR_HIP_CHECK(hipMemcpy(wh, (uint32_t *)(hits + n_prev) + 16 + 2 * (size_t)n_prev + NBINS, sizeof(wh),
+                                            hipMemcpyDeviceToHost));
+                    fprintf(stderr, "  walk cost (nodes+triangles) log2 histogram:");
+                    for (int b = 0; b < 32; ++b) if (wh[b]) fprintf(stderr, " [%u,%u):%u", 1u << b, 2u << b, wh[b]);
+                    fprintf(stderr, "\n  worst walk: cost %u photon %u\n", wh[33], wh[32]);
+                }
+            }
             pinned[1] = 1;
             CHR_HIP_CHECK(hipMemcpyAsync(q[cur ^ 1], pinned + 1, 4, hipMemcpyHostToDevice, stream));
             if (n == 0) break;
@@ -2194,6 +2620,7 @@ extern "C" int chr_propagate(const chr_geometry *g, const chr_photons *ph, uint3
         st.wave_triangle_steps = c[4];
     }
     st.kernel_ms = kernel_ms;
+    st.trace_ms = trace_ms;
     st.final_alive = (step < max_steps) ? (uint32_t)n : 0u;
     if (stats) *stats = st;
     return CHR_OK;

@@ -166,6 +166,10 @@ typedef struct chr_propagate_stats {
     uint64_t wave_triangle_steps; /* nodes_visited / (64 * wave_node_steps)); counting variant only */
     uint64_t wave_fill_cycles;    /* s_memtime cycles waves spent in fill_state (traversal) and in */
     uint64_t wave_step_cycles;    /* whole photon step loops; counting variant only */
+    double trace_ms;              /* device time of the BVH-walk kernel (trace_kernel) alone, HIP events */
+    uint32_t trace_launches;      /* one-step launches walked by trace_kernel */
+    uint32_t reserved;
+    uint64_t trace_rays;          /* queued photons handed to those launches */
 } chr_propagate_stats;
 
 /* replaces: GPUPhotons.propagate host loop (chroma/gpu/photon.py:226-293) for

@@ -31,7 +31,9 @@ def main():
     torch.cuda.set_device(0)
     os.environ['CHR_NODE_LAYOUT_AB'] = '1'      # keep both node layouts on the device (":n128" variants)
     det = bench.build_geometry(args.detector, '/tmp/chroma_bench_cache')
+    t0 = time.time()
     gdet = gpu.GPUDetector(det)
+    print('geometry on device in %.1fs' % (time.time() - t0), flush=True)
     photons = isotropic(args.photons, seed=20260102)
     pristine = SimpleNamespace(pos=ga.to_gpu(gpu.to_float3(photons.pos)), dir=ga.to_gpu(gpu.to_float3(photons.dir)),
                                pol=ga.to_gpu(gpu.to_float3(photons.pol)), wavelengths=ga.to_gpu(photons.wavelengths),
@@ -55,6 +57,7 @@ def main():
             gp.propagate(gdet, rng, nthreads_per_block=512, max_blocks=1024, max_steps=args.max_steps)
             torch.cuda.synchronize()
             dt = time.perf_counter() - t0
+            print('  round %d variant %s: %.1f ms' % (r, v, 1e3 * dt), flush=True)
             fl = (gp.flags.get(), gp.last_hit_triangles.get(), gp.pos.get().view(np.uint32).reshape(len(fl0 := gp.flags.get()), -1))
             if ref_flags is None:
                 ref_flags = fl

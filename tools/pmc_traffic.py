@@ -26,21 +26,29 @@ def per_kernel(d, counter):
                 vals[key] = vals.get(key, 0.0) + float(row['Counter_Value'])
     out = {}
     for (_, name), v in vals.items():
-        if re.search(r'propagate_(step_)?kernel<[^>]*, false>', name):
-            short = 'chr::propagate_kernel'
-        elif 'propagate' in name and 'kernel' in name and ', true>' in name:
-            short = 'counting_variant'
-        else:
-            short = name.split('(')[0]
-        out.setdefault(short, []).append(v)
+        out.setdefault(kernel_class(name), []).append(v)
     return out
+
+
+def kernel_class(name):
+    """Kernels of the propagate path by role (the counting variant, run untimed
+    by bench.py, is kept apart)."""
+    if ', true>' in name:
+        return 'counting_variant'
+    if 'trace_kernel' in name:
+        return 'chr::trace_kernel'
+    if re.search(r'propagate_step_kernel<[^>]*9000', name):
+        return 'chr::propagate_step_kernel (shade)'
+    if re.search(r'propagate_(step_)?kernel<', name):
+        return 'chr::propagate_step_kernel (fused walk + shade)'
+    return name.split('(')[0]
 
 
 def main():
     d = sys.argv[1]
     fetch = per_kernel(os.path.join(d, 'fetch'), 'FETCH_SIZE')
     write = per_kernel(os.path.join(d, 'write'), 'WRITE_SIZE')
-    k = 'chr::propagate_kernel'
+    k = 'chr::trace_kernel'     # the dominant kernel (bench.py roofline)
     res = {'kernel': k}
     if k in fetch:
         f = fetch[k]
@@ -53,6 +61,14 @@ def main():
         res['write_bytes_per_launch'] = 1024.0 * sum(w) / len(w)
     if 'read_bytes_per_launch' in res and 'write_bytes_per_launch' in res:
         res['hbm_bytes_per_launch'] = res['read_bytes_per_launch'] + res['write_bytes_per_launch']
+    # every propagate-path kernel: total HBM bytes over the pass, by role
+    res['by_kernel'] = {}
+    for name in sorted(set(fetch) | set(write)):
+        if 'propagate' not in name and 'trace' not in name and 'scan' not in name and 'bin_' not in name:
+            continue
+        res['by_kernel'][name] = {'launches': len(fetch.get(name, [])),
+                                  'read_bytes_total': 2.0 * 1024.0 * sum(fetch.get(name, [])),
+                                  'write_bytes_total': 1024.0 * sum(write.get(name, []))}
     # the workload the passes ran (bench.py only uses a summary of its own workload)
     try:
         with open(os.path.join(d, 'bench_fetch.json')) as f:
