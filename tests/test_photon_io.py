@@ -1,0 +1,150 @@
+"""Photon I/O formats either side of the path:
+the RAT ZeroMQ wire format (reference bin/chroma-server-rat:29-70) and the
+chroma-profile photon archives (reference bin/chroma-profile:206-251)."""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+
+BIN = os.path.join(ROOT, 'chroma-lite_amd', 'bin')
+
+
+def _photons(n, seed=3):
+    from chroma.io.photons_npz import synthetic_photons
+    return synthetic_photons(n, seed)
+
+
+def test_rat_request_round_trip():
+    from chroma.io import rat
+    ph = _photons(1000)
+    ph.t = np.linspace(0, 50, 1000).astype(np.float32)
+    msg = rat.encode_request(ph, 42, trackids=np.arange(1000))
+    assert len(msg) == 8 + 88 * 1000 + 4 * 1000
+    assert np.array_equal(np.frombuffer(msg[:8], '<u4'), [1000, 42])
+    # plane order x y z dx dy dz polx poly polz wavelength t, f64
+    planes = np.frombuffer(msg[8:8 + 88 * 1000], '<f8').reshape(11, 1000)
+    assert np.array_equal(planes[1], ph.pos[:, 1].astype(np.float64))
+    assert np.array_equal(planes[9], ph.wavelengths.astype(np.float64))
+    got, evid, tid = rat.decode_request(msg)
+    assert evid == 42 and np.array_equal(tid, np.arange(1000))
+    for f in ('pos', 'dir', 'pol', 'wavelengths', 't'):
+        assert getattr(got, f).dtype == np.float32
+        assert np.array_equal(getattr(got, f), getattr(ph, f))
+    with pytest.raises(ValueError):
+        rat.decode_request(msg[:-4])
+    empty = rat.encode_request(_photons(0), 7)
+    got, evid, tid = rat.decode_request(empty)
+    assert len(got) == 0 and evid == 7
+
+
+def test_rat_reply_layout():
+    """Hits grouped by ascending channel, photon order inside a channel; 11 f32
+    planes, then the channel ids twice."""
+    from chroma.io import rat
+    from chroma.event import Photons
+    a, b = _photons(3, 1), _photons(2, 2)
+    reply = rat.encode_reply({17: a, 4: b}, 9)
+    n = 5
+    assert len(reply) == 8 + 44 * n + 8 * n
+    assert np.array_equal(np.frombuffer(reply[:8], '<u4'), [5, 9])
+    planes = np.frombuffer(reply[8:8 + 44 * n], '<f4').reshape(11, n)
+    assert np.array_equal(planes[0], np.concatenate([b.pos[:, 0], a.pos[:, 0]]))
+    assert np.array_equal(planes[10], np.concatenate([b.t, a.t]))
+    ids = np.frombuffer(reply[8 + 44 * n:], '<u4').reshape(2, n)
+    assert np.array_equal(ids[0], [4, 4, 17, 17, 17]) and np.array_equal(ids[1], ids[0])
+    got, evid = rat.decode_reply(reply)
+    assert evid == 9 and np.array_equal(got.channel, ids[0])
+    assert np.array_equal(got.dir, np.concatenate([b.dir, a.dir]))
+    assert rat.decode_reply(rat.encode_reply({}, 3))[0].pos.shape == (0, 3)
+    assert isinstance(got, Photons)
+
+
+def test_rat_server_needs_zmq():
+    from chroma.io import rat
+    try:
+        import zmq  # noqa: F401
+        pytest.skip('pyzmq present')
+    except ImportError:
+        with pytest.raises(ImportError, match='pyzmq'):
+            rat.serve(None)
+
+
+def test_photons_npz_round_trip(tmp_path):
+    from chroma.io.photons_npz import load_photons_npz, save_photons_npz
+    ph = _photons(500)
+    ph.flags[:] = 4
+    ph.evidx[:] = 2
+    path = str(tmp_path / 'p.npz')
+    save_photons_npz(path, ph)
+    got = load_photons_npz(path)
+    for f in ('pos', 'dir', 'pol', 'wavelengths', 't', 'last_hit_triangles', 'flags', 'weights', 'evidx'):
+        assert np.array_equal(getattr(got, f), getattr(ph, f)), f
+    # only the required arrays: t zeros, Photons defaults for the rest
+    path2 = str(tmp_path / 'q.npz')
+    np.savez(path2, pos=ph.pos, dir=ph.dir, pol=ph.pol, wavelengths=ph.wavelengths)
+    got = load_photons_npz(path2)
+    assert (got.t == 0).all() and (got.last_hit_triangles == -1).all() and (got.weights == 1).all()
+    path3 = str(tmp_path / 'r.npz')
+    np.savez(path3, pos=ph.pos, dir=ph.dir)
+    with pytest.raises(RuntimeError, match='pol, wavelengths'):
+        load_photons_npz(path3)
+
+
+def test_synthetic_source():
+    """chroma-profile's generator: reproducible per seed, unit directions,
+    polarisation perpendicular to direction, wavelengths in [380, 500)."""
+    from chroma.io.photons_npz import synthetic_photons
+    a, b = synthetic_photons(2000, 11), synthetic_photons(2000, 11)
+    assert np.array_equal(a.pos, b.pos) and np.array_equal(a.pol, b.pol)
+    assert np.allclose(np.linalg.norm(a.dir, axis=1), 1, atol=1e-6)
+    assert np.abs((a.dir * a.pol).sum(axis=1)).max() < 1e-5
+    assert a.wavelengths.min() >= 380 and a.wavelengths.max() < 500 and (np.abs(a.pos) <= 1000).all()
+
+
+def test_cli_help():
+    for script in ('chroma-profile', 'chroma-server-rat'):
+        out = subprocess.run([sys.executable, os.path.join(BIN, script), '--help'], capture_output=True, text=True,
+                             timeout=120)
+        assert out.returncode == 0, out.stderr
+        assert 'usage' in out.stdout
+
+
+@pytest.mark.gpu
+def test_rat_request_end_to_end():
+    """A RAT request through Simulation gives the reply built from the same
+    Simulation's per-channel hits (same seed)."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip('no HIP device')
+    from chroma import demo, loader
+    from chroma.io import rat
+    from chroma.sim import Simulation
+    from chroma.photon_source import isotropic
+    det = loader.create_geometry_from_obj(demo.detector(600.0, 900.0, 1500.0))
+    ph = isotropic(20000, seed=4)
+    msg = rat.encode_request(ph, 5, trackids=np.arange(20000))
+    reply = rat.handle_request(Simulation(det, seed=77, nthreads_per_block=64, max_blocks=256), msg)
+    ev = next(Simulation(det, seed=77, nthreads_per_block=64, max_blocks=256).simulate(
+        ph, keep_hits=True, run_daq=False, max_steps=1000))
+    assert reply == rat.encode_reply(ev.hits, 5)
+    got, evid = rat.decode_reply(reply)
+    assert evid == 5 and len(got) == sum(len(v) for v in ev.hits.values()) > 0
+
+
+@pytest.mark.gpu
+def test_chroma_profile_runs(tmp_path):
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip('no HIP device')
+    from chroma.io.photons_npz import save_photons_npz
+    path = str(tmp_path / 'ph.npz')
+    save_photons_npz(path, _photons(50000, 8))
+    out = subprocess.run([sys.executable, os.path.join(BIN, 'chroma-profile'), '@chroma.demo.tiny', '--photons-npz',
+                          path, '--seed', '3', '--keep-hits', '--max-steps', '100'], capture_output=True, text=True,
+                         timeout=300)
+    assert out.returncode == 0, out.stderr[-2000:]
+    assert 'Total photons: 50,000' in out.stdout and 'propagate' in out.stdout and 'Detected hits' in out.stdout
