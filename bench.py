@@ -220,7 +220,16 @@ def main():
     from chroma.photon_source import isotropic
     from types import SimpleNamespace
 
-    det = build_geometry(args.detector, args.cache_dir)
+    if dist is not None and args.cache_dir:
+        # rank 0 builds (flatten + BVH, minutes for the 29k detector) and fills the
+        # local cache; the other ranks of the node wait, then load it
+        if rank == 0:
+            det = build_geometry(args.detector, args.cache_dir)
+        dist.barrier()
+        if rank != 0:
+            det = build_geometry(args.detector, args.cache_dir)
+    else:
+        det = build_geometry(args.detector, args.cache_dir)
     t0 = time.time()
     gdet = gpu.GPUDetector(det)
     log('rank %d: geometry on device in %.1fs (%.2f GB)' % (rank, time.time() - t0, gdet.device_bytes() / 1e9))

@@ -240,7 +240,8 @@ def geometry_from_arrays(z, man):
 
 
 def _write_npz(path, arrays):
-    tmp = path + '.tmp.npz'
+    # unique temporary name: concurrent writers (one process per GPU) never share it
+    tmp = '%s.%d.tmp.npz' % (path, os.getpid())
     np.savez(tmp, **arrays)
     os.replace(tmp, path)
 
