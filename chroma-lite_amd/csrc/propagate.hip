@@ -277,8 +277,10 @@ constexpr int WIDE_LDS = 12;
 constexpr int LEAFQ = 16;          // per-lane parked-leaf queue (speculative walk), LDS
 // LDS words per work-item: traversal stack (node + entry distance) [+ leaf queue]
 constexpr int HITS_MODE = 9000;    // shade-only step kernel: the walk's result comes from trace_kernel
+constexpr int GROUP_MODE = 7000;   // group walk of G = WIDE - 7000 lanes per photon (propagate_group_kernel)
 constexpr int lds_words(int wide) {
-    return wide == HITS_MODE ? 1 : (wide >= 2000 ? 2 * WIDE_LDS + LEAFQ : (wide ? 2 * WIDE_LDS : 0));
+    return (wide == HITS_MODE || (wide >= GROUP_MODE && wide < GROUP_MODE + 16)) ? 1
+           : (wide >= 2000 ? 2 * WIDE_LDS + LEAFQ : (wide ? 2 * WIDE_LDS : 0));
 }
 
 // The LDS column pointers are typed (ds_* ops) and the scratch spill array is
@@ -290,6 +292,7 @@ struct WStack {
     CHR_LDS float *dist;
     uint2 *spill;             // entries >= WIDE_LDS (scratch)
     CHR_LDS uint32_t *leafq;  // parked leaves (speculative walk): entry i at leafq[i * BLOCK]
+    CHR_LDS uint32_t *group;  // group walk: the group's shared stack, entry i = (node, entry distance) at [2i, 2i+1]
 };
 // SL: stack entries kept in LDS (the rest spill to scratch)
 template <int SL = WIDE_LDS>
@@ -725,6 +728,170 @@ __device__ int intersect_wide_spec(const DevGeom &g, V3 o, V3 d, float &min_dist
     return best_id;
 }
 
+// Group walk: G lanes (G | 8) walk ONE ray of the wide BVH together, for
+// launches with few photons where the latency of each dependent step, not
+// throughput, sets the time (the multi-step tail launch of the nsteps policy).
+// Each lane slab-tests 8/G children of the current node; the nearest hit inner
+// child (first of the smallest entry distance, as expand_node) is found by an
+// in-group min over (distance, child) keys; the other hit inner children are
+// pushed in child order onto the group's LDS stack by the lanes that own them;
+// each lane tests the triangles of its own hit leaves and the group keeps the
+// min over (distance, reference rank) -- the nearest-hit rule of every other
+// walk, with the same reference leaf check and a running best that never
+// drops below the final one, so the result is unchanged.  All lanes of a group
+// hold identical walk state and take identical branches.
+constexpr int GROUP_STACK = WIDE_STACK;
+__device__ __forceinline__ uint32_t byte_of(uint32_t lo4, uint32_t hi4, int k) {
+    return ((k < 4 ? lo4 : hi4) >> (8 * (k & 3))) & 0xFFu;
+}
+template <int G>
+__device__ int intersect_group(const DevGeom &g, V3 o, V3 d, float &min_distance, int last_hit,
+                               CHR_LDS uint32_t *stk, uint32_t &overflow) {
+    static_assert(G == 2 || G == 4 || G == 8, "group size divides 8");
+    constexpr int C = 8 / G;                       // children per lane: k = sub + G * c
+    constexpr uint32_t INVALID = 0xFFFFFFFFu;
+    constexpr unsigned long long NONE = ~0ull;
+    const uint32_t lane = __lane_id();
+    const uint32_t sub = lane & (uint32_t)(G - 1), gbase = lane & ~(uint32_t)(G - 1);
+    const V3 noid = v3(-o.x / d.x, -o.y / d.y, -o.z / d.z);
+    const V3 inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    const RaySlab r = make_slab(noid, inv);
+    float best = __builtin_inff();
+    uint32_t best_rank = 0xFFFFFFFFu;
+    int best_id = -1;
+    const uint32_t last = (uint32_t)last_hit;
+    int sp = 0;
+    uint32_t node = 0;
+    while (true) {
+        if (node == INVALID) {                       // pop, culling against the best (mesh.h:94-96)
+            bool found = false;
+            while (sp > 0) {
+                sp--;
+                const uint32_t en = stk[2 * sp], et = stk[2 * sp + 1];
+                if (!(__uint_as_float(et) > best)) { node = en; found = true; break; }
+            }
+            if (!found) break;
+        }
+        const uint4 *np = g.wnodes + (size_t)g.wstride * node;
+        const uint4 h = gld(np), a1 = gld(np + 1), a2 = gld(np + 2), a3 = gld(np + 3), a4 = gld(np + 4),
+                    a5 = gld(np + 5);
+        const V3 org = v3(__uint_as_float(h.x), __uint_as_float(h.y), __uint_as_float(h.z));
+        const float sx = exp_scale(h.w), sy = exp_scale(h.w >> 8), sz = exp_scale(h.w >> 16);
+        const uint32_t nx0 = r.negx ? a2.z : a1.x, nx1 = r.negx ? a2.w : a1.y;
+        const uint32_t fx0 = r.negx ? a1.x : a2.z, fx1 = r.negx ? a1.y : a2.w;
+        const uint32_t ny0 = r.negy ? a3.x : a1.z, ny1 = r.negy ? a3.y : a1.w;
+        const uint32_t fy0 = r.negy ? a1.z : a3.x, fy1 = r.negy ? a1.w : a3.y;
+        const uint32_t nz0 = r.negz ? a3.z : a2.x, nz1 = r.negz ? a3.w : a2.y;
+        const uint32_t fz0 = r.negz ? a2.x : a3.z, fz1 = r.negz ? a2.y : a3.w;
+        float tk[C];
+        bool inner[C], leaf[C];
+        uint32_t kind_k[C];
+        unsigned long long key = NONE;
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+            const int k = (int)sub + G * c;
+            const uint32_t kind = byte_of(a4.z, a4.w, k);
+            const float tnx = __builtin_fmaf(__builtin_fmaf(byte_f(nx0, nx1, k), sx, org.x), r.inx, r.onx);
+            const float tfx = __builtin_fmaf(__builtin_fmaf(byte_f(fx0, fx1, k), sx, org.x), r.inx, r.ofx);
+            const float tny = __builtin_fmaf(__builtin_fmaf(byte_f(ny0, ny1, k), sy, org.y), r.iny, r.ony);
+            const float tfy = __builtin_fmaf(__builtin_fmaf(byte_f(fy0, fy1, k), sy, org.y), r.iny, r.ofy);
+            const float tnz = __builtin_fmaf(__builtin_fmaf(byte_f(nz0, nz1, k), sz, org.z), r.inz, r.onz);
+            const float tfz = __builtin_fmaf(__builtin_fmaf(byte_f(fz0, fz1, k), sz, org.z), r.inz, r.ofz);
+            const float tmin = __builtin_fmaxf(__builtin_fmaxf(__builtin_fmaxf(tnx, tny), tnz), 0.0f);
+            const float tmax = __builtin_fminf(__builtin_fminf(tfx, tfy), tfz);
+            const bool hit = (kind != 0u) & !(tmin > tmax) & !(tmin > best);
+            inner[c] = hit & (kind == WIDE_INNER);
+            leaf[c] = hit & (kind != WIDE_INNER);
+            tk[c] = tmin;
+            kind_k[c] = kind;
+            const unsigned long long cand = ((unsigned long long)__float_as_uint(tmin) << 32) | (uint32_t)k;
+            if (inner[c] && cand < key) key = cand;
+        }
+        uint32_t m_inner = 0;
+#pragma unroll
+        for (int c = 0; c < C; ++c)
+            m_inner |= (uint32_t)((__ballot(inner[c]) >> gbase) & ((1ull << G) - 1ull)) << (G * c);
+#pragma unroll
+        for (int off = 1; off < G; off <<= 1) {
+            const unsigned long long other = __shfl_xor(key, off, G);
+            key = other < key ? other : key;
+        }
+        uint32_t near = INVALID;
+        float near_t = 0.0f;
+        uint32_t m_push = m_inner;
+        if (key != NONE) {
+            const int nk = (int)(key & 7u);
+            near_t = __uint_as_float((uint32_t)(key >> 32));
+            near = a4.x + byte_of(a5.x, a5.y, nk);
+            m_push &= ~(1u << nk);
+        }
+        const int npush = __builtin_popcount(m_push);
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+            const int k = (int)sub + G * c;
+            if ((m_push >> k) & 1u) {
+                const int pos = sp + __builtin_popcount(m_push & ((1u << k) - 1u));
+                if (pos < GROUP_STACK) {
+                    stk[2 * pos] = a4.x + byte_of(a5.x, a5.y, k);
+                    stk[2 * pos + 1] = __float_as_uint(tk[c]);
+                }
+            }
+        }
+        if (sp + npush > GROUP_STACK) {
+            if (sub == 0) overflow += (uint32_t)(sp + npush - GROUP_STACK);
+            sp = GROUP_STACK;
+        } else {
+            sp += npush;
+        }
+        // this lane's hit leaves, each triangle in record order (intersect_wide_spec's test)
+        float lbest = best;
+        uint32_t lrank = best_rank;
+        int lid = -1;
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+            if (!leaf[c]) continue;
+            const int k = (int)sub + G * c;
+            const uint32_t first = a4.y + byte_of(a5.x, a5.y, k);
+            for (uint32_t j = 0; j < kind_k[c]; ++j) {
+                const float4 *rr = g.wtri + 4 * (size_t)(first + j);
+                const float4 r0 = gld(rr), r1 = gld(rr + 1), r2 = gld(rr + 2);
+                const uint32_t id = __float_as_uint(r2.y);
+                float dist;
+                if (id == last ||
+                    !intersect_triangle(o, d, v3(r0.x, r0.y, r0.z), v3(r0.w, r1.x, r1.y), v3(r1.z, r1.w, r2.x), dist))
+                    continue;
+                const uint32_t rank = __float_as_uint(r2.z);
+                if (!(dist < lbest || (dist == lbest && rank < lrank))) continue;
+                const float4 r3 = gld(rr + 3);
+                V3 lo, hi;
+                node_bounds(g, make_uint4(__float_as_uint(r2.w), __float_as_uint(r3.x), __float_as_uint(r3.y), 0u),
+                            lo, hi);
+                float bd;
+                if (!intersect_box(noid, inv, lo, hi, bd) || bd > lbest) continue;   // mesh.h:94-96
+                lbest = dist;
+                lrank = rank;
+                lid = (int)id;
+            }
+        }
+        unsigned long long lkey = lid == -1 ? NONE : (((unsigned long long)__float_as_uint(lbest) << 32) | lrank);
+#pragma unroll
+        for (int off = 1; off < G; off <<= 1) {
+            const unsigned long long ok = __shfl_xor(lkey, off, G);
+            const int oid = __shfl_xor(lid, off, G);
+            if (ok < lkey) { lkey = ok; lid = oid; }
+        }
+        if (lkey != NONE) {
+            best = __uint_as_float((uint32_t)(lkey >> 32));
+            best_rank = (uint32_t)lkey;
+            best_id = lid;
+        }
+        node = (near != INVALID && !(near_t > best)) ? near : INVALID;
+        __builtin_amdgcn_wave_barrier();             // pushes land before the group's next pop
+    }
+    min_distance = best_id == -1 ? -1.0f : best;
+    return best_id;
+}
+
 // ---------------------------------------------------------------- photon.h
 __device__ __forceinline__ int convert(int c) { return (c & 0x80) ? (int)(0xFFFFFF00u | (uint32_t)c) : c; }
 __device__ __forceinline__ float get_theta(V3 a, V3 b) { return chr_acosf(fmax_(-1.0f, fmin_(1.0f, dot(a, b)))); }
@@ -886,6 +1053,8 @@ __device__ __forceinline__ void fill_state(const DevGeom &g, State &s, Photon &p
         const int2 h = *hit;
         mesh_triangle = h.x;
         s.distance = __int_as_float(h.y);
+    } else if constexpr (WIDE >= GROUP_MODE && WIDE < GROUP_MODE + 16) {   // group walk, G = WIDE - GROUP_MODE
+        mesh_triangle = intersect_group<WIDE - GROUP_MODE>(g, p.pos, p.dir, s.distance, p.last_hit, wst.group, overflow);
     } else if constexpr (WIDE == 1)
         mesh_triangle = intersect_wide<COUNT>(g, p.pos, p.dir, s.distance, p.last_hit, wst, overflow, cnt);
     else if constexpr (WIDE >= 3000)   // speculative walk + branch-light node expansion
@@ -1527,6 +1696,42 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_step_kernel(const DevGe
     }
     if (have_rng) store_rng(a, slot, rng);
     flush_counters<COUNT>(a, overflow, cnt);
+}
+
+// Multi-step launches (the tail of the nsteps policy, photon.py:261-264): a
+// group of G work-items per RNG slot runs the slot's photons through
+// run_photon with the group walk; the group's lanes hold identical photon and
+// RNG state and compute identical results (every lane stores the same words),
+// so each photon computes exactly what the one-lane kernels compute.  Alive
+// bits are OR-ed per queue position into zeroed mask words.
+template <int G, int MINW>
+__global__ __launch_bounds__(BLOCK, MINW) void propagate_group_kernel(const DevGeom *__restrict__ gdev, PropagateArgs a,
+                                                                      uint32_t cap) {
+    __shared__ uint32_t group_stacks[(BLOCK / G) * GROUP_STACK * 2];
+    const uint32_t tid = blockIdx.x * BLOCK + threadIdx.x;
+    const uint32_t slot = tid / G, sub = tid & (uint32_t)(G - 1);
+    const uint32_t n = (uint32_t)a.nthreads;
+    if (slot >= cap || slot >= n) return;          // whole groups
+    Stack st;
+    st.lds = nullptr;
+    WStack wst;
+    wst.node = nullptr; wst.dist = nullptr; wst.spill = nullptr; wst.leafq = nullptr;
+    wst.group = (CHR_LDS uint32_t *)group_stacks + (threadIdx.x / G) * GROUP_STACK * 2;
+    uint32_t overflow = 0;
+    WalkCounts cnt{0u, 0u, 0u, 0u, 0u, 0ull, 0ull};
+    const DevGeom &g = *gdev;
+    chr_xorwow rng;
+    bool have_rng = false;
+    for (uint32_t q = slot; q < n; q += cap) {
+        const uint32_t photon_id = a.input_queue[q];
+        const uint32_t history = a.flags[photon_id] & 0xFFFFu;   // photon.h:29
+        if (history & DEAD_MASK) continue;
+        if (!have_rng) { load_rng(a, slot, rng); have_rng = true; }
+        const bool alive = run_photon<8, GROUP_MODE + G, false>(g, a, photon_id, q, history, rng, st, wst, overflow, cnt);
+        if (alive && sub == 0) atomicOr(a.alive_masks + (q >> 6), 1ull << (q & 63u));
+    }
+    if (have_rng && sub == 0) store_rng(a, slot, rng);
+    if (sub == 0 && overflow) atomicAdd(a.counters, overflow);
 }
 
 // ---------------------------------------------------------------- ray binning (trace order)
@@ -2204,6 +2409,9 @@ struct StepVariant {
     trace_fn trace;           // one-step launches: trace_kernel + shade kernel (nullptr: fused)
     propagate_step_fn shade;
     int trace_waves;          // waves per SIMD of the trace kernel (persistent grid size)
+    propagate_step_fn tail = nullptr;   // multi-step launches: group-walk kernel (nullptr: fn)
+    int tail_group = 0;                 // its lanes per photon
+    uint32_t group_step_max = 0;        // one-step launches of fewer photons also use the group walk
     int binned;               // trace rays in direction-binned order: 1 atomic counting sort, 2 radix sort,
                               // 3 radix sort on the first host step of a propagate only (n >= kBinFirstMin)
 };
@@ -2218,13 +2426,13 @@ static StepVariant select_step_variant(const chr_geometry *g) {
     if (g->dev.nwnodes == 0) v = kExactVariant;
     const bool queue_ok = g->dev.nwtri < (1u << 30);   // leaf-queue entries hold 30-bit record indices
     if (!queue_ok && (v == 0 || v == 5 || v >= 12)) v = (v == 5) ? 11 : 10;
-    // 0 (default) = 64, 5 (counting form of the default) = 65; 66 / 67: the fused
-    // step kernel alone (previous default) and its counting form
-    if (v == 0) v = 64;
+    // 0 (default) = 70, 5 (counting form of the default) = 65; 66 / 67: the fused
+    // step kernel alone (an earlier default) and its counting form
+    if (v == 0) v = 70;
     else if (v == 5) v = 65;
     else if (v == 66) v = 0;
     else if (v == 67) v = 5;
-    StepVariant sv{select_step_fn(v), nullptr, nullptr, 0, 0};
+    StepVariant sv{select_step_fn(v), nullptr, nullptr, 0, nullptr, 0, 0, 0};
     propagate_step_fn shade = propagate_step_kernel<8, 4, HITS_MODE>;
     switch (v) {   // wavefront split: trace_kernel<COUNT, F, SL, MINW, R>
         case 50: sv.trace = trace_kernel<false, 6, 12, 4, 16>; sv.trace_waves = 4; break;
@@ -2250,6 +2458,21 @@ static StepVariant select_step_variant(const chr_geometry *g) {
                  shade = propagate_step_kernel<8, 2, HITS_MODE>; break;
         case 65: sv.trace = trace_kernel<true, 6, 12, 4, 32>; sv.trace_waves = 4; sv.binned = 3;
                  shade = propagate_step_kernel<8, 2, HITS_MODE>; sv.fn = select_step_fn(5); break;
+        case 70: sv.trace = trace_kernel<false, 6, 12, 4, 32>; sv.trace_waves = 4; sv.binned = 3;
+                 shade = propagate_step_kernel<8, 2, HITS_MODE>;
+                 sv.tail = propagate_group_kernel<8, 4>; sv.tail_group = 8; break;
+        case 71: sv.trace = trace_kernel<false, 6, 12, 4, 32>; sv.trace_waves = 4; sv.binned = 3;
+                 shade = propagate_step_kernel<8, 2, HITS_MODE>;
+                 sv.tail = propagate_group_kernel<4, 2>; sv.tail_group = 4; break;
+        case 72: sv.tail = propagate_group_kernel<8, 4>; sv.tail_group = 8; break;   // fused steps + group tail
+        case 74: case 75: case 76:
+                 sv.trace = trace_kernel<false, 6, 12, 4, 32>; sv.trace_waves = 4; sv.binned = 3;
+                 shade = propagate_step_kernel<8, 2, HITS_MODE>;
+                 sv.tail = propagate_group_kernel<8, 4>; sv.tail_group = 8;
+                 sv.group_step_max = v == 74 ? 65536u : (v == 75 ? 131072u : 262144u); break;
+        case 73: sv.trace = trace_kernel<false, 6, 12, 4, 32>; sv.trace_waves = 4; sv.binned = 3;
+                 shade = propagate_step_kernel<8, 2, HITS_MODE>;
+                 sv.tail = propagate_group_kernel<8, 2>; sv.tail_group = 8; break;
         default: break;
     }
     if (sv.trace) sv.shade = shade;
@@ -2359,7 +2582,8 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
     a.hits = nullptr;
     const uint32_t threads = std::min(cap, (n + 63u) & ~63u);
     const StepVariant sv = select_step_variant(g);
-    const bool split = sv.trace && hits && max_steps == 1;
+    const bool small = sv.tail && max_steps == 1 && n < sv.group_step_max;
+    const bool split = sv.trace && hits && max_steps == 1 && !small;
     if (split) {
         uint32_t *next = (uint32_t *)(hits + n);
         CHR_HIP_CHECK(hipMemsetAsync(next, 0, 4, stream));
@@ -2403,8 +2627,15 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
         CHR_HIP_CHECK(hipEventRecord(ev0, stream));
     }
     if (split_out) *split_out = split;
-    hipLaunchKernelGGL(split ? sv.shade : sv.fn, dim3(grid_for(threads)), dim3(BLOCK), 0, stream,
-                       (const DevGeom *)g->d_dev, a, cap);
+    if (!split && sv.tail && (max_steps > 1 || small)) {   // group walk, alive bits OR-ed
+        CHR_HIP_CHECK(hipMemsetAsync(masks, 0, (size_t)nwords * 8, stream));
+        if (ev0) CHR_HIP_CHECK(hipEventRecord(ev0, stream));
+        hipLaunchKernelGGL(sv.tail, dim3(grid_for((uint64_t)threads * sv.tail_group)), dim3(BLOCK), 0, stream,
+                           (const DevGeom *)g->d_dev, a, cap);
+    } else {
+        hipLaunchKernelGGL(split ? sv.shade : sv.fn, dim3(grid_for(threads)), dim3(BLOCK), 0, stream,
+                           (const DevGeom *)g->d_dev, a, cap);
+    }
     if (ev1) CHR_HIP_CHECK(hipEventRecord(ev1, stream));
     launch_mask_scan(masks, nwords, offsets, bsums, out_queue, counters + 1, nullptr, stream);
     hipLaunchKernelGGL(scatter_queue_kernel, dim3(grid_for(n)), dim3(BLOCK), 0, stream, masks, offsets, bsums,
