@@ -1698,6 +1698,89 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_step_kernel(const DevGe
     flush_counters<COUNT>(a, overflow, cnt);
 }
 
+// Shade pass of a split one-step launch (max_steps == 1): the loop body of
+// propagate.cu:286-341 run once per queued photon with the walk result of
+// trace_kernel, the photon write-back of 343-353 and the alive mask word per
+// 64 queue positions.  A slot's photons (queue positions slot, slot + cap, ...)
+// share only the RNG state, so the next photon's queue entry, state and walk
+// result are loaded while the current one's physics runs.
+struct QueuedPhoton {
+    uint32_t pid, history;
+    V3 pos, dir, pol;
+    float wavelength, time, weight;
+    int last_hit;
+    int2 hit;
+};
+__device__ __forceinline__ void fetch_queued(const PropagateArgs &a, uint32_t q, QueuedPhoton &f) {
+    f.pid = a.input_queue[q];
+    f.history = a.flags[f.pid] & 0xFFFFu;   // photon.h:29
+    f.pos = load3(a.pos, f.pid);
+    f.dir = load3(a.dir, f.pid);
+    f.pol = load3(a.pol, f.pid);
+    f.wavelength = a.wl[f.pid];
+    f.time = a.t[f.pid];
+    f.weight = a.weights[f.pid];
+    f.last_hit = a.last_hit[f.pid];
+    f.hit = a.hits[q];
+}
+template <int MINW>
+__global__ __launch_bounds__(BLOCK, MINW) void shade_kernel(const DevGeom *__restrict__ gdev, PropagateArgs a,
+                                                            uint32_t cap) {
+    const uint32_t slot = blockIdx.x * BLOCK + threadIdx.x;
+    const uint32_t n = (uint32_t)a.nthreads;
+    if (slot >= cap || (slot & ~63u) >= n) return;   // whole waves (cap % 64 == 0)
+    const DevGeom &g = *gdev;
+    chr_xorwow rng;
+    bool have_rng = false;
+    QueuedPhoton nx;
+    if (slot < n) fetch_queued(a, slot, nx);
+    uint32_t pos = slot;
+    for (uint32_t qb = slot & ~63u; qb < n; qb += cap, pos += cap) {   // wave-uniform trip count
+        const QueuedPhoton cur = nx;
+        if (pos + cap < n) fetch_queued(a, pos + cap, nx);
+        bool alive = false;
+        if (pos < n && !(cur.history & DEAD_MASK)) {
+            if (!have_rng) { load_rng(a, slot, rng); have_rng = true; }
+            Photon p;
+            p.history = cur.history;
+            p.pos = cur.pos;
+            p.dir = cur.dir / norm(cur.dir);
+            p.pol = cur.pol / norm(cur.pol);
+            p.wavelength = cur.wavelength;
+            p.time = cur.time;
+            p.last_hit = cur.last_hit;
+            p.weight = cur.weight;
+            const float prod = ((((p.dir.x * p.dir.y) * p.dir.z) * p.pos.x) * p.pos.y) * p.pos.z;
+            if (chr_isnan(prod)) {
+                p.history |= CHR_NO_HIT | CHR_NAN_ABORT;
+            } else {
+                State s;
+                s.distance = __int_as_float(cur.hit.y);
+                finish_fill(g, s, p, cur.hit.x);
+                if (p.last_hit != -1) {
+                    int command = propagate_to_boundary(g, p, s, rng, a.use_weights, a.scatter_first);
+                    if (command == PASS && s.surface_index != -1)
+                        command = propagate_at_surface(g, p, s, rng, a.use_weights);
+                    if (command == PASS) propagate_at_boundary(p, s, rng);
+                }
+            }
+            const uint32_t pid = cur.pid;
+            store3(a.pos, pid, p.pos);
+            store3(a.dir, pid, p.dir);
+            store3(a.pol, pid, p.pol);
+            a.wl[pid] = p.wavelength;
+            a.t[pid] = p.time;
+            a.flags[pid] = p.history;
+            a.last_hit[pid] = p.last_hit;
+            a.weights[pid] = p.weight;
+            alive = (p.history & DEAD_MASK) == 0;
+        }
+        const unsigned long long mask = __ballot(alive);
+        if ((slot & 63u) == 0) a.alive_masks[qb >> 6] = mask;
+    }
+    if (have_rng) store_rng(a, slot, rng);
+}
+
 // Multi-step launches (the tail of the nsteps policy, photon.py:261-264): a
 // group of G work-items per RNG slot runs the slot's photons through
 // run_photon with the group walk; the group's lanes hold identical photon and
@@ -2426,9 +2509,9 @@ static StepVariant select_step_variant(const chr_geometry *g) {
     if (g->dev.nwnodes == 0) v = kExactVariant;
     const bool queue_ok = g->dev.nwtri < (1u << 30);   // leaf-queue entries hold 30-bit record indices
     if (!queue_ok && (v == 0 || v == 5 || v >= 12)) v = (v == 5) ? 11 : 10;
-    // 0 (default) = 70, 5 (counting form of the default) = 65; 66 / 67: the fused
-    // step kernel alone (an earlier default) and its counting form
-    if (v == 0) v = 70;
+    // 0 (default) = 84, 5 (counting form of the default walk) = 65; 66 / 67: the
+    // fused step kernel alone (an earlier default) and its counting form
+    if (v == 0) v = 84;
     else if (v == 5) v = 65;
     else if (v == 66) v = 0;
     else if (v == 67) v = 5;
@@ -2470,6 +2553,10 @@ static StepVariant select_step_variant(const chr_geometry *g) {
                  shade = propagate_step_kernel<8, 2, HITS_MODE>;
                  sv.tail = propagate_group_kernel<8, 4>; sv.tail_group = 8;
                  sv.group_step_max = v == 74 ? 65536u : (v == 75 ? 131072u : 262144u); break;
+        case 83: case 84: case 85:
+                 sv.trace = trace_kernel<false, 6, 12, 4, 32>; sv.trace_waves = 4; sv.binned = 3;
+                 shade = v == 83 ? shade_kernel<2> : (v == 84 ? shade_kernel<3> : shade_kernel<4>);
+                 sv.tail = propagate_group_kernel<8, 4>; sv.tail_group = 8; break;
         case 73: sv.trace = trace_kernel<false, 6, 12, 4, 32>; sv.trace_waves = 4; sv.binned = 3;
                  shade = propagate_step_kernel<8, 2, HITS_MODE>;
                  sv.tail = propagate_group_kernel<8, 2>; sv.tail_group = 8; break;
