@@ -38,7 +38,13 @@
 namespace chr {
 namespace {
 
-constexpr int LEAF_MAX = 4;
+constexpr int LEAF_MAX = 4;     // largest leaf (kind byte 1..4, 2-bit count in the walk's leaf queue)
+// CHR_WIDE_LEAF_MAX=1..4 (build-time A/B of the leaf size; default LEAF_MAX)
+inline uint32_t leaf_max_env() {
+    const char *e = std::getenv("CHR_WIDE_LEAF_MAX");
+    const int v = e ? std::atoi(e) : LEAF_MAX;
+    return (uint32_t)std::min(LEAF_MAX, std::max(1, v));
+}
 constexpr int NBINS = 32;
 
 struct Box {
@@ -65,6 +71,7 @@ struct Cluster {
 
 struct Builder {
     bool fill_leaves;
+    uint32_t leaf_max;
     const std::vector<Box> &tri_box;
     const std::vector<float> &centroid;   // 3 per triangle
     std::vector<uint32_t> &idx;
@@ -177,7 +184,7 @@ struct Builder {
             int pick = -1;
             double best = -1.0;
             for (int i = 0; i < n; ++i)
-                if (out[i].count() > LEAF_MAX && out[i].box.area() > best) { best = out[i].box.area(); pick = i; }
+                if (out[i].count() > leaf_max && out[i].box.area() > best) { best = out[i].box.area(); pick = i; }
             if (pick < 0 && fill_leaves)
                 for (int i = 0; i < n; ++i)
                     if (out[i].count() > 1 && out[i].box.area() > best) { best = out[i].box.area(); pick = i; }
@@ -286,7 +293,7 @@ int build_wide_bvh(const chr_geometry_desc *d, WideBVH &out) {
     for (int64_t t = 0; t < (int64_t)ntri; ++t)
         for (int a = 0; a < 3; ++a) centroid[3 * t + a] = 0.5f * (tri_box[t].lo[a] + tri_box[t].hi[a]);
 
-    Builder B{!std::getenv("CHR_WIDE_NO_FILL"), tri_box, centroid, idx};
+    Builder B{!std::getenv("CHR_WIDE_NO_FILL"), leaf_max_env(), tri_box, centroid, idx};
     out.nodes.clear();
     out.tri.clear();
     out.nodes.resize(1);
@@ -317,7 +324,7 @@ int build_wide_bvh(const chr_geometry_desc *d, WideBVH &out) {
             uint32_t ninner = 0;
             for (int k = 0; k < ncl[i]; ++k) {
                 const Cluster &c = cl[8 * i + k];
-                if (c.count() > (uint32_t)LEAF_MAX) {
+                if (c.count() > B.leaf_max) {
                     next.push_back(Task{c.begin, c.end, child_base[i] + ninner});
                     ninner++;
                 } else {
@@ -349,7 +356,7 @@ int build_wide_bvh(const chr_geometry_desc *d, WideBVH &out) {
             uint32_t ninner = 0, toff = 0;
             for (int k = 0; k < n; ++k) {
                 const Cluster &c = cl[8 * i + k];
-                if (c.count() > (uint32_t)LEAF_MAX) {
+                if (c.count() > B.leaf_max) {
                     W.kind[k] = WIDE_INNER;
                     W.off[k] = (uint8_t)ninner++;
                 } else {
