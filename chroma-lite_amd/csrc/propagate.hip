@@ -276,10 +276,9 @@ __device__ __forceinline__ int intersect_mesh(const DevGeom &g, V3 o, V3 d, floa
 constexpr int WIDE_LDS = 12;
 constexpr int LEAFQ = 16;          // per-lane parked-leaf queue (speculative walk), LDS
 // LDS words per work-item: traversal stack (node + entry distance) [+ leaf queue]
-constexpr int HITS_MODE = 9000;    // shade-only step kernel: the walk's result comes from trace_kernel
 constexpr int GROUP_MODE = 7000;   // group walk of G = WIDE - 7000 lanes per photon (propagate_group_kernel)
 constexpr int lds_words(int wide) {
-    return (wide == HITS_MODE || (wide >= GROUP_MODE && wide < GROUP_MODE + 16)) ? 1
+    return (wide >= GROUP_MODE && wide < GROUP_MODE + 16) ? 1
            : (wide >= 2000 ? 2 * WIDE_LDS + LEAFQ : (wide ? 2 * WIDE_LDS : 0));
 }
 
@@ -383,68 +382,6 @@ __device__ __forceinline__ uint32_t expand_node(const uint4 h, const uint4 a1, c
     return leaf_mask;
 }
 
-// Branch-light form of expand_node for a lane whose LDS stack has room for a
-// whole node (sp + 7 <= WIDE_LDS): all eight slab tests first (no control
-// flow), the nearest hit inner child chosen with selects (first of the
-// smallest entry distance, as expand_node), then the other hit inner children
-// pushed in child order with predicated LDS stores.  The pushed set and the
-// near child are expand_node's; only the push order can differ (which changes
-// the walk's order, not what it finds: the nearest hit is argmin(distance,
-// reference rank) over a superset of the reference's tested triangles).
-__device__ __forceinline__ uint32_t expand_node_fast(const uint4 h, const uint4 a1, const uint4 a2, const uint4 a3,
-                                                     const uint4 a4, const uint4 a5, const RaySlab &r, float best,
-                                                     uint32_t &near_node, float &near_t, WStack &st, int &sp) {
-    const V3 org = v3(__uint_as_float(h.x), __uint_as_float(h.y), __uint_as_float(h.z));
-    const float sx = exp_scale(h.w), sy = exp_scale(h.w >> 8), sz = exp_scale(h.w >> 16);
-    const uint32_t nx0 = r.negx ? a2.z : a1.x, nx1 = r.negx ? a2.w : a1.y;
-    const uint32_t fx0 = r.negx ? a1.x : a2.z, fx1 = r.negx ? a1.y : a2.w;
-    const uint32_t ny0 = r.negy ? a3.x : a1.z, ny1 = r.negy ? a3.y : a1.w;
-    const uint32_t fy0 = r.negy ? a1.z : a3.x, fy1 = r.negy ? a1.w : a3.y;
-    const uint32_t nz0 = r.negz ? a3.z : a2.x, nz1 = r.negz ? a3.w : a2.y;
-    const uint32_t fz0 = r.negz ? a2.x : a3.z, fz1 = r.negz ? a2.y : a3.w;
-    uint32_t leaf_mask = 0, inner_mask = 0;
-    float tk[8];
-    float nt = __builtin_inff();
-    int nk = -1;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        const uint32_t kind = ((k < 4 ? a4.z : a4.w) >> (8 * (k & 3))) & 0xFFu;
-        const float tnx = __builtin_fmaf(__builtin_fmaf(byte_f(nx0, nx1, k), sx, org.x), r.inx, r.onx);
-        const float tfx = __builtin_fmaf(__builtin_fmaf(byte_f(fx0, fx1, k), sx, org.x), r.inx, r.ofx);
-        const float tny = __builtin_fmaf(__builtin_fmaf(byte_f(ny0, ny1, k), sy, org.y), r.iny, r.ony);
-        const float tfy = __builtin_fmaf(__builtin_fmaf(byte_f(fy0, fy1, k), sy, org.y), r.iny, r.ofy);
-        const float tnz = __builtin_fmaf(__builtin_fmaf(byte_f(nz0, nz1, k), sz, org.z), r.inz, r.onz);
-        const float tfz = __builtin_fmaf(__builtin_fmaf(byte_f(fz0, fz1, k), sz, org.z), r.inz, r.ofz);
-        const float tmin = __builtin_fmaxf(__builtin_fmaxf(__builtin_fmaxf(tnx, tny), tnz), 0.0f);
-        const float tmax = __builtin_fminf(__builtin_fminf(tfx, tfy), tfz);
-        const bool hit = (kind != 0u) & !(tmin > tmax) & !(tmin > best);
-        const bool inner = hit & (kind == WIDE_INNER);
-        leaf_mask |= (hit & !inner) ? (1u << k) : 0u;
-        inner_mask |= inner ? (1u << k) : 0u;
-        tk[k] = tmin;
-        const bool take = inner & ((nk < 0) | (tmin < nt));
-        nt = take ? tmin : nt;
-        nk = take ? k : nk;
-    }
-    near_node = 0xFFFFFFFFu;
-    near_t = 0.0f;
-    if (nk >= 0) {
-        near_t = nt;
-        near_node = a4.x + ((((nk < 4 ? a5.x : a5.y) >> (8 * (nk & 3))) & 0xFFu));
-        inner_mask &= ~(1u << nk);
-    }
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        if ((inner_mask >> k) & 1u) {
-            const uint32_t child = a4.x + (((k < 4 ? a5.x : a5.y) >> (8 * (k & 3))) & 0xFFu);
-            st.node[sp * BLOCK] = child;
-            st.dist[sp * BLOCK] = tk[k];
-            sp++;
-        }
-    }
-    return leaf_mask;
-}
-
 struct WalkCounts {   // filled only by the counting variant (bench: algorithmic bytes per photon)
     uint32_t nodes, tris, walks;
     uint32_t wave_nodes, wave_tris;   // steps the whole wave executed (counted by its first active lane)
@@ -454,74 +391,6 @@ __device__ __forceinline__ bool wave_leader() {
     const unsigned long long m = __ballot(1);
     return (unsigned)__lane_id() == (unsigned)(__ffsll((long long)m) - 1);
 }
-
-template <bool COUNT>
-__device__ int intersect_wide(const DevGeom &g, V3 o, V3 d, float &min_distance, int last_hit, WStack &st,
-                              uint32_t &overflow, WalkCounts &cnt) {
-    if constexpr (COUNT) cnt.walks++;
-    const V3 noid = v3(-o.x / d.x, -o.y / d.y, -o.z / d.z);
-    const V3 inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
-    const RaySlab slab = make_slab(noid, inv);
-    float best = __builtin_inff();
-    uint32_t best_rank = 0xFFFFFFFFu;
-    int best_id = -1;
-    const uint32_t last = (uint32_t)last_hit;
-    int sp = 0;
-    uint32_t node = 0;
-    while (true) {
-        if constexpr (COUNT) { cnt.nodes++; if (wave_leader()) cnt.wave_nodes++; }
-        const uint4 *np = g.wnodes + (size_t)g.wstride * node;
-        const uint4 h = gld(np), a1 = gld(np + 1), a2 = gld(np + 2), a3 = gld(np + 3), a4 = gld(np + 4),
-                    a5 = gld(np + 5);
-        uint32_t near_node;
-        float near_t;
-        uint32_t leaf_mask = expand_node(h, a1, a2, a3, a4, a5, slab, best, near_node, near_t, st, sp, overflow);
-        const unsigned long long kinds = ((unsigned long long)a4.w << 32) | a4.z;
-        const unsigned long long offs = ((unsigned long long)a5.y << 32) | a5.x;
-        while (leaf_mask) {
-            const int k = __builtin_ctz(leaf_mask);
-            leaf_mask &= leaf_mask - 1;
-            const uint32_t ntri = (uint32_t)(kinds >> (8 * k)) & 0xFFu;
-            const uint32_t first = a4.y + ((uint32_t)(offs >> (8 * k)) & 0xFFu);
-            for (uint32_t j = 0; j < ntri; ++j) {
-                if constexpr (COUNT) { cnt.tris++; if (wave_leader()) cnt.wave_tris++; }
-                const float4 *r = g.wtri + 4 * (size_t)(first + j);
-                const float4 r0 = gld(r), r1 = gld(r + 1), r2 = gld(r + 2), r3 = gld(r + 3);
-                const uint32_t id = __float_as_uint(r2.y);
-                if (id == last) continue;
-                V3 lo, hi;
-                node_bounds(g, make_uint4(__float_as_uint(r2.w), __float_as_uint(r3.x), __float_as_uint(r3.y), 0u), lo, hi);
-                float bd;
-                if (!intersect_box(noid, inv, lo, hi, bd) || bd > best) continue;   // mesh.h:94-96
-                float dist;
-                if (!intersect_triangle(o, d, v3(r0.x, r0.y, r0.z), v3(r0.w, r1.x, r1.y), v3(r1.z, r1.w, r2.x), dist))
-                    continue;
-                const uint32_t rank = __float_as_uint(r2.z);
-                if (dist < best || (dist == best && rank < best_rank)) {
-                    best = dist;
-                    best_rank = rank;
-                    best_id = (int)id;
-                }
-            }
-        }
-        if (near_node != 0xFFFFFFFFu && !(near_t > best)) {
-            node = near_node;
-            continue;
-        }
-        // pop, culling entries whose box starts beyond the best hit
-        bool found = false;
-        while (sp > 0) {
-            sp--;
-            float t;
-            wpop(st, sp, node, t);
-            if (!(t > best)) { found = true; break; }
-        }
-        if (!found) break;
-    }
-    min_distance = best_id == -1 ? -1.0f : best;
-    return best_id;
-}
-
 
 // The same query, scheduled for 64-wide SIMT (default).  Leaf triangles are
 // not tested inside the node step of the lane that reached them: a lane that
@@ -637,7 +506,7 @@ __device__ int intersect_wide_sched(const DevGeom &g, V3 o, V3 d, float &min_dis
 // (a superset: culling uses a best that never drops below the final one), so
 // the nearest hit is unchanged.
 // Leaf queue entry: first triangle record (bits 0-29) | (count-1) << 30.
-template <bool COUNT, int F, bool FASTX>
+template <bool COUNT, int F>
 __device__ int intersect_wide_spec(const DevGeom &g, V3 o, V3 d, float &min_distance, int last_hit, WStack &st,
                                    uint32_t &overflow, WalkCounts &cnt) {
     if constexpr (COUNT) cnt.walks++;
@@ -679,11 +548,7 @@ __device__ int intersect_wide_spec(const DevGeom &g, V3 o, V3 d, float &min_dist
                         a5 = gld(np + 5);
             uint32_t near_node;
             float near_t;
-            uint32_t leaf_mask;
-            if (FASTX && sp + 7 <= WIDE_LDS)
-                leaf_mask = expand_node_fast(h, a1, a2, a3, a4, a5, slab, best, near_node, near_t, st, sp);
-            else
-                leaf_mask = expand_node(h, a1, a2, a3, a4, a5, slab, best, near_node, near_t, st, sp, overflow);
+            uint32_t leaf_mask = expand_node(h, a1, a2, a3, a4, a5, slab, best, near_node, near_t, st, sp, overflow);
             node = near_node;
             while (leaf_mask) {
                 const int k = __builtin_ctz(leaf_mask);
@@ -1047,22 +912,13 @@ __device__ __forceinline__ void finish_fill(const DevGeom &g, State &s, Photon &
 // photon.h:87-397
 template <int BATCH, int WIDE, bool COUNT>
 __device__ __forceinline__ void fill_state(const DevGeom &g, State &s, Photon &p, Stack st, WStack &wst,
-                                           uint32_t &overflow, WalkCounts &cnt, const int2 *hit) {
+                                           uint32_t &overflow, WalkCounts &cnt) {
     int mesh_triangle;
-    if constexpr (WIDE == HITS_MODE) {   // walked by trace_kernel: (triangle, distance)
-        const int2 h = *hit;
-        mesh_triangle = h.x;
-        s.distance = __int_as_float(h.y);
-    } else if constexpr (WIDE >= GROUP_MODE && WIDE < GROUP_MODE + 16) {   // group walk, G = WIDE - GROUP_MODE
+    if constexpr (WIDE >= GROUP_MODE && WIDE < GROUP_MODE + 16) {   // group walk, G = WIDE - GROUP_MODE
         mesh_triangle = intersect_group<WIDE - GROUP_MODE>(g, p.pos, p.dir, s.distance, p.last_hit, wst.group, overflow);
-    } else if constexpr (WIDE == 1)
-        mesh_triangle = intersect_wide<COUNT>(g, p.pos, p.dir, s.distance, p.last_hit, wst, overflow, cnt);
-    else if constexpr (WIDE >= 3000)   // speculative walk + branch-light node expansion
+    } else if constexpr (WIDE >= 2000)   // speculative walk, triangle-step threshold (WIDE - 2000)/8 of live lanes
         mesh_triangle =
-            intersect_wide_spec<COUNT, WIDE - 3000, true>(g, p.pos, p.dir, s.distance, p.last_hit, wst, overflow, cnt);
-    else if constexpr (WIDE >= 2000)   // speculative walk, triangle-step threshold (WIDE - 2000)/8 of live lanes
-        mesh_triangle =
-            intersect_wide_spec<COUNT, WIDE - 2000, false>(g, p.pos, p.dir, s.distance, p.last_hit, wst, overflow, cnt);
+            intersect_wide_spec<COUNT, WIDE - 2000>(g, p.pos, p.dir, s.distance, p.last_hit, wst, overflow, cnt);
     else if constexpr (WIDE >= 1000)   // scheduled walk, triangle batch threshold WIDE - 1000
         mesh_triangle =
             intersect_wide_sched<COUNT, WIDE - 1000>(g, p.pos, p.dir, s.distance, p.last_hit, wst, overflow, cnt);
@@ -1507,7 +1363,7 @@ struct PropagateArgs {
     unsigned long long *alive_masks;   // one word per 64 slots
     uint32_t *counters;                // [0]: stack overflows
     const uint32_t *order;             // coherence order: work-item t runs slot order[t] (nullptr: t)
-    const int2 *hits;                  // HITS_MODE: walk result per queue position (trace_kernel)
+    const int2 *hits;                  // shade_kernel: walk result per queue position (trace_kernel)
 };
 
 __device__ __forceinline__ V3 load3(const float *p, uint32_t i) { return v3(p[3 * i], p[3 * i + 1], p[3 * i + 2]); }
@@ -1518,7 +1374,7 @@ __device__ __forceinline__ void store3(float *p, uint32_t i, V3 v) { p[3 * i] = 
 // its write-back (propagate.cu:343-353).  Returns whether it is still alive.
 template <int BATCH, int WIDE, bool COUNT>
 __device__ __forceinline__ bool run_photon(const DevGeom &g, const PropagateArgs &a, uint32_t photon_id,
-                                           uint32_t qpos, uint32_t history, chr_xorwow &rng, Stack st, WStack &wst,
+                                           uint32_t history, chr_xorwow &rng, Stack st, WStack &wst,
                                            uint32_t &overflow, WalkCounts &cnt) {
     Photon p;
     p.history = history;
@@ -1542,7 +1398,7 @@ __device__ __forceinline__ bool run_photon(const DevGeom &g, const PropagateArgs
         if (chr_isnan(prod)) { p.history |= CHR_NO_HIT | CHR_NAN_ABORT; break; }
         unsigned long long t0 = 0;
         if constexpr (COUNT) t0 = __builtin_amdgcn_s_memtime();
-        fill_state<BATCH, WIDE, COUNT>(g, s, p, st, wst, overflow, cnt, a.hits + qpos);
+        fill_state<BATCH, WIDE, COUNT>(g, s, p, st, wst, overflow, cnt);
         if constexpr (COUNT) {
             const unsigned long long t1 = __builtin_amdgcn_s_memtime();
             if (wave_leader()) cnt.wave_fill_cycles += t1 - t0;
@@ -1633,8 +1489,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_kernel(const DevGeom *_
             uint32_t overflow = 0;
             WalkCounts cnt{0u, 0u, 0u, 0u, 0u, 0ull, 0ull};
             const DevGeom &g = *gdev;   // device-resident: uniform s_loads, no private copy
-            alive = run_photon<BATCH, WIDE, COUNT>(g, a, photon_id, a.first + id, history, rng, st, wst, overflow,
-                                                   cnt);
+            alive = run_photon<BATCH, WIDE, COUNT>(g, a, photon_id, history, rng, st, wst, overflow, cnt);
             store_rng(a, (uint32_t)id, rng);
             flush_counters<COUNT>(a, overflow, cnt);
         }
@@ -1688,7 +1543,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_step_kernel(const DevGe
             const uint32_t history = a.flags[photon_id] & 0xFFFFu;   // photon.h:29
             if (!(history & DEAD_MASK)) {
                 if (!have_rng) { load_rng(a, slot, rng); have_rng = true; }
-                alive = run_photon<BATCH, WIDE, COUNT>(g, a, photon_id, pos, history, rng, st, wst, overflow, cnt);
+                alive = run_photon<BATCH, WIDE, COUNT>(g, a, photon_id, history, rng, st, wst, overflow, cnt);
             }
         }
         const unsigned long long mask = __ballot(alive);
@@ -1810,7 +1665,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_group_kernel(const DevG
         const uint32_t history = a.flags[photon_id] & 0xFFFFu;   // photon.h:29
         if (history & DEAD_MASK) continue;
         if (!have_rng) { load_rng(a, slot, rng); have_rng = true; }
-        const bool alive = run_photon<8, GROUP_MODE + G, false>(g, a, photon_id, q, history, rng, st, wst, overflow, cnt);
+        const bool alive = run_photon<8, GROUP_MODE + G, false>(g, a, photon_id, history, rng, st, wst, overflow, cnt);
         if (alive && sub == 0) atomicOr(a.alive_masks + (q >> 6), 1ull << (q & 63u));
     }
     if (have_rng && sub == 0) store_rng(a, slot, rng);
@@ -1820,9 +1675,8 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_group_kernel(const DevG
 // ---------------------------------------------------------------- ray binning (trace order)
 // The order in which trace_kernel walks the queued rays does not change any
 // result (each walk's result is stored at its queue position), so rays are
-// binned by direction cell (counting sort, 65,536 octahedral cells) to make the
+// binned by direction cell (16-bit radix sort, 65,536 octahedral cells) to make the
 // 64 rays of a wave walk the same subtrees: better L1/L2 reuse of nodes.
-constexpr uint32_t NBINS = 65536;
 __device__ __forceinline__ uint32_t octa_cell(V3 d) {   // octahedral map of a unit vector, 8 bits per axis
     const float s = fabsf(d.x) + fabsf(d.y) + fabsf(d.z);
     float u = d.x / s, v = d.y / s;
@@ -1835,17 +1689,6 @@ __device__ __forceinline__ uint32_t octa_cell(V3 d) {   // octahedral map of a u
     const uint32_t iv = (uint32_t)fminf(fmaxf((v + 1.0f) * 128.0f, 0.0f), 255.0f);
     return (iv << 8) | iu;
 }
-__global__ __launch_bounds__(BLOCK) void bin_count_kernel(const float *dir, const uint32_t *queue, uint32_t n,
-                                                          uint32_t *keys, uint32_t *hist) {
-    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
-    if (i >= n) return;
-    const uint32_t pid = queue[i];
-    V3 d = v3(dir[3 * pid], dir[3 * pid + 1], dir[3 * pid + 2]);
-    const float l = sqrtf(d.x * d.x + d.y * d.y + d.z * d.z);
-    const uint32_t key = (l > 0.0f && l < __builtin_inff()) ? octa_cell(v3(d.x / l, d.y / l, d.z / l)) : 0u;
-    keys[i] = key;
-    atomicAdd(hist + key, 1u);
-}
 __global__ __launch_bounds__(BLOCK) void bin_key_kernel(const float *dir, const uint32_t *queue, uint32_t n,
                                                         uint32_t *keys, uint32_t *vals) {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
@@ -1856,42 +1699,14 @@ __global__ __launch_bounds__(BLOCK) void bin_key_kernel(const float *dir, const 
     keys[i] = (l > 0.0f && l < __builtin_inff()) ? octa_cell(v3(d.x / l, d.y / l, d.z / l)) : 0u;
     vals[i] = i;
 }
-// exclusive scan of NBINS counts in place (one workgroup of 1024, 64 bins each)
-__global__ __launch_bounds__(1024) void bin_scan_kernel(uint32_t *hist) {
-    __shared__ uint32_t part[1024];
-    const uint32_t t = threadIdx.x;
-    uint32_t sum = 0;
-    for (uint32_t k = 0; k < NBINS / 1024; ++k) sum += hist[t * (NBINS / 1024) + k];
-    part[t] = sum;
-    __syncthreads();
-    for (uint32_t off = 1; off < 1024; off <<= 1) {
-        const uint32_t v = t >= off ? part[t - off] : 0u;
-        __syncthreads();
-        part[t] += v;
-        __syncthreads();
-    }
-    uint32_t run = part[t] - sum;
-    for (uint32_t k = 0; k < NBINS / 1024; ++k) {
-        const uint32_t c = hist[t * (NBINS / 1024) + k];
-        hist[t * (NBINS / 1024) + k] = run;
-        run += c;
-    }
-}
-__global__ __launch_bounds__(BLOCK) void bin_scatter_kernel(const uint32_t *keys, uint32_t n, uint32_t *cursor,
-                                                            uint32_t *order) {
-    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
-    if (i >= n) return;
-    order[atomicAdd(cursor + keys[i], 1u)] = i;
-}
-
 // ---------------------------------------------------------------- wavefront split
 // A one-step launch (max_steps == 1, every host step above the tail) is split
 // in two kernels:
 //   trace_kernel  -- the BVH walk of fill_state (mesh.h:45-126) for every live
 //                    queued photon, written as (triangle, distance) per queue
 //                    position;
-//   propagate_step_kernel<..., HITS_MODE> -- the rest of the step, unchanged,
-//                    reading that walk result instead of walking.
+//   shade_kernel  -- the rest of the step, unchanged, reading that walk result
+//                    instead of walking.
 // A photon's walk depends only on its position, direction and last hit, which
 // the step does not change before fill_state, so every result is identical.
 // The trace kernel holds only the walk state (no photon physics, no RNG): it
@@ -2450,53 +2265,50 @@ extern "C" uint64_t chr_propagate_scratch_words(uint32_t nthreads) {
     return 16 + mask_scan_words(nthreads) + 4 * (uint64_t)nthreads + 64 + (sort_temp_bytes(nthreads) + 3) / 4;
 }
 
-// Kernel variants (A/B-able at run time with CHR_PROPAGATE_VARIANT=<n>;
-// all produce identical results, they differ only in schedule/occupancy).
+// Kernel variants (CHR_PROPAGATE_VARIANT=<n>, read per launch so one process
+// can A/B them; every variant gives identical results -- tools/ab_variants.py
+// checks histories, last hits and positions).  Measured choices: DESIGN.md
+// section 5 and profiles/r01/ab_*.log.
+//   0  default.  One-step launches: trace_kernel (BVH walk, first step's rays
+//      binned by direction) + shade_kernel<3>; multi-step launches (the tail):
+//      propagate_group_kernel (8 lanes per photon).
+//   5  counting form of 0 (bench: node/triangle counts of the walk); its
+//      multi-step launches run the counting fused kernel.
+//   1  exact-order walk of the reference BVH (fused step kernel).
+//   2  fused step kernel with the speculative wide walk (walk + physics per
+//      lane: the design the split replaced); 3 = its counting form.
+//   4  scheduled wide walk (fused); used automatically when the triangle
+//      records do not fit the 30-bit leaf queue; 6 = its counting form.
+//   7  the split with binning on every step; 8 the split without binning.
 typedef void (*propagate_fn)(const DevGeom *, PropagateArgs);
-// measured on demo.detector(), 4M photons (profiles/r01/ab_variants.log):
-// <1,3> 89.2 ms, <4,3> 74.9, <4,4> 66.8, <4,5> 66.5, <8,4> 64.3, <8,3> 74.1, <2,3> 76.5
-// Walk schedules, demo.detector() 4M photons, one launch per step (gpurun_out r1h-r1j):
-// scheduled (1002) 13.2 ms, speculative 2004 13.1, 2006 11.8, 2008 ~12.0, 3006 (branch-light
-// node expansion) 12.8 -> the speculative walk with threshold 6/8 is the default.
-static constexpr int kWalk = 2006;        // default walk (wide BVH)
-static constexpr int kWalkSched = 1002;   // scheduled walk; also used when the leaf queue cannot index the triangles
-static const propagate_fn kVariants[] = {
-    propagate_kernel<8, 4, kWalk>,       // 0: default -- 8-wide SAH BVH, speculative walk (parked-leaf queue)
-    propagate_kernel<8, 4, 0>,           // 1: exact-order walk of the reference BVH, 8 children in flight
-    propagate_kernel<8, 4, 1>,           // 2: 8-wide BVH, leaf triangles tested inside the node step
-    propagate_kernel<8, 4, 1001>,        // 3: scheduled, triangle batch 1
-    propagate_kernel<8, 4, 1004>,        // 4: scheduled, triangle batch 4
-    propagate_kernel<8, 4, kWalk, true>, // 5: default + node/triangle counters (bench's byte count)
-    propagate_kernel<8, 4, 1008>,        // 6: scheduled, triangle batch 8
-    propagate_kernel<8, 4, 1000>,        // 7: scheduled, per-lane choice
-    propagate_kernel<8, 3, kWalk>,       // 8: default at 3 waves/SIMD
-    propagate_kernel<8, 5, kWalk>,       // 9: default at 5 waves/SIMD
-    propagate_kernel<8, 4, kWalkSched>,  // 10: scheduled walk, triangle batch 2 (the previous default)
-    propagate_kernel<8, 4, kWalkSched, true>,   // 11: scheduled walk + counters
-};
+static constexpr int kWalk = 2006;        // speculative wide walk, triangle steps at 6/8 of the live lanes
+static constexpr int kWalkSched = 1002;   // scheduled wide walk, triangle batch 2
 static constexpr int kExactVariant = 1;
+static bool wide_queue_ok(const chr_geometry *g) { return g->dev.nwtri < (1u << 30); }   // 30-bit leaf queue entries
+
+// one launch per chunk (the reference's launch structure: slot counts that are
+// not a multiple of 64, or CHR_STEP_LAUNCH=0)
 static propagate_fn select_variant(const chr_geometry *g) {
-    const char *e = getenv("CHR_PROPAGATE_VARIANT");   // read per launch: A/B in one process
+    const char *e = getenv("CHR_PROPAGATE_VARIANT");
     int v = e ? atoi(e) : 0;
-    if (v < 0 || v >= (int)(sizeof(kVariants) / sizeof(kVariants[0]))) v = 0;
-    if (g->dev.nwnodes == 0 && v != 1) v = kExactVariant;   // no wide BVH for this geometry
-    if (g->dev.nwtri >= (1u << 30) && (v == 0 || v == 5 || v == 8 || v == 9)) v = (v == 5) ? 11 : 10;
-    return kVariants[v];
+    if (g->dev.nwnodes == 0) v = kExactVariant;   // no wide BVH for this geometry
+    const bool counting = (v == 3 || v == 5 || v == 6);
+    if (v == kExactVariant) return propagate_kernel<8, 4, 0>;
+    if (v == 4 || v == 6 || !wide_queue_ok(g))
+        return counting ? propagate_kernel<8, 4, kWalkSched, true> : propagate_kernel<8, 4, kWalkSched>;
+    return counting ? propagate_kernel<8, 4, kWalk, true> : propagate_kernel<8, 4, kWalk>;
 }
 
 typedef void (*propagate_step_fn)(const DevGeom *, PropagateArgs, uint32_t);
 typedef void (*trace_fn)(const DevGeom *, TraceArgs);
-static propagate_step_fn select_step_fn(int v);
 struct StepVariant {
-    propagate_step_fn fn;     // fused step kernel (any max_steps)
-    trace_fn trace;           // one-step launches: trace_kernel + shade kernel (nullptr: fused)
-    propagate_step_fn shade;
-    int trace_waves;          // waves per SIMD of the trace kernel (persistent grid size)
+    propagate_step_fn fn;           // fused step kernel (any max_steps)
+    trace_fn trace = nullptr;       // one-step launches: trace_kernel + shade (nullptr: fn)
+    propagate_step_fn shade = nullptr;
+    int trace_waves = 4;            // waves per SIMD of the trace kernel (persistent grid size)
     propagate_step_fn tail = nullptr;   // multi-step launches: group-walk kernel (nullptr: fn)
     int tail_group = 0;                 // its lanes per photon
-    uint32_t group_step_max = 0;        // one-step launches of fewer photons also use the group walk
-    int binned;               // trace rays in direction-binned order: 1 atomic counting sort, 2 radix sort,
-                              // 3 radix sort on the first host step of a propagate only (n >= kBinFirstMin)
+    int binned = 0;                 // trace order binned by direction: 1 every step, 2 first host step only
 };
 // Direction binning pays where the rays of a step share an origin -- the
 // first step of a point or track source -- and not after the first bounce
@@ -2506,81 +2318,35 @@ static constexpr uint32_t kBinFirstMin = 1u << 20;
 static StepVariant select_step_variant(const chr_geometry *g) {
     const char *e = getenv("CHR_PROPAGATE_VARIANT");
     int v = e ? atoi(e) : 0;
-    if (g->dev.nwnodes == 0) v = kExactVariant;
-    const bool queue_ok = g->dev.nwtri < (1u << 30);   // leaf-queue entries hold 30-bit record indices
-    if (!queue_ok && (v == 0 || v == 5 || v >= 12)) v = (v == 5) ? 11 : 10;
-    // 0 (default) = 84, 5 (counting form of the default walk) = 65; 66 / 67: the
-    // fused step kernel alone (an earlier default) and its counting form
-    if (v == 0) v = 84;
-    else if (v == 5) v = 65;
-    else if (v == 66) v = 0;
-    else if (v == 67) v = 5;
-    StepVariant sv{select_step_fn(v), nullptr, nullptr, 0, nullptr, 0, 0, 0};
-    propagate_step_fn shade = propagate_step_kernel<8, 4, HITS_MODE>;
-    switch (v) {   // wavefront split: trace_kernel<COUNT, F, SL, MINW, R>
-        case 50: sv.trace = trace_kernel<false, 6, 12, 4, 16>; sv.trace_waves = 4; break;
-        case 51: sv.trace = trace_kernel<true, 6, 12, 4, 16>; sv.trace_waves = 4;
-                 sv.fn = select_step_fn(5); break;
-        case 52: sv.trace = trace_kernel<false, 6, 8, 5, 16>; sv.trace_waves = 5; break;
-        case 53: sv.trace = trace_kernel<false, 6, 4, 6, 16>; sv.trace_waves = 6; break;
-        case 54: sv.trace = trace_kernel<false, 6, 12, 4, 32>; sv.trace_waves = 4; break;
-        case 55: sv.trace = trace_kernel<false, 6, 12, 4, 8>; sv.trace_waves = 4; break;
-        case 56: sv.trace = trace_kernel<false, 4, 12, 4, 16>; sv.trace_waves = 4; break;
-        case 57: sv.trace = trace_kernel<false, 6, 12, 4, 32>; sv.trace_waves = 4; sv.binned = 1; break;
-        case 58: sv.trace = trace_kernel<true, 6, 12, 4, 32>; sv.trace_waves = 4; sv.binned = 1;
-                 sv.fn = select_step_fn(5); break;
-        case 59: sv.trace = trace_kernel<false, 6, 4, 6, 32>; sv.trace_waves = 6; sv.binned = 1; break;
-        case 60: sv.trace = trace_kernel<false, 6, 12, 4, 32>; sv.trace_waves = 4; sv.binned = 2; break;
-        case 61: sv.trace = trace_kernel<false, 6, 12, 4, 32>; sv.trace_waves = 4; sv.binned = 2;
-                 shade = propagate_step_kernel<8, 2, HITS_MODE>; break;
-        case 62: sv.trace = trace_kernel<false, 6, 12, 4, 32>; sv.trace_waves = 4; sv.binned = 2;
-                 shade = propagate_step_kernel<8, 3, HITS_MODE>; break;
-        case 63: sv.trace = trace_kernel<false, 6, 12, 4, 32>; sv.trace_waves = 4;
-                 shade = propagate_step_kernel<8, 2, HITS_MODE>; break;
-        case 64: sv.trace = trace_kernel<false, 6, 12, 4, 32>; sv.trace_waves = 4; sv.binned = 3;
-                 shade = propagate_step_kernel<8, 2, HITS_MODE>; break;
-        case 65: sv.trace = trace_kernel<true, 6, 12, 4, 32>; sv.trace_waves = 4; sv.binned = 3;
-                 shade = propagate_step_kernel<8, 2, HITS_MODE>; sv.fn = select_step_fn(5); break;
-        case 70: sv.trace = trace_kernel<false, 6, 12, 4, 32>; sv.trace_waves = 4; sv.binned = 3;
-                 shade = propagate_step_kernel<8, 2, HITS_MODE>;
-                 sv.tail = propagate_group_kernel<8, 4>; sv.tail_group = 8; break;
-        case 71: sv.trace = trace_kernel<false, 6, 12, 4, 32>; sv.trace_waves = 4; sv.binned = 3;
-                 shade = propagate_step_kernel<8, 2, HITS_MODE>;
-                 sv.tail = propagate_group_kernel<4, 2>; sv.tail_group = 4; break;
-        case 72: sv.tail = propagate_group_kernel<8, 4>; sv.tail_group = 8; break;   // fused steps + group tail
-        case 74: case 75: case 76:
-                 sv.trace = trace_kernel<false, 6, 12, 4, 32>; sv.trace_waves = 4; sv.binned = 3;
-                 shade = propagate_step_kernel<8, 2, HITS_MODE>;
-                 sv.tail = propagate_group_kernel<8, 4>; sv.tail_group = 8;
-                 sv.group_step_max = v == 74 ? 65536u : (v == 75 ? 131072u : 262144u); break;
-        case 83: case 84: case 85:
-                 sv.trace = trace_kernel<false, 6, 12, 4, 32>; sv.trace_waves = 4; sv.binned = 3;
-                 shade = v == 83 ? shade_kernel<2> : (v == 84 ? shade_kernel<3> : shade_kernel<4>);
-                 sv.tail = propagate_group_kernel<8, 4>; sv.tail_group = 8; break;
-        case 73: sv.trace = trace_kernel<false, 6, 12, 4, 32>; sv.trace_waves = 4; sv.binned = 3;
-                 shade = propagate_step_kernel<8, 2, HITS_MODE>;
-                 sv.tail = propagate_group_kernel<8, 2>; sv.tail_group = 8; break;
-        default: break;
+    StepVariant sv;
+    if (g->dev.nwnodes == 0 || v == kExactVariant) {
+        sv.fn = propagate_step_kernel<8, 4, 0>;
+        return sv;
     }
-    if (sv.trace) sv.shade = shade;
-    return sv;
-}
-static propagate_step_fn select_step_fn(int v) {
+    if (!wide_queue_ok(g) || v == 4 || v == 6) {
+        sv.fn = (v == 3 || v == 5 || v == 6) ? propagate_step_kernel<8, 4, kWalkSched, true>
+                                              : propagate_step_kernel<8, 4, kWalkSched>;
+        return sv;
+    }
     switch (v) {
-        case 1: return propagate_step_kernel<8, 4, 0>;
-        case 5: return propagate_step_kernel<8, 4, kWalk, true>;
-        case 8: return propagate_step_kernel<8, 3, kWalk>;
-        case 9: return propagate_step_kernel<8, 5, kWalk>;
-        case 10: return propagate_step_kernel<8, 4, kWalkSched>;
-        case 11: return propagate_step_kernel<8, 4, kWalkSched, true>;
-        case 12: return propagate_step_kernel<8, 4, 2002>;
-        case 14: return propagate_step_kernel<8, 4, 2004>;
-        case 15: return propagate_step_kernel<8, 4, 2004, true>;
-        case 18: return propagate_step_kernel<8, 4, 2008>;
-        case 26: return propagate_step_kernel<8, 4, 3006>;
-        case 27: return propagate_step_kernel<8, 4, 3006, true>;
-        default: return propagate_step_kernel<8, 4, kWalk>;
+        case 2: sv.fn = propagate_step_kernel<8, 4, kWalk>; break;
+        case 3: sv.fn = propagate_step_kernel<8, 4, kWalk, true>; break;
+        case 5:
+            sv.fn = propagate_step_kernel<8, 4, kWalk, true>;
+            sv.trace = trace_kernel<true, 6, 12, 4, 32>;
+            sv.shade = shade_kernel<3>;
+            sv.binned = 2;
+            break;
+        default:   // 0, 7, 8
+            sv.fn = propagate_step_kernel<8, 4, kWalk>;
+            sv.trace = trace_kernel<false, 6, 12, 4, 32>;
+            sv.shade = shade_kernel<3>;
+            sv.tail = propagate_group_kernel<8, 4>;
+            sv.tail_group = 8;
+            sv.binned = v == 7 ? 1 : (v == 8 ? 0 : 2);
+            break;
     }
+    return sv;
 }
 
 static constexpr int32_t kSortMin = 16384;   // below this a launch is a few waves: no reordering
@@ -2669,8 +2435,7 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
     a.hits = nullptr;
     const uint32_t threads = std::min(cap, (n + 63u) & ~63u);
     const StepVariant sv = select_step_variant(g);
-    const bool small = sv.tail && max_steps == 1 && n < sv.group_step_max;
-    const bool split = sv.trace && hits && max_steps == 1 && !small;
+    const bool split = sv.trace && hits && max_steps == 1;
     if (split) {
         uint32_t *next = (uint32_t *)(hits + n);
         CHR_HIP_CHECK(hipMemsetAsync(next, 0, 4, stream));
@@ -2679,19 +2444,13 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
         ta.queue = in_queue; ta.n = n; ta.hits = hits; ta.next = next; ta.counters = counters; ta.order = nullptr;
         ta.walk_hist = nullptr;
         if (trace_steps()) {   // debugging: per-walk cost histogram (counting variants), printed per step
-            ta.walk_hist = next + 16 + 2 * (size_t)n + NBINS;
+            ta.walk_hist = next + 16 + 2 * (size_t)n;
             CHR_HIP_CHECK(hipMemsetAsync(ta.walk_hist, 0, 34 * 4, stream));
         }
         if (ev0) CHR_HIP_CHECK(hipEventRecord(ev0, stream));
-        if (sv.binned == 1) {   // hits region: [hits n x int2][next][pad] [keys n][order n][hist NBINS]
-            uint32_t *keys = next + 16, *order = keys + n, *hist = order + n;
-            CHR_HIP_CHECK(hipMemsetAsync(hist, 0, NBINS * 4, stream));
-            hipLaunchKernelGGL(bin_count_kernel, dim3(grid_for(n)), dim3(BLOCK), 0, stream, ph->d_dir, in_queue, n,
-                               keys, hist);
-            hipLaunchKernelGGL(bin_scan_kernel, dim3(1), dim3(1024), 0, stream, hist);
-            hipLaunchKernelGGL(bin_scatter_kernel, dim3(grid_for(n)), dim3(BLOCK), 0, stream, keys, n, hist, order);
-            ta.order = order;
-        } else if (sv.binned == 2 || (sv.binned == 3 && first_step && n >= kBinFirstMin)) {   // 16-bit radix sort of (cell, queue position); temp space after the hits region
+        if (sv.binned == 1 || (sv.binned == 2 && first_step && n >= kBinFirstMin)) {
+            // 16-bit radix sort of (direction cell, queue position); hits region:
+            // [hits n x int2][next + pad, 16 words][keys n][values n][walk hist 64 words]
             uint32_t *keys = next + 16, *order = keys + n;
             hipLaunchKernelGGL(bin_key_kernel, dim3(grid_for(n)), dim3(BLOCK), 0, stream, ph->d_dir, in_queue, n, keys,
                                order);
@@ -2714,7 +2473,7 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
         CHR_HIP_CHECK(hipEventRecord(ev0, stream));
     }
     if (split_out) *split_out = split;
-    if (!split && sv.tail && (max_steps > 1 || small)) {   // group walk, alive bits OR-ed
+    if (!split && sv.tail && max_steps > 1) {   // group walk, alive bits OR-ed
         CHR_HIP_CHECK(hipMemsetAsync(masks, 0, (size_t)nwords * 8, stream));
         if (ev0) CHR_HIP_CHECK(hipEventRecord(ev0, stream));
         hipLaunchKernelGGL(sv.tail, dim3(grid_for((uint64_t)threads * sv.tail_group)), dim3(BLOCK), 0, stream,
@@ -2818,7 +2577,7 @@ extern "C" int chr_propagate(const chr_geometry *g, const chr_photons *ph, uint3
     if (fused) swords = std::max<uint64_t>(swords, 16 + mask_scan_words(nphotons) + 16);
     const size_t qbytes = ((size_t)nphotons + 1) * 4;
     // split path: hits, ray counter, binning keys/order/histogram
-    const size_t hbytes = fused ? (size_t)nphotons * 24 + 128 + NBINS * 4 + 256 + 512 + sort_temp_bytes16(nphotons) : 0;
+    const size_t hbytes = fused ? (size_t)nphotons * 24 + 128 + 256 + 512 + sort_temp_bytes16(nphotons) : 0;
     void *buf = nullptr;
     int rc = scratch_get(2 * qbytes + swords * 4 + 64 + hbytes, &buf);
     if (rc) return rc;
@@ -2829,7 +2588,7 @@ extern "C" int chr_propagate(const chr_geometry *g, const chr_photons *ph, uint3
     int2 *hits = fused ? (int2 *)(((uintptr_t)(scratch + swords) + 15) & ~(uintptr_t)15) : nullptr;
     // radix-sort space after [hits][next+pad][keys][order][hist][walk hist]
     uint32_t *sort_space = fused ? (uint32_t *)(((uintptr_t)((uint32_t *)(hits + nphotons) + 16 + 2 * (size_t)nphotons +
-                                                            NBINS + 64) + 255) & ~(uintptr_t)255) : nullptr;
+                                                            64) + 255) & ~(uintptr_t)255) : nullptr;
     uint32_t *pinned = nullptr;
     if ((rc = pinned_words(&pinned))) return rc;
     const size_t max_chunks = fused ? 2 : (nphotons + chunk_cap - 1) / chunk_cap;   // fused: step + its walk
@@ -2906,7 +2665,7 @@ extern "C" int chr_propagate(const chr_geometry *g, const chr_photons *ph, uint3
                 fprintf(stderr, "chr_propagate: step %d nsteps %d -> %lld alive\n", step, nsteps, (long long)n);
                 if (nsteps == 1 && hits) {   // walk-cost histogram of a counting trace variant (zeros otherwise)
                     uint32_t wh[34];
-                    CHR_HIP_CHECK(hipMemcpy(wh, (uint32_t *)(hits + n_prev) + 16 + 2 * (size_t)n_prev + NBINS, sizeof(wh),
+                    CHR_HIP_CHECK(hipMemcpy(wh, (uint32_t *)(hits + n_prev) + 16 + 2 * (size_t)n_prev, sizeof(wh),
                                             hipMemcpyDeviceToHost));
                     fprintf(stderr, "  walk cost (nodes+triangles) log2 histogram:");
                     for (int b = 0; b < 32; ++b) if (wh[b]) fprintf(stderr, " [%u,%u):%u", 1u << b, 2u << b, wh[b]);
