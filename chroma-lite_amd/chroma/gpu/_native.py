@@ -105,6 +105,14 @@ _SIGNATURES = {
     'chr_init_rng_subseq': (c_i32, [c_vp, c_u32, c_u64, c_u64, c_u64, c_vp]),
     'chr_channel_hit_counts': (c_i32, [ctypes.POINTER(PhotonsDesc), c_i32, c_i32, c_u32, c_vp, c_vp, c_vp, c_i32,
                                        c_vp]),
+    'chr_pdf_bin_hits': (c_i32, [c_i32, c_vp, c_vp, c_vp, c_i32, c_f32, c_f32, c_i32, c_f32, c_f32, c_vp, c_vp]),
+    'chr_pdf_accumulate_bincount': (c_i32, [c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_f32, c_f32, c_f32, c_i32,
+                                            c_vp, c_vp, c_vp]),
+    'chr_pdf_accumulate_nearest': (c_i32, [c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_vp]),
+    'chr_pdf_accumulate_moments': (c_i32, [c_i32, c_i32, c_vp, c_vp, c_f32, c_f32, c_f32, c_f32, c_vp, c_vp, c_vp,
+                                           c_vp, c_vp, c_vp]),
+    'chr_pdf_accumulate_kernel_eval': (c_i32, [c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_f32, c_f32, c_f32, c_f32,
+                                               c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     'chr_last_error': (ctypes.c_char_p, []),
     'chr_version': (c_i32, []),
 }

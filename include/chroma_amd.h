@@ -290,6 +290,46 @@ int chr_channel_hit_counts(const chr_photons *ph, int32_t start_photon, int32_t 
                            const int32_t *d_solid_id_to_channel_index, uint32_t *d_counts,
                            int32_t nchannels, void *stream);
 
+/* ------------------------------------------------------------------- PDF
+ * replaces: chroma/cuda/pdf.cu, launched by GPUPDF / GPUKernelPDF
+ * (chroma/gpu/pdf.py:7-372).  Inputs are GPUChannels words (t, q: f32; DAQ
+ * copy i of channel c at i*nchannels + c).  One work-item per channel, the
+ * reference's accumulation order and float accumulators.  All async. */
+
+/* replaces: bin_hits (pdf.cu:9-32; GPUPDF.add_hits_to_pdf, pdf.py:206-222).
+ * d_pdf is [nchannels][tbins][qbins] u32.  Bins are clamped to the channel's
+ * last bin (the reference can spill t == tmax-ulp into the next row). */
+int chr_pdf_bin_hits(int32_t nchannels, const float *d_channel_q, const float *d_channel_time,
+                     uint32_t *d_hitcount, int32_t tbins, float tmin, float tmax, int32_t qbins, float qmin,
+                     float qmax, uint32_t *d_pdf, void *stream);
+/* replaces: accumulate_bincount (pdf.cu:34-96; GPUPDF.accumulate_pdf_eval,
+ * pdf.py:296-316).  d_work_queues: nhit*(ndaq+1) u32, word 0 of each queue
+ * = 1 + queued entries (the caller fills 1). */
+int chr_pdf_accumulate_bincount(int32_t nchannels, int32_t ndaq, const uint32_t *d_event_hit,
+                                const float *d_event_time, const float *d_mc_time, uint32_t *d_hitcount,
+                                uint32_t *d_bincount, float min_twidth, float tmin, float tmax,
+                                int32_t min_bin_content, const uint32_t *d_map_channel_to_hit,
+                                uint32_t *d_work_queues, void *stream);
+/* replaces: accumulate_nearest_neighbor_block (pdf.cu:152-219; pdf.py:318-328):
+ * per hit, the min_bin_content smallest of (stored table + queued distances),
+ * ascending.  min_bin_content <= 8192 (the reference's table holds 1000). */
+int chr_pdf_accumulate_nearest(int32_t nhit, int32_t ndaq, const uint32_t *d_map_hit_to_channel,
+                               const uint32_t *d_work_queues, const float *d_event_time,
+                               const float *d_mc_time, float *d_nearest_mc, int32_t min_bin_content,
+                               void *stream);
+/* replaces: accumulate_moments (pdf.cu:223-266; GPUKernelPDF.accumulate_moments, pdf.py:42-59) */
+int chr_pdf_accumulate_moments(int32_t time_only, int32_t nchannels, const float *d_mc_time,
+                               const float *d_mc_charge, float tmin, float tmax, float qmin, float qmax,
+                               uint32_t *d_mom0, float *d_t_mom1, float *d_t_mom2, float *d_q_mom1,
+                               float *d_q_mom2, void *stream);
+/* replaces: accumulate_kernel_eval (pdf.cu:271-368; GPUKernelPDF.accumulate_kernel, pdf.py:139-158) */
+int chr_pdf_accumulate_kernel_eval(int32_t time_only, int32_t nchannels, const uint32_t *d_event_hit,
+                                   const float *d_event_time, const float *d_event_charge,
+                                   const float *d_mc_time, const float *d_mc_charge, float tmin, float tmax,
+                                   float qmin, float qmax, const float *d_inv_time_bw,
+                                   const float *d_inv_charge_bw, uint32_t *d_hitcount, float *d_time_pdf,
+                                   float *d_charge_pdf, void *stream);
+
 /* ------------------------------------------------------------- misc */
 const char *chr_last_error(void);
 int chr_version(void);

@@ -224,4 +224,35 @@ CHR_FN float chr_atan2f(float y, float x) {
     return ysign ? -r : r;
 }
 
+/* ---------------------------------------------------------------- erf
+ * Used by the kernel-density PDF normalisation (reference pdf.cu:311-362,
+ * erff under --use_fast_math).  |x| < 0.5: Maclaurin series to x^13
+ * (truncation < 5e-10 relative); 0.5 <= |x| < 4: Abramowitz & Stegun 7.1.26
+ * (absolute error <= 1.5e-7); |x| >= 4: +-1.  Parity with CUDA's erff is
+ * unpinned (a few 1e-7 absolute), identical between HIP and the oracle. */
+CHR_FN float chr_erff(float x) {
+    if (chr_isnan(x)) return x;
+    const float a = chr_fabsf(x);
+    if (a < 0.5f) {
+        const float z = x * x;
+        float p = chr_fmaf(1.0683760684e-4f, z, -7.5757575758e-4f);
+        p = chr_fmaf(p, z, 4.6296296296e-3f);
+        p = chr_fmaf(p, z, -2.3809523810e-2f);
+        p = chr_fmaf(p, z, 1.0000000000e-1f);
+        p = chr_fmaf(p, z, -3.3333333333e-1f);
+        p = chr_fmaf(p, z, 1.0f);
+        return (x * 1.1283791671f) * p;
+    }
+    float r = 1.0f;
+    if (a < 4.0f) {
+        const float t = 1.0f / chr_fmaf(0.3275911f, a, 1.0f);
+        float p = chr_fmaf(1.061405429f, t, -1.453152027f);
+        p = chr_fmaf(p, t, 1.421413741f);
+        p = chr_fmaf(p, t, -0.284496736f);
+        p = chr_fmaf(p, t, 0.254829592f);
+        r = 1.0f - (p * t) * chr_expf(-(a * a));
+    }
+    return (chr_f2u(x) >> 31) ? -r : r;
+}
+
 #endif /* CHROMA_FMATH_H */
