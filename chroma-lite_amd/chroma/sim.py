@@ -36,6 +36,8 @@ class Simulation(object):
         if hasattr(detector, 'num_channels'):
             self.gpu_geometry = gpu.GPUDetector(detector)
             self.gpu_daq = gpu.GPUDaq(self.gpu_geometry) if self.gpu_geometry.nchannels > 0 else None
+            self.gpu_pdf = gpu.GPUPDF()                # sim.py:45-46
+            self.gpu_pdf_kernel = gpu.GPUKernelPDF()
         else:
             self.gpu_geometry = gpu.GPUGeometry(detector)
         self.rng_states = gpu.get_rng_states(self.nthreads_per_block * self.max_blocks, seed=self.seed)

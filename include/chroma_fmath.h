@@ -228,7 +228,7 @@ CHR_FN float chr_atan2f(float y, float x) {
  * Used by the kernel-density PDF normalisation (reference pdf.cu:311-362,
  * erff under --use_fast_math).  |x| < 0.5: Maclaurin series to x^13
  * (truncation < 5e-10 relative); 0.5 <= |x| < 4: Abramowitz & Stegun 7.1.26
- * (absolute error <= 1.5e-7); |x| >= 4: +-1.  Parity with CUDA's erff is
+ * (absolute error <= 1.5e-7; <= 2.5e-7 measured in float32); |x| >= 4: +-1.  Parity with CUDA's erff is
  * unpinned (a few 1e-7 absolute), identical between HIP and the oracle. */
 CHR_FN float chr_erff(float x) {
     if (chr_isnan(x)) return x;

@@ -185,3 +185,74 @@ def daq(photons, solid_id, solid_id_to_channel_index, time_cdf, charge_cdf, char
     q = np.zeros(total, dtype=np.float32)
     q[:nchannels] = q_int[:nchannels].astype(np.float32) * np.float32(charge_unit)
     return t, q, hist
+
+
+# ------------------------------------------------------------------ PDF (pdf_oracle.c)
+def _pdf_lib():
+    l = lib()
+    if not getattr(l, '_pdf_bound', False):
+        vp, i32, f32 = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
+        l.orc_pdf_bin_hits.argtypes = [i32, vp, vp, vp, i32, f32, f32, i32, f32, f32, vp]
+        l.orc_pdf_accumulate_bincount.argtypes = [i32, i32, vp, vp, vp, vp, vp, f32, f32, f32, i32, vp, vp]
+        l.orc_pdf_accumulate_nearest.argtypes = [i32, i32, vp, vp, vp, vp, vp, i32]
+        l.orc_pdf_accumulate_moments.argtypes = [i32, i32, vp, vp, f32, f32, f32, f32, vp, vp, vp, vp, vp]
+        l.orc_pdf_accumulate_kernel_eval.argtypes = [i32, i32, vp, vp, vp, vp, vp, f32, f32, f32, f32, vp, vp,
+                                                     vp, vp, vp]
+        l.orc_erff.argtypes = [i32, vp, vp]
+        l._pdf_bound = True
+    return l
+
+
+def _f32(a):
+    return np.ascontiguousarray(a, dtype=np.float32)
+
+
+def _u32(a):
+    return np.ascontiguousarray(a, dtype=np.uint32)
+
+
+def erff(x):
+    x = _f32(x)
+    y = np.zeros_like(x)
+    _pdf_lib().orc_erff(len(x), _p(x), _p(y))
+    return y
+
+
+def pdf_bin_hits(q, t, hitcount, pdf, tbins, trange, qbins, qrange):
+    """bin_hits (pdf.cu:9-32); hitcount / pdf (u32) updated in place."""
+    q, t = _f32(q), _f32(t)
+    _pdf_lib().orc_pdf_bin_hits(len(hitcount), _p(q), _p(t), _p(hitcount), tbins, trange[0], trange[1], qbins,
+                                qrange[0], qrange[1], _p(pdf))
+
+
+def pdf_accumulate_bincount(event_hit, event_time, mc_time, ndaq, hitcount, bincount, work_queues, min_twidth,
+                            trange, min_bin_content, map_channel_to_hit):
+    """accumulate_bincount (pdf.cu:34-96); hitcount / bincount / work_queues in place."""
+    eh, et, mt, m = _u32(event_hit), _f32(event_time), _f32(mc_time), _u32(map_channel_to_hit)
+    _pdf_lib().orc_pdf_accumulate_bincount(len(eh), ndaq, _p(eh), _p(et), _p(mt), _p(hitcount), _p(bincount),
+                                           min_twidth, trange[0], trange[1], min_bin_content, _p(m),
+                                           _p(work_queues))
+
+
+def pdf_accumulate_nearest(map_hit_to_channel, work_queues, event_time, mc_time, ndaq, nearest_mc, min_bin_content):
+    """accumulate_nearest_neighbor (pdf.cu:98-150); nearest_mc in place."""
+    m, et, mt = _u32(map_hit_to_channel), _f32(event_time), _f32(mc_time)
+    _pdf_lib().orc_pdf_accumulate_nearest(len(m), ndaq, _p(m), _p(work_queues), _p(et), _p(mt), _p(nearest_mc),
+                                          min_bin_content)
+
+
+def pdf_accumulate_moments(time_only, mc_time, mc_charge, trange, qrange, mom0, tm1, tm2, qm1, qm2):
+    """accumulate_moments (pdf.cu:223-266); accumulators in place."""
+    mt, mq = _f32(mc_time), _f32(mc_charge)
+    _pdf_lib().orc_pdf_accumulate_moments(int(time_only), len(mom0), _p(mt), _p(mq), trange[0], trange[1], qrange[0],
+                                          qrange[1], _p(mom0), _p(tm1), _p(tm2), _p(qm1), _p(qm2))
+
+
+def pdf_accumulate_kernel_eval(time_only, event_hit, event_time, event_charge, mc_time, mc_charge, trange, qrange,
+                               inv_tbw, inv_qbw, hitcount, time_pdf, charge_pdf):
+    """accumulate_kernel_eval (pdf.cu:271-368); accumulators in place."""
+    eh, et, eq = _u32(event_hit), _f32(event_time), _f32(event_charge)
+    mt, mq, it, iq = _f32(mc_time), _f32(mc_charge), _f32(inv_tbw), _f32(inv_qbw)
+    _pdf_lib().orc_pdf_accumulate_kernel_eval(int(time_only), len(eh), _p(eh), _p(et), _p(eq), _p(mt), _p(mq),
+                                              trange[0], trange[1], qrange[0], qrange[1], _p(it), _p(iq),
+                                              _p(hitcount), _p(time_pdf), _p(charge_pdf))
