@@ -107,25 +107,36 @@ def test_kernel_pdf_parity(cuda, time_only):
 
 
 def test_pdf_from_propagate_and_daq(cuda, small_detector):
-    """test/test_pdf.py testGPUPDF with an isotropic source (10 events)."""
+    """test/test_pdf.py testGPUPDF with an isotropic source (20 events)."""
     from chroma import gpu
     from chroma.photon_source import isotropic
+    saved = small_detector.time_cdf, small_detector.charge_cdf
     small_detector.set_time_dist_gaussian(1.2, -6.0, 6.0)
     small_detector.set_charge_dist_gaussian(1.0, 0.1, 0.5, 1.5)
-    gdet = gpu.GPUDetector(small_detector)
+    try:
+        gdet = gpu.GPUDetector(small_detector)
+    finally:
+        small_detector.time_cdf, small_detector.charge_cdf = saved
     nthreads_per_block, max_blocks = 64, 1024
     rng = gpu.get_rng_states(nthreads_per_block * max_blocks)
     daq = gpu.GPUDaq(gdet)
     p = gpu.GPUPDF()
-    p.setup_pdf(small_detector.num_channels(), 100, (-0.5, 999.5), 10, (-0.5, 9.5))
+    p.setup_pdf(gdet.nchannels, 100, (-0.5, 999.5), 10, (-0.5, 9.5))
     p.clear_pdf()
-    for ev in range(10):
-        gp = gpu.GPUPhotons(isotropic(20000, seed=ev))
-        gp.propagate(gdet, rng, nthreads_per_block, max_blocks)
+    detected = channel_hits = 0
+    for ev in range(20):     # a few hundred photons per event: channel charges of a few p.e. (qrange 0-9.5)
+        gp = gpu.GPUPhotons(isotropic(400, seed=ev))
+        gp.propagate(gdet, rng, nthreads_per_block, max_blocks, max_steps=100)
+        detected += int(((gp.flags.get() & 4) != 0).sum())
         daq.begin_acquire()
         daq.acquire(gp, rng, nthreads_per_block, max_blocks)
-        p.add_hits_to_pdf(daq.end_acquire())
+        ch = daq.end_acquire()
+        c = ch.get()
+        channel_hits += int(c.hit.sum())
+        seen = (c.t[c.hit], c.q[c.hit], len(ch.t), gdet.nchannels)
+        p.add_hits_to_pdf(ch)
+    assert detected > 0 and channel_hits > 0, (detected, channel_hits)
     hitcount, pdf = p.get_pdfs()
-    assert (hitcount > 0).any() and (pdf > 0).any()
+    assert (hitcount > 0).any() and (pdf > 0).any(), (channel_hits, hitcount.sum(), seen)
     for i, nhits in enumerate(hitcount):
         assert nhits == pdf[i].sum()
