@@ -16,21 +16,25 @@ photons are histogrammed per PMT channel on the device and SUM-reduced over
 the ranks (RCCL, chroma.gpu.shard) -- the only exchange the path has.  The
 timed region is bracketed by barriers and the max over ranks is reported.
 
+Parity: rank 0 runs the CPU oracle (cpu_baseline leg, the only place bench.py
+touches oracle/) on a bounded sample of the same photons with the same RNG
+initialisation, then propagates the SAME sample on the GPU and compares the
+two photon by photon (history flags, last-hit triangles and channels
+bit-exact; positions, directions, polarisations, times and wavelengths as a
+max relative difference) -- every bench line checks its own workload.
+
 Roofline: the dominant kernel is trace_kernel, the
-BVH walk of every one-step launch (the last, multi-step launch of the
-reference's nsteps policy runs the fused step kernel).  It is bound by HBM/L2
-latency-bandwidth on dependent node/triangle gathers.
+BVH walk of every one-step launch.  It is bound by HBM/L2 latency-bandwidth on
+dependent node/triangle gathers.
     achieved = algorithmic bytes per trace launch / average trace launch time
 with the average from HIP events around each trace launch on its stream, and
 the algorithmic bytes of section 8(d): per walk 16 * reference-BVH nodes +
 48 * reference triangles + 4, counted by the CPU oracle walking the REFERENCE
 BVH in the reference's DFS order on the cpu_baseline sample of the same
-workload (layout-independent, comparable across builds), times the rays of
-the launch.  The bytes of this build's own layout (96-byte wide nodes, 64-byte
-triangle records) are counted on every photon by one extra, untimed propagate
-with the counting variant (CHR_PROPAGATE_VARIANT=5) and reported beside it;
-traffic = HBM bytes per trace launch from the rocprofv3 FETCH_SIZE/WRITE_SIZE
-passes of this workload (profiles/latest_pmc.json).
+workload, times the rays of the launch.  traffic = HBM bytes per trace launch
+from the rocprofv3 FETCH_SIZE/WRITE_SIZE passes of this workload; those
+counters cannot be read from inside this process, so the value is copied
+from the committed PMC summary (profiles/latest_pmc.json) and labelled so.
 """
 import argparse
 import json
@@ -45,6 +49,9 @@ import numpy as np  # noqa: E402
 
 METRIC = 'propagated photons/sec, 29k-PMT detector, 10M isotropic photons, 1/2/4/8 GPUs'
 HBM_PEAK_GBS = 8000.0
+PHOTON_SEED = 20260102
+
+
 def _demo_detector(**kw):
     from chroma import demo
     return demo.detector(**kw)
@@ -72,6 +79,20 @@ DETECTORS = {
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
+
+
+def usable_cpus():
+    """Host cores this job may use: the affinity mask, capped by a cgroup CPU
+    quota (a GPU box shares its host: nproc shows every core of the machine)."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        with open('/sys/fs/cgroup/cpu.max') as f:
+            quota, period = f.read().split()[:2]
+        if quota != 'max':
+            n = min(n, max(1, int(int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    return n
 
 
 def build_geometry(name, cache_dir):
@@ -107,16 +128,82 @@ def build_geometry(name, cache_dir):
     return det
 
 
+def shared_geometry(name, cache_dir, rank, dist):
+    """Rank 0 builds (flatten + BVH: minutes for the 29k detector) and fills
+    the node-local cache; the other ranks wait at a barrier, then load it."""
+    if dist is None or not cache_dir:
+        return build_geometry(name, cache_dir)
+    if rank == 0:
+        det = build_geometry(name, cache_dir)
+    dist.barrier()
+    if rank != 0:
+        det = build_geometry(name, cache_dir)
+    return det
+
+
+def rng_first_subsequence(rank, nslots):
+    """Rank r's RNG slots are curand subsequences [r*nslots, (r+1)*nslots):
+    disjoint streams, and rank 0 draws what a single-GPU run draws."""
+    return rank * nslots
+
+
+def timed_loop(step, steps, warmup, dist, sync):
+    """W untimed steps, then K timed steps bracketed by barrier + sync on both
+    sides; returns (elapsed max over ranks, this rank's per-step seconds,
+    per-step results)."""
+    for _ in range(warmup):
+        step()
+    sync()
+    if dist is not None:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    marks, results = [], []
+    for _ in range(steps):
+        results.append(step())
+        marks.append(time.perf_counter())   # propagate is synchronous: a mark per step
+    sync()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        import torch
+        dev = 'cuda' if (torch.cuda.is_available() and dist.get_backend() != 'gloo') else 'cpu'
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    per_step = [b - a for a, b in zip([t0] + marks[:-1], marks)]
+    return elapsed, per_step, results
+
+
+def result_line(args, world, elapsed, per_step_s, detector_info, detail):
+    total = args.photons * world * args.steps
+    value = total / elapsed
+    return {
+        'metric': METRIC, 'value': value, 'unit': 'photons/s', 'n_gpus': world, 'steps': args.steps,
+        'warmup': args.warmup, 'ms_per_step': 1e3 * elapsed / args.steps, 'higher_is_better': True,
+        'scaling': 'weak', 'vs_baseline': (value / 2.5e6) if args.detector == '29k' else None,
+        'dtype': 'f32', 'data': 'synthetic isotropic point source (BASELINE.md section 3), seed %d+rank' % PHOTON_SEED,
+        'config': dict({'workload': 'GPUPhotons.propagate of %d isotropic photons per GPU per step on %s, '
+                                    'max_steps=%d, launch shape %dx%d (%d RNG slots)' % (
+                                        args.photons, DETECTORS[args.detector][0], args.max_steps,
+                                        args.nthreads_per_block, args.max_blocks,
+                                        args.nthreads_per_block * args.max_blocks),
+                        'detector': args.detector, 'photons_per_gpu': args.photons, 'max_steps': args.max_steps,
+                        'parallelism': 'photon-sharded x%d, geometry replicated' % world}, **detector_info),
+        'detail': dict({'step_ms': [round(1e3 * s, 3) for s in per_step_s]}, **detail),
+        'roofline': None, 'cpu_baseline': None, 'parity': None,
+    }
+
+
 def cpu_baseline(packed, photons, nslots, ntpb, max_blocks, max_steps, seed, budget_s, threads):
     """Oracle (plain C port of the reference kernel, OpenMP) on a bounded
-    sample of the same workload; also returns the per-photon algorithmic
-    byte count for the roofline."""
+    sample of the same workload; also returns the oracle's photons (the parity
+    reference) and its walk counts on the reference BVH (roofline bytes)."""
     sys.path.insert(0, os.path.join(ROOT, 'oracle'))
     import oracle
     from chroma.event import Photons
     n = 2000
-    total_t = 0.0
-    agg = None
     while True:
         sample = Photons(photons.pos[:n], photons.dir[:n], photons.pol[:n], photons.wavelengths[:n])
         host = oracle.HostPhotons(sample)
@@ -124,55 +211,82 @@ def cpu_baseline(packed, photons, nslots, ntpb, max_blocks, max_steps, seed, bud
         t0 = time.time()
         stats = oracle.propagate(packed, host, st, nslots, ntpb, max_blocks, max_steps, threads=threads)
         dt = time.time() - t0
-        total_t, agg = dt, (n, stats)
         if dt > budget_s / 4 or n * 4 > len(photons.pos):
             break
         n = int(min(len(photons.pos), n * max(2.0, min(8.0, (budget_s / 2) / max(dt, 1e-3)))))
-    n, stats = agg
     b_alg = 120.0 + (16.0 * stats['nodes_visited'] + 48.0 * stats['tris_tested'] + 4.0 * stats['traversals']) / n
-    return dict(value=n / total_t, unit='photons/s', cores=threads, kind='port',
-                sample='%d of the same isotropic photons, same geometry and launch shape, max_steps=%d; %.1fs on %d '
-                       'threads' % (n, max_steps, total_t, threads)), b_alg, stats, n
+    cpu = dict(value=n / dt, unit='photons/s', cores=threads, kind='port',
+               sample='%d of the same isotropic photons, same geometry and launch shape, max_steps=%d; %.1fs on %d '
+                      'threads (nproc %d)' % (n, max_steps, dt, threads, os.cpu_count() or 0))
+    return cpu, b_alg, stats, n, host
 
 
-def roofline(args, live, cst, ref, n):
-    """roofline object of the bench line for the dominant kernel (trace_kernel).
-    live: timed-region sums of the propagate stats; cst: counting pass (own
-    layout); ref: oracle counts on the reference BVH (None without cpu_baseline)."""
-    launches = max(1, live['trace_launches'])
-    rays_per_launch = live['trace_rays'] / launches
-    avg_launch_s = live['trace_ms'] / launches / 1e3
-    own = None
-    if cst is not None and cst.traversals:
-        own = (96.0 * cst.nodes_visited + 64.0 * cst.triangles_tested + 52.0 * cst.traversals) / cst.traversals
-    if ref is not None:
-        per_walk, basis = (16.0 * ref['nodes_visited'] + 48.0 * ref['tris_tested']) / ref['traversals'] + 4.0, \
-            'SURVEY 8(d): 16 B x reference-BVH nodes + 48 B x triangles + 4 B per walk (oracle, reference DFS order)'
-    else:
-        per_walk, basis = own, 'own layout: 96 B x wide nodes + 64 B x triangle records + 52 B per walk'
-    alg_per_launch = rays_per_launch * per_walk if per_walk else 0.0
+def gpu_parity(gdet, photons, n, host, args, solid_map, s2c):
+    """Propagate the oracle's sample on the GPU (same RNG initialisation, same
+    launch shape) and compare photon by photon."""
+    from chroma import gpu
+    from chroma.event import Photons
+    sample = Photons(photons.pos[:n], photons.dir[:n], photons.pol[:n], photons.wavelengths[:n])
+    nslots = args.nthreads_per_block * args.max_blocks
+    gp = gpu.GPUPhotons(sample, copy_flags=True, copy_triangles=False, copy_weights=False)
+    gp.propagate(gdet, gpu.get_rng_states(nslots, seed=args.seed), nthreads_per_block=args.nthreads_per_block,
+                 max_blocks=args.max_blocks, max_steps=args.max_steps)
+    got = gp.get()
+
+    def channel(flags, last_hit):
+        ch = np.full(len(flags), -1, np.int64)
+        det = ((flags & 4) != 0) & (last_hit > -1)
+        ch[det] = s2c[solid_map[last_hit[det]]]
+        return ch
+
+    def max_rel(a, b):
+        a = np.asarray(a, np.float64)
+        b = np.asarray(b, np.float64)
+        return float(np.max(np.abs(a - b) / np.maximum(np.abs(b), 1e-30))) if a.size else 0.0
+
+    flags_eq = bool(np.array_equal(got.flags, host.flags))
+    hits_eq = bool(np.array_equal(got.last_hit_triangles, host.last_hit_triangles))
+    ch_gpu, ch_ref = channel(got.flags, got.last_hit_triangles), channel(host.flags, host.last_hit_triangles)
+    rel = max(max_rel(got.pos, host.pos), max_rel(got.t, host.t), max_rel(got.wavelengths, host.wavelengths))
+    dp = max(float(np.max(np.abs(got.dir - host.dir))) if n else 0.0,
+             float(np.max(np.abs(got.pol - host.pol))) if n else 0.0)
+    return {'n': int(n), 'flags_equal': flags_eq, 'last_hit_equal': hits_eq,
+            'channel_equal': bool(np.array_equal(ch_gpu, ch_ref)),
+            'flags_mismatches': int(np.count_nonzero(got.flags != host.flags)),
+            'detected': int(np.count_nonzero(ch_ref >= 0)), 'max_rel': rel, 'dir_pol_max_abs': dp,
+            'binned_first_step': bool(n >= (1 << 20)),
+            'stack_overflows': int(gp.last_stats.stack_overflows)}
+
+
+def _kernel_info(native):
+    try:
+        return native.kernel_info()
+    except (AttributeError, native.NativeError) as e:     # an older library (A/B runs)
+        return 'unavailable: %s' % e
+
+
+def roofline(args, trace_ms, trace_launches, trace_rays, ref, launch_ms):
+    """roofline object of the bench line for the dominant kernel (trace_kernel)."""
+    launches = max(1, trace_launches)
+    rays_per_launch = trace_rays / launches
+    avg_launch_s = trace_ms / launches / 1e3
+    per_walk = (16.0 * ref['nodes_visited'] + 48.0 * ref['tris_tested']) / ref['traversals'] + 4.0
+    alg_per_launch = rays_per_launch * per_walk
     achieved = alg_per_launch / avg_launch_s / 1e9 if avg_launch_s > 0 else 0.0
+    lm = np.asarray(launch_ms, np.float64)
     rl = {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
           'frac': achieved / HBM_PEAK_GBS, 'traffic': None,
           'kernel': 'chr::trace_kernel (BVH walk of the one-step launches)',
-          'basis': basis,
-          'alg_bytes_per_launch': alg_per_launch,
-          'alg_bytes_per_walk': per_walk,
-          'rays_per_launch': rays_per_launch,
-          'avg_launch_ms': 1e3 * avg_launch_s,
-          'launches_timed': live['trace_launches']}
-    if own is not None:
-        rl['own_layout_bytes_per_walk'] = own
-        rl['own_layout_achieved'] = rays_per_launch * own / avg_launch_s / 1e9 if avg_launch_s > 0 else 0.0
-        rl['nodes_per_photon'] = cst.nodes_visited / n
-        rl['triangles_per_photon'] = cst.triangles_tested / n
-        rl['traversals_per_photon'] = cst.traversals / n
-        rl['simd_efficiency_nodes'] = cst.nodes_visited / max(1.0, 64.0 * cst.wave_node_steps)
-        rl['simd_efficiency_triangles'] = cst.triangles_tested / max(1.0, 64.0 * cst.wave_triangle_steps)
-    if ref is not None:
-        rl['reference_bvh_nodes_per_walk'] = ref['nodes_visited'] / ref['traversals']
-        rl['reference_bvh_triangles_per_walk'] = ref['tris_tested'] / ref['traversals']
-    # HBM bytes per launch from the PMC passes (tools/rocprof_bench.sh) of this same workload
+          'basis': 'SURVEY 8(d): 16 B x reference-BVH nodes + 48 B x triangles + 4 B per walk '
+                   '(oracle, reference DFS order, on the cpu_baseline sample)',
+          'alg_bytes_per_launch': alg_per_launch, 'alg_bytes_per_walk': per_walk,
+          'rays_per_launch': rays_per_launch, 'avg_launch_ms': 1e3 * avg_launch_s,
+          'launches_timed': trace_launches,
+          'launch_ms_min': float(lm.min()) if lm.size else None,
+          'launch_ms_median': float(np.median(lm)) if lm.size else None,
+          'launch_ms_max': float(lm.max()) if lm.size else None,
+          'reference_bvh_nodes_per_walk': ref['nodes_visited'] / ref['traversals'],
+          'reference_bvh_triangles_per_walk': ref['tris_tested'] / ref['traversals']}
     pmc_path = os.path.join(ROOT, 'profiles', 'latest_pmc.json')
     if os.path.exists(pmc_path):
         with open(pmc_path) as f:
@@ -182,7 +296,8 @@ def roofline(args, live, cst, ref, n):
                 and pmc.get('kernel') == 'chr::trace_kernel' and 'hbm_bytes_per_launch' in pmc:
             rl['traffic'] = pmc['hbm_bytes_per_launch']
             rl['traffic_unit'] = 'bytes/launch (FETCH_SIZE x2 + WRITE_SIZE)'
-            rl['traffic_source'] = pmc.get('source')
+            rl['traffic_source'] = 'copied, not measured in this run: %s (%s)' % (
+                os.path.relpath(pmc_path, ROOT), pmc.get('source'))
     return rl
 
 
@@ -198,7 +313,7 @@ def main():
     ap.add_argument('--max-blocks', type=int, default=1024)
     ap.add_argument('--seed', type=int, default=1)
     ap.add_argument('--cpu-budget', type=float, default=20.0, help='seconds of CPU-baseline work')
-    ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--no-cpu-baseline', action='store_true', help='also skips the parity check')
     ap.add_argument('--no-count', action='store_true',
                     help='skip the untimed counting pass (profiling runs: keeps rocprof averages to one variant)')
     ap.add_argument('--cache-dir', default=os.environ.get('CHROMA_BENCH_CACHE', '/tmp/chroma_bench_cache'))
@@ -220,23 +335,14 @@ def main():
     from chroma.photon_source import isotropic
     from types import SimpleNamespace
 
-    if dist is not None and args.cache_dir:
-        # rank 0 builds (flatten + BVH, minutes for the 29k detector) and fills the
-        # local cache; the other ranks of the node wait, then load it
-        if rank == 0:
-            det = build_geometry(args.detector, args.cache_dir)
-        dist.barrier()
-        if rank != 0:
-            det = build_geometry(args.detector, args.cache_dir)
-    else:
-        det = build_geometry(args.detector, args.cache_dir)
+    det = shared_geometry(args.detector, args.cache_dir, rank, dist)
     t0 = time.time()
     gdet = gpu.GPUDetector(det)
     log('rank %d: geometry on device in %.1fs (%.2f GB)' % (rank, time.time() - t0, gdet.device_bytes() / 1e9))
     nslots = args.nthreads_per_block * args.max_blocks
-    rng = gpu.get_rng_states(nslots, seed=args.seed, first_subsequence=rank * nslots)
+    rng = gpu.get_rng_states(nslots, seed=args.seed, first_subsequence=rng_first_subsequence(rank, nslots))
 
-    photons = isotropic(args.photons, seed=20260102 + rank)
+    photons = isotropic(args.photons, seed=PHOTON_SEED + rank)
     pristine = SimpleNamespace(
         pos=ga.to_gpu(gpu.to_float3(photons.pos)), dir=ga.to_gpu(gpu.to_float3(photons.dir)),
         pol=ga.to_gpu(gpu.to_float3(photons.pol)), wavelengths=ga.to_gpu(photons.wavelengths),
@@ -261,41 +367,27 @@ def main():
                      gdet.solid_id_map.gpudata, gdet.solid_id_to_channel_index_gpu.gpudata, counts.gpudata,
                      gdet.nchannels, current_stream())
         reduced['counts'] = shard.allreduce_channel_counts(counts.tensor)
-        return gp
+        reduced['gp'] = gp
+        return gp.last_stats
 
-    for _ in range(args.warmup):
-        gp = step()
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    live = dict(kernel_ms=0.0, launches=0, host_steps=0, trace_ms=0.0, trace_launches=0, trace_rays=0)
-    for _ in range(args.steps):
-        gp = step()
-        ls = gp.last_stats
-        live['kernel_ms'] += ls.kernel_ms
-        live['launches'] += ls.launches
-        live['host_steps'] += ls.steps_run
-        live['trace_ms'] += ls.trace_ms
-        live['trace_launches'] += ls.trace_launches
-        live['trace_rays'] += ls.trace_rays
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if dist:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device='cuda')
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
+    elapsed, per_step, stats = timed_loop(step, args.steps, args.warmup, dist, torch.cuda.synchronize)
+    gp = reduced.pop('gp')
     detected = int(((gp.flags.get() & 4) != 0).sum())
+    del gp
     channel_hits = int(reduced['counts'].sum().item())     # all ranks, detected with a channel
-    # untimed: same propagate with the counting kernel variant -> algorithmic bytes
+    launch_ms = [s.trace_launch_ms[i] for s in stats for i in range(s.trace_ms_n)]
+    live = dict(kernel_ms=sum(s.kernel_ms for s in stats), launches=sum(s.launches for s in stats),
+                host_steps=sum(s.steps_run for s in stats), trace_ms=sum(s.trace_ms for s in stats),
+                trace_launches=sum(s.trace_launches for s in stats), trace_rays=sum(s.trace_rays for s in stats),
+                overflows=sum(s.stack_overflows for s in stats), flat=sum(s.flat_walks for s in stats),
+                flat_whole=sum(s.flat_walks_whole for s in stats))
+    # untimed: same propagate with the counting kernel variant -> own-layout bytes and SIMD efficiency
     cst = None
     if not args.no_count:
         prev = os.environ.get('CHR_PROPAGATE_VARIANT')
         os.environ['CHR_PROPAGATE_VARIANT'] = '5'
-        cst = step().last_stats
+        cst = step()
+        reduced.pop('gp', None)
         if prev is None:
             del os.environ['CHR_PROPAGATE_VARIANT']
         else:
@@ -303,41 +395,50 @@ def main():
         torch.cuda.synchronize()
 
     if rank == 0:
-        total = args.photons * world * args.steps
-        value = total / elapsed
-        result = {
-            'metric': METRIC, 'value': value, 'unit': 'photons/s', 'n_gpus': world, 'steps': args.steps,
-            'warmup': args.warmup, 'ms_per_step': 1e3 * elapsed / args.steps, 'higher_is_better': True,
-            'scaling': 'weak', 'vs_baseline': (value / 2.5e6) if args.detector == '29k' else None,
-            'dtype': 'f32', 'data': 'synthetic isotropic point source (BASELINE.md section 3), seed 20260102+rank',
-            'config': {'workload': 'GPUPhotons.propagate of %d isotropic photons per GPU per step on %s, '
-                                   'max_steps=%d, launch shape %dx%d (524,288 RNG slots)' % (
-                                       args.photons, DETECTORS[args.detector][0], args.max_steps,
-                                       args.nthreads_per_block, args.max_blocks),
-                       'detector': args.detector, 'photons_per_gpu': args.photons, 'max_steps': args.max_steps, 'triangles': len(det.mesh.triangles),
-                       'bvh_nodes': len(det.bvh.nodes), 'channels': det.num_channels(),
-                       'parallelism': 'photon-sharded x%d, geometry replicated' % world},
-            'detail': {'kernel_ms_per_step': live['kernel_ms'] / args.steps,
-                       'trace_ms_per_step': live['trace_ms'] / args.steps,
-                       'launches_per_step': live['launches'] / args.steps,
-                       'host_steps_per_propagate': live['host_steps'] / args.steps,
-                       'detected_fraction': detected / args.photons,
-                       'channel_hits_all_ranks': channel_hits},
-            'roofline': None, 'cpu_baseline': None,
-        }
-        n = float(args.photons)
-        ostats = None
+        props = torch.cuda.get_device_properties(local)
+        free_b, total_b = torch.cuda.mem_get_info(local)
+        steps = max(1, args.steps)
+        detail = {'kernel_ms_per_step': live['kernel_ms'] / steps,
+                  'trace_ms_per_step': live['trace_ms'] / steps,
+                  'launches_per_step': live['launches'] / steps,
+                  'host_steps_per_propagate': live['host_steps'] / steps,
+                  'stack_overflows': int(live['overflows']),
+                  'flat_walks_decomposed': int(live['flat']), 'flat_walks_whole': int(live['flat_whole']),
+                  'detected_fraction': detected / args.photons,
+                  'channel_hits_all_ranks': channel_hits,
+                  'device': {'name': props.name, 'arch': getattr(props, 'gcnArchName', ''),
+                             'compute_units': props.multi_processor_count,
+                             'hbm_total_gb': total_b / 1e9, 'hbm_free_gb_after': free_b / 1e9},
+                  'kernels': _kernel_info(_native)}
+        if cst is not None and cst.traversals:
+            detail['own_layout'] = {
+                'bytes_per_walk': (96.0 * cst.nodes_visited + 64.0 * cst.triangles_tested + 52.0 * cst.traversals)
+                / cst.traversals,
+                'nodes_per_photon': cst.nodes_visited / args.photons,
+                'triangles_per_photon': cst.triangles_tested / args.photons,
+                'traversals_per_photon': cst.traversals / args.photons,
+                'simd_efficiency_nodes': cst.nodes_visited / max(1.0, 64.0 * cst.wave_node_steps),
+                'simd_efficiency_triangles': cst.triangles_tested / max(1.0, 64.0 * cst.wave_triangle_steps),
+                'stack_overflows': int(cst.stack_overflows)}
+        info = {'triangles': len(det.mesh.triangles), 'bvh_nodes': len(det.bvh.nodes),
+                'channels': det.num_channels()}
+        result = result_line(args, world, elapsed, per_step, info, detail)
         if not args.no_cpu_baseline and world == 1:
-            threads = min(16, len(os.sched_getaffinity(0)))
-            cpu, b_ref, ostats, nsample = cpu_baseline(PackedGeometry(det), photons, nslots, args.nthreads_per_block,
-                                                   args.max_blocks, args.max_steps, args.seed, args.cpu_budget,
-                                                   threads)
+            threads = usable_cpus()
+            packed = PackedGeometry(det)
+            cpu, b_ref, ostats, nsample, host = cpu_baseline(packed, photons, nslots, args.nthreads_per_block,
+                                                             args.max_blocks, args.max_steps, args.seed,
+                                                             args.cpu_budget, threads)
             result['cpu_baseline'] = cpu
-            result['detail']['reference_bvh_nodes_per_photon'] = ostats['nodes_visited'] / nsample
-            result['detail']['reference_bvh_triangles_per_photon'] = ostats['tris_tested'] / nsample
-            result['detail']['bytes_per_photon_alg_8d'] = b_ref
-        if live['trace_launches']:
-            result['roofline'] = roofline(args, live, cst, ostats, n)
+            detail['reference_bvh_nodes_per_photon'] = ostats['nodes_visited'] / nsample
+            detail['reference_bvh_triangles_per_photon'] = ostats['tris_tested'] / nsample
+            detail['bytes_per_photon_alg_8d'] = b_ref
+            result['parity'] = gpu_parity(gdet, photons, nsample, host, args,
+                                          np.asarray(det.solid_id, np.int64),
+                                          np.asarray(det.solid_id_to_channel_index, np.int64))
+            if live['trace_launches']:
+                result['roofline'] = roofline(args, live['trace_ms'], live['trace_launches'], live['trace_rays'],
+                                              ostats, launch_ms)
         print(json.dumps(result), flush=True)
     if dist:
         dist.destroy_process_group()

@@ -66,7 +66,14 @@ class PropagateStats(ctypes.Structure):
                 ('kernel_ms', ctypes.c_double), ('nodes_visited', c_u64), ('triangles_tested', c_u64),
                 ('traversals', c_u64), ('wave_node_steps', c_u64), ('wave_triangle_steps', c_u64),
                 ('wave_fill_cycles', c_u64), ('wave_step_cycles', c_u64), ('trace_ms', ctypes.c_double),
-                ('trace_launches', c_u32), ('reserved', c_u32), ('trace_rays', c_u64)]
+                ('trace_launches', c_u32), ('reserved', c_u32), ('trace_rays', c_u64),
+                ('trace_ms_n', c_u32), ('trace_launch_ms', c_f32 * 32), ('flat_walks', c_u32),
+                ('flat_walks_whole', c_u32)]
+
+
+class KernelAttr(ctypes.Structure):
+    _fields_ = [('private_bytes', c_u64), ('lds_bytes', c_u64), ('vgprs', ctypes.c_int32),
+                ('max_threads', ctypes.c_int32), ('name', ctypes.c_char * 96)]
 
 
 _SIGNATURES = {
@@ -88,6 +95,10 @@ _SIGNATURES = {
                                       c_vp]),
     'chr_photon_duplicate': (c_i32, [ctypes.POINTER(PhotonsDesc), c_i32, c_i32, c_i32, c_i32, c_vp]),
     'chr_distance_to_mesh': (c_i32, [c_vp, c_u32, c_vp, c_vp, c_vp, c_vp]),
+    'chr_kernel_info': (c_i32, [c_i32, ctypes.POINTER(KernelAttr)]),
+    'chr_selftest_linalg': (c_i32, [c_i32, c_u32, c_vp, c_vp, c_f32, c_vp, c_vp]),
+    'chr_selftest_rotate': (c_i32, [c_u32, c_vp, c_vp, c_f32, c_f32, c_f32, c_vp, c_vp]),
+    'chr_selftest_sample_cdf': (c_i32, [c_u32, c_vp, c_u32, c_i32, c_vp, c_vp, c_f32, c_f32, c_i32, c_vp, c_vp]),
     'chr_bvh_build_grid': (c_i32, [c_vp, c_u32, c_vp, c_u32, c_i32, ctypes.POINTER(c_vp)]),
     'chr_bvh_result_info': (c_i32, [c_vp, ctypes.POINTER(c_u32), ctypes.POINTER(c_u32), c_vp,
                                     ctypes.POINTER(c_f32)]),
@@ -157,3 +168,15 @@ def check(rc, what=''):
 
 def call(name, *args):
     return check(getattr(lib(), name)(*args), name)
+
+
+def kernel_info():
+    """Code-object resources of the default propagate kernels (chr_kernel_info):
+    list of dicts {name, private_bytes, lds_bytes, vgprs, max_threads}."""
+    out = []
+    for which in range(4):
+        a = KernelAttr()
+        call('chr_kernel_info', which, ctypes.byref(a))
+        out.append(dict(name=a.name.decode(), private_bytes=int(a.private_bytes), lds_bytes=int(a.lds_bytes),
+                        vgprs=int(a.vgprs), max_threads=int(a.max_threads)))
+    return out

@@ -175,12 +175,18 @@ class ShardedSimulation(Simulation):
         from chroma.gpu import shard
         self.group = group
         self.rank, self.world = shard.dist_info(group)
+        # bind this rank's GPU before any collective: RCCL stages on the current
+        # device, which is cuda:0 on every rank unless set (all ranks would collide)
+        if torch.cuda.is_available():
+            torch.cuda.set_device(shard.local_device())
         if seed is None:
             seed = pick_seed()
-            if self.world > 1:      # one seed for the job
-                box = [seed]
-                dist.broadcast_object_list(box, src=0, group=group)
-                seed = box[0]
+            if self.world > 1:      # one seed for the job, as a tensor on the backend's device
+                on_gpu = torch.cuda.is_available() and dist.get_backend(group) != 'gloo'
+                box = torch.tensor([seed], dtype=torch.int64,
+                                   device=torch.device('cuda', shard.local_device()) if on_gpu else 'cpu')
+                dist.broadcast(box, src=0, group=group)
+                seed = int(box.item())
         Simulation.__init__(self, detector, seed=seed, cuda_device=shard.local_device(),
                             nthreads_per_block=nthreads_per_block, max_blocks=max_blocks)
         nslots = self.nthreads_per_block * self.max_blocks

@@ -57,6 +57,9 @@ struct DevGeom {
     const chr_wireplane_desc *wireplanes;
     const uint4 *wnodes;             // 8-wide SAH BVH, node i at wnodes[wstride * i] (wide_bvh.h)
     const float4 *wtri;              // 3 float4 per leaf triangle record (wide_bvh.h)
+    const uint2 *wcut;               // sub-walk items (node, child mask) of a decomposed walk (wide_bvh.h)
+    const uint32_t *wrank_id;        // reference DFS rank -> triangle id
+    uint32_t nwcut;
     uint32_t nwnodes, nwtri;
     uint32_t wstride;                // uint4 per node slot: 8 (96-byte node padded to one 128-byte line) or 6
     float ox, oy, oz, scale;         // world_origin, world_scale
@@ -74,7 +77,7 @@ struct chr_geometry {
     void *d_dev;          // a device copy of dev: kernels take `const DevGeom *` (uniform scalar loads)
     int device;
     uint64_t bytes;
-    void *allocs[12];
+    void *allocs[16];
     int nallocs;
     const uint4 *wnodes_alt;   // the other node layout (only with CHR_NODE_LAYOUT_AB set at creation; A/B tooling)
     uint32_t wstride_alt;

@@ -12,6 +12,8 @@
 
 namespace chr {
 
+constexpr float PI_F = 3.141592653589793f;   // physical_constants.h
+
 struct V3 {
     float x, y, z;
 };
@@ -22,6 +24,19 @@ __device__ __forceinline__ V3 operator-(V3 a, V3 b) { return v3(a.x - b.x, a.y -
 __device__ __forceinline__ V3 operator-(V3 a) { return v3(-a.x, -a.y, -a.z); }
 __device__ __forceinline__ V3 operator*(V3 a, float c) { return v3(a.x * c, a.y * c, a.z * c); }
 __device__ __forceinline__ V3 operator/(V3 a, float c) { return v3(a.x / c, a.y / c, a.z / c); }
+// the rest of linalg.h's float3/float operators (self-test kernels, selftest.hip)
+__device__ __forceinline__ V3 operator*(float c, V3 a) { return v3(c * a.x, c * a.y, c * a.z); }
+__device__ __forceinline__ V3 operator/(float c, V3 a) { return v3(c / a.x, c / a.y, c / a.z); }
+__device__ __forceinline__ V3 operator+(V3 a, float c) { return v3(a.x + c, a.y + c, a.z + c); }
+__device__ __forceinline__ V3 operator+(float c, V3 a) { return v3(c + a.x, c + a.y, c + a.z); }
+__device__ __forceinline__ V3 operator-(V3 a, float c) { return v3(a.x - c, a.y - c, a.z - c); }
+__device__ __forceinline__ V3 operator-(float c, V3 a) { return v3(c - a.x, c - a.y, c - a.z); }
+__device__ __forceinline__ V3 &operator+=(V3 &a, V3 b) { a = a + b; return a; }
+__device__ __forceinline__ V3 &operator-=(V3 &a, V3 b) { a = a - b; return a; }
+__device__ __forceinline__ V3 &operator+=(V3 &a, float c) { a = a + c; return a; }
+__device__ __forceinline__ V3 &operator-=(V3 &a, float c) { a = a - c; return a; }
+__device__ __forceinline__ V3 &operator*=(V3 &a, float c) { a = a * c; return a; }
+__device__ __forceinline__ V3 &operator/=(V3 &a, float c) { a = a / c; return a; }
 
 __device__ __forceinline__ float dot(V3 a, V3 b) { return __builtin_fmaf(a.z, b.z, __builtin_fmaf(a.y, b.y, a.x * b.x)); }
 __device__ __forceinline__ V3 cross(V3 a, V3 b) {

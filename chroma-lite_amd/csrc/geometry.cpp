@@ -42,6 +42,8 @@ struct Blob {
 int dev_upload(chr_geometry *g, const void *host, size_t bytes, void **dptr) {
     void *p = nullptr;
     if (bytes == 0) bytes = 16;
+    if (g->nallocs >= (int)(sizeof(g->allocs) / sizeof(g->allocs[0])))
+        return chr::fail(CHR_ERR_INVALID, "chr_geometry_create: too many device allocations");
     hipError_t e = hipMalloc(&p, bytes);
     if (e != hipSuccess) return chr::fail(CHR_ERR_NOMEM, "hipMalloc(%zu) failed: %s", bytes, hipGetErrorString(e));
     g->allocs[g->nallocs++] = p;
@@ -160,6 +162,11 @@ extern "C" int chr_geometry_create(const chr_geometry_desc *d, chr_geometry **ou
                 dg.wtri = (const float4 *)p;
                 dg.nwnodes = (uint32_t)wb.nodes.size();
                 dg.nwtri = (uint32_t)wb.tri.size();
+                if ((rc = dev_upload(g, wb.cut.data(), wb.cut.size() * 4, &p))) throw rc;
+                dg.wcut = (const uint2 *)p;
+                dg.nwcut = (uint32_t)(wb.cut.size() / 2);
+                if ((rc = dev_upload(g, wb.rank_id.data(), wb.rank_id.size() * 4, &p))) throw rc;
+                dg.wrank_id = (const uint32_t *)p;
             }
         }
 

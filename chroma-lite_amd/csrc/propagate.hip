@@ -32,6 +32,7 @@
 #include "common.h"
 #include "device_geometry.h"
 #include "device_math.h"
+#include "sampling.h"
 #include "wide_bvh.h"
 
 namespace chr {
@@ -42,7 +43,6 @@ constexpr int STACK_LDS = 24;      // entries kept in LDS per work-item
 constexpr uint32_t DEAD_MASK = CHR_NO_HIT | CHR_BULK_ABSORB | CHR_SURFACE_DETECT | CHR_SURFACE_ABSORB | CHR_NAN_ABORT;
 constexpr float WEIGHT_LOWER_THRESHOLD = 0.0001f;
 constexpr float SPEED_OF_LIGHT = 299.792458f;
-constexpr float PI_F = 3.141592653589793f;
 // float thresholds equivalent to the reference's float-vs-double compares
 // (intersect.h:259-267): (double)u < -1e-6, (double)u > 1+1e-6, (double)t > 1e-6
 constexpr float T_NEG_EPS = -9.99999997e-07f;
@@ -117,39 +117,6 @@ __device__ __forceinline__ float interp_property(const DevGeom &g, float x, cons
     const float base = __builtin_fmaf((float)jl, step, start);
     const float f0 = gld(fp + jl), f1 = gld(fp + jl + 1);
     return f0 + ((x - base) * (f1 - f0)) / step;
-}
-
-__device__ float interp_idx(float x, int n, const float *xp) {
-    int lower = 0, upper = n - 1;
-    if (x <= xp[lower]) return (float)lower;
-    if (x >= xp[upper]) return (float)upper;
-    while (lower < upper - 1) {
-        int half = (lower + upper) / 2;
-        if (x < xp[half]) upper = half; else lower = half;
-    }
-    float dx = xp[upper] - xp[lower];
-    return (float)((double)lower + (double)(x - xp[lower]) / (double)dx);
-}
-
-// ---------------------------------------------------------------- random.h
-__device__ __forceinline__ V3 uniform_sphere(chr_xorwow &s) {
-    const float theta = chr_uniform(&s, 0.0f, 2 * PI_F);
-    const float u = chr_uniform(&s, -1.0f, 1.0f);
-    const float c = chr_sqrtf(__builtin_fmaf(-u, u, 1.0f));
-    float st, ct;
-    chr_sincosf(theta, &st, &ct);
-    return v3(c * ct, c * st, u);
-}
-
-__device__ float sample_cdf(chr_xorwow &rng, int ncdf, float x0, float delta, const float *cdf_y) {
-    const float u = chr_uniform01(&rng);
-    int lower = 0, upper = ncdf - 1;
-    while (lower < upper - 1) {
-        int half = (lower + upper) / 2;
-        if (u < cdf_y[half]) upper = half; else lower = half;
-    }
-    const float dcy = cdf_y[upper] - cdf_y[lower];
-    return __builtin_fmaf(delta, (float)lower, x0) + (delta * (u - cdf_y[lower])) / dcy;
 }
 
 // ---------------------------------------------------------------- intersect.h / mesh.h
@@ -289,7 +256,8 @@ constexpr int lds_words(int wide) {
 struct WStack {
     CHR_LDS uint32_t *node;   // this work-item's LDS column: entry i at node[i * BLOCK]
     CHR_LDS float *dist;
-    uint2 *spill;             // entries >= WIDE_LDS (scratch)
+    uint2 *spill;             // entries >= SL: private array (sstride 1) or a lane-strided HBM column
+    uint32_t sstride;         // uint2 between consecutive spill entries of this work-item
     CHR_LDS uint32_t *leafq;  // parked leaves (speculative walk): entry i at leafq[i * BLOCK]
     CHR_LDS uint32_t *group;  // group walk: the group's shared stack, entry i = (node, entry distance) at [2i, 2i+1]
 };
@@ -297,12 +265,12 @@ struct WStack {
 template <int SL = WIDE_LDS>
 __device__ __forceinline__ void wpush(WStack &s, int i, uint32_t n, float t) {
     if (i < SL) { s.node[i * BLOCK] = n; s.dist[i * BLOCK] = t; }
-    else s.spill[i - SL] = make_uint2(n, __float_as_uint(t));
+    else s.spill[(size_t)(i - SL) * s.sstride] = make_uint2(n, __float_as_uint(t));
 }
 template <int SL = WIDE_LDS>
 __device__ __forceinline__ void wpop(const WStack &s, int i, uint32_t &n, float &t) {
     if (i < SL) { n = s.node[i * BLOCK]; t = s.dist[i * BLOCK]; }
-    else { const uint2 e = s.spill[i - SL]; n = e.x; t = __uint_as_float(e.y); }
+    else { const uint2 e = s.spill[(size_t)(i - SL) * s.sstride]; n = e.x; t = __uint_as_float(e.y); }
 }
 
 __device__ __forceinline__ float byte_f(uint32_t lo4, uint32_t hi4, int k) {   // byte k of (hi4:lo4) as float
@@ -335,6 +303,22 @@ __device__ __forceinline__ RaySlab make_slab(V3 noid, V3 inv) {
     return r;
 }
 
+// What a queued photon's walk is: 0 none (NaN state: the step aborts it,
+// propagate.cu:307-310), 1 an ordinary walk, 2 a FLAT walk -- a direction
+// component whose reciprocal is not finite (+-0 or denormal).  The reference's
+// slab test skips such an axis (intersect.h:121-144), so every box is tested
+// in 2D (or 1D) and the walk visits every box the ray's projection crosses
+// before the nearest hit: tens of millions of node and triangle fetches on the
+// 29k-PMT detector (one such ray made one trace launch last 19 s, round 2).
+// Flat walks are split into independent sub-walks (wide_bvh.h cut items) that
+// the whole persistent grid shares.  d must be the normalised direction.
+__device__ __forceinline__ int walk_kind(V3 o, V3 d) {
+    const float prod = ((((d.x * d.y) * d.z) * o.x) * o.y) * o.z;
+    if (chr_isnan(prod)) return 0;
+    const float ix = 1.0f / d.x, iy = 1.0f / d.y, iz = 1.0f / d.z;
+    return (chr_isfinite(ix) && chr_isfinite(iy) && chr_isfinite(iz)) ? 1 : 2;
+}
+
 // Slab-test the up-to-8 children of one wide node.  Returns the leaf children
 // hit (bit mask), leaves the nearest hit inner child in near_node/near_t and
 // pushes the other hit inner children.  Boxes entered beyond `best` are culled
@@ -343,7 +327,7 @@ template <int SL = WIDE_LDS>
 __device__ __forceinline__ uint32_t expand_node(const uint4 h, const uint4 a1, const uint4 a2, const uint4 a3,
                                                 const uint4 a4, const uint4 a5, const RaySlab &r, float best,
                                                 uint32_t &near_node, float &near_t, WStack &st, int &sp,
-                                                uint32_t &overflow) {
+                                                uint32_t &overflow, uint32_t cmask = 0xFFu) {
     const V3 org = v3(__uint_as_float(h.x), __uint_as_float(h.y), __uint_as_float(h.z));
     const float sx = exp_scale(h.w), sy = exp_scale(h.w >> 8), sz = exp_scale(h.w >> 16);
     // byte arrays: x lo = a1.xy, y lo = a1.zw, z lo = a2.xy, x hi = a2.zw, y hi = a3.xy, z hi = a3.zw
@@ -359,7 +343,7 @@ __device__ __forceinline__ uint32_t expand_node(const uint4 h, const uint4 a1, c
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
         const uint32_t kind = ((k < 4 ? a4.z : a4.w) >> (8 * (k & 3))) & 0xFFu;
-        if (kind == 0) continue;
+        if (kind == 0 || !((cmask >> k) & 1u)) continue;
         const float tnx = __builtin_fmaf(__builtin_fmaf(byte_f(nx0, nx1, k), sx, org.x), r.inx, r.onx);
         const float tfx = __builtin_fmaf(__builtin_fmaf(byte_f(fx0, fx1, k), sx, org.x), r.inx, r.ofx);
         const float tny = __builtin_fmaf(__builtin_fmaf(byte_f(ny0, ny1, k), sy, org.y), r.iny, r.ony);
@@ -386,6 +370,7 @@ struct WalkCounts {   // filled only by the counting variant (bench: algorithmic
     uint32_t nodes, tris, walks;
     uint32_t wave_nodes, wave_tris;   // steps the whole wave executed (counted by its first active lane)
     unsigned long long wave_fill_cycles, wave_other_cycles;   // s_memtime spent in fill_state / rest of the step loop
+    uint32_t flat;                    // flat walks (walk_kind 2) walked whole (group walk; always counted)
 };
 __device__ __forceinline__ bool wave_leader() {
     const unsigned long long m = __ballot(1);
@@ -611,7 +596,7 @@ __device__ __forceinline__ uint32_t byte_of(uint32_t lo4, uint32_t hi4, int k) {
 }
 template <int G>
 __device__ int intersect_group(const DevGeom &g, V3 o, V3 d, float &min_distance, int last_hit,
-                               CHR_LDS uint32_t *stk, uint32_t &overflow) {
+                               CHR_LDS uint32_t *stk, uint32_t &overflow, WalkCounts &cnt) {
     static_assert(G == 2 || G == 4 || G == 8, "group size divides 8");
     constexpr int C = 8 / G;                       // children per lane: k = sub + G * c
     constexpr uint32_t INVALID = 0xFFFFFFFFu;
@@ -621,6 +606,7 @@ __device__ int intersect_group(const DevGeom &g, V3 o, V3 d, float &min_distance
     const V3 noid = v3(-o.x / d.x, -o.y / d.y, -o.z / d.z);
     const V3 inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
     const RaySlab r = make_slab(noid, inv);
+    if (!(chr_isfinite(inv.x) && chr_isfinite(inv.y) && chr_isfinite(inv.z))) cnt.flat++;   // walk_kind 2
     float best = __builtin_inff();
     uint32_t best_rank = 0xFFFFFFFFu;
     int best_id = -1;
@@ -915,7 +901,8 @@ __device__ __forceinline__ void fill_state(const DevGeom &g, State &s, Photon &p
                                            uint32_t &overflow, WalkCounts &cnt) {
     int mesh_triangle;
     if constexpr (WIDE >= GROUP_MODE && WIDE < GROUP_MODE + 16) {   // group walk, G = WIDE - GROUP_MODE
-        mesh_triangle = intersect_group<WIDE - GROUP_MODE>(g, p.pos, p.dir, s.distance, p.last_hit, wst.group, overflow);
+        mesh_triangle =
+            intersect_group<WIDE - GROUP_MODE>(g, p.pos, p.dir, s.distance, p.last_hit, wst.group, overflow, cnt);
     } else if constexpr (WIDE >= 2000)   // speculative walk, triangle-step threshold (WIDE - 2000)/8 of live lanes
         mesh_triangle =
             intersect_wide_spec<COUNT, WIDE - 2000>(g, p.pos, p.dir, s.distance, p.last_hit, wst, overflow, cnt);
@@ -1364,7 +1351,13 @@ struct PropagateArgs {
     uint32_t *counters;                // [0]: stack overflows
     const uint32_t *order;             // coherence order: work-item t runs slot order[t] (nullptr: t)
     const int2 *hits;                  // shade_kernel: walk result per queue position (trace_kernel)
+    const unsigned long long *flat_best;   // shade_kernel: results of the flat walks (FLAT_HIT entries of hits)
+    uint32_t *zero_word;               // shade_kernel: word cleared once (next step's flat-walk count)
+    uint32_t *diag;                    // multi-step kernels: [0] += flat walks walked whole (nullptr: off)
 };
+// hits[q] = (FLAT_HIT, f): queue position q holds flat walk f of this step,
+// its result is flat_best[f] (trace_kernel)
+constexpr int FLAT_HIT = -3;
 
 __device__ __forceinline__ V3 load3(const float *p, uint32_t i) { return v3(p[3 * i], p[3 * i + 1], p[3 * i + 2]); }
 __device__ __forceinline__ void store3(float *p, uint32_t i, V3 v) { p[3 * i] = v.x; p[3 * i + 1] = v.y; p[3 * i + 2] = v.z; }
@@ -1482,12 +1475,13 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_kernel(const DevGeom *_
             st.lds = (CHR_LDS uint32_t *)(lds_stack + threadIdx.x);
             uint2 wspill[WIDE_STACK - WIDE_LDS];
             wst.spill = wspill;
+            wst.sstride = 1;
             wst.node = (CHR_LDS uint32_t *)(lds_stack + threadIdx.x);
             wst.dist = (CHR_LDS float *)(lds_stack + WIDE_LDS * BLOCK + threadIdx.x);
     wst.leafq = (CHR_LDS uint32_t *)(lds_stack + 2 * WIDE_LDS * BLOCK + threadIdx.x);
             wst.leafq = (CHR_LDS uint32_t *)(lds_stack + 2 * WIDE_LDS * BLOCK + threadIdx.x);
             uint32_t overflow = 0;
-            WalkCounts cnt{0u, 0u, 0u, 0u, 0u, 0ull, 0ull};
+            WalkCounts cnt{0u, 0u, 0u, 0u, 0u, 0ull, 0ull, 0u};
             const DevGeom &g = *gdev;   // device-resident: uniform s_loads, no private copy
             alive = run_photon<BATCH, WIDE, COUNT>(g, a, photon_id, history, rng, st, wst, overflow, cnt);
             store_rng(a, (uint32_t)id, rng);
@@ -1527,11 +1521,12 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_step_kernel(const DevGe
     st.lds = (CHR_LDS uint32_t *)(lds_stack + threadIdx.x);
     uint2 wspill[WIDE_STACK - WIDE_LDS];
     wst.spill = wspill;
+    wst.sstride = 1;
     wst.node = (CHR_LDS uint32_t *)(lds_stack + threadIdx.x);
     wst.dist = (CHR_LDS float *)(lds_stack + WIDE_LDS * BLOCK + threadIdx.x);
     wst.leafq = (CHR_LDS uint32_t *)(lds_stack + 2 * WIDE_LDS * BLOCK + threadIdx.x);
     uint32_t overflow = 0;
-    WalkCounts cnt{0u, 0u, 0u, 0u, 0u, 0ull, 0ull};
+    WalkCounts cnt{0u, 0u, 0u, 0u, 0u, 0ull, 0ull, 0u};
     const DevGeom &g = *gdev;
     chr_xorwow rng;
     bool have_rng = false;
@@ -1583,6 +1578,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void shade_kernel(const DevGeom *__res
                                                             uint32_t cap) {
     const uint32_t slot = blockIdx.x * BLOCK + threadIdx.x;
     const uint32_t n = (uint32_t)a.nthreads;
+    if (slot == 0 && a.zero_word) *a.zero_word = 0u;
     if (slot >= cap || (slot & ~63u) >= n) return;   // whole waves (cap % 64 == 0)
     const DevGeom &g = *gdev;
     chr_xorwow rng;
@@ -1610,8 +1606,14 @@ __global__ __launch_bounds__(BLOCK, MINW) void shade_kernel(const DevGeom *__res
                 p.history |= CHR_NO_HIT | CHR_NAN_ABORT;
             } else {
                 State s;
+                int tri = cur.hit.x;
                 s.distance = __int_as_float(cur.hit.y);
-                finish_fill(g, s, p, cur.hit.x);
+                if (tri == FLAT_HIT) {            // (distance bits, reference rank) of a decomposed walk
+                    const unsigned long long key = a.flat_best[cur.hit.y];
+                    tri = key == ~0ull ? -1 : (int)g.wrank_id[(uint32_t)key];
+                    s.distance = key == ~0ull ? -1.0f : __uint_as_float((uint32_t)(key >> 32));
+                }
+                finish_fill(g, s, p, tri);
                 if (p.last_hit != -1) {
                     int command = propagate_to_boundary(g, p, s, rng, a.use_weights, a.scatter_first);
                     if (command == PASS && s.surface_index != -1)
@@ -1653,10 +1655,10 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_group_kernel(const DevG
     Stack st;
     st.lds = nullptr;
     WStack wst;
-    wst.node = nullptr; wst.dist = nullptr; wst.spill = nullptr; wst.leafq = nullptr;
+    wst.node = nullptr; wst.dist = nullptr; wst.spill = nullptr; wst.sstride = 1; wst.leafq = nullptr;
     wst.group = (CHR_LDS uint32_t *)group_stacks + (threadIdx.x / G) * GROUP_STACK * 2;
     uint32_t overflow = 0;
-    WalkCounts cnt{0u, 0u, 0u, 0u, 0u, 0ull, 0ull};
+    WalkCounts cnt{0u, 0u, 0u, 0u, 0u, 0ull, 0ull, 0u};
     const DevGeom &g = *gdev;
     chr_xorwow rng;
     bool have_rng = false;
@@ -1670,6 +1672,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_group_kernel(const DevG
     }
     if (have_rng && sub == 0) store_rng(a, slot, rng);
     if (sub == 0 && overflow) atomicAdd(a.counters, overflow);
+    if (sub == 0 && cnt.flat && a.diag) atomicAdd(a.diag, cnt.flat);
 }
 
 // ---------------------------------------------------------------- ray binning (trace order)
@@ -1725,7 +1728,39 @@ struct TraceArgs {
     uint32_t *counters;          // [0] overflows, [2..] u64 walk counters (COUNT)
     const uint32_t *order;       // fetch order: the j-th ray walked is queue position order[j] (nullptr: j)
     uint32_t *walk_hist;         // COUNT: [0..31] walks by log2(nodes + triangles), [32..33] u64 max (cost << 32 | photon)
+    uint2 *spill;                // stack entries >= SL: (WIDE_STACK - SL) x gridDim.x*BLOCK, entry-major (HBM, no scratch)
+    // flat walks of this step (walk_kind 2), enrolled before the launch:
+    const uint32_t *flat_q;      // queue positions
+    const uint32_t *flat_count;  // how many (device word)
+    unsigned long long *flat_best;   // per flat walk: min over its sub-walks of (distance bits << 32 | rank)
+    uint32_t *diag;              // [0] += flat walks of this launch (nullptr: off)
 };
+
+// Enrol queue position p for the next trace launch if its walk is flat
+// (walk_kind 2): f = slot in the flat list, hits[p] = (FLAT_HIT, f).
+__device__ __forceinline__ void enrol_flat(const float *pos, const float *dir, uint32_t pid, uint32_t p, int2 *hits,
+                                           uint32_t *flat_q, uint32_t *flat_count, unsigned long long *flat_best) {
+    const V3 o = load3(pos, pid);
+    V3 d = load3(dir, pid);
+    d = d / norm(d);
+    if (walk_kind(o, d) != 2) return;
+    const uint32_t f = atomicAdd(flat_count, 1u);
+    flat_q[f] = p;
+    flat_best[f] = ~0ull;
+    hits[p] = make_int2(FLAT_HIT, (int)f);
+}
+
+// first host step: enrol the flat walks of the initial queue
+__global__ __launch_bounds__(BLOCK) void classify_kernel(const float *pos, const float *dir, const uint32_t *flags,
+                                                         const uint32_t *queue, uint32_t n, int2 *hits,
+                                                         uint32_t *flat_q, uint32_t *flat_count,
+                                                         unsigned long long *flat_best) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t pid = queue[i];
+    if ((flags[pid] & 0xFFFFu) & DEAD_MASK) return;
+    enrol_flat(pos, dir, pid, i, hits, flat_q, flat_count, flat_best);
+}
 
 // COUNT: walk counters; F: triangle step once F/8 of the walking lanes have
 // parked leaves (intersect_wide_spec); SL: stack entries in LDS; MINW: waves
@@ -1734,17 +1769,28 @@ template <bool COUNT, int F, int SL, int MINW, int R>
 __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__restrict__ gdev, TraceArgs a) {
     __shared__ uint32_t lds[(2 * SL + LEAFQ) * BLOCK];
     WStack st;
-    uint2 spill[WIDE_STACK - SL];
-    st.spill = spill;
+    // Deep stack entries live in a lane-strided HBM column sized for this
+    // persistent grid, not in private scratch: a kernel with a private segment
+    // depends on the runtime's scratch allocation, which can throttle the waves
+    // a dispatch keeps resident (the persistent grid then drains on a few waves).
+    st.spill = a.spill + (blockIdx.x * BLOCK + threadIdx.x);
+    st.sstride = gridDim.x * BLOCK;
     st.node = (CHR_LDS uint32_t *)(lds + threadIdx.x);
     st.dist = (CHR_LDS float *)(lds + SL * BLOCK + threadIdx.x);
     st.leafq = (CHR_LDS uint32_t *)(lds + 2 * SL * BLOCK + threadIdx.x);
     const DevGeom &g = *gdev;
     const uint32_t lane = __lane_id();
     uint32_t overflow = 0;
-    WalkCounts cnt{0u, 0u, 0u, 0u, 0u, 0ull, 0ull};
+    WalkCounts cnt{0u, 0u, 0u, 0u, 0u, 0ull, 0ull, 0u};
     bool has_ray = false, exhausted = false;
     uint32_t q = 0, pid = 0, walk_cost = 0;
+    // work items: [0, n) the queued rays (flat ones skipped), then K sub-walks
+    // per flat walk (K = the geometry's cut size; 1 = the whole walk)
+    const uint32_t nflat = a.flat_count ? *a.flat_count : 0u;
+    const uint32_t K = (g.nwcut > 1u && nflat <= (1u << 30) / g.nwcut) ? g.nwcut : 1u;
+    const uint32_t total = a.n + nflat * K;
+    int flat_f = -1;                // flat walk of the current sub-walk (-1: an ordinary ray)
+    uint32_t cmask = 0xFFu;         // children of the first node this walk may enter
     V3 o = v3(0.0f, 0.0f, 0.0f), d = v3(0.0f, 0.0f, 1.0f);
     RaySlab slab = make_slab(o, d);
     float best = 0.0f;
@@ -1755,7 +1801,9 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
     constexpr uint32_t INVALID = 0xFFFFFFFFu;
     while (true) {
         if (has_ray && walk_done && pleft == 0 && qh == qt) {   // walk over: publish (mesh.h:123-125)
-            a.hits[q] = make_int2(best_id, __float_as_int(best_id == -1 ? -1.0f : best));
+            if (flat_f < 0) a.hits[q] = make_int2(best_id, __float_as_int(best_id == -1 ? -1.0f : best));
+            else if (best_id != -1)   // a sub-walk: its best joins the flat walk's minimum
+                atomicMin(a.flat_best + flat_f, ((unsigned long long)__float_as_uint(best) << 32) | best_rank);
             has_ray = false;
             if constexpr (COUNT) {
                 if (a.walk_hist) {
@@ -1772,33 +1820,55 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
                 uint32_t base = 0;
                 if ((int)lane == leader) base = atomicAdd(a.next, (uint32_t)__popcll(need));
                 base = __shfl(base, leader);
-                if (base + (uint32_t)__popcll(need) >= a.n) exhausted = true;
+                if (base + (uint32_t)__popcll(need) >= total) exhausted = true;
                 if (!has_ray) {
-                    q = base + (uint32_t)__popcll(need & ((1ull << lane) - 1ull));
-                    if (q < a.n) {
-                        if (a.order) q = a.order[q];
+                    const uint32_t j = base + (uint32_t)__popcll(need & ((1ull << lane) - 1ull));
+                    bool start = false;
+                    if (j < a.n) {
+                        q = a.order ? a.order[j] : j;
                         pid = a.queue[q];
-                        // dead on entry / NaN: no walk (the step kernel skips / aborts them)
+                        // dead on entry / NaN: no walk (the step kernel skips / aborts them);
+                        // flat: enrolled before the launch, walked as sub-walks below
                         if (!((a.flags[pid] & 0xFFFFu) & DEAD_MASK)) {
                             o = load3(a.pos, pid);
                             d = load3(a.dir, pid);
                             d = d / norm(d);                        // propagate.cu:280-281
-                            const float prod = ((((d.x * d.y) * d.z) * o.x) * o.y) * o.z;
-                            if (!chr_isnan(prod)) {
-                                slab = make_slab(v3(-o.x / d.x, -o.y / d.y, -o.z / d.z),
-                                                 v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z));
+                            if (walk_kind(o, d) == 1) {
+                                start = true;
+                                flat_f = -1;
+                                node = 0;
+                                cmask = 0xFFu;
                                 best = __builtin_inff();
                                 best_rank = 0xFFFFFFFFu;
-                                best_id = -1;
-                                last = (uint32_t)a.last_hit[pid];
-                                sp = 0;
-                                node = 0;
-                                walk_done = false;
-                                has_ray = true;
-                                walk_cost = 0;
-                                if constexpr (COUNT) cnt.walks++;
                             }
                         }
+                    } else if (j < total) {                       // sub-walk k of flat walk f
+                        const uint32_t it = j - a.n, f = it / K, k = it - f * K;
+                        q = a.flat_q[f];
+                        pid = a.queue[q];
+                        o = load3(a.pos, pid);
+                        d = load3(a.dir, pid);
+                        d = d / norm(d);
+                        const uint2 item = K == 1u ? make_uint2(0u, 0xFFu) : g.wcut[k];
+                        // start from the best any sub-walk has published (only ever larger
+                        // than the final minimum, so culling with it is conservative)
+                        const unsigned long long key = a.flat_best[f];
+                        start = true;
+                        flat_f = (int)f;
+                        node = item.x;
+                        cmask = item.y;
+                        best = key == ~0ull ? __builtin_inff() : __uint_as_float((uint32_t)(key >> 32));
+                        best_rank = key == ~0ull ? 0xFFFFFFFFu : (uint32_t)key;
+                    }
+                    if (start) {
+                        slab = make_slab(v3(-o.x / d.x, -o.y / d.y, -o.z / d.z), v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z));
+                        best_id = -1;
+                        last = (uint32_t)a.last_hit[pid];
+                        sp = 0;
+                        walk_done = false;
+                        has_ray = true;
+                        walk_cost = 0;
+                        if constexpr (COUNT) cnt.walks++;
                     }
                 }
             }
@@ -1831,7 +1901,8 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
             uint32_t near_node;
             float near_t;
             uint32_t leaf_mask =
-                expand_node<SL>(h, a1, a2, a3, a4, a5, slab, best, near_node, near_t, st, sp, overflow);
+                expand_node<SL>(h, a1, a2, a3, a4, a5, slab, best, near_node, near_t, st, sp, overflow, cmask);
+            cmask = 0xFFu;
             node = near_node;
             while (leaf_mask) {
                 const int k = __builtin_ctz(leaf_mask);
@@ -1876,6 +1947,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
         }
     }
     if (overflow) atomicAdd(a.counters, overflow);
+    if (a.diag && nflat && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(a.diag, nflat);
     if constexpr (COUNT) {
         unsigned long long *c64 = reinterpret_cast<unsigned long long *>(a.counters + 2);
         atomicAdd(c64, (unsigned long long)cnt.nodes);
@@ -1992,17 +2064,29 @@ __device__ __forceinline__ uint32_t word_offset(const uint32_t *word_offsets, co
     return word_offsets[w] + block_prefix[w / SCAN_WORDS];
 }
 
+// Survivors of a split step also enrol their next walk if it is flat
+// (FlatEnrol: next step's flat list; pos == nullptr: off).
+struct FlatEnrol {
+    const float *pos, *dir;
+    int2 *hits;
+    uint32_t *flat_q, *flat_count;
+    unsigned long long *flat_best;
+};
 __global__ __launch_bounds__(BLOCK) void scatter_queue_kernel(const unsigned long long *masks, const uint32_t *word_offsets,
                                                                const uint32_t *block_prefix, const uint32_t *base,
                                                                const uint32_t *in_queue, int32_t first, int32_t n,
-                                                               uint32_t *out_queue) {
+                                                               uint32_t *out_queue, FlatEnrol fe) {
     const int id = blockIdx.x * BLOCK + threadIdx.x;
     if (id >= n) return;
     const unsigned long long m = masks[id >> 6];
     const int lane = id & 63;
     if ((m >> lane) & 1ull) {
         const uint32_t rank = __popcll(m & ((1ull << lane) - 1ull));
-        out_queue[base[0] + word_offset(word_offsets, block_prefix, (uint32_t)id >> 6) + rank] = in_queue[first + id];
+        const uint32_t o = base[0] + word_offset(word_offsets, block_prefix, (uint32_t)id >> 6) + rank;
+        const uint32_t pid = in_queue[first + id];
+        out_queue[o] = pid;
+        // out_queue[0] is the count header: position o - 1 of the next step's queue
+        if (fe.pos) enrol_flat(fe.pos, fe.dir, pid, o - 1u, fe.hits, fe.flat_q, fe.flat_count, fe.flat_best);
     }
 }
 
@@ -2120,6 +2204,7 @@ __global__ __launch_bounds__(BLOCK) void distance_kernel(const DevGeom *__restri
         WStack st;
         uint2 wspill[WIDE_STACK - WIDE_LDS];
         st.spill = wspill;
+        st.sstride = 1;
         st.node = (CHR_LDS uint32_t *)(lds_stack + threadIdx.x);
         st.dist = (CHR_LDS float *)(lds_stack + WIDE_LDS * BLOCK + threadIdx.x);
         st.leafq = nullptr;
@@ -2214,6 +2299,23 @@ int scratch_get(size_t bytes, void **out) {
     return CHR_OK;
 }
 
+// HBM column for the deep walk-stack entries of the persistent trace grid
+// (per thread and device, grown on demand; see trace_kernel)
+int walk_stack_get(size_t bytes, uint2 **out) {
+    static thread_local Scratch s[16];
+    int dev = 0;
+    CHR_HIP_CHECK(hipGetDevice(&dev));
+    Scratch &x = s[dev & 15];
+    if (x.bytes < bytes) {
+        if (x.ptr) CHR_HIP_CHECK(hipFree(x.ptr));
+        x.ptr = nullptr;
+        CHR_HIP_CHECK(hipMalloc(&x.ptr, bytes));
+        x.bytes = bytes;
+    }
+    *out = (uint2 *)x.ptr;
+    return CHR_OK;
+}
+
 }  // namespace
 
 extern "C" int chr_init_rng_subseq(uint32_t *d_states, uint32_t nslots, uint64_t seed, uint64_t first_subsequence,
@@ -2284,6 +2386,12 @@ typedef void (*propagate_fn)(const DevGeom *, PropagateArgs);
 static constexpr int kWalk = 2006;        // speculative wide walk, triangle steps at 6/8 of the live lanes
 static constexpr int kWalkSched = 1002;   // scheduled wide walk, triangle batch 2
 static constexpr int kExactVariant = 1;
+// the tail's group kernel at 4 waves/SIMD: it spills ~67 VGPRs to scratch
+// there, but at 2 waves/SIMD (no spills) the tail ran 2-3x longer (r02 rocprof:
+// a tail launch is up to 65,536 photons x 8 lanes = 8,192 waves, and the
+// launch lasts as long as its longest-lived photon, so fewer resident waves
+// means more rounds of waves behind it)
+static constexpr int kGroupWaves = 4;
 static bool wide_queue_ok(const chr_geometry *g) { return g->dev.nwtri < (1u << 30); }   // 30-bit leaf queue entries
 
 // one launch per chunk (the reference's launch structure: slot counts that are
@@ -2341,7 +2449,7 @@ static StepVariant select_step_variant(const chr_geometry *g) {
             sv.fn = propagate_step_kernel<8, 4, kWalk>;
             sv.trace = trace_kernel<false, 6, 12, 4, 32>;
             sv.shade = shade_kernel<3>;
-            sv.tail = propagate_group_kernel<8, 4>;
+            sv.tail = propagate_group_kernel<8, kGroupWaves>;
             sv.tail_group = 8;
             sv.binned = v == 7 ? 1 : (v == 8 ? 0 : 2);
             break;
@@ -2397,7 +2505,8 @@ static int launch_chunk(const chr_geometry *g, const chr_photons *ph, uint32_t *
     if (ev1) CHR_HIP_CHECK(hipEventRecord(ev1, stream));
     launch_mask_scan(masks, nwords, offsets, bsums, out_queue, counters + 1, nullptr, stream);
     hipLaunchKernelGGL(scatter_queue_kernel, dim3(grid_for(nthreads)), dim3(BLOCK), 0, stream, masks, offsets, bsums,
-                       counters + 1, in_queue, first, nthreads, out_queue);
+                       counters + 1, in_queue, first, nthreads, out_queue,
+                       FlatEnrol{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr});
     CHR_HIP_CHECK(hipGetLastError());
     return CHR_OK;
 }
@@ -2413,13 +2522,46 @@ static int device_cus() {
     return cus[dev & 15];
 }
 
+// Flat-walk bookkeeping of one propagate (trace_kernel): one list of queue
+// positions (the step's flat walks; the next step's list is written by the
+// step's scatter after the trace has read this one), their results, and
+// control words: ctl[1 + cur] the list count of the step, ctl[2 - cur] the
+// next step's, ctl[3] flat walks decomposed (diagnostic), ctl[4] flat walks
+// walked whole by the multi-step kernels (diagnostic).
+struct FlatCtx {
+    uint32_t *flat_q;
+    unsigned long long *flat_best;
+    uint32_t *ctl;
+    int cur;
+    bool enrol_next;
+};
+static int flat_get(uint32_t n, FlatCtx &fc) {
+    static thread_local Scratch s[16];
+    int dev = 0;
+    CHR_HIP_CHECK(hipGetDevice(&dev));
+    Scratch &x = s[dev & 15];
+    const size_t bytes = 256 + (size_t)n * 12 + 64;
+    if (x.bytes < bytes) {
+        if (x.ptr) CHR_HIP_CHECK(hipFree(x.ptr));
+        x.ptr = nullptr;
+        CHR_HIP_CHECK(hipMalloc(&x.ptr, bytes));
+        x.bytes = bytes;
+    }
+    fc.ctl = (uint32_t *)x.ptr;
+    fc.flat_best = (unsigned long long *)((char *)x.ptr + 256);
+    fc.flat_q = (uint32_t *)(fc.flat_best + n);
+    fc.cur = 0;
+    fc.enrol_next = false;
+    return CHR_OK;
+}
+
 static bool trace_steps();
 // hits: n (triangle, distance) slots + a ray counter word, for the split path
 static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *rng, uint32_t nslots, uint32_t cap,
                        uint32_t n, const uint32_t *in_queue, uint32_t *out_queue, int32_t max_steps,
                        int32_t use_weights, int32_t scatter_first, uint32_t *scratch, hipStream_t stream,
                        hipEvent_t ev0, hipEvent_t ev1, int2 *hits, uint32_t *sort_space, bool first_step,
-                       hipEvent_t evt0, hipEvent_t evt1, bool *split_out) {
+                       hipEvent_t evt0, hipEvent_t evt1, bool *split_out, const FlatCtx *fc) {
     const uint32_t nwords = (n + 63) / 64;
     uint32_t *counters = scratch;
     unsigned long long *masks = (unsigned long long *)(scratch + 16);
@@ -2433,16 +2575,29 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
     a.alive_masks = masks; a.counters = counters;
     a.order = nullptr;
     a.hits = nullptr;
+    a.flat_best = nullptr;
+    a.zero_word = nullptr;
+    a.diag = fc ? fc->ctl + 4 : nullptr;
+    FlatEnrol fe{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
     const uint32_t threads = std::min(cap, (n + 63u) & ~63u);
     const StepVariant sv = select_step_variant(g);
-    const bool split = sv.trace && hits && max_steps == 1;
+    const bool split = sv.trace && hits && max_steps == 1 && fc;
     if (split) {
         uint32_t *next = (uint32_t *)(hits + n);
         CHR_HIP_CHECK(hipMemsetAsync(next, 0, 4, stream));
+        uint32_t *count_cur = fc->ctl + 1 + fc->cur, *count_next = fc->ctl + 1 + (fc->cur ^ 1);
+        if (first_step)   // flat walks of the initial queue (later steps: enrolled by the previous scatter)
+            hipLaunchKernelGGL(classify_kernel, dim3(grid_for(n)), dim3(BLOCK), 0, stream, ph->d_pos, ph->d_dir,
+                               ph->d_flags, in_queue, n, hits, fc->flat_q, count_cur, fc->flat_best);
         TraceArgs ta;
         ta.pos = ph->d_pos; ta.dir = ph->d_dir; ta.flags = ph->d_flags; ta.last_hit = ph->d_last_hit_triangles;
         ta.queue = in_queue; ta.n = n; ta.hits = hits; ta.next = next; ta.counters = counters; ta.order = nullptr;
         ta.walk_hist = nullptr;
+        ta.flat_q = fc->flat_q; ta.flat_count = count_cur; ta.flat_best = fc->flat_best; ta.diag = fc->ctl + 3;
+        a.flat_best = fc->flat_best;
+        a.zero_word = count_next;   // cleared by the shade pass, filled by this step's scatter
+        if (fc->enrol_next)
+            fe = FlatEnrol{ph->d_pos, ph->d_dir, hits, fc->flat_q, count_next, fc->flat_best};
         if (trace_steps()) {   // debugging: per-walk cost histogram (counting variants), printed per step
             ta.walk_hist = next + 16 + 2 * (size_t)n;
             CHR_HIP_CHECK(hipMemsetAsync(ta.walk_hist, 0, 34 * 4, stream));
@@ -2465,6 +2620,7 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
         if (cus <= 0) return chr::fail(CHR_ERR_HIP, "launch_step: no compute units");
         const uint64_t resident = (uint64_t)cus * 4 * sv.trace_waves * 64 / BLOCK;   // persistent grid
         const uint32_t blocks = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(resident, grid_for(n)));
+        if (int rc = walk_stack_get((size_t)WIDE_STACK * blocks * BLOCK * sizeof(uint2), &ta.spill)) return rc;
         if (evt0) CHR_HIP_CHECK(hipEventRecord(evt0, stream));
         hipLaunchKernelGGL(sv.trace, dim3(blocks), dim3(BLOCK), 0, stream, (const DevGeom *)g->d_dev, ta);
         if (evt1) CHR_HIP_CHECK(hipEventRecord(evt1, stream));
@@ -2485,7 +2641,7 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
     if (ev1) CHR_HIP_CHECK(hipEventRecord(ev1, stream));
     launch_mask_scan(masks, nwords, offsets, bsums, out_queue, counters + 1, nullptr, stream);
     hipLaunchKernelGGL(scatter_queue_kernel, dim3(grid_for(n)), dim3(BLOCK), 0, stream, masks, offsets, bsums,
-                       counters + 1, in_queue, 0, (int32_t)n, out_queue);
+                       counters + 1, in_queue, 0, (int32_t)n, out_queue, fe);
     CHR_HIP_CHECK(hipGetLastError());
     return CHR_OK;
 }
@@ -2591,6 +2747,12 @@ extern "C" int chr_propagate(const chr_geometry *g, const chr_photons *ph, uint3
                                                             64) + 255) & ~(uintptr_t)255) : nullptr;
     uint32_t *pinned = nullptr;
     if ((rc = pinned_words(&pinned))) return rc;
+    FlatCtx fc{};
+    if (fused) {
+        if ((rc = flat_get(nphotons, fc))) return rc;
+        CHR_HIP_CHECK(hipMemsetAsync(fc.ctl, 0, 64, stream));
+        fc.enrol_next = true;
+    }
     const size_t max_chunks = fused ? 2 : (nphotons + chunk_cap - 1) / chunk_cap;   // fused: step + its walk
     std::vector<hipEvent_t> *evp = nullptr;
     if ((rc = timing_events(2 * max_chunks, &evp))) return rc;
@@ -2607,6 +2769,7 @@ extern "C" int chr_propagate(const chr_geometry *g, const chr_photons *ph, uint3
             float ms = 0.0f;
             CHR_HIP_CHECK(hipEventElapsedTime(&ms, events[2], events[3]));
             trace_ms += ms;
+            if (st.trace_ms_n < CHR_TRACE_MS_MAX) st.trace_launch_ms[st.trace_ms_n++] = ms;
         }
         return CHR_OK;
     };
@@ -2625,8 +2788,9 @@ extern "C" int chr_propagate(const chr_geometry *g, const chr_photons *ph, uint3
         if (fused) {
             rc = launch_step(g, ph, d_rng_states, rng_nslots, (uint32_t)cap, (uint32_t)n, q[cur] + 1, q[cur ^ 1],
                              nsteps, use_weights, scatter_first, scratch, stream, events[0], events[1], hits,
-                             sort_space, step == 0, events[2], events[3], &split_step);
+                             sort_space, step == 0, events[2], events[3], &split_step, &fc);
             if (rc) return rc;
+            fc.cur ^= 1;   // the step's scatter enrolled the next step's flat walks in the other list
             st.launches++;
             nchunks = 1;
             if (split_step) {
@@ -2683,8 +2847,11 @@ extern "C" int chr_propagate(const chr_geometry *g, const chr_photons *ph, uint3
     }
     CHR_HIP_CHECK(hipMemcpyAsync(pinned + 2, scratch, 4, hipMemcpyDeviceToHost, stream));
     CHR_HIP_CHECK(hipMemcpyAsync(pinned + 4, scratch + 2, 56, hipMemcpyDeviceToHost, stream));
+    if (fused) CHR_HIP_CHECK(hipMemcpyAsync(pinned + 20, fc.ctl + 3, 8, hipMemcpyDeviceToHost, stream));
     CHR_HIP_CHECK(hipStreamSynchronize(stream));
     st.stack_overflows = pinned[2];
+    st.flat_walks = fused ? pinned[20] : 0u;
+    st.flat_walks_whole = fused ? pinned[21] : 0u;
     {
         uint64_t c[7];
         std::memcpy(c, pinned + 4, 56);
@@ -2767,6 +2934,27 @@ extern "C" int chr_photon_duplicate(const chr_photons *ph, int32_t first_photon,
     hipLaunchKernelGGL(duplicate_kernel, dim3(grid_for(nphotons)), dim3(BLOCK), 0, (hipStream_t)stream, to_ptrs(ph),
                        first_photon, nphotons, copies, stride);
     CHR_HIP_CHECK(hipGetLastError());
+    return CHR_OK;
+}
+
+extern "C" int chr_kernel_info(int32_t which, chr_kernel_attr *out) {
+    if (!out) return chr::fail(CHR_ERR_INVALID, "chr_kernel_info: null output");
+    const void *fn = nullptr;
+    const char *name = nullptr;
+    switch (which) {
+        case 0: fn = (const void *)trace_kernel<false, 6, 12, 4, 32>; name = "chr::trace_kernel<false,6,12,4,32>"; break;
+        case 1: fn = (const void *)shade_kernel<3>; name = "chr::shade_kernel<3>"; break;
+        case 2: fn = (const void *)propagate_group_kernel<8, kGroupWaves>; name = "chr::propagate_group_kernel<8,4>"; break;
+        case 3: fn = (const void *)propagate_step_kernel<8, 4, kWalk>; name = "chr::propagate_step_kernel<8,4,2006>"; break;
+        default: return chr::fail(CHR_ERR_INVALID, "chr_kernel_info: unknown kernel %d", which);
+    }
+    hipFuncAttributes fa;
+    CHR_HIP_CHECK(hipFuncGetAttributes(&fa, fn));
+    out->private_bytes = fa.localSizeBytes;
+    out->lds_bytes = fa.sharedSizeBytes;
+    out->vgprs = fa.numRegs;
+    out->max_threads = fa.maxThreadsPerBlock;
+    std::snprintf(out->name, sizeof(out->name), "%s", name);
     return CHR_OK;
 }
 

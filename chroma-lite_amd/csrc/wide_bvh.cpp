@@ -386,6 +386,30 @@ int build_wide_bvh(const chr_geometry_desc *d, WideBVH &out) {
     }
     out.tri.resize(tri_next);
     if (7 * (out.max_depth + 1) + 1 > (uint32_t)WIDE_STACK) out.usable = false;
+    // rank -> triangle id (the tie-break rank identifies the triangle of a
+    // decomposed walk's (distance, rank) result)
+    out.rank_id.assign(nreach, 0xFFFFFFFFu);
+    for (uint32_t t = 0; t < ntri; ++t)
+        if (rank[t] != 0xFFFFFFFFu) out.rank_id[rank[t]] = t;
+    // cut: BFS frontier of inner nodes until it holds WIDE_CUT_TARGET nodes;
+    // nodes above it contribute their leaf children as (node, leaf mask) items
+    out.cut.clear();
+    std::vector<uint32_t> frontier{0}, nextf;
+    while (!frontier.empty() && frontier.size() < WIDE_CUT_TARGET) {
+        nextf.clear();
+        for (uint32_t n : frontier) {
+            const WideNode &W = out.nodes[n];
+            uint32_t leaf_mask = 0;
+            for (int k = 0; k < 8; ++k) {
+                if (W.kind[k] == 0) continue;
+                if (W.kind[k] == WIDE_INNER) nextf.push_back(W.child_base + W.off[k]);
+                else leaf_mask |= 1u << k;
+            }
+            if (leaf_mask) { out.cut.push_back(n); out.cut.push_back(leaf_mask); }
+        }
+        frontier.swap(nextf);
+    }
+    for (uint32_t n : frontier) { out.cut.push_back(n); out.cut.push_back(0xFFu); }
     return CHR_OK;
 }
 

@@ -53,7 +53,18 @@ struct WideBVH {
     std::vector<WideTri> tri;      // leaf order
     uint32_t max_depth = 0;        // levels below the root
     bool usable = true;            // false: the exact-order traversal must be used
+    // Decomposition of one walk into independent sub-walks (flat rays, see
+    // propagate.hip trace_kernel): (node, child mask) pairs whose subtrees
+    // partition the triangle records -- the nodes of one BFS frontier (all
+    // children) plus the leaf children of the nodes above it.
+    std::vector<uint32_t> cut;     // 2 words per item
+    std::vector<uint32_t> rank_id; // reference DFS rank -> triangle id
 };
+
+// target number of sub-walks per decomposed walk (frontier size): the longest
+// sub-walk sets the launch time (32,768 items: ~1,200-node subtrees on the
+// 29k detector, one flat walk = a 15 ms launch, r02 rocprof)
+constexpr uint32_t WIDE_CUT_TARGET = 1u << 18;
 
 // stack capacity of the wide traversal (entries); the builder marks a tree
 // whose worst-case stack (7 pushes per level) would not fit as unusable

@@ -170,7 +170,26 @@ typedef struct chr_propagate_stats {
     uint32_t trace_launches;      /* one-step launches walked by trace_kernel */
     uint32_t reserved;
     uint64_t trace_rays;          /* queued photons handed to those launches */
+    uint32_t trace_ms_n;          /* entries of trace_launch_ms filled (first CHR_TRACE_MS_MAX launches) */
+    float trace_launch_ms[32];    /* device time of each trace_kernel launch, in order */
+    uint32_t flat_walks;          /* walks with a direction component of non-finite reciprocal (the reference's
+                                     slab test then skips that axis): split into sub-walks by trace_kernel */
+    uint32_t flat_walks_whole;    /* such walks done whole by the multi-step (tail) kernel */
 } chr_propagate_stats;
+#define CHR_TRACE_MS_MAX 32
+
+/* Resources of the kernels on the default propagate path, from the code object
+ * (hipFuncGetAttributes): which = 0 trace_kernel (BVH walk of one-step launches),
+ * 1 shade_kernel, 2 the tail's group-walk kernel, 3 the fused step kernel.
+ * No reference counterpart (bench diagnostics). */
+typedef struct chr_kernel_attr {
+    uint64_t private_bytes;     /* scratch per work-item (0: no private segment) */
+    uint64_t lds_bytes;         /* static LDS per workgroup */
+    int32_t vgprs;              /* architected VGPRs per work-item */
+    int32_t max_threads;        /* max workgroup size */
+    char name[96];
+} chr_kernel_attr;
+int chr_kernel_info(int32_t which, chr_kernel_attr *out);
 
 /* replaces: GPUPhotons.propagate host loop (chroma/gpu/photon.py:226-293) for
  * track=False: queue setup (clones interleaved, 242-250), the nsteps policy
@@ -329,6 +348,30 @@ int chr_pdf_accumulate_kernel_eval(int32_t time_only, int32_t nchannels, const u
                                    float qmin, float qmax, const float *d_inv_time_bw,
                                    const float *d_inv_charge_bw, uint32_t *d_hitcount, float *d_time_pdf,
                                    float *d_charge_pdf, void *stream);
+
+/* ------------------------------------------------------------ self tests
+ * The reference's unit-test kernels, run over this build's device math (the
+ * functions the propagate kernels inline).  Tests only. */
+enum chr_linalg_op {   /* replaces: the 20 kernels of test/linalg_test.cu, in order */
+    CHR_LINALG_FLOAT3ADD = 0, CHR_LINALG_FLOAT3ADDEQUAL, CHR_LINALG_FLOAT3SUB, CHR_LINALG_FLOAT3SUBEQUAL,
+    CHR_LINALG_FLOAT3ADDFLOAT, CHR_LINALG_FLOAT3ADDFLOATEQUAL, CHR_LINALG_FLOATADDFLOAT3, CHR_LINALG_FLOAT3SUBFLOAT,
+    CHR_LINALG_FLOAT3SUBFLOATEQUAL, CHR_LINALG_FLOATSUBFLOAT3, CHR_LINALG_FLOAT3MULFLOAT,
+    CHR_LINALG_FLOAT3MULFLOATEQUAL, CHR_LINALG_FLOATMULFLOAT3, CHR_LINALG_FLOAT3DIVFLOAT,
+    CHR_LINALG_FLOAT3DIVFLOATEQUAL, CHR_LINALG_FLOATDIVFLOAT3, CHR_LINALG_DOT, CHR_LINALG_CROSS, CHR_LINALG_NORM,
+    CHR_LINALG_MINUSFLOAT3, CHR_LINALG_NOPS
+};
+/* d_a, d_b: float3-packed [n*3]; d_out [n*3] (or [n] for DOT/NORM) */
+int chr_selftest_linalg(int32_t op, uint32_t n, const float *d_a, const float *d_b, float c, float *d_out,
+                        void *stream);
+/* replaces: test/rotate_test.cu (rotate.h:21-28): d_out[i] = rotate(a[i], phi[i], n) */
+int chr_selftest_rotate(uint32_t n, const float *d_a, const float *d_phi, float nx, float ny, float nz,
+                        float *d_out, void *stream);
+/* replaces: test/test_sample_cdf.cu (random.h:27-55): one draw per slot i < n from
+ * RNG slot state i (SoA, chr_init_rng layout; states are not written back);
+ * uniform_grid = 0: sample_cdf(cdf_x, cdf_y), 1: sample_cdf(x0, delta, cdf_y) */
+int chr_selftest_sample_cdf(uint32_t n, const uint32_t *d_states, uint32_t nslots, int32_t ncdf,
+                            const float *d_cdf_x, const float *d_cdf_y, float x0, float delta,
+                            int32_t uniform_grid, float *d_out, void *stream);
 
 /* ------------------------------------------------------------- misc */
 const char *chr_last_error(void);
