@@ -869,7 +869,7 @@ typedef struct {
 /* propagate.cu:254-366 for one slot; returns 1 if the photon is still alive.
  * *processed is 0 when the photon was dead on entry (no write-back). */
 static int propagate_one(Geo *g, Photons *ph, uint32_t photon_id, chr_xorwow *rng, int max_steps,
-                         int use_weights, int scatter_first, int *processed) {
+                         int use_weights, int scatter_first, int *processed, int *steps_run) {
     Photon p;
     uint32_t i = photon_id;
     p.pos = mk(ph->pos[3 * i], ph->pos[3 * i + 1], ph->pos[3 * i + 2]);
@@ -905,6 +905,7 @@ static int propagate_one(Geo *g, Photons *ph, uint32_t photon_id, chr_xorwow *rn
         }
         propagate_at_boundary(&p, &s, rng);
     }
+    *steps_run = steps;
     ph->pos[3 * i] = p.pos.x; ph->pos[3 * i + 1] = p.pos.y; ph->pos[3 * i + 2] = p.pos.z;
     ph->dir[3 * i] = p.dir.x; ph->dir[3 * i + 1] = p.dir.y; ph->dir[3 * i + 2] = p.dir.z;
     ph->pol[3 * i] = p.pol.x; ph->pol[3 * i + 1] = p.pol.y; ph->pol[3 * i + 2] = p.pol.z;
@@ -931,6 +932,11 @@ static inline void rng_store(uint32_t *st, uint32_t nslots, uint32_t s, const ch
     st[3 * nslots + s] = r->v2; st[4 * nslots + s] = r->v3; st[5 * nslots + s] = r->v4;
 }
 
+/* Optional per-photon profile (diagnostics, orc_set_profile): steps run and
+ * reference-BVH nodes visited, summed over launches; NULL: off. */
+static uint32_t *g_prof_steps = NULL, *g_prof_nodes = NULL;
+EXPORT void orc_set_profile(uint32_t *steps, uint32_t *nodes) { g_prof_steps = steps; g_prof_nodes = nodes; }
+
 /* one kernel launch (propagate.cu:254): slots [0,nthreads) in parallel */
 static void launch_chunk(const chr_geometry_desc *d, Photons *ph, uint32_t *rng, uint32_t nslots,
                          const uint32_t *input_queue, int first, int nthreads, uint8_t *alive,
@@ -943,9 +949,12 @@ static void launch_chunk(const chr_geometry_desc *d, Photons *ph, uint32_t *rng,
         chr_xorwow r;
         rng_load(rng, nslots, (uint32_t)id, &r);
         uint32_t photon_id = input_queue[first + id];
-        int processed;
-        alive[id] = (uint8_t)propagate_one(&g, ph, photon_id, &r, max_steps, use_weights, scatter_first, &processed);
+        int processed, steps_run = 0;
+        alive[id] = (uint8_t)propagate_one(&g, ph, photon_id, &r, max_steps, use_weights, scatter_first, &processed,
+                                           &steps_run);
         if (processed) rng_store(rng, nslots, (uint32_t)id, &r);
+        if (processed && g_prof_steps) g_prof_steps[photon_id] += (uint32_t)steps_run;
+        if (processed && g_prof_nodes) g_prof_nodes[photon_id] += (uint32_t)g.nodes_visited;
         nv += g.nodes_visited; nt += g.tris_tested; ov += g.overflows; tv += g.traversals;
         if (g.max_depth > md) md = g.max_depth;
     }
@@ -1163,7 +1172,7 @@ static float sample_cdf_xy(chr_xorwow *rng, int ncdf, const float *cdf_x, const 
 static void daq_record(uint32_t *time_int, uint32_t *q_int, uint32_t *hist, int c, float time, float charge,
                        float charge_unit, uint32_t history) {
     uint32_t ti = chr_f2u(time);                             /* float_to_sortable_int: bit cast (daq.cu:5-10) */
-    uint32_t qi = (uint32_t)roundf(charge / charge_unit);    /* daq.cu:72 */
+    uint32_t qi = chr_sat_u32(roundf(charge / charge_unit));  /* daq.cu:72, saturating as CUDA */
     if (ti < time_int[c]) time_int[c] = ti;                  /* atomicMin (unsigned) */
     q_int[c] += qi;                                          /* atomicAdd */
     hist[c] |= history;                                      /* atomicOr */
