@@ -105,7 +105,11 @@ class GPUKernelPDF(object):
                      self.charge_pdf_values_gpu.gpudata, current_stream())
 
     def get_kernel_eval(self):
-        """pdf.py:161-175 -> (hitcount, pdf values, zero uncertainties)."""
+        """pdf.py:161-175 -> (hitcount, pdf values, zero uncertainties).
+
+        As in the reference, a channel whose charge bandwidth is NaN (its
+        charge variance is not clipped at zero in compute_bandwidth,
+        pdf.py:99-110) yields a NaN value when time and charge are combined."""
         hitcount = self.hitcount_gpu.get()
         norm = np.maximum(1, hitcount)
         time_pdf = self.time_pdf_values_gpu.get() / norm

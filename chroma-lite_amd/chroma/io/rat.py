@@ -16,6 +16,8 @@ Difference: the reference slices the track ids from byte 8*11*n instead of
 8 + 8*11*n (it keeps the last 8 bytes of the t plane and drops the last two
 ids); the ids are unused there.  decode_request reads them at their offset.
 """
+import sys
+
 import numpy as np
 
 from chroma import event
@@ -39,11 +41,14 @@ def decode_request(msg):
     if len(msg) < 8:
         raise ValueError('RAT request shorter than its header')
     n, eventid = (int(v) for v in np.frombuffer(msg[:8], dtype='<u4'))
-    need = 8 + 8 * 11 * n + 4 * n
-    if len(msg) != need:
-        raise ValueError('RAT request of %d bytes for %d photons (expected %d)' % (len(msg), n, need))
-    planes = np.frombuffer(msg[8:8 + 88 * n], dtype='<f8').reshape(11, n)
-    trackids = np.frombuffer(msg[8 + 88 * n:], dtype='<u4').copy()
+    need = 8 + 8 * 11 * n
+    if len(msg) < need:
+        raise ValueError('RAT request of %d bytes for %d photons (expected at least %d)' % (len(msg), n, need))
+    planes = np.frombuffer(msg[8:need], dtype='<f8').reshape(11, n)
+    # the track-id block is optional: the reference server slices it loosely
+    # (bin/chroma-server-rat:34) and never uses it
+    tail = msg[need:]
+    trackids = np.frombuffer(tail[:len(tail) - len(tail) % 4], dtype='<u4').copy()
     photons = event.Photons(planes[0:3].T, planes[3:6].T, planes[6:9].T, planes[9], planes[10])
     return photons, eventid, trackids
 
@@ -107,5 +112,12 @@ def serve(detector, address='ipc:///tmp/ipc_chroma', max_requests=None):
     socket.bind(address)
     served = 0
     while max_requests is None or served < max_requests:
-        socket.send(handle_request(sim, socket.recv()))
+        msg = socket.recv()
+        try:
+            reply = handle_request(sim, msg)
+        except ValueError as e:       # malformed request: empty reply keeps the REP state machine going
+            print('chroma-server-rat: bad request: %s' % e, file=sys.stderr, flush=True)
+            eventid = int(np.frombuffer(msg[4:8], dtype='<u4')[0]) if len(msg) >= 8 else 0
+            reply = encode_reply({}, eventid)
+        socket.send(reply)
         served += 1

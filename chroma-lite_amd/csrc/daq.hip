@@ -92,7 +92,7 @@ __global__ __launch_bounds__(BLOCK) void run_daq_kernel(uint32_t *rng_states, ui
         if (chr_uniform01(&rng) < weight) {
             const float time = ph.t[photon_id] + sample_cdf_xy(rng, det.time_cdf_len, det.d_time_cdf_x, det.d_time_cdf_y);
             const float charge = sample_cdf_xy(rng, det.charge_cdf_len, det.d_charge_cdf_x, det.d_charge_cdf_y);
-            const uint32_t charge_int = (uint32_t)__builtin_roundf(charge / det.charge_unit);
+            const uint32_t charge_int = chr_sat_u32(__builtin_roundf(charge / det.charge_unit));
             atomicMin(time_int + channel_index, __float_as_uint(time));
             atomicAdd(q_int + channel_index, charge_int);
             atomicOr(hist + channel_index, history);
@@ -137,7 +137,7 @@ __global__ void run_daq_many_kernel(uint32_t *rng_states, uint32_t nslots, uint3
                 float time = photon_time + chr_normal(&rng, &nflag, &nextra);
                 time = time + sample_cdf_xy(rng, det.time_cdf_len, det.d_time_cdf_x, det.d_time_cdf_y);
                 const float charge = sample_cdf_xy(rng, det.charge_cdf_len, det.d_charge_cdf_x, det.d_charge_cdf_y);
-                const uint32_t charge_int = (uint32_t)__builtin_roundf(charge / det.charge_unit);
+                const uint32_t charge_int = chr_sat_u32(__builtin_roundf(charge / det.charge_unit));
                 atomicMin(time_int + channel_offset, __float_as_uint(time));
                 atomicAdd(q_int + channel_offset, charge_int);
                 atomicOr(hist + channel_offset, history);

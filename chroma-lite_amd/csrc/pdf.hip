@@ -39,11 +39,7 @@ constexpr int NEAREST_LDS = 8192;   // candidates staged in LDS (32 KB); larger 
 constexpr float INV_ROOT2 = 0.70710678118654746f;   // pdf.cu:268
 constexpr float ROOT_PI_BY_2 = 1.2533141373155001f;  // pdf.cu:269
 
-__device__ __forceinline__ uint32_t sat_u32(float x) {
-    if (!(x > 0.0f)) return 0u;                 // NaN, negatives, -0
-    if (x >= 4294967296.0f) return 0xFFFFFFFFu;
-    return (uint32_t)x;
-}
+__device__ __forceinline__ uint32_t sat_u32(float x) { return chr_sat_u32(x); }   // NaN, negatives, -0 -> 0
 
 // pdf.cu:9-32
 __global__ __launch_bounds__(BLOCK) void bin_hits_kernel(int nchannels, const float *channel_q,
@@ -121,12 +117,18 @@ __global__ __launch_bounds__(NEAREST_BLOCK) void nearest_kernel(int ndaq, const 
         for (int j = threadIdx.x; j < n; j += NEAREST_BLOCK) cand_lds[j] = value(j);
         __syncthreads();
     }
+    // total order: ascending, NaN after every number (all NaNs tie), ties by
+    // position -- every rank below min(n, k) is taken exactly once
     for (int i = threadIdx.x; i < n; i += NEAREST_BLOCK) {
         const float v = staged ? cand_lds[i] : value(i);
+        const bool vnan = v != v;
         int rank = 0;
         for (int j = 0; j < n && rank < k; j++) {
             const float w = staged ? cand_lds[j] : value(j);
-            rank += (w < v) || (w == v && j < i);
+            const bool wnan = w != w;
+            const bool before = vnan ? !wnan : (w < v);
+            const bool tie = vnan ? wnan : (w == v);
+            rank += before || (tie && j < i);
         }
         if (rank < k) out_lds[rank] = v;
     }

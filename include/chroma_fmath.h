@@ -33,6 +33,15 @@
 #define CHR_PI_F 3.141592653589793f
 #define CHR_PIO2_F 1.57079632679489661923f
 
+/* float -> uint32 with CUDA's saturating conversion (cvt.rzi.sat.u32.f32:
+ * NaN and negatives -> 0, >= 2^32 -> 0xFFFFFFFF); a plain C cast is undefined
+ * there (DAQ / PDF charge words, daq.cu:72, pdf.cu:15) */
+CHR_FN uint32_t chr_sat_u32(float x) {
+    if (!(x > 0.0f)) return 0u;
+    if (x >= 4294967296.0f) return 0xFFFFFFFFu;
+    return (uint32_t)x;
+}
+
 CHR_FN uint32_t chr_f2u(float x) {
 #if defined(__HIPCC__)
     return __builtin_bit_cast(uint32_t, x);

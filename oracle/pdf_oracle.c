@@ -65,8 +65,11 @@ void orc_pdf_accumulate_bincount(int nchannels, int ndaq, const uint32_t *event_
     }
 }
 
+/* ascending, NaN after every number (the HIP kernel's total order) */
 static int cmp_float(const void *a, const void *b) {
     const float x = *(const float *)a, y = *(const float *)b;
+    const int xn = x != x, yn = y != y;
+    if (xn || yn) return xn - yn;
     return (x > y) - (x < y);
 }
 

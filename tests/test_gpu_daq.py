@@ -18,15 +18,19 @@ def cuda():
     return create_cuda_context()
 
 
-@pytest.mark.parametrize('ndaq,ntpb,max_blocks', [(1, 64, 8), (1, 256, 1024), (5, 64, 16)])
-def test_daq_parity(cuda, small_detector, small_packed, ndaq, ntpb, max_blocks):
+@pytest.mark.parametrize('ndaq,ntpb,max_blocks,charge', [
+    (1, 64, 8, (1.0, 0.1, 0.5, 1.5)), (1, 256, 1024, (1.0, 0.1, 0.5, 1.5)), (5, 64, 16, (1.0, 0.1, 0.5, 1.5)),
+    # a pedestal-like charge CDF with negative support: negative charges convert
+    # to 0 (CUDA's saturating float -> u32; a plain cast is undefined)
+    (1, 64, 8, (0.1, 0.5, -2.0, 2.0)), (5, 64, 16, (0.1, 0.5, -2.0, 2.0))])
+def test_daq_parity(cuda, small_detector, small_packed, ndaq, ntpb, max_blocks, charge):
     from chroma import gpu
     from chroma.gpu.detector import cdf_arrays
     from chroma.photon_source import isotropic
     from test_gpu_parity import _run_both, _compare
     saved = small_detector.time_cdf, small_detector.charge_cdf
     small_detector.set_time_dist_gaussian(1.2, -6.0, 6.0)
-    small_detector.set_charge_dist_gaussian(1.0, 0.1, 0.5, 1.5)
+    small_detector.set_charge_dist_gaussian(*charge)
     try:
         photons = isotropic(20000, seed=31)
         nslots = 64 * 1024

@@ -34,8 +34,11 @@ def test_rat_request_round_trip():
     for f in ('pos', 'dir', 'pol', 'wavelengths', 't'):
         assert getattr(got, f).dtype == np.float32
         assert np.array_equal(getattr(got, f), getattr(ph, f))
+    # the track-id block is optional (the reference server never reads it)
+    got, evid, tid = rat.decode_request(msg[:8 + 88 * 1000])
+    assert evid == 42 and len(tid) == 0 and np.array_equal(got.t, ph.t)
     with pytest.raises(ValueError):
-        rat.decode_request(msg[:-4])
+        rat.decode_request(msg[:8 + 88 * 1000 - 8])    # a truncated t plane
     empty = rat.encode_request(_photons(0), 7)
     got, evid, tid = rat.decode_request(empty)
     assert len(got) == 0 and evid == 7
