@@ -380,7 +380,10 @@ def main():
                 host_steps=sum(s.steps_run for s in stats), trace_ms=sum(s.trace_ms for s in stats),
                 trace_launches=sum(s.trace_launches for s in stats), trace_rays=sum(s.trace_rays for s in stats),
                 overflows=sum(s.stack_overflows for s in stats), flat=sum(s.flat_walks for s in stats),
-                flat_whole=sum(s.flat_walks_whole for s in stats))
+                flat_whole=sum(s.flat_walks_whole for s in stats),
+                tail=[{'ms': round(s.tail_ms, 3), 'photons': int(s.tail_photons), 'max_steps': int(s.tail_max_steps),
+                       'slowest_photon_ms': round(s.tail_max_cycles / 1e5, 3),
+                       'slowest_photon_steps': int(s.tail_slowest_steps)} for s in stats])
     # untimed: same propagate with the counting kernel variant -> own-layout bytes and SIMD efficiency
     cst = None
     if not args.no_count:
@@ -404,6 +407,7 @@ def main():
                   'host_steps_per_propagate': live['host_steps'] / steps,
                   'stack_overflows': int(live['overflows']),
                   'flat_walks_decomposed': int(live['flat']), 'flat_walks_whole': int(live['flat_whole']),
+                  'tail_launch': live['tail'],
                   'detected_fraction': detected / args.photons,
                   'channel_hits_all_ranks': channel_hits,
                   'device': {'name': props.name, 'arch': getattr(props, 'gcnArchName', ''),

@@ -68,7 +68,8 @@ class PropagateStats(ctypes.Structure):
                 ('wave_fill_cycles', c_u64), ('wave_step_cycles', c_u64), ('trace_ms', ctypes.c_double),
                 ('trace_launches', c_u32), ('reserved', c_u32), ('trace_rays', c_u64),
                 ('trace_ms_n', c_u32), ('trace_launch_ms', c_f32 * 32), ('flat_walks', c_u32),
-                ('flat_walks_whole', c_u32)]
+                ('flat_walks_whole', c_u32), ('tail_photons', c_u32), ('tail_ms', ctypes.c_double),
+                ('tail_max_steps', c_u32), ('tail_slowest_steps', c_u32), ('tail_max_cycles', c_u64)]
 
 
 class KernelAttr(ctypes.Structure):

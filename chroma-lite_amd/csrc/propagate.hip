@@ -1353,7 +1353,8 @@ struct PropagateArgs {
     const int2 *hits;                  // shade_kernel: walk result per queue position (trace_kernel)
     const unsigned long long *flat_best;   // shade_kernel: results of the flat walks (FLAT_HIT entries of hits)
     uint32_t *zero_word;               // shade_kernel: word cleared once (next step's flat-walk count)
-    uint32_t *diag;                    // multi-step kernels: [0] += flat walks walked whole (nullptr: off)
+    uint32_t *diag;                    // multi-step kernels (nullptr: off): [0] += flat walks walked whole,
+                                       // [1] max steps of one photon, [2..3] u64 max of (cycles << 16 | steps)
 };
 // hits[q] = (FLAT_HIT, f): queue position q holds flat walk f of this step,
 // its result is flat_best[f] (trace_kernel)
@@ -1368,7 +1369,7 @@ __device__ __forceinline__ void store3(float *p, uint32_t i, V3 v) { p[3 * i] = 
 template <int BATCH, int WIDE, bool COUNT>
 __device__ __forceinline__ bool run_photon(const DevGeom &g, const PropagateArgs &a, uint32_t photon_id,
                                            uint32_t history, chr_xorwow &rng, Stack st, WStack &wst,
-                                           uint32_t &overflow, WalkCounts &cnt) {
+                                           uint32_t &overflow, WalkCounts &cnt, int *steps_run = nullptr) {
     Photon p;
     p.history = history;
     p.pos = load3(a.pos, photon_id);
@@ -1412,6 +1413,7 @@ __device__ __forceinline__ bool run_photon(const DevGeom &g, const PropagateArgs
         const unsigned long long tend = __builtin_amdgcn_s_memtime();
         if (wave_leader()) cnt.wave_other_cycles += tend - tstart;   // includes fill; split on the host
     }
+    if (steps_run) *steps_run = steps;
     store3(a.pos, photon_id, p.pos);
     store3(a.dir, photon_id, p.dir);
     store3(a.pol, photon_id, p.pol);
@@ -1667,8 +1669,17 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_group_kernel(const DevG
         const uint32_t history = a.flags[photon_id] & 0xFFFFu;   // photon.h:29
         if (history & DEAD_MASK) continue;
         if (!have_rng) { load_rng(a, slot, rng); have_rng = true; }
-        const bool alive = run_photon<8, GROUP_MODE + G, false>(g, a, photon_id, history, rng, st, wst, overflow, cnt);
+        int steps = 0;
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();   // 100 MHz
+        const bool alive = run_photon<8, GROUP_MODE + G, false>(g, a, photon_id, history, rng, st, wst, overflow, cnt,
+                                                                &steps);
         if (alive && sub == 0) atomicOr(a.alive_masks + (q >> 6), 1ull << (q & 63u));
+        if (sub == 0 && a.diag) {   // the tail's serial chain: longest photon in steps and in time
+            const unsigned long long cyc = __builtin_amdgcn_s_memrealtime() - t0;
+            atomicMax(a.diag + 1, (uint32_t)steps);
+            atomicMax(reinterpret_cast<unsigned long long *>(a.diag + 2),
+                      (cyc << 16) | (unsigned long long)(steps > 0xFFFF ? 0xFFFF : steps));
+        }
     }
     if (have_rng && sub == 0) store_rng(a, slot, rng);
     if (sub == 0 && overflow) atomicAdd(a.counters, overflow);
@@ -2758,12 +2769,13 @@ extern "C" int chr_propagate(const chr_geometry *g, const chr_photons *ph, uint3
     if ((rc = timing_events(2 * max_chunks, &evp))) return rc;
     std::vector<hipEvent_t> &events = *evp;
     double kernel_ms = 0.0, trace_ms = 0.0;
-    bool split_step = false;
+    bool split_step = false, tail_step = false;
     auto collect = [&](size_t nchunks) -> int {
         for (size_t c = 0; c < nchunks; ++c) {
             float ms = 0.0f;
             CHR_HIP_CHECK(hipEventElapsedTime(&ms, events[2 * c], events[2 * c + 1]));
             kernel_ms += ms;
+            if (tail_step) st.tail_ms += ms;
         }
         if (fused && split_step) {
             float ms = 0.0f;
@@ -2784,6 +2796,8 @@ extern "C" int chr_propagate(const chr_geometry *g, const chr_photons *ph, uint3
     while (step < max_steps) {
         const int nsteps = (n < (int64_t)ntpb * 16 * 8 || use_weights) ? max_steps - step : 1;   // photon.py:261-264
         const int64_t n_prev = n;
+        tail_step = nsteps > 1;
+        if (tail_step) st.tail_photons += (uint32_t)n;
         size_t nchunks = 0;
         if (fused) {
             rc = launch_step(g, ph, d_rng_states, rng_nslots, (uint32_t)cap, (uint32_t)n, q[cur] + 1, q[cur ^ 1],
@@ -2847,11 +2861,18 @@ extern "C" int chr_propagate(const chr_geometry *g, const chr_photons *ph, uint3
     }
     CHR_HIP_CHECK(hipMemcpyAsync(pinned + 2, scratch, 4, hipMemcpyDeviceToHost, stream));
     CHR_HIP_CHECK(hipMemcpyAsync(pinned + 4, scratch + 2, 56, hipMemcpyDeviceToHost, stream));
-    if (fused) CHR_HIP_CHECK(hipMemcpyAsync(pinned + 20, fc.ctl + 3, 8, hipMemcpyDeviceToHost, stream));
+    if (fused) CHR_HIP_CHECK(hipMemcpyAsync(pinned + 20, fc.ctl + 3, 20, hipMemcpyDeviceToHost, stream));
     CHR_HIP_CHECK(hipStreamSynchronize(stream));
     st.stack_overflows = pinned[2];
     st.flat_walks = fused ? pinned[20] : 0u;
     st.flat_walks_whole = fused ? pinned[21] : 0u;
+    if (fused) {
+        uint64_t key;
+        std::memcpy(&key, pinned + 23, 8);
+        st.tail_max_steps = pinned[22];
+        st.tail_max_cycles = key >> 16;
+        st.tail_slowest_steps = (uint32_t)(key & 0xFFFFu);
+    }
     {
         uint64_t c[7];
         std::memcpy(c, pinned + 4, 56);

@@ -175,6 +175,11 @@ typedef struct chr_propagate_stats {
     uint32_t flat_walks;          /* walks with a direction component of non-finite reciprocal (the reference's
                                      slab test then skips that axis): split into sub-walks by trace_kernel */
     uint32_t flat_walks_whole;    /* such walks done whole by the multi-step (tail) kernel */
+    uint32_t tail_photons;        /* photons handed to the multi-step (tail) launch (nsteps policy) */
+    double tail_ms;               /* device time of that launch (HIP events) */
+    uint32_t tail_max_steps;      /* most steps one photon ran in the tail launch */
+    uint32_t tail_slowest_steps;  /* steps of the photon that took longest in the tail launch */
+    uint64_t tail_max_cycles;     /* that photon's time in ticks of the 100 MHz s_memrealtime clock */
 } chr_propagate_stats;
 #define CHR_TRACE_MS_MAX 32
 

@@ -38,6 +38,8 @@ def main():
     ap.add_argument('--max-steps', type=int, default=1000)
     ap.add_argument('--seed', type=int, default=1)
     ap.add_argument('--top', type=int, default=20)
+    ap.add_argument('--repeat', type=int, default=1,
+                    help='propagates of the same photons with the RNG states carried on (bench.py steps)')
     ap.add_argument('--cache-dir', default='/tmp/chroma_bench_cache')
     args = ap.parse_args()
     import bench
@@ -48,26 +50,28 @@ def main():
     det = bench.build_geometry(args.detector, args.cache_dir)
     packed = PackedGeometry(det)
     src = isotropic(args.photons, seed=bench.PHOTON_SEED)
-    host = oracle.HostPhotons(Photons(src.pos, src.dir, src.pol, src.wavelengths))
     nslots = 512 * 1024
     st = oracle.rng_init(nslots, seed=args.seed)
-    steps = np.zeros(args.photons, np.uint32)
-    nodes = np.zeros(args.photons, np.uint32)
     oracle.lib().orc_set_profile.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
-    oracle.lib().orc_set_profile(steps.ctypes.data, nodes.ctypes.data)
-    t0 = time.time()
-    stats = oracle.propagate(packed, host, st, nslots, 512, 1024, args.max_steps)
-    oracle.lib().orc_set_profile(None, None)
-    print('propagate %.1fs, host steps %d, stats %s' % (time.time() - t0, stats['host_steps'], stats))
-    q = [50, 90, 99, 99.9, 99.99, 100]
-    print('steps per photon percentiles', dict(zip(q, np.percentile(steps, q))))
-    order = np.argsort(steps)[::-1][:args.top]
-    for i in order:
-        print('photon %8d steps %4d nodes/step %7.1f flags %-60s pos %s r %.0f' % (
-            i, steps[i], nodes[i] / max(1, steps[i]), names(int(host.flags[i])), np.round(host.pos[i], 1),
-            np.linalg.norm(host.pos[i])))
-    hist = np.bincount(np.minimum(steps, 1000) // 50)
-    print('steps histogram (bins of 50):', hist.tolist())
+    for rep in range(args.repeat):
+        host = oracle.HostPhotons(Photons(src.pos, src.dir, src.pol, src.wavelengths))
+        steps = np.zeros(args.photons, np.uint32)
+        nodes = np.zeros(args.photons, np.uint32)
+        oracle.lib().orc_set_profile(steps.ctypes.data, nodes.ctypes.data)
+        t0 = time.time()
+        stats = oracle.propagate(packed, host, st, nslots, 512, 1024, args.max_steps)
+        oracle.lib().orc_set_profile(None, None)
+        print('propagate %d: %.1fs, host steps %d, stats %s' % (rep, time.time() - t0, stats['host_steps'], stats))
+        q = [50, 90, 99, 99.9, 99.99, 100]
+        print('steps per photon percentiles', dict(zip(q, np.percentile(steps, q))))
+        order = np.argsort(steps)[::-1][:args.top]
+        for i in order:
+            print('photon %8d steps %4d nodes/step %7.1f flags %-60s pos %s r %.0f' % (
+                i, steps[i], nodes[i] / max(1, steps[i]), names(int(host.flags[i])), np.round(host.pos[i], 1),
+                np.linalg.norm(host.pos[i])))
+        worst = np.argsort(nodes)[::-1][:5]
+        print('most nodes:', [(int(i), int(steps[i]), int(nodes[i])) for i in worst])
+        sys.stdout.flush()
 
 
 if __name__ == '__main__':
