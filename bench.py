@@ -383,7 +383,12 @@ def main():
                 flat_whole=sum(s.flat_walks_whole for s in stats),
                 tail=[{'ms': round(s.tail_ms, 3), 'photons': int(s.tail_photons), 'max_steps': int(s.tail_max_steps),
                        'slowest_photon_ms': round(s.tail_max_cycles / 1e5, 3),
-                       'slowest_photon_steps': int(s.tail_slowest_steps)} for s in stats])
+                       'slowest_photon_steps': int(s.tail_slowest_steps),
+                       'long_photons': int(s.tail_long_photons),
+                       'long_us_per_step': round(s.tail_long_ticks / 100.0 / max(1, s.tail_long_steps), 3),
+                       'long_walk_us_per_step': round(s.tail_long_walk_ticks / 100.0 / max(1, s.tail_long_steps), 3),
+                       'long_walk_iterations_per_step': round(s.tail_long_walk_iterations / max(1, s.tail_long_steps),
+                                                              2)} for s in stats])
     # untimed: same propagate with the counting kernel variant -> own-layout bytes and SIMD efficiency
     cst = None
     if not args.no_count:

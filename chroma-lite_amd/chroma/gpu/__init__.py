@@ -8,3 +8,4 @@ from chroma.gpu.detector import GPUDetector  # noqa: F401
 from chroma.gpu.photon import GPUPhotons, GPUPhotonsSlice  # noqa: F401
 from chroma.gpu.daq import GPUDaq, GPUChannels  # noqa: F401
 from chroma.gpu.pdf import GPUPDF, GPUKernelPDF  # noqa: F401
+from chroma.gpu.render import GPURays  # noqa: F401

@@ -69,7 +69,9 @@ class PropagateStats(ctypes.Structure):
                 ('trace_launches', c_u32), ('reserved', c_u32), ('trace_rays', c_u64),
                 ('trace_ms_n', c_u32), ('trace_launch_ms', c_f32 * 32), ('flat_walks', c_u32),
                 ('flat_walks_whole', c_u32), ('tail_photons', c_u32), ('tail_ms', ctypes.c_double),
-                ('tail_max_steps', c_u32), ('tail_slowest_steps', c_u32), ('tail_max_cycles', c_u64)]
+                ('tail_max_steps', c_u32), ('tail_slowest_steps', c_u32), ('tail_max_cycles', c_u64),
+                ('tail_long_photons', c_u32), ('reserved2', c_u32), ('tail_long_steps', c_u64),
+                ('tail_long_ticks', c_u64), ('tail_long_walk_ticks', c_u64), ('tail_long_walk_iterations', c_u64)]
 
 
 class KernelAttr(ctypes.Structure):
@@ -125,6 +127,16 @@ _SIGNATURES = {
                                            c_vp, c_vp, c_vp]),
     'chr_pdf_accumulate_kernel_eval': (c_i32, [c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_f32, c_f32, c_f32, c_f32,
                                                c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    'chr_render': (c_i32, [c_vp, c_u32, c_vp, c_vp, c_vp, c_u32, c_vp, c_vp, c_vp, c_vp, c_u32, c_vp]),
+    'chr_transform_translate': (c_i32, [c_u32, c_vp, c_f32, c_f32, c_f32, c_vp]),
+    'chr_transform_rotate': (c_i32, [c_u32, c_vp, c_f32, c_f32, c_f32, c_f32, c_vp]),
+    'chr_transform_rotate_around_point': (c_i32, [c_u32, c_vp, c_f32, c_f32, c_f32, c_f32, c_f32, c_f32, c_f32,
+                                                  c_vp]),
+    'chr_hybrid_update_xyz_lookup': (c_i32, [c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_vp, c_vp, c_u32, c_f32, c_vp,
+                                             c_vp, c_vp, c_i32, c_vp]),
+    'chr_hybrid_update_xyz_image': (c_i32, [c_vp, c_i32, c_vp, c_u32, c_vp, c_vp, c_f32, c_vp, c_vp, c_vp, c_vp,
+                                            c_i32, c_i32, c_vp]),
+    'chr_hybrid_process_image': (c_i32, [c_i32, c_vp, c_vp, c_i32, c_vp]),
     'chr_last_error': (ctypes.c_char_p, []),
     'chr_version': (c_i32, []),
 }

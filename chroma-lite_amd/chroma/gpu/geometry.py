@@ -39,6 +39,32 @@ class GPUGeometry(object):
     def gpudata(self):
         return self._handle.value
 
+    # The mesh arrays and triangle colours the renderers read (reference
+    # geometry.py:389-406 uploads them with the geometry; here on first use,
+    # since the propagate path does not need them).
+    @property
+    def colors(self):
+        if getattr(self, '_colors', None) is None:
+            colors = getattr(self.geometry, 'colors', None)
+            if colors is None or len(colors) != len(self.packed.triangles):
+                colors = np.zeros(len(self.packed.triangles), np.uint32)
+            self._colors = ga.to_gpu(np.asarray(colors).astype(np.uint32))
+        return self._colors
+
+    @property
+    def vertices(self):
+        if getattr(self, '_vertices', None) is None:
+            from chroma.gpu.tools import to_float3
+            self._vertices = ga.to_gpu(to_float3(self.packed.vertices))
+        return self._vertices
+
+    @property
+    def triangles(self):
+        if getattr(self, '_triangles', None) is None:
+            from chroma.gpu.tools import to_uint3
+            self._triangles = ga.to_gpu(to_uint3(self.packed.triangles))
+        return self._triangles
+
     def device_bytes(self):
         b = ctypes.c_uint64()
         _native.call('chr_geometry_device_bytes', self._handle, ctypes.byref(b))

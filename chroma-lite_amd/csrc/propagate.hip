@@ -62,6 +62,7 @@ struct State {
     V3 normal;
     float n1, n2, absorption_length, scattering_length, distance;
     int material1, surface_index;
+    bool inside_to_outside;   // photon.h:38 (the hybrid renderer reads it)
 };
 
 #define CHR_LDS __attribute__((address_space(3)))
@@ -868,8 +869,8 @@ __device__ __forceinline__ void finish_fill(const DevGeom &g, State &s, Photon &
         s.distance = a_distance;
         s.surface_index = a_surface;
         p.last_hit = -2;
-        if (a_dot_raw > 0.0f) { m1 = a_outer; m2 = a_inner; s.normal = a_normal_raw; }
-        else { m1 = a_inner; m2 = a_outer; s.normal = -a_normal_raw; }
+        if (a_dot_raw > 0.0f) { m1 = a_outer; m2 = a_inner; s.normal = a_normal_raw; s.inside_to_outside = false; }
+        else { m1 = a_inner; m2 = a_outer; s.normal = -a_normal_raw; s.inside_to_outside = true; }
     } else if (mesh_triangle != -1) {
         p.last_hit = mesh_triangle;
         const float4 *r = g.tri + 3 * (size_t)mesh_triangle;
@@ -879,8 +880,8 @@ __device__ __forceinline__ void finish_fill(const DevGeom &g, State &s, Photon &
         const int outer = convert(0xFF & (int)(code >> 16));
         s.surface_index = convert(0xFF & (int)(code >> 8));
         s.normal = normalize(cross(v3(r0.w, r1.x, r1.y), v3(r2.y, r2.z, r2.w)));
-        if (dot(s.normal, -p.dir) > 0.0f) { m1 = outer; m2 = inner; }
-        else { m1 = inner; m2 = outer; s.normal = -s.normal; }
+        if (dot(s.normal, -p.dir) > 0.0f) { m1 = outer; m2 = inner; s.inside_to_outside = false; }
+        else { m1 = inner; m2 = outer; s.normal = -s.normal; s.inside_to_outside = true; }
     } else {
         p.last_hit = -1;
         p.history |= CHR_NO_HIT;
@@ -1354,7 +1355,9 @@ struct PropagateArgs {
     const unsigned long long *flat_best;   // shade_kernel: results of the flat walks (FLAT_HIT entries of hits)
     uint32_t *zero_word;               // shade_kernel: word cleared once (next step's flat-walk count)
     uint32_t *diag;                    // multi-step kernels (nullptr: off): [0] += flat walks walked whole,
-                                       // [1] max steps of one photon, [2..3] u64 max of (cycles << 16 | steps)
+                                       // [1] max steps of one photon, [2..3] u64 max of (cycles << 16 | steps),
+                                       // [4..13] u64 sums over photons of > 64 steps (tail kernel): walk
+                                       // ticks, step ticks, walk iterations, steps, photons
 };
 // hits[q] = (FLAT_HIT, f): queue position q holds flat walk f of this step,
 // its result is flat_best[f] (trace_kernel)
@@ -1684,6 +1687,320 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_group_kernel(const DevG
     if (have_rng && sub == 0) store_rng(a, slot, rng);
     if (sub == 0 && overflow) atomicAdd(a.counters, overflow);
     if (sub == 0 && cnt.flat && a.diag) atomicAdd(a.diag, cnt.flat);
+}
+
+// ---------------------------------------------------------------- wave-adaptive tail
+// The multi-step tail launch lasts as long as its longest-lived photon: on the
+// 29k detector one photon bouncing ~500 times between opposite walls set
+// 12-25 ms launches at ~25 us per step (r02 tail diagnostics), with the rest of
+// the chip idle.  Here the 64 lanes of a wave hold 8 photons (8 lanes each, as
+// propagate_group_kernel) and run one step of each per iteration; the walk of
+// an iteration spreads the whole wave over the photons that walk in it: with w
+// walkers each gets a segment of Gs = 64 / pow2ceil(w) lanes = P = Gs/8
+// sub-groups of 8, and a segment advances P depth-first cursors over one
+// shared LDS stack (P nodes per dependent fetch), then tests every triangle of
+// the iteration's hit leaves at once, one per lane (not leaf after leaf).  The
+// physics of a step stays with the photon's own 8 lanes.  Culling uses the
+// segment's best of the previous iteration (never below the final one) and the
+// nearest hit is the min over (distance, reference rank) with the reference
+// leaf check of every other walk, so the result does not depend on P.
+constexpr int TAIL_STACK = 128;   // stack entries per 8 lanes; a segment of Gs lanes holds TAIL_STACK * Gs / 8
+constexpr int TAIL_TRI = 4 * 64;  // triangle-list words per wave (<= 4 triangles per lane per iteration)
+
+// All 64 lanes call this (converged).  act: the segment has a ray (segment-
+// uniform).  Returns the nearest triangle (-1: none) and its distance in
+// every lane of the segment.
+__device__ int walk_segment(const DevGeom &g, bool act, V3 o, V3 d, uint32_t last, int Gs,
+                            CHR_LDS uint32_t *stk, int cap, CHR_LDS uint32_t *tlist, uint32_t &overflow,
+                            float &min_distance, uint32_t &iters) {
+    constexpr uint32_t INVALID = 0xFFFFFFFFu;
+    constexpr unsigned long long NONE = ~0ull;
+    const uint32_t lane = __lane_id();
+    const uint32_t seg0 = lane & ~(uint32_t)(Gs - 1);
+    const uint32_t L = lane - seg0;                   // lane within the segment
+    const uint32_t k = L & 7u;                        // child slot of this lane
+    const unsigned long long segmask = Gs == 64 ? ~0ull : (((1ull << Gs) - 1ull) << seg0);
+    const unsigned long long below = (1ull << lane) - 1ull;
+    const V3 noid = v3(-o.x / d.x, -o.y / d.y, -o.z / d.z);
+    const V3 inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    const RaySlab r = make_slab(noid, inv);
+    float best = __builtin_inff();
+    uint32_t best_rank = 0xFFFFFFFFu;
+    int best_id = -1;
+    uint32_t cur = (act && L < 8u) ? 0u : INVALID;   // cursor 0 starts at the root
+    float cur_t = 0.0f;
+    int sp = 0;
+    bool done = !act;
+    iters = 0;
+    while (__ballot(!done) != 0) {
+        if (done) continue;
+        iters++;
+        // cursors without a node take unculled stack entries, in sub-group order
+        unsigned long long em = __ballot(k == 0u && cur == INVALID) & segmask;
+        while (em != 0 && sp > 0) {
+            sp--;
+            const uint32_t en = stk[2 * sp], et = stk[2 * sp + 1];
+            if (__uint_as_float(et) > best) continue;     // mesh.h:94-96
+            if ((lane & ~7u) == (uint32_t)(__ffsll((long long)em) - 1)) { cur = en; cur_t = __uint_as_float(et); }
+            em &= em - 1;
+        }
+        if ((__ballot(cur != INVALID) & segmask) == 0) { done = true; continue; }
+        // expand: sub-group j's 8 lanes slab-test the 8 children of its node
+        bool inner = false, leafhit = false;
+        float tk = 0.0f;
+        uint32_t kind = 0, child = 0, first = 0, near = INVALID;
+        uint4 a4 = make_uint4(0u, 0u, 0u, 0u), a5 = a4;
+        if (cur != INVALID) {
+            const uint4 *np = g.wnodes + (size_t)g.wstride * cur;
+            const uint4 h = gld(np), a1 = gld(np + 1), a2 = gld(np + 2), a3 = gld(np + 3);
+            a4 = gld(np + 4);
+            a5 = gld(np + 5);
+            const V3 org = v3(__uint_as_float(h.x), __uint_as_float(h.y), __uint_as_float(h.z));
+            const float sx = exp_scale(h.w), sy = exp_scale(h.w >> 8), sz = exp_scale(h.w >> 16);
+            const int kk = (int)k;
+            kind = byte_of(a4.z, a4.w, kk);
+            const float tnx = __builtin_fmaf(__builtin_fmaf(byte_f(r.negx ? a2.z : a1.x, r.negx ? a2.w : a1.y, kk), sx, org.x), r.inx, r.onx);
+            const float tfx = __builtin_fmaf(__builtin_fmaf(byte_f(r.negx ? a1.x : a2.z, r.negx ? a1.y : a2.w, kk), sx, org.x), r.inx, r.ofx);
+            const float tny = __builtin_fmaf(__builtin_fmaf(byte_f(r.negy ? a3.x : a1.z, r.negy ? a3.y : a1.w, kk), sy, org.y), r.iny, r.ony);
+            const float tfy = __builtin_fmaf(__builtin_fmaf(byte_f(r.negy ? a1.z : a3.x, r.negy ? a1.w : a3.y, kk), sy, org.y), r.iny, r.ofy);
+            const float tnz = __builtin_fmaf(__builtin_fmaf(byte_f(r.negz ? a3.z : a2.x, r.negz ? a3.w : a2.y, kk), sz, org.z), r.inz, r.onz);
+            const float tfz = __builtin_fmaf(__builtin_fmaf(byte_f(r.negz ? a2.x : a3.z, r.negz ? a2.y : a3.w, kk), sz, org.z), r.inz, r.ofz);
+            const float tmin = __builtin_fmaxf(__builtin_fmaxf(__builtin_fmaxf(tnx, tny), tnz), 0.0f);
+            const float tmax = __builtin_fminf(__builtin_fminf(tfx, tfy), tfz);
+            const bool hit = (kind != 0u) & !(tmin > tmax) & !(tmin > best);
+            inner = hit & (kind == WIDE_INNER);
+            leafhit = hit & (kind != WIDE_INNER);
+            tk = tmin;
+            const uint32_t off = byte_of(a5.x, a5.y, kk);
+            child = a4.x + off;
+            first = a4.y + off;
+        }
+        // each sub-group continues with its nearest inner child (first of the
+        // smallest entry distance) and pushes the others
+        unsigned long long key = inner ? (((unsigned long long)__float_as_uint(tk) << 32) | k) : NONE;
+#pragma unroll
+        for (int off = 1; off < 8; off <<= 1) {
+            const unsigned long long other = __shfl_xor(key, off, 8);
+            key = other < key ? other : key;
+        }
+        float near_t = 0.0f;
+        if (key != NONE) {
+            near = a4.x + byte_of(a5.x, a5.y, (int)(key & 7u));
+            near_t = __uint_as_float((uint32_t)(key >> 32));
+        }
+        const bool push = inner && (key & 7u) != k;
+        const unsigned long long pm = __ballot(push) & segmask;
+        const int pos = sp + __popcll(pm & below);
+        if (push && pos < cap) {
+            stk[2 * pos] = child;
+            stk[2 * pos + 1] = __float_as_uint(tk);
+        }
+        const int npush = __popcll(pm);
+        if (sp + npush > cap) {
+            if (L == 0) overflow += (uint32_t)(sp + npush - cap);
+            sp = cap;
+        } else {
+            sp += npush;
+        }
+        cur = near;
+        cur_t = near_t;
+        // the iteration's hit-leaf triangles, listed in lane order, one per lane
+        const uint32_t cnt = leafhit ? kind : 0u;
+        const unsigned long long b0 = __ballot(cnt & 1u) & segmask, b1 = __ballot(cnt & 2u) & segmask,
+                                 b2 = __ballot(cnt & 4u) & segmask;
+        const uint32_t pre = __popcll(b0 & below) + 2u * __popcll(b1 & below) + 4u * __popcll(b2 & below);
+        const uint32_t T = __popcll(b0) + 2u * __popcll(b1) + 4u * __popcll(b2);
+        for (uint32_t t = 0; t < cnt; ++t) tlist[pre + t] = first + t;
+        __builtin_amdgcn_wave_barrier();
+        float lbest = best;
+        uint32_t lrank = best_rank;
+        int lid = -1;
+        for (uint32_t i = L; i < T; i += (uint32_t)Gs) {
+            const float4 *rr = g.wtri + 4 * (size_t)tlist[i];
+            const float4 r0 = gld(rr), r1 = gld(rr + 1), r2 = gld(rr + 2);
+            const uint32_t id = __float_as_uint(r2.y);
+            float dist;
+            if (id == last ||
+                !intersect_triangle(o, d, v3(r0.x, r0.y, r0.z), v3(r0.w, r1.x, r1.y), v3(r1.z, r1.w, r2.x), dist))
+                continue;
+            const uint32_t rank = __float_as_uint(r2.z);
+            if (!(dist < lbest || (dist == lbest && rank < lrank))) continue;
+            const float4 r3 = gld(rr + 3);
+            V3 lo, hi;
+            node_bounds(g, make_uint4(__float_as_uint(r2.w), __float_as_uint(r3.x), __float_as_uint(r3.y), 0u), lo, hi);
+            float bd;
+            if (!intersect_box(noid, inv, lo, hi, bd) || bd > lbest) continue;   // mesh.h:94-96
+            lbest = dist;
+            lrank = rank;
+            lid = (int)id;
+        }
+        __builtin_amdgcn_wave_barrier();   // list reads land before the next iteration's writes
+        unsigned long long lkey = lid == -1 ? NONE : (((unsigned long long)__float_as_uint(lbest) << 32) | lrank);
+        for (int off = 1; off < Gs; off <<= 1) {
+            const unsigned long long ok = __shfl_xor(lkey, off);
+            const int oid = __shfl_xor(lid, off);
+            if (ok < lkey) { lkey = ok; lid = oid; }
+        }
+        if (lkey != NONE) {
+            best = __uint_as_float((uint32_t)(lkey >> 32));
+            best_rank = (uint32_t)lkey;
+            best_id = lid;
+        }
+        if (cur != INVALID && cur_t > best) cur = INVALID;
+    }
+    min_distance = best_id == -1 ? -1.0f : best;
+    return best_id;
+}
+
+template <int MINW>
+__global__ __launch_bounds__(BLOCK, MINW) void propagate_tail_kernel(const DevGeom *__restrict__ gdev, PropagateArgs a,
+                                                                     uint32_t cap) {
+    __shared__ uint32_t stacks[(BLOCK / 8) * TAIL_STACK * 2];
+    __shared__ uint32_t tris[(BLOCK / 64) * TAIL_TRI];
+    const uint32_t tid = blockIdx.x * BLOCK + threadIdx.x;
+    const uint32_t lane = __lane_id();
+    const uint32_t slot = tid / 8, sub = tid & 7u;
+    const uint32_t n = (uint32_t)a.nthreads;
+    const uint32_t nslot = cap < n ? cap : n;
+    if ((tid & ~63u) / 8 >= nslot) return;             // whole waves: the others help walk
+    CHR_LDS uint32_t *wstack = (CHR_LDS uint32_t *)stacks + (threadIdx.x >> 6) * 8 * TAIL_STACK * 2;
+    CHR_LDS uint32_t *wtris = (CHR_LDS uint32_t *)tris + (threadIdx.x >> 6) * TAIL_TRI;
+    const DevGeom &g = *gdev;
+    chr_xorwow rng;
+    bool have_rng = false;
+    uint32_t overflow = 0, flat = 0;
+    Photon p;
+    State s;
+    int steps = 0, scatter_first = 0;
+    uint32_t q = slot, pid = 0, iters = 0;
+    bool live = false, exhausted = slot >= nslot;
+    unsigned long long t0 = 0, walk_ticks = 0;
+    // run_photon's write-back (propagate.cu:343-353) and the alive bit
+    auto finish = [&]() {
+        store3(a.pos, pid, p.pos);
+        store3(a.dir, pid, p.dir);
+        store3(a.pol, pid, p.pol);
+        a.wl[pid] = p.wavelength;
+        a.t[pid] = p.time;
+        a.flags[pid] = p.history;
+        a.last_hit[pid] = p.last_hit;
+        a.weights[pid] = p.weight;
+        if (sub == 0) {
+            if ((p.history & DEAD_MASK) == 0) atomicOr(a.alive_masks + (q >> 6), 1ull << (q & 63u));
+            if (a.diag) {   // the tail's serial chain: longest photon in steps and in time
+                const unsigned long long cyc = __builtin_amdgcn_s_memrealtime() - t0;
+                atomicMax(a.diag + 1, (uint32_t)steps);
+                atomicMax(reinterpret_cast<unsigned long long *>(a.diag + 2),
+                          (cyc << 16) | (unsigned long long)(steps > 0xFFFF ? 0xFFFF : steps));
+                if (steps > 64) {   // where a long-lived photon's step time goes
+                    unsigned long long *d64 = reinterpret_cast<unsigned long long *>(a.diag + 4);
+                    atomicAdd(d64, walk_ticks);
+                    atomicAdd(d64 + 1, cyc);
+                    atomicAdd(d64 + 2, (unsigned long long)iters);
+                    atomicAdd(d64 + 3, (unsigned long long)steps);
+                    atomicAdd(d64 + 4, 1ull);
+                }
+            }
+        }
+        live = false;
+        q += cap;
+    };
+    while (true) {
+        if (!live && !exhausted) {   // the slot's next queued photon (dead on entry: skipped, no write-back)
+            while (q < n) {
+                pid = a.input_queue[q];
+                const uint32_t history = a.flags[pid] & 0xFFFFu;   // photon.h:29
+                if (history & DEAD_MASK) { q += cap; continue; }
+                if (!have_rng) { load_rng(a, slot, rng); have_rng = true; }
+                p.history = history;
+                p.pos = load3(a.pos, pid);
+                p.dir = load3(a.dir, pid);
+                p.dir = p.dir / norm(p.dir);
+                p.pol = load3(a.pol, pid);
+                p.pol = p.pol / norm(p.pol);
+                p.wavelength = a.wl[pid];
+                p.time = a.t[pid];
+                p.last_hit = a.last_hit[pid];
+                p.weight = a.weights[pid];
+                steps = 0;
+                iters = 0;
+                walk_ticks = 0;
+                scatter_first = a.scatter_first;
+                live = true;
+                t0 = __builtin_amdgcn_s_memrealtime();   // 100 MHz
+                break;
+            }
+            if (!live) exhausted = true;
+        }
+        if (__ballot(live) == 0) break;
+        // step head (propagate.cu:279-285 / run_photon)
+        bool walk = false;
+        if (live) {
+            if (steps < a.max_steps) {
+                steps++;
+                const float prod = ((((p.dir.x * p.dir.y) * p.dir.z) * p.pos.x) * p.pos.y) * p.pos.z;
+                if (chr_isnan(prod)) p.history |= CHR_NO_HIT | CHR_NAN_ABORT;
+                else walk = true;
+            }
+            if (!walk) finish();
+        }
+        // the walk, spread over the wave
+        const unsigned long long wm = __ballot(walk && sub == 0);   // bit 8g: group g walks
+        int tri = -1;
+        float dist = -1.0f;
+        const int w = __popcll(wm);
+        const unsigned long long tw0 = __builtin_amdgcn_s_memrealtime();
+        if (w > 0) {
+            const int Gs = w == 1 ? 64 : (w == 2 ? 32 : (w <= 4 ? 16 : 8));
+            const int si = (int)lane / Gs;
+            unsigned long long m = wm;
+            for (int i = 0; i < si && m != 0; ++i) m &= m - 1;
+            const int src = m != 0 ? __ffsll((long long)m) - 1 : (int)(lane & ~7u);
+            const bool act = m != 0;
+            const V3 o = v3(__shfl(p.pos.x, src), __shfl(p.pos.y, src), __shfl(p.pos.z, src));
+            const V3 dd = v3(__shfl(p.dir.x, src), __shfl(p.dir.y, src), __shfl(p.dir.z, src));
+            const uint32_t last = (uint32_t)__shfl(p.last_hit, src);
+            const uint32_t seg0 = lane & ~(uint32_t)(Gs - 1);
+            float sd;
+            uint32_t it;
+            const int st = walk_segment(g, act, o, dd, last, Gs, wstack + seg0 / 8 * TAIL_STACK * 2,
+                                        TAIL_STACK * Gs / 8, wtris + 4 * seg0, overflow, sd, it);
+            const int mine = __popcll(wm & ((1ull << (lane & ~7u)) - 1ull)) * Gs;   // my group's segment
+            tri = __shfl(st, mine);
+            dist = __shfl(sd, mine);
+            it = (uint32_t)__shfl((int)it, mine);
+            if (walk) {
+                iters += it;
+                walk_ticks += __builtin_amdgcn_s_memrealtime() - tw0;
+            }
+        }
+        if (walk) {   // the rest of the step (run_photon's loop body)
+            if (sub == 0) {
+                const V3 inv = v3(1.0f / p.dir.x, 1.0f / p.dir.y, 1.0f / p.dir.z);
+                if (!(chr_isfinite(inv.x) && chr_isfinite(inv.y) && chr_isfinite(inv.z))) flat++;
+            }
+            s.distance = dist;
+            finish_fill(g, s, p, tri);
+            bool stop = p.last_hit == -1;
+            if (!stop) {
+                int command = propagate_to_boundary(g, p, s, rng, a.use_weights, scatter_first);
+                scatter_first = 0;
+                if (command == BREAK) {
+                    stop = true;
+                } else if (command == PASS) {
+                    if (s.surface_index != -1) {
+                        command = propagate_at_surface(g, p, s, rng, a.use_weights);
+                        if (command == BREAK) stop = true;
+                    }
+                    if (command == PASS) propagate_at_boundary(p, s, rng);
+                }
+            }
+            if (stop) finish();
+        }
+    }
+    if (have_rng && sub == 0) store_rng(a, slot, rng);
+    if (sub == 0 && overflow) atomicAdd(a.counters, overflow);
+    if (sub == 0 && flat && a.diag) atomicAdd(a.diag, flat);
 }
 
 // ---------------------------------------------------------------- ray binning (trace order)
@@ -2403,6 +2720,11 @@ static constexpr int kExactVariant = 1;
 // launch lasts as long as its longest-lived photon, so fewer resident waves
 // means more rounds of waves behind it)
 static constexpr int kGroupWaves = 4;
+static constexpr int kTailWaves = 4;   // propagate_tail_kernel (wave-adaptive walk)
+static bool tail_group_walk() {        // CHR_TAIL=group: the fixed 8-lane group kernel (A/B)
+    const char *e = getenv("CHR_TAIL");
+    return e && std::strcmp(e, "group") == 0;
+}
 static bool wide_queue_ok(const chr_geometry *g) { return g->dev.nwtri < (1u << 30); }   // 30-bit leaf queue entries
 
 // one launch per chunk (the reference's launch structure: slot counts that are
@@ -2460,7 +2782,7 @@ static StepVariant select_step_variant(const chr_geometry *g) {
             sv.fn = propagate_step_kernel<8, 4, kWalk>;
             sv.trace = trace_kernel<false, 6, 12, 4, 32>;
             sv.shade = shade_kernel<3>;
-            sv.tail = propagate_group_kernel<8, kGroupWaves>;
+            sv.tail = tail_group_walk() ? propagate_group_kernel<8, kGroupWaves> : propagate_tail_kernel<kTailWaves>;
             sv.tail_group = 8;
             sv.binned = v == 7 ? 1 : (v == 8 ? 0 : 2);
             break;
@@ -2675,7 +2997,7 @@ static int pinned_words(uint32_t **out) {
     static thread_local uint32_t *p[16] = {};
     int dev = 0;
     CHR_HIP_CHECK(hipGetDevice(&dev));
-    if (!p[dev & 15]) CHR_HIP_CHECK(hipHostMalloc((void **)&p[dev & 15], 128, hipHostMallocDefault));
+    if (!p[dev & 15]) CHR_HIP_CHECK(hipHostMalloc((void **)&p[dev & 15], 256, hipHostMallocDefault));
     *out = p[dev & 15];
     return CHR_OK;
 }
@@ -2761,7 +3083,7 @@ extern "C" int chr_propagate(const chr_geometry *g, const chr_photons *ph, uint3
     FlatCtx fc{};
     if (fused) {
         if ((rc = flat_get(nphotons, fc))) return rc;
-        CHR_HIP_CHECK(hipMemsetAsync(fc.ctl, 0, 64, stream));
+        CHR_HIP_CHECK(hipMemsetAsync(fc.ctl, 0, 128, stream));
         fc.enrol_next = true;
     }
     const size_t max_chunks = fused ? 2 : (nphotons + chunk_cap - 1) / chunk_cap;   // fused: step + its walk
@@ -2861,7 +3183,7 @@ extern "C" int chr_propagate(const chr_geometry *g, const chr_photons *ph, uint3
     }
     CHR_HIP_CHECK(hipMemcpyAsync(pinned + 2, scratch, 4, hipMemcpyDeviceToHost, stream));
     CHR_HIP_CHECK(hipMemcpyAsync(pinned + 4, scratch + 2, 56, hipMemcpyDeviceToHost, stream));
-    if (fused) CHR_HIP_CHECK(hipMemcpyAsync(pinned + 20, fc.ctl + 3, 20, hipMemcpyDeviceToHost, stream));
+    if (fused) CHR_HIP_CHECK(hipMemcpyAsync(pinned + 20, fc.ctl + 3, 60, hipMemcpyDeviceToHost, stream));
     CHR_HIP_CHECK(hipStreamSynchronize(stream));
     st.stack_overflows = pinned[2];
     st.flat_walks = fused ? pinned[20] : 0u;
@@ -2872,6 +3194,13 @@ extern "C" int chr_propagate(const chr_geometry *g, const chr_photons *ph, uint3
         st.tail_max_steps = pinned[22];
         st.tail_max_cycles = key >> 16;
         st.tail_slowest_steps = (uint32_t)(key & 0xFFFFu);
+        uint64_t lp[5];
+        std::memcpy(lp, pinned + 25, 40);   // ctl[8..17]
+        st.tail_long_walk_ticks = lp[0];
+        st.tail_long_ticks = lp[1];
+        st.tail_long_walk_iterations = lp[2];
+        st.tail_long_steps = lp[3];
+        st.tail_long_photons = (uint32_t)lp[4];
     }
     {
         uint64_t c[7];
@@ -2965,7 +3294,7 @@ extern "C" int chr_kernel_info(int32_t which, chr_kernel_attr *out) {
     switch (which) {
         case 0: fn = (const void *)trace_kernel<false, 6, 12, 4, 32>; name = "chr::trace_kernel<false,6,12,4,32>"; break;
         case 1: fn = (const void *)shade_kernel<3>; name = "chr::shade_kernel<3>"; break;
-        case 2: fn = (const void *)propagate_group_kernel<8, kGroupWaves>; name = "chr::propagate_group_kernel<8,4>"; break;
+        case 2: fn = (const void *)propagate_tail_kernel<kTailWaves>; name = "chr::propagate_tail_kernel<4>"; break;
         case 3: fn = (const void *)propagate_step_kernel<8, 4, kWalk>; name = "chr::propagate_step_kernel<8,4,2006>"; break;
         default: return chr::fail(CHR_ERR_INVALID, "chr_kernel_info: unknown kernel %d", which);
     }
@@ -2991,3 +3320,7 @@ extern "C" int chr_distance_to_mesh(const chr_geometry *g, uint32_t n, const flo
     CHR_HIP_CHECK(hipGetLastError());
     return CHR_OK;
 }
+
+// The renderer (render.cu, hybrid_render.cu, transform.cu): same translation
+// unit, it walks the same BVH and runs the same photon physics.
+#include "render.hip"

@@ -180,6 +180,12 @@ typedef struct chr_propagate_stats {
     uint32_t tail_max_steps;      /* most steps one photon ran in the tail launch */
     uint32_t tail_slowest_steps;  /* steps of the photon that took longest in the tail launch */
     uint64_t tail_max_cycles;     /* that photon's time in ticks of the 100 MHz s_memrealtime clock */
+    uint32_t tail_long_photons;   /* photons of > 64 steps in the tail launch, and summed over them: */
+    uint32_t reserved2;
+    uint64_t tail_long_steps;     /*   steps, */
+    uint64_t tail_long_ticks;     /*   100 MHz ticks from load to write-back, */
+    uint64_t tail_long_walk_ticks;        /*   ticks in the BVH walk (wave-adaptive tail kernel), */
+    uint64_t tail_long_walk_iterations;   /*   and dependent walk iterations */
 } chr_propagate_stats;
 #define CHR_TRACE_MS_MAX 32
 
@@ -353,6 +359,43 @@ int chr_pdf_accumulate_kernel_eval(int32_t time_only, int32_t nchannels, const u
                                    float qmin, float qmax, const float *d_inv_time_bw,
                                    const float *d_inv_charge_bw, uint32_t *d_hitcount, float *d_time_pdf,
                                    float *d_charge_pdf, void *stream);
+
+/* ---------------------------------------------------------------- renderer
+ * replaces: the `render` kernel (chroma/cuda/render.cu:37-183) as launched by
+ * GPURays.render (chroma/gpu/render.py:47-62).  Rays float3-packed [n*3] (not
+ * normalised, as the reference); d_colors: one ARGB word per triangle
+ * (reference GPUGeometry.colors); per ray: d_dx / d_color (float4) hold
+ * alpha_depth entries, d_dxlen the entries kept (0 = start afresh; a
+ * non-zero count merges this render into the previous one, keep_last_render).
+ * d_pixels[i] = composited ARGB or bg_color. */
+int chr_render(const chr_geometry *g, uint32_t nrays, const float *d_pos, const float *d_dir,
+               const uint32_t *d_colors, uint32_t alpha_depth, uint32_t *d_pixels, float *d_dx,
+               uint32_t *d_dxlen, float *d_color, uint32_t bg_color, void *stream);
+/* replaces: transform.cu:9-48 (translate / rotate / rotate_around_point of float3 arrays,
+ * GPURays.translate/rotate/rotate_around_point, gpu/render.py:30-45) */
+int chr_transform_translate(uint32_t n, float *d_a, float vx, float vy, float vz, void *stream);
+int chr_transform_rotate(uint32_t n, float *d_a, float phi, float ax, float ay, float az, void *stream);
+int chr_transform_rotate_around_point(uint32_t n, float *d_a, float phi, float ax, float ay, float az,
+                                      float px, float py, float pz, void *stream);
+/* replaces: hybrid_render.cu:61-131 update_xyz_lookup (camera.py:246-258): work-item k
+ * (k < nthreads, triangle id = k + offset < total_threads, RNG slot k) shoots light from
+ * position[3] at a random point of its triangle; if that triangle is the first hit, the
+ * photon is propagated to its first diffuse reflection and cos_theta * xyz[3] is added to
+ * the reflecting triangle's float3 entry of d_lookup1 (inside-to-outside) or d_lookup2.
+ * d_vertices / d_triangles: the mesh (float3 / uint3 packed). */
+int chr_hybrid_update_xyz_lookup(const chr_geometry *g, const float *d_vertices, const uint32_t *d_triangles,
+                                 int32_t nthreads, int32_t total_threads, int32_t offset, const float *position,
+                                 uint32_t *d_rng_states, uint32_t rng_nslots, float wavelength, const float *xyz,
+                                 float *d_lookup1, float *d_lookup2, int32_t max_steps, void *stream);
+/* replaces: hybrid_render.cu:133-166 update_xyz_image (camera.py:260-275) */
+int chr_hybrid_update_xyz_image(const chr_geometry *g, int32_t nthreads, uint32_t *d_rng_states,
+                                uint32_t rng_nslots, const float *d_positions, const float *d_directions,
+                                float wavelength, const float *xyz, const float *d_lookup1,
+                                const float *d_lookup2, float *d_image, int32_t nlookup_calls,
+                                int32_t max_steps, void *stream);
+/* replaces: hybrid_render.cu:168-200 process_image (camera.py:277-282) */
+int chr_hybrid_process_image(int32_t nthreads, const float *d_image, uint32_t *d_pixels, int32_t nimages,
+                             void *stream);
 
 /* ------------------------------------------------------------ self tests
  * The reference's unit-test kernels, run over this build's device math (the

@@ -1252,3 +1252,242 @@ EXPORT int orc_daq(const float *t, const uint32_t *flags, const int32_t *last_hi
     }
     return 0;
 }
+
+/* ================================================================ renderer
+ * render.cu:37-183, transform.cu:9-48, hybrid_render.cu:17-200, sorting.h:58-97,
+ * restated sequentially: the reference BVH walked in the reference order with
+ * no pruning, each hit inserted at searchsorted's position as it is found. */
+
+/* sorting.h:62-88 */
+static unsigned long searchsorted_f(unsigned long n, const float *arr, float x) {
+    unsigned long ju, jm, jl;
+    int ascnd;
+    jl = 0;
+    ju = n;
+    ascnd = (arr[n - 1] >= arr[0]);
+    while (ju - jl > 1) {
+        jm = (ju + jl) >> 1;
+        if ((x > arr[jm]) == ascnd) jl = jm;
+        else ju = jm;
+    }
+    if ((x <= arr[0]) == ascnd) return 0;
+    return ju;
+}
+
+/* render.cu:12-32 */
+static void get_color(f3 direction, f3 v0, f3 v1, f3 v2, uint32_t rgba, float out[4]) {
+    f3 n = normalize(cross(sub(v1, v0), sub(v2, v1)));
+    float c = dot(n, neg(direction));
+    if (c < 0.0f) c = -c;
+    uint32_t a0 = 0xFFu & (rgba >> 24), r0 = 0xFFu & (rgba >> 16), g0 = 0xFFu & (rgba >> 8), b0 = 0xFFu & rgba;
+    out[0] = (float)r0 * c;
+    out[1] = (float)g0 * c;
+    out[2] = (float)b0 * c;
+    out[3] = (float)(255u - a0) / 255.0f;
+}
+
+EXPORT int orc_render(const chr_geometry_desc *d, int nrays, const float *origin, const float *direction,
+                      const uint32_t *colors, uint32_t alpha_depth, uint32_t *pixels, float *dx_all, uint32_t *dxlen,
+                      float *color_all, uint32_t bg_color) {
+    init_once();
+    if (alpha_depth < 1) return CHR_ERR_INVALID;
+#pragma omp parallel for schedule(dynamic, 64)
+    for (int id = 0; id < nrays; ++id) {
+        Geo g = {d, 0, 0, 0, 0, 0};
+        f3 o = mk(origin[3 * id], origin[3 * id + 1], origin[3 * id + 2]);
+        f3 dir = mk(direction[3 * id], direction[3 * id + 1], direction[3 * id + 2]);
+        uint32_t n = dxlen[id];
+        f3 noid = mk(-o.x / dir.x, -o.y / dir.y, -o.z / dir.z);
+        f3 inv = mk(1.0f / dir.x, 1.0f / dir.y, 1.0f / dir.z);
+        Node root = get_node(&g, 0);
+        if (n < 1 && !intersect_node(noid, inv, &root, -1.0f)) { pixels[id] = bg_color; continue; }
+        uint32_t *cs = (uint32_t *)malloc(sizeof(uint32_t) * 2 * STACK_SIZE), *ns = cs + STACK_SIZE;
+        cs[0] = root.child;
+        ns[0] = root.nchild;
+        int curr = 0;
+        float *dx = dx_all + (size_t)id * alpha_depth;
+        float *col = color_all + 4 * (size_t)id * alpha_depth;
+        while (curr >= 0) {
+            uint32_t first = cs[curr], nchild = ns[curr];
+            curr--;
+            for (uint32_t i = first; i < first + nchild; i++) {
+                Node node = get_node(&g, i);
+                if (!intersect_node(noid, inv, &node, -1.0f)) continue;
+                if (node.nchild == 0) {
+                    f3 v0, v1, v2;
+                    float distance;
+                    get_triangle(&g, node.child, &v0, &v1, &v2);
+                    if (!intersect_triangle(o, dir, v0, v1, v2, &distance)) continue;
+                    float c4[4];
+                    if (n < 1) {
+                        dx[0] = distance;
+                        get_color(dir, v0, v1, v2, colors[node.child], c4);
+                        memcpy(col, c4, 16);
+                    } else {
+                        unsigned long j = searchsorted_f(n, dx, distance);
+                        if (j <= alpha_depth - 1) {
+                            for (unsigned long k = alpha_depth - 1; k > j; k--) dx[k] = dx[k - 1];   /* insert() */
+                            dx[j] = distance;
+                            get_color(dir, v0, v1, v2, colors[node.child], c4);
+                            for (unsigned long k = alpha_depth - 1; k > j; k--) memcpy(col + 4 * k, col + 4 * (k - 1), 16);
+                            memcpy(col + 4 * j, c4, 16);
+                        }
+                    }
+                    if (n < alpha_depth) n++;
+                } else if (curr + 1 < STACK_SIZE) {
+                    curr++;
+                    cs[curr] = node.child;
+                    ns[curr] = node.nchild;
+                }
+            }
+        }
+        free(cs);
+        if (n < 1) { pixels[id] = bg_color; continue; }
+        dxlen[id] = n;
+        float scale = 1.0f, fr = 0.0f, fg = 0.0f, fb = 0.0f;
+        for (uint32_t i = 0; i < n; i++) {
+            float alpha = col[4 * i + 3];
+            fr = fmaf(scale * col[4 * i], alpha, fr);
+            fg = fmaf(scale * col[4 * i + 1], alpha, fg);
+            fb = fmaf(scale * col[4 * i + 2], alpha, fb);
+            scale *= (1.0f - alpha);
+        }
+        float alpha = (float)((double)((bg_color & 0xFF000000u) >> 24) / 255.0);
+        fr = fmaf(scale * (float)((bg_color & 0xFF0000u) >> 16), alpha, fr);
+        fg = fmaf(scale * (float)((bg_color & 0xFF00u) >> 8), alpha, fg);
+        fb = fmaf(scale * (float)(bg_color & 0xFFu), alpha, fb);
+        scale *= (1.0f - alpha);
+        uint32_t a = n < alpha_depth ? chr_sat_u32(floorf(255.0f * (1.0f - scale))) : 255u;
+        uint32_t red = chr_sat_u32(floorf(fr / (1.0f - scale)));
+        uint32_t green = chr_sat_u32(floorf(fg / (1.0f - scale)));
+        uint32_t blue = chr_sat_u32(floorf(fb / (1.0f - scale)));
+        pixels[id] = a << 24 | red << 16 | green << 8 | blue;
+    }
+    return 0;
+}
+
+/* transform.cu: mode 0 translate(v), 1 rotate(phi, axis), 2 rotate_around_point(phi, axis, v) */
+EXPORT void orc_transform(int n, float *a, int mode, float phi, const float *axis, const float *v) {
+    f3 ax = mk(axis[0], axis[1], axis[2]), vv = mk(v[0], v[1], v[2]);
+    for (int i = 0; i < n; ++i) {
+        f3 x = mk(a[3 * i], a[3 * i + 1], a[3 * i + 2]);
+        if (mode == 0) x = add(x, vv);
+        else if (mode == 1) x = rotate(x, phi, ax);
+        else x = add(rotate(sub(x, vv), phi, ax), vv);
+        a[3 * i] = x.x; a[3 * i + 1] = x.y; a[3 * i + 2] = x.z;
+    }
+}
+
+/* hybrid_render.cu:17-55 */
+static void to_diffuse(Geo *g, Photon *p, State *s, chr_xorwow *rng, int max_steps) {
+    int steps = 0;
+    while (steps < max_steps) {
+        steps++;
+        fill_state(g, s, p);
+        if (p->last_hit_triangle == -1) break;
+        int command = propagate_to_boundary(g, p, s, rng, 0, 0);
+        if (command == BREAK) break;
+        if (command == CONTINUE) continue;
+        if (s->surface_index != -1) {
+            command = propagate_at_surface(g, p, s, rng, 0);
+            if (p->history & CHR_REFLECT_DIFFUSE) break;
+            if (command == BREAK) break;
+            if (command == CONTINUE) continue;
+        }
+        propagate_at_boundary(p, s, rng);
+    }
+}
+
+/* hybrid_render.cu:61-131, work-items in id order (the lookup sums are float
+ * adds in that order; the device's atomic adds may order them differently) */
+EXPORT void orc_hybrid_update_xyz_lookup(const chr_geometry_desc *d, int nthreads, int total_threads, int offset,
+                                         const float *position, uint32_t *rng, uint32_t nslots, float wavelength,
+                                         const float *xyz, float *lookup1, float *lookup2, int max_steps) {
+    init_once();
+    Geo g = {d, 0, 0, 0, 0, 0};
+    f3 pos = mk(position[0], position[1], position[2]), w = mk(xyz[0], xyz[1], xyz[2]);
+    for (int kid = 0; kid < nthreads; ++kid) {
+        int id = kid + offset;
+        if (id >= total_threads) break;
+        chr_xorwow r;
+        rng_load(rng, nslots, (uint32_t)kid, &r);
+        f3 v0, v1, v2;
+        get_triangle(&g, (uint32_t)id, &v0, &v1, &v2);
+        float a = chr_uniform01(&r);
+        float b = chr_uniform(&r, 0.0f, 1.0f - a);
+        float c = (1.0f - a) - b;
+        f3 dir = sub(mk(fmaf(c, v2.x, fmaf(b, v1.x, a * v0.x)), fmaf(c, v2.y, fmaf(b, v1.y, a * v0.y)),
+                        fmaf(c, v2.z, fmaf(b, v1.z, a * v0.z))), pos);
+        dir = divf(dir, norm(dir));
+        float distance;
+        int hit = intersect_mesh(&g, pos, dir, &distance, -1);
+        if (hit == id) {
+            f3 nrm = normalize(cross(sub(v1, v0), sub(v2, v1)));
+            float cos_theta = dot(nrm, neg(dir));
+            if (cos_theta < 0.0f) cos_theta = dot(neg(nrm), neg(dir));
+            Photon p;
+            memset(&p, 0, sizeof(p));
+            p.pos = pos;
+            p.dir = dir;
+            p.wavelength = wavelength;
+            p.pol = uniform_sphere(&r);
+            p.last_hit_triangle = -1;
+            p.weight = 1.0f;
+            State s;
+            to_diffuse(&g, &p, &s, &r, max_steps);
+            if ((p.history & CHR_REFLECT_DIFFUSE) && p.last_hit_triangle >= 0) {
+                float *lk = (s.inside_to_outside ? lookup1 : lookup2) + 3 * (size_t)p.last_hit_triangle;
+                lk[0] += w.x * cos_theta;
+                lk[1] += w.y * cos_theta;
+                lk[2] += w.z * cos_theta;
+            }
+        }
+        rng_store(rng, nslots, (uint32_t)kid, &r);
+    }
+}
+
+/* hybrid_render.cu:133-166 */
+EXPORT void orc_hybrid_update_xyz_image(const chr_geometry_desc *d, int nthreads, uint32_t *rng, uint32_t nslots,
+                                        const float *positions, const float *directions, float wavelength,
+                                        const float *xyz, const float *lookup1, const float *lookup2, float *image,
+                                        int nlookup_calls, int max_steps) {
+    init_once();
+#pragma omp parallel for schedule(dynamic, 64)
+    for (int id = 0; id < nthreads; ++id) {
+        Geo g = {d, 0, 0, 0, 0, 0};
+        chr_xorwow r;
+        rng_load(rng, nslots, (uint32_t)id, &r);
+        Photon p;
+        memset(&p, 0, sizeof(p));
+        p.pos = mk(positions[3 * id], positions[3 * id + 1], positions[3 * id + 2]);
+        p.dir = mk(directions[3 * id], directions[3 * id + 1], directions[3 * id + 2]);
+        p.dir = divf(p.dir, norm(p.dir));
+        p.wavelength = wavelength;
+        p.pol = uniform_sphere(&r);
+        p.last_hit_triangle = -1;
+        p.weight = 1.0f;
+        State s;
+        to_diffuse(&g, &p, &s, &r, max_steps);
+        if ((p.history & CHR_REFLECT_DIFFUSE) && p.last_hit_triangle >= 0) {
+            const float *lk = (s.inside_to_outside ? lookup1 : lookup2) + 3 * (size_t)p.last_hit_triangle;
+            image[3 * id] = image[3 * id] + (xyz[0] * lk[0]) / (float)nlookup_calls;
+            image[3 * id + 1] = image[3 * id + 1] + (xyz[1] * lk[1]) / (float)nlookup_calls;
+            image[3 * id + 2] = image[3 * id + 2] + (xyz[2] * lk[2]) / (float)nlookup_calls;
+        }
+        rng_store(rng, nslots, (uint32_t)id, &r);
+    }
+}
+
+/* hybrid_render.cu:168-200 */
+EXPORT void orc_hybrid_process_image(int nthreads, const float *image, uint32_t *pixels, int nimages) {
+    for (int id = 0; id < nthreads; ++id) {
+        float c[3];
+        for (int k = 0; k < 3; ++k) {
+            float v = image[3 * id + k] / (float)nimages;
+            c[k] = v < 0.0f ? 0.0f : (v > 1.0f ? 1.0f : v);
+        }
+        uint32_t r = chr_sat_u32(floorf(c[0] * 255.0f)), g = chr_sat_u32(floorf(c[1] * 255.0f)),
+                 b = chr_sat_u32(floorf(c[2] * 255.0f));
+        pixels[id] = 255u << 24 | r << 16 | g << 8 | b;
+    }
+}

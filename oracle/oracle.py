@@ -37,6 +37,11 @@ def lib():
         l.orc_fill_state.argtypes = [vp, vp, ctypes.c_int32, ctypes.c_float, vp, vp]
         l.orc_math.argtypes = [i32, i32, vp, vp, vp]
         l.orc_rayleigh.argtypes = [i32, vp, vp, vp, u32]
+        l.orc_render.argtypes = [vp, i32, vp, vp, vp, u32, vp, vp, vp, vp, u32]
+        l.orc_transform.argtypes = [i32, vp, i32, ctypes.c_float, vp, vp]
+        l.orc_hybrid_update_xyz_lookup.argtypes = [vp, i32, i32, i32, vp, vp, u32, ctypes.c_float, vp, vp, vp, i32]
+        l.orc_hybrid_update_xyz_image.argtypes = [vp, i32, vp, u32, vp, vp, ctypes.c_float, vp, vp, vp, vp, i32, i32]
+        l.orc_hybrid_process_image.argtypes = [i32, vp, vp, i32]
         _lib = l
     return _lib
 
@@ -256,3 +261,60 @@ def pdf_accumulate_kernel_eval(time_only, event_hit, event_time, event_charge, m
     _pdf_lib().orc_pdf_accumulate_kernel_eval(int(time_only), len(eh), _p(eh), _p(et), _p(eq), _p(mt), _p(mq),
                                               trange[0], trange[1], qrange[0], qrange[1], _p(it), _p(iq),
                                               _p(hitcount), _p(time_pdf), _p(charge_pdf))
+
+
+# ---------------------------------------------------------------- renderer
+def render(packed, pos, dir, colors, alpha_depth, dx=None, dxlen=None, color=None, bg_color=0):
+    """render.cu:37-183 restated (reference BVH, reference order, searchsorted
+    insertion).  Returns (pixels, dx, dxlen, color); pass dx/dxlen/color of a
+    previous call to merge (keep_last_render)."""
+    pos = np.ascontiguousarray(pos, np.float32).reshape(-1, 3)
+    dir = np.ascontiguousarray(dir, np.float32).reshape(-1, 3)
+    n = len(pos)
+    colors = np.ascontiguousarray(colors, np.uint32)
+    dx = np.zeros(n * alpha_depth, np.float32) if dx is None else dx
+    dxlen = np.zeros(n, np.uint32) if dxlen is None else dxlen
+    color = np.zeros(n * alpha_depth * 4, np.float32) if color is None else color
+    pixels = np.zeros(n, np.uint32)
+    desc = packed.desc()
+    rc = lib().orc_render(ctypes.addressof(desc), n, _p(pos), _p(dir), _p(colors), alpha_depth, _p(pixels), _p(dx),
+                          _p(dxlen), _p(color), int(bg_color) & 0xFFFFFFFF)
+    if rc != 0:
+        raise RuntimeError('orc_render failed with status %d' % rc)
+    return pixels, dx, dxlen, color
+
+
+def transform(a, mode, phi=0.0, axis=(0, 0, 1), v=(0, 0, 0)):
+    """transform.cu: mode 0 translate by v, 1 rotate(phi, axis), 2 rotate about point v."""
+    a = np.ascontiguousarray(a, np.float32).reshape(-1, 3).copy()
+    ax = np.asarray(axis, np.float32)
+    vv = np.asarray(v, np.float32)
+    lib().orc_transform(len(a), _p(a), mode, float(phi), _p(ax), _p(vv))
+    return a
+
+
+def hybrid_update_xyz_lookup(packed, nthreads, total_threads, offset, position, rng_states, nslots, wavelength, xyz,
+                             lookup1, lookup2, max_steps):
+    p = np.asarray(position, np.float32)
+    w = np.asarray(xyz, np.float32)
+    desc = packed.desc()
+    lib().orc_hybrid_update_xyz_lookup(ctypes.addressof(desc), nthreads, total_threads, offset, _p(p), _p(rng_states),
+                                       nslots, float(wavelength), _p(w), _p(lookup1), _p(lookup2), max_steps)
+
+
+def hybrid_update_xyz_image(packed, pos, dir, rng_states, nslots, wavelength, xyz, lookup1, lookup2, image,
+                            nlookup_calls, max_steps):
+    pos = np.ascontiguousarray(pos, np.float32).reshape(-1, 3)
+    dir = np.ascontiguousarray(dir, np.float32).reshape(-1, 3)
+    w = np.asarray(xyz, np.float32)
+    desc = packed.desc()
+    lib().orc_hybrid_update_xyz_image(ctypes.addressof(desc), len(pos), _p(rng_states), nslots, _p(pos), _p(dir),
+                                      float(wavelength), _p(w), _p(lookup1), _p(lookup2), _p(image), nlookup_calls,
+                                      max_steps)
+
+
+def hybrid_process_image(image, nimages):
+    image = np.ascontiguousarray(image, np.float32)
+    pixels = np.zeros(len(image) // 3, np.uint32)
+    lib().orc_hybrid_process_image(len(pixels), _p(image), _p(pixels), nimages)
+    return pixels

@@ -119,3 +119,22 @@ def photon_sources(n, seed=7):
     parts = [isotropic(n // len(centres) + (1 if i < n % len(centres) else 0), seed=seed + i, pos=c,
                        wavelength_range=(300.0, 600.0)) for i, c in enumerate(centres)]
     return Photons.join(parts)
+
+
+def camera_rays(width, height, position, look_at, fov_deg=40.0, up=(0.0, 0.0, 1.0)):
+    """Pinhole-camera rays (camera.py-style): one per pixel, unit directions,
+    float32 (positions all `position`)."""
+    position = np.asarray(position, np.float64)
+    forward = np.asarray(look_at, np.float64) - position
+    forward /= np.linalg.norm(forward)
+    right = np.cross(forward, np.asarray(up, np.float64))
+    right /= np.linalg.norm(right)
+    upv = np.cross(right, forward)
+    half = np.tan(np.radians(fov_deg) / 2)
+    xs = (np.arange(width) + 0.5) / width * 2 - 1
+    ys = (np.arange(height) + 0.5) / height * 2 - 1
+    gx, gy = np.meshgrid(xs * half * width / height, ys * half)
+    d = forward[None, :] + gx.reshape(-1, 1) * right[None, :] + gy.reshape(-1, 1) * upv[None, :]
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    pos = np.tile(position, (len(d), 1))
+    return pos.astype(np.float32), d.astype(np.float32)

@@ -111,11 +111,15 @@ def test_kernel_pdf_parity(cuda, time_only):
     with np.errstate(invalid='ignore'):
         hitcount, values, _ = k.get_kernel_eval()
     assert np.array_equal(hitcount, hc) and (values > 0).any()
-    # NaN values come from the reference's own charge bandwidth: its variance
-    # is not clipped at 0 (pdf.py:99-110, unlike the time branch), so channels
-    # with roundoff-negative or zero variance get a NaN inverse bandwidth.
-    # They are the only NaNs (and the oracle has them bit for bit, above).
-    assert not np.isnan(values[np.isfinite(iqb) & np.isfinite(itb)]).any()
+    # NaN values are the reference formula's own (time_pdf * charge_pdf,
+    # pdf.py:161-175): a NaN inverse charge bandwidth (its variance is not
+    # clipped at 0, pdf.py:99-110) or an infinite kernel sum times a zero one.
+    # The oracle has them bit for bit (above); none comes from finite factors.
+    with np.errstate(invalid='ignore', divide='ignore'):
+        norm = np.maximum(1, hc)
+        tpn, qpn = tp / norm, qp / norm
+    if not time_only:
+        assert not np.isnan(values[np.isfinite(tpn) & np.isfinite(qpn)]).any()
 
 
 def test_pdf_from_propagate_and_daq(cuda, small_detector):
