@@ -40,8 +40,9 @@ def _compare(rays, pix, want, depth):
     assert np.array_equal(pix.get(), wpix)
     ln = rays.dxlen.get()
     assert np.array_equal(ln, wlen)
-    dx = rays.dx.get().reshape(n, -1)[:, :depth]
-    col = rays.color.get().view(np.float32).reshape(n, -1, 4)[:, :depth]
+    # entries of ray i at [i * alpha_depth, (i + 1) * alpha_depth) (render.cu:84-85)
+    dx = rays.dx.get()[:n * depth].reshape(n, depth)
+    col = rays.color.get().view(np.float32)[:4 * n * depth].reshape(n, depth, 4)
     wdx = wdx.reshape(n, depth)
     wcol = wcol.reshape(n, depth, 4)
     for i in np.flatnonzero(ln):
