@@ -24,6 +24,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/chroma_amd.h"
@@ -1705,11 +1706,35 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_group_kernel(const DevG
 // nearest hit is the min over (distance, reference rank) with the reference
 // leaf check of every other walk, so the result does not depend on P.
 constexpr int TAIL_STACK = 128;   // stack entries per 8 lanes; a segment of Gs lanes holds TAIL_STACK * Gs / 8
-constexpr int TAIL_TRI = 4 * 64;  // triangle-list words per wave (<= 4 triangles per lane per iteration)
+constexpr int TAIL_TRI = 4 * 64;  // triangle-list words per wave and buffer (<= 4 triangles per lane per iteration)
+
+// 64-bit min over the 8 lanes of each aligned lane group, by DPP (quad xor 1,
+// quad xor 2, half-row mirror): VALU moves, no LDS round trips.
+__device__ __forceinline__ unsigned long long dpp_min8(unsigned long long k) {
+    auto step = [](unsigned long long v, auto ctrl) {
+        const int lo = __builtin_amdgcn_mov_dpp((int)(uint32_t)v, decltype(ctrl)::value, 0xF, 0xF, true);
+        const int hi = __builtin_amdgcn_mov_dpp((int)(uint32_t)(v >> 32), decltype(ctrl)::value, 0xF, 0xF, true);
+        const unsigned long long o = ((unsigned long long)(uint32_t)hi << 32) | (uint32_t)lo;
+        return o < v ? o : v;
+    };
+    k = step(k, std::integral_constant<int, 0xB1>());    // quad_perm [1,0,3,2]
+    k = step(k, std::integral_constant<int, 0x4E>());    // quad_perm [2,3,0,1]
+    k = step(k, std::integral_constant<int, 0x141>());   // row_half_mirror
+    return k;
+}
+
+// index of the r-th set bit of m (r < popcount(m))
+__device__ __forceinline__ int nth_bit(unsigned long long m, int r) {
+    for (int i = 0; i < r; ++i) m &= m - 1;
+    return __ffsll((long long)m) - 1;
+}
 
 // All 64 lanes call this (converged).  act: the segment has a ray (segment-
 // uniform).  Returns the nearest triangle (-1: none) and its distance in
-// every lane of the segment.
+// every lane of the segment.  One dependent global fetch per iteration: the
+// triangles of the leaves found in iteration i are fetched together with the
+// nodes of iteration i + 1 (their best then culls one iteration later, still
+// with a best that never drops below the final one).
 __device__ int walk_segment(const DevGeom &g, bool act, V3 o, V3 d, uint32_t last, int Gs,
                             CHR_LDS uint32_t *stk, int cap, CHR_LDS uint32_t *tlist, uint32_t &overflow,
                             float &min_distance, uint32_t &iters) {
@@ -1730,31 +1755,67 @@ __device__ int walk_segment(const DevGeom &g, bool act, V3 o, V3 d, uint32_t las
     uint32_t cur = (act && L < 8u) ? 0u : INVALID;   // cursor 0 starts at the root
     float cur_t = 0.0f;
     int sp = 0;
+    uint32_t Tp = 0;                                  // triangles listed by the previous iteration
+    int pb = 0;                                       // their list buffer (double-buffered)
     bool done = !act;
     iters = 0;
     while (__ballot(!done) != 0) {
         if (done) continue;
         iters++;
-        // cursors without a node take unculled stack entries, in sub-group order
+        // cursors without a node take the topmost unculled stack entries: a
+        // window of up to 8 entries read at once, the r-th empty cursor (in
+        // sub-group order) taking the r-th unculled entry (from the top)
         unsigned long long em = __ballot(k == 0u && cur == INVALID) & segmask;
+        const bool refill = em != 0 && sp > 0;
         while (em != 0 && sp > 0) {
-            sp--;
-            const uint32_t en = stk[2 * sp], et = stk[2 * sp + 1];
-            if (__uint_as_float(et) > best) continue;     // mesh.h:94-96
-            if ((lane & ~7u) == (uint32_t)(__ffsll((long long)em) - 1)) { cur = en; cur_t = __uint_as_float(et); }
-            em &= em - 1;
+            const int W = sp < 8 ? sp : 8;
+            uint32_t en = 0, et = 0;
+            bool ok = false;
+            if (L < (uint32_t)W) {
+                en = stk[2 * (sp - 1 - (int)L)];
+                et = stk[2 * (sp - 1 - (int)L) + 1];
+                ok = !(__uint_as_float(et) > best);           // mesh.h:94-96
+            }
+            const unsigned long long vm = (__ballot(ok) & segmask) >> seg0;
+            const int need = __popcll(em), nv = __popcll(vm);
+            const int take = need < nv ? need : nv;
+            const int consumed = take == nv ? W : nth_bit(vm, take);   // entries above the first kept one
+            if (k == 0u && cur == INVALID) {
+                const int rnk = __popcll(em & below);
+                if (rnk < take) {
+                    const int src = nth_bit(vm, rnk);
+                    cur = stk[2 * (sp - 1 - src)];
+                    cur_t = __uint_as_float(stk[2 * (sp - 1 - src) + 1]);
+                }
+            }
+            sp -= consumed;
+            for (int i = 0; i < take; ++i) em &= em - 1;
+            if (take == 0 && consumed == 0) break;
         }
-        if ((__ballot(cur != INVALID) & segmask) == 0) { done = true; continue; }
+        if (refill) {   // the sub-group's cursor, from its leader lane
+            cur = (uint32_t)__shfl((int)cur, (int)(lane & ~7u));
+            cur_t = __shfl(cur_t, (int)(lane & ~7u));
+        }
+        const bool walking = (__ballot(cur != INVALID) & segmask) != 0;
+        if (!walking && Tp == 0) { done = true; continue; }
+        // fetch: this iteration's nodes and the previous iteration's triangles together
+        uint4 h = make_uint4(0u, 0u, 0u, 0u), a1 = h, a2 = h, a3 = h, a4 = h, a5 = h;
+        if (cur != INVALID) {
+            const uint4 *np = g.wnodes + (size_t)g.wstride * cur;
+            h = gld(np); a1 = gld(np + 1); a2 = gld(np + 2); a3 = gld(np + 3); a4 = gld(np + 4); a5 = gld(np + 5);
+        }
+        const bool has_tri = L < Tp;
+        float4 r0 = make_float4(0.0f, 0.0f, 0.0f, 0.0f), r1 = r0, r2 = r0, r3 = r0;
+        const float4 *rr = nullptr;
+        if (has_tri) {
+            rr = g.wtri + 4 * (size_t)tlist[pb * TAIL_TRI + L];
+            r0 = gld(rr); r1 = gld(rr + 1); r2 = gld(rr + 2); r3 = gld(rr + 3);
+        }
         // expand: sub-group j's 8 lanes slab-test the 8 children of its node
         bool inner = false, leafhit = false;
         float tk = 0.0f;
-        uint32_t kind = 0, child = 0, first = 0, near = INVALID;
-        uint4 a4 = make_uint4(0u, 0u, 0u, 0u), a5 = a4;
+        uint32_t kind = 0, child = 0, first = 0;
         if (cur != INVALID) {
-            const uint4 *np = g.wnodes + (size_t)g.wstride * cur;
-            const uint4 h = gld(np), a1 = gld(np + 1), a2 = gld(np + 2), a3 = gld(np + 3);
-            a4 = gld(np + 4);
-            a5 = gld(np + 5);
             const V3 org = v3(__uint_as_float(h.x), __uint_as_float(h.y), __uint_as_float(h.z));
             const float sx = exp_scale(h.w), sy = exp_scale(h.w >> 8), sz = exp_scale(h.w >> 16);
             const int kk = (int)k;
@@ -1777,12 +1838,9 @@ __device__ int walk_segment(const DevGeom &g, bool act, V3 o, V3 d, uint32_t las
         }
         // each sub-group continues with its nearest inner child (first of the
         // smallest entry distance) and pushes the others
-        unsigned long long key = inner ? (((unsigned long long)__float_as_uint(tk) << 32) | k) : NONE;
-#pragma unroll
-        for (int off = 1; off < 8; off <<= 1) {
-            const unsigned long long other = __shfl_xor(key, off, 8);
-            key = other < key ? other : key;
-        }
+        const unsigned long long key =
+            dpp_min8(inner ? (((unsigned long long)__float_as_uint(tk) << 32) | k) : NONE);
+        uint32_t near = INVALID;
         float near_t = 0.0f;
         if (key != NONE) {
             near = a4.x + byte_of(a5.x, a5.y, (int)(key & 7u));
@@ -1804,20 +1862,23 @@ __device__ int walk_segment(const DevGeom &g, bool act, V3 o, V3 d, uint32_t las
         }
         cur = near;
         cur_t = near_t;
-        // the iteration's hit-leaf triangles, listed in lane order, one per lane
+        // this iteration's hit-leaf triangles, listed in lane order for the next fetch
         const uint32_t cnt = leafhit ? kind : 0u;
         const unsigned long long b0 = __ballot(cnt & 1u) & segmask, b1 = __ballot(cnt & 2u) & segmask,
                                  b2 = __ballot(cnt & 4u) & segmask;
         const uint32_t pre = __popcll(b0 & below) + 2u * __popcll(b1 & below) + 4u * __popcll(b2 & below);
-        const uint32_t T = __popcll(b0) + 2u * __popcll(b1) + 4u * __popcll(b2);
-        for (uint32_t t = 0; t < cnt; ++t) tlist[pre + t] = first + t;
-        __builtin_amdgcn_wave_barrier();
+        const uint32_t Tn = __popcll(b0) + 2u * __popcll(b1) + 4u * __popcll(b2);
+        for (uint32_t t = 0; t < cnt; ++t) tlist[(pb ^ 1) * TAIL_TRI + pre + t] = first + t;
+        // test the previous iteration's triangles (entries beyond the segment's
+        // lanes, rare, are fetched now)
         float lbest = best;
         uint32_t lrank = best_rank;
         int lid = -1;
-        for (uint32_t i = L; i < T; i += (uint32_t)Gs) {
-            const float4 *rr = g.wtri + 4 * (size_t)tlist[i];
-            const float4 r0 = gld(rr), r1 = gld(rr + 1), r2 = gld(rr + 2);
+        for (uint32_t i = L; i < Tp; i += (uint32_t)Gs) {
+            if (i != L) {
+                rr = g.wtri + 4 * (size_t)tlist[pb * TAIL_TRI + i];
+                r0 = gld(rr); r1 = gld(rr + 1); r2 = gld(rr + 2); r3 = gld(rr + 3);
+            }
             const uint32_t id = __float_as_uint(r2.y);
             float dist;
             if (id == last ||
@@ -1825,7 +1886,6 @@ __device__ int walk_segment(const DevGeom &g, bool act, V3 o, V3 d, uint32_t las
                 continue;
             const uint32_t rank = __float_as_uint(r2.z);
             if (!(dist < lbest || (dist == lbest && rank < lrank))) continue;
-            const float4 r3 = gld(rr + 3);
             V3 lo, hi;
             node_bounds(g, make_uint4(__float_as_uint(r2.w), __float_as_uint(r3.x), __float_as_uint(r3.y), 0u), lo, hi);
             float bd;
@@ -1835,17 +1895,28 @@ __device__ int walk_segment(const DevGeom &g, bool act, V3 o, V3 d, uint32_t las
             lid = (int)id;
         }
         __builtin_amdgcn_wave_barrier();   // list reads land before the next iteration's writes
-        unsigned long long lkey = lid == -1 ? NONE : (((unsigned long long)__float_as_uint(lbest) << 32) | lrank);
-        for (int off = 1; off < Gs; off <<= 1) {
-            const unsigned long long ok = __shfl_xor(lkey, off);
-            const int oid = __shfl_xor(lid, off);
-            if (ok < lkey) { lkey = ok; lid = oid; }
-        }
-        if (lkey != NONE) {
+        // segment min over (distance, rank): usually no lane or one lane has a hit
+        const unsigned long long hm = __ballot(lid != -1) & segmask;
+        if (hm != 0) {
+            unsigned long long lkey = lid == -1 ? NONE : (((unsigned long long)__float_as_uint(lbest) << 32) | lrank);
+            if ((hm & (hm - 1)) == 0) {
+                const int src = __ffsll((long long)hm) - 1;
+                lkey = ((unsigned long long)(uint32_t)__shfl((int)(uint32_t)(lkey >> 32), src) << 32) |
+                       (uint32_t)__shfl((int)(uint32_t)lkey, src);
+                lid = __shfl(lid, src);
+            } else {
+                for (int off = 1; off < Gs; off <<= 1) {
+                    const unsigned long long ok = __shfl_xor(lkey, off);
+                    const int oid = __shfl_xor(lid, off);
+                    if (ok < lkey) { lkey = ok; lid = oid; }
+                }
+            }
             best = __uint_as_float((uint32_t)(lkey >> 32));
             best_rank = (uint32_t)lkey;
             best_id = lid;
         }
+        Tp = Tn;
+        pb ^= 1;
         if (cur != INVALID && cur_t > best) cur = INVALID;
     }
     min_distance = best_id == -1 ? -1.0f : best;
@@ -1856,7 +1927,7 @@ template <int MINW>
 __global__ __launch_bounds__(BLOCK, MINW) void propagate_tail_kernel(const DevGeom *__restrict__ gdev, PropagateArgs a,
                                                                      uint32_t cap) {
     __shared__ uint32_t stacks[(BLOCK / 8) * TAIL_STACK * 2];
-    __shared__ uint32_t tris[(BLOCK / 64) * TAIL_TRI];
+    __shared__ uint32_t tris[(BLOCK / 64) * 2 * TAIL_TRI];
     const uint32_t tid = blockIdx.x * BLOCK + threadIdx.x;
     const uint32_t lane = __lane_id();
     const uint32_t slot = tid / 8, sub = tid & 7u;
@@ -1864,7 +1935,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_tail_kernel(const DevGe
     const uint32_t nslot = cap < n ? cap : n;
     if ((tid & ~63u) / 8 >= nslot) return;             // whole waves: the others help walk
     CHR_LDS uint32_t *wstack = (CHR_LDS uint32_t *)stacks + (threadIdx.x >> 6) * 8 * TAIL_STACK * 2;
-    CHR_LDS uint32_t *wtris = (CHR_LDS uint32_t *)tris + (threadIdx.x >> 6) * TAIL_TRI;
+    CHR_LDS uint32_t *wtris = (CHR_LDS uint32_t *)tris + (threadIdx.x >> 6) * 2 * TAIL_TRI;
     const DevGeom &g = *gdev;
     chr_xorwow rng;
     bool have_rng = false;
@@ -2720,7 +2791,13 @@ static constexpr int kExactVariant = 1;
 // launch lasts as long as its longest-lived photon, so fewer resident waves
 // means more rounds of waves behind it)
 static constexpr int kGroupWaves = 4;
-static constexpr int kTailWaves = 4;   // propagate_tail_kernel (wave-adaptive walk)
+// propagate_tail_kernel (wave-adaptive walk) at 3 waves/SIMD: 168 VGPRs, no
+// VGPR spills (at 4: 64 spilled; r02 A/B on the 29k bench: 380.4 vs 376.9 M/s)
+static constexpr int kTailWaves = 3;
+static int tail_waves() {              // CHR_TAIL_WAVES=4: the tail kernel at 4 waves/SIMD (A/B)
+    const char *e = getenv("CHR_TAIL_WAVES");
+    return e ? atoi(e) : kTailWaves;
+}
 static bool tail_group_walk() {        // CHR_TAIL=group: the fixed 8-lane group kernel (A/B)
     const char *e = getenv("CHR_TAIL");
     return e && std::strcmp(e, "group") == 0;
@@ -2782,7 +2859,8 @@ static StepVariant select_step_variant(const chr_geometry *g) {
             sv.fn = propagate_step_kernel<8, 4, kWalk>;
             sv.trace = trace_kernel<false, 6, 12, 4, 32>;
             sv.shade = shade_kernel<3>;
-            sv.tail = tail_group_walk() ? propagate_group_kernel<8, kGroupWaves> : propagate_tail_kernel<kTailWaves>;
+            sv.tail = tail_group_walk() ? propagate_group_kernel<8, kGroupWaves>
+                      : (tail_waves() == 4 ? propagate_tail_kernel<4> : propagate_tail_kernel<kTailWaves>);
             sv.tail_group = 8;
             sv.binned = v == 7 ? 1 : (v == 8 ? 0 : 2);
             break;
@@ -3294,7 +3372,7 @@ extern "C" int chr_kernel_info(int32_t which, chr_kernel_attr *out) {
     switch (which) {
         case 0: fn = (const void *)trace_kernel<false, 6, 12, 4, 32>; name = "chr::trace_kernel<false,6,12,4,32>"; break;
         case 1: fn = (const void *)shade_kernel<3>; name = "chr::shade_kernel<3>"; break;
-        case 2: fn = (const void *)propagate_tail_kernel<kTailWaves>; name = "chr::propagate_tail_kernel<4>"; break;
+        case 2: fn = (const void *)propagate_tail_kernel<kTailWaves>; name = "chr::propagate_tail_kernel<3>"; break;
         case 3: fn = (const void *)propagate_step_kernel<8, 4, kWalk>; name = "chr::propagate_step_kernel<8,4,2006>"; break;
         default: return chr::fail(CHR_ERR_INVALID, "chr_kernel_info: unknown kernel %d", which);
     }
