@@ -376,8 +376,10 @@ def main():
     del gp
     channel_hits = int(reduced['counts'].sum().item())     # all ranks, detected with a channel
     launch_ms = [s.trace_launch_ms[i] for s in stats for i in range(s.trace_ms_n)]
+    launch_rays = [int(stats[0].trace_launch_rays[i]) for i in range(stats[0].trace_ms_n)] if stats else []
     live = dict(kernel_ms=sum(s.kernel_ms for s in stats), launches=sum(s.launches for s in stats),
-                host_steps=sum(s.steps_run for s in stats), trace_ms=sum(s.trace_ms for s in stats),
+                host_steps=sum(s.steps_run for s in stats), host_syncs=sum(s.host_syncs for s in stats),
+                trace_ms=sum(s.trace_ms for s in stats),
                 trace_launches=sum(s.trace_launches for s in stats), trace_rays=sum(s.trace_rays for s in stats),
                 overflows=sum(s.stack_overflows for s in stats), flat=sum(s.flat_walks for s in stats),
                 flat_whole=sum(s.flat_walks_whole for s in stats),
@@ -402,6 +404,19 @@ def main():
             os.environ['CHR_PROPAGATE_VARIANT'] = prev
         torch.cuda.synchronize()
 
+    # untimed, CHROMA_DEVICE_PROFILE=1 only (libchroma_amd_prof.so, whose timed numbers
+    # carry the counters): the device region profile of one more propagate
+    dprof = None
+    if _native.DEVICE_PROFILE:
+        from chroma.gpu import profiler
+        profiler.device_reset()
+        step()
+        reduced.pop('gp', None)
+        torch.cuda.synchronize()
+        dprof = {'regions': profiler.device_fetch(), 'clock_khz': profiler.device_fetch.clock_khz,
+                 'library': os.path.basename(_native.library_path()),
+                 'cycles': 'lane-cycles of the shader clock (include/chroma_amd.h CHR_PROF_*)'}
+
     if rank == 0:
         props = torch.cuda.get_device_properties(local)
         free_b, total_b = torch.cuda.mem_get_info(local)
@@ -410,15 +425,20 @@ def main():
                   'trace_ms_per_step': live['trace_ms'] / steps,
                   'launches_per_step': live['launches'] / steps,
                   'host_steps_per_propagate': live['host_steps'] / steps,
+                  'stream_draining_host_syncs_per_propagate': live['host_syncs'] / steps,
                   'stack_overflows': int(live['overflows']),
                   'flat_walks_decomposed': int(live['flat']), 'flat_walks_whole': int(live['flat_whole']),
                   'tail_launch': live['tail'],
+                  'first_propagate_trace_launches': [{'rays': r, 'ms': round(float(m), 3)} for r, m in
+                                                     zip(launch_rays, launch_ms[:len(launch_rays)])],
                   'detected_fraction': detected / args.photons,
                   'channel_hits_all_ranks': channel_hits,
                   'device': {'name': props.name, 'arch': getattr(props, 'gcnArchName', ''),
                              'compute_units': props.multi_processor_count,
                              'hbm_total_gb': total_b / 1e9, 'hbm_free_gb_after': free_b / 1e9},
                   'kernels': _kernel_info(_native)}
+        if dprof is not None:
+            detail['device_profile'] = dprof
         if cst is not None and cst.traversals:
             detail['own_layout'] = {
                 'bytes_per_walk': (96.0 * cst.nodes_visited + 64.0 * cst.triangles_tested + 52.0 * cst.traversals)

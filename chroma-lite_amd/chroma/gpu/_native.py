@@ -8,8 +8,11 @@ library raises immediately.
 import ctypes
 import os
 
-_LIBPATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), '_lib',
-                        'libchroma_amd.so')
+_LIBDIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), '_lib')
+# CHROMA_DEVICE_PROFILE=1: the build with the device region counters compiled in
+# (the reference's -DCHROMA_DEVICE_PROFILE=1 kernels, profile.h; chroma.gpu.profiler.device_*)
+DEVICE_PROFILE = os.environ.get('CHROMA_DEVICE_PROFILE', '').strip().lower() in ('1', 'true', 'yes', 'on')
+_LIBPATH = os.path.join(_LIBDIR, 'libchroma_amd_prof.so' if DEVICE_PROFILE else 'libchroma_amd.so')
 # dev A/B of alternative builds (still in-tree): CHROMA_AMD_LIB=/path/to/libchroma_amd*.so
 _LIBPATH = os.environ.get('CHROMA_AMD_LIB', _LIBPATH)
 
@@ -71,7 +74,8 @@ class PropagateStats(ctypes.Structure):
                 ('flat_walks_whole', c_u32), ('tail_photons', c_u32), ('tail_ms', ctypes.c_double),
                 ('tail_max_steps', c_u32), ('tail_slowest_steps', c_u32), ('tail_max_cycles', c_u64),
                 ('tail_long_photons', c_u32), ('reserved2', c_u32), ('tail_long_steps', c_u64),
-                ('tail_long_ticks', c_u64), ('tail_long_walk_ticks', c_u64), ('tail_long_walk_iterations', c_u64)]
+                ('tail_long_ticks', c_u64), ('tail_long_walk_ticks', c_u64), ('tail_long_walk_iterations', c_u64),
+                ('host_syncs', c_u32), ('reserved3', c_u32), ('trace_launch_rays', c_u32 * 32)]
 
 
 class KernelAttr(ctypes.Structure):
@@ -137,6 +141,9 @@ _SIGNATURES = {
     'chr_hybrid_update_xyz_image': (c_i32, [c_vp, c_i32, c_vp, c_u32, c_vp, c_vp, c_f32, c_vp, c_vp, c_vp, c_vp,
                                             c_i32, c_i32, c_vp]),
     'chr_hybrid_process_image': (c_i32, [c_i32, c_vp, c_vp, c_i32, c_vp]),
+    'chr_device_profile_enabled': (c_i32, []),
+    'chr_device_profile_reset': (c_i32, [c_vp]),
+    'chr_device_profile_fetch': (c_i32, [c_vp, c_vp, c_i32, ctypes.POINTER(c_u32)]),
     'chr_last_error': (ctypes.c_char_p, []),
     'chr_version': (c_i32, []),
 }
@@ -159,8 +166,8 @@ def lib():
     global _lib
     if _lib is None:
         if not os.path.exists(_LIBPATH):
-            raise ImportError('libchroma_amd.so not found at %s: build it with '
-                              '`make -C chroma-lite_amd/csrc` (or __graft_entry__.build())' % _LIBPATH)
+            raise ImportError('%s not found at %s: build it with `make -C chroma-lite_amd/csrc` '
+                              '(or __graft_entry__.build())' % (os.path.basename(_LIBPATH), _LIBPATH))
         l = ctypes.CDLL(_LIBPATH)
         for name, (res, args) in _SIGNATURES.items():
             if 'CHROMA_AMD_LIB' in os.environ and not hasattr(l, name):
@@ -179,7 +186,15 @@ def check(rc, what=''):
     return rc
 
 
+# chroma.gpu.profiler installs a timer here while host-side profiling is on
+# (the reference wraps every PyCUDA kernel function, profiler.py:68-139; every
+# launch here goes through call())
+call_hook = None
+
+
 def call(name, *args):
+    if call_hook is not None:
+        return call_hook(name, lambda: check(getattr(lib(), name)(*args), name))
     return check(getattr(lib(), name)(*args), name)
 
 

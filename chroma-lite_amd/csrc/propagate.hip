@@ -305,6 +305,28 @@ __device__ __forceinline__ RaySlab make_slab(V3 noid, V3 inv) {
     return r;
 }
 
+// intersect_box (intersect.h:113-157) from the ray's slab constants: an axis
+// whose 1/d is not finite has multiplier 0 there and is skipped, the others
+// compute fmaf(bound, inv, noid) exactly as intersect_box does.
+__device__ __forceinline__ bool intersect_box_slab(const RaySlab &r, V3 lo, V3 hi, float &dist) {
+    float tmin = 0.0f, tmax = __builtin_inff();
+    if (r.inx != 0.0f) {
+        const float t0 = __builtin_fmaf(lo.x, r.inx, r.onx), t1 = __builtin_fmaf(hi.x, r.inx, r.onx);
+        tmin = fmax_(tmin, fmin_(t0, t1)); tmax = fmin_(tmax, fmax_(t0, t1));
+    }
+    if (r.iny != 0.0f) {
+        const float t0 = __builtin_fmaf(lo.y, r.iny, r.ony), t1 = __builtin_fmaf(hi.y, r.iny, r.ony);
+        tmin = fmax_(tmin, fmin_(t0, t1)); tmax = fmin_(tmax, fmax_(t0, t1));
+    }
+    if (r.inz != 0.0f) {
+        const float t0 = __builtin_fmaf(lo.z, r.inz, r.onz), t1 = __builtin_fmaf(hi.z, r.inz, r.onz);
+        tmin = fmax_(tmin, fmin_(t0, t1)); tmax = fmin_(tmax, fmax_(t0, t1));
+    }
+    if (tmin > tmax) return false;
+    dist = tmin;
+    return true;
+}
+
 // What a queued photon's walk is: 0 none (NaN state: the step aborts it,
 // propagate.cu:307-310), 1 an ordinary walk, 2 a FLAT walk -- a direction
 // component whose reciprocal is not finite (+-0 or denormal).  The reference's
@@ -323,8 +345,12 @@ __device__ __forceinline__ int walk_kind(V3 o, V3 d) {
 
 // Slab-test the up-to-8 children of one wide node.  Returns the leaf children
 // hit (bit mask), leaves the nearest hit inner child in near_node/near_t and
-// pushes the other hit inner children.  Boxes entered beyond `best` are culled
-// (strict '>', mesh.h:94-96).
+// pushes the other hit inner children in child order.  Boxes entered beyond
+// `best` are culled (strict '>', mesh.h:94-96).  Branch-free over the children
+// (the per-child early-outs of a loop cost ~3 scalar exec-mask instructions
+// each and divide the wave anyway): all 8 slab tests, the near child as the
+// first of the smallest entry distance, then one predicated push per child at
+// its prefix position.
 template <int SL = WIDE_LDS>
 __device__ __forceinline__ uint32_t expand_node(const uint4 h, const uint4 a1, const uint4 a2, const uint4 a3,
                                                 const uint4 a4, const uint4 a5, const RaySlab &r, float best,
@@ -339,13 +365,11 @@ __device__ __forceinline__ uint32_t expand_node(const uint4 h, const uint4 a1, c
     const uint32_t fy0 = r.negy ? a1.z : a3.x, fy1 = r.negy ? a1.w : a3.y;
     const uint32_t nz0 = r.negz ? a3.z : a2.x, nz1 = r.negz ? a3.w : a2.y;
     const uint32_t fz0 = r.negz ? a2.x : a3.z, fz1 = r.negz ? a2.y : a3.w;
-    uint32_t leaf_mask = 0;
-    near_node = 0xFFFFFFFFu;
-    near_t = 0.0f;
+    float tk[8];
+    uint32_t inner = 0, leaf = 0;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
         const uint32_t kind = ((k < 4 ? a4.z : a4.w) >> (8 * (k & 3))) & 0xFFu;
-        if (kind == 0 || !((cmask >> k) & 1u)) continue;
         const float tnx = __builtin_fmaf(__builtin_fmaf(byte_f(nx0, nx1, k), sx, org.x), r.inx, r.onx);
         const float tfx = __builtin_fmaf(__builtin_fmaf(byte_f(fx0, fx1, k), sx, org.x), r.inx, r.ofx);
         const float tny = __builtin_fmaf(__builtin_fmaf(byte_f(ny0, ny1, k), sy, org.y), r.iny, r.ony);
@@ -354,18 +378,54 @@ __device__ __forceinline__ uint32_t expand_node(const uint4 h, const uint4 a1, c
         const float tfz = __builtin_fmaf(__builtin_fmaf(byte_f(fz0, fz1, k), sz, org.z), r.inz, r.ofz);
         const float tmin = __builtin_fmaxf(__builtin_fmaxf(__builtin_fmaxf(tnx, tny), tnz), 0.0f);
         const float tmax = __builtin_fminf(__builtin_fminf(tfx, tfy), tfz);
-        if (tmin > tmax || tmin > best) continue;
-        if (kind != WIDE_INNER) { leaf_mask |= 1u << k; continue; }
-        const uint32_t child = a4.x + (((k < 4 ? a5.x : a5.y) >> (8 * (k & 3))) & 0xFFu);
-        if (near_node == 0xFFFFFFFFu) { near_node = child; near_t = tmin; continue; }
-        uint32_t pn = child;
-        float pt = tmin;
-        if (tmin < near_t) { pn = near_node; pt = near_t; near_node = child; near_t = tmin; }
-        if (sp >= WIDE_STACK) { overflow++; break; }
-        wpush<SL>(st, sp, pn, pt);
-        sp++;
+        const bool hit = (kind != 0u) & (((cmask >> k) & 1u) != 0u) & !(tmin > tmax) & !(tmin > best);
+        inner |= (uint32_t)(hit & (kind == WIDE_INNER)) << k;
+        leaf |= (uint32_t)(hit & (kind != WIDE_INNER)) << k;
+        tk[k] = tmin;
     }
-    return leaf_mask;
+    // nearest inner child: first of the smallest entry distance
+    int nk = -1;
+    float nt = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const bool take = ((inner >> k) & 1u) && (nk < 0 || tk[k] < nt);
+        nk = take ? k : nk;
+        nt = take ? tk[k] : nt;
+    }
+    near_node = 0xFFFFFFFFu;
+    near_t = 0.0f;
+    if (nk >= 0) {
+        near_node = a4.x + (((nk < 4 ? a5.x : a5.y) >> (8 * (nk & 3))) & 0xFFu);
+        near_t = nt;
+    }
+    const uint32_t push = nk >= 0 ? inner & ~(1u << nk) : 0u;
+    if (push) {
+        const int npush = __builtin_popcount(push);
+        if (sp + npush < SL) {
+            // all in LDS: every child writes, the ones not pushed to the slot above
+            // the new top (free, so harmless) -- no per-child branch
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const int pos = ((push >> k) & 1u) ? sp + __builtin_popcount(push & ((1u << k) - 1u)) : sp + npush;
+                st.node[pos * BLOCK] = a4.x + (((k < 4 ? a5.x : a5.y) >> (8 * (k & 3))) & 0xFFu);
+                st.dist[pos * BLOCK] = tk[k];
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const int pos = sp + __builtin_popcount(push & ((1u << k) - 1u));
+                if (((push >> k) & 1u) && pos < WIDE_STACK)
+                    wpush<SL>(st, pos, a4.x + (((k < 4 ? a5.x : a5.y) >> (8 * (k & 3))) & 0xFFu), tk[k]);
+            }
+        }
+        if (sp + npush > WIDE_STACK) {
+            overflow += (uint32_t)(sp + npush - WIDE_STACK);
+            sp = WIDE_STACK;
+        } else {
+            sp += npush;
+        }
+    }
+    return leaf;
 }
 
 struct WalkCounts {   // filled only by the counting variant (bench: algorithmic bytes per photon)
@@ -378,6 +438,64 @@ __device__ __forceinline__ bool wave_leader() {
     const unsigned long long m = __ballot(1);
     return (unsigned)__lane_id() == (unsigned)(__ffsll((long long)m) - 1);
 }
+
+// ---------------------------------------------------------------- device profile
+// The reference's CHROMA_DEVICE_PROFILE regions (profile.h:9-37: per-call
+// clock64 spans atomically added to per-region counters) for the split step
+// kernels, built only into libchroma_amd_prof.so (-DCHR_DEVICE_PROFILE=1).
+// Instead of two global atomics per call, each work-item keeps its region
+// lane-cycles and calls in registers and a wave adds its sums once at exit.
+// A kernel marks region boundaries with tick(next): the wave time since the
+// last tick goes to the region the work-item was in (a work-item masked off in
+// a branch keeps its region, so the time it waits is charged there).
+#ifdef CHR_DEVICE_PROFILE
+__device__ unsigned long long chr_prof_calls[CHR_PROF_COUNT];
+__device__ unsigned long long chr_prof_cycles[CHR_PROF_COUNT];
+
+// one wave's sum of (calls, cycles) added to region id; every lane of the wave active
+__device__ __forceinline__ void prof_add(int id, unsigned long long calls, unsigned long long cycles) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        calls += __shfl_xor(calls, o);
+        cycles += __shfl_xor(cycles, o);
+    }
+    if (__lane_id() == 0) {
+        if (calls) atomicAdd(&chr_prof_calls[id], calls);
+        if (cycles) atomicAdd(&chr_prof_cycles[id], cycles);
+    }
+}
+template <int N>
+struct Prof {
+    uint32_t cyc[N], calls[N];
+    unsigned long long t, t0;
+    int cur;
+    __device__ __forceinline__ void start(int c) {
+        t0 = t = __builtin_amdgcn_s_memtime();
+        cur = c;
+#pragma unroll
+        for (int i = 0; i < N; ++i) cyc[i] = calls[i] = 0u;
+    }
+    __device__ __forceinline__ void tick(int next) {
+        const unsigned long long now = __builtin_amdgcn_s_memtime();
+        const uint32_t dt = (uint32_t)(now - t);
+        t = now;
+#pragma unroll
+        for (int i = 0; i < N; ++i) cyc[i] += cur == i ? dt : 0u;
+        cur = next;
+    }
+    __device__ __forceinline__ void set(int c) { cur = c; }
+    __device__ __forceinline__ void call(int i, uint32_t k = 1u) { calls[i] += k; }
+    __device__ __forceinline__ unsigned long long total() const { return t - t0; }
+};
+#else
+template <int N>
+struct Prof {
+    __device__ __forceinline__ void start(int) {}
+    __device__ __forceinline__ void tick(int) {}
+    __device__ __forceinline__ void set(int) {}
+    __device__ __forceinline__ void call(int, uint32_t = 1u) {}
+};
+#endif
 
 // The same query, scheduled for 64-wide SIMT (default).  Leaf triangles are
 // not tested inside the node step of the lane that reached them: a lane that
@@ -1359,7 +1477,14 @@ struct PropagateArgs {
                                        // [1] max steps of one photon, [2..3] u64 max of (cycles << 16 | steps),
                                        // [4..13] u64 sums over photons of > 64 steps (tail kernel): walk
                                        // ticks, step ticks, walk iterations, steps, photons
+    // device-driven steps (nullptr: host-driven): the queue length is *dev_n - 1
+    // and the launch runs only if *mode == want
+    const uint32_t *dev_n;
+    const uint32_t *mode;
+    uint32_t want;
 };
+// modes of a device-driven step slot (step_head_kernel)
+constexpr uint32_t STEP_IDLE = 0, STEP_ONE = 1, STEP_TAIL = 2;
 // hits[q] = (FLAT_HIT, f): queue position q holds flat walk f of this step,
 // its result is flat_best[f] (trace_kernel)
 constexpr int FLAT_HIT = -3;
@@ -1582,13 +1707,17 @@ __device__ __forceinline__ void fetch_queued(const PropagateArgs &a, uint32_t q,
 template <int MINW>
 __global__ __launch_bounds__(BLOCK, MINW) void shade_kernel(const DevGeom *__restrict__ gdev, PropagateArgs a,
                                                             uint32_t cap) {
+    if (a.mode && *a.mode != a.want) return;
     const uint32_t slot = blockIdx.x * BLOCK + threadIdx.x;
-    const uint32_t n = (uint32_t)a.nthreads;
+    const uint32_t n = a.dev_n ? *a.dev_n - 1u : (uint32_t)a.nthreads;
     if (slot == 0 && a.zero_word) *a.zero_word = 0u;
     if (slot >= cap || (slot & ~63u) >= n) return;   // whole waves (cap % 64 == 0)
     const DevGeom &g = *gdev;
     chr_xorwow rng;
     bool have_rng = false;
+    enum { P_FILL, P_PHYS, P_OTHER };
+    Prof<3> pf;
+    pf.start(P_OTHER);
     QueuedPhoton nx;
     if (slot < n) fetch_queued(a, slot, nx);
     uint32_t pos = slot;
@@ -1619,13 +1748,18 @@ __global__ __launch_bounds__(BLOCK, MINW) void shade_kernel(const DevGeom *__res
                     tri = key == ~0ull ? -1 : (int)g.wrank_id[(uint32_t)key];
                     s.distance = key == ~0ull ? -1.0f : __uint_as_float((uint32_t)(key >> 32));
                 }
+                pf.tick(P_FILL);
+                pf.call(P_FILL);
                 finish_fill(g, s, p, tri);
+                pf.tick(P_PHYS);
                 if (p.last_hit != -1) {
+                    pf.call(P_PHYS);
                     int command = propagate_to_boundary(g, p, s, rng, a.use_weights, a.scatter_first);
                     if (command == PASS && s.surface_index != -1)
                         command = propagate_at_surface(g, p, s, rng, a.use_weights);
                     if (command == PASS) propagate_at_boundary(p, s, rng);
                 }
+                pf.tick(P_OTHER);
             }
             const uint32_t pid = cur.pid;
             store3(a.pos, pid, p.pos);
@@ -1642,6 +1776,13 @@ __global__ __launch_bounds__(BLOCK, MINW) void shade_kernel(const DevGeom *__res
         if ((slot & 63u) == 0) a.alive_masks[qb >> 6] = mask;
     }
     if (have_rng) store_rng(a, slot, rng);
+#ifdef CHR_DEVICE_PROFILE
+    pf.tick(P_OTHER);
+    prof_add(CHR_PROF_FILL_MATERIAL, pf.calls[P_FILL], pf.cyc[P_FILL]);
+    prof_add(CHR_PROF_SHADE_PHYSICS, pf.calls[P_PHYS], pf.cyc[P_PHYS]);
+    prof_add(CHR_PROF_SHADE_OTHER, 0ull, pf.cyc[P_OTHER]);
+    prof_add(CHR_PROF_SHADE_KERNEL, 1ull, pf.total());
+#endif
 }
 
 // Multi-step launches (the tail of the nsteps policy, photon.py:261-264): a
@@ -1655,8 +1796,9 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_group_kernel(const DevG
                                                                       uint32_t cap) {
     __shared__ uint32_t group_stacks[(BLOCK / G) * GROUP_STACK * 2];
     const uint32_t tid = blockIdx.x * BLOCK + threadIdx.x;
+    if (a.mode && *a.mode != a.want) return;
     const uint32_t slot = tid / G, sub = tid & (uint32_t)(G - 1);
-    const uint32_t n = (uint32_t)a.nthreads;
+    const uint32_t n = a.dev_n ? *a.dev_n - 1u : (uint32_t)a.nthreads;
     if (slot >= cap || slot >= n) return;          // whole groups
     Stack st;
     st.lds = nullptr;
@@ -1769,10 +1911,9 @@ __device__ int walk_segment(const DevGeom &g, bool act, V3 o, V3 d, uint32_t las
         const bool refill = em != 0 && sp > 0;
         while (em != 0 && sp > 0) {
             const int W = sp < 8 ? sp : 8;
-            uint32_t en = 0, et = 0;
+            uint32_t et = 0;
             bool ok = false;
             if (L < (uint32_t)W) {
-                en = stk[2 * (sp - 1 - (int)L)];
                 et = stk[2 * (sp - 1 - (int)L) + 1];
                 ok = !(__uint_as_float(et) > best);           // mesh.h:94-96
             }
@@ -1930,8 +2071,9 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_tail_kernel(const DevGe
     __shared__ uint32_t tris[(BLOCK / 64) * 2 * TAIL_TRI];
     const uint32_t tid = blockIdx.x * BLOCK + threadIdx.x;
     const uint32_t lane = __lane_id();
+    if (a.mode && *a.mode != a.want) return;
     const uint32_t slot = tid / 8, sub = tid & 7u;
-    const uint32_t n = (uint32_t)a.nthreads;
+    const uint32_t n = a.dev_n ? *a.dev_n - 1u : (uint32_t)a.nthreads;
     const uint32_t nslot = cap < n ? cap : n;
     if ((tid & ~63u) / 8 >= nslot) return;             // whole waves: the others help walk
     CHR_LDS uint32_t *wstack = (CHR_LDS uint32_t *)stacks + (threadIdx.x >> 6) * 8 * TAIL_STACK * 2;
@@ -1946,6 +2088,9 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_tail_kernel(const DevGe
     uint32_t q = slot, pid = 0, iters = 0;
     bool live = false, exhausted = slot >= nslot;
     unsigned long long t0 = 0, walk_ticks = 0;
+    enum { P_WALK, P_PHYS, P_OTHER };
+    Prof<3> pf;
+    pf.start(P_OTHER);
     // run_photon's write-back (propagate.cu:343-353) and the alive bit
     auto finish = [&]() {
         store3(a.pos, pid, p.pos);
@@ -2022,6 +2167,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_tail_kernel(const DevGe
         const int w = __popcll(wm);
         const unsigned long long tw0 = __builtin_amdgcn_s_memrealtime();
         if (w > 0) {
+            pf.tick(P_WALK);   // the whole wave walks
             const int Gs = w == 1 ? 64 : (w == 2 ? 32 : (w <= 4 ? 16 : 8));
             const int si = (int)lane / Gs;
             unsigned long long m = wm;
@@ -2044,9 +2190,13 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_tail_kernel(const DevGe
                 iters += it;
                 walk_ticks += __builtin_amdgcn_s_memrealtime() - tw0;
             }
+            pf.tick(P_OTHER);
         }
         if (walk) {   // the rest of the step (run_photon's loop body)
+            pf.tick(P_PHYS);
             if (sub == 0) {
+                pf.call(P_WALK);
+                pf.call(P_PHYS);
                 const V3 inv = v3(1.0f / p.dir.x, 1.0f / p.dir.y, 1.0f / p.dir.z);
                 if (!(chr_isfinite(inv.x) && chr_isfinite(inv.y) && chr_isfinite(inv.z))) flat++;
             }
@@ -2066,12 +2216,20 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_tail_kernel(const DevGe
                     if (command == PASS) propagate_at_boundary(p, s, rng);
                 }
             }
+            pf.tick(P_OTHER);
             if (stop) finish();
         }
     }
     if (have_rng && sub == 0) store_rng(a, slot, rng);
     if (sub == 0 && overflow) atomicAdd(a.counters, overflow);
     if (sub == 0 && flat && a.diag) atomicAdd(a.diag, flat);
+#ifdef CHR_DEVICE_PROFILE
+    pf.tick(P_OTHER);
+    prof_add(CHR_PROF_TAIL_WALK, pf.calls[P_WALK], pf.cyc[P_WALK]);
+    prof_add(CHR_PROF_TAIL_PHYSICS, pf.calls[P_PHYS], pf.cyc[P_PHYS]);
+    prof_add(CHR_PROF_TAIL_OTHER, 0ull, pf.cyc[P_OTHER]);
+    prof_add(CHR_PROF_TAIL_KERNEL, 1ull, pf.total());
+#endif
 }
 
 // ---------------------------------------------------------------- ray binning (trace order)
@@ -2133,6 +2291,10 @@ struct TraceArgs {
     const uint32_t *flat_count;  // how many (device word)
     unsigned long long *flat_best;   // per flat walk: min over its sub-walks of (distance bits << 32 | rank)
     uint32_t *diag;              // [0] += flat walks of this launch (nullptr: off)
+    // device-driven steps (nullptr: host-driven): the queue length is *dev_n - 1
+    // (the input queue's count header) and the launch runs only if *mode is STEP_ONE
+    const uint32_t *dev_n;
+    const uint32_t *mode;
 };
 
 // Enrol queue position p for the next trace launch if its walk is flat
@@ -2177,6 +2339,8 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
     st.node = (CHR_LDS uint32_t *)(lds + threadIdx.x);
     st.dist = (CHR_LDS float *)(lds + SL * BLOCK + threadIdx.x);
     st.leafq = (CHR_LDS uint32_t *)(lds + 2 * SL * BLOCK + threadIdx.x);
+    if (a.mode && *a.mode != STEP_ONE) return;
+    const uint32_t n = a.dev_n ? *a.dev_n - 1u : a.n;
     const DevGeom &g = *gdev;
     const uint32_t lane = __lane_id();
     uint32_t overflow = 0;
@@ -2187,7 +2351,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
     // per flat walk (K = the geometry's cut size; 1 = the whole walk)
     const uint32_t nflat = a.flat_count ? *a.flat_count : 0u;
     const uint32_t K = (g.nwcut > 1u && nflat <= (1u << 30) / g.nwcut) ? g.nwcut : 1u;
-    const uint32_t total = a.n + nflat * K;
+    const uint32_t total = n + nflat * K;
     int flat_f = -1;                // flat walk of the current sub-walk (-1: an ordinary ray)
     uint32_t cmask = 0xFFu;         // children of the first node this walk may enter
     V3 o = v3(0.0f, 0.0f, 0.0f), d = v3(0.0f, 0.0f, 1.0f);
@@ -2198,7 +2362,11 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
     bool walk_done = true;
     uint32_t qh = 0, qt = 0, pcur = 0, pleft = 0;
     constexpr uint32_t INVALID = 0xFFFFFFFFu;
+    enum { P_NODE, P_TRI, P_REFILL, P_IDLE, P_BOX = 3 };   // regions (calls: P_REFILL = walks, P_BOX = boxes)
+    Prof<4> pf;
+    pf.start(P_REFILL);
     while (true) {
+        pf.tick(P_REFILL);   // the last step goes to the region each work-item was in
         if (has_ray && walk_done && pleft == 0 && qh == qt) {   // walk over: publish (mesh.h:123-125)
             if (flat_f < 0) a.hits[q] = make_int2(best_id, __float_as_int(best_id == -1 ? -1.0f : best));
             else if (best_id != -1)   // a sub-walk: its best joins the flat walk's minimum
@@ -2223,7 +2391,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
                 if (!has_ray) {
                     const uint32_t j = base + (uint32_t)__popcll(need & ((1ull << lane) - 1ull));
                     bool start = false;
-                    if (j < a.n) {
+                    if (j < n) {
                         q = a.order ? a.order[j] : j;
                         pid = a.queue[q];
                         // dead on entry / NaN: no walk (the step kernel skips / aborts them);
@@ -2242,7 +2410,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
                             }
                         }
                     } else if (j < total) {                       // sub-walk k of flat walk f
-                        const uint32_t it = j - a.n, f = it / K, k = it - f * K;
+                        const uint32_t it = j - n, f = it / K, k = it - f * K;
                         q = a.flat_q[f];
                         pid = a.queue[q];
                         o = load3(a.pos, pid);
@@ -2267,11 +2435,13 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
                         walk_done = false;
                         has_ray = true;
                         walk_cost = 0;
+                        pf.call(P_REFILL);
                         if constexpr (COUNT) cnt.walks++;
                     }
                 }
             }
         }
+        pf.tick(P_IDLE);
         const bool has_work = has_ray && (pleft != 0 || qh != qt);
         const bool can_walk = has_ray && !walk_done && (qt - qh) <= (uint32_t)(LEAFQ - 8);
         const unsigned long long mw = __ballot(can_walk);
@@ -2283,6 +2453,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
         if (mw != 0 && 8 * __popcll(mt) < F * __popcll(mw | mt)) {
             // ------------------------------------------------ node step
             if (!can_walk) continue;
+            pf.set(P_NODE);
             if (node == INVALID) {
                 bool found = false;
                 while (sp > 0) {
@@ -2297,6 +2468,11 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
             const uint4 *np = g.wnodes + (size_t)g.wstride * node;
             const uint4 h = gld(np), a1 = gld(np + 1), a2 = gld(np + 2), a3 = gld(np + 3), a4 = gld(np + 4),
                         a5 = gld(np + 5);
+#ifdef CHR_DEVICE_PROFILE
+            pf.call(P_NODE);
+            for (int k = 0; k < 8; ++k)
+                pf.call(P_BOX, ((((k < 4 ? a4.z : a4.w) >> (8 * (k & 3))) & 0xFFu) != 0u && ((cmask >> k) & 1u)) ? 1u : 0u);
+#endif
             uint32_t near_node;
             float near_t;
             uint32_t leaf_mask =
@@ -2314,6 +2490,8 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
         } else {
             // ------------------------------------------------ triangle step
             if (!has_work) continue;
+            pf.set(P_TRI);
+            pf.call(P_TRI);
             if (pleft == 0) {
                 const uint32_t e = st.leafq[(qh % LEAFQ) * BLOCK];
                 qh++;
@@ -2336,15 +2514,22 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
             V3 lo, hi;
             node_bounds(g, make_uint4(__float_as_uint(r2.w), __float_as_uint(r3.x), __float_as_uint(r3.y), 0u), lo, hi);
             float bd;
-            if (!intersect_box(v3(-o.x / d.x, -o.y / d.y, -o.z / d.z), v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z), lo, hi,
-                               bd) ||
-                bd > best)
-                continue;                                // mesh.h:94-96
+            if (!intersect_box_slab(slab, lo, hi, bd) || bd > best) continue;   // mesh.h:94-96
             best = dist;
             best_rank = rank;
             best_id = (int)id;
         }
     }
+#ifdef CHR_DEVICE_PROFILE
+    pf.tick(P_IDLE);
+    prof_add(CHR_PROF_INTERSECT_MESH, pf.calls[P_REFILL], (unsigned long long)pf.cyc[P_NODE] + pf.cyc[P_TRI]);
+    prof_add(CHR_PROF_INTERSECT_NODE, pf.calls[P_NODE], pf.cyc[P_NODE]);
+    prof_add(CHR_PROF_INTERSECT_TRIANGLE, pf.calls[P_TRI], pf.cyc[P_TRI]);
+    prof_add(CHR_PROF_INTERSECT_BOX, pf.calls[P_BOX], 0ull);
+    prof_add(CHR_PROF_TRACE_REFILL, 0ull, pf.cyc[P_REFILL]);
+    prof_add(CHR_PROF_TRACE_IDLE, 0ull, pf.cyc[P_IDLE]);
+    prof_add(CHR_PROF_TRACE_KERNEL, 1ull, pf.total());
+#endif
     if (overflow) atomicAdd(a.counters, overflow);
     if (a.diag && nflat && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(a.diag, nflat);
     if constexpr (COUNT) {
@@ -2407,8 +2592,11 @@ __global__ __launch_bounds__(BLOCK) void sort_key_kernel(const float *pos, const
 // Consumers add block_prefix[w >> 8] to word_offsets[w].
 constexpr int SCAN_WORDS = 256;
 __global__ __launch_bounds__(SCAN_WORDS) void mask_block_scan_kernel(const unsigned long long *masks, uint32_t nwords,
-                                                                     uint32_t *word_offsets, uint32_t *block_sums) {
+                                                                     uint32_t *word_offsets, uint32_t *block_sums,
+                                                                     const uint32_t *dev_n, const uint32_t *mode) {
     __shared__ uint32_t wave_tot[SCAN_WORDS / 64];
+    if (mode && *mode == STEP_IDLE) return;
+    if (dev_n) nwords = (*dev_n - 1u + 63u) / 64u;
     const uint32_t w = blockIdx.x * SCAN_WORDS + threadIdx.x;
     const uint32_t c = w < nwords ? (uint32_t)__popcll(masks[w]) : 0u;
     // inclusive scan within the wave (shuffles), then across the 4 waves
@@ -2430,8 +2618,9 @@ __global__ __launch_bounds__(SCAN_WORDS) void mask_block_scan_kernel(const unsig
 
 __global__ __launch_bounds__(1024) void scan_block_sums_kernel(uint32_t *block_sums, uint32_t nblocks,
                                                                uint32_t *out_counter, uint32_t *base,
-                                                               uint32_t *total_out) {
+                                                               uint32_t *total_out, const uint32_t *mode) {
     __shared__ uint32_t partial[1024];
+    if (mode && *mode == STEP_IDLE) return;
     const uint32_t tid = threadIdx.x;
     const uint32_t per = (nblocks + 1023) / 1024;
     const uint32_t b0 = tid * per;
@@ -2474,29 +2663,66 @@ struct FlatEnrol {
 __global__ __launch_bounds__(BLOCK) void scatter_queue_kernel(const unsigned long long *masks, const uint32_t *word_offsets,
                                                                const uint32_t *block_prefix, const uint32_t *base,
                                                                const uint32_t *in_queue, int32_t first, int32_t n,
-                                                               uint32_t *out_queue, FlatEnrol fe) {
-    const int id = blockIdx.x * BLOCK + threadIdx.x;
-    if (id >= n) return;
-    const unsigned long long m = masks[id >> 6];
-    const int lane = id & 63;
-    if ((m >> lane) & 1ull) {
-        const uint32_t rank = __popcll(m & ((1ull << lane) - 1ull));
-        const uint32_t o = base[0] + word_offset(word_offsets, block_prefix, (uint32_t)id >> 6) + rank;
-        const uint32_t pid = in_queue[first + id];
-        out_queue[o] = pid;
-        // out_queue[0] is the count header: position o - 1 of the next step's queue
-        if (fe.pos) enrol_flat(fe.pos, fe.dir, pid, o - 1u, fe.hits, fe.flat_q, fe.flat_count, fe.flat_best);
+                                                               uint32_t *out_queue, FlatEnrol fe, const uint32_t *dev_n,
+                                                               const uint32_t *mode) {
+    if (mode && *mode == STEP_IDLE) return;
+    if (dev_n) n = (int32_t)(*dev_n - 1u);
+    // grid-stride (device-driven steps launch one grid for any queue length)
+    for (int id = blockIdx.x * BLOCK + threadIdx.x; id < n; id += gridDim.x * BLOCK) {
+        const unsigned long long m = masks[id >> 6];
+        const int lane = id & 63;
+        if ((m >> lane) & 1ull) {
+            const uint32_t rank = __popcll(m & ((1ull << lane) - 1ull));
+            const uint32_t o = base[0] + word_offset(word_offsets, block_prefix, (uint32_t)id >> 6) + rank;
+            const uint32_t pid = in_queue[first + id];
+            out_queue[o] = pid;
+            // out_queue[0] is the count header: position o - 1 of the next step's queue
+            if (fe.pos) enrol_flat(fe.pos, fe.dir, pid, o - 1u, fe.hits, fe.flat_q, fe.flat_count, fe.flat_best);
+        }
     }
 }
 
+// Head of a device-driven step slot: the input queue's length picks the slot's
+// mode -- the nsteps policy of photon.py:261-264 (one-step launch; the
+// multi-step tail below `tail_below` photons or with use_weights, when more
+// than one step remains; nothing once the queue is empty or the tail ran) --
+// and the slot's bookkeeping is reset: output queue header, trace ray counter.
+__global__ void step_head_kernel(const uint32_t *in_hdr, uint32_t *out_hdr, uint32_t *mode, uint32_t *n_out,
+                                 uint32_t *done, uint32_t *ray_counter, uint32_t tail_below, int32_t remaining,
+                                 int32_t use_weights, uint32_t max_n) {
+    if (threadIdx.x != 0) return;
+    const uint32_t n = in_hdr[0] - 1u;
+    uint32_t m = STEP_IDLE;
+    if (!done[0]) {
+        if (n == 0 || n > max_n) done[0] = 1u;   // empty (or a corrupt header: run nothing)
+        else if ((n < tail_below || use_weights) && remaining > 1) { m = STEP_TAIL; done[0] = 1u; }
+        else m = STEP_ONE;
+    }
+    mode[0] = m;
+    n_out[0] = n;
+    if (m != STEP_IDLE) {
+        out_hdr[0] = 1u;
+        ray_counter[0] = 0u;
+    }
+}
+
+// alive-mask words of a tail slot (OR-ed by its kernel) zeroed, for the slot's queue length
+__global__ __launch_bounds__(BLOCK) void clear_masks_kernel(unsigned long long *masks, const uint32_t *dev_n,
+                                                            const uint32_t *mode) {
+    if (*mode != STEP_TAIL) return;
+    const uint32_t nwords = (*dev_n - 1u + 63u) / 64u;
+    for (uint32_t w = blockIdx.x * BLOCK + threadIdx.x; w < nwords; w += gridDim.x * BLOCK) masks[w] = 0ull;
+}
+
 // photon.py:242-250: input queue entries (from q0[1]) = photon ids with the
-// ncopies clones of a photon interleaved; q0[0] = 0, q1[0] = 1 (count + 1)
+// ncopies clones of a photon interleaved; count headers q0[0] = n + 1 (the
+// input's length, read by device-driven steps), q1[0] = 1 (empty output)
 __global__ __launch_bounds__(BLOCK) void init_queue_kernel(uint32_t *q0, uint32_t *q1, uint32_t n, uint32_t true_n,
                                                            uint32_t ncopies) {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     if (i >= n) return;
     q0[1 + i] = i / ncopies + (i % ncopies) * true_n;
-    if (i == 0) { q0[0] = 0u; q1[0] = 1u; }
+    if (i == 0) { q0[0] = n + 1u; q1[0] = 1u; }
 }
 
 // ---------------------------------------------------------------- RNG init
@@ -2631,12 +2857,13 @@ inline uint32_t scan_blocks(uint32_t nwords) { return (nwords + SCAN_WORDS - 1) 
 
 // word_offsets (nwords) + block prefixes (scan_blocks(nwords)) of the masks
 void launch_mask_scan(const unsigned long long *masks, uint32_t nwords, uint32_t *word_offsets, uint32_t *block_sums,
-                      uint32_t *out_counter, uint32_t *base, uint32_t *total_out, hipStream_t stream) {
-    const uint32_t nb = scan_blocks(nwords);
+                      uint32_t *out_counter, uint32_t *base, uint32_t *total_out, hipStream_t stream,
+                      const uint32_t *dev_n = nullptr, const uint32_t *mode = nullptr) {
+    const uint32_t nb = scan_blocks(nwords);   // device-driven: nwords is an upper bound
     if (nb) hipLaunchKernelGGL(mask_block_scan_kernel, dim3(nb), dim3(SCAN_WORDS), 0, stream, masks, nwords, word_offsets,
-                               block_sums);
+                               block_sums, dev_n, mode);
     hipLaunchKernelGGL(scan_block_sums_kernel, dim3(1), dim3(1024), 0, stream, block_sums, nb, out_counter, base,
-                       total_out);
+                       total_out, mode);
 }
 
 PhotonPtrs to_ptrs(const chr_photons *p) {
@@ -2894,6 +3121,12 @@ static int launch_chunk(const chr_geometry *g, const chr_photons *ph, uint32_t *
     a.alive_masks = masks; a.counters = counters;
     a.order = nullptr;
     a.hits = nullptr;
+    a.flat_best = nullptr;
+    a.zero_word = nullptr;
+    a.diag = nullptr;
+    a.dev_n = nullptr;
+    a.mode = nullptr;
+    a.want = STEP_ONE;
     if (sort_enabled() && nthreads >= kSortMin) {
         // coherence order (sort_key_kernel): rays that start close together in
         // similar directions share a wave
@@ -2917,7 +3150,8 @@ static int launch_chunk(const chr_geometry *g, const chr_photons *ph, uint32_t *
     launch_mask_scan(masks, nwords, offsets, bsums, out_queue, counters + 1, nullptr, stream);
     hipLaunchKernelGGL(scatter_queue_kernel, dim3(grid_for(nthreads)), dim3(BLOCK), 0, stream, masks, offsets, bsums,
                        counters + 1, in_queue, first, nthreads, out_queue,
-                       FlatEnrol{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr});
+                       FlatEnrol{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr}, (const uint32_t *)nullptr,
+                       (const uint32_t *)nullptr);
     CHR_HIP_CHECK(hipGetLastError());
     return CHR_OK;
 }
@@ -2967,17 +3201,33 @@ static int flat_get(uint32_t n, FlatCtx &fc) {
 }
 
 static bool trace_steps();
+// A device-driven step slot (chr_propagate without a host round trip per
+// step): the slot's kernels read the queue length from the input queue's
+// header and run by the mode step_head_kernel picks; n passed to launch_step
+// is then an upper bound that sizes grids and scratch.
+struct SlotCtl {
+    uint32_t *mode;        // this slot's mode word (device)
+    uint32_t *nk;          // this slot's queue length, written by the head kernel (device)
+    uint32_t *done;        // set once the queue is empty or the tail ran (device)
+    uint32_t n_layout;     // photons of the propagate: layout of the hits / binning regions
+    int32_t remaining;     // steps left (max_steps - step)
+    uint32_t tail_below;   // the nsteps policy's threshold, nthreads_per_block * 128
+};
+
 // hits: n (triangle, distance) slots + a ray counter word, for the split path
 static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *rng, uint32_t nslots, uint32_t cap,
                        uint32_t n, const uint32_t *in_queue, uint32_t *out_queue, int32_t max_steps,
                        int32_t use_weights, int32_t scatter_first, uint32_t *scratch, hipStream_t stream,
                        hipEvent_t ev0, hipEvent_t ev1, int2 *hits, uint32_t *sort_space, bool first_step,
-                       hipEvent_t evt0, hipEvent_t evt1, bool *split_out, const FlatCtx *fc) {
+                       hipEvent_t evt0, hipEvent_t evt1, bool *split_out, const FlatCtx *fc,
+                       const SlotCtl *sc = nullptr) {
     const uint32_t nwords = (n + 63) / 64;
     uint32_t *counters = scratch;
     unsigned long long *masks = (unsigned long long *)(scratch + 16);
     uint32_t *offsets = scratch + 16 + 2 * (size_t)nwords;
     uint32_t *bsums = offsets + nwords;
+    const uint32_t *dev_n = sc ? in_queue - 1 : nullptr;   // the input queue's count header
+    const uint32_t *mode = sc ? sc->mode : nullptr;
     PropagateArgs a;
     a.pos = ph->d_pos; a.dir = ph->d_dir; a.pol = ph->d_pol; a.wl = ph->d_wavelengths; a.t = ph->d_t;
     a.weights = ph->d_weights; a.flags = ph->d_flags; a.last_hit = ph->d_last_hit_triangles; a.evidx = ph->d_evidx;
@@ -2989,15 +3239,30 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
     a.flat_best = nullptr;
     a.zero_word = nullptr;
     a.diag = fc ? fc->ctl + 4 : nullptr;
+    a.dev_n = dev_n;
+    a.mode = mode;
+    a.want = STEP_ONE;
     FlatEnrol fe{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
     const uint32_t threads = std::min(cap, (n + 63u) & ~63u);
     const StepVariant sv = select_step_variant(g);
-    const bool split = sv.trace && hits && max_steps == 1 && fc;
-    if (split) {
-        uint32_t *next = (uint32_t *)(hits + n);
+    // host-driven: the split when this launch is one step; device-driven: the
+    // one-step kernels and the tail kernel are both queued and the head picks
+    const bool split = sv.trace && hits && fc && (sc ? true : max_steps == 1);
+    const bool tail = sv.tail && (sc ? sc->remaining > 1 : (!split && max_steps > 1));
+    // the first step's length and mode are known on the host (binning, flat-walk enrolment)
+    const bool first_one_step = first_step && (!sc || !((n < sc->tail_below || use_weights) && sc->remaining > 1));
+    uint32_t *next = split ? (uint32_t *)(hits + (sc ? sc->n_layout : n)) : nullptr;
+    if (ev0) CHR_HIP_CHECK(hipEventRecord(ev0, stream));
+    if (sc) {
+        if (!next) return chr::fail(CHR_ERR_INVALID, "launch_step: device-driven steps need the split path");
+        hipLaunchKernelGGL(step_head_kernel, dim3(1), dim3(64), 0, stream, in_queue - 1, out_queue, sc->mode, sc->nk,
+                           sc->done, next, sc->tail_below, sc->remaining, use_weights, sc->n_layout);
+    } else if (split) {
         CHR_HIP_CHECK(hipMemsetAsync(next, 0, 4, stream));
+    }
+    if (split) {
         uint32_t *count_cur = fc->ctl + 1 + fc->cur, *count_next = fc->ctl + 1 + (fc->cur ^ 1);
-        if (first_step)   // flat walks of the initial queue (later steps: enrolled by the previous scatter)
+        if (first_one_step)   // flat walks of the initial queue (later steps: enrolled by the previous scatter)
             hipLaunchKernelGGL(classify_kernel, dim3(grid_for(n)), dim3(BLOCK), 0, stream, ph->d_pos, ph->d_dir,
                                ph->d_flags, in_queue, n, hits, fc->flat_q, count_cur, fc->flat_best);
         TraceArgs ta;
@@ -3005,27 +3270,31 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
         ta.queue = in_queue; ta.n = n; ta.hits = hits; ta.next = next; ta.counters = counters; ta.order = nullptr;
         ta.walk_hist = nullptr;
         ta.flat_q = fc->flat_q; ta.flat_count = count_cur; ta.flat_best = fc->flat_best; ta.diag = fc->ctl + 3;
+        ta.dev_n = dev_n;
+        ta.mode = mode;
         a.flat_best = fc->flat_best;
         a.zero_word = count_next;   // cleared by the shade pass, filled by this step's scatter
         if (fc->enrol_next)
             fe = FlatEnrol{ph->d_pos, ph->d_dir, hits, fc->flat_q, count_next, fc->flat_best};
         if (trace_steps()) {   // debugging: per-walk cost histogram (counting variants), printed per step
-            ta.walk_hist = next + 16 + 2 * (size_t)n;
+            ta.walk_hist = next + 16 + 2 * (size_t)(sc ? sc->n_layout : n);
             CHR_HIP_CHECK(hipMemsetAsync(ta.walk_hist, 0, 34 * 4, stream));
         }
-        if (ev0) CHR_HIP_CHECK(hipEventRecord(ev0, stream));
-        if (sv.binned == 1 || (sv.binned == 2 && first_step && n >= kBinFirstMin)) {
+        if (sv.binned == 1 || (sv.binned == 2 && first_one_step && n >= kBinFirstMin)) {
             // 16-bit radix sort of (direction cell, queue position); hits region:
             // [hits n x int2][next + pad, 16 words][keys n][values n][walk hist 64 words]
-            uint32_t *keys = next + 16, *order = keys + n;
-            hipLaunchKernelGGL(bin_key_kernel, dim3(grid_for(n)), dim3(BLOCK), 0, stream, ph->d_dir, in_queue, n, keys,
-                               order);
-            uint32_t *keys_out = sort_space, *vals_out = keys_out + n;
-            void *temp = (void *)(((uintptr_t)(vals_out + n) + 255) & ~(uintptr_t)255);
-            size_t temp_bytes = sort_temp_bytes16(n);
-            CHR_HIP_CHECK(rocprim::radix_sort_pairs(temp, temp_bytes, keys, keys_out, order, vals_out, n, 0, 16,
-                                                    stream));
-            ta.order = vals_out;
+            // (device-driven slots bin only the first step, whose length the host knows)
+            if (!sc || first_one_step) {
+                uint32_t *keys = next + 16, *order = keys + n;
+                hipLaunchKernelGGL(bin_key_kernel, dim3(grid_for(n)), dim3(BLOCK), 0, stream, ph->d_dir, in_queue, n,
+                                   keys, order);
+                uint32_t *keys_out = sort_space, *vals_out = keys_out + n;
+                void *temp = (void *)(((uintptr_t)(vals_out + n) + 255) & ~(uintptr_t)255);
+                size_t temp_bytes = sort_temp_bytes16(n);
+                CHR_HIP_CHECK(rocprim::radix_sort_pairs(temp, temp_bytes, keys, keys_out, order, vals_out, n, 0, 16,
+                                                        stream));
+                ta.order = vals_out;
+            }
         }
         const int cus = device_cus();
         if (cus <= 0) return chr::fail(CHR_ERR_HIP, "launch_step: no compute units");
@@ -3036,23 +3305,26 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
         hipLaunchKernelGGL(sv.trace, dim3(blocks), dim3(BLOCK), 0, stream, (const DevGeom *)g->d_dev, ta);
         if (evt1) CHR_HIP_CHECK(hipEventRecord(evt1, stream));
         a.hits = hits;
-    } else if (ev0) {
-        CHR_HIP_CHECK(hipEventRecord(ev0, stream));
+        a.max_steps = 1;
+        hipLaunchKernelGGL(sv.shade, dim3(grid_for(threads)), dim3(BLOCK), 0, stream, (const DevGeom *)g->d_dev, a, cap);
     }
     if (split_out) *split_out = split;
-    if (!split && sv.tail && max_steps > 1) {   // group walk, alive bits OR-ed
-        CHR_HIP_CHECK(hipMemsetAsync(masks, 0, (size_t)nwords * 8, stream));
-        if (ev0) CHR_HIP_CHECK(hipEventRecord(ev0, stream));
+    if (tail) {   // group / wave-adaptive walk, alive bits OR-ed into zeroed words
+        if (sc) hipLaunchKernelGGL(clear_masks_kernel, dim3(std::min<uint32_t>(1024u, grid_for(nwords))), dim3(BLOCK), 0,
+                                   stream, masks, dev_n, mode);
+        else CHR_HIP_CHECK(hipMemsetAsync(masks, 0, (size_t)nwords * 8, stream));
+        a.max_steps = sc ? sc->remaining : max_steps;
+        a.want = STEP_TAIL;
         hipLaunchKernelGGL(sv.tail, dim3(grid_for((uint64_t)threads * sv.tail_group)), dim3(BLOCK), 0, stream,
                            (const DevGeom *)g->d_dev, a, cap);
-    } else {
-        hipLaunchKernelGGL(split ? sv.shade : sv.fn, dim3(grid_for(threads)), dim3(BLOCK), 0, stream,
-                           (const DevGeom *)g->d_dev, a, cap);
+    } else if (!split) {
+        hipLaunchKernelGGL(sv.fn, dim3(grid_for(threads)), dim3(BLOCK), 0, stream, (const DevGeom *)g->d_dev, a, cap);
     }
     if (ev1) CHR_HIP_CHECK(hipEventRecord(ev1, stream));
-    launch_mask_scan(masks, nwords, offsets, bsums, out_queue, counters + 1, nullptr, stream);
-    hipLaunchKernelGGL(scatter_queue_kernel, dim3(grid_for(n)), dim3(BLOCK), 0, stream, masks, offsets, bsums,
-                       counters + 1, in_queue, 0, (int32_t)n, out_queue, fe);
+    launch_mask_scan(masks, nwords, offsets, bsums, out_queue, counters + 1, nullptr, stream, dev_n, mode);
+    hipLaunchKernelGGL(scatter_queue_kernel, dim3(sc ? std::min<uint32_t>(4096u, grid_for(n)) : grid_for(n)), dim3(BLOCK),
+                       0, stream, masks, offsets, bsums, counters + 1, in_queue, 0, (int32_t)n, out_queue, fe, dev_n,
+                       mode);
     CHR_HIP_CHECK(hipGetLastError());
     return CHR_OK;
 }
@@ -3075,7 +3347,7 @@ static int pinned_words(uint32_t **out) {
     static thread_local uint32_t *p[16] = {};
     int dev = 0;
     CHR_HIP_CHECK(hipGetDevice(&dev));
-    if (!p[dev & 15]) CHR_HIP_CHECK(hipHostMalloc((void **)&p[dev & 15], 256, hipHostMallocDefault));
+    if (!p[dev & 15]) CHR_HIP_CHECK(hipHostMalloc((void **)&p[dev & 15], 512, hipHostMallocDefault));
     *out = p[dev & 15];
     return CHR_OK;
 }
@@ -3118,6 +3390,28 @@ static bool trace_steps() {   // CHR_TRACE_STEPS=1: one stderr line per host ste
 static bool step_launch_enabled() {   // CHR_STEP_LAUNCH=0: the reference's one-launch-per-chunk structure (A/B)
     const char *e = getenv("CHR_STEP_LAUNCH");
     return !(e && e[0] == '0');
+}
+
+static bool host_steps_forced() {     // CHR_HOST_STEPS=1: read the survivor count on the host every step (A/B)
+    const char *e = getenv("CHR_HOST_STEPS");
+    return e && e[0] == '1';
+}
+
+// per-slot control words of a device-driven propagate: [2k] mode, [2k + 1]
+// queue length of slot k, then the done flag (per thread and device, grown on demand)
+static int slot_ctl_get(size_t words, uint32_t **out) {
+    static thread_local Scratch s[16];
+    int dev = 0;
+    CHR_HIP_CHECK(hipGetDevice(&dev));
+    Scratch &x = s[dev & 15];
+    if (x.bytes < words * 4) {
+        if (x.ptr) CHR_HIP_CHECK(hipFree(x.ptr));
+        x.ptr = nullptr;
+        CHR_HIP_CHECK(hipMalloc(&x.ptr, words * 4));
+        x.bytes = words * 4;
+    }
+    *out = (uint32_t *)x.ptr;
+    return CHR_OK;
 }
 
 extern "C" int chr_propagate(const chr_geometry *g, const chr_photons *ph, uint32_t nphotons, uint32_t true_nphotons,
@@ -3170,6 +3464,7 @@ extern "C" int chr_propagate(const chr_geometry *g, const chr_photons *ph, uint3
     std::vector<hipEvent_t> &events = *evp;
     double kernel_ms = 0.0, trace_ms = 0.0;
     bool split_step = false, tail_step = false;
+    int64_t n_launch = 0;   // queue length of the launch being collected
     auto collect = [&](size_t nchunks) -> int {
         for (size_t c = 0; c < nchunks; ++c) {
             float ms = 0.0f;
@@ -3181,7 +3476,10 @@ extern "C" int chr_propagate(const chr_geometry *g, const chr_photons *ph, uint3
             float ms = 0.0f;
             CHR_HIP_CHECK(hipEventElapsedTime(&ms, events[2], events[3]));
             trace_ms += ms;
-            if (st.trace_ms_n < CHR_TRACE_MS_MAX) st.trace_launch_ms[st.trace_ms_n++] = ms;
+            if (st.trace_ms_n < CHR_TRACE_MS_MAX) {
+                st.trace_launch_rays[st.trace_ms_n] = (uint32_t)n_launch;
+                st.trace_launch_ms[st.trace_ms_n++] = ms;
+            }
         }
         return CHR_OK;
     };
@@ -3193,9 +3491,82 @@ extern "C" int chr_propagate(const chr_geometry *g, const chr_photons *ph, uint3
     int cur = 0;
     int64_t n = nphotons;
     int step = 0;
-    while (step < max_steps) {
+    // Device-driven steps: every slot's kernels read the queue length from the
+    // queue header and the head kernel applies the nsteps policy, so the host
+    // queues slot k + 1 while slot k runs and only waits (on slot k - 1's
+    // event, already done by then) to learn when the tail has run -- no
+    // survivor-count round trip between steps.  Same launches, same results.
+    const bool device_steps = fused && !trace_steps() && !host_steps_forced() && select_step_variant(g).trace != nullptr;
+    if (device_steps) {
+        const uint32_t tail_below = (uint32_t)ntpb * 16 * 8;   // photon.py:261-264
+        uint32_t *ctl = nullptr;
+        if ((rc = slot_ctl_get(2 * (size_t)max_steps + 8, &ctl))) return rc;
+        uint32_t *done = ctl + 2 * (size_t)max_steps;
+        CHR_HIP_CHECK(hipMemsetAsync(done, 0, 4, stream));
+        uint32_t *ring = pinned + 64;   // (mode, n) of recent slots, 32 entries (copied after each slot)
+        uint32_t n_ub = nphotons;
+        int k = 0;
+        bool stop = false;
+        while (k < max_steps && !stop) {
+            if ((rc = timing_events(5 * (size_t)(k + 1), &evp))) return rc;
+            hipEvent_t *ev = events.data() + 5 * (size_t)k;
+            SlotCtl sc{ctl + 2 * (size_t)k, ctl + 2 * (size_t)k + 1, done, nphotons, max_steps - k, tail_below};
+            bool split = false;
+            rc = launch_step(g, ph, d_rng_states, rng_nslots, (uint32_t)cap, n_ub, q[cur] + 1, q[cur ^ 1], 1,
+                             use_weights, scatter_first, scratch, stream, ev[0], ev[1], hits, sort_space, k == 0,
+                             ev[2], ev[3], &split, &fc, &sc);
+            if (rc) return rc;
+            CHR_HIP_CHECK(hipMemcpyAsync(ring + 2 * (k % 32), ctl + 2 * (size_t)k, 8, hipMemcpyDeviceToHost, stream));
+            CHR_HIP_CHECK(hipEventRecord(ev[4], stream));
+            fc.cur ^= 1;
+            cur ^= 1;
+            scatter_first = 0;
+            if (k >= 1) {   // slot k - 1 finished before slot k started: is there a slot k + 1?
+                CHR_HIP_CHECK(hipEventSynchronize(events[5 * (size_t)(k - 1) + 4]));
+                const uint32_t m = ring[2 * ((k - 1) % 32)], nk = ring[2 * ((k - 1) % 32) + 1];
+                if (m != STEP_ONE) stop = true;   // the tail ran or the queue emptied: slot k is idle
+                else n_ub = nk;                   // later queues are no longer
+            }
+            k++;
+        }
+        CHR_HIP_CHECK(hipStreamSynchronize(stream));
+        st.host_syncs = 1;
+        std::vector<uint32_t> h(2 * (size_t)k);
+        CHR_HIP_CHECK(hipMemcpy(h.data(), ctl, 8 * (size_t)k, hipMemcpyDeviceToHost));
+        uint32_t last_mode = STEP_IDLE;
+        for (int j = 0; j < k; ++j) {
+            const uint32_t m = h[2 * j], nj = h[2 * j + 1];
+            float ms = 0.0f;
+            CHR_HIP_CHECK(hipEventElapsedTime(&ms, events[5 * (size_t)j], events[5 * (size_t)j + 1]));
+            kernel_ms += ms;
+            if (m == STEP_IDLE) continue;
+            last_mode = m;
+            st.launches++;
+            st.steps_run++;
+            if (m == STEP_ONE) {
+                CHR_HIP_CHECK(hipEventElapsedTime(&ms, events[5 * (size_t)j + 2], events[5 * (size_t)j + 3]));
+                trace_ms += ms;
+                if (st.trace_ms_n < CHR_TRACE_MS_MAX) {
+                    st.trace_launch_rays[st.trace_ms_n] = nj;
+                    st.trace_launch_ms[st.trace_ms_n++] = ms;
+                }
+                st.trace_launches++;
+                st.trace_rays += nj;
+                step++;
+            } else {
+                CHR_HIP_CHECK(hipEventElapsedTime(&ms, events[5 * (size_t)j], events[5 * (size_t)j + 1]));
+                st.tail_ms += ms;
+                st.tail_photons += nj;
+                step = max_steps;
+            }
+        }
+        (void)last_mode;
+        n = 0;   // as the host loop: it leaves early only on an empty queue
+    }
+    while (!device_steps && step < max_steps) {
         const int nsteps = (n < (int64_t)ntpb * 16 * 8 || use_weights) ? max_steps - step : 1;   // photon.py:261-264
         const int64_t n_prev = n;
+        n_launch = n;
         tail_step = nsteps > 1;
         if (tail_step) st.tail_photons += (uint32_t)n;
         size_t nchunks = 0;
@@ -3236,6 +3607,7 @@ extern "C" int chr_propagate(const chr_geometry *g, const chr_photons *ph, uint3
             // read the survivor count (photon.py:284) and reset the other header
             CHR_HIP_CHECK(hipMemcpyAsync(pinned, q[cur], 4, hipMemcpyDeviceToHost, stream));
             CHR_HIP_CHECK(hipStreamSynchronize(stream));
+            st.host_syncs++;
             if ((rc = collect(nchunks))) return rc;
             nchunks = 0;
             n = (int64_t)pinned[0] - 1;
@@ -3256,6 +3628,7 @@ extern "C" int chr_propagate(const chr_geometry *g, const chr_photons *ph, uint3
         }
         if (nchunks) {   // last step (no survivor read-back): drain before collecting
             CHR_HIP_CHECK(hipStreamSynchronize(stream));
+            st.host_syncs++;
             if ((rc = collect(nchunks))) return rc;
         }
     }
@@ -3397,6 +3770,53 @@ extern "C" int chr_distance_to_mesh(const chr_geometry *g, uint32_t n, const flo
                        (uint32_t *)nullptr);
     CHR_HIP_CHECK(hipGetLastError());
     return CHR_OK;
+}
+
+// Device profile counters (profile.h; profiler.py:217-262 device_fetch / device_reset)
+extern "C" int chr_device_profile_enabled(void) {
+#ifdef CHR_DEVICE_PROFILE
+    return 1;
+#else
+    return 0;
+#endif
+}
+
+extern "C" int chr_device_profile_reset(void *stream) {
+#ifdef CHR_DEVICE_PROFILE
+    void *calls = nullptr, *cycles = nullptr;
+    CHR_HIP_CHECK(hipGetSymbolAddress(&calls, HIP_SYMBOL(chr::chr_prof_calls)));
+    CHR_HIP_CHECK(hipGetSymbolAddress(&cycles, HIP_SYMBOL(chr::chr_prof_cycles)));
+    CHR_HIP_CHECK(hipMemsetAsync(calls, 0, sizeof(unsigned long long) * CHR_PROF_COUNT, (hipStream_t)stream));
+    CHR_HIP_CHECK(hipMemsetAsync(cycles, 0, sizeof(unsigned long long) * CHR_PROF_COUNT, (hipStream_t)stream));
+    return CHR_OK;
+#else
+    (void)stream;
+    return chr::fail(CHR_ERR_INVALID, "device profiling symbols not found: load libchroma_amd_prof.so "
+                                      "(built with -DCHR_DEVICE_PROFILE=1; CHROMA_DEVICE_PROFILE=1)");
+#endif
+}
+
+extern "C" int chr_device_profile_fetch(uint64_t *h_calls, uint64_t *h_cycles, int32_t n, uint32_t *clock_khz) {
+#ifdef CHR_DEVICE_PROFILE
+    if (!h_calls || !h_cycles || n < 0 || n > CHR_PROF_COUNT)
+        return chr::fail(CHR_ERR_INVALID, "device_profile_fetch: bad arguments");
+    CHR_HIP_CHECK(hipDeviceSynchronize());
+    unsigned long long c[CHR_PROF_COUNT], y[CHR_PROF_COUNT];
+    CHR_HIP_CHECK(hipMemcpyFromSymbol(c, HIP_SYMBOL(chr::chr_prof_calls), sizeof(c)));
+    CHR_HIP_CHECK(hipMemcpyFromSymbol(y, HIP_SYMBOL(chr::chr_prof_cycles), sizeof(y)));
+    for (int i = 0; i < n; ++i) { h_calls[i] = c[i]; h_cycles[i] = y[i]; }
+    if (clock_khz) {
+        int dev = 0, khz = 0;
+        CHR_HIP_CHECK(hipGetDevice(&dev));
+        CHR_HIP_CHECK(hipDeviceGetAttribute(&khz, hipDeviceAttributeClockRate, dev));
+        *clock_khz = (uint32_t)khz;
+    }
+    return CHR_OK;
+#else
+    (void)h_calls; (void)h_cycles; (void)n; (void)clock_khz;
+    return chr::fail(CHR_ERR_INVALID, "device profiling symbols not found: load libchroma_amd_prof.so "
+                                      "(built with -DCHR_DEVICE_PROFILE=1; CHROMA_DEVICE_PROFILE=1)");
+#endif
 }
 
 // The renderer (render.cu, hybrid_render.cu, transform.cu): same translation

@@ -226,7 +226,7 @@ __global__ __launch_bounds__(BLOCK) void update_xyz_lookup_kernel(const DevGeom 
     const int id = kid + offset;
     if (kid >= nthreads || id >= total_threads) return;
     const DevGeom &g = *gdev;
-    PropagateArgs ra;
+    PropagateArgs ra{};
     ra.rng = rng_states;
     ra.nslots = nslots;
     chr_xorwow rng;
@@ -281,7 +281,7 @@ __global__ __launch_bounds__(BLOCK) void update_xyz_image_kernel(const DevGeom *
     const int id = blockIdx.x * BLOCK + threadIdx.x;
     if (id >= nthreads) return;
     const DevGeom &g = *gdev;
-    PropagateArgs ra;
+    PropagateArgs ra{};
     ra.rng = rng_states;
     ra.nslots = nslots;
     chr_xorwow rng;

@@ -186,6 +186,10 @@ typedef struct chr_propagate_stats {
     uint64_t tail_long_ticks;     /*   100 MHz ticks from load to write-back, */
     uint64_t tail_long_walk_ticks;        /*   ticks in the BVH walk (wave-adaptive tail kernel), */
     uint64_t tail_long_walk_iterations;   /*   and dependent walk iterations */
+    uint32_t host_syncs;          /* waits that drain the stream (the host reads the survivor count): one
+                                     per host step when host-driven, 1 when the steps are device-driven */
+    uint32_t reserved3;
+    uint32_t trace_launch_rays[32];   /* queued photons of each trace_kernel launch, in order */
 } chr_propagate_stats;
 #define CHR_TRACE_MS_MAX 32
 
@@ -420,6 +424,43 @@ int chr_selftest_rotate(uint32_t n, const float *d_a, const float *d_phi, float 
 int chr_selftest_sample_cdf(uint32_t n, const uint32_t *d_states, uint32_t nslots, int32_t ncdf,
                             const float *d_cdf_x, const float *d_cdf_y, float x0, float delta,
                             int32_t uniform_grid, float *d_out, void *stream);
+
+/* ------------------------------------------------------------- device profile
+ * replaces: the CHROMA_DEVICE_PROFILE build (chroma/cuda/profile.h:9-37) and
+ * chroma.gpu.profiler.device_fetch / device_reset / device_report
+ * (chroma/gpu/profiler.py:207-288).  Region counters (calls, cycles) of the split
+ * step kernels, compiled only into libchroma_amd_prof.so (-DCHR_DEVICE_PROFILE=1;
+ * chroma.gpu._native loads it when $CHROMA_DEVICE_PROFILE is set).  cycles are
+ * lane-cycles of the shader clock (s_memtime): per work-item, the wave's time spent in
+ * the region while that work-item took part, summed over work-items -- the reference's
+ * per-thread clock64 sums.  Regions 0-5 keep the reference's ids. */
+enum {
+    CHR_PROF_INTERSECT_MESH = 0,      /* trace_kernel walks: calls = walks, cycles = node + triangle steps */
+    CHR_PROF_INTERSECT_NODE = 1,      /* trace_kernel node steps (8-child slab test + stack) */
+    CHR_PROF_INTERSECT_TRIANGLE = 2,  /* trace_kernel triangle steps (incl. the reference leaf-box check) */
+    CHR_PROF_INTERSECT_BOX = 3,       /* child boxes slab-tested (calls only: part of the node steps) */
+    CHR_PROF_FILL_MATERIAL = 4,       /* shade_kernel finish_fill (normal, material, surface of the hit) */
+    CHR_PROF_FILL_ANALYTIC = 5,       /* kept for the reference's id (no analytic solids here: 0) */
+    CHR_PROF_TRACE_REFILL = 6,        /* trace_kernel: publishing results + fetching the next rays */
+    CHR_PROF_TRACE_IDLE = 7,          /* trace_kernel: lanes without work while their wave steps */
+    CHR_PROF_SHADE_PHYSICS = 8,       /* shade_kernel propagate_to_boundary / _at_surface / _at_boundary */
+    CHR_PROF_SHADE_OTHER = 9,         /* shade_kernel: state fetch wait, write-back, masks */
+    CHR_PROF_TAIL_WALK = 10,          /* propagate_tail_kernel: the wave-spread walks (calls = walks) */
+    CHR_PROF_TAIL_PHYSICS = 11,       /* propagate_tail_kernel: finish_fill + physics of the steps */
+    CHR_PROF_TAIL_OTHER = 12,         /* propagate_tail_kernel: photon load / write-back / waiting */
+    CHR_PROF_TRACE_KERNEL = 13,       /* whole trace_kernel (calls = work-items) */
+    CHR_PROF_SHADE_KERNEL = 14,       /* whole shade_kernel */
+    CHR_PROF_TAIL_KERNEL = 15,        /* whole propagate_tail_kernel */
+    CHR_PROF_NREGIONS = 16,
+    CHR_PROF_COUNT = 64               /* counter array length (profile.h:16) */
+};
+/* 1 when this library was built with the device profile, else 0 */
+int chr_device_profile_enabled(void);
+/* zero the counters (replaces the chroma_prof_reset kernel); CHR_ERR_INVALID without the profile build */
+int chr_device_profile_reset(void *stream);
+/* copy n <= CHR_PROF_COUNT counters to host arrays and the shader clock (kHz) the
+ * cycles convert with (hipDeviceAttributeClockRate); synchronises the device */
+int chr_device_profile_fetch(uint64_t *h_calls, uint64_t *h_cycles, int32_t n, uint32_t *clock_khz);
 
 /* ------------------------------------------------------------- misc */
 const char *chr_last_error(void);
