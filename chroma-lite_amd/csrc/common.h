@@ -31,3 +31,10 @@ inline int fail(int code, const char *fmt, ...) {
             return chr::fail(CHR_ERR_HIP, "%s failed at %s:%d: %s", #expr, __FILE__, __LINE__, \
                              hipGetErrorString(_e));                                        \
     } while (0)
+
+// propagate a nonzero chr status
+#define CHR_TRY(expr)                   \
+    do {                                \
+        const int _rc = (expr);         \
+        if (_rc != CHR_OK) return _rc;  \
+    } while (0)

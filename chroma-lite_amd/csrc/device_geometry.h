@@ -11,7 +11,8 @@
 //    passes a pointer (a by-value kernel argument whose address escapes gets
 //    copied into every work-item's scratch);
 //  * BVH nodes stay the reference's 16-byte quantised uint4 (the exact-order
-//    traversal variant walks them); the default traversal walks an 8-wide SAH
+//    traversal variant walks them; resident in HBM only once a call needs them,
+//    chr::geometry_ref_nodes); the default traversal walks an 8-wide SAH
 //    BVH built over the same leaf boxes with the reference DFS rank as the
 //    nearest-hit tie-break (wide_bvh.h) -- same answers, far fewer nodes;
 //  * triangles are de-indexed into 48-byte records of three float4:
@@ -24,6 +25,7 @@
 //    by one element, see chr_geometry_desc), addressed by 32-bit offsets held
 //    in small DevMaterial / DevSurface records.
 #pragma once
+#include <vector>
 
 #include <cstdint>
 
@@ -81,4 +83,13 @@ struct chr_geometry {
     int nallocs;
     const uint4 *wnodes_alt;   // the other node layout (only with CHR_NODE_LAYOUT_AB set at creation; A/B tooling)
     uint32_t wstride_alt;
+    // The reference BVH nodes (16 B each) are walked only by the exact-order
+    // variant, the no-wide-BVH fallback and distance_to_mesh's exact form.  With a
+    // wide BVH only the root stays in HBM (the renderer's world box) and the
+    // rest waits here until chr_geometry_ref_nodes() uploads it (once).
+    std::vector<uint4> *h_ref_nodes;
 };
+namespace chr {
+// make every reference node resident in HBM (no-op when it is); CHR_OK or an error
+int geometry_ref_nodes(const chr_geometry *g);
+}

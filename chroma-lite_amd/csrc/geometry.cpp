@@ -65,7 +65,22 @@ extern "C" int chr_geometry_destroy(chr_geometry *g) {
     hipSetDevice(g->device);
     for (int i = 0; i < g->nallocs; ++i) hipFree(g->allocs[i]);
     hipSetDevice(prev);
+    delete g->h_ref_nodes;
     delete g;
+    return CHR_OK;
+}
+
+int chr::geometry_ref_nodes(const chr_geometry *cg) {
+    chr_geometry *g = const_cast<chr_geometry *>(cg);
+    if (!g->h_ref_nodes) return CHR_OK;
+    void *p = nullptr;
+    int rc = dev_upload(g, g->h_ref_nodes->data(), g->h_ref_nodes->size() * sizeof(uint4), &p);
+    if (rc) return rc;
+    g->dev.nodes = (const uint4 *)p;
+    const hipError_t e = hipMemcpy(g->d_dev, &g->dev, sizeof(g->dev), hipMemcpyHostToDevice);
+    if (e != hipSuccess) return chr::fail(CHR_ERR_HIP, "hipMemcpy H2D failed: %s", hipGetErrorString(e));
+    delete g->h_ref_nodes;
+    g->h_ref_nodes = nullptr;
     return CHR_OK;
 }
 
@@ -117,9 +132,6 @@ extern "C" int chr_geometry_create(const chr_geometry_desc *d, chr_geometry **ou
         dg.t_n = d->time_n; dg.t_start = d->time_start; dg.t_step = d->time_step;
 
         void *p;
-        if ((rc = dev_upload(g, d->h_nodes, (size_t)d->nnodes * 16, &p))) throw rc;
-        dg.nodes = (const uint4 *)p;
-
         // de-indexed triangle records: v0, e1 = v1-v0, e2 = v2-v0, e3 = v2-v1
         std::vector<float> tri((size_t)d->ntriangles * 12);
         const float *v = d->h_vertices;
@@ -169,6 +181,16 @@ extern "C" int chr_geometry_create(const chr_geometry_desc *d, chr_geometry **ou
                 dg.wrank_id = (const uint32_t *)p;
             }
         }
+
+        // reference BVH nodes: all resident only without a wide BVH (or with
+        // CHR_REF_NODES_RESIDENT); otherwise the root, the rest on first use
+        if (dg.nwnodes == 0 || std::getenv("CHR_REF_NODES_RESIDENT")) {
+            if ((rc = dev_upload(g, d->h_nodes, (size_t)d->nnodes * 16, &p))) throw rc;
+        } else {
+            g->h_ref_nodes = new std::vector<uint4>((const uint4 *)d->h_nodes, (const uint4 *)d->h_nodes + d->nnodes);
+            if ((rc = dev_upload(g, d->h_nodes, 16, &p))) throw rc;
+        }
+        dg.nodes = (const uint4 *)p;
 
         if ((rc = dev_upload(g, d->h_material_codes, (size_t)d->ntriangles * 4, &p))) throw rc;
         dg.material_codes = (const uint32_t *)p;

@@ -3033,6 +3033,12 @@ static bool wide_queue_ok(const chr_geometry *g) { return g->dev.nwtri < (1u << 
 
 // one launch per chunk (the reference's launch structure: slot counts that are
 // not a multiple of 64, or CHR_STEP_LAUNCH=0)
+// whether this call's kernels walk the reference BVH (its nodes must be resident)
+static bool walks_reference_bvh(const chr_geometry *g) {
+    const char *e = getenv("CHR_PROPAGATE_VARIANT");
+    return g->dev.nwnodes == 0 || (e && atoi(e) == kExactVariant);
+}
+
 static propagate_fn select_variant(const chr_geometry *g) {
     const char *e = getenv("CHR_PROPAGATE_VARIANT");
     int v = e ? atoi(e) : 0;
@@ -3338,6 +3344,7 @@ extern "C" int chr_propagate_chunk(const chr_geometry *g, const chr_photons *ph,
     if (nthreads <= 0) return CHR_OK;
     if ((uint32_t)nthreads > rng_nslots)
         return chr::fail(CHR_ERR_INVALID, "chr_propagate_chunk: %d threads but only %u rng states", nthreads, rng_nslots);
+    if (walks_reference_bvh(g)) CHR_TRY(chr::geometry_ref_nodes(g));
     return launch_chunk(g, ph, d_rng_states, rng_nslots, first_photon, nthreads, d_input_queue, d_output_queue,
                         max_steps, use_weights, scatter_first, d_scratch, (hipStream_t)stream);
 }
@@ -3426,6 +3433,7 @@ extern "C" int chr_propagate(const chr_geometry *g, const chr_photons *ph, uint3
     if (ncopies == 0 || (uint64_t)true_nphotons * ncopies != nphotons)
         return chr::fail(CHR_ERR_INVALID, "chr_propagate: nphotons != true_nphotons*ncopies");
     if (nphotons > 0x7FFFFFFFu) return chr::fail(CHR_ERR_INVALID, "chr_propagate: more than 2^31-1 photons");
+    if (walks_reference_bvh(g)) CHR_TRY(chr::geometry_ref_nodes(g));
     hipStream_t stream = (hipStream_t)vstream;
     chr_propagate_stats st{};
     if (nphotons == 0) { if (stats) *stats = st; return CHR_OK; }
@@ -3763,8 +3771,8 @@ extern "C" int chr_distance_to_mesh(const chr_geometry *g, uint32_t n, const flo
                                     float *d_distance, void *stream) {
     if (!g || !d_origin || !d_direction || !d_distance) return chr::fail(CHR_ERR_INVALID, "distance_to_mesh: null argument");
     if (n == 0) return CHR_OK;
-    const char *e = getenv("CHR_PROPAGATE_VARIANT");
-    const bool wide = g->dev.nwnodes != 0 && !(e && atoi(e) == 1);
+    const bool wide = !walks_reference_bvh(g);
+    if (!wide) CHR_TRY(chr::geometry_ref_nodes(g));
     hipLaunchKernelGGL(wide ? distance_kernel<true> : distance_kernel<false>, dim3(grid_for(n)), dim3(BLOCK), 0,
                        (hipStream_t)stream, (const DevGeom *)g->d_dev, n, d_origin, d_direction, d_distance,
                        (uint32_t *)nullptr);
