@@ -49,8 +49,9 @@ DEVICE_REGION_NAMES = {
     13: 'trace_kernel',
     14: 'shade_kernel',
     15: 'tail_kernel',
+    16: 'trace_drain',
 }
-NREGIONS = 16        # CHR_PROF_NREGIONS
+NREGIONS = 17        # CHR_PROF_NREGIONS
 COUNTERS = 64        # CHR_PROF_COUNT (profile.h:16)
 
 

@@ -1871,15 +1871,34 @@ __device__ __forceinline__ int nth_bit(unsigned long long m, int r) {
     return __ffsll((long long)m) - 1;
 }
 
+// LDS word arrays of walk_segment: contiguous (the tail kernel's per-wave
+// stacks), or a wave's rows of trace_kernel's lane-strided LDS (row r = the 64
+// words of the wave's lanes at r * BLOCK), reused when the wave drains.
+struct LdsFlat {
+    CHR_LDS uint32_t *p;
+    __device__ __forceinline__ CHR_LDS uint32_t &operator[](int i) const { return p[i]; }
+};
+struct LdsRows {
+    CHR_LDS uint32_t *p;   // the wave's word 0 (row 0, its first lane)
+    int off;
+    __device__ __forceinline__ CHR_LDS uint32_t &operator[](int i) const {
+        return p[((i + off) >> 6) * BLOCK + ((i + off) & 63)];
+    }
+};
+
 // All 64 lanes call this (converged).  act: the segment has a ray (segment-
 // uniform).  Returns the nearest triangle (-1: none) and its distance in
 // every lane of the segment.  One dependent global fetch per iteration: the
 // triangles of the leaves found in iteration i are fetched together with the
 // nodes of iteration i + 1 (their best then culls one iteration later, still
-// with a best that never drops below the final one).
-__device__ int walk_segment(const DevGeom &g, bool act, V3 o, V3 d, uint32_t last, int Gs,
-                            CHR_LDS uint32_t *stk, int cap, CHR_LDS uint32_t *tlist, uint32_t &overflow,
-                            float &min_distance, uint32_t &iters) {
+// with a best that never drops below the final one).  best / best_rank /
+// best_id seed the walk with a hit already found (a trace_kernel walk handed
+// over mid-way): culling with it is conservative, and the result is the min
+// over the seed and every triangle this walk tests.
+template <class M>
+__device__ int walk_segment(const DevGeom &g, bool act, V3 o, V3 d, uint32_t last, int Gs, M stk, int cap, M tlist,
+                            uint32_t &overflow, float &min_distance, uint32_t &iters,
+                            float best = __builtin_inff(), uint32_t best_rank = 0xFFFFFFFFu, int best_id = -1) {
     constexpr uint32_t INVALID = 0xFFFFFFFFu;
     constexpr unsigned long long NONE = ~0ull;
     const uint32_t lane = __lane_id();
@@ -1891,9 +1910,6 @@ __device__ int walk_segment(const DevGeom &g, bool act, V3 o, V3 d, uint32_t las
     const V3 noid = v3(-o.x / d.x, -o.y / d.y, -o.z / d.z);
     const V3 inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
     const RaySlab r = make_slab(noid, inv);
-    float best = __builtin_inff();
-    uint32_t best_rank = 0xFFFFFFFFu;
-    int best_id = -1;
     uint32_t cur = (act && L < 8u) ? 0u : INVALID;   // cursor 0 starts at the root
     float cur_t = 0.0f;
     int sp = 0;
@@ -2180,8 +2196,8 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_tail_kernel(const DevGe
             const uint32_t seg0 = lane & ~(uint32_t)(Gs - 1);
             float sd;
             uint32_t it;
-            const int st = walk_segment(g, act, o, dd, last, Gs, wstack + seg0 / 8 * TAIL_STACK * 2,
-                                        TAIL_STACK * Gs / 8, wtris + 4 * seg0, overflow, sd, it);
+            const int st = walk_segment(g, act, o, dd, last, Gs, LdsFlat{wstack + seg0 / 8 * TAIL_STACK * 2},
+                                        TAIL_STACK * Gs / 8, LdsFlat{wtris + 4 * seg0}, overflow, sd, it);
             const int mine = __popcll(wm & ((1ull << (lane & ~7u)) - 1ull)) * Gs;   // my group's segment
             tri = __shfl(st, mine);
             dist = __shfl(sd, mine);
@@ -2295,6 +2311,7 @@ struct TraceArgs {
     // (the input queue's count header) and the launch runs only if *mode is STEP_ONE
     const uint32_t *dev_n;
     const uint32_t *mode;
+    uint32_t drain_max;          // a wave drains its last <= drain_max walks whole-wave (0: never; at most 8)
 };
 
 // Enrol queue position p for the next trace launch if its walk is flat
@@ -2329,6 +2346,8 @@ __global__ __launch_bounds__(BLOCK) void classify_kernel(const float *pos, const
 template <bool COUNT, int F, int SL, int MINW, int R>
 __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__restrict__ gdev, TraceArgs a) {
     __shared__ uint32_t lds[(2 * SL + LEAFQ) * BLOCK];
+    // a draining wave's walk_segment stacks (8 x TAIL_STACK entries) + triangle lists in its LDS rows
+    static_assert((2 * SL + LEAFQ) * 64 >= 8 * TAIL_STACK * 2 + 2 * TAIL_TRI, "drain needs the wave's LDS rows");
     WStack st;
     // Deep stack entries live in a lane-strided HBM column sized for this
     // persistent grid, not in private scratch: a kernel with a private segment
@@ -2359,11 +2378,11 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
     float best = 0.0f;
     uint32_t best_rank = 0, last = 0, node = 0;
     int best_id = -1, sp = 0;
-    bool walk_done = true;
+    bool walk_done = true, drain = false;
     uint32_t qh = 0, qt = 0, pcur = 0, pleft = 0;
     constexpr uint32_t INVALID = 0xFFFFFFFFu;
-    enum { P_NODE, P_TRI, P_REFILL, P_IDLE, P_BOX = 3 };   // regions (calls: P_REFILL = walks, P_BOX = boxes)
-    Prof<4> pf;
+    enum { P_NODE, P_TRI, P_REFILL, P_IDLE, P_DRAIN, P_BOX = 3 };   // regions (calls: P_REFILL = walks, P_BOX = boxes)
+    Prof<5> pf;
     pf.start(P_REFILL);
     while (true) {
         pf.tick(P_REFILL);   // the last step goes to the region each work-item was in
@@ -2439,6 +2458,22 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
                         if constexpr (COUNT) cnt.walks++;
                     }
                 }
+            }
+        }
+        if constexpr (!COUNT) {
+            // Drain: once the ray counter is exhausted and at most 8 ordinary walks
+            // are left in the wave, the whole wave finishes them together
+            // (walk_segment: 8..64 lanes per walk, Gs/8 cursors each, a dependent
+            // step's triangles in parallel) instead of one lane each.  The last
+            // walks of a launch are its longest (~200 node + triangle steps at
+            // ~2 us per dependent step on the 29k detector: the 0.4 ms floor of
+            // every small launch).  Each restarts from the root seeded with its
+            // best so far (conservative culling, the same nearest hit); the
+            // lanes' stacks are abandoned and their LDS rows reused.
+            if (exhausted && __ballot(has_ray) != 0 && (uint32_t)__popcll(__ballot(has_ray)) <= a.drain_max &&
+                __ballot(has_ray && flat_f >= 0) == 0) {
+                drain = true;   // after the loop, where the walk state below is no longer live
+                break;
             }
         }
         pf.tick(P_IDLE);
@@ -2520,6 +2555,40 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
             best_id = (int)id;
         }
     }
+    if constexpr (!COUNT) {
+        if (drain) {
+            pf.tick(P_DRAIN);
+            const unsigned long long rm = __ballot(has_ray);
+            const int w = __popcll(rm);
+            const int Gs = w == 1 ? 64 : (w == 2 ? 32 : (w <= 4 ? 16 : 8));
+            const int si = (int)lane / Gs;
+            unsigned long long m = rm;
+            for (int i = 0; i < si && m != 0; ++i) m &= m - 1;
+            const bool act = m != 0;
+            const int src = act ? __ffsll((long long)m) - 1 : (int)lane;
+            const V3 so = v3(__shfl(o.x, src), __shfl(o.y, src), __shfl(o.z, src));
+            const V3 sdir = v3(__shfl(d.x, src), __shfl(d.y, src), __shfl(d.z, src));
+            const uint32_t slast = (uint32_t)__shfl((int)last, src);
+            const float sbest = __shfl(best, src);
+            const uint32_t srank = (uint32_t)__shfl((int)best_rank, src);
+            const int sid = __shfl(best_id, src);
+            const int seg0 = (int)lane & ~(Gs - 1);
+            CHR_LDS uint32_t *wbase = (CHR_LDS uint32_t *)(lds + (threadIdx.x & ~63u));
+            float sdist;
+            uint32_t sit;
+            const int tri = walk_segment(g, act, so, sdir, slast, Gs, LdsRows{wbase, seg0 / 8 * TAIL_STACK * 2},
+                                         TAIL_STACK * Gs / 8, LdsRows{wbase, 8 * TAIL_STACK * 2 + 4 * seg0}, overflow,
+                                         sdist, sit, sbest, srank, sid);
+            const int mine = (__popcll(rm & ((1ull << lane) - 1ull)) * Gs) & 63;   // my segment's first lane
+            const int rt = __shfl(tri, mine);
+            const float rd = __shfl(sdist, mine);
+            if (has_ray) {                                        // publish (mesh.h:123-125)
+                a.hits[q] = make_int2(rt, __float_as_int(rt == -1 ? -1.0f : rd));
+                pf.call(P_DRAIN);
+            }
+            pf.tick(P_IDLE);
+        }
+    }
 #ifdef CHR_DEVICE_PROFILE
     pf.tick(P_IDLE);
     prof_add(CHR_PROF_INTERSECT_MESH, pf.calls[P_REFILL], (unsigned long long)pf.cyc[P_NODE] + pf.cyc[P_TRI]);
@@ -2528,6 +2597,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
     prof_add(CHR_PROF_INTERSECT_BOX, pf.calls[P_BOX], 0ull);
     prof_add(CHR_PROF_TRACE_REFILL, 0ull, pf.cyc[P_REFILL]);
     prof_add(CHR_PROF_TRACE_IDLE, 0ull, pf.cyc[P_IDLE]);
+    prof_add(CHR_PROF_TRACE_DRAIN, pf.calls[P_DRAIN], pf.cyc[P_DRAIN]);
     prof_add(CHR_PROF_TRACE_KERNEL, 1ull, pf.total());
 #endif
     if (overflow) atomicAdd(a.counters, overflow);
@@ -3029,6 +3099,12 @@ static bool tail_group_walk() {        // CHR_TAIL=group: the fixed 8-lane group
     const char *e = getenv("CHR_TAIL");
     return e && std::strcmp(e, "group") == 0;
 }
+// CHR_TRACE_DRAIN=k: trace_kernel waves drain their last <= k walks whole-wave (default 8, 0 = off; A/B)
+static uint32_t trace_drain_max() {
+    const char *e = getenv("CHR_TRACE_DRAIN");
+    const int k = e ? atoi(e) : 8;
+    return (uint32_t)(k < 0 ? 0 : (k > 8 ? 8 : k));
+}
 static bool wide_queue_ok(const chr_geometry *g) { return g->dev.nwtri < (1u << 30); }   // 30-bit leaf queue entries
 
 // one launch per chunk (the reference's launch structure: slot counts that are
@@ -3278,6 +3354,7 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
         ta.flat_q = fc->flat_q; ta.flat_count = count_cur; ta.flat_best = fc->flat_best; ta.diag = fc->ctl + 3;
         ta.dev_n = dev_n;
         ta.mode = mode;
+        ta.drain_max = trace_drain_max();
         a.flat_best = fc->flat_best;
         a.zero_word = count_next;   // cleared by the shade pass, filled by this step's scatter
         if (fc->enrol_next)

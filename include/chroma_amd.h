@@ -451,7 +451,8 @@ enum {
     CHR_PROF_TRACE_KERNEL = 13,       /* whole trace_kernel (calls = work-items) */
     CHR_PROF_SHADE_KERNEL = 14,       /* whole shade_kernel */
     CHR_PROF_TAIL_KERNEL = 15,        /* whole propagate_tail_kernel */
-    CHR_PROF_NREGIONS = 16,
+    CHR_PROF_TRACE_DRAIN = 16,        /* trace_kernel: a wave's last <= 8 walks, whole-wave (calls = walks) */
+    CHR_PROF_NREGIONS = 17,
     CHR_PROF_COUNT = 64               /* counter array length (profile.h:16) */
 };
 /* 1 when this library was built with the device profile, else 0 */

@@ -53,7 +53,9 @@ def test_device_profile_regions(tmp_path, small_detector, small_packed):
     assert c['intersect_box'] >= c['intersect_node']
     assert y['intersect_mesh'] == y['intersect_node'] + y['intersect_triangle']
     assert y['trace_kernel'] == (y['intersect_node'] + y['intersect_triangle'] + y['trace_refill']
-                                 + y['trace_idle'])
+                                 + y['trace_idle'] + y['trace_drain'])
+    # every walk is either finished by its lane or handed to its draining wave
+    assert c['trace_drain'] <= c['intersect_mesh']
     assert 0 < c['shade_physics'] <= c['fill_material']
     assert y['shade_kernel'] == y['fill_material'] + y['shade_physics'] + y['shade_other']
     assert c['tail_walk'] > 0 and c['tail_physics'] == c['tail_walk']
