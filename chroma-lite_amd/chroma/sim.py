@@ -23,6 +23,22 @@ def pick_seed():
     return int(time.time()) ^ (os.getpid() << 16) & 2 ** 32 - 1
 
 
+def agree_seed(seed, group=None):
+    """Rank 0's seed on every rank of `group` (a sharded job draws one seed).  The
+    value travels as a tensor on the backend's device: the rank's own GPU for
+    RCCL (bound by the caller before this collective), the CPU for gloo."""
+    import torch
+    import torch.distributed as dist
+    from chroma.gpu import shard
+    if shard.dist_info(group)[1] <= 1:
+        return seed
+    on_gpu = torch.cuda.is_available() and dist.get_backend(group) != 'gloo'
+    box = torch.tensor([seed], dtype=torch.int64,
+                       device=torch.device('cuda', shard.local_device()) if on_gpu else 'cpu')
+    dist.broadcast(box, src=0, group=group)
+    return int(box.item())
+
+
 class Simulation(object):
     def __init__(self, detector, seed=None, cuda_device=None, photon_tracking=False, nthreads_per_block=512,
                  max_blocks=1024):
@@ -180,13 +196,7 @@ class ShardedSimulation(Simulation):
         if torch.cuda.is_available():
             torch.cuda.set_device(shard.local_device())
         if seed is None:
-            seed = pick_seed()
-            if self.world > 1:      # one seed for the job, as a tensor on the backend's device
-                on_gpu = torch.cuda.is_available() and dist.get_backend(group) != 'gloo'
-                box = torch.tensor([seed], dtype=torch.int64,
-                                   device=torch.device('cuda', shard.local_device()) if on_gpu else 'cpu')
-                dist.broadcast(box, src=0, group=group)
-                seed = int(box.item())
+            seed = agree_seed(pick_seed(), group)
         Simulation.__init__(self, detector, seed=seed, cuda_device=shard.local_device(),
                             nthreads_per_block=nthreads_per_block, max_blocks=max_blocks)
         nslots = self.nthreads_per_block * self.max_blocks

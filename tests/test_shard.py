@@ -134,3 +134,16 @@ def test_shard_range_partitions():
             assert r[0][0] == 0 and r[-1][1] == n
             assert all(r[k][1] == r[k + 1][0] for k in range(world - 1))
             assert max(b - a for a, b in r) - min(b - a for a, b in r) <= 1
+
+
+def seed_agreement(rank, world):
+    from chroma.sim import agree_seed, pick_seed
+    mine = pick_seed() + 7919 * rank          # ranks draw different seeds
+    return np.array([mine, agree_seed(mine)], dtype=np.int64)
+
+
+def test_seed_none_agrees_across_ranks(tmp_path):
+    """ShardedSimulation(seed=None): rank 0's seed reaches every rank (the
+    seed collective of the seed=None path)."""
+    r0, r1 = _run('seed_agreement', tmp_path)
+    assert r0[1] == r0[0] and r1[1] == r0[0] and r1[0] != r0[0]
