@@ -9,6 +9,15 @@ Simulation (nthreads_per_block=512, max_blocks=1024 -> 524,288 RNG slots).
 Photon inputs are resident in HBM before the timed region; each step restores
 them from a device-resident copy (D2D, inside the timed region).
 
+Steps are pipelined (default; --no-pipeline for one synchronous propagate per
+step): up to --pipeline-depth steps go to one chroma.gpu.propagate_batches
+call, which propagates them in order with the one rng_states exactly as that
+many propagate calls would (bit-identical photons and RNG states, tested in
+tests/test_gpu_batches.py) while each batch's multi-step tail -- as long as
+its longest-lived photon's serial chain -- runs on a second HIP stream under
+the next batch's first-step queueing, binning and BVH walk (which draw no
+random numbers).  detail.step_ms is then each call's time split over its steps.
+
 Multi-GPU: one process per GPU (torchrun), geometry replicated, photons
 sharded (each rank propagates its own batch: weak scaling, RNG subsequences
 disjoint per rank).  Each step ends with the hit-channel reduce: detected
@@ -147,21 +156,28 @@ def rng_first_subsequence(rank, nslots):
     return rank * nslots
 
 
-def timed_loop(step, steps, warmup, dist, sync):
+def timed_loop(run, steps, warmup, dist, sync, group=1):
     """W untimed steps, then K timed steps bracketed by barrier + sync on both
-    sides; returns (elapsed max over ranks, this rank's per-step seconds,
-    per-step results)."""
-    for _ in range(warmup):
-        step()
+    sides; run(m) performs m steps and returns their results (m > 1: one
+    pipelined call, see main).  Returns (elapsed max over ranks, this rank's
+    per-step seconds -- a group's time split evenly over its steps --, per-step
+    results)."""
+    if warmup:
+        run(warmup)
     sync()
     if dist is not None:
         dist.barrier()
     sync()
     t0 = time.perf_counter()
-    marks, results = [], []
-    for _ in range(steps):
-        results.append(step())
-        marks.append(time.perf_counter())   # propagate is synchronous: a mark per step
+    marks, results, per_step = [], [], []
+    left = steps
+    while left > 0:
+        m = min(group, left)
+        t1 = time.perf_counter()
+        results.extend(run(m))
+        t2 = time.perf_counter()   # the calls are synchronous: a mark per group
+        per_step.extend([(t2 - t1) / m] * m)
+        left -= m
     sync()
     if dist is not None:
         dist.barrier()
@@ -172,7 +188,6 @@ def timed_loop(step, steps, warmup, dist, sync):
         tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
-    per_step = [b - a for a, b in zip([t0] + marks[:-1], marks)]
     return elapsed, per_step, results
 
 
@@ -316,6 +331,10 @@ def main():
     ap.add_argument('--no-cpu-baseline', action='store_true', help='also skips the parity check')
     ap.add_argument('--no-count', action='store_true',
                     help='skip the untimed counting pass (profiling runs: keeps rocprof averages to one variant)')
+    ap.add_argument('--no-pipeline', dest='pipeline', action='store_false',
+                    help='one synchronous propagate per step (no tail / next-batch overlap)')
+    ap.add_argument('--pipeline-depth', type=int, default=32,
+                    help='steps per pipelined call (each holds its own copy of the batch in HBM)')
     ap.add_argument('--cache-dir', default=os.environ.get('CHROMA_BENCH_CACHE', '/tmp/chroma_bench_cache'))
     args = ap.parse_args()
 
@@ -356,21 +375,35 @@ def main():
     counts = ga.zeros(gdet.nchannels, np.uint32)
     reduced = {}
 
-    def step():
-        gp = gpu.GPUPhotons(pristine, copy_flags=True, copy_triangles=False, copy_weights=False)
-        gp.propagate(gdet, rng, nthreads_per_block=args.nthreads_per_block, max_blocks=args.max_blocks,
-                     max_steps=args.max_steps)
-        # hit-channel reduce: detected photons per PMT channel on each rank,
-        # SUM-reduced over ranks (RCCL for N > 1)
-        counts.fill(0)
-        _native.call('chr_channel_hit_counts', ctypes.byref(gp._desc()), 0, args.photons, 0x4,
-                     gdet.solid_id_map.gpudata, gdet.solid_id_to_channel_index_gpu.gpudata, counts.gpudata,
-                     gdet.nchannels, current_stream())
-        reduced['counts'] = shard.allreduce_channel_counts(counts.tensor)
-        reduced['gp'] = gp
-        return gp.last_stats
+    def run(m):
+        """m steps: m fresh copies of the source batch propagated with one
+        rng_states -- pipelined (gpu.propagate_batches: each batch's tail runs
+        on a second stream while the next batch starts; results identical to m
+        propagate calls) unless --no-pipeline -- then each batch's hit-channel
+        reduce."""
+        gps = [gpu.GPUPhotons(pristine, copy_flags=True, copy_triangles=False, copy_weights=False)
+               for _ in range(m)]
+        kw = dict(nthreads_per_block=args.nthreads_per_block, max_blocks=args.max_blocks, max_steps=args.max_steps)
+        if args.pipeline and m > 1:
+            sts = list(gpu.propagate_batches(gps, gdet, rng, **kw))
+        else:
+            sts = []
+            for gp in gps:
+                gp.propagate(gdet, rng, **kw)
+                sts.append(gp.last_stats)
+        for gp in gps:
+            # hit-channel reduce: detected photons per PMT channel on each rank,
+            # SUM-reduced over ranks (RCCL for N > 1)
+            counts.fill(0)
+            _native.call('chr_channel_hit_counts', ctypes.byref(gp._desc()), 0, args.photons, 0x4,
+                         gdet.solid_id_map.gpudata, gdet.solid_id_to_channel_index_gpu.gpudata, counts.gpudata,
+                         gdet.nchannels, current_stream())
+            reduced['counts'] = shard.allreduce_channel_counts(counts.tensor)
+        reduced['gp'] = gps[-1]
+        return sts
 
-    elapsed, per_step, stats = timed_loop(step, args.steps, args.warmup, dist, torch.cuda.synchronize)
+    group = max(1, min(args.steps, args.pipeline_depth)) if args.pipeline else 1
+    elapsed, per_step, stats = timed_loop(run, args.steps, args.warmup, dist, torch.cuda.synchronize, group)
     gp = reduced.pop('gp')
     detected = int(((gp.flags.get() & 4) != 0).sum())
     del gp
@@ -396,7 +429,7 @@ def main():
     if not args.no_count:
         prev = os.environ.get('CHR_PROPAGATE_VARIANT')
         os.environ['CHR_PROPAGATE_VARIANT'] = '5'
-        cst = step()
+        cst = run(1)[0]
         reduced.pop('gp', None)
         if prev is None:
             del os.environ['CHR_PROPAGATE_VARIANT']
@@ -410,7 +443,7 @@ def main():
     if _native.DEVICE_PROFILE:
         from chroma.gpu import profiler
         profiler.device_reset()
-        step()
+        run(1)
         reduced.pop('gp', None)
         torch.cuda.synchronize()
         dprof = {'regions': profiler.device_fetch(), 'clock_khz': profiler.device_fetch.clock_khz,
@@ -421,7 +454,8 @@ def main():
         props = torch.cuda.get_device_properties(local)
         free_b, total_b = torch.cuda.mem_get_info(local)
         steps = max(1, args.steps)
-        detail = {'kernel_ms_per_step': live['kernel_ms'] / steps,
+        detail = {'pipelined_steps_per_call': group,
+                  'kernel_ms_per_step': live['kernel_ms'] / steps,
                   'trace_ms_per_step': live['trace_ms'] / steps,
                   'launches_per_step': live['launches'] / steps,
                   'host_steps_per_propagate': live['host_steps'] / steps,

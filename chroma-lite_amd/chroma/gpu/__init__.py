@@ -5,7 +5,7 @@ from chroma.gpu.tools import (chunk_iterator, to_float3, to_uint3, create_cuda_c
                               RNGStates, current_stream)
 from chroma.gpu.geometry import GPUGeometry  # noqa: F401
 from chroma.gpu.detector import GPUDetector  # noqa: F401
-from chroma.gpu.photon import GPUPhotons, GPUPhotonsSlice  # noqa: F401
+from chroma.gpu.photon import GPUPhotons, GPUPhotonsSlice, propagate_batches  # noqa: F401
 from chroma.gpu.daq import GPUDaq, GPUChannels  # noqa: F401
 from chroma.gpu.pdf import GPUPDF, GPUKernelPDF  # noqa: F401
 from chroma.gpu.render import GPURays  # noqa: F401

@@ -94,6 +94,8 @@ _SIGNATURES = {
                                     c_i32, c_i32, c_i32, c_vp, c_vp]),
     'chr_propagate': (c_i32, [c_vp, ctypes.POINTER(PhotonsDesc), c_u32, c_u32, c_u32, c_vp, c_u32, c_i32, c_i32,
                               c_i32, c_i32, c_i32, ctypes.POINTER(PropagateStats), c_vp]),
+    'chr_propagate_batches': (c_i32, [c_vp, ctypes.POINTER(PhotonsDesc), c_vp, c_vp, c_vp, c_u32, c_vp, c_u32, c_i32,
+                                      c_i32, c_i32, c_i32, c_i32, ctypes.POINTER(PropagateStats), c_vp]),
     'chr_photon_hits': (c_i32, [ctypes.POINTER(PhotonsDesc), c_i32, c_i32, c_u32, c_vp, c_vp,
                                 ctypes.POINTER(PhotonsDesc), c_vp, ctypes.POINTER(c_u32), c_vp]),
     'chr_select_photons': (c_i32, [ctypes.POINTER(PhotonsDesc), c_i32, c_i32, c_u32, ctypes.POINTER(PhotonsDesc),

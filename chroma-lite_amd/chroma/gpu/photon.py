@@ -257,3 +257,37 @@ class GPUPhotonsSlice(GPUPhotons):
         self.last_hit_triangles, self.flags, self.weights, self.evidx = last_hit_triangles, flags, weights, evidx
         self.true_nphotons = len(pos)
         self.ncopies = 1
+
+
+def propagate_batches(photon_batches, gpu_geometry, rng_states, nthreads_per_block=256, max_blocks=1024,
+                      max_steps=10, use_weights=False, scatter_first=0):
+    """Propagate several GPUPhotons in order with one rng_states, as a loop of
+    ``gp.propagate(gpu_geometry, rng_states, ...)`` calls would (the event loop
+    of Simulation.simulate, reference sim.py:116-160) -- photons and RNG slot
+    states end bit-identical -- but pipelined (chr_propagate_batches): batch
+    i's multi-step tail, which is as long as its longest-lived photon's serial
+    chain, runs on a second HIP stream while batch i+1 is queued, binned and
+    walked for its first step.  Each batch's ``last_stats`` is set.  Returns the
+    list of stats."""
+    batches = list(photon_batches)
+    nslots = len(rng_states)
+    if nthreads_per_block * max_blocks > nslots:
+        raise ValueError('rng_states must have at least nthreads_per_block*max_blocks states')
+    nb = len(batches)
+    if nb == 0:
+        return []
+    descs = (_native.PhotonsDesc * nb)(*[gp._desc() for gp in batches])
+    n = np.array([gp.pos.size for gp in batches], dtype=np.uint32)
+    true_n = np.array([gp.true_nphotons for gp in batches], dtype=np.uint32)
+    copies = np.array([gp.ncopies for gp in batches], dtype=np.uint32)
+    stats = (_native.PropagateStats * nb)()
+    _native.call('chr_propagate_batches', ctypes.c_void_p(gpu_geometry.gpudata), descs, n.ctypes.data,
+                 true_n.ctypes.data, copies.ctypes.data, nb, rng_states.gpudata, nslots, nthreads_per_block,
+                 max_blocks, max_steps, int(bool(use_weights)), int(scatter_first), stats, current_stream())
+    out = []
+    for gp, st in zip(batches, stats):
+        gp.last_stats = st
+        if st.stack_overflows:
+            print('WARNING: %d BVH traversals exceeded the 1000-entry stack' % st.stack_overflows, file=sys.stderr)
+        out.append(st)
+    return out

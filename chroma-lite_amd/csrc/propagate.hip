@@ -280,6 +280,9 @@ __device__ __forceinline__ float byte_f(uint32_t lo4, uint32_t hi4, int k) {   /
     return (float)((w >> (8 * (k & 3))) & 0xFFu);
 }
 __device__ __forceinline__ float exp_scale(uint32_t e) { return __uint_as_float((e & 0xFFu) << 23); }
+typedef float F2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ F2 f2(float a, float b) { F2 v; v.x = a; v.y = b; return v; }
+__device__ __forceinline__ F2 pk_fma(F2 a, F2 b, F2 c) { return __builtin_elementwise_fma(a, b, c); }
 
 // Per-ray constants of the branch-free slab test used on wide nodes.  For an
 // axis with finite 1/d the near/far plane distances are fmaf(x, inv, noid) --
@@ -2663,9 +2666,10 @@ __global__ __launch_bounds__(BLOCK) void sort_key_kernel(const float *pos, const
 constexpr int SCAN_WORDS = 256;
 __global__ __launch_bounds__(SCAN_WORDS) void mask_block_scan_kernel(const unsigned long long *masks, uint32_t nwords,
                                                                      uint32_t *word_offsets, uint32_t *block_sums,
-                                                                     const uint32_t *dev_n, const uint32_t *mode) {
+                                                                     const uint32_t *dev_n, const uint32_t *mode,
+                                                                     uint32_t skip) {
     __shared__ uint32_t wave_tot[SCAN_WORDS / 64];
-    if (mode && *mode == STEP_IDLE) return;
+    if (mode && (*mode == STEP_IDLE || *mode == skip)) return;
     if (dev_n) nwords = (*dev_n - 1u + 63u) / 64u;
     const uint32_t w = blockIdx.x * SCAN_WORDS + threadIdx.x;
     const uint32_t c = w < nwords ? (uint32_t)__popcll(masks[w]) : 0u;
@@ -2688,9 +2692,10 @@ __global__ __launch_bounds__(SCAN_WORDS) void mask_block_scan_kernel(const unsig
 
 __global__ __launch_bounds__(1024) void scan_block_sums_kernel(uint32_t *block_sums, uint32_t nblocks,
                                                                uint32_t *out_counter, uint32_t *base,
-                                                               uint32_t *total_out, const uint32_t *mode) {
+                                                               uint32_t *total_out, const uint32_t *mode,
+                                                               uint32_t skip) {
     __shared__ uint32_t partial[1024];
-    if (mode && *mode == STEP_IDLE) return;
+    if (mode && (*mode == STEP_IDLE || *mode == skip)) return;
     const uint32_t tid = threadIdx.x;
     const uint32_t per = (nblocks + 1023) / 1024;
     const uint32_t b0 = tid * per;
@@ -2734,8 +2739,10 @@ __global__ __launch_bounds__(BLOCK) void scatter_queue_kernel(const unsigned lon
                                                                const uint32_t *block_prefix, const uint32_t *base,
                                                                const uint32_t *in_queue, int32_t first, int32_t n,
                                                                uint32_t *out_queue, FlatEnrol fe, const uint32_t *dev_n,
-                                                               const uint32_t *mode) {
-    if (mode && *mode == STEP_IDLE) return;
+                                                               const uint32_t *mode, uint32_t skip) {
+    // skip: a second mode that runs nothing here (a tail run on its own stream
+    // by chr_propagate_batches leaves no queue behind)
+    if (mode && (*mode == STEP_IDLE || *mode == skip)) return;
     if (dev_n) n = (int32_t)(*dev_n - 1u);
     // grid-stride (device-driven steps launch one grid for any queue length)
     for (int id = blockIdx.x * BLOCK + threadIdx.x; id < n; id += gridDim.x * BLOCK) {
@@ -2928,12 +2935,12 @@ inline uint32_t scan_blocks(uint32_t nwords) { return (nwords + SCAN_WORDS - 1) 
 // word_offsets (nwords) + block prefixes (scan_blocks(nwords)) of the masks
 void launch_mask_scan(const unsigned long long *masks, uint32_t nwords, uint32_t *word_offsets, uint32_t *block_sums,
                       uint32_t *out_counter, uint32_t *base, uint32_t *total_out, hipStream_t stream,
-                      const uint32_t *dev_n = nullptr, const uint32_t *mode = nullptr) {
+                      const uint32_t *dev_n = nullptr, const uint32_t *mode = nullptr, uint32_t skip = STEP_IDLE) {
     const uint32_t nb = scan_blocks(nwords);   // device-driven: nwords is an upper bound
     if (nb) hipLaunchKernelGGL(mask_block_scan_kernel, dim3(nb), dim3(SCAN_WORDS), 0, stream, masks, nwords, word_offsets,
-                               block_sums, dev_n, mode);
+                               block_sums, dev_n, mode, skip);
     hipLaunchKernelGGL(scan_block_sums_kernel, dim3(1), dim3(1024), 0, stream, block_sums, nb, out_counter, base,
-                       total_out, mode);
+                       total_out, mode, skip);
 }
 
 PhotonPtrs to_ptrs(const chr_photons *p) {
@@ -2980,11 +2987,13 @@ struct Scratch {
     int device = -1;
 };
 
-int scratch_get(size_t bytes, void **out) {
-    static thread_local Scratch s[16];
+// ctx: which of a thread's two propagate contexts (chr_propagate_batches
+// alternates them so one batch's tail can run while the next batch starts)
+int scratch_get(size_t bytes, void **out, int ctx = 0) {
+    static thread_local Scratch s[2][16];
     int dev = 0;
     CHR_HIP_CHECK(hipGetDevice(&dev));
-    Scratch &x = s[dev & 15];
+    Scratch &x = s[ctx & 1][dev & 15];
     if (x.bytes < bytes) {
         if (x.ptr) CHR_HIP_CHECK(hipFree(x.ptr));
         x.ptr = nullptr;
@@ -3233,7 +3242,7 @@ static int launch_chunk(const chr_geometry *g, const chr_photons *ph, uint32_t *
     hipLaunchKernelGGL(scatter_queue_kernel, dim3(grid_for(nthreads)), dim3(BLOCK), 0, stream, masks, offsets, bsums,
                        counters + 1, in_queue, first, nthreads, out_queue,
                        FlatEnrol{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr}, (const uint32_t *)nullptr,
-                       (const uint32_t *)nullptr);
+                       (const uint32_t *)nullptr, STEP_IDLE);
     CHR_HIP_CHECK(hipGetLastError());
     return CHR_OK;
 }
@@ -3262,11 +3271,11 @@ struct FlatCtx {
     int cur;
     bool enrol_next;
 };
-static int flat_get(uint32_t n, FlatCtx &fc) {
-    static thread_local Scratch s[16];
+static int flat_get(uint32_t n, FlatCtx &fc, int ctx = 0) {
+    static thread_local Scratch s[2][16];
     int dev = 0;
     CHR_HIP_CHECK(hipGetDevice(&dev));
-    Scratch &x = s[dev & 15];
+    Scratch &x = s[ctx & 1][dev & 15];
     const size_t bytes = 256 + (size_t)n * 12 + 64;
     if (x.bytes < bytes) {
         if (x.ptr) CHR_HIP_CHECK(hipFree(x.ptr));
@@ -3294,6 +3303,15 @@ struct SlotCtl {
     uint32_t n_layout;     // photons of the propagate: layout of the hits / binning regions
     int32_t remaining;     // steps left (max_steps - step)
     uint32_t tail_below;   // the nsteps policy's threshold, nthreads_per_block * 128
+    // chr_propagate_batches: the slot's tail kernel runs on its own stream
+    // (after the slot's one-step kernels, ev1), so the caller's stream moves on
+    // to the next batch while a tail's long-lived photons finish.  The tail
+    // leaves no queue (it runs every remaining step): its alive bits go to
+    // tail_masks and the slot's scan / scatter skip the tail mode.
+    hipStream_t tail_stream = nullptr;
+    unsigned long long *tail_masks = nullptr;
+    hipEvent_t evt_tail0 = nullptr, evt_tail1 = nullptr;   // around the tail kernel, on tail_stream
+    hipEvent_t rng_ready = nullptr;   // the previous batch's tail done: the first RNG use waits for it
 };
 
 // hits: n (triangle, distance) slots + a ray counter word, for the split path
@@ -3389,9 +3407,32 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
         if (evt1) CHR_HIP_CHECK(hipEventRecord(evt1, stream));
         a.hits = hits;
         a.max_steps = 1;
+        if (sc && sc->rng_ready) CHR_HIP_CHECK(hipStreamWaitEvent(stream, sc->rng_ready, 0));
         hipLaunchKernelGGL(sv.shade, dim3(grid_for(threads)), dim3(BLOCK), 0, stream, (const DevGeom *)g->d_dev, a, cap);
     }
     if (split_out) *split_out = split;
+    if (tail && sc && sc->tail_stream) {   // the tail on its own stream (chr_propagate_batches)
+        if (!ev1) return chr::fail(CHR_ERR_INVALID, "launch_step: a tail stream needs the slot's end event");
+        hipStream_t ts = sc->tail_stream;
+        CHR_HIP_CHECK(hipEventRecord(ev1, stream));
+        CHR_HIP_CHECK(hipStreamWaitEvent(ts, ev1, 0));
+        if (sc->evt_tail0) CHR_HIP_CHECK(hipEventRecord(sc->evt_tail0, ts));
+        hipLaunchKernelGGL(clear_masks_kernel, dim3(std::min<uint32_t>(1024u, grid_for(nwords))), dim3(BLOCK), 0, ts,
+                           sc->tail_masks, dev_n, mode);
+        PropagateArgs at = a;
+        at.alive_masks = sc->tail_masks;
+        at.max_steps = sc->remaining;
+        at.want = STEP_TAIL;
+        hipLaunchKernelGGL(sv.tail, dim3(grid_for((uint64_t)threads * sv.tail_group)), dim3(BLOCK), 0, ts,
+                           (const DevGeom *)g->d_dev, at, cap);
+        if (sc->evt_tail1) CHR_HIP_CHECK(hipEventRecord(sc->evt_tail1, ts));
+        launch_mask_scan(masks, nwords, offsets, bsums, out_queue, counters + 1, nullptr, stream, dev_n, mode, STEP_TAIL);
+        hipLaunchKernelGGL(scatter_queue_kernel, dim3(std::min<uint32_t>(4096u, grid_for(n))), dim3(BLOCK), 0, stream,
+                           masks, offsets, bsums, counters + 1, in_queue, 0, (int32_t)n, out_queue, fe, dev_n, mode,
+                           STEP_TAIL);
+        CHR_HIP_CHECK(hipGetLastError());
+        return CHR_OK;
+    }
     if (tail) {   // group / wave-adaptive walk, alive bits OR-ed into zeroed words
         if (sc) hipLaunchKernelGGL(clear_masks_kernel, dim3(std::min<uint32_t>(1024u, grid_for(nwords))), dim3(BLOCK), 0,
                                    stream, masks, dev_n, mode);
@@ -3407,7 +3448,7 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
     launch_mask_scan(masks, nwords, offsets, bsums, out_queue, counters + 1, nullptr, stream, dev_n, mode);
     hipLaunchKernelGGL(scatter_queue_kernel, dim3(sc ? std::min<uint32_t>(4096u, grid_for(n)) : grid_for(n)), dim3(BLOCK),
                        0, stream, masks, offsets, bsums, counters + 1, in_queue, 0, (int32_t)n, out_queue, fe, dev_n,
-                       mode);
+                       mode, STEP_IDLE);
     CHR_HIP_CHECK(hipGetLastError());
     return CHR_OK;
 }
@@ -3427,21 +3468,22 @@ extern "C" int chr_propagate_chunk(const chr_geometry *g, const chr_photons *ph,
 }
 
 // pinned host words for survivor counts / counters (per thread and device, reused)
-static int pinned_words(uint32_t **out) {
-    static thread_local uint32_t *p[16] = {};
+static int pinned_words(uint32_t **out, int ctx = 0) {
+    static thread_local uint32_t *p[2][16] = {};
     int dev = 0;
     CHR_HIP_CHECK(hipGetDevice(&dev));
-    if (!p[dev & 15]) CHR_HIP_CHECK(hipHostMalloc((void **)&p[dev & 15], 512, hipHostMallocDefault));
-    *out = p[dev & 15];
+    uint32_t *&w = p[ctx & 1][dev & 15];
+    if (!w) CHR_HIP_CHECK(hipHostMalloc((void **)&w, 512, hipHostMallocDefault));
+    *out = w;
     return CHR_OK;
 }
 
 // timing events, reused across calls (per thread)
-static int timing_events(size_t n, std::vector<hipEvent_t> **out) {
-    static thread_local std::vector<hipEvent_t> ev[16];
+static int timing_events(size_t n, std::vector<hipEvent_t> **out, int ctx = 0) {
+    static thread_local std::vector<hipEvent_t> ev[2][16];
     int dev = 0;
     CHR_HIP_CHECK(hipGetDevice(&dev));
-    std::vector<hipEvent_t> &v = ev[dev & 15];
+    std::vector<hipEvent_t> &v = ev[ctx & 1][dev & 15];
     while (v.size() < n) {
         hipEvent_t e;
         CHR_HIP_CHECK(hipEventCreate(&e));
@@ -3483,11 +3525,11 @@ static bool host_steps_forced() {     // CHR_HOST_STEPS=1: read the survivor cou
 
 // per-slot control words of a device-driven propagate: [2k] mode, [2k + 1]
 // queue length of slot k, then the done flag (per thread and device, grown on demand)
-static int slot_ctl_get(size_t words, uint32_t **out) {
-    static thread_local Scratch s[16];
+static int slot_ctl_get(size_t words, uint32_t **out, int ctx = 0) {
+    static thread_local Scratch s[2][16];
     int dev = 0;
     CHR_HIP_CHECK(hipGetDevice(&dev));
-    Scratch &x = s[dev & 15];
+    Scratch &x = s[ctx & 1][dev & 15];
     if (x.bytes < words * 4) {
         if (x.ptr) CHR_HIP_CHECK(hipFree(x.ptr));
         x.ptr = nullptr;
@@ -3498,51 +3540,234 @@ static int slot_ctl_get(size_t words, uint32_t **out) {
     return CHR_OK;
 }
 
+// per-slot events of a device-driven propagate: [0] slot start, [1] its
+// one-step kernels done (with the tail when that runs on the same stream),
+// [2,3] around trace_kernel, [4] slot done (ring copied), [5,6] around the tail
+// kernel when it runs on the tail stream (chr_propagate_batches)
+constexpr int SLOT_EVENTS = 7;
+
+// Device buffers of one propagate (context ctx of the calling thread):
+// queues, step scratch, the split path's hits / binning region, the flat-walk
+// lists, and (tail_masks) alive words for a tail run on its own stream.
+struct PropBufs {
+    uint64_t cap = 0;        // slots of one chunk, nthreads_per_block * max_blocks
+    bool fused = false;      // one launch per step
+    uint32_t *q[2] = {nullptr, nullptr};
+    uint32_t *scratch = nullptr;
+    int2 *hits = nullptr;
+    uint32_t *sort_space = nullptr;
+    unsigned long long *tail_masks = nullptr;
+    uint32_t *pinned = nullptr;
+    FlatCtx fc{};
+};
+
+static int prop_bufs(uint32_t nphotons, int32_t ntpb, int32_t max_blocks, int ctx, bool tail_masks, PropBufs &b) {
+    b.cap = (uint64_t)ntpb * max_blocks;   // slots of one chunk (chunk_iterator)
+    const uint32_t chunk_cap = (uint32_t)std::min<uint64_t>(b.cap, nphotons);
+    // one launch per step when a wave's 64 slots map to whole mask words
+    b.fused = (b.cap % 64 == 0) && b.cap <= 0x7FFFFFFFull && step_launch_enabled() && !sort_enabled();
+    uint64_t swords = chr_propagate_scratch_words(chunk_cap);
+    if (b.fused) swords = std::max<uint64_t>(swords, 16 + mask_scan_words(nphotons) + 16);
+    const size_t qbytes = ((size_t)nphotons + 1) * 4;
+    // split path: hits, ray counter, binning keys/order/histogram
+    const size_t hbytes = b.fused ? (size_t)nphotons * 24 + 128 + 256 + 512 + sort_temp_bytes16(nphotons) : 0;
+    const size_t base_bytes = 2 * qbytes + swords * 4 + 64 + hbytes;
+    const size_t mbytes = tail_masks ? ((size_t)nphotons + 63) / 64 * 8 + 512 : 0;
+    void *buf = nullptr;
+    int rc = scratch_get(base_bytes + mbytes, &buf, ctx);
+    if (rc) return rc;
+    b.q[0] = (uint32_t *)buf;
+    b.q[1] = b.q[0] + (nphotons + 1);
+    b.scratch = (uint32_t *)(((uintptr_t)(b.q[1] + nphotons + 1) + 15) & ~(uintptr_t)15);
+    b.hits = b.fused ? (int2 *)(((uintptr_t)(b.scratch + swords) + 15) & ~(uintptr_t)15) : nullptr;
+    // radix-sort space after [hits][next+pad][keys][order][hist][walk hist]
+    b.sort_space = b.fused ? (uint32_t *)(((uintptr_t)((uint32_t *)(b.hits + nphotons) + 16 + 2 * (size_t)nphotons +
+                                                       64) + 255) & ~(uintptr_t)255) : nullptr;
+    b.tail_masks = tail_masks ? (unsigned long long *)(((uintptr_t)buf + base_bytes + 255) & ~(uintptr_t)255) : nullptr;
+    if ((rc = pinned_words(&b.pinned, ctx))) return rc;
+    if (b.fused && (rc = flat_get(nphotons, b.fc, ctx))) return rc;
+    return CHR_OK;
+}
+
+// queues (photon.py:242-250: clones interleaved, q[1] header = 1), step counters, flat-walk control words
+static int prop_start(const PropBufs &b, uint32_t nphotons, uint32_t true_nphotons, uint32_t ncopies, hipStream_t stream) {
+    if (b.fused) CHR_HIP_CHECK(hipMemsetAsync(b.fc.ctl, 0, 128, stream));
+    hipLaunchKernelGGL(init_queue_kernel, dim3(grid_for(nphotons)), dim3(BLOCK), 0, stream, b.q[0], b.q[1], nphotons,
+                       true_nphotons, ncopies);
+    CHR_HIP_CHECK(hipGetLastError());
+    CHR_HIP_CHECK(hipMemsetAsync(b.scratch, 0, 64, stream));
+    return CHR_OK;
+}
+
+// Device-driven steps: every slot's kernels read the queue length from the
+// queue header and the head kernel applies the nsteps policy, so the host
+// queues slot k + 1 while slot k runs and only waits (on slot k - 1's event,
+// already done by then) to learn when the tail has run -- no survivor-count
+// round trip between steps.  Same launches, same results.  tstream: the tail
+// kernels go there (chr_propagate_batches); rng_ready: the first RNG use waits
+// for it.  *k_out = slots queued, *ctl_out = their [mode, length] words.
+static int device_slots(const chr_geometry *g, const chr_photons *ph, uint32_t nphotons, uint32_t *rng, uint32_t nslots,
+                        int32_t ntpb, int32_t max_steps, int32_t use_weights, int32_t scatter_first, PropBufs &b,
+                        int ctx, hipStream_t stream, hipStream_t tstream, hipEvent_t rng_ready, uint32_t **ctl_out,
+                        int *k_out) {
+    const uint32_t tail_below = (uint32_t)ntpb * 16 * 8;   // photon.py:261-264
+    uint32_t *ctl = nullptr;
+    int rc = slot_ctl_get(2 * (size_t)max_steps + 8, &ctl, ctx);
+    if (rc) return rc;
+    uint32_t *done = ctl + 2 * (size_t)max_steps;
+    CHR_HIP_CHECK(hipMemsetAsync(done, 0, 4, stream));
+    b.fc.enrol_next = true;
+    uint32_t *ring = b.pinned + 64;   // (mode, n) of recent slots, 32 entries (copied after each slot)
+    std::vector<hipEvent_t> *evp = nullptr;
+    uint32_t n_ub = nphotons;
+    int k = 0, cur = 0;
+    bool stop = false;
+    while (k < max_steps && !stop) {
+        if ((rc = timing_events(SLOT_EVENTS * (size_t)(k + 1), &evp, ctx))) return rc;
+        hipEvent_t *ev = evp->data() + SLOT_EVENTS * (size_t)k;
+        SlotCtl sc{ctl + 2 * (size_t)k, ctl + 2 * (size_t)k + 1, done, nphotons, max_steps - k, tail_below};
+        sc.tail_stream = tstream;
+        sc.tail_masks = b.tail_masks;
+        sc.evt_tail0 = ev[5];
+        sc.evt_tail1 = ev[6];
+        sc.rng_ready = k == 0 ? rng_ready : nullptr;
+        bool split = false;
+        rc = launch_step(g, ph, rng, nslots, (uint32_t)b.cap, n_ub, b.q[cur] + 1, b.q[cur ^ 1], 1, use_weights,
+                         scatter_first, b.scratch, stream, ev[0], ev[1], b.hits, b.sort_space, k == 0, ev[2], ev[3],
+                         &split, &b.fc, &sc);
+        if (rc) return rc;
+        CHR_HIP_CHECK(hipMemcpyAsync(ring + 2 * (k % 32), ctl + 2 * (size_t)k, 8, hipMemcpyDeviceToHost, stream));
+        CHR_HIP_CHECK(hipEventRecord(ev[4], stream));
+        b.fc.cur ^= 1;   // the step's scatter enrolled the next step's flat walks in the other list
+        cur ^= 1;
+        scatter_first = 0;
+        if (k >= 1) {   // slot k - 1 finished before slot k started: is there a slot k + 1?
+            CHR_HIP_CHECK(hipEventSynchronize((*evp)[SLOT_EVENTS * (size_t)(k - 1) + 4]));
+            const uint32_t m = ring[2 * ((k - 1) % 32)], nk = ring[2 * ((k - 1) % 32) + 1];
+            if (m != STEP_ONE) stop = true;   // the tail ran or the queue emptied: slot k is idle
+            else n_ub = nk;                   // later queues are no longer
+        }
+        k++;
+    }
+    *ctl_out = ctl;
+    *k_out = k;
+    return CHR_OK;
+}
+
+// per-slot statistics of a finished device-driven propagate (h: [mode, length] per slot)
+static int slot_stats(chr_propagate_stats &st, const uint32_t *h, int k, const std::vector<hipEvent_t> &events,
+                      bool tail_stream) {
+    for (int j = 0; j < k; ++j) {
+        const uint32_t m = h[2 * j], nj = h[2 * j + 1];
+        const hipEvent_t *ev = events.data() + SLOT_EVENTS * (size_t)j;
+        float ms = 0.0f;
+        CHR_HIP_CHECK(hipEventElapsedTime(&ms, ev[0], ev[1]));
+        st.kernel_ms += ms;
+        if (m == STEP_IDLE) continue;
+        st.launches++;
+        st.steps_run++;
+        if (m == STEP_ONE) {
+            CHR_HIP_CHECK(hipEventElapsedTime(&ms, ev[2], ev[3]));
+            st.trace_ms += ms;
+            if (st.trace_ms_n < CHR_TRACE_MS_MAX) {
+                st.trace_launch_rays[st.trace_ms_n] = nj;
+                st.trace_launch_ms[st.trace_ms_n++] = ms;
+            }
+            st.trace_launches++;
+            st.trace_rays += nj;
+        } else {
+            if (tail_stream) {
+                CHR_HIP_CHECK(hipEventElapsedTime(&ms, ev[5], ev[6]));
+                st.kernel_ms += ms;
+            }
+            st.tail_ms += ms;
+            st.tail_photons += nj;
+        }
+    }
+    return CHR_OK;
+}
+
+// device counters of a propagate -> pinned words [2] overflows, [4..17] walk
+// counters, [20..34] flat-walk and tail diagnostics (fused path)
+static int counter_readback(const PropBufs &b, hipStream_t s) {
+    CHR_HIP_CHECK(hipMemcpyAsync(b.pinned + 2, b.scratch, 4, hipMemcpyDeviceToHost, s));
+    CHR_HIP_CHECK(hipMemcpyAsync(b.pinned + 4, b.scratch + 2, 56, hipMemcpyDeviceToHost, s));
+    if (b.fused) CHR_HIP_CHECK(hipMemcpyAsync(b.pinned + 20, b.fc.ctl + 3, 60, hipMemcpyDeviceToHost, s));
+    return CHR_OK;
+}
+
+static void counter_stats(chr_propagate_stats &st, const PropBufs &b) {
+    const uint32_t *pinned = b.pinned;
+    st.stack_overflows = pinned[2];
+    st.flat_walks = b.fused ? pinned[20] : 0u;
+    st.flat_walks_whole = b.fused ? pinned[21] : 0u;
+    if (b.fused) {
+        uint64_t key;
+        std::memcpy(&key, pinned + 23, 8);
+        st.tail_max_steps = pinned[22];
+        st.tail_max_cycles = key >> 16;
+        st.tail_slowest_steps = (uint32_t)(key & 0xFFFFu);
+        uint64_t lp[5];
+        std::memcpy(lp, pinned + 25, 40);   // ctl[8..17]
+        st.tail_long_walk_ticks = lp[0];
+        st.tail_long_ticks = lp[1];
+        st.tail_long_walk_iterations = lp[2];
+        st.tail_long_steps = lp[3];
+        st.tail_long_photons = (uint32_t)lp[4];
+    }
+    uint64_t c[7];
+    std::memcpy(c, pinned + 4, 56);
+    st.wave_fill_cycles = c[5];
+    st.wave_step_cycles = c[6];
+    st.nodes_visited = c[0];
+    st.triangles_tested = c[1];
+    st.traversals = c[2];
+    st.wave_node_steps = c[3];
+    st.wave_triangle_steps = c[4];
+}
+
+static int check_propagate_args(const char *fn, const chr_geometry *g, const chr_photons *ph, uint32_t nphotons,
+                                uint32_t true_nphotons, uint32_t ncopies, const uint32_t *d_rng_states,
+                                uint32_t rng_nslots, int32_t ntpb, int32_t max_blocks) {
+    if (!g || !photons_ok(ph) || !d_rng_states) return chr::fail(CHR_ERR_INVALID, "%s: null argument", fn);
+    if (ntpb <= 0 || max_blocks <= 0) return chr::fail(CHR_ERR_INVALID, "%s: bad launch shape", fn);
+    if ((uint64_t)ntpb * (uint64_t)max_blocks > rng_nslots)
+        return chr::fail(CHR_ERR_INVALID, "%s: rng_states must hold nthreads_per_block*max_blocks=%lld states (have %u)",
+                         fn, (long long)ntpb * max_blocks, rng_nslots);
+    if (ncopies == 0 || (uint64_t)true_nphotons * ncopies != nphotons)
+        return chr::fail(CHR_ERR_INVALID, "%s: nphotons != true_nphotons*ncopies", fn);
+    if (nphotons > 0x7FFFFFFFu) return chr::fail(CHR_ERR_INVALID, "%s: more than 2^31-1 photons", fn);
+    return CHR_OK;
+}
+
+static bool device_steps_ok(const chr_geometry *g, const PropBufs &b) {
+    return b.fused && !trace_steps() && !host_steps_forced() && select_step_variant(g).trace != nullptr;
+}
+
 extern "C" int chr_propagate(const chr_geometry *g, const chr_photons *ph, uint32_t nphotons, uint32_t true_nphotons,
                              uint32_t ncopies, uint32_t *d_rng_states, uint32_t rng_nslots, int32_t ntpb,
                              int32_t max_blocks, int32_t max_steps, int32_t use_weights, int32_t scatter_first,
                              chr_propagate_stats *stats, void *vstream) {
-    if (!g || !photons_ok(ph) || !d_rng_states) return chr::fail(CHR_ERR_INVALID, "chr_propagate: null argument");
-    if (ntpb <= 0 || max_blocks <= 0) return chr::fail(CHR_ERR_INVALID, "chr_propagate: bad launch shape");
-    if ((uint64_t)ntpb * (uint64_t)max_blocks > rng_nslots)
-        return chr::fail(CHR_ERR_INVALID, "chr_propagate: rng_states must hold nthreads_per_block*max_blocks=%lld states (have %u)",
-                         (long long)ntpb * max_blocks, rng_nslots);
-    if (ncopies == 0 || (uint64_t)true_nphotons * ncopies != nphotons)
-        return chr::fail(CHR_ERR_INVALID, "chr_propagate: nphotons != true_nphotons*ncopies");
-    if (nphotons > 0x7FFFFFFFu) return chr::fail(CHR_ERR_INVALID, "chr_propagate: more than 2^31-1 photons");
+    CHR_TRY(check_propagate_args("chr_propagate", g, ph, nphotons, true_nphotons, ncopies, d_rng_states, rng_nslots,
+                                 ntpb, max_blocks));
     if (walks_reference_bvh(g)) CHR_TRY(chr::geometry_ref_nodes(g));
     hipStream_t stream = (hipStream_t)vstream;
     chr_propagate_stats st{};
     if (nphotons == 0) { if (stats) *stats = st; return CHR_OK; }
     if (int lrc = apply_node_layout(g, stream)) return lrc;
-    const uint64_t cap = (uint64_t)ntpb * max_blocks;   // slots of one chunk (chunk_iterator)
-    const uint32_t chunk_cap = (uint32_t)std::min<uint64_t>(cap, nphotons);
-    // one launch per step when a wave's 64 slots map to whole mask words
-    const bool fused = (cap % 64 == 0) && cap <= 0x7FFFFFFFull && step_launch_enabled() && !sort_enabled();
-    uint64_t swords = chr_propagate_scratch_words(chunk_cap);
-    if (fused) swords = std::max<uint64_t>(swords, 16 + mask_scan_words(nphotons) + 16);
-    const size_t qbytes = ((size_t)nphotons + 1) * 4;
-    // split path: hits, ray counter, binning keys/order/histogram
-    const size_t hbytes = fused ? (size_t)nphotons * 24 + 128 + 256 + 512 + sort_temp_bytes16(nphotons) : 0;
-    void *buf = nullptr;
-    int rc = scratch_get(2 * qbytes + swords * 4 + 64 + hbytes, &buf);
+    PropBufs b;
+    int rc = prop_bufs(nphotons, ntpb, max_blocks, 0, false, b);
     if (rc) return rc;
-    uint32_t *q[2];
-    q[0] = (uint32_t *)buf;
-    q[1] = q[0] + (nphotons + 1);
-    uint32_t *scratch = (uint32_t *)(((uintptr_t)(q[1] + nphotons + 1) + 15) & ~(uintptr_t)15);
-    int2 *hits = fused ? (int2 *)(((uintptr_t)(scratch + swords) + 15) & ~(uintptr_t)15) : nullptr;
-    // radix-sort space after [hits][next+pad][keys][order][hist][walk hist]
-    uint32_t *sort_space = fused ? (uint32_t *)(((uintptr_t)((uint32_t *)(hits + nphotons) + 16 + 2 * (size_t)nphotons +
-                                                            64) + 255) & ~(uintptr_t)255) : nullptr;
-    uint32_t *pinned = nullptr;
-    if ((rc = pinned_words(&pinned))) return rc;
-    FlatCtx fc{};
-    if (fused) {
-        if ((rc = flat_get(nphotons, fc))) return rc;
-        CHR_HIP_CHECK(hipMemsetAsync(fc.ctl, 0, 128, stream));
-        fc.enrol_next = true;
-    }
+    const uint64_t cap = b.cap;
+    const uint32_t chunk_cap = (uint32_t)std::min<uint64_t>(cap, nphotons);
+    const bool fused = b.fused;
+    uint32_t *const *q = b.q;
+    uint32_t *scratch = b.scratch, *pinned = b.pinned;
+    int2 *hits = b.hits;
+    uint32_t *sort_space = b.sort_space;
+    FlatCtx &fc = b.fc;
+    if ((rc = prop_start(b, nphotons, true_nphotons, ncopies, stream))) return rc;
+    fc.enrol_next = fused;
     const size_t max_chunks = fused ? 2 : (nphotons + chunk_cap - 1) / chunk_cap;   // fused: step + its walk
     std::vector<hipEvent_t> *evp = nullptr;
     if ((rc = timing_events(2 * max_chunks, &evp))) return rc;
@@ -3568,85 +3793,24 @@ extern "C" int chr_propagate(const chr_geometry *g, const chr_photons *ph, uint3
         }
         return CHR_OK;
     };
-    // queues (photon.py:242-250): clones interleaved, q[1] header = 1 (count + 1)
-    hipLaunchKernelGGL(init_queue_kernel, dim3(grid_for(nphotons)), dim3(BLOCK), 0, stream, q[0], q[1], nphotons,
-                       true_nphotons, ncopies);
-    CHR_HIP_CHECK(hipGetLastError());
-    CHR_HIP_CHECK(hipMemsetAsync(scratch, 0, 64, stream));
     int cur = 0;
     int64_t n = nphotons;
     int step = 0;
-    // Device-driven steps: every slot's kernels read the queue length from the
-    // queue header and the head kernel applies the nsteps policy, so the host
-    // queues slot k + 1 while slot k runs and only waits (on slot k - 1's
-    // event, already done by then) to learn when the tail has run -- no
-    // survivor-count round trip between steps.  Same launches, same results.
-    const bool device_steps = fused && !trace_steps() && !host_steps_forced() && select_step_variant(g).trace != nullptr;
+    const bool device_steps = device_steps_ok(g, b);
     if (device_steps) {
-        const uint32_t tail_below = (uint32_t)ntpb * 16 * 8;   // photon.py:261-264
         uint32_t *ctl = nullptr;
-        if ((rc = slot_ctl_get(2 * (size_t)max_steps + 8, &ctl))) return rc;
-        uint32_t *done = ctl + 2 * (size_t)max_steps;
-        CHR_HIP_CHECK(hipMemsetAsync(done, 0, 4, stream));
-        uint32_t *ring = pinned + 64;   // (mode, n) of recent slots, 32 entries (copied after each slot)
-        uint32_t n_ub = nphotons;
         int k = 0;
-        bool stop = false;
-        while (k < max_steps && !stop) {
-            if ((rc = timing_events(5 * (size_t)(k + 1), &evp))) return rc;
-            hipEvent_t *ev = events.data() + 5 * (size_t)k;
-            SlotCtl sc{ctl + 2 * (size_t)k, ctl + 2 * (size_t)k + 1, done, nphotons, max_steps - k, tail_below};
-            bool split = false;
-            rc = launch_step(g, ph, d_rng_states, rng_nslots, (uint32_t)cap, n_ub, q[cur] + 1, q[cur ^ 1], 1,
-                             use_weights, scatter_first, scratch, stream, ev[0], ev[1], hits, sort_space, k == 0,
-                             ev[2], ev[3], &split, &fc, &sc);
-            if (rc) return rc;
-            CHR_HIP_CHECK(hipMemcpyAsync(ring + 2 * (k % 32), ctl + 2 * (size_t)k, 8, hipMemcpyDeviceToHost, stream));
-            CHR_HIP_CHECK(hipEventRecord(ev[4], stream));
-            fc.cur ^= 1;
-            cur ^= 1;
-            scatter_first = 0;
-            if (k >= 1) {   // slot k - 1 finished before slot k started: is there a slot k + 1?
-                CHR_HIP_CHECK(hipEventSynchronize(events[5 * (size_t)(k - 1) + 4]));
-                const uint32_t m = ring[2 * ((k - 1) % 32)], nk = ring[2 * ((k - 1) % 32) + 1];
-                if (m != STEP_ONE) stop = true;   // the tail ran or the queue emptied: slot k is idle
-                else n_ub = nk;                   // later queues are no longer
-            }
-            k++;
-        }
+        if ((rc = device_slots(g, ph, nphotons, d_rng_states, rng_nslots, ntpb, max_steps, use_weights, scatter_first,
+                               b, 0, stream, nullptr, nullptr, &ctl, &k)))
+            return rc;
         CHR_HIP_CHECK(hipStreamSynchronize(stream));
         st.host_syncs = 1;
         std::vector<uint32_t> h(2 * (size_t)k);
         CHR_HIP_CHECK(hipMemcpy(h.data(), ctl, 8 * (size_t)k, hipMemcpyDeviceToHost));
-        uint32_t last_mode = STEP_IDLE;
-        for (int j = 0; j < k; ++j) {
-            const uint32_t m = h[2 * j], nj = h[2 * j + 1];
-            float ms = 0.0f;
-            CHR_HIP_CHECK(hipEventElapsedTime(&ms, events[5 * (size_t)j], events[5 * (size_t)j + 1]));
-            kernel_ms += ms;
-            if (m == STEP_IDLE) continue;
-            last_mode = m;
-            st.launches++;
-            st.steps_run++;
-            if (m == STEP_ONE) {
-                CHR_HIP_CHECK(hipEventElapsedTime(&ms, events[5 * (size_t)j + 2], events[5 * (size_t)j + 3]));
-                trace_ms += ms;
-                if (st.trace_ms_n < CHR_TRACE_MS_MAX) {
-                    st.trace_launch_rays[st.trace_ms_n] = nj;
-                    st.trace_launch_ms[st.trace_ms_n++] = ms;
-                }
-                st.trace_launches++;
-                st.trace_rays += nj;
-                step++;
-            } else {
-                CHR_HIP_CHECK(hipEventElapsedTime(&ms, events[5 * (size_t)j], events[5 * (size_t)j + 1]));
-                st.tail_ms += ms;
-                st.tail_photons += nj;
-                step = max_steps;
-            }
-        }
-        (void)last_mode;
-        n = 0;   // as the host loop: it leaves early only on an empty queue
+        if ((rc = timing_events(0, &evp))) return rc;
+        if ((rc = slot_stats(st, h.data(), k, *evp, false))) return rc;
+        step = max_steps;   // as the host loop: it leaves early only on an empty queue
+        n = 0;
     }
     while (!device_steps && step < max_steps) {
         const int nsteps = (n < (int64_t)ntpb * 16 * 8 || use_weights) ? max_steps - step : 1;   // photon.py:261-264
@@ -3717,42 +3881,152 @@ extern "C" int chr_propagate(const chr_geometry *g, const chr_photons *ph, uint3
             if ((rc = collect(nchunks))) return rc;
         }
     }
-    CHR_HIP_CHECK(hipMemcpyAsync(pinned + 2, scratch, 4, hipMemcpyDeviceToHost, stream));
-    CHR_HIP_CHECK(hipMemcpyAsync(pinned + 4, scratch + 2, 56, hipMemcpyDeviceToHost, stream));
-    if (fused) CHR_HIP_CHECK(hipMemcpyAsync(pinned + 20, fc.ctl + 3, 60, hipMemcpyDeviceToHost, stream));
+    if ((rc = counter_readback(b, stream))) return rc;
     CHR_HIP_CHECK(hipStreamSynchronize(stream));
-    st.stack_overflows = pinned[2];
-    st.flat_walks = fused ? pinned[20] : 0u;
-    st.flat_walks_whole = fused ? pinned[21] : 0u;
-    if (fused) {
-        uint64_t key;
-        std::memcpy(&key, pinned + 23, 8);
-        st.tail_max_steps = pinned[22];
-        st.tail_max_cycles = key >> 16;
-        st.tail_slowest_steps = (uint32_t)(key & 0xFFFFu);
-        uint64_t lp[5];
-        std::memcpy(lp, pinned + 25, 40);   // ctl[8..17]
-        st.tail_long_walk_ticks = lp[0];
-        st.tail_long_ticks = lp[1];
-        st.tail_long_walk_iterations = lp[2];
-        st.tail_long_steps = lp[3];
-        st.tail_long_photons = (uint32_t)lp[4];
-    }
-    {
-        uint64_t c[7];
-        std::memcpy(c, pinned + 4, 56);
-        st.wave_fill_cycles = c[5];
-        st.wave_step_cycles = c[6];
-        st.nodes_visited = c[0];
-        st.triangles_tested = c[1];
-        st.traversals = c[2];
-        st.wave_node_steps = c[3];
-        st.wave_triangle_steps = c[4];
-    }
-    st.kernel_ms = kernel_ms;
-    st.trace_ms = trace_ms;
+    counter_stats(st, b);
+    st.kernel_ms += kernel_ms;
+    st.trace_ms += trace_ms;
     st.final_alive = (step < max_steps) ? (uint32_t)n : 0u;
     if (stats) *stats = st;
+    return CHR_OK;
+}
+
+// the stream the tails of chr_propagate_batches run on (per thread and device;
+// non-blocking: no implicit ordering with the legacy default stream)
+static int tail_stream_get(hipStream_t *out, hipEvent_t done[2]) {
+    struct TS { hipStream_t s = nullptr; hipEvent_t done[2] = {nullptr, nullptr}; };
+    static thread_local TS ts[16];
+    int dev = 0;
+    CHR_HIP_CHECK(hipGetDevice(&dev));
+    TS &t = ts[dev & 15];
+    if (!t.s) {
+        CHR_HIP_CHECK(hipStreamCreateWithFlags(&t.s, hipStreamNonBlocking));
+        for (int i = 0; i < 2; ++i) CHR_HIP_CHECK(hipEventCreateWithFlags(&t.done[i], hipEventDisableTiming));
+    }
+    *out = t.s;
+    done[0] = t.done[0];
+    done[1] = t.done[1];
+    return CHR_OK;
+}
+
+// pinned host copy of a batch's slot control words (per thread, device and context)
+static int pinned_ctl_get(size_t words, uint32_t **out, int ctx) {
+    struct P { uint32_t *p = nullptr; size_t words = 0; };
+    static thread_local P ps[2][16];
+    int dev = 0;
+    CHR_HIP_CHECK(hipGetDevice(&dev));
+    P &x = ps[ctx & 1][dev & 15];
+    if (x.words < words) {
+        if (x.p) CHR_HIP_CHECK(hipHostFree(x.p));
+        x.p = nullptr;
+        CHR_HIP_CHECK(hipHostMalloc((void **)&x.p, words * 4, hipHostMallocDefault));
+        x.words = words;
+    }
+    *out = x.p;
+    return CHR_OK;
+}
+
+static bool ranges_overlap(const void *a, size_t na, const void *b, size_t nb) {
+    const uintptr_t x = (uintptr_t)a, y = (uintptr_t)b;
+    return a && b && x < y + nb && y < x + na;
+}
+// whether two batches share any photon array (then the later one waits for the earlier one's tail)
+static bool photons_alias(const chr_photons *a, uint32_t na, const chr_photons *b, uint32_t nb) {
+    const void *pa[9] = {a->d_pos, a->d_dir, a->d_pol, a->d_wavelengths, a->d_t, a->d_weights, a->d_flags,
+                         a->d_last_hit_triangles, a->d_evidx};
+    const void *pb[9] = {b->d_pos, b->d_dir, b->d_pol, b->d_wavelengths, b->d_t, b->d_weights, b->d_flags,
+                         b->d_last_hit_triangles, b->d_evidx};
+    const size_t w[9] = {12, 12, 12, 4, 4, 4, 4, 4, 4};
+    for (int i = 0; i < 9; ++i)
+        for (int j = 0; j < 9; ++j)
+            if (ranges_overlap(pa[i], w[i] * na, pb[j], w[j] * nb)) return true;
+    return false;
+}
+
+extern "C" int chr_propagate_batches(const chr_geometry *g, const chr_photons *phs, const uint32_t *nphotons,
+                                     const uint32_t *true_nphotons, const uint32_t *ncopies, uint32_t nbatch,
+                                     uint32_t *d_rng_states, uint32_t rng_nslots, int32_t ntpb, int32_t max_blocks,
+                                     int32_t max_steps, int32_t use_weights, int32_t scatter_first,
+                                     chr_propagate_stats *stats, void *vstream) {
+    if (nbatch && (!phs || !nphotons || !true_nphotons || !ncopies))
+        return chr::fail(CHR_ERR_INVALID, "chr_propagate_batches: null argument");
+    for (uint32_t i = 0; i < nbatch; ++i)
+        CHR_TRY(check_propagate_args("chr_propagate_batches", g, phs + i, nphotons[i], true_nphotons[i], ncopies[i],
+                                     d_rng_states, rng_nslots, ntpb, max_blocks));
+    hipStream_t stream = (hipStream_t)vstream;
+    if (nbatch == 0) return CHR_OK;
+    if (walks_reference_bvh(g)) CHR_TRY(chr::geometry_ref_nodes(g));
+    if (int lrc = apply_node_layout(g, stream)) return lrc;
+    PropBufs probe;
+    probe.cap = (uint64_t)ntpb * max_blocks;
+    probe.fused = (probe.cap % 64 == 0) && probe.cap <= 0x7FFFFFFFull && step_launch_enabled() && !sort_enabled();
+    if (nbatch == 1 || !device_steps_ok(g, probe)) {   // nothing to overlap: one propagate after the other
+        for (uint32_t i = 0; i < nbatch; ++i)
+            CHR_TRY(chr_propagate(g, phs + i, nphotons[i], true_nphotons[i], ncopies[i], d_rng_states, rng_nslots,
+                                  ntpb, max_blocks, max_steps, use_weights, scatter_first, stats ? stats + i : nullptr,
+                                  vstream));
+        return CHR_OK;
+    }
+    hipStream_t ts = nullptr;
+    hipEvent_t done[2];
+    CHR_TRY(tail_stream_get(&ts, done));
+    // a batch in flight on context c: its tail may still run on ts; its
+    // statistics are read once done[c] (recorded on ts after its last slot) fires
+    struct Pending {
+        bool on = false;
+        int k = 0;
+        uint32_t *hctl = nullptr;
+        PropBufs b;
+        chr_propagate_stats *out = nullptr;
+    } pend[2];
+    std::vector<chr_propagate_stats> local(stats ? 0 : nbatch);
+    auto finish = [&](int c) -> int {
+        Pending &p = pend[c];
+        if (!p.on) return CHR_OK;
+        CHR_HIP_CHECK(hipEventSynchronize(done[c]));
+        std::vector<hipEvent_t> *evp = nullptr;
+        CHR_TRY(timing_events(0, &evp, c));
+        chr_propagate_stats &st = *p.out;
+        CHR_TRY(slot_stats(st, p.hctl, p.k, *evp, true));
+        counter_stats(st, p.b);
+        st.host_syncs = 1;
+        st.final_alive = 0;
+        p.on = false;
+        return CHR_OK;
+    };
+    int c = 0, prev = -1;
+    uint32_t prev_i = 0;
+    for (uint32_t i = 0; i < nbatch; ++i) {
+        chr_propagate_stats &st = stats ? stats[i] : local[i];
+        st = chr_propagate_stats{};
+        if (nphotons[i] == 0) continue;
+        CHR_TRY(finish(c));   // the batch that last used this context (two batches ago)
+        Pending &p = pend[c];
+        CHR_TRY(prop_bufs(nphotons[i], ntpb, max_blocks, c, true, p.b));
+        CHR_TRY(pinned_ctl_get(2 * (size_t)max_steps + 8, &p.hctl, c));
+        // the previous batch's tail may still run: its photon arrays are off
+        // limits, and its RNG slots are needed by this batch's first shade pass
+        if (prev >= 0 && photons_alias(phs + i, nphotons[i], phs + prev_i, nphotons[prev_i]))
+            CHR_HIP_CHECK(hipStreamWaitEvent(stream, done[prev], 0));
+        CHR_TRY(prop_start(p.b, nphotons[i], true_nphotons[i], ncopies[i], stream));
+        uint32_t *ctl = nullptr;
+        CHR_TRY(device_slots(g, phs + i, nphotons[i], d_rng_states, rng_nslots, ntpb, max_steps, use_weights,
+                             scatter_first, p.b, c, stream, ts, prev >= 0 ? done[prev] : nullptr, &ctl, &p.k));
+        // after the batch's last slot (and every tail before it on ts): read its counters back
+        std::vector<hipEvent_t> *evp = nullptr;
+        CHR_TRY(timing_events(0, &evp, c));
+        CHR_HIP_CHECK(hipStreamWaitEvent(ts, (*evp)[SLOT_EVENTS * (size_t)(p.k - 1) + 4], 0));
+        CHR_HIP_CHECK(hipMemcpyAsync(p.hctl, ctl, 8 * (size_t)p.k, hipMemcpyDeviceToHost, ts));
+        CHR_TRY(counter_readback(p.b, ts));
+        CHR_HIP_CHECK(hipEventRecord(done[c], ts));
+        p.out = &st;
+        p.on = true;
+        prev = c;
+        prev_i = i;
+        c ^= 1;
+    }
+    CHR_TRY(finish(c));
+    CHR_TRY(finish(c ^ 1));
     return CHR_OK;
 }
 

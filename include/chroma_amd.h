@@ -217,6 +217,22 @@ int chr_propagate(const chr_geometry *g, const chr_photons *ph, uint32_t nphoton
                   int32_t use_weights, int32_t scatter_first,
                   chr_propagate_stats *stats, void *stream);
 
+/* replaces: a sequence of GPUPhotons.propagate calls sharing one rng_states
+ * (the event loop of Simulation.simulate, chroma/sim.py:116-160, one propagate
+ * per event): batch i = photons phs[i] (nphotons[i] = true_nphotons[i] *
+ * ncopies[i]), propagated in order with the same RNG slot states and the same
+ * launch shape.  Results (photons, RNG states) are bit-identical to nbatch
+ * chr_propagate calls; the multi-step tail of batch i runs on a second stream
+ * while batch i+1 queues, bins and walks its first step (which needs no RNG),
+ * and batch i+1's first RNG use waits for that tail.  stats: nbatch entries
+ * (or NULL).  Batches whose photon arrays overlap are serialised.  Synchronous. */
+int chr_propagate_batches(const chr_geometry *g, const chr_photons *phs, const uint32_t *nphotons,
+                          const uint32_t *true_nphotons, const uint32_t *ncopies, uint32_t nbatch,
+                          uint32_t *d_rng_states, uint32_t rng_nslots,
+                          int32_t nthreads_per_block, int32_t max_blocks, int32_t max_steps,
+                          int32_t use_weights, int32_t scatter_first,
+                          chr_propagate_stats *stats, void *stream);
+
 /* ------------------------------------------------------------ selection */
 /* replaces: count_photon_hits + copy_photon_hits (propagate.cu:172-251),
  * driven by GPUPhotons.get_flat_hits (photon.py:141-209).  Hits are compacted

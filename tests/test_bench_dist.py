@@ -38,14 +38,17 @@ def _worker(rank, world, port, out_dir):
         counts = torch.zeros(nch, dtype=torch.int32)
         reduced = {}
 
-        def step():
-            time.sleep(0.02 * (rank + 1))               # rank 1 is the slow one
-            counts.fill_(0)
-            counts[rank % nch] = 3 + rank                # this rank's "hits"
-            reduced['c'] = shard.allreduce_channel_counts(counts)
-            return rank
+        def run(m):   # m steps per call, as bench.py's pipelined groups
+            out = []
+            for _ in range(m):
+                time.sleep(0.02 * (rank + 1))               # rank 1 is the slow one
+                counts.fill_(0)
+                counts[rank % nch] = 3 + rank                # this rank's "hits"
+                reduced['c'] = shard.allreduce_channel_counts(counts)
+                out.append(rank)
+            return out
 
-        elapsed, per_step, results = bench.timed_loop(step, 3, 1, dist, lambda: None)
+        elapsed, per_step, results = bench.timed_loop(run, 3, 1, dist, lambda: None, group=2)
         c = reduced['c'].numpy()
         res = np.array([elapsed, sum(per_step), md5, nch, bench.rng_first_subsequence(rank, 524288),
                         c[0], c[1 % nch], c.sum(), len(results)], dtype=np.float64)

@@ -1,0 +1,143 @@
+"""chr_propagate_batches (chroma.gpu.propagate_batches): several photon
+batches propagated with one rng_states, batch i's multi-step tail on a second
+stream while batch i+1 starts.  The contract is bit-identity with the same
+GPUPhotons.propagate calls made one after the other (the event loop of the
+reference Simulation, sim.py:116-160): every photon array and every RNG slot
+state, plus the oracle run sequentially on the small detector.
+"""
+import numpy as np
+import pytest
+
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+FIELDS = ('pos', 'dir', 'pol', 'wavelengths', 't', 'flags', 'last_hit_triangles', 'weights')
+
+
+@pytest.fixture(scope='module')
+def cuda():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip('no HIP device')
+    torch.cuda.set_device(0)
+
+
+def _sources(sizes, seed):
+    from chroma.photon_source import isotropic
+    return [isotropic(n, seed=seed + i) if n else None for i, n in enumerate(sizes)]
+
+
+def _gpu_photons(src):
+    from chroma import gpu
+    return gpu.GPUPhotons(src, copy_flags=True, copy_triangles=False, copy_weights=False)
+
+
+def _run(det, sources, ntpb, max_blocks, max_steps, batched, seed=3):
+    from chroma import gpu
+    rng = gpu.get_rng_states(ntpb * max_blocks, seed=seed)
+    gps = [_gpu_photons(s) for s in sources if s is not None]
+    if batched:
+        stats = gpu.propagate_batches(gps, det, rng, nthreads_per_block=ntpb, max_blocks=max_blocks,
+                                      max_steps=max_steps)
+    else:
+        stats = []
+        for gp in gps:
+            gp.propagate(det, rng, nthreads_per_block=ntpb, max_blocks=max_blocks, max_steps=max_steps)
+            stats.append(gp.last_stats)
+    return [gp.get() for gp in gps], rng.get(), stats
+
+
+def _same(a, b, label):
+    for f in FIELDS:
+        assert np.array_equal(getattr(a, f), getattr(b, f)), '%s: %s differs' % (label, f)
+
+
+@pytest.mark.parametrize('ntpb,max_blocks', [(64, 64), (256, 64)])
+def test_batches_equal_sequential_and_oracle(cuda, small_detector, small_packed, ntpb, max_blocks):
+    """Batches of 30k / 70k / 5k / 120k photons (one-step slots, then tails of
+    < ntpb*128 photons) on the 2-PMT detector: batched == sequential GPU ==
+    sequential oracle, photons and RNG states."""
+    from chroma import gpu
+    det = gpu.GPUDetector(small_detector)
+    sources = _sources([30000, 70000, 5000, 120000], seed=11)
+    seq, rng_seq, st_seq = _run(det, sources, ntpb, max_blocks, 1000, batched=False)
+    bat, rng_bat, st_bat = _run(det, sources, ntpb, max_blocks, 1000, batched=True)
+    for i, (a, b) in enumerate(zip(bat, seq)):
+        _same(a, b, 'batch %d' % i)
+    assert np.array_equal(rng_bat, rng_seq)
+    for sa, sb in zip(st_bat, st_seq):
+        assert sa.steps_run == sb.steps_run and sa.tail_photons == sb.tail_photons
+        assert sa.trace_rays == sb.trace_rays and sa.stack_overflows == 0
+    assert sum(s.tail_photons for s in st_bat) > 0     # tails ran (on the tail stream)
+    nslots = ntpb * max_blocks
+    states = oracle.rng_init(nslots, seed=3)
+    for i, src in enumerate(sources):
+        host = oracle.HostPhotons(src)
+        host.last_hit_triangles[:] = -1
+        host.weights[:] = 1.0
+        oracle.propagate(small_packed, host, states, nslots, ntpb, max_blocks, 1000)
+        for f in ('flags', 'last_hit_triangles'):
+            assert np.array_equal(getattr(bat[i], f), getattr(host, f)), 'oracle batch %d: %s' % (i, f)
+        for f in ('pos', 'dir', 'pol', 't', 'wavelengths'):
+            a = getattr(bat[i], f).astype(np.float64)
+            b = getattr(host, f).astype(np.float64)
+            assert np.all(np.abs(a - b) <= 1e-5 * np.maximum(np.abs(b), 1.0)), 'oracle batch %d: %s' % (i, f)
+    assert np.array_equal(rng_bat, states.reshape(6, nslots))
+
+
+def test_batches_same_photons_twice(cuda, small_detector):
+    """The same GPUPhotons listed twice (aliasing arrays: the second batch
+    waits for the first one's tail) == propagating it twice."""
+    from chroma import gpu
+    det = gpu.GPUDetector(small_detector)
+    src = _sources([40000], seed=5)[0]
+    out = {}
+    for batched in (False, True):
+        rng = gpu.get_rng_states(64 * 64, seed=9)
+        gp = _gpu_photons(src)
+        if batched:
+            gpu.propagate_batches([gp, gp], det, rng, nthreads_per_block=64, max_blocks=64, max_steps=7)
+        else:
+            for _ in range(2):
+                gp.propagate(det, rng, nthreads_per_block=64, max_blocks=64, max_steps=7)
+        out[batched] = (gp.get(), rng.get())
+    _same(out[True][0], out[False][0], 'twice')
+    assert np.array_equal(out[True][1], out[False][1])
+
+
+def test_batches_empty_and_single(cuda, small_detector):
+    """Empty batches are skipped; one batch is one chr_propagate."""
+    from chroma import gpu
+    det = gpu.GPUDetector(small_detector)
+    rng = gpu.get_rng_states(64 * 64, seed=2)
+    assert gpu.propagate_batches([], det, rng, nthreads_per_block=64, max_blocks=64) == []
+    src = _sources([20000], seed=8)[0]
+    a, b = _gpu_photons(src), _gpu_photons(src)
+    r1, r2 = gpu.get_rng_states(64 * 64, seed=2), gpu.get_rng_states(64 * 64, seed=2)
+    gpu.propagate_batches([a], det, r1, nthreads_per_block=64, max_blocks=64, max_steps=50)
+    b.propagate(det, r2, nthreads_per_block=64, max_blocks=64, max_steps=50)
+    _same(a.get(), b.get(), 'single')
+    assert np.array_equal(r1.get(), r2.get())
+
+
+@pytest.fixture(scope='module')
+def tiny_geo():
+    from chroma import demo, loader
+    return loader.create_geometry_from_obj(demo.tiny())
+
+
+@pytest.mark.timeout(600)
+def test_batches_c2_scale(cuda, tiny_geo):
+    """Three 2^20-photon batches on demo.tiny() with the bench launch shape
+    (512 x 1024): binned first steps overlapping the previous tail; batched ==
+    sequential, photons and RNG states."""
+    from chroma import gpu
+    det = gpu.GPUDetector(tiny_geo)
+    sources = _sources([1 << 20, 1 << 20, 1 << 20], seed=20260102)
+    seq, rng_seq, _ = _run(det, sources, 512, 1024, 1000, batched=False)
+    bat, rng_bat, st = _run(det, sources, 512, 1024, 1000, batched=True)
+    for i, (a, b) in enumerate(zip(bat, seq)):
+        _same(a, b, 'C2 batch %d' % i)
+    assert np.array_equal(rng_bat, rng_seq)
+    assert all(s.trace_launches >= 1 and s.tail_photons > 0 for s in st)
