@@ -15,12 +15,14 @@
 //    chr::geometry_ref_nodes); the default traversal walks an 8-wide SAH
 //    BVH built over the same leaf boxes with the reference DFS rank as the
 //    nearest-hit tie-break (wide_bvh.h) -- same answers, far fewer nodes;
-//  * triangles are de-indexed into 48-byte records of three float4:
+//  * the wide BVH's 64-byte triangle records (v0, v1, v2, id, rank, leaf box;
+//    wide_bvh.h) serve the walk AND the hit's normal; the reference walk's
+//    de-indexed 48-byte records of three float4
 //        (v0.x v0.y v0.z e1.x) (e1.y e1.z e2.x e2.y) (e2.z e3.x e3.y e3.z)
 //    with e1 = v1-v0, e2 = v2-v0 (the Moller-Trumbore edges, intersect.h:26-101)
-//    and e3 = v2-v1 (the normal edge of fill_state, photon.h:365-367), all
-//    computed on the host in float32 exactly as the kernel would: one
-//    16-byte-aligned 48-byte gather per tested triangle instead of 12+3x12;
+//    and e3 = v2-v1 (the normal edge of fill_state, photon.h:365-367) are
+//    resident only once a call walks the reference BVH (built on the device
+//    from the wide records, chr::geometry_ref_nodes);
 //  * every wavelength / time table lives in one float blob (each table padded
 //    by one element, see chr_geometry_desc), addressed by 32-bit offsets held
 //    in small DevMaterial / DevSurface records.
@@ -51,7 +53,7 @@ struct DevSurface {
 
 struct DevGeom {
     const uint4 *nodes;
-    const float4 *tri;               // 3 float4 per triangle
+    const float4 *tri;               // 3 float4 per triangle (reference walk; resident on first use)
     const uint32_t *material_codes;
     const float *tables;
     const DevMaterial *materials;
@@ -60,7 +62,7 @@ struct DevGeom {
     const uint4 *wnodes;             // 8-wide SAH BVH, node i at wnodes[wstride * i] (wide_bvh.h)
     const float4 *wtri;              // 3 float4 per leaf triangle record (wide_bvh.h)
     const uint2 *wcut;               // sub-walk items (node, child mask) of a decomposed walk (wide_bvh.h)
-    const uint32_t *wrank_id;        // reference DFS rank -> triangle id
+    const uint32_t *wrank_rec;       // reference DFS rank -> triangle record (wtri index)
     uint32_t nwcut;
     uint32_t nwnodes, nwtri;
     uint32_t wstride;                // uint4 per node slot: 8 (96-byte node padded to one 128-byte line) or 6
@@ -88,8 +90,12 @@ struct chr_geometry {
     // wide BVH only the root stays in HBM (the renderer's world box) and the
     // rest waits here until chr_geometry_ref_nodes() uploads it (once).
     std::vector<uint4> *h_ref_nodes;
+    bool ref_tri_pending;   // the 48-byte reference triangle records are built on first use
 };
 namespace chr {
-// make every reference node resident in HBM (no-op when it is); CHR_OK or an error
+// make every reference node and the reference triangle records resident in
+// HBM (no-op when they are); CHR_OK or an error
 int geometry_ref_nodes(const chr_geometry *g);
+// fill the 48-byte reference triangle records from the wide records (propagate.hip)
+int build_ref_triangles(const DevGeom &dg, float4 *tri);
 }

@@ -72,15 +72,23 @@ extern "C" int chr_geometry_destroy(chr_geometry *g) {
 
 int chr::geometry_ref_nodes(const chr_geometry *cg) {
     chr_geometry *g = const_cast<chr_geometry *>(cg);
-    if (!g->h_ref_nodes) return CHR_OK;
+    if (!g->h_ref_nodes && !g->ref_tri_pending) return CHR_OK;
     void *p = nullptr;
-    int rc = dev_upload(g, g->h_ref_nodes->data(), g->h_ref_nodes->size() * sizeof(uint4), &p);
-    if (rc) return rc;
-    g->dev.nodes = (const uint4 *)p;
+    int rc;
+    if (g->h_ref_nodes) {
+        if ((rc = dev_upload(g, g->h_ref_nodes->data(), g->h_ref_nodes->size() * sizeof(uint4), &p))) return rc;
+        g->dev.nodes = (const uint4 *)p;
+        delete g->h_ref_nodes;
+        g->h_ref_nodes = nullptr;
+    }
+    if (g->ref_tri_pending) {
+        if ((rc = dev_upload(g, nullptr, (size_t)g->dev.ntriangles * 48, &p))) return rc;
+        if ((rc = chr::build_ref_triangles(g->dev, (float4 *)p))) return rc;
+        g->dev.tri = (const float4 *)p;
+        g->ref_tri_pending = false;
+    }
     const hipError_t e = hipMemcpy(g->d_dev, &g->dev, sizeof(g->dev), hipMemcpyHostToDevice);
     if (e != hipSuccess) return chr::fail(CHR_ERR_HIP, "hipMemcpy H2D failed: %s", hipGetErrorString(e));
-    delete g->h_ref_nodes;
-    g->h_ref_nodes = nullptr;
     return CHR_OK;
 }
 
@@ -132,23 +140,6 @@ extern "C" int chr_geometry_create(const chr_geometry_desc *d, chr_geometry **ou
         dg.t_n = d->time_n; dg.t_start = d->time_start; dg.t_step = d->time_step;
 
         void *p;
-        // de-indexed triangle records: v0, e1 = v1-v0, e2 = v2-v0, e3 = v2-v1
-        std::vector<float> tri((size_t)d->ntriangles * 12);
-        const float *v = d->h_vertices;
-#pragma omp parallel for schedule(static)
-        for (int64_t t = 0; t < (int64_t)d->ntriangles; ++t) {
-            const uint32_t *ix = d->h_triangles + 3 * t;
-            const float *a = v + 3 * (size_t)ix[0], *b = v + 3 * (size_t)ix[1], *c = v + 3 * (size_t)ix[2];
-            float *r = tri.data() + 12 * t;
-            r[0] = a[0]; r[1] = a[1]; r[2] = a[2];
-            r[3] = b[0] - a[0]; r[4] = b[1] - a[1]; r[5] = b[2] - a[2];
-            r[6] = c[0] - a[0]; r[7] = c[1] - a[1]; r[8] = c[2] - a[2];
-            r[9] = c[0] - b[0]; r[10] = c[1] - b[1]; r[11] = c[2] - b[2];
-        }
-        if ((rc = dev_upload(g, tri.data(), tri.size() * sizeof(float), &p))) throw rc;
-        dg.tri = (const float4 *)p;
-        std::vector<float>().swap(tri);
-
         {
             chr::WideBVH wb;
             if ((rc = chr::build_wide_bvh(d, wb))) throw rc;
@@ -177,9 +168,32 @@ extern "C" int chr_geometry_create(const chr_geometry_desc *d, chr_geometry **ou
                 if ((rc = dev_upload(g, wb.cut.data(), wb.cut.size() * 4, &p))) throw rc;
                 dg.wcut = (const uint2 *)p;
                 dg.nwcut = (uint32_t)(wb.cut.size() / 2);
-                if ((rc = dev_upload(g, wb.rank_id.data(), wb.rank_id.size() * 4, &p))) throw rc;
-                dg.wrank_id = (const uint32_t *)p;
+                if ((rc = dev_upload(g, wb.rank_rec.data(), wb.rank_rec.size() * 4, &p))) throw rc;
+                dg.wrank_rec = (const uint32_t *)p;
             }
+        }
+
+        // de-indexed reference triangle records (v0, e1 = v1-v0, e2 = v2-v0,
+        // e3 = v2-v1) for the reference walk: uploaded now only without a wide
+        // BVH (or with CHR_REF_NODES_RESIDENT); otherwise built on the device
+        // from the wide records the first time a call walks the reference BVH
+        if (dg.nwnodes == 0 || std::getenv("CHR_REF_NODES_RESIDENT")) {
+            std::vector<float> tri((size_t)d->ntriangles * 12);
+            const float *v = d->h_vertices;
+#pragma omp parallel for schedule(static)
+            for (int64_t t = 0; t < (int64_t)d->ntriangles; ++t) {
+                const uint32_t *ix = d->h_triangles + 3 * t;
+                const float *a = v + 3 * (size_t)ix[0], *b = v + 3 * (size_t)ix[1], *c = v + 3 * (size_t)ix[2];
+                float *r = tri.data() + 12 * t;
+                r[0] = a[0]; r[1] = a[1]; r[2] = a[2];
+                r[3] = b[0] - a[0]; r[4] = b[1] - a[1]; r[5] = b[2] - a[2];
+                r[6] = c[0] - a[0]; r[7] = c[1] - a[1]; r[8] = c[2] - a[2];
+                r[9] = c[0] - b[0]; r[10] = c[1] - b[1]; r[11] = c[2] - b[2];
+            }
+            if ((rc = dev_upload(g, tri.data(), tri.size() * sizeof(float), &p))) throw rc;
+            dg.tri = (const float4 *)p;
+        } else {
+            g->ref_tri_pending = true;
         }
 
         // reference BVH nodes: all resident only without a wide BVH (or with

@@ -161,6 +161,17 @@ __device__ __forceinline__ bool intersect_triangle(V3 o, V3 d, V3 v0, V3 e1, V3 
     return false;
 }
 
+// Moller-Trumbore on a wide-BVH triangle record (wide_bvh.h: v0, v1, v2 in
+// r0..r2): the edges v1-v0, v2-v0 are the reference's own float subtractions
+// (intersect.h:26-101), so this is intersect_triangle on the same operands.
+__device__ __forceinline__ bool intersect_record(V3 o, V3 d, float4 r0, float4 r1, float4 r2, float &distance) {
+    const V3 v0 = v3(r0.x, r0.y, r0.z), v1 = v3(r0.w, r1.x, r1.y), v2 = v3(r1.z, r1.w, r2.x);
+    return intersect_triangle(o, d, v0, v1 - v0, v2 - v0, distance);
+}
+// the record index of a wide-BVH triangle record pointer: what the wide walks
+// return for a hit (finish_fill<true> reads the triangle id and normal from it)
+__device__ __forceinline__ int rec_of(const DevGeom &g, const float4 *r) { return (int)((r - g.wtri) >> 2); }
+
 // mesh.h:45-126 -- nearest triangle != last_hit; reference DFS order.
 // The children of a popped group are fetched BATCH at a time (independent
 // 16-byte loads in flight together), their slab tests computed up front, and
@@ -370,21 +381,32 @@ __device__ __forceinline__ uint32_t expand_node(const uint4 h, const uint4 a1, c
     const uint32_t fz0 = r.negz ? a2.x : a3.z, fz1 = r.negz ? a2.y : a3.w;
     float tk[8];
     uint32_t inner = 0, leaf = 0;
+    // two children per packed FMA (v_pk_fma_f32: each half a fused fmaf, so the
+    // plane distances are bit-identical to the scalar form above)
+    const F2 sx2 = f2(sx, sx), sy2 = f2(sy, sy), sz2 = f2(sz, sz);
+    const F2 ox2 = f2(org.x, org.x), oy2 = f2(org.y, org.y), oz2 = f2(org.z, org.z);
+    const F2 ix2 = f2(r.inx, r.inx), iy2 = f2(r.iny, r.iny), iz2 = f2(r.inz, r.inz);
+    const F2 nx2 = f2(r.onx, r.onx), ny2 = f2(r.ony, r.ony), nz2 = f2(r.onz, r.onz);
+    const F2 fx2 = f2(r.ofx, r.ofx), fy2 = f2(r.ofy, r.ofy), fz2 = f2(r.ofz, r.ofz);
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        const uint32_t kind = ((k < 4 ? a4.z : a4.w) >> (8 * (k & 3))) & 0xFFu;
-        const float tnx = __builtin_fmaf(__builtin_fmaf(byte_f(nx0, nx1, k), sx, org.x), r.inx, r.onx);
-        const float tfx = __builtin_fmaf(__builtin_fmaf(byte_f(fx0, fx1, k), sx, org.x), r.inx, r.ofx);
-        const float tny = __builtin_fmaf(__builtin_fmaf(byte_f(ny0, ny1, k), sy, org.y), r.iny, r.ony);
-        const float tfy = __builtin_fmaf(__builtin_fmaf(byte_f(fy0, fy1, k), sy, org.y), r.iny, r.ofy);
-        const float tnz = __builtin_fmaf(__builtin_fmaf(byte_f(nz0, nz1, k), sz, org.z), r.inz, r.onz);
-        const float tfz = __builtin_fmaf(__builtin_fmaf(byte_f(fz0, fz1, k), sz, org.z), r.inz, r.ofz);
-        const float tmin = __builtin_fmaxf(__builtin_fmaxf(__builtin_fmaxf(tnx, tny), tnz), 0.0f);
-        const float tmax = __builtin_fminf(__builtin_fminf(tfx, tfy), tfz);
-        const bool hit = (kind != 0u) & (((cmask >> k) & 1u) != 0u) & !(tmin > tmax) & !(tmin > best);
-        inner |= (uint32_t)(hit & (kind == WIDE_INNER)) << k;
-        leaf |= (uint32_t)(hit & (kind != WIDE_INNER)) << k;
-        tk[k] = tmin;
+    for (int k = 0; k < 8; k += 2) {
+        const F2 tnx = pk_fma(pk_fma(f2(byte_f(nx0, nx1, k), byte_f(nx0, nx1, k + 1)), sx2, ox2), ix2, nx2);
+        const F2 tfx = pk_fma(pk_fma(f2(byte_f(fx0, fx1, k), byte_f(fx0, fx1, k + 1)), sx2, ox2), ix2, fx2);
+        const F2 tny = pk_fma(pk_fma(f2(byte_f(ny0, ny1, k), byte_f(ny0, ny1, k + 1)), sy2, oy2), iy2, ny2);
+        const F2 tfy = pk_fma(pk_fma(f2(byte_f(fy0, fy1, k), byte_f(fy0, fy1, k + 1)), sy2, oy2), iy2, fy2);
+        const F2 tnz = pk_fma(pk_fma(f2(byte_f(nz0, nz1, k), byte_f(nz0, nz1, k + 1)), sz2, oz2), iz2, nz2);
+        const F2 tfz = pk_fma(pk_fma(f2(byte_f(fz0, fz1, k), byte_f(fz0, fz1, k + 1)), sz2, oz2), iz2, fz2);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int c = k + h;
+            const uint32_t kind = ((c < 4 ? a4.z : a4.w) >> (8 * (c & 3))) & 0xFFu;
+            const float tmin = __builtin_fmaxf(__builtin_fmaxf(__builtin_fmaxf(tnx[h], tny[h]), tnz[h]), 0.0f);
+            const float tmax = __builtin_fminf(__builtin_fminf(tfx[h], tfy[h]), tfz[h]);
+            const bool hit = (kind != 0u) & (((cmask >> c) & 1u) != 0u) & !(tmin > tmax) & !(tmin > best);
+            inner |= (uint32_t)(hit & (kind == WIDE_INNER)) << c;
+            leaf |= (uint32_t)(hit & (kind != WIDE_INNER)) << c;
+            tk[c] = tmin;
+        }
     }
     // nearest inner child: first of the smallest entry distance
     int nk = -1;
@@ -584,7 +606,7 @@ __device__ int intersect_wide_sched(const DevGeom &g, V3 o, V3 d, float &min_dis
             const uint32_t id = __float_as_uint(r2.y);
             float dist;
             if (id == last ||
-                !intersect_triangle(o, d, v3(r0.x, r0.y, r0.z), v3(r0.w, r1.x, r1.y), v3(r1.z, r1.w, r2.x), dist))
+                !intersect_record(o, d, r0, r1, r2, dist))
                 continue;
             const uint32_t rank = __float_as_uint(r2.z);
             if (!(dist < best || (dist == best && rank < best_rank))) continue;
@@ -595,7 +617,7 @@ __device__ int intersect_wide_sched(const DevGeom &g, V3 o, V3 d, float &min_dis
             if (!intersect_box(noid, inv, lo, hi, bd) || bd > best) continue;   // mesh.h:94-96
             best = dist;
             best_rank = rank;
-            best_id = (int)id;
+            best_id = rec_of(g, r);
         }
     }
     min_distance = best_id == -1 ? -1.0f : best;
@@ -683,7 +705,7 @@ __device__ int intersect_wide_spec(const DevGeom &g, V3 o, V3 d, float &min_dist
             const uint32_t id = __float_as_uint(r2.y);
             float dist;
             if (id == last ||
-                !intersect_triangle(o, d, v3(r0.x, r0.y, r0.z), v3(r0.w, r1.x, r1.y), v3(r1.z, r1.w, r2.x), dist))
+                !intersect_record(o, d, r0, r1, r2, dist))
                 continue;
             const uint32_t rank = __float_as_uint(r2.z);
             if (!(dist < best || (dist == best && rank < best_rank))) continue;
@@ -694,7 +716,7 @@ __device__ int intersect_wide_spec(const DevGeom &g, V3 o, V3 d, float &min_dist
             if (!intersect_box(noid, inv, lo, hi, bd) || bd > best) continue;   // mesh.h:94-96
             best = dist;
             best_rank = rank;
-            best_id = (int)id;
+            best_id = rec_of(g, r);
         }
     }
     min_distance = best_id == -1 ? -1.0f : best;
@@ -832,7 +854,7 @@ __device__ int intersect_group(const DevGeom &g, V3 o, V3 d, float &min_distance
                 const uint32_t id = __float_as_uint(r2.y);
                 float dist;
                 if (id == last ||
-                    !intersect_triangle(o, d, v3(r0.x, r0.y, r0.z), v3(r0.w, r1.x, r1.y), v3(r1.z, r1.w, r2.x), dist))
+                    !intersect_record(o, d, r0, r1, r2, dist))
                     continue;
                 const uint32_t rank = __float_as_uint(r2.z);
                 if (!(dist < lbest || (dist == lbest && rank < lrank))) continue;
@@ -844,7 +866,7 @@ __device__ int intersect_group(const DevGeom &g, V3 o, V3 d, float &min_distance
                 if (!intersect_box(noid, inv, lo, hi, bd) || bd > lbest) continue;   // mesh.h:94-96
                 lbest = dist;
                 lrank = rank;
-                lid = (int)id;
+                lid = rec_of(g, rr);
             }
         }
         unsigned long long lkey = lid == -1 ? NONE : (((unsigned long long)__float_as_uint(lbest) << 32) | lrank);
@@ -975,7 +997,10 @@ __device__ CHR_COLD void wireplanes(const DevGeom &g, const Photon &p, float bes
 // Second half of fill_state (photon.h:272-397): the mesh hit (or an analytic
 // wire plane, FP64) -> material pair, surface, oriented normal and the four
 // interpolated bulk properties; no hit -> NO_HIT.  s.distance holds the mesh
-// hit distance on entry.
+// hit distance on entry.  REC: mesh_triangle is a wide-BVH triangle record
+// (what the wide walks return: triangle id and vertices read from it); else a
+// triangle id of the reference walk (the 48-byte reference records).
+template <bool REC>
 __device__ __forceinline__ void finish_fill(const DevGeom &g, State &s, Photon &p, int mesh_triangle) {
     int m1, m2;
     bool use_analytic = false;
@@ -994,14 +1019,28 @@ __device__ __forceinline__ void finish_fill(const DevGeom &g, State &s, Photon &
         if (a_dot_raw > 0.0f) { m1 = a_outer; m2 = a_inner; s.normal = a_normal_raw; s.inside_to_outside = false; }
         else { m1 = a_inner; m2 = a_outer; s.normal = -a_normal_raw; s.inside_to_outside = true; }
     } else if (mesh_triangle != -1) {
-        p.last_hit = mesh_triangle;
-        const float4 *r = g.tri + 3 * (size_t)mesh_triangle;
-        const float4 r0 = gld(r), r1 = gld(r + 1), r2 = gld(r + 2);
-        const uint32_t code = gld(g.material_codes + mesh_triangle);
+        V3 e1, e3;   // v1 - v0, v2 - v1 (photon.h:365-367)
+        int tid;
+        if constexpr (REC) {
+            const float4 *r = g.wtri + 4 * (size_t)mesh_triangle;
+            const float4 r0 = gld(r), r1 = gld(r + 1), r2 = gld(r + 2);
+            const V3 v0 = v3(r0.x, r0.y, r0.z), v1 = v3(r0.w, r1.x, r1.y), v2 = v3(r1.z, r1.w, r2.x);
+            e1 = v1 - v0;
+            e3 = v2 - v1;
+            tid = (int)__float_as_uint(r2.y);
+        } else {
+            const float4 *r = g.tri + 3 * (size_t)mesh_triangle;
+            const float4 r0 = gld(r), r1 = gld(r + 1), r2 = gld(r + 2);
+            e1 = v3(r0.w, r1.x, r1.y);
+            e3 = v3(r2.y, r2.z, r2.w);
+            tid = mesh_triangle;
+        }
+        p.last_hit = tid;
+        const uint32_t code = gld(g.material_codes + tid);
         const int inner = convert(0xFF & (int)(code >> 24));
         const int outer = convert(0xFF & (int)(code >> 16));
         s.surface_index = convert(0xFF & (int)(code >> 8));
-        s.normal = normalize(cross(v3(r0.w, r1.x, r1.y), v3(r2.y, r2.z, r2.w)));
+        s.normal = normalize(cross(e1, e3));
         if (dot(s.normal, -p.dir) > 0.0f) { m1 = outer; m2 = inner; s.inside_to_outside = false; }
         else { m1 = inner; m2 = outer; s.normal = -s.normal; s.inside_to_outside = true; }
     } else {
@@ -1033,7 +1072,7 @@ __device__ __forceinline__ void fill_state(const DevGeom &g, State &s, Photon &p
         mesh_triangle =
             intersect_wide_sched<COUNT, WIDE - 1000>(g, p.pos, p.dir, s.distance, p.last_hit, wst, overflow, cnt);
     else mesh_triangle = intersect_mesh<BATCH>(g, p.pos, p.dir, s.distance, p.last_hit, st, overflow);
-    finish_fill(g, s, p, mesh_triangle);
+    finish_fill<(WIDE != 0)>(g, s, p, mesh_triangle);
 }
 
 // photon.h:399-427
@@ -1484,6 +1523,7 @@ struct PropagateArgs {
     // and the launch runs only if *mode == want
     const uint32_t *dev_n;
     const uint32_t *mode;
+    uint32_t prio;                     // tail kernel: raise its waves' issue priority (s_setprio)
     uint32_t want;
 };
 // modes of a device-driven step slot (step_head_kernel)
@@ -1748,12 +1788,12 @@ __global__ __launch_bounds__(BLOCK, MINW) void shade_kernel(const DevGeom *__res
                 s.distance = __int_as_float(cur.hit.y);
                 if (tri == FLAT_HIT) {            // (distance bits, reference rank) of a decomposed walk
                     const unsigned long long key = a.flat_best[cur.hit.y];
-                    tri = key == ~0ull ? -1 : (int)g.wrank_id[(uint32_t)key];
+                    tri = key == ~0ull ? -1 : (int)g.wrank_rec[(uint32_t)key];
                     s.distance = key == ~0ull ? -1.0f : __uint_as_float((uint32_t)(key >> 32));
                 }
                 pf.tick(P_FILL);
                 pf.call(P_FILL);
-                finish_fill(g, s, p, tri);
+                finish_fill<true>(g, s, p, tri);
                 pf.tick(P_PHYS);
                 if (p.last_hit != -1) {
                     pf.call(P_PHYS);
@@ -2042,7 +2082,7 @@ __device__ int walk_segment(const DevGeom &g, bool act, V3 o, V3 d, uint32_t las
             const uint32_t id = __float_as_uint(r2.y);
             float dist;
             if (id == last ||
-                !intersect_triangle(o, d, v3(r0.x, r0.y, r0.z), v3(r0.w, r1.x, r1.y), v3(r1.z, r1.w, r2.x), dist))
+                !intersect_record(o, d, r0, r1, r2, dist))
                 continue;
             const uint32_t rank = __float_as_uint(r2.z);
             if (!(dist < lbest || (dist == lbest && rank < lrank))) continue;
@@ -2052,7 +2092,7 @@ __device__ int walk_segment(const DevGeom &g, bool act, V3 o, V3 d, uint32_t las
             if (!intersect_box(noid, inv, lo, hi, bd) || bd > lbest) continue;   // mesh.h:94-96
             lbest = dist;
             lrank = rank;
-            lid = (int)id;
+            lid = rec_of(g, rr);
         }
         __builtin_amdgcn_wave_barrier();   // list reads land before the next iteration's writes
         // segment min over (distance, rank): usually no lane or one lane has a hit
@@ -2091,6 +2131,9 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_tail_kernel(const DevGe
     const uint32_t tid = blockIdx.x * BLOCK + threadIdx.x;
     const uint32_t lane = __lane_id();
     if (a.mode && *a.mode != a.want) return;
+    // a tail overlapped by the next batch (chr_propagate_batches) is the critical
+    // path: its waves win the SIMD's issue arbitration over that batch's walk
+    if (a.prio) __builtin_amdgcn_s_setprio(3);
     const uint32_t slot = tid / 8, sub = tid & 7u;
     const uint32_t n = a.dev_n ? *a.dev_n - 1u : (uint32_t)a.nthreads;
     const uint32_t nslot = cap < n ? cap : n;
@@ -2220,7 +2263,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_tail_kernel(const DevGe
                 if (!(chr_isfinite(inv.x) && chr_isfinite(inv.y) && chr_isfinite(inv.z))) flat++;
             }
             s.distance = dist;
-            finish_fill(g, s, p, tri);
+            finish_fill<true>(g, s, p, tri);
             bool stop = p.last_hit == -1;
             if (!stop) {
                 int command = propagate_to_boundary(g, p, s, rng, a.use_weights, scatter_first);
@@ -2249,6 +2292,21 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_tail_kernel(const DevGe
     prof_add(CHR_PROF_TAIL_OTHER, 0ull, pf.cyc[P_OTHER]);
     prof_add(CHR_PROF_TAIL_KERNEL, 1ull, pf.total());
 #endif
+}
+
+// The reference walk's 48-byte triangle records (v0, e1 = v1-v0, e2 = v2-v0,
+// e3 = v2-v1; device_geometry.h) from the wide records, which hold every
+// triangle once with its float vertices (chr::geometry_ref_nodes, first use).
+__global__ __launch_bounds__(BLOCK) void ref_triangles_kernel(const float4 *wtri, uint32_t nwtri, float4 *tri) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= nwtri) return;
+    const float4 r0 = wtri[4 * (size_t)i], r1 = wtri[4 * (size_t)i + 1], r2 = wtri[4 * (size_t)i + 2];
+    const V3 v0 = v3(r0.x, r0.y, r0.z), v1 = v3(r0.w, r1.x, r1.y), v2 = v3(r1.z, r1.w, r2.x);
+    const V3 e1 = v1 - v0, e2 = v2 - v0, e3 = v2 - v1;
+    float4 *o = tri + 3 * (size_t)__float_as_uint(r2.y);
+    o[0] = make_float4(v0.x, v0.y, v0.z, e1.x);
+    o[1] = make_float4(e1.y, e1.z, e2.x, e2.y);
+    o[2] = make_float4(e2.z, e3.x, e3.y, e3.z);
 }
 
 // ---------------------------------------------------------------- ray binning (trace order)
@@ -2544,7 +2602,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
             const uint32_t id = __float_as_uint(r2.y);
             float dist;
             if (id == last ||
-                !intersect_triangle(o, d, v3(r0.x, r0.y, r0.z), v3(r0.w, r1.x, r1.y), v3(r1.z, r1.w, r2.x), dist))
+                !intersect_record(o, d, r0, r1, r2, dist))
                 continue;
             const uint32_t rank = __float_as_uint(r2.z);
             if (!(dist < best || (dist == best && rank < best_rank))) continue;
@@ -2555,7 +2613,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
             if (!intersect_box_slab(slab, lo, hi, bd) || bd > best) continue;   // mesh.h:94-96
             best = dist;
             best_rank = rank;
-            best_id = (int)id;
+            best_id = rec_of(g, r);
         }
     }
     if constexpr (!COUNT) {
@@ -2987,13 +3045,14 @@ struct Scratch {
     int device = -1;
 };
 
-// ctx: which of a thread's two propagate contexts (chr_propagate_batches
-// alternates them so one batch's tail can run while the next batch starts)
+// ctx: which of a thread's NCTX propagate buffer contexts (chr_propagate_batches
+// rotates them so batches can overlap: a tail, the next batches' first steps)
+constexpr int NCTX = 3;
 int scratch_get(size_t bytes, void **out, int ctx = 0) {
-    static thread_local Scratch s[2][16];
+    static thread_local Scratch s[NCTX][16];
     int dev = 0;
     CHR_HIP_CHECK(hipGetDevice(&dev));
-    Scratch &x = s[ctx & 1][dev & 15];
+    Scratch &x = s[ctx % NCTX][dev & 15];
     if (x.bytes < bytes) {
         if (x.ptr) CHR_HIP_CHECK(hipFree(x.ptr));
         x.ptr = nullptr;
@@ -3006,11 +3065,11 @@ int scratch_get(size_t bytes, void **out, int ctx = 0) {
 
 // HBM column for the deep walk-stack entries of the persistent trace grid
 // (per thread and device, grown on demand; see trace_kernel)
-int walk_stack_get(size_t bytes, uint2 **out) {
-    static thread_local Scratch s[16];
+int walk_stack_get(size_t bytes, uint2 **out, int ctx = 0) {
+    static thread_local Scratch s[NCTX][16];
     int dev = 0;
     CHR_HIP_CHECK(hipGetDevice(&dev));
-    Scratch &x = s[dev & 15];
+    Scratch &x = s[ctx % NCTX][dev & 15];
     if (x.bytes < bytes) {
         if (x.ptr) CHR_HIP_CHECK(hipFree(x.ptr));
         x.ptr = nullptr;
@@ -3022,6 +3081,15 @@ int walk_stack_get(size_t bytes, uint2 **out) {
 }
 
 }  // namespace
+
+int chr::build_ref_triangles(const DevGeom &dg, float4 *tri) {
+    if (!dg.wtri || !dg.nwtri) return chr::fail(CHR_ERR_INVALID, "build_ref_triangles: no wide triangle records");
+    CHR_HIP_CHECK(hipMemset(tri, 0, (size_t)dg.ntriangles * 48));
+    hipLaunchKernelGGL(ref_triangles_kernel, dim3(grid_for(dg.nwtri)), dim3(BLOCK), 0, 0, dg.wtri, dg.nwtri, tri);
+    CHR_HIP_CHECK(hipGetLastError());
+    CHR_HIP_CHECK(hipDeviceSynchronize());
+    return CHR_OK;
+}
 
 extern "C" int chr_init_rng_subseq(uint32_t *d_states, uint32_t nslots, uint64_t seed, uint64_t first_subsequence,
                                    uint64_t offset, void *stream) {
@@ -3113,6 +3181,11 @@ static uint32_t trace_drain_max() {
     const char *e = getenv("CHR_TRACE_DRAIN");
     const int k = e ? atoi(e) : 8;
     return (uint32_t)(k < 0 ? 0 : (k > 8 ? 8 : k));
+}
+// CHR_TAIL_PRIO=0: the batches' overlapped tail kernel at normal wave priority (A/B)
+static bool tail_prio() {
+    const char *e = getenv("CHR_TAIL_PRIO");
+    return !(e && e[0] == '0');
 }
 static bool wide_queue_ok(const chr_geometry *g) { return g->dev.nwtri < (1u << 30); }   // 30-bit leaf queue entries
 
@@ -3218,6 +3291,7 @@ static int launch_chunk(const chr_geometry *g, const chr_photons *ph, uint32_t *
     a.dev_n = nullptr;
     a.mode = nullptr;
     a.want = STEP_ONE;
+    a.prio = 0;
     if (sort_enabled() && nthreads >= kSortMin) {
         // coherence order (sort_key_kernel): rays that start close together in
         // similar directions share a wave
@@ -3272,10 +3346,10 @@ struct FlatCtx {
     bool enrol_next;
 };
 static int flat_get(uint32_t n, FlatCtx &fc, int ctx = 0) {
-    static thread_local Scratch s[2][16];
+    static thread_local Scratch s[NCTX][16];
     int dev = 0;
     CHR_HIP_CHECK(hipGetDevice(&dev));
-    Scratch &x = s[ctx & 1][dev & 15];
+    Scratch &x = s[ctx % NCTX][dev & 15];
     const size_t bytes = 256 + (size_t)n * 12 + 64;
     if (x.bytes < bytes) {
         if (x.ptr) CHR_HIP_CHECK(hipFree(x.ptr));
@@ -3312,7 +3386,15 @@ struct SlotCtl {
     unsigned long long *tail_masks = nullptr;
     hipEvent_t evt_tail0 = nullptr, evt_tail1 = nullptr;   // around the tail kernel, on tail_stream
     hipEvent_t rng_ready = nullptr;   // the previous batch's tail done: the first RNG use waits for it
+    // chr_propagate_batches runs a batch's first slot in two parts: PHASE_PREFIX
+    // (head, flat-walk classification, binning, the BVH walk: no random numbers)
+    // on the prefix stream, ending with prefix_done; PHASE_REST (shade pass on)
+    // on the batch stream after prefix_done, starting with ev_rest0
+    int phase = 0;
+    int ctx = 0;                      // buffer context (walk-stack column)
+    hipEvent_t prefix_done = nullptr, ev_rest0 = nullptr;
 };
+constexpr int PHASE_ALL = 0, PHASE_PREFIX = 1, PHASE_REST = 2;
 
 // hits: n (triangle, distance) slots + a ray counter word, for the split path
 static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *rng, uint32_t nslots, uint32_t cap,
@@ -3342,6 +3424,7 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
     a.dev_n = dev_n;
     a.mode = mode;
     a.want = STEP_ONE;
+    a.prio = 0;
     FlatEnrol fe{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
     const uint32_t threads = std::min(cap, (n + 63u) & ~63u);
     const StepVariant sv = select_step_variant(g);
@@ -3352,8 +3435,15 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
     // the first step's length and mode are known on the host (binning, flat-walk enrolment)
     const bool first_one_step = first_step && (!sc || !((n < sc->tail_below || use_weights) && sc->remaining > 1));
     uint32_t *next = split ? (uint32_t *)(hits + (sc ? sc->n_layout : n)) : nullptr;
-    if (ev0) CHR_HIP_CHECK(hipEventRecord(ev0, stream));
-    if (sc) {
+    const bool pre = !sc || sc->phase != PHASE_REST, rest = !sc || sc->phase != PHASE_PREFIX;
+    if (sc && sc->phase != PHASE_ALL && (!split || !sc->prefix_done))
+        return chr::fail(CHR_ERR_INVALID, "launch_step: a split slot needs the split path and its prefix event");
+    if (ev0 && pre) CHR_HIP_CHECK(hipEventRecord(ev0, stream));
+    if (!pre) {
+        CHR_HIP_CHECK(hipStreamWaitEvent(stream, sc->prefix_done, 0));
+        if (sc->ev_rest0) CHR_HIP_CHECK(hipEventRecord(sc->ev_rest0, stream));
+    }
+    if (sc && pre) {
         if (!next) return chr::fail(CHR_ERR_INVALID, "launch_step: device-driven steps need the split path");
         hipLaunchKernelGGL(step_head_kernel, dim3(1), dim3(64), 0, stream, in_queue - 1, out_queue, sc->mode, sc->nk,
                            sc->done, next, sc->tail_below, sc->remaining, use_weights, sc->n_layout);
@@ -3362,7 +3452,7 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
     }
     if (split) {
         uint32_t *count_cur = fc->ctl + 1 + fc->cur, *count_next = fc->ctl + 1 + (fc->cur ^ 1);
-        if (first_one_step)   // flat walks of the initial queue (later steps: enrolled by the previous scatter)
+        if (first_one_step && pre)   // flat walks of the initial queue (later steps: enrolled by the previous scatter)
             hipLaunchKernelGGL(classify_kernel, dim3(grid_for(n)), dim3(BLOCK), 0, stream, ph->d_pos, ph->d_dir,
                                ph->d_flags, in_queue, n, hits, fc->flat_q, count_cur, fc->flat_best);
         TraceArgs ta;
@@ -3377,7 +3467,7 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
         a.zero_word = count_next;   // cleared by the shade pass, filled by this step's scatter
         if (fc->enrol_next)
             fe = FlatEnrol{ph->d_pos, ph->d_dir, hits, fc->flat_q, count_next, fc->flat_best};
-        if (trace_steps()) {   // debugging: per-walk cost histogram (counting variants), printed per step
+        if (trace_steps() && pre) {   // debugging: per-walk cost histogram (counting variants), printed per step
             ta.walk_hist = next + 16 + 2 * (size_t)(sc ? sc->n_layout : n);
             CHR_HIP_CHECK(hipMemsetAsync(ta.walk_hist, 0, 34 * 4, stream));
         }
@@ -3385,7 +3475,7 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
             // 16-bit radix sort of (direction cell, queue position); hits region:
             // [hits n x int2][next + pad, 16 words][keys n][values n][walk hist 64 words]
             // (device-driven slots bin only the first step, whose length the host knows)
-            if (!sc || first_one_step) {
+            if ((!sc || first_one_step) && pre) {
                 uint32_t *keys = next + 16, *order = keys + n;
                 hipLaunchKernelGGL(bin_key_kernel, dim3(grid_for(n)), dim3(BLOCK), 0, stream, ph->d_dir, in_queue, n,
                                    keys, order);
@@ -3397,14 +3487,22 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
                 ta.order = vals_out;
             }
         }
-        const int cus = device_cus();
-        if (cus <= 0) return chr::fail(CHR_ERR_HIP, "launch_step: no compute units");
-        const uint64_t resident = (uint64_t)cus * 4 * sv.trace_waves * 64 / BLOCK;   // persistent grid
-        const uint32_t blocks = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(resident, grid_for(n)));
-        if (int rc = walk_stack_get((size_t)WIDE_STACK * blocks * BLOCK * sizeof(uint2), &ta.spill)) return rc;
-        if (evt0) CHR_HIP_CHECK(hipEventRecord(evt0, stream));
-        hipLaunchKernelGGL(sv.trace, dim3(blocks), dim3(BLOCK), 0, stream, (const DevGeom *)g->d_dev, ta);
-        if (evt1) CHR_HIP_CHECK(hipEventRecord(evt1, stream));
+        if (pre) {
+            const int cus = device_cus();
+            if (cus <= 0) return chr::fail(CHR_ERR_HIP, "launch_step: no compute units");
+            const uint64_t resident = (uint64_t)cus * 4 * sv.trace_waves * 64 / BLOCK;   // persistent grid
+            const uint32_t blocks = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(resident, grid_for(n)));
+            if (int rc = walk_stack_get((size_t)WIDE_STACK * blocks * BLOCK * sizeof(uint2), &ta.spill, sc ? sc->ctx : 0))
+                return rc;
+            if (evt0) CHR_HIP_CHECK(hipEventRecord(evt0, stream));
+            hipLaunchKernelGGL(sv.trace, dim3(blocks), dim3(BLOCK), 0, stream, (const DevGeom *)g->d_dev, ta);
+            if (evt1) CHR_HIP_CHECK(hipEventRecord(evt1, stream));
+        }
+        if (!rest) {
+            CHR_HIP_CHECK(hipEventRecord(sc->prefix_done, stream));
+            CHR_HIP_CHECK(hipGetLastError());
+            return CHR_OK;
+        }
         a.hits = hits;
         a.max_steps = 1;
         if (sc && sc->rng_ready) CHR_HIP_CHECK(hipStreamWaitEvent(stream, sc->rng_ready, 0));
@@ -3420,6 +3518,7 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
         hipLaunchKernelGGL(clear_masks_kernel, dim3(std::min<uint32_t>(1024u, grid_for(nwords))), dim3(BLOCK), 0, ts,
                            sc->tail_masks, dev_n, mode);
         PropagateArgs at = a;
+        at.prio = tail_prio() ? 1u : 0u;
         at.alive_masks = sc->tail_masks;
         at.max_steps = sc->remaining;
         at.want = STEP_TAIL;
@@ -3526,10 +3625,10 @@ static bool host_steps_forced() {     // CHR_HOST_STEPS=1: read the survivor cou
 // per-slot control words of a device-driven propagate: [2k] mode, [2k + 1]
 // queue length of slot k, then the done flag (per thread and device, grown on demand)
 static int slot_ctl_get(size_t words, uint32_t **out, int ctx = 0) {
-    static thread_local Scratch s[2][16];
+    static thread_local Scratch s[NCTX][16];
     int dev = 0;
     CHR_HIP_CHECK(hipGetDevice(&dev));
-    Scratch &x = s[ctx & 1][dev & 15];
+    Scratch &x = s[ctx % NCTX][dev & 15];
     if (x.bytes < words * 4) {
         if (x.ptr) CHR_HIP_CHECK(hipFree(x.ptr));
         x.ptr = nullptr;
@@ -3543,8 +3642,9 @@ static int slot_ctl_get(size_t words, uint32_t **out, int ctx = 0) {
 // per-slot events of a device-driven propagate: [0] slot start, [1] its
 // one-step kernels done (with the tail when that runs on the same stream),
 // [2,3] around trace_kernel, [4] slot done (ring copied), [5,6] around the tail
-// kernel when it runs on the tail stream (chr_propagate_batches)
-constexpr int SLOT_EVENTS = 7;
+// kernel when it runs on the tail stream, [7] start of the rest of a slot whose
+// prefix ran on the prefix stream (chr_propagate_batches)
+constexpr int SLOT_EVENTS = 8;
 
 // Device buffers of one propagate (context ctx of the calling thread):
 // queues, step scratch, the split path's hits / binning region, the flat-walk
@@ -3599,38 +3699,61 @@ static int prop_start(const PropBufs &b, uint32_t nphotons, uint32_t true_nphoto
     return CHR_OK;
 }
 
+// grow a slot event list to n events
+static int grow_events(std::vector<hipEvent_t> &v, size_t n) {
+    while (v.size() < n) {
+        hipEvent_t e;
+        CHR_HIP_CHECK(hipEventCreate(&e));
+        v.push_back(e);
+    }
+    return CHR_OK;
+}
+
+// How device_slots runs a propagate besides its buffers.
+struct SlotRun {
+    std::vector<hipEvent_t> *events = nullptr;   // SLOT_EVENTS per slot (grown here)
+    hipStream_t tstream = nullptr;     // tail kernels go there (chr_propagate_batches; nullptr: on the stream)
+    hipEvent_t rng_ready = nullptr;    // the first RNG use waits for it
+    hipEvent_t prefix_done = nullptr;  // slot 0's prefix was queued by queue_prefix and ends with this event
+    int ctx = 0;
+};
+
 // Device-driven steps: every slot's kernels read the queue length from the
 // queue header and the head kernel applies the nsteps policy, so the host
 // queues slot k + 1 while slot k runs and only waits (on slot k - 1's event,
 // already done by then) to learn when the tail has run -- no survivor-count
-// round trip between steps.  Same launches, same results.  tstream: the tail
-// kernels go there (chr_propagate_batches); rng_ready: the first RNG use waits
-// for it.  *k_out = slots queued, *ctl_out = their [mode, length] words.
+// round trip between steps.  Same launches, same results.  *k_out = slots
+// queued, *ctl_out = their [mode, length] words.
 static int device_slots(const chr_geometry *g, const chr_photons *ph, uint32_t nphotons, uint32_t *rng, uint32_t nslots,
                         int32_t ntpb, int32_t max_steps, int32_t use_weights, int32_t scatter_first, PropBufs &b,
-                        int ctx, hipStream_t stream, hipStream_t tstream, hipEvent_t rng_ready, uint32_t **ctl_out,
-                        int *k_out) {
+                        const SlotRun &run, hipStream_t stream, uint32_t **ctl_out, int *k_out) {
     const uint32_t tail_below = (uint32_t)ntpb * 16 * 8;   // photon.py:261-264
     uint32_t *ctl = nullptr;
-    int rc = slot_ctl_get(2 * (size_t)max_steps + 8, &ctl, ctx);
+    int rc = slot_ctl_get(2 * (size_t)max_steps + 8, &ctl, run.ctx);
     if (rc) return rc;
     uint32_t *done = ctl + 2 * (size_t)max_steps;
-    CHR_HIP_CHECK(hipMemsetAsync(done, 0, 4, stream));
+    if (!run.prefix_done) CHR_HIP_CHECK(hipMemsetAsync(done, 0, 4, stream));
     b.fc.enrol_next = true;
     uint32_t *ring = b.pinned + 64;   // (mode, n) of recent slots, 32 entries (copied after each slot)
-    std::vector<hipEvent_t> *evp = nullptr;
+    std::vector<hipEvent_t> &events = *run.events;
     uint32_t n_ub = nphotons;
     int k = 0, cur = 0;
     bool stop = false;
     while (k < max_steps && !stop) {
-        if ((rc = timing_events(SLOT_EVENTS * (size_t)(k + 1), &evp, ctx))) return rc;
-        hipEvent_t *ev = evp->data() + SLOT_EVENTS * (size_t)k;
+        if ((rc = grow_events(events, SLOT_EVENTS * (size_t)(k + 1)))) return rc;
+        hipEvent_t *ev = events.data() + SLOT_EVENTS * (size_t)k;
         SlotCtl sc{ctl + 2 * (size_t)k, ctl + 2 * (size_t)k + 1, done, nphotons, max_steps - k, tail_below};
-        sc.tail_stream = tstream;
+        sc.tail_stream = run.tstream;
         sc.tail_masks = b.tail_masks;
         sc.evt_tail0 = ev[5];
         sc.evt_tail1 = ev[6];
-        sc.rng_ready = k == 0 ? rng_ready : nullptr;
+        sc.rng_ready = k == 0 ? run.rng_ready : nullptr;
+        sc.ctx = run.ctx;
+        if (k == 0 && run.prefix_done) {
+            sc.phase = PHASE_REST;
+            sc.prefix_done = run.prefix_done;
+            sc.ev_rest0 = ev[7];
+        }
         bool split = false;
         rc = launch_step(g, ph, rng, nslots, (uint32_t)b.cap, n_ub, b.q[cur] + 1, b.q[cur ^ 1], 1, use_weights,
                          scatter_first, b.scratch, stream, ev[0], ev[1], b.hits, b.sort_space, k == 0, ev[2], ev[3],
@@ -3642,7 +3765,7 @@ static int device_slots(const chr_geometry *g, const chr_photons *ph, uint32_t n
         cur ^= 1;
         scatter_first = 0;
         if (k >= 1) {   // slot k - 1 finished before slot k started: is there a slot k + 1?
-            CHR_HIP_CHECK(hipEventSynchronize((*evp)[SLOT_EVENTS * (size_t)(k - 1) + 4]));
+            CHR_HIP_CHECK(hipEventSynchronize(events[SLOT_EVENTS * (size_t)(k - 1) + 4]));
             const uint32_t m = ring[2 * ((k - 1) % 32)], nk = ring[2 * ((k - 1) % 32) + 1];
             if (m != STEP_ONE) stop = true;   // the tail ran or the queue emptied: slot k is idle
             else n_ub = nk;                   // later queues are no longer
@@ -3654,14 +3777,22 @@ static int device_slots(const chr_geometry *g, const chr_photons *ph, uint32_t n
     return CHR_OK;
 }
 
-// per-slot statistics of a finished device-driven propagate (h: [mode, length] per slot)
+// per-slot statistics of a finished device-driven propagate (h: [mode, length]
+// per slot); prefixed: slot 0 ran as prefix + rest (chr_propagate_batches)
 static int slot_stats(chr_propagate_stats &st, const uint32_t *h, int k, const std::vector<hipEvent_t> &events,
-                      bool tail_stream) {
+                      bool tail_stream, bool prefixed = false) {
     for (int j = 0; j < k; ++j) {
         const uint32_t m = h[2 * j], nj = h[2 * j + 1];
         const hipEvent_t *ev = events.data() + SLOT_EVENTS * (size_t)j;
         float ms = 0.0f;
-        CHR_HIP_CHECK(hipEventElapsedTime(&ms, ev[0], ev[1]));
+        if (j == 0 && prefixed) {   // the prefix on its stream, the rest after it on the batch stream
+            float ms2 = 0.0f;
+            CHR_HIP_CHECK(hipEventElapsedTime(&ms, ev[0], ev[3]));
+            CHR_HIP_CHECK(hipEventElapsedTime(&ms2, ev[7], ev[1]));
+            ms += ms2;
+        } else {
+            CHR_HIP_CHECK(hipEventElapsedTime(&ms, ev[0], ev[1]));
+        }
         st.kernel_ms += ms;
         if (m == STEP_IDLE) continue;
         st.launches++;
@@ -3800,8 +3931,10 @@ extern "C" int chr_propagate(const chr_geometry *g, const chr_photons *ph, uint3
     if (device_steps) {
         uint32_t *ctl = nullptr;
         int k = 0;
+        SlotRun run;
+        if ((rc = timing_events(0, &run.events))) return rc;
         if ((rc = device_slots(g, ph, nphotons, d_rng_states, rng_nslots, ntpb, max_steps, use_weights, scatter_first,
-                               b, 0, stream, nullptr, nullptr, &ctl, &k)))
+                               b, run, stream, &ctl, &k)))
             return rc;
         CHR_HIP_CHECK(hipStreamSynchronize(stream));
         st.host_syncs = 1;
@@ -3891,38 +4024,53 @@ extern "C" int chr_propagate(const chr_geometry *g, const chr_photons *ph, uint3
     return CHR_OK;
 }
 
-// the stream the tails of chr_propagate_batches run on (per thread and device;
-// non-blocking: no implicit ordering with the legacy default stream)
-static int tail_stream_get(hipStream_t *out, hipEvent_t done[2]) {
-    struct TS { hipStream_t s = nullptr; hipEvent_t done[2] = {nullptr, nullptr}; };
-    static thread_local TS ts[16];
+// the streams of chr_propagate_batches (per thread and device; non-blocking:
+// no implicit ordering with the legacy default stream): tails, and the
+// prefixes (first-step queueing, binning and walk) of the batches ahead
+static int batch_streams_get(hipStream_t *tail, hipStream_t *prefix) {
+    static thread_local hipStream_t ts[16][2] = {};
     int dev = 0;
     CHR_HIP_CHECK(hipGetDevice(&dev));
-    TS &t = ts[dev & 15];
-    if (!t.s) {
-        CHR_HIP_CHECK(hipStreamCreateWithFlags(&t.s, hipStreamNonBlocking));
-        for (int i = 0; i < 2; ++i) CHR_HIP_CHECK(hipEventCreateWithFlags(&t.done[i], hipEventDisableTiming));
+    hipStream_t *s = ts[dev & 15];
+    if (!s[0]) {   // the tails are the critical path: the highest stream priority
+        int least = 0, greatest = 0;
+        CHR_HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+        CHR_HIP_CHECK(hipStreamCreateWithPriority(&s[0], hipStreamNonBlocking, greatest));
+        CHR_HIP_CHECK(hipStreamCreateWithPriority(&s[1], hipStreamNonBlocking, least));
     }
-    *out = t.s;
-    done[0] = t.done[0];
-    done[1] = t.done[1];
+    *tail = s[0];
+    *prefix = s[1];
     return CHR_OK;
 }
 
-// pinned host copy of a batch's slot control words (per thread, device and context)
-static int pinned_ctl_get(size_t words, uint32_t **out, int ctx) {
-    struct P { uint32_t *p = nullptr; size_t words = 0; };
-    static thread_local P ps[2][16];
+// Host-side resources of one batch of a chr_propagate_batches call: its slot
+// events, its prefix / done events, pinned words ([0..63] counters read back,
+// [64..127] the slot ring, [128..] the slot control words).  Per thread and
+// device, reused across calls (every call drains before it returns).
+struct BatchHost {
+    std::vector<hipEvent_t> ev;
+    hipEvent_t prefix_done = nullptr, done = nullptr;
+    uint32_t *pinned = nullptr;
+    size_t words = 0;
+};
+static int batch_host_get(size_t nb, size_t words, std::vector<BatchHost> **out) {
+    static thread_local std::vector<BatchHost> pool[16];
     int dev = 0;
     CHR_HIP_CHECK(hipGetDevice(&dev));
-    P &x = ps[ctx & 1][dev & 15];
-    if (x.words < words) {
-        if (x.p) CHR_HIP_CHECK(hipHostFree(x.p));
-        x.p = nullptr;
-        CHR_HIP_CHECK(hipHostMalloc((void **)&x.p, words * 4, hipHostMallocDefault));
-        x.words = words;
+    std::vector<BatchHost> &v = pool[dev & 15];
+    if (v.size() < nb) v.resize(nb);
+    for (size_t i = 0; i < nb; ++i) {
+        BatchHost &b = v[i];
+        if (!b.prefix_done) CHR_HIP_CHECK(hipEventCreateWithFlags(&b.prefix_done, hipEventDisableTiming));
+        if (!b.done) CHR_HIP_CHECK(hipEventCreateWithFlags(&b.done, hipEventDisableTiming));
+        if (b.words < words) {
+            if (b.pinned) CHR_HIP_CHECK(hipHostFree(b.pinned));
+            b.pinned = nullptr;
+            CHR_HIP_CHECK(hipHostMalloc((void **)&b.pinned, words * 4, hipHostMallocDefault));
+            b.words = words;
+        }
     }
-    *out = x.p;
+    *out = &v;
     return CHR_OK;
 }
 
@@ -3930,7 +4078,7 @@ static bool ranges_overlap(const void *a, size_t na, const void *b, size_t nb) {
     const uintptr_t x = (uintptr_t)a, y = (uintptr_t)b;
     return a && b && x < y + nb && y < x + na;
 }
-// whether two batches share any photon array (then the later one waits for the earlier one's tail)
+// whether two batches share any photon array (then the later one waits for the earlier one)
 static bool photons_alias(const chr_photons *a, uint32_t na, const chr_photons *b, uint32_t nb) {
     const void *pa[9] = {a->d_pos, a->d_dir, a->d_pol, a->d_wavelengths, a->d_t, a->d_weights, a->d_flags,
                          a->d_last_hit_triangles, a->d_evidx};
@@ -3941,6 +4089,41 @@ static bool photons_alias(const chr_photons *a, uint32_t na, const chr_photons *
         for (int j = 0; j < 9; ++j)
             if (ranges_overlap(pa[i], w[i] * na, pb[j], w[j] * nb)) return true;
     return false;
+}
+
+// CHR_BATCH_LOOKAHEAD=k (0..NCTX-1, default 0): prefixes queued for the k
+// batches after the running one as well.  Measured on the 29k bench (r02,
+// profiles/r02/ab_lookahead): 0 416.8, 1 417.3, 2 378.2 M photons/s -- a second
+// batch's walk queued early competes with the running batch's walks (two
+// persistent grids, twice the node working set) and the step loses the overlap.
+static size_t batch_lookahead() {
+    const char *e = getenv("CHR_BATCH_LOOKAHEAD");
+    const int k = e ? atoi(e) : 0;
+    return (size_t)(k < 0 ? 0 : (k > NCTX - 1 ? NCTX - 1 : k));
+}
+
+// The RNG-free part of a propagate's first slot on stream ps: queues, counters,
+// the head kernel, flat-walk classification, direction binning and the BVH
+// walk (launch_step PHASE_PREFIX), ending with prefix_done.
+static int queue_prefix(const chr_geometry *g, const chr_photons *ph, uint32_t nphotons, uint32_t true_nphotons,
+                        uint32_t ncopies, uint32_t *rng, uint32_t nslots, int32_t ntpb, int32_t max_steps,
+                        int32_t use_weights, int32_t scatter_first, PropBufs &b, int ctx,
+                        std::vector<hipEvent_t> &events, hipEvent_t prefix_done, hipStream_t ps) {
+    CHR_TRY(prop_start(b, nphotons, true_nphotons, ncopies, ps));
+    uint32_t *ctl = nullptr;
+    CHR_TRY(slot_ctl_get(2 * (size_t)max_steps + 8, &ctl, ctx));
+    uint32_t *done = ctl + 2 * (size_t)max_steps;
+    CHR_HIP_CHECK(hipMemsetAsync(done, 0, 4, ps));
+    b.fc.enrol_next = true;
+    CHR_TRY(grow_events(events, SLOT_EVENTS));
+    SlotCtl sc{ctl, ctl + 1, done, nphotons, max_steps, (uint32_t)ntpb * 16 * 8};
+    sc.phase = PHASE_PREFIX;
+    sc.ctx = ctx;
+    sc.prefix_done = prefix_done;
+    hipEvent_t *ev = events.data();
+    return launch_step(g, ph, rng, nslots, (uint32_t)b.cap, nphotons, b.q[0] + 1, b.q[1], 1, use_weights,
+                       scatter_first, b.scratch, ps, ev[0], ev[1], b.hits, b.sort_space, true, ev[2], ev[3], nullptr,
+                       &b.fc, &sc);
 }
 
 extern "C" int chr_propagate_batches(const chr_geometry *g, const chr_photons *phs, const uint32_t *nphotons,
@@ -3954,79 +4137,111 @@ extern "C" int chr_propagate_batches(const chr_geometry *g, const chr_photons *p
         CHR_TRY(check_propagate_args("chr_propagate_batches", g, phs + i, nphotons[i], true_nphotons[i], ncopies[i],
                                      d_rng_states, rng_nslots, ntpb, max_blocks));
     hipStream_t stream = (hipStream_t)vstream;
-    if (nbatch == 0) return CHR_OK;
+    if (stats)
+        for (uint32_t i = 0; i < nbatch; ++i) stats[i] = chr_propagate_stats{};
+    // the non-empty batches, in order
+    std::vector<uint32_t> idx;
+    uint32_t max_n = 0;
+    for (uint32_t i = 0; i < nbatch; ++i)
+        if (nphotons[i]) { idx.push_back(i); max_n = std::max(max_n, nphotons[i]); }
+    if (idx.empty()) return CHR_OK;
     if (walks_reference_bvh(g)) CHR_TRY(chr::geometry_ref_nodes(g));
     if (int lrc = apply_node_layout(g, stream)) return lrc;
     PropBufs probe;
     probe.cap = (uint64_t)ntpb * max_blocks;
     probe.fused = (probe.cap % 64 == 0) && probe.cap <= 0x7FFFFFFFull && step_launch_enabled() && !sort_enabled();
-    if (nbatch == 1 || !device_steps_ok(g, probe)) {   // nothing to overlap: one propagate after the other
-        for (uint32_t i = 0; i < nbatch; ++i)
+    if (idx.size() == 1 || !device_steps_ok(g, probe)) {   // nothing to overlap: one propagate after the other
+        for (uint32_t i : idx)
             CHR_TRY(chr_propagate(g, phs + i, nphotons[i], true_nphotons[i], ncopies[i], d_rng_states, rng_nslots,
                                   ntpb, max_blocks, max_steps, use_weights, scatter_first, stats ? stats + i : nullptr,
                                   vstream));
         return CHR_OK;
     }
-    hipStream_t ts = nullptr;
-    hipEvent_t done[2];
-    CHR_TRY(tail_stream_get(&ts, done));
-    // a batch in flight on context c: its tail may still run on ts; its
-    // statistics are read once done[c] (recorded on ts after its last slot) fires
-    struct Pending {
-        bool on = false;
-        int k = 0;
-        uint32_t *hctl = nullptr;
-        PropBufs b;
-        chr_propagate_stats *out = nullptr;
-    } pend[2];
-    std::vector<chr_propagate_stats> local(stats ? 0 : nbatch);
-    auto finish = [&](int c) -> int {
-        Pending &p = pend[c];
-        if (!p.on) return CHR_OK;
-        CHR_HIP_CHECK(hipEventSynchronize(done[c]));
-        std::vector<hipEvent_t> *evp = nullptr;
-        CHR_TRY(timing_events(0, &evp, c));
-        chr_propagate_stats &st = *p.out;
-        CHR_TRY(slot_stats(st, p.hctl, p.k, *evp, true));
-        counter_stats(st, p.b);
-        st.host_syncs = 1;
-        st.final_alive = 0;
-        p.on = false;
-        return CHR_OK;
+    hipStream_t ts = nullptr, ps = nullptr;
+    CHR_TRY(batch_streams_get(&ts, &ps));
+    const size_t nb = idx.size();
+    std::vector<BatchHost> *pool = nullptr;
+    CHR_TRY(batch_host_get(nb, 128 + 2 * (size_t)max_steps + 8, &pool));
+    std::vector<BatchHost> &bh = *pool;
+    // every context sized for the largest batch up front: no buffer is
+    // reallocated while an earlier batch may still use it
+    PropBufs bufs[NCTX];
+    for (int c = 0; c < NCTX && c < (int)nb; ++c) {
+        CHR_TRY(prop_bufs(max_n, ntpb, max_blocks, c, true, bufs[c]));
+        uint32_t *ctl = nullptr;
+        CHR_TRY(slot_ctl_get(2 * (size_t)max_steps + 8, &ctl, c));
+        const int cus = device_cus();
+        const StepVariant sv = select_step_variant(g);
+        const uint64_t blocks = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)cus * 4 * sv.trace_waves * 64 / BLOCK,
+                                                                          grid_for(max_n)));
+        uint2 *spill = nullptr;
+        CHR_TRY(walk_stack_get((size_t)WIDE_STACK * blocks * BLOCK * sizeof(uint2), &spill, c));
+    }
+    // the photon inputs were written on the caller's stream
+    std::vector<hipEvent_t> *entry_ev = nullptr;
+    CHR_TRY(timing_events(1, &entry_ev, 1));
+    CHR_HIP_CHECK(hipEventRecord((*entry_ev)[0], stream));
+    CHR_HIP_CHECK(hipStreamWaitEvent(ps, (*entry_ev)[0], 0));
+    auto aliases_earlier = [&](size_t j, size_t from) {   // batch j shares arrays with one of batches [from, j)
+        for (size_t e = from; e < j; ++e)
+            if (photons_alias(phs + idx[j], nphotons[idx[j]], phs + idx[e], nphotons[idx[e]])) return true;
+        return false;
     };
-    int c = 0, prev = -1;
-    uint32_t prev_i = 0;
-    for (uint32_t i = 0; i < nbatch; ++i) {
-        chr_propagate_stats &st = stats ? stats[i] : local[i];
-        st = chr_propagate_stats{};
-        if (nphotons[i] == 0) continue;
-        CHR_TRY(finish(c));   // the batch that last used this context (two batches ago)
-        Pending &p = pend[c];
-        CHR_TRY(prop_bufs(nphotons[i], ntpb, max_blocks, c, true, p.b));
-        CHR_TRY(pinned_ctl_get(2 * (size_t)max_steps + 8, &p.hctl, c));
-        // the previous batch's tail may still run: its photon arrays are off
-        // limits, and its RNG slots are needed by this batch's first shade pass
-        if (prev >= 0 && photons_alias(phs + i, nphotons[i], phs + prev_i, nphotons[prev_i]))
-            CHR_HIP_CHECK(hipStreamWaitEvent(stream, done[prev], 0));
-        CHR_TRY(prop_start(p.b, nphotons[i], true_nphotons[i], ncopies[i], stream));
+    size_t queued = 0;   // batches whose prefix is queued
+    const size_t lookahead = batch_lookahead();
+    auto prefix = [&](size_t j) -> int {
+        const uint32_t i = idx[j];
+        const int c = (int)(j % NCTX);
+        if (j >= (size_t)NCTX) CHR_HIP_CHECK(hipStreamWaitEvent(ps, bh[j - NCTX].done, 0));   // the context is free
+        for (size_t e = j >= (size_t)NCTX ? j - NCTX + 1 : 0; e < j; ++e)   // shared photon arrays: after that batch
+            if (photons_alias(phs + i, nphotons[i], phs + idx[e], nphotons[idx[e]]))
+                CHR_HIP_CHECK(hipStreamWaitEvent(ps, bh[e].done, 0));
+        CHR_TRY(prop_bufs(nphotons[i], ntpb, max_blocks, c, true, bufs[c]));
+        bufs[c].pinned = bh[j].pinned;
+        return queue_prefix(g, phs + i, nphotons[i], true_nphotons[i], ncopies[i], d_rng_states, rng_nslots, ntpb,
+                            max_steps, use_weights, scatter_first, bufs[c], c, bh[j].ev, bh[j].prefix_done, ps);
+    };
+    std::vector<int> slots(nb, 0);
+    for (size_t j = 0; j < nb; ++j) {
+        // queue the prefixes of the batches ahead (as many as there are free
+        // contexts); one sharing photon arrays with a batch not yet queued in
+        // full waits until that batch's done event exists
+        while (queued < nb && queued < j + 1 + lookahead) {
+            if (queued > j && aliases_earlier(queued, j)) break;
+            CHR_TRY(prefix(queued));
+            queued++;
+        }
+        const uint32_t i = idx[j];
+        const int c = (int)(j % NCTX);
+        PropBufs &b = bufs[c];
+        SlotRun run;
+        run.events = &bh[j].ev;
+        run.tstream = ts;
+        run.rng_ready = j > 0 ? bh[j - 1].done : nullptr;   // the previous batch's tail advances the RNG slots
+        run.prefix_done = bh[j].prefix_done;
+        run.ctx = c;
         uint32_t *ctl = nullptr;
         CHR_TRY(device_slots(g, phs + i, nphotons[i], d_rng_states, rng_nslots, ntpb, max_steps, use_weights,
-                             scatter_first, p.b, c, stream, ts, prev >= 0 ? done[prev] : nullptr, &ctl, &p.k));
+                             scatter_first, b, run, stream, &ctl, &slots[j]));
         // after the batch's last slot (and every tail before it on ts): read its counters back
-        std::vector<hipEvent_t> *evp = nullptr;
-        CHR_TRY(timing_events(0, &evp, c));
-        CHR_HIP_CHECK(hipStreamWaitEvent(ts, (*evp)[SLOT_EVENTS * (size_t)(p.k - 1) + 4], 0));
-        CHR_HIP_CHECK(hipMemcpyAsync(p.hctl, ctl, 8 * (size_t)p.k, hipMemcpyDeviceToHost, ts));
-        CHR_TRY(counter_readback(p.b, ts));
-        CHR_HIP_CHECK(hipEventRecord(done[c], ts));
-        p.out = &st;
-        p.on = true;
-        prev = c;
-        prev_i = i;
-        c ^= 1;
+        CHR_HIP_CHECK(hipStreamWaitEvent(ts, bh[j].ev[SLOT_EVENTS * (size_t)(slots[j] - 1) + 4], 0));
+        CHR_HIP_CHECK(hipMemcpyAsync(bh[j].pinned + 128, ctl, 8 * (size_t)slots[j], hipMemcpyDeviceToHost, ts));
+        CHR_TRY(counter_readback(b, ts));
+        CHR_HIP_CHECK(hipEventRecord(bh[j].done, ts));
     }
-    CHR_TRY(finish(c));
-    CHR_TRY(finish(c ^ 1));
+    // the last batch's done event follows every earlier one on the tail stream
+    CHR_HIP_CHECK(hipEventSynchronize(bh[nb - 1].done));
+    for (size_t j = 0; j < nb; ++j) {
+        chr_propagate_stats st{};
+        CHR_TRY(slot_stats(st, bh[j].pinned + 128, slots[j], bh[j].ev, true, true));
+        PropBufs view;
+        view.fused = true;
+        view.pinned = bh[j].pinned;
+        counter_stats(st, view);
+        st.host_syncs = 1;
+        st.final_alive = 0;
+        if (stats) stats[idx[j]] = st;
+    }
     return CHR_OK;
 }
 

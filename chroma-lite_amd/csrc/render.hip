@@ -24,9 +24,10 @@
 namespace chr {
 
 // render.cu:12-32 (get_color): shading by |cos| of the triangle normal
-__device__ __forceinline__ float4 render_color(V3 dir, const float4 *tri, uint32_t rgba) {
-    const float4 r0 = gld(tri), r1 = gld(tri + 1), r2 = gld(tri + 2);
-    const V3 v01 = v3(r0.w, r1.x, r1.y), v12 = v3(r2.y, r2.z, r2.w);   // e1 = v1 - v0, e3 = v2 - v1
+// r0..r2: the hit's wide triangle record (v0, v1, v2)
+__device__ __forceinline__ float4 render_color(V3 dir, float4 r0, float4 r1, float4 r2, uint32_t rgba) {
+    const V3 v0 = v3(r0.x, r0.y, r0.z), v1 = v3(r0.w, r1.x, r1.y), v2 = v3(r1.z, r1.w, r2.x);
+    const V3 v01 = v1 - v0, v12 = v2 - v1;
     const V3 n = normalize(cross(v01, v12));
     float c = dot(n, -dir);
     if (c < 0.0f) c = -c;
@@ -102,7 +103,7 @@ __global__ __launch_bounds__(BLOCK) void render_kernel(const DevGeom *__restrict
                 float bd, dist;
                 node_bounds(g, make_uint4(__float_as_uint(r2.w), __float_as_uint(r3.x), __float_as_uint(r3.y), 0u), lo, hi);
                 if (!intersect_box(noid, inv, lo, hi, bd)) continue;   // the reference's leaf node test
-                if (!intersect_triangle(o, d, v3(r0.x, r0.y, r0.z), v3(r0.w, r1.x, r1.y), v3(r1.z, r1.w, r2.x), dist))
+                if (!intersect_record(o, d, r0, r1, r2, dist))
                     continue;
                 const uint32_t tid = __float_as_uint(r2.y), rank = __float_as_uint(r2.z) + 1u;
                 // position under (distance asc, rank desc); a full list drops its last entry
@@ -119,7 +120,7 @@ __global__ __launch_bounds__(BLOCK) void render_kernel(const DevGeom *__restrict
                     rk[i] = rk[i - 1];
                 }
                 dx[pos] = dist;
-                col[pos] = render_color(d, g.tri + 3 * (size_t)tid, gld(colors + tid));
+                col[pos] = render_color(d, r0, r1, r2, gld(colors + tid));
                 rk[pos] = rank;
                 if (n < alpha_depth) n++;
             }
@@ -245,7 +246,8 @@ __global__ __launch_bounds__(BLOCK) void update_xyz_lookup_kernel(const DevGeom 
     uint32_t overflow = 0;
     WalkCounts cnt;
     float distance;
-    const int hit = intersect_wide_sched<false, 2>(g, position, dir, distance, -1, wst, overflow, cnt);
+    const int rec = intersect_wide_sched<false, 2>(g, position, dir, distance, -1, wst, overflow, cnt);
+    const int hit = rec == -1 ? -1 : (int)__float_as_uint(gld(g.wtri + 4 * (size_t)rec + 2).y);   // the record's triangle
     if (hit == id) {
         const V3 nrm = normalize(cross(v1 - v0, v2 - v1));
         float cos_theta = dot(nrm, -dir);

@@ -371,7 +371,7 @@ int build_wide_bvh(const chr_geometry_desc *d, WideBVH &out) {
                         const float *v2 = d->h_vertices + 3 * (size_t)ix[2];
                         WideTri &R = out.tri[slot];
                         R.v0[0] = v0[0]; R.v0[1] = v0[1]; R.v0[2] = v0[2];
-                        for (int a = 0; a < 3; ++a) { R.e1[a] = v1[a] - v0[a]; R.e2[a] = v2[a] - v0[a]; }
+                        for (int a = 0; a < 3; ++a) { R.v1[a] = v1[a]; R.v2[a] = v2[a]; }
                         R.id = t;
                         R.rank = rank[t];
                         std::memcpy(R.leaf, &leafq[3 * (size_t)t], 12);
@@ -386,11 +386,11 @@ int build_wide_bvh(const chr_geometry_desc *d, WideBVH &out) {
     }
     out.tri.resize(tri_next);
     if (7 * (out.max_depth + 1) + 1 > (uint32_t)WIDE_STACK) out.usable = false;
-    // rank -> triangle id (the tie-break rank identifies the triangle of a
+    // rank -> triangle record (the tie-break rank identifies the triangle of a
     // decomposed walk's (distance, rank) result)
-    out.rank_id.assign(nreach, 0xFFFFFFFFu);
-    for (uint32_t t = 0; t < ntri; ++t)
-        if (rank[t] != 0xFFFFFFFFu) out.rank_id[rank[t]] = t;
+    out.rank_rec.assign(nreach, 0xFFFFFFFFu);
+    for (size_t i = 0; i < out.tri.size(); ++i)
+        if (out.tri[i].rank < nreach) out.rank_rec[out.tri[i].rank] = (uint32_t)i;
     // cut: BFS frontier of inner nodes until it holds WIDE_CUT_TARGET nodes;
     // nodes above it contribute their leaf children as (node, leaf mask) items
     out.cut.clear();

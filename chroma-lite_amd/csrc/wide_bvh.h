@@ -7,11 +7,15 @@
 //   [64,72)  child_base (first inner child node), tri_base (first triangle record)
 //   [72,88)  kind[8]: 0 empty, 1..4 leaf with that many triangles, WIDE_INNER;
 //            off[8]:  inner -> node child_base+off, leaf -> records tri_base+off..
-// WideTri, 64 bytes = four 16-byte loads (half a 128-byte line): v0, e1 = v1-v0,
-// e2 = v2-v0 (float32, the Moller-Trumbore operands of intersect.h:26-101), the
-// original triangle id, its rank in the reference BVH's DFS order (the
-// nearest-hit tie-break) and the x/y/z words of its reference leaf node, so the
-// kernel applies the reference's own leaf slab test + prune before Moller-Trumbore.
+// WideTri, 64 bytes = four 16-byte loads (half a 128-byte line): the float32
+// vertices v0, v1, v2 (the kernels form the Moller-Trumbore edges v1-v0, v2-v0
+// of intersect.h:26-101 and fill_state's normal edge v2-v1, photon.h:365-367,
+// with the same float subtractions the reference makes -- so a hit's normal
+// comes from the record the walk found and no second triangle array is kept
+// in HBM), the original triangle id, its rank in the reference BVH's DFS order
+// (the nearest-hit tie-break) and the x/y/z words of its reference leaf node,
+// so the kernel applies the reference's own leaf slab test + prune before
+// Moller-Trumbore.  The first three loads (v0, v1, v2, id, rank) are the hot part.
 #pragma once
 
 #include <cstdint>
@@ -39,8 +43,8 @@ static_assert(sizeof(WideNode) == 96, "WideNode must be 96 bytes");
 
 struct alignas(16) WideTri {
     float v0[3];
-    float e1[3];
-    float e2[3];
+    float v1[3];
+    float v2[3];
     uint32_t id;
     uint32_t rank;
     uint32_t leaf[3];      // reference leaf node words x, y, z (lo | hi << 16)
@@ -58,7 +62,7 @@ struct WideBVH {
     // partition the triangle records -- the nodes of one BFS frontier (all
     // children) plus the leaf children of the nodes above it.
     std::vector<uint32_t> cut;     // 2 words per item
-    std::vector<uint32_t> rank_id; // reference DFS rank -> triangle id
+    std::vector<uint32_t> rank_rec; // reference DFS rank -> triangle record (index into tri)
 };
 
 // target number of sub-walks per decomposed walk (frontier size): the longest

@@ -86,24 +86,44 @@ def test_batches_equal_sequential_and_oracle(cuda, small_detector, small_packed,
     assert np.array_equal(rng_bat, states.reshape(6, nslots))
 
 
-def test_batches_same_photons_twice(cuda, small_detector):
-    """The same GPUPhotons listed twice (aliasing arrays: the second batch
-    waits for the first one's tail) == propagating it twice."""
+@pytest.mark.parametrize('pattern', ['aa', 'aba', 'abcdeb'])
+def test_batches_shared_photons(cuda, small_detector, pattern):
+    """Batches listing the same GPUPhotons more than once (aliasing arrays: a
+    batch waits for the earlier one it shares photons with, also when that one
+    is two batches back) and more batches than buffer contexts == the same
+    propagate calls in order."""
     from chroma import gpu
     det = gpu.GPUDetector(small_detector)
-    src = _sources([40000], seed=5)[0]
+    names = sorted(set(pattern))
+    src = dict(zip(names, _sources([40000 + 7000 * i for i in range(len(names))], seed=5)))
     out = {}
     for batched in (False, True):
         rng = gpu.get_rng_states(64 * 64, seed=9)
-        gp = _gpu_photons(src)
+        gps = {k: _gpu_photons(src[k]) for k in names}
+        seq = [gps[k] for k in pattern]
         if batched:
-            gpu.propagate_batches([gp, gp], det, rng, nthreads_per_block=64, max_blocks=64, max_steps=7)
+            gpu.propagate_batches(seq, det, rng, nthreads_per_block=64, max_blocks=64, max_steps=7)
         else:
-            for _ in range(2):
+            for gp in seq:
                 gp.propagate(det, rng, nthreads_per_block=64, max_blocks=64, max_steps=7)
-        out[batched] = (gp.get(), rng.get())
-    _same(out[True][0], out[False][0], 'twice')
+        out[batched] = ({k: gps[k].get() for k in names}, rng.get())
+    for k in names:
+        _same(out[True][0][k], out[False][0][k], '%s:%s' % (pattern, k))
     assert np.array_equal(out[True][1], out[False][1])
+
+
+@pytest.mark.parametrize('lookahead', ['0', '1'])
+def test_batches_lookahead_settings(cuda, small_detector, monkeypatch, lookahead):
+    """CHR_BATCH_LOOKAHEAD (prefixes queued ahead) changes nothing in the results."""
+    from chroma import gpu
+    monkeypatch.setenv('CHR_BATCH_LOOKAHEAD', lookahead)
+    det = gpu.GPUDetector(small_detector)
+    sources = _sources([30000, 50000, 20000, 60000], seed=17)
+    seq, rng_seq, _ = _run(det, sources, 64, 64, 1000, batched=False)
+    bat, rng_bat, _ = _run(det, sources, 64, 64, 1000, batched=True)
+    for i, (a, b) in enumerate(zip(bat, seq)):
+        _same(a, b, 'lookahead %s batch %d' % (lookahead, i))
+    assert np.array_equal(rng_bat, rng_seq)
 
 
 def test_batches_empty_and_single(cuda, small_detector):

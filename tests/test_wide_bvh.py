@@ -65,11 +65,11 @@ def _check(packed):
     rank, leaf = _reference_dfs(packed.nodes)
     assert np.array_equal(tris['rank'], rank[tris['id']])
     assert np.array_equal(tris['leaf'], leaf[tris['id']])
-    # Moller-Trumbore operands
+    # the triangle's own float vertices (edges and normal formed in the kernels)
     v = packed.vertices[packed.triangles[tris['id']]]
     assert np.array_equal(tris['v0'], v[:, 0])
-    assert np.array_equal(tris['e1'], v[:, 1] - v[:, 0])
-    assert np.array_equal(tris['e2'], v[:, 2] - v[:, 0])
+    assert np.array_equal(tris['v1'], v[:, 1])
+    assert np.array_equal(tris['v2'], v[:, 2])
     # reference leaf boxes (decoded as the reference does)
     q = tris['leaf']
     tlo = _fma32(q & 0xFFFF, packed.world_scale, packed.world_origin[None, :])
