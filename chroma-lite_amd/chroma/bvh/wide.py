@@ -19,7 +19,7 @@ wide_node_dtype = np.dtype([('origin', '<f4', 3), ('exp', 'u1', 3), ('nchild', '
                             ('child_base', '<u4'), ('tri_base', '<u4'),
                             ('kind', 'u1', 8), ('off', 'u1', 8), ('pad', '<u4', 2)])
 wide_tri_dtype = np.dtype([('v0', '<f4', 3), ('v1', '<f4', 3), ('v2', '<f4', 3), ('id', '<u4'),
-                           ('rank', '<u4'), ('leaf', '<u4', 3), ('pad', '<u4', 2)])
+                           ('rank', '<u4'), ('leaf', '<u4', 3), ('code', '<u4'), ('pad', '<u4')])
 assert wide_node_dtype.itemsize == 96 and wide_tri_dtype.itemsize == 64
 
 

@@ -1021,22 +1021,24 @@ __device__ __forceinline__ void finish_fill(const DevGeom &g, State &s, Photon &
     } else if (mesh_triangle != -1) {
         V3 e1, e3;   // v1 - v0, v2 - v1 (photon.h:365-367)
         int tid;
-        if constexpr (REC) {
+        uint32_t code;
+        if constexpr (REC) {   // one record, four independent loads (no dependent material-code gather)
             const float4 *r = g.wtri + 4 * (size_t)mesh_triangle;
-            const float4 r0 = gld(r), r1 = gld(r + 1), r2 = gld(r + 2);
+            const float4 r0 = gld(r), r1 = gld(r + 1), r2 = gld(r + 2), r3 = gld(r + 3);
             const V3 v0 = v3(r0.x, r0.y, r0.z), v1 = v3(r0.w, r1.x, r1.y), v2 = v3(r1.z, r1.w, r2.x);
             e1 = v1 - v0;
             e3 = v2 - v1;
             tid = (int)__float_as_uint(r2.y);
+            code = __float_as_uint(r3.z);
         } else {
             const float4 *r = g.tri + 3 * (size_t)mesh_triangle;
             const float4 r0 = gld(r), r1 = gld(r + 1), r2 = gld(r + 2);
             e1 = v3(r0.w, r1.x, r1.y);
             e3 = v3(r2.y, r2.z, r2.w);
             tid = mesh_triangle;
+            code = gld(g.material_codes + tid);
         }
         p.last_hit = tid;
-        const uint32_t code = gld(g.material_codes + tid);
         const int inner = convert(0xFF & (int)(code >> 24));
         const int outer = convert(0xFF & (int)(code >> 16));
         s.surface_index = convert(0xFF & (int)(code >> 8));
@@ -1076,7 +1078,7 @@ __device__ __forceinline__ void fill_state(const DevGeom &g, State &s, Photon &p
 }
 
 // photon.h:399-427
-__device__ V3 pick_new_direction(V3 axis, float theta, float phi) {
+__device__ __forceinline__ V3 pick_new_direction(V3 axis, float theta, float phi) {
     float st, ct, sp, cp;
     chr_sincosf(theta, &st, &ct);
     chr_sincosf(phi, &sp, &cp);
@@ -1091,7 +1093,7 @@ __device__ V3 pick_new_direction(V3 axis, float theta, float phi) {
 }
 
 // photon.h:429-453
-__device__ void rayleigh_scatter(Photon &p, chr_xorwow &rng) {
+__device__ __forceinline__ void rayleigh_scatter(Photon &p, chr_xorwow &rng) {
     const float u = chr_uniform01(&rng);
     float cos_theta = 2.0f * chr_cosf((chr_acosf(__builtin_fmaf(-2.0f, u, 1.0f)) - 2 * PI_F) / 3.0f);
     if (cos_theta > 1.0f) cos_theta = 1.0f;
@@ -1109,7 +1111,7 @@ __device__ void rayleigh_scatter(Photon &p, chr_xorwow &rng) {
 }
 
 // photon.h:455-570
-__device__ int propagate_to_boundary(const DevGeom &g, Photon &p, State &s, chr_xorwow &rng, int use_weights,
+__device__ __forceinline__ int propagate_to_boundary(const DevGeom &g, Photon &p, State &s, chr_xorwow &rng, int use_weights,
                                      int scatter_first) {
     float absorption_distance = -s.absorption_length * chr_logf(chr_uniform01(&rng));
     float scattering_distance = -s.scattering_length * chr_logf(chr_uniform01(&rng));
@@ -1190,7 +1192,7 @@ __device__ int propagate_to_boundary(const DevGeom &g, Photon &p, State &s, chr_
 }
 
 // photon.h:572-632 (Fresnel)
-__device__ void propagate_at_boundary(Photon &p, const State &s, chr_xorwow &rng) {
+__device__ __forceinline__ void propagate_at_boundary(Photon &p, const State &s, chr_xorwow &rng) {
     const float incident_angle = get_theta(s.normal, -p.dir);
     const float refracted_angle = chr_asinf((chr_sinf(incident_angle) * s.n1) / s.n2);
     V3 ipn = cross(p.dir, s.normal);
@@ -1222,7 +1224,7 @@ __device__ void propagate_at_boundary(Photon &p, const State &s, chr_xorwow &rng
 }
 
 // photon.h:634-667
-__device__ int specular_reflector(Photon &p, const State &s) {
+__device__ __forceinline__ int specular_reflector(Photon &p, const State &s) {
     const float incident_angle = get_theta(s.normal, -p.dir);
     V3 ipn = cross(p.dir, s.normal);
     ipn = ipn / norm(ipn);
@@ -1231,7 +1233,7 @@ __device__ int specular_reflector(Photon &p, const State &s) {
     return CONTINUE;
 }
 
-__device__ int diffuse_reflector(Photon &p, const State &s, chr_xorwow &rng) {
+__device__ __forceinline__ int diffuse_reflector(Photon &p, const State &s, chr_xorwow &rng) {
     float ndotv;
     do {
         p.dir = uniform_sphere(rng);
@@ -1252,7 +1254,7 @@ __device__ __forceinline__ Cx csub(Cx a, Cx b) { return cxm(a.r - b.r, a.i - b.i
 __device__ __forceinline__ Cx cmul(Cx a, Cx b) {
     return cxm(__builtin_fmaf(a.r, b.r, -(a.i * b.i)), __builtin_fmaf(a.r, b.i, a.i * b.r));
 }
-__device__ Cx cdiv(Cx x, Cx y) {
+__device__ __forceinline__ Cx cdiv(Cx x, Cx y) {
     float s = chr_fabsf(y.r) + chr_fabsf(y.i);
     float oos = 1.0f / s;
     const float ars = x.r * oos, ais = x.i * oos, brs = y.r * oos, bis = y.i * oos;
@@ -1260,7 +1262,7 @@ __device__ Cx cdiv(Cx x, Cx y) {
     oos = 1.0f / s;
     return cxm(__builtin_fmaf(ais, bis, ars * brs) * oos, __builtin_fmaf(ais, brs, -(ars * bis)) * oos);
 }
-__device__ float cabs_(Cx x) {
+__device__ __forceinline__ float cabs_(Cx x) {
     const float a = chr_fabsf(x.r), b = chr_fabsf(x.i);
     float v, w, t;
     if (a > b) { v = a; w = b; } else { v = b; w = a; }
@@ -1271,7 +1273,7 @@ __device__ float cabs_(Cx x) {
     return t;
 }
 __device__ __forceinline__ float carg_(Cx x) { return chr_atan2f(x.i, x.r); }
-__device__ Cx csqrt_(Cx x) {
+__device__ __forceinline__ Cx csqrt_(Cx x) {
     const float r = chr_sqrtf(cabs_(x));
     const float t = carg_(x) / 2.0f;
     float st, ct;
@@ -1939,7 +1941,7 @@ struct LdsRows {
 // over mid-way): culling with it is conservative, and the result is the min
 // over the seed and every triangle this walk tests.
 template <class M>
-__device__ int walk_segment(const DevGeom &g, bool act, V3 o, V3 d, uint32_t last, int Gs, M stk, int cap, M tlist,
+__device__ __forceinline__ int walk_segment(const DevGeom &g, bool act, V3 o, V3 d, uint32_t last, int Gs, M stk, int cap, M tlist,
                             uint32_t &overflow, float &min_distance, uint32_t &iters,
                             float best = __builtin_inff(), uint32_t best_rank = 0xFFFFFFFFu, int best_id = -1) {
     constexpr uint32_t INVALID = 0xFFFFFFFFu;
@@ -3251,7 +3253,8 @@ static StepVariant select_step_variant(const chr_geometry *g) {
             sv.trace = trace_kernel<false, 6, 12, 4, 32>;
             sv.shade = shade_kernel<3>;
             sv.tail = tail_group_walk() ? propagate_group_kernel<8, kGroupWaves>
-                      : (tail_waves() == 4 ? propagate_tail_kernel<4> : propagate_tail_kernel<kTailWaves>);
+                      : (tail_waves() == 4 ? propagate_tail_kernel<4>
+                         : (tail_waves() == 2 ? propagate_tail_kernel<2> : propagate_tail_kernel<kTailWaves>));
             sv.tail_group = 8;
             sv.binned = v == 7 ? 1 : (v == 8 ? 0 : 2);
             break;

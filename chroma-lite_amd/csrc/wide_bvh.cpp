@@ -375,7 +375,8 @@ int build_wide_bvh(const chr_geometry_desc *d, WideBVH &out) {
                         R.id = t;
                         R.rank = rank[t];
                         std::memcpy(R.leaf, &leafq[3 * (size_t)t], 12);
-                        R.pad[0] = R.pad[1] = 0;
+                        R.code = d->h_material_codes ? d->h_material_codes[t] : 0u;
+                        R.pad = 0;
                     }
                 }
             }

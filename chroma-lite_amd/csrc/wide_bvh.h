@@ -15,7 +15,10 @@
 // in HBM), the original triangle id, its rank in the reference BVH's DFS order
 // (the nearest-hit tie-break) and the x/y/z words of its reference leaf node,
 // so the kernel applies the reference's own leaf slab test + prune before
-// Moller-Trumbore.  The first three loads (v0, v1, v2, id, rank) are the hot part.
+// Moller-Trumbore, and the triangle's material code (geometry_types.h: inner,
+// outer, surface, the reference's material_codes[id]), so a hit's fill_state
+// reads everything it needs from one 64-byte record in four parallel loads.
+// The first three loads (v0, v1, v2, id, rank) are the walk's hot part.
 #pragma once
 
 #include <cstdint>
@@ -48,7 +51,8 @@ struct alignas(16) WideTri {
     uint32_t id;
     uint32_t rank;
     uint32_t leaf[3];      // reference leaf node words x, y, z (lo | hi << 16)
-    uint32_t pad[2];
+    uint32_t code;         // material code (inner << 24 | outer << 16 | surface << 8)
+    uint32_t pad;
 };
 static_assert(sizeof(WideTri) == 64, "WideTri must be 64 bytes");
 

@@ -70,6 +70,7 @@ def _check(packed):
     assert np.array_equal(tris['v0'], v[:, 0])
     assert np.array_equal(tris['v1'], v[:, 1])
     assert np.array_equal(tris['v2'], v[:, 2])
+    assert np.array_equal(tris['code'], np.asarray(packed.material_codes, np.uint32)[tris['id']])
     # reference leaf boxes (decoded as the reference does)
     q = tris['leaf']
     tlo = _fma32(q & 0xFFFF, packed.world_scale, packed.world_origin[None, :])
