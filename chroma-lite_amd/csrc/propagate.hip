@@ -24,6 +24,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <type_traits>
 #include <vector>
 
@@ -3719,6 +3720,9 @@ struct SlotRun {
     hipEvent_t rng_ready = nullptr;    // the first RNG use waits for it
     hipEvent_t prefix_done = nullptr;  // slot 0's prefix was queued by queue_prefix and ends with this event
     int ctx = 0;
+    // called with each one-step slot's queue length as the host learns it
+    // (chr_propagate_batches: queue the next batch's prefix once few photons remain)
+    std::function<int(uint32_t)> on_length;
 };
 
 // Device-driven steps: every slot's kernels read the queue length from the
@@ -3772,6 +3776,7 @@ static int device_slots(const chr_geometry *g, const chr_photons *ph, uint32_t n
             const uint32_t m = ring[2 * ((k - 1) % 32)], nk = ring[2 * ((k - 1) % 32) + 1];
             if (m != STEP_ONE) stop = true;   // the tail ran or the queue emptied: slot k is idle
             else n_ub = nk;                   // later queues are no longer
+            if (run.on_length) CHR_TRY(run.on_length(m == STEP_ONE ? nk : 0u));
         }
         k++;
     }
@@ -4105,6 +4110,14 @@ static size_t batch_lookahead() {
     return (size_t)(k < 0 ? 0 : (k > NCTX - 1 ? NCTX - 1 : k));
 }
 
+// CHR_BATCH_PREFIX_BELOW=n: queue the next batch's prefix once the running
+// batch's queue is below n photons (its late steps under-fill the chip); 0
+// (default): when the next batch starts, i.e. when this batch's tail starts
+static uint32_t batch_prefix_below() {
+    const char *e = getenv("CHR_BATCH_PREFIX_BELOW");
+    return e ? (uint32_t)strtoul(e, nullptr, 10) : 0u;
+}
+
 // The RNG-free part of a propagate's first slot on stream ps: queues, counters,
 // the head kernel, flat-walk classification, direction binning and the BVH
 // walk (launch_step PHASE_PREFIX), ending with prefix_done.
@@ -4192,6 +4205,7 @@ extern "C" int chr_propagate_batches(const chr_geometry *g, const chr_photons *p
     };
     size_t queued = 0;   // batches whose prefix is queued
     const size_t lookahead = batch_lookahead();
+    const uint32_t prefix_below = batch_prefix_below();
     auto prefix = [&](size_t j) -> int {
         const uint32_t i = idx[j];
         const int c = (int)(j % NCTX);
@@ -4223,6 +4237,16 @@ extern "C" int chr_propagate_batches(const chr_geometry *g, const chr_photons *p
         run.rng_ready = j > 0 ? bh[j - 1].done : nullptr;   // the previous batch's tail advances the RNG slots
         run.prefix_done = bh[j].prefix_done;
         run.ctx = c;
+        // the next batch's prefix as soon as this batch is down to its late,
+        // under-occupied steps (CHR_BATCH_PREFIX_BELOW photons; 0: at the next batch's start)
+        if (prefix_below && queued == j + 1 && queued < nb && !aliases_earlier(queued, j))
+            run.on_length = [&, j](uint32_t n) -> int {
+                if (queued == j + 1 && queued < nb && n < prefix_below) {
+                    CHR_TRY(prefix(queued));
+                    queued++;
+                }
+                return CHR_OK;
+            };
         uint32_t *ctl = nullptr;
         CHR_TRY(device_slots(g, phs + i, nphotons[i], d_rng_states, rng_nslots, ntpb, max_steps, use_weights,
                              scatter_first, b, run, stream, &ctl, &slots[j]));

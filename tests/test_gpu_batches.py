@@ -112,11 +112,15 @@ def test_batches_shared_photons(cuda, small_detector, pattern):
     assert np.array_equal(out[True][1], out[False][1])
 
 
-@pytest.mark.parametrize('lookahead', ['0', '1'])
-def test_batches_lookahead_settings(cuda, small_detector, monkeypatch, lookahead):
-    """CHR_BATCH_LOOKAHEAD (prefixes queued ahead) changes nothing in the results."""
+@pytest.mark.parametrize('env', [('CHR_BATCH_LOOKAHEAD', '0'), ('CHR_BATCH_LOOKAHEAD', '1'),
+                                 ('CHR_BATCH_PREFIX_BELOW', '20000')])
+def test_batches_lookahead_settings(cuda, small_detector, monkeypatch, env):
+    """When the next batches' prefixes are queued (CHR_BATCH_LOOKAHEAD: that
+    many batches ahead; CHR_BATCH_PREFIX_BELOW: once the running batch is down
+    to that many photons) changes nothing in the results."""
     from chroma import gpu
-    monkeypatch.setenv('CHR_BATCH_LOOKAHEAD', lookahead)
+    monkeypatch.setenv(*env)
+    lookahead = '%s=%s' % env
     det = gpu.GPUDetector(small_detector)
     sources = _sources([30000, 50000, 20000, 60000], seed=17)
     seq, rng_seq, _ = _run(det, sources, 64, 64, 1000, batched=False)
