@@ -50,9 +50,18 @@ def main():
     write = per_kernel(os.path.join(d, 'write'), 'WRITE_SIZE')
     k = 'chr::trace_kernel'     # the dominant kernel (bench.py roofline)
     res = {'kernel': k}
+    # device-driven steps launch trace_kernel in every step slot; in the tail's
+    # and the idle slots it reads its mode word and exits (a few KiB): the
+    # per-launch figures are over the launches that walked rays (>= 64 KiB;
+    # a one-step launch holds >= 65,536 rays and writes 8 B of hit per ray)
+    for dct in (fetch, write):
+        if k in dct:
+            dct[k + ' (exited)'] = [v for v in dct[k] if v < 64.0]
+            dct[k] = [v for v in dct[k] if v >= 64.0]
     if k in fetch:
         f = fetch[k]
         res['launches_fetch_pass'] = len(f)
+        res['exited_launches_fetch_pass'] = len(fetch.get(k + ' (exited)', []))
         res['fetch_kib_per_launch_raw'] = sum(f) / len(f)
         res['read_bytes_per_launch'] = 2.0 * 1024.0 * sum(f) / len(f)
     if k in write:
