@@ -4142,11 +4142,11 @@ static int queue_prefix(const chr_geometry *g, const chr_photons *ph, uint32_t n
                        &b.fc, &sc);
 }
 
-extern "C" int chr_propagate_batches(const chr_geometry *g, const chr_photons *phs, const uint32_t *nphotons,
-                                     const uint32_t *true_nphotons, const uint32_t *ncopies, uint32_t nbatch,
-                                     uint32_t *d_rng_states, uint32_t rng_nslots, int32_t ntpb, int32_t max_blocks,
-                                     int32_t max_steps, int32_t use_weights, int32_t scatter_first,
-                                     chr_propagate_stats *stats, void *vstream) {
+static int propagate_batches(const chr_geometry *g, const chr_photons *phs, const uint32_t *nphotons,
+                             const uint32_t *true_nphotons, const uint32_t *ncopies, uint32_t nbatch,
+                             uint32_t *d_rng_states, uint32_t rng_nslots, int32_t ntpb, int32_t max_blocks,
+                             int32_t max_steps, int32_t use_weights, int32_t scatter_first, chr_propagate_stats *stats,
+                             void *vstream) {
     if (nbatch && (!phs || !nphotons || !true_nphotons || !ncopies))
         return chr::fail(CHR_ERR_INVALID, "chr_propagate_batches: null argument");
     for (uint32_t i = 0; i < nbatch; ++i)
@@ -4270,6 +4270,19 @@ extern "C" int chr_propagate_batches(const chr_geometry *g, const chr_photons *p
         if (stats) stats[idx[j]] = st;
     }
     return CHR_OK;
+}
+
+extern "C" int chr_propagate_batches(const chr_geometry *g, const chr_photons *phs, const uint32_t *nphotons,
+                                     const uint32_t *true_nphotons, const uint32_t *ncopies, uint32_t nbatch,
+                                     uint32_t *d_rng_states, uint32_t rng_nslots, int32_t ntpb, int32_t max_blocks,
+                                     int32_t max_steps, int32_t use_weights, int32_t scatter_first,
+                                     chr_propagate_stats *stats, void *vstream) {
+    const int rc = propagate_batches(g, phs, nphotons, true_nphotons, ncopies, nbatch, d_rng_states, rng_nslots, ntpb,
+                                     max_blocks, max_steps, use_weights, scatter_first, stats, vstream);
+    // a failure part-way leaves work queued on three streams: drain it, so no
+    // buffer of this call is still in use when the caller frees or retries
+    if (rc != CHR_OK) (void)hipDeviceSynchronize();
+    return rc;
 }
 
 static int select_common(const chr_photons *ph, int32_t start, int32_t n, uint32_t state, const uint32_t *solid_map,
