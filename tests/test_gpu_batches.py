@@ -130,6 +130,31 @@ def test_batches_lookahead_settings(cuda, small_detector, monkeypatch, env):
     assert np.array_equal(rng_bat, rng_seq)
 
 
+def test_batches_with_copies_and_weights(cuda, small_detector):
+    """Batches of GPUPhotons with ncopies > 1 (clones interleaved in the queue,
+    photon.py:242-250), and use_weights (every slot a multi-step tail) ==
+    the same propagate calls in order."""
+    from chroma import gpu
+    det = gpu.GPUDetector(small_detector)
+    srcs = _sources([12000, 9000, 15000], seed=31)
+    for use_weights, copies in ((False, (3, 1, 2)), (True, (1, 2, 1))):
+        out = {}
+        for batched in (False, True):
+            rng = gpu.get_rng_states(64 * 64, seed=4)
+            gps = [gpu.GPUPhotons(s, ncopies=c, copy_flags=True, copy_triangles=False, copy_weights=False)
+                   for s, c in zip(srcs, copies)]
+            kw = dict(nthreads_per_block=64, max_blocks=64, max_steps=40, use_weights=use_weights)
+            if batched:
+                gpu.propagate_batches(gps, det, rng, **kw)
+            else:
+                for gp in gps:
+                    gp.propagate(det, rng, **kw)
+            out[batched] = ([gp.get() for gp in gps], rng.get())
+        for i, (a, b) in enumerate(zip(out[True][0], out[False][0])):
+            _same(a, b, 'weights=%s batch %d' % (use_weights, i))
+        assert np.array_equal(out[True][1], out[False][1])
+
+
 def test_batches_empty_and_single(cuda, small_detector):
     """Empty batches are skipped; one batch is one chr_propagate."""
     from chroma import gpu
