@@ -2329,14 +2329,17 @@ __device__ __forceinline__ uint32_t octa_cell(V3 d) {   // octahedral map of a u
     const uint32_t iv = (uint32_t)fminf(fmaxf((v + 1.0f) * 128.0f, 0.0f), 255.0f);
     return (iv << 8) | iu;
 }
+// direction-binning key of a queued photon (0 for a zero / non-finite direction)
+__device__ __forceinline__ uint32_t bin_key_of(V3 d) {
+    const float l = sqrtf(d.x * d.x + d.y * d.y + d.z * d.z);
+    return (l > 0.0f && l < __builtin_inff()) ? octa_cell(v3(d.x / l, d.y / l, d.z / l)) : 0u;
+}
 __global__ __launch_bounds__(BLOCK) void bin_key_kernel(const float *dir, const uint32_t *queue, uint32_t n,
                                                         uint32_t *keys, uint32_t *vals) {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     if (i >= n) return;
     const uint32_t pid = queue[i];
-    V3 d = v3(dir[3 * pid], dir[3 * pid + 1], dir[3 * pid + 2]);
-    const float l = sqrtf(d.x * d.x + d.y * d.y + d.z * d.z);
-    keys[i] = (l > 0.0f && l < __builtin_inff()) ? octa_cell(v3(d.x / l, d.y / l, d.z / l)) : 0u;
+    keys[i] = bin_key_of(v3(dir[3 * pid], dir[3 * pid + 1], dir[3 * pid + 2]));
     vals[i] = i;
 }
 // ---------------------------------------------------------------- wavefront split
@@ -2392,14 +2395,20 @@ __device__ __forceinline__ void enrol_flat(const float *pos, const float *dir, u
     hits[p] = make_int2(FLAT_HIT, (int)f);
 }
 
-// first host step: enrol the flat walks of the initial queue
+// first host step: enrol the flat walks of the initial queue; with keys, also
+// the direction-binning key of every queue position (bin_key_kernel's, one
+// pass over the photons instead of two)
 __global__ __launch_bounds__(BLOCK) void classify_kernel(const float *pos, const float *dir, const uint32_t *flags,
                                                          const uint32_t *queue, uint32_t n, int2 *hits,
                                                          uint32_t *flat_q, uint32_t *flat_count,
-                                                         unsigned long long *flat_best) {
+                                                         unsigned long long *flat_best, uint32_t *keys, uint32_t *vals) {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     if (i >= n) return;
     const uint32_t pid = queue[i];
+    if (keys) {
+        keys[i] = bin_key_of(v3(dir[3 * pid], dir[3 * pid + 1], dir[3 * pid + 2]));
+        vals[i] = i;
+    }
     if ((flags[pid] & 0xFFFFu) & DEAD_MASK) return;
     enrol_flat(pos, dir, pid, i, hits, flat_q, flat_count, flat_best);
 }
@@ -2854,10 +2863,20 @@ __global__ __launch_bounds__(BLOCK) void clear_masks_kernel(unsigned long long *
 
 // photon.py:242-250: input queue entries (from q0[1]) = photon ids with the
 // ncopies clones of a photon interleaved; count headers q0[0] = n + 1 (the
-// input's length, read by device-driven steps), q1[0] = 1 (empty output)
+// input's length, read by device-driven steps), q1[0] = 1 (empty output).
+// The first block also zeroes the propagate's small control regions (step
+// counters, flat-walk control words, the slot loop's done flag): one launch
+// instead of a fill dispatch each.
+struct ZeroWords {
+    uint32_t *p[3];
+    uint32_t n[3];   // words (<= BLOCK each)
+};
 __global__ __launch_bounds__(BLOCK) void init_queue_kernel(uint32_t *q0, uint32_t *q1, uint32_t n, uint32_t true_n,
-                                                           uint32_t ncopies) {
+                                                           uint32_t ncopies, ZeroWords z) {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (blockIdx.x == 0)
+        for (int k = 0; k < 3; ++k)
+            if (z.p[k] && threadIdx.x < z.n[k]) z.p[k][threadIdx.x] = 0u;
     if (i >= n) return;
     q0[1 + i] = i / ncopies + (i % ncopies) * true_n;
     if (i == 0) { q0[0] = n + 1u; q1[0] = 1u; }
@@ -3456,9 +3475,16 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
     }
     if (split) {
         uint32_t *count_cur = fc->ctl + 1 + fc->cur, *count_next = fc->ctl + 1 + (fc->cur ^ 1);
+        // direction binning: 16-bit radix sort of (direction cell, queue position); hits region:
+        // [hits n x int2][next + pad, 16 words][keys n][values n][walk hist 64 words]
+        // (device-driven slots bin only the first step, whose length the host knows)
+        const bool bin_now = (sv.binned == 1 || (sv.binned == 2 && first_one_step && n >= kBinFirstMin)) &&
+                             (!sc || first_one_step) && pre;
+        uint32_t *keys = next + 16, *order = keys + n;
         if (first_one_step && pre)   // flat walks of the initial queue (later steps: enrolled by the previous scatter)
             hipLaunchKernelGGL(classify_kernel, dim3(grid_for(n)), dim3(BLOCK), 0, stream, ph->d_pos, ph->d_dir,
-                               ph->d_flags, in_queue, n, hits, fc->flat_q, count_cur, fc->flat_best);
+                               ph->d_flags, in_queue, n, hits, fc->flat_q, count_cur, fc->flat_best,
+                               bin_now ? keys : nullptr, bin_now ? order : nullptr);
         TraceArgs ta;
         ta.pos = ph->d_pos; ta.dir = ph->d_dir; ta.flags = ph->d_flags; ta.last_hit = ph->d_last_hit_triangles;
         ta.queue = in_queue; ta.n = n; ta.hits = hits; ta.next = next; ta.counters = counters; ta.order = nullptr;
@@ -3475,14 +3501,11 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
             ta.walk_hist = next + 16 + 2 * (size_t)(sc ? sc->n_layout : n);
             CHR_HIP_CHECK(hipMemsetAsync(ta.walk_hist, 0, 34 * 4, stream));
         }
-        if (sv.binned == 1 || (sv.binned == 2 && first_one_step && n >= kBinFirstMin)) {
-            // 16-bit radix sort of (direction cell, queue position); hits region:
-            // [hits n x int2][next + pad, 16 words][keys n][values n][walk hist 64 words]
-            // (device-driven slots bin only the first step, whose length the host knows)
-            if ((!sc || first_one_step) && pre) {
-                uint32_t *keys = next + 16, *order = keys + n;
-                hipLaunchKernelGGL(bin_key_kernel, dim3(grid_for(n)), dim3(BLOCK), 0, stream, ph->d_dir, in_queue, n,
-                                   keys, order);
+        if (bin_now) {
+            {
+                if (!first_one_step)   // the first step's keys came with its classification
+                    hipLaunchKernelGGL(bin_key_kernel, dim3(grid_for(n)), dim3(BLOCK), 0, stream, ph->d_dir, in_queue,
+                                       n, keys, order);
                 uint32_t *keys_out = sort_space, *vals_out = keys_out + n;
                 void *temp = (void *)(((uintptr_t)(vals_out + n) + 255) & ~(uintptr_t)255);
                 size_t temp_bytes = sort_temp_bytes16(n);
@@ -3694,12 +3717,13 @@ static int prop_bufs(uint32_t nphotons, int32_t ntpb, int32_t max_blocks, int ct
 }
 
 // queues (photon.py:242-250: clones interleaved, q[1] header = 1), step counters, flat-walk control words
-static int prop_start(const PropBufs &b, uint32_t nphotons, uint32_t true_nphotons, uint32_t ncopies, hipStream_t stream) {
-    if (b.fused) CHR_HIP_CHECK(hipMemsetAsync(b.fc.ctl, 0, 128, stream));
+// (done: the device-driven slot loop's done flag, zeroed too)
+static int prop_start(const PropBufs &b, uint32_t nphotons, uint32_t true_nphotons, uint32_t ncopies, hipStream_t stream,
+                      uint32_t *done = nullptr) {
+    ZeroWords z{{b.fused ? b.fc.ctl : nullptr, b.scratch, done}, {32u, 16u, 1u}};
     hipLaunchKernelGGL(init_queue_kernel, dim3(grid_for(nphotons)), dim3(BLOCK), 0, stream, b.q[0], b.q[1], nphotons,
-                       true_nphotons, ncopies);
+                       true_nphotons, ncopies, z);
     CHR_HIP_CHECK(hipGetLastError());
-    CHR_HIP_CHECK(hipMemsetAsync(b.scratch, 0, 64, stream));
     return CHR_OK;
 }
 
@@ -4125,11 +4149,10 @@ static int queue_prefix(const chr_geometry *g, const chr_photons *ph, uint32_t n
                         uint32_t ncopies, uint32_t *rng, uint32_t nslots, int32_t ntpb, int32_t max_steps,
                         int32_t use_weights, int32_t scatter_first, PropBufs &b, int ctx,
                         std::vector<hipEvent_t> &events, hipEvent_t prefix_done, hipStream_t ps) {
-    CHR_TRY(prop_start(b, nphotons, true_nphotons, ncopies, ps));
     uint32_t *ctl = nullptr;
     CHR_TRY(slot_ctl_get(2 * (size_t)max_steps + 8, &ctl, ctx));
     uint32_t *done = ctl + 2 * (size_t)max_steps;
-    CHR_HIP_CHECK(hipMemsetAsync(done, 0, 4, ps));
+    CHR_TRY(prop_start(b, nphotons, true_nphotons, ncopies, ps, done));
     b.fc.enrol_next = true;
     CHR_TRY(grow_events(events, SLOT_EVENTS));
     SlotCtl sc{ctl, ctl + 1, done, nphotons, max_steps, (uint32_t)ntpb * 16 * 8};
