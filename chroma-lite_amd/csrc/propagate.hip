@@ -3744,9 +3744,11 @@ struct SlotRun {
     hipEvent_t rng_ready = nullptr;    // the first RNG use waits for it
     hipEvent_t prefix_done = nullptr;  // slot 0's prefix was queued by queue_prefix and ends with this event
     int ctx = 0;
-    // called with each one-step slot's queue length as the host learns it
+    // called with each one-step slot's survivor count (the next slot's queue
+    // length) as the host learns it, read through out_ring (32 pinned words)
     // (chr_propagate_batches: queue the next batch's prefix once few photons remain)
     std::function<int(uint32_t)> on_length;
+    uint32_t *out_ring = nullptr;
 };
 
 // Device-driven steps: every slot's kernels read the queue length from the
@@ -3791,6 +3793,8 @@ static int device_slots(const chr_geometry *g, const chr_photons *ph, uint32_t n
                          &split, &b.fc, &sc);
         if (rc) return rc;
         CHR_HIP_CHECK(hipMemcpyAsync(ring + 2 * (k % 32), ctl + 2 * (size_t)k, 8, hipMemcpyDeviceToHost, stream));
+        if (run.on_length)   // the output queue's count header (+1)
+            CHR_HIP_CHECK(hipMemcpyAsync(run.out_ring + k % 32, b.q[cur ^ 1], 4, hipMemcpyDeviceToHost, stream));
         CHR_HIP_CHECK(hipEventRecord(ev[4], stream));
         b.fc.cur ^= 1;   // the step's scatter enrolled the next step's flat walks in the other list
         cur ^= 1;
@@ -3800,7 +3804,7 @@ static int device_slots(const chr_geometry *g, const chr_photons *ph, uint32_t n
             const uint32_t m = ring[2 * ((k - 1) % 32)], nk = ring[2 * ((k - 1) % 32) + 1];
             if (m != STEP_ONE) stop = true;   // the tail ran or the queue emptied: slot k is idle
             else n_ub = nk;                   // later queues are no longer
-            if (run.on_length) CHR_TRY(run.on_length(m == STEP_ONE ? nk : 0u));
+            if (run.on_length) CHR_TRY(run.on_length(m == STEP_ONE ? run.out_ring[(k - 1) % 32] - 1u : 0u));
         }
         k++;
     }
@@ -4134,9 +4138,10 @@ static size_t batch_lookahead() {
     return (size_t)(k < 0 ? 0 : (k > NCTX - 1 ? NCTX - 1 : k));
 }
 
-// CHR_BATCH_PREFIX_BELOW=n: queue the next batch's prefix once the running
-// batch's queue is below n photons (its late steps under-fill the chip); 0
-// (default): when the next batch starts, i.e. when this batch's tail starts
+// CHR_BATCH_PREFIX_BELOW=n: queue the next batch's prefix once a step of the
+// running batch leaves fewer than n survivors (n = nthreads_per_block * 128:
+// as soon as the next slot is known to be the tail); 0 (default): when the
+// next batch starts, i.e. once the host has seen the tail slot start
 static uint32_t batch_prefix_below() {
     const char *e = getenv("CHR_BATCH_PREFIX_BELOW");
     return e ? (uint32_t)strtoul(e, nullptr, 10) : 0u;
@@ -4200,7 +4205,7 @@ static int propagate_batches(const chr_geometry *g, const chr_photons *phs, cons
     CHR_TRY(batch_streams_get(&ts, &ps));
     const size_t nb = idx.size();
     std::vector<BatchHost> *pool = nullptr;
-    CHR_TRY(batch_host_get(nb, 128 + 2 * (size_t)max_steps + 8, &pool));
+    CHR_TRY(batch_host_get(nb, 128 + 2 * (size_t)max_steps + 8 + 32, &pool));   // + the survivor-count ring
     std::vector<BatchHost> &bh = *pool;
     // every context sized for the largest batch up front: no buffer is
     // reallocated while an earlier batch may still use it
@@ -4262,7 +4267,8 @@ static int propagate_batches(const chr_geometry *g, const chr_photons *phs, cons
         run.ctx = c;
         // the next batch's prefix as soon as this batch is down to its late,
         // under-occupied steps (CHR_BATCH_PREFIX_BELOW photons; 0: at the next batch's start)
-        if (prefix_below && queued == j + 1 && queued < nb && !aliases_earlier(queued, j))
+        if (prefix_below && queued == j + 1 && queued < nb && !aliases_earlier(queued, j)) {
+            run.out_ring = bh[j].pinned + 128 + 2 * (size_t)max_steps + 8;
             run.on_length = [&, j](uint32_t n) -> int {
                 if (queued == j + 1 && queued < nb && n < prefix_below) {
                     CHR_TRY(prefix(queued));
@@ -4270,6 +4276,7 @@ static int propagate_batches(const chr_geometry *g, const chr_photons *phs, cons
                 }
                 return CHR_OK;
             };
+        }
         uint32_t *ctl = nullptr;
         CHR_TRY(device_slots(g, phs + i, nphotons[i], d_rng_states, rng_nslots, ntpb, max_steps, use_weights,
                              scatter_first, b, run, stream, &ctl, &slots[j]));
