@@ -3,7 +3,7 @@
 hot path, chroma/gpu/photon.py:226-293) on a demo PMT detector.
 
 One "step" = one propagate of a fresh batch of isotropic photons (BASELINE.md
-section 3 source: centre point source, seed 20260102) to termination or
+section 3 source: centre point source, seed 20260102+rank) to termination or
 max_steps (default 1000, the Simulation.simulate default), launch shape of
 Simulation (nthreads_per_block=512, max_blocks=1024 -> 524,288 RNG slots).
 Photon inputs are resident in HBM before the timed region; each step restores
@@ -16,21 +16,31 @@ many propagate calls would (bit-identical photons and RNG states, tested in
 tests/test_gpu_batches.py) while each batch's multi-step tail -- as long as
 its longest-lived photon's serial chain -- runs on a second HIP stream under
 the next batch's first-step queueing, binning and BVH walk (which draw no
-random numbers).  detail.step_ms is then each call's time split over its steps.
+random numbers).  detail.step_ms is then each call's time split over its
+steps.  A short sequential run of the same steps follows, untimed for the
+headline, and is reported as detail.sequential (the figure a caller making one
+propagate call at a time gets).
 
-Multi-GPU: one process per GPU (torchrun), geometry replicated, photons
-sharded (each rank propagates its own batch: weak scaling, RNG subsequences
-disjoint per rank).  Each step ends with the hit-channel reduce: detected
-photons are histogrammed per PMT channel on the device and SUM-reduced over
-the ranks (RCCL, chroma.gpu.shard) -- the only exchange the path has.  The
-timed region is bracketed by barriers and the max over ranks is reported.
+Multi-GPU: one process per GPU.  Under torchrun (WORLD_SIZE set) this process
+is one rank; with --gpus N > 1 and no WORLD_SIZE, bench.py starts the N rank
+processes itself (before touching any GPU) and exits with the first failing
+rank's status.  The geometry is replicated, the photons sharded: --photons
+per GPU (weak scaling, the default) or --total-photons over all GPUs (strong
+scaling; C4 is --gpus 8 --total-photons 100000000).  Each rank draws disjoint
+RNG subsequences (rank*nslots + slot).  Each step ends with the hit-channel
+reduce: detected photons are histogrammed per PMT channel on the device and
+SUM-reduced over the ranks (RCCL, chroma.gpu.shard) -- the only exchange the
+path has.  The timed region is bracketed by barriers and the max over ranks
+is reported; value = photons of all ranks / that time.
 
 Parity: rank 0 runs the CPU oracle (cpu_baseline leg, the only place bench.py
-touches oracle/) on a bounded sample of the same photons with the same RNG
-initialisation, then propagates the SAME sample on the GPU and compares the
-two photon by photon (history flags, last-hit triangles and channels
+touches oracle/) on a bounded sample of its photons with the same RNG
+initialisation, as two batches in order, then propagates the SAME two batches
+on the GPU through the path the headline used (pipelined or sequential) and
+compares photon by photon (history flags, last-hit triangles and channels
 bit-exact; positions, directions, polarisations, times and wavelengths as a
-max relative difference) -- every bench line checks its own workload.
+max relative difference).  Ranks > 0 check a smaller sample of their own shard
+(their own photon seed and RNG subsequences): parity.per_rank.
 
 Roofline: the dominant kernel is trace_kernel, the
 BVH walk of every one-step launch.  It is bound by HBM/L2 latency-bandwidth on
@@ -40,14 +50,20 @@ with the average from HIP events around each trace launch on its stream, and
 the algorithmic bytes of section 8(d): per walk 16 * reference-BVH nodes +
 48 * reference triangles + 4, counted by the CPU oracle walking the REFERENCE
 BVH in the reference's DFS order on the cpu_baseline sample of the same
-workload, times the rays of the launch.  traffic = HBM bytes per trace launch
-from the rocprofv3 FETCH_SIZE/WRITE_SIZE passes of this workload; those
-counters cannot be read from inside this process, so the value is copied
-from the committed PMC summary (profiles/latest_pmc.json) and labelled so.
+workload, times the rays of the launch.  Every rank reports its own launches
+(roofline.per_rank).  traffic = HBM bytes per trace launch from the rocprofv3
+FETCH_SIZE/WRITE_SIZE passes of this workload and l2_hit_rate from its
+TCC_HIT/TCC_MISS pass; those counters cannot be read from inside this
+process, so they are copied from profiles/latest_pmc.json, which is stamped
+with the sha of the kernel sources it measured: a stamp that differs from
+this tree's sources is reported as stale.
 """
 import argparse
+import hashlib
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -59,6 +75,7 @@ import numpy as np  # noqa: E402
 METRIC = 'propagated photons/sec, 29k-PMT detector, 10M isotropic photons, 1/2/4/8 GPUs'
 HBM_PEAK_GBS = 8000.0
 PHOTON_SEED = 20260102
+PUBLISHED_29K = 2.5e6      # reference README, 29k PMTs, photons/s
 
 
 def _demo_detector(**kw):
@@ -102,6 +119,22 @@ def usable_cpus():
     except (OSError, ValueError):
         pass
     return n
+
+
+def kernel_source_sha():
+    """sha256 (16 hex) of the sources libchroma_amd.so is built from: the stamp
+    that ties a committed PMC record to the kernels it measured."""
+    h = hashlib.sha256()
+    csrc = os.path.join(ROOT, 'chroma-lite_amd', 'csrc')
+    inc = os.path.join(ROOT, 'include')
+    files = sorted(os.path.join(csrc, f) for f in os.listdir(csrc)
+                   if f.endswith(('.hip', '.h', '.cpp')) or f == 'Makefile')
+    files += sorted(os.path.join(inc, f) for f in os.listdir(inc) if f.endswith('.h'))
+    for p in files:
+        h.update(os.path.relpath(p, ROOT).encode())
+        with open(p, 'rb') as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
 
 
 def build_geometry(name, cache_dir):
@@ -156,6 +189,15 @@ def rng_first_subsequence(rank, nslots):
     return rank * nslots
 
 
+def photons_for_rank(args, rank, world):
+    """Photons this rank propagates per step: --photons (weak scaling) or its
+    contiguous share of --total-photons (strong scaling, chroma.gpu.shard)."""
+    if args.total_photons:
+        lo, hi = args.total_photons * rank // world, args.total_photons * (rank + 1) // world
+        return hi - lo
+    return args.photons
+
+
 def timed_loop(run, steps, warmup, dist, sync, group=1):
     """W untimed steps, then K timed steps bracketed by barrier + sync on both
     sides; run(m) performs m steps and returns their results (m > 1: one
@@ -169,7 +211,7 @@ def timed_loop(run, steps, warmup, dist, sync, group=1):
         dist.barrier()
     sync()
     t0 = time.perf_counter()
-    marks, results, per_step = [], [], []
+    results, per_step = [], []
     left = steps
     while left > 0:
         m = min(group, left)
@@ -183,94 +225,41 @@ def timed_loop(run, steps, warmup, dist, sync, group=1):
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if dist is not None:
-        import torch
-        dev = 'cuda' if (torch.cuda.is_available() and dist.get_backend() != 'gloo') else 'cpu'
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
+        elapsed = _allreduce(dist, elapsed, 'max')
     return elapsed, per_step, results
 
 
-def result_line(args, world, elapsed, per_step_s, detector_info, detail):
-    total = args.photons * world * args.steps
-    value = total / elapsed
+def _allreduce(dist, x, op):
+    import torch
+    dev = 'cuda' if (torch.cuda.is_available() and dist.get_backend() != 'gloo') else 'cpu'
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX if op == 'max' else dist.ReduceOp.SUM)
+    return float(t.item())
+
+
+def result_line(args, world, elapsed, per_step_s, total_photons, detector_info, detail):
+    value = total_photons / elapsed
+    workload = ('GPUPhotons.propagate of %s isotropic photons per step on %s, max_steps=%d, launch shape %dx%d '
+                '(%d RNG slots)' % (
+                    ('%d in total over %d GPUs' % (args.total_photons, world)) if args.total_photons
+                    else ('%d per GPU' % args.photons), DETECTORS[args.detector][0], args.max_steps,
+                    args.nthreads_per_block, args.max_blocks, args.nthreads_per_block * args.max_blocks))
+    cfg = {'workload': workload, 'detector': args.detector, 'max_steps': args.max_steps,
+           'parallelism': 'photon-sharded x%d, geometry replicated' % world}
+    if args.total_photons:
+        cfg['total_photons'] = args.total_photons
+    else:
+        cfg['photons_per_gpu'] = args.photons
     return {
         'metric': METRIC, 'value': value, 'unit': 'photons/s', 'n_gpus': world, 'steps': args.steps,
         'warmup': args.warmup, 'ms_per_step': 1e3 * elapsed / args.steps, 'higher_is_better': True,
-        'scaling': 'weak', 'vs_baseline': (value / 2.5e6) if args.detector == '29k' else None,
+        'scaling': 'strong' if args.total_photons else 'weak',
+        'vs_baseline': (value / PUBLISHED_29K) if args.detector == '29k' else None,
         'dtype': 'f32', 'data': 'synthetic isotropic point source (BASELINE.md section 3), seed %d+rank' % PHOTON_SEED,
-        'config': dict({'workload': 'GPUPhotons.propagate of %d isotropic photons per GPU per step on %s, '
-                                    'max_steps=%d, launch shape %dx%d (%d RNG slots)' % (
-                                        args.photons, DETECTORS[args.detector][0], args.max_steps,
-                                        args.nthreads_per_block, args.max_blocks,
-                                        args.nthreads_per_block * args.max_blocks),
-                        'detector': args.detector, 'photons_per_gpu': args.photons, 'max_steps': args.max_steps,
-                        'parallelism': 'photon-sharded x%d, geometry replicated' % world}, **detector_info),
+        'config': dict(cfg, **detector_info),
         'detail': dict({'step_ms': [round(1e3 * s, 3) for s in per_step_s]}, **detail),
         'roofline': None, 'cpu_baseline': None, 'parity': None,
     }
-
-
-def cpu_baseline(packed, photons, nslots, ntpb, max_blocks, max_steps, seed, budget_s, threads):
-    """Oracle (plain C port of the reference kernel, OpenMP) on a bounded
-    sample of the same workload; also returns the oracle's photons (the parity
-    reference) and its walk counts on the reference BVH (roofline bytes)."""
-    sys.path.insert(0, os.path.join(ROOT, 'oracle'))
-    import oracle
-    from chroma.event import Photons
-    n = 2000
-    while True:
-        sample = Photons(photons.pos[:n], photons.dir[:n], photons.pol[:n], photons.wavelengths[:n])
-        host = oracle.HostPhotons(sample)
-        st = oracle.rng_init(nslots, seed=seed)
-        t0 = time.time()
-        stats = oracle.propagate(packed, host, st, nslots, ntpb, max_blocks, max_steps, threads=threads)
-        dt = time.time() - t0
-        if dt > budget_s / 4 or n * 4 > len(photons.pos):
-            break
-        n = int(min(len(photons.pos), n * max(2.0, min(8.0, (budget_s / 2) / max(dt, 1e-3)))))
-    b_alg = 120.0 + (16.0 * stats['nodes_visited'] + 48.0 * stats['tris_tested'] + 4.0 * stats['traversals']) / n
-    cpu = dict(value=n / dt, unit='photons/s', cores=threads, kind='port',
-               sample='%d of the same isotropic photons, same geometry and launch shape, max_steps=%d; %.1fs on %d '
-                      'threads (nproc %d)' % (n, max_steps, dt, threads, os.cpu_count() or 0))
-    return cpu, b_alg, stats, n, host
-
-
-def gpu_parity(gdet, photons, n, host, args, solid_map, s2c):
-    """Propagate the oracle's sample on the GPU (same RNG initialisation, same
-    launch shape) and compare photon by photon."""
-    from chroma import gpu
-    from chroma.event import Photons
-    sample = Photons(photons.pos[:n], photons.dir[:n], photons.pol[:n], photons.wavelengths[:n])
-    nslots = args.nthreads_per_block * args.max_blocks
-    gp = gpu.GPUPhotons(sample, copy_flags=True, copy_triangles=False, copy_weights=False)
-    gp.propagate(gdet, gpu.get_rng_states(nslots, seed=args.seed), nthreads_per_block=args.nthreads_per_block,
-                 max_blocks=args.max_blocks, max_steps=args.max_steps)
-    got = gp.get()
-
-    def channel(flags, last_hit):
-        ch = np.full(len(flags), -1, np.int64)
-        det = ((flags & 4) != 0) & (last_hit > -1)
-        ch[det] = s2c[solid_map[last_hit[det]]]
-        return ch
-
-    def max_rel(a, b):
-        a = np.asarray(a, np.float64)
-        b = np.asarray(b, np.float64)
-        return float(np.max(np.abs(a - b) / np.maximum(np.abs(b), 1e-30))) if a.size else 0.0
-
-    flags_eq = bool(np.array_equal(got.flags, host.flags))
-    hits_eq = bool(np.array_equal(got.last_hit_triangles, host.last_hit_triangles))
-    ch_gpu, ch_ref = channel(got.flags, got.last_hit_triangles), channel(host.flags, host.last_hit_triangles)
-    rel = max(max_rel(got.pos, host.pos), max_rel(got.t, host.t), max_rel(got.wavelengths, host.wavelengths))
-    dp = max(float(np.max(np.abs(got.dir - host.dir))) if n else 0.0,
-             float(np.max(np.abs(got.pol - host.pol))) if n else 0.0)
-    return {'n': int(n), 'flags_equal': flags_eq, 'last_hit_equal': hits_eq,
-            'channel_equal': bool(np.array_equal(ch_gpu, ch_ref)),
-            'flags_mismatches': int(np.count_nonzero(got.flags != host.flags)),
-            'detected': int(np.count_nonzero(ch_ref >= 0)), 'max_rel': rel, 'dir_pol_max_abs': dp,
-            'binned_first_step': bool(n >= (1 << 20)),
-            'stack_overflows': int(gp.last_stats.stack_overflows)}
 
 
 def _kernel_info(native):
@@ -280,54 +269,374 @@ def _kernel_info(native):
         return 'unavailable: %s' % e
 
 
-def roofline(args, trace_ms, trace_launches, trace_rays, ref, launch_ms):
-    """roofline object of the bench line for the dominant kernel (trace_kernel)."""
-    launches = max(1, trace_launches)
-    rays_per_launch = trace_rays / launches
-    avg_launch_s = trace_ms / launches / 1e3
+def pmc_record(args):
+    """The committed PMC summary of this workload (profiles/latest_pmc.json):
+    (record, note) -- note says why it is not used or that it is stale."""
+    pmc_path = os.path.join(ROOT, 'profiles', 'latest_pmc.json')
+    if not os.path.exists(pmc_path):
+        return None, 'no profiles/latest_pmc.json'
+    with open(pmc_path) as f:
+        pmc = json.load(f)
+    w = pmc.get('workload', {})
+    if (w.get('detector'), w.get('photons'), w.get('max_steps')) != (args.detector, args.photons, args.max_steps) \
+            or pmc.get('kernel') != 'chr::trace_kernel':
+        return None, 'profiles/latest_pmc.json measured another workload'
+    return pmc, None
+
+
+def roofline(args, reports, ref):
+    """roofline object of the bench line for the dominant kernel (trace_kernel):
+    rank 0's launches as the headline, every rank's in per_rank."""
     per_walk = (16.0 * ref['nodes_visited'] + 48.0 * ref['tris_tested']) / ref['traversals'] + 4.0
-    alg_per_launch = rays_per_launch * per_walk
-    achieved = alg_per_launch / avg_launch_s / 1e9 if avg_launch_s > 0 else 0.0
-    lm = np.asarray(launch_ms, np.float64)
+
+    def of(rep):
+        launches = max(1, rep['trace_launches'])
+        rays_per_launch = rep['trace_rays'] / launches
+        avg_launch_s = rep['trace_ms'] / launches / 1e3
+        alg = rays_per_launch * per_walk
+        ach = alg / avg_launch_s / 1e9 if avg_launch_s > 0 else 0.0
+        return alg, rays_per_launch, avg_launch_s, ach
+
+    r0 = reports[0]
+    alg, rays_per_launch, avg_launch_s, achieved = of(r0)
+    lm = np.asarray(r0['launch_ms'], np.float64)
     rl = {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
           'frac': achieved / HBM_PEAK_GBS, 'traffic': None,
           'kernel': 'chr::trace_kernel (BVH walk of the one-step launches)',
           'basis': 'SURVEY 8(d): 16 B x reference-BVH nodes + 48 B x triangles + 4 B per walk '
                    '(oracle, reference DFS order, on the cpu_baseline sample)',
-          'alg_bytes_per_launch': alg_per_launch, 'alg_bytes_per_walk': per_walk,
+          'alg_bytes_per_launch': alg, 'alg_bytes_per_walk': per_walk,
           'rays_per_launch': rays_per_launch, 'avg_launch_ms': 1e3 * avg_launch_s,
-          'launches_timed': trace_launches,
+          'launches_timed': r0['trace_launches'],
           'launch_ms_min': float(lm.min()) if lm.size else None,
           'launch_ms_median': float(np.median(lm)) if lm.size else None,
           'launch_ms_max': float(lm.max()) if lm.size else None,
           'reference_bvh_nodes_per_walk': ref['nodes_visited'] / ref['traversals'],
-          'reference_bvh_triangles_per_walk': ref['tris_tested'] / ref['traversals']}
-    pmc_path = os.path.join(ROOT, 'profiles', 'latest_pmc.json')
-    if os.path.exists(pmc_path):
-        with open(pmc_path) as f:
-            pmc = json.load(f)
-        w = pmc.get('workload', {})
-        if (w.get('detector'), w.get('photons'), w.get('max_steps')) == (args.detector, args.photons, args.max_steps) \
-                and pmc.get('kernel') == 'chr::trace_kernel' and 'hbm_bytes_per_launch' in pmc:
-            rl['traffic'] = pmc['hbm_bytes_per_launch']
-            rl['traffic_unit'] = 'bytes/launch (FETCH_SIZE x2 + WRITE_SIZE)'
-            rl['traffic_source'] = 'copied, not measured in this run: %s (%s)' % (
-                os.path.relpath(pmc_path, ROOT), pmc.get('source'))
+          'reference_bvh_triangles_per_walk': ref['tris_tested'] / ref['traversals'],
+          'l2_hit_rate': None}
+    if len(reports) > 1:
+        rl['per_rank'] = []
+        for rep in reports:
+            a, rpl, avg, ach = of(rep)
+            rl['per_rank'].append({'rank': rep['rank'], 'avg_launch_ms': 1e3 * avg, 'rays_per_launch': rpl,
+                                   'launches_timed': rep['trace_launches'], 'achieved': ach,
+                                   'frac': ach / HBM_PEAK_GBS})
+    pmc, note = pmc_record(args)
+    sha = kernel_source_sha()
+    rl['kernel_source_sha'] = sha
+    if pmc is None:
+        rl['traffic_source'] = note
+        return rl
+    stamp = pmc.get('kernel_source_sha')
+    stale = stamp != sha
+    if 'hbm_bytes_per_launch' in pmc:
+        rl['traffic'] = pmc['hbm_bytes_per_launch']
+        rl['traffic_unit'] = 'bytes/launch (FETCH_SIZE x2 + WRITE_SIZE)'
+    l2 = pmc.get('l2_hit_rate', {}).get('chr::trace_kernel')
+    if l2 is not None:
+        rl['l2_hit_rate'] = l2
+    rl['traffic_source'] = '%s: profiles/latest_pmc.json (%s; commit %s, kernel_source_sha %s%s)' % (
+        'STALE (kernel sources changed since the PMC passes)' if stale else 'copied, same kernel sources',
+        pmc.get('source'), pmc.get('commit'), stamp,
+        '' if not stale else ' != this tree %s' % sha)
+    rl['traffic_stale'] = stale
     return rl
 
 
-def main():
-    ap = argparse.ArgumentParser(description=__doc__)
-    ap.add_argument('--gpus', type=int, default=1)
+class PropagateWorkload(object):
+    """One rank's share of the bench: geometry on its GPU, its photon batches
+    resident in HBM, and the steps.  bench.py's rank logic (timing, reduces,
+    the line) only calls the methods below."""
+
+    def __init__(self, args, rank, world, local, dist, nphotons):
+        import torch
+        from chroma import gpu
+        from chroma.gpu import gpuarray as ga
+        from chroma.photon_source import isotropic
+        from types import SimpleNamespace
+        self.args, self.rank, self.world, self.local, self.nphotons = args, rank, world, local, nphotons
+        self.torch = torch
+        self.det = shared_geometry(args.detector, args.cache_dir, rank, dist)
+        t0 = time.time()
+        self.gdet = gpu.GPUDetector(self.det)
+        log('rank %d: geometry on device in %.1fs (%.2f GB)' % (rank, time.time() - t0,
+                                                               self.gdet.device_bytes() / 1e9))
+        self.nslots = args.nthreads_per_block * args.max_blocks
+        self.rng = gpu.get_rng_states(self.nslots, seed=args.seed,
+                                      first_subsequence=rng_first_subsequence(rank, self.nslots))
+        self.photons = isotropic(nphotons, seed=PHOTON_SEED + rank)
+        ph = self.photons
+        self.pristine = SimpleNamespace(
+            pos=ga.to_gpu(gpu.to_float3(ph.pos)), dir=ga.to_gpu(gpu.to_float3(ph.dir)),
+            pol=ga.to_gpu(gpu.to_float3(ph.pol)), wavelengths=ga.to_gpu(ph.wavelengths),
+            t=ga.to_gpu(ph.t), flags=ga.to_gpu(ph.flags), evidx=ga.to_gpu(ph.evidx), true_nphotons=nphotons)
+        torch.cuda.synchronize()
+        self.counts = ga.zeros(self.gdet.nchannels, np.uint32)
+        self.reduced = {}
+        self.group = max(1, min(args.steps, args.pipeline_depth)) if args.pipeline else 1
+        # the batches' device arrays, allocated once before any timing (a step
+        # restores its batch from the device-resident source, D2D, inside the
+        # timed region -- what GPUPhotons(pristine, ...) does, without the allocation)
+        self.pool = [gpu.GPUPhotons(self.pristine, copy_flags=True, copy_triangles=False, copy_weights=False)
+                     for _ in range(max(self.group, args.warmup, 2 if args.pipeline else 1))]
+
+    def sync(self):
+        self.torch.cuda.synchronize()
+
+    def _restore(self, gp):
+        for f in ('pos', 'dir', 'pol', 'wavelengths', 't', 'flags', 'evidx'):
+            getattr(gp, f).tensor.copy_(getattr(self.pristine, f).tensor)
+        gp.last_hit_triangles.fill(-1)
+        gp.weights.fill(1.0)
+
+    def run(self, m, pipeline=None):
+        """m steps: m fresh copies of the source batch propagated with one
+        rng_states -- pipelined (gpu.propagate_batches: each batch's tail runs
+        on a second stream while the next batch starts; results identical to m
+        propagate calls) unless --no-pipeline -- then each batch's hit-channel
+        reduce."""
+        import ctypes
+        from chroma import gpu
+        from chroma.gpu import _native, shard
+        from chroma.gpu.tools import current_stream
+        args = self.args
+        pipeline = args.pipeline if pipeline is None else pipeline
+        gps = self.pool[:m]
+        for gp in gps:
+            self._restore(gp)
+        kw = dict(nthreads_per_block=args.nthreads_per_block, max_blocks=args.max_blocks, max_steps=args.max_steps)
+        if pipeline and m > 1:
+            sts = list(gpu.propagate_batches(gps, self.gdet, self.rng, **kw))
+        else:
+            sts = []
+            for gp in gps:
+                gp.propagate(self.gdet, self.rng, **kw)
+                sts.append(gp.last_stats)
+        for gp in gps:
+            # hit-channel reduce: detected photons per PMT channel on each rank,
+            # SUM-reduced over ranks (RCCL for N > 1)
+            self.counts.fill(0)
+            _native.call('chr_channel_hit_counts', ctypes.byref(gp._desc()), 0, self.nphotons, 0x4,
+                         self.gdet.solid_id_map.gpudata, self.gdet.solid_id_to_channel_index_gpu.gpudata,
+                         self.counts.gpudata, self.gdet.nchannels, current_stream())
+            self.reduced['counts'] = shard.allreduce_channel_counts(self.counts.tensor)
+        self.reduced['gp'] = gps[-1]
+        return sts
+
+    def run_sequential(self, m):
+        return self.run(m, pipeline=False)
+
+    def rank_report(self, stats):
+        """This rank's own numbers from the timed steps' stats."""
+        launch_ms = [float(s.trace_launch_ms[i]) for s in stats for i in range(s.trace_ms_n)]
+        gp = self.reduced.get('gp')
+        return {'rank': self.rank, 'photons_per_step': self.nphotons,
+                'device': self.torch.cuda.get_device_properties(self.local).name, 'local_rank': self.local,
+                'host': socket.gethostname(),
+                'kernel_ms': sum(s.kernel_ms for s in stats), 'launches': sum(s.launches for s in stats),
+                'host_steps': sum(s.steps_run for s in stats), 'host_syncs': sum(s.host_syncs for s in stats),
+                'trace_ms': sum(s.trace_ms for s in stats), 'trace_launches': sum(s.trace_launches for s in stats),
+                'trace_rays': sum(s.trace_rays for s in stats), 'launch_ms': launch_ms,
+                'launch_rays': [int(stats[0].trace_launch_rays[i]) for i in range(stats[0].trace_ms_n)]
+                if stats else [],
+                'overflows': sum(s.stack_overflows for s in stats), 'flat': sum(s.flat_walks for s in stats),
+                'flat_whole': sum(s.flat_walks_whole for s in stats),
+                'detected_last_step': int(((gp.flags.get() & 4) != 0).sum()) if gp is not None else 0,
+                'channel_hits_all_ranks': int(self.reduced['counts'].sum().item()) if 'counts' in self.reduced
+                else 0,
+                'tail': [{'ms': round(s.tail_ms, 3), 'photons': int(s.tail_photons),
+                          'max_steps': int(s.tail_max_steps),
+                          'slowest_photon_ms': round(s.tail_max_cycles / 1e5, 3),
+                          'slowest_photon_steps': int(s.tail_slowest_steps),
+                          'long_photons': int(s.tail_long_photons),
+                          'long_us_per_step': round(s.tail_long_ticks / 100.0 / max(1, s.tail_long_steps), 3),
+                          'long_walk_us_per_step': round(s.tail_long_walk_ticks / 100.0 /
+                                                         max(1, s.tail_long_steps), 3),
+                          'long_walk_iterations_per_step': round(s.tail_long_walk_iterations /
+                                                                 max(1, s.tail_long_steps), 2)} for s in stats]}
+
+    def untimed_passes(self):
+        """After timing: the counting variant (own-layout bytes, SIMD efficiency)
+        and, with CHROMA_DEVICE_PROFILE=1, the device region profile."""
+        from chroma.gpu import _native
+        out = {}
+        if not self.args.no_count:
+            prev = os.environ.get('CHR_PROPAGATE_VARIANT')
+            os.environ['CHR_PROPAGATE_VARIANT'] = '5'
+            cst = self.run(1)[0]
+            self.reduced.pop('gp', None)
+            if prev is None:
+                del os.environ['CHR_PROPAGATE_VARIANT']
+            else:
+                os.environ['CHR_PROPAGATE_VARIANT'] = prev
+            self.sync()
+            if cst.traversals:
+                out['own_layout'] = {
+                    'bytes_per_walk': (96.0 * cst.nodes_visited + 64.0 * cst.triangles_tested +
+                                       52.0 * cst.traversals) / cst.traversals,
+                    'nodes_per_photon': cst.nodes_visited / self.nphotons,
+                    'triangles_per_photon': cst.triangles_tested / self.nphotons,
+                    'traversals_per_photon': cst.traversals / self.nphotons,
+                    'simd_efficiency_nodes': cst.nodes_visited / max(1.0, 64.0 * cst.wave_node_steps),
+                    'simd_efficiency_triangles': cst.triangles_tested / max(1.0, 64.0 * cst.wave_triangle_steps),
+                    'stack_overflows': int(cst.stack_overflows)}
+        if _native.DEVICE_PROFILE:
+            from chroma.gpu import profiler
+            profiler.device_reset()
+            self.run(1)
+            self.reduced.pop('gp', None)
+            self.sync()
+            out['device_profile'] = {'regions': profiler.device_fetch(),
+                                     'clock_khz': profiler.device_fetch.clock_khz,
+                                     'library': os.path.basename(_native.library_path()),
+                                     'cycles': 'lane-cycles of the shader clock (include/chroma_amd.h CHR_PROF_*)'}
+        return out
+
+    def device_info(self):
+        from chroma.gpu import _native
+        props = self.torch.cuda.get_device_properties(self.local)
+        free_b, total_b = self.torch.cuda.mem_get_info(self.local)
+        return {'device': {'name': props.name, 'arch': getattr(props, 'gcnArchName', ''),
+                           'compute_units': props.multi_processor_count,
+                           'hbm_total_gb': total_b / 1e9, 'hbm_free_gb_after': free_b / 1e9},
+                'kernels': _kernel_info(_native)}
+
+    def detector_info(self):
+        return {'triangles': len(self.det.mesh.triangles), 'bvh_nodes': len(self.det.bvh.nodes),
+                'channels': self.det.num_channels()}
+
+    # ------------------------------------------------------------ oracle checks
+    def _oracle_batches(self, n, threads):
+        """The oracle on this rank's first n photons as two batches in order
+        (the RNG states carried from one to the next, as two propagate calls),
+        from the rank's own RNG subsequences.  Returns (hosts, walk stats, seconds)."""
+        sys.path.insert(0, os.path.join(ROOT, 'oracle'))
+        import oracle
+        from chroma.event import Photons
+        from chroma.gpu.packing import PackedGeometry
+        if not hasattr(self, '_packed'):
+            self._packed = PackedGeometry(self.det)
+        a = self.args
+        ph = self.photons
+        cuts = [0, n // 2, n]
+        hosts = [oracle.HostPhotons(Photons(ph.pos[lo:hi], ph.dir[lo:hi], ph.pol[lo:hi], ph.wavelengths[lo:hi]))
+                 for lo, hi in zip(cuts[:-1], cuts[1:])]
+        st = oracle.rng_init(self.nslots, seed=a.seed, first_subsequence=rng_first_subsequence(self.rank, self.nslots))
+        tot = {}
+        t0 = time.time()
+        for h in hosts:
+            s = oracle.propagate(self._packed, h, st, self.nslots, a.nthreads_per_block, a.max_blocks, a.max_steps,
+                                 threads=threads)
+            for k, v in s.items():
+                tot[k] = tot.get(k, 0) + v
+        return hosts, tot, time.time() - t0
+
+    def cpu_baseline(self, budget_s, threads):
+        """Oracle (plain C port of the reference kernel, OpenMP) on a bounded
+        sample of the same workload (grown until it takes ~budget/4 .. budget/2
+        seconds); also returns the oracle's photons (the parity reference) and
+        its walk counts on the reference BVH (roofline bytes)."""
+        n = 4000
+        while True:
+            hosts, stats, dt = self._oracle_batches(n, threads)
+            if dt > budget_s / 4 or n * 4 > self.nphotons:
+                break
+            n = int(min(self.nphotons, n * max(2.0, min(8.0, (budget_s / 2) / max(dt, 1e-3)))))
+        cpu = dict(value=n / dt, unit='photons/s', cores=threads, kind='port',
+                   sample='%d of the same isotropic photons (two propagate calls of %d and %d, one RNG state set), '
+                          'same geometry and launch shape, max_steps=%d; %.1fs on %d threads (nproc %d)' % (
+                              n, n // 2, n - n // 2, self.args.max_steps, dt, threads, os.cpu_count() or 0))
+        return cpu, stats, n, hosts
+
+    def gpu_parity(self, n, hosts, pipeline):
+        """Propagate the oracle's two batches on the GPU (same RNG initialisation,
+        same launch shape) -- through propagate_batches when the headline is
+        pipelined, one propagate call each otherwise -- and compare photon by photon."""
+        from chroma import gpu
+        from chroma.event import Photons
+        a = self.args
+        ph = self.photons
+        cuts = [0, n // 2, n]
+        gps = [gpu.GPUPhotons(Photons(ph.pos[lo:hi], ph.dir[lo:hi], ph.pol[lo:hi], ph.wavelengths[lo:hi]),
+                              copy_flags=True, copy_triangles=False, copy_weights=False)
+               for lo, hi in zip(cuts[:-1], cuts[1:])]
+        rng = gpu.get_rng_states(self.nslots, seed=a.seed,
+                                 first_subsequence=rng_first_subsequence(self.rank, self.nslots))
+        kw = dict(nthreads_per_block=a.nthreads_per_block, max_blocks=a.max_blocks, max_steps=a.max_steps)
+        if pipeline:
+            sts = gpu.propagate_batches(gps, self.gdet, rng, **kw)
+        else:
+            sts = []
+            for gp in gps:
+                gp.propagate(self.gdet, rng, **kw)
+                sts.append(gp.last_stats)
+        got = [gp.get() for gp in gps]
+        solid_map = np.asarray(self.det.solid_id, np.int64)
+        s2c = np.asarray(self.det.solid_id_to_channel_index, np.int64)
+
+        def cat(objs, f):
+            return np.concatenate([getattr(o, f) for o in objs])
+
+        def channel(flags, last_hit):
+            ch = np.full(len(flags), -1, np.int64)
+            det = ((flags & 4) != 0) & (last_hit > -1)
+            ch[det] = s2c[solid_map[last_hit[det]]]
+            return ch
+
+        def max_rel(x, y):
+            x = np.asarray(x, np.float64)
+            y = np.asarray(y, np.float64)
+            return float(np.max(np.abs(x - y) / np.maximum(np.abs(y), 1e-30))) if x.size else 0.0
+
+        gf, hf = cat(got, 'flags'), cat(hosts, 'flags')
+        gl, hl = cat(got, 'last_hit_triangles'), cat(hosts, 'last_hit_triangles')
+        ch_gpu, ch_ref = channel(gf, gl), channel(hf, hl)
+        rel = max(max_rel(cat(got, f), cat(hosts, f)) for f in ('pos', 't', 'wavelengths'))
+        dp = max(float(np.max(np.abs(cat(got, f) - cat(hosts, f)))) if n else 0.0 for f in ('dir', 'pol'))
+        return {'rank': self.rank, 'n': int(n), 'batches': [int(c) for c in np.diff(cuts)],
+                'path': 'propagate_batches (pipelined)' if pipeline else 'propagate (sequential)',
+                'rng_first_subsequence': rng_first_subsequence(self.rank, self.nslots),
+                'photon_seed': PHOTON_SEED + self.rank,
+                'flags_equal': bool(np.array_equal(gf, hf)), 'last_hit_equal': bool(np.array_equal(gl, hl)),
+                'channel_equal': bool(np.array_equal(ch_gpu, ch_ref)),
+                'flags_mismatches': int(np.count_nonzero(gf != hf)),
+                'detected': int(np.count_nonzero(ch_ref >= 0)), 'max_rel': rel, 'dir_pol_max_abs': dp,
+                'binned_first_step': bool(n // 2 >= (1 << 20)),
+                'stack_overflows': int(sum(s.stack_overflows for s in sts))}
+
+    def check(self, full, budget_s, threads, sample):
+        """Rank 0 (full): cpu_baseline + parity on the adaptive sample.  Other
+        ranks: parity on `sample` photons of their own shard.  Returns
+        (cpu_baseline or None, oracle walk stats, parity)."""
+        if full:
+            cpu, stats, n, hosts = self.cpu_baseline(budget_s, threads)
+        else:
+            n = min(self.nphotons, sample)
+            hosts, stats, _ = self._oracle_batches(n, threads)
+            cpu = None
+        return cpu, stats, self.gpu_parity(n, hosts, self.args.pipeline)
+
+
+WORKLOAD = PropagateWorkload     # replaced by tests/bench_stub_main.py (CPU rehearsal of the rank logic)
+
+
+def parse_args(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument('--gpus', type=int, default=1,
+                    help='GPUs (ranks); > 1 without WORLD_SIZE in the environment starts the ranks itself')
     ap.add_argument('--steps', type=int, default=3)
     ap.add_argument('--warmup', type=int, default=1)
-    ap.add_argument('--photons', type=int, default=10_000_000, help='photons per GPU per step')
+    ap.add_argument('--photons', type=int, default=10_000_000, help='photons per GPU per step (weak scaling)')
+    ap.add_argument('--total-photons', type=int, default=0,
+                    help='photons per step over all GPUs (strong scaling; overrides --photons)')
     ap.add_argument('--detector', default='29k', choices=sorted(DETECTORS))
     ap.add_argument('--max-steps', type=int, default=1000)
     ap.add_argument('--nthreads-per-block', type=int, default=512)
     ap.add_argument('--max-blocks', type=int, default=1024)
     ap.add_argument('--seed', type=int, default=1)
     ap.add_argument('--cpu-budget', type=float, default=20.0, help='seconds of CPU-baseline work')
+    ap.add_argument('--rank-parity-photons', type=int, default=1 << 17,
+                    help='photons of its own shard each rank > 0 checks against the oracle')
     ap.add_argument('--no-cpu-baseline', action='store_true', help='also skips the parity check')
     ap.add_argument('--no-count', action='store_true',
                     help='skip the untimed counting pass (profiling runs: keeps rocprof averages to one variant)')
@@ -335,193 +644,169 @@ def main():
                     help='one synchronous propagate per step (no tail / next-batch overlap)')
     ap.add_argument('--pipeline-depth', type=int, default=32,
                     help='steps per pipelined call (each holds its own copy of the batch in HBM)')
+    ap.add_argument('--sequential-steps', type=int, default=5,
+                    help='after the pipelined headline: this many one-call-per-step steps, timed the same way '
+                         '(detail.sequential; 0: skip)')
     ap.add_argument('--cache-dir', default=os.environ.get('CHROMA_BENCH_CACHE', '/tmp/chroma_bench_cache'))
-    args = ap.parse_args()
+    args = ap.parse_args(argv)
+    if args.gpus < 1:
+        ap.error('--gpus must be >= 1')
+    if args.total_photons and args.total_photons < args.gpus:
+        ap.error('--total-photons must give every GPU at least one photon')
+    return args
 
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n, cmd):
+    """Start n rank processes of `cmd` (this script, same arguments) with the
+    torchrun environment, one GPU each (LOCAL_RANK), and wait.  Called before
+    this process touches any GPU.  A rank that fails ends the others; the exit
+    status is the first failing rank's (0 when all succeed)."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), GROUP_RANK='0')
+        procs.append(subprocess.Popen(cmd, env=env))
+    rc = 0
+    alive = list(procs)
+    while alive:
+        for p in list(alive):
+            c = p.poll()
+            if c is None:
+                continue
+            alive.remove(p)
+            if c != 0 and rc == 0:
+                rc = c if c > 0 else 128 - c
+                log('bench.py: rank %d exited with %d; stopping the other ranks' % (procs.index(p), c))
+                for q in alive:
+                    q.terminate()
+        time.sleep(0.05)
+    for p in procs:
+        p.wait()
+    return rc
+
+
+def rank_env():
+    return (int(os.environ.get('WORLD_SIZE', '1')), int(os.environ.get('RANK', '0')),
+            int(os.environ.get('LOCAL_RANK', '0')))
+
+
+def run_rank(args):
+    world, rank, local = rank_env()
+    if world != args.gpus:
+        raise SystemExit('bench.py: --gpus %d but WORLD_SIZE=%d: the line would mislabel the run' % (args.gpus, world))
     import torch
-    world = int(os.environ.get('WORLD_SIZE', '1'))
-    rank = int(os.environ.get('RANK', '0'))
-    local = int(os.environ.get('LOCAL_RANK', '0'))
-    torch.cuda.set_device(local)
     dist = None
+    on_gpu = torch.cuda.is_available()
+    if on_gpu:
+        torch.cuda.set_device(local)
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
-
-    from chroma import gpu
-    from chroma.gpu import gpuarray as ga
-    from chroma.gpu.packing import PackedGeometry
-    from chroma.photon_source import isotropic
-    from types import SimpleNamespace
-
-    det = shared_geometry(args.detector, args.cache_dir, rank, dist)
-    t0 = time.time()
-    gdet = gpu.GPUDetector(det)
-    log('rank %d: geometry on device in %.1fs (%.2f GB)' % (rank, time.time() - t0, gdet.device_bytes() / 1e9))
-    nslots = args.nthreads_per_block * args.max_blocks
-    rng = gpu.get_rng_states(nslots, seed=args.seed, first_subsequence=rng_first_subsequence(rank, nslots))
-
-    photons = isotropic(args.photons, seed=PHOTON_SEED + rank)
-    pristine = SimpleNamespace(
-        pos=ga.to_gpu(gpu.to_float3(photons.pos)), dir=ga.to_gpu(gpu.to_float3(photons.dir)),
-        pol=ga.to_gpu(gpu.to_float3(photons.pol)), wavelengths=ga.to_gpu(photons.wavelengths),
-        t=ga.to_gpu(photons.t), flags=ga.to_gpu(photons.flags), evidx=ga.to_gpu(photons.evidx),
-        true_nphotons=args.photons)
-    torch.cuda.synchronize()
-
-    import ctypes
-    from chroma.gpu import _native, shard
-    from chroma.gpu.tools import current_stream
-    counts = ga.zeros(gdet.nchannels, np.uint32)
-    reduced = {}
-
-    group = max(1, min(args.steps, args.pipeline_depth)) if args.pipeline else 1
-    # the batches' device arrays, allocated once before any timing (a step
-    # restores its batch from the device-resident source, D2D, inside the timed
-    # region -- what GPUPhotons(pristine, ...) does, without the allocation)
-    pool = [gpu.GPUPhotons(pristine, copy_flags=True, copy_triangles=False, copy_weights=False)
-            for _ in range(max(group, args.warmup, 2 if args.pipeline else 1))]
-
-    def restore(gp):
-        for f in ('pos', 'dir', 'pol', 'wavelengths', 't', 'flags', 'evidx'):
-            getattr(gp, f).tensor.copy_(getattr(pristine, f).tensor)
-        gp.last_hit_triangles.fill(-1)
-        gp.weights.fill(1.0)
-
-    def run(m):
-        """m steps: m fresh copies of the source batch propagated with one
-        rng_states -- pipelined (gpu.propagate_batches: each batch's tail runs
-        on a second stream while the next batch starts; results identical to m
-        propagate calls) unless --no-pipeline -- then each batch's hit-channel
-        reduce."""
-        gps = pool[:m]
-        for gp in gps:
-            restore(gp)
-        kw = dict(nthreads_per_block=args.nthreads_per_block, max_blocks=args.max_blocks, max_steps=args.max_steps)
-        if args.pipeline and m > 1:
-            sts = list(gpu.propagate_batches(gps, gdet, rng, **kw))
+        if on_gpu:
+            dist.init_process_group('nccl', device_id=torch.device('cuda', local))
         else:
-            sts = []
-            for gp in gps:
-                gp.propagate(gdet, rng, **kw)
-                sts.append(gp.last_stats)
-        for gp in gps:
-            # hit-channel reduce: detected photons per PMT channel on each rank,
-            # SUM-reduced over ranks (RCCL for N > 1)
-            counts.fill(0)
-            _native.call('chr_channel_hit_counts', ctypes.byref(gp._desc()), 0, args.photons, 0x4,
-                         gdet.solid_id_map.gpudata, gdet.solid_id_to_channel_index_gpu.gpudata, counts.gpudata,
-                         gdet.nchannels, current_stream())
-            reduced['counts'] = shard.allreduce_channel_counts(counts.tensor)
-        reduced['gp'] = gps[-1]
-        return sts
+            dist.init_process_group('gloo')
+        if dist.get_world_size() != args.gpus:
+            raise SystemExit('bench.py: process group has %d ranks, --gpus %d' % (dist.get_world_size(), args.gpus))
+    nphotons = photons_for_rank(args, rank, world)
+    wl = WORKLOAD(args, rank, world, local, dist, nphotons)
 
     # pipelined runs warm up with at least 2 steps: a 1-batch call does not use
     # (so would not allocate) the batches' extra buffer contexts, streams and events
     warmup = max(args.warmup, 2) if (args.pipeline and args.warmup > 0) else args.warmup
-    elapsed, per_step, stats = timed_loop(run, args.steps, warmup, dist, torch.cuda.synchronize, group)
-    gp = reduced.pop('gp')
-    detected = int(((gp.flags.get() & 4) != 0).sum())
-    del gp
-    channel_hits = int(reduced['counts'].sum().item())     # all ranks, detected with a channel
-    launch_ms = [s.trace_launch_ms[i] for s in stats for i in range(s.trace_ms_n)]
-    launch_rays = [int(stats[0].trace_launch_rays[i]) for i in range(stats[0].trace_ms_n)] if stats else []
-    live = dict(kernel_ms=sum(s.kernel_ms for s in stats), launches=sum(s.launches for s in stats),
-                host_steps=sum(s.steps_run for s in stats), host_syncs=sum(s.host_syncs for s in stats),
-                trace_ms=sum(s.trace_ms for s in stats),
-                trace_launches=sum(s.trace_launches for s in stats), trace_rays=sum(s.trace_rays for s in stats),
-                overflows=sum(s.stack_overflows for s in stats), flat=sum(s.flat_walks for s in stats),
-                flat_whole=sum(s.flat_walks_whole for s in stats),
-                tail=[{'ms': round(s.tail_ms, 3), 'photons': int(s.tail_photons), 'max_steps': int(s.tail_max_steps),
-                       'slowest_photon_ms': round(s.tail_max_cycles / 1e5, 3),
-                       'slowest_photon_steps': int(s.tail_slowest_steps),
-                       'long_photons': int(s.tail_long_photons),
-                       'long_us_per_step': round(s.tail_long_ticks / 100.0 / max(1, s.tail_long_steps), 3),
-                       'long_walk_us_per_step': round(s.tail_long_walk_ticks / 100.0 / max(1, s.tail_long_steps), 3),
-                       'long_walk_iterations_per_step': round(s.tail_long_walk_iterations / max(1, s.tail_long_steps),
-                                                              2)} for s in stats])
-    # untimed: same propagate with the counting kernel variant -> own-layout bytes and SIMD efficiency
-    cst = None
-    if not args.no_count:
-        prev = os.environ.get('CHR_PROPAGATE_VARIANT')
-        os.environ['CHR_PROPAGATE_VARIANT'] = '5'
-        cst = run(1)[0]
-        reduced.pop('gp', None)
-        if prev is None:
-            del os.environ['CHR_PROPAGATE_VARIANT']
-        else:
-            os.environ['CHR_PROPAGATE_VARIANT'] = prev
-        torch.cuda.synchronize()
+    elapsed, per_step, stats = timed_loop(wl.run, args.steps, warmup, dist, wl.sync, wl.group)
+    total_photons = nphotons * args.steps
+    if dist is not None:
+        total_photons = int(round(_allreduce(dist, float(total_photons), 'sum')))
+    report = wl.rank_report(stats)
+    seq = None
+    if args.pipeline and args.sequential_steps > 0:
+        s_el, _, _ = timed_loop(wl.run_sequential, args.sequential_steps, 0, dist, wl.sync, 1)
+        s_total = nphotons * args.sequential_steps
+        if dist is not None:
+            s_total = _allreduce(dist, float(s_total), 'sum')
+        seq = {'photons_per_s': s_total / s_el, 'steps': args.sequential_steps,
+               'ms_per_step': 1e3 * s_el / args.sequential_steps,
+               'path': 'one GPUPhotons.propagate call per step (the reference caller\'s loop)'}
+    wl.reduced.pop('gp', None)
+    extra = wl.untimed_passes()
 
-    # untimed, CHROMA_DEVICE_PROFILE=1 only (libchroma_amd_prof.so, whose timed numbers
-    # carry the counters): the device region profile of one more propagate
-    dprof = None
-    if _native.DEVICE_PROFILE:
-        from chroma.gpu import profiler
-        profiler.device_reset()
-        run(1)
-        reduced.pop('gp', None)
-        torch.cuda.synchronize()
-        dprof = {'regions': profiler.device_fetch(), 'clock_khz': profiler.device_fetch.clock_khz,
-                 'library': os.path.basename(_native.library_path()),
-                 'cycles': 'lane-cycles of the shader clock (include/chroma_amd.h CHR_PROF_*)'}
+    # oracle checks: ranks > 0 check a sample of their own shard first (small,
+    # concurrently), then rank 0 runs the timed cpu_baseline alone on the host
+    check = None
+    if not args.no_cpu_baseline and rank > 0:
+        check = wl.check(False, args.cpu_budget, max(1, usable_cpus() // world), args.rank_parity_photons)
+    if dist is not None:
+        dist.barrier()
+    if not args.no_cpu_baseline and rank == 0:
+        check = wl.check(True, args.cpu_budget, usable_cpus(), 0)
+    report['parity'] = check[2] if check else None
+    if dist is not None:
+        reports = [None] * world
+        dist.all_gather_object(reports, report)
+    else:
+        reports = [report]
 
     if rank == 0:
-        props = torch.cuda.get_device_properties(local)
-        free_b, total_b = torch.cuda.mem_get_info(local)
         steps = max(1, args.steps)
-        detail = {'pipelined_steps_per_call': group, 'warmup_steps_run': warmup,
-                  'kernel_ms_per_step': live['kernel_ms'] / steps,
-                  'trace_ms_per_step': live['trace_ms'] / steps,
-                  'launches_per_step': live['launches'] / steps,
-                  'host_steps_per_propagate': live['host_steps'] / steps,
-                  'stream_draining_host_syncs_per_propagate': live['host_syncs'] / steps,
-                  'stack_overflows': int(live['overflows']),
-                  'flat_walks_decomposed': int(live['flat']), 'flat_walks_whole': int(live['flat_whole']),
-                  'tail_launch': live['tail'],
+        r0 = reports[0]
+        detail = {'pipelined_steps_per_call': wl.group, 'warmup_steps_run': warmup,
+                  'ranks_seen': len(reports), 'ranks': [{k: rep[k] for k in ('rank', 'local_rank', 'host', 'device',
+                                                                             'photons_per_step')}
+                                                        for rep in reports],
+                  'kernel_ms_per_step': r0['kernel_ms'] / steps,
+                  'trace_ms_per_step': r0['trace_ms'] / steps,
+                  'launches_per_step': r0['launches'] / steps,
+                  'host_steps_per_propagate': r0['host_steps'] / steps,
+                  'stream_draining_host_syncs_per_propagate': r0['host_syncs'] / steps,
+                  'stack_overflows': int(sum(r['overflows'] for r in reports)),
+                  'flat_walks_decomposed': int(sum(r['flat'] for r in reports)),
+                  'flat_walks_whole': int(sum(r['flat_whole'] for r in reports)),
+                  'tail_launch': r0['tail'],
                   'first_propagate_trace_launches': [{'rays': r, 'ms': round(float(m), 3)} for r, m in
-                                                     zip(launch_rays, launch_ms[:len(launch_rays)])],
-                  'detected_fraction': detected / args.photons,
-                  'channel_hits_all_ranks': channel_hits,
-                  'device': {'name': props.name, 'arch': getattr(props, 'gcnArchName', ''),
-                             'compute_units': props.multi_processor_count,
-                             'hbm_total_gb': total_b / 1e9, 'hbm_free_gb_after': free_b / 1e9},
-                  'kernels': _kernel_info(_native)}
-        if dprof is not None:
-            detail['device_profile'] = dprof
-        if cst is not None and cst.traversals:
-            detail['own_layout'] = {
-                'bytes_per_walk': (96.0 * cst.nodes_visited + 64.0 * cst.triangles_tested + 52.0 * cst.traversals)
-                / cst.traversals,
-                'nodes_per_photon': cst.nodes_visited / args.photons,
-                'triangles_per_photon': cst.triangles_tested / args.photons,
-                'traversals_per_photon': cst.traversals / args.photons,
-                'simd_efficiency_nodes': cst.nodes_visited / max(1.0, 64.0 * cst.wave_node_steps),
-                'simd_efficiency_triangles': cst.triangles_tested / max(1.0, 64.0 * cst.wave_triangle_steps),
-                'stack_overflows': int(cst.stack_overflows)}
-        info = {'triangles': len(det.mesh.triangles), 'bvh_nodes': len(det.bvh.nodes),
-                'channels': det.num_channels()}
-        result = result_line(args, world, elapsed, per_step, info, detail)
-        if not args.no_cpu_baseline and world == 1:
-            threads = usable_cpus()
-            packed = PackedGeometry(det)
-            cpu, b_ref, ostats, nsample, host = cpu_baseline(packed, photons, nslots, args.nthreads_per_block,
-                                                             args.max_blocks, args.max_steps, args.seed,
-                                                             args.cpu_budget, threads)
+                                                     zip(r0['launch_rays'], r0['launch_ms'][:len(r0['launch_rays'])])],
+                  'detected_fraction': r0['detected_last_step'] / max(1, nphotons),
+                  'channel_hits_all_ranks': r0['channel_hits_all_ranks'],
+                  'sequential': seq}
+        detail.update(wl.device_info())
+        detail.update(extra)
+        result = result_line(args, world, elapsed, per_step, total_photons, wl.detector_info(), detail)
+        if check is not None:
+            cpu, ostats, par = check
             result['cpu_baseline'] = cpu
+            nsample = par['n']
             detail['reference_bvh_nodes_per_photon'] = ostats['nodes_visited'] / nsample
             detail['reference_bvh_triangles_per_photon'] = ostats['tris_tested'] / nsample
-            detail['bytes_per_photon_alg_8d'] = b_ref
-            result['parity'] = gpu_parity(gdet, photons, nsample, host, args,
-                                          np.asarray(det.solid_id, np.int64),
-                                          np.asarray(det.solid_id_to_channel_index, np.int64))
-            if live['trace_launches']:
-                result['roofline'] = roofline(args, live['trace_ms'], live['trace_launches'], live['trace_rays'],
-                                              ostats, launch_ms)
+            detail['bytes_per_photon_alg_8d'] = 120.0 + (16.0 * ostats['nodes_visited'] + 48.0 * ostats['tris_tested'] +
+                                                         4.0 * ostats['traversals']) / nsample
+            parity = dict(par)
+            if world > 1:
+                parity['per_rank'] = [r['parity'] for r in reports]
+                parity['all_ranks_equal'] = all(p is not None and p['flags_equal'] and p['last_hit_equal'] and
+                                                p['channel_equal'] for p in parity['per_rank'])
+            result['parity'] = parity
+            if r0['trace_launches']:
+                result['roofline'] = roofline(args, reports, ostats)
         print(json.dumps(result), flush=True)
-    if dist:
+    if dist is not None:
+        dist.barrier()
         dist.destroy_process_group()
+    return 0
+
+
+def main(argv=None):
+    args = parse_args(argv)
+    if args.gpus > 1 and 'WORLD_SIZE' not in os.environ:
+        return spawn_ranks(args.gpus, [sys.executable, os.path.abspath(sys.argv[0])] +
+                           (sys.argv[1:] if argv is None else list(argv)))
+    return run_rank(args)
 
 
 if __name__ == '__main__':
-    main()
+    sys.exit(main())

@@ -9,7 +9,8 @@ path has a reduction step:
 
   * detected hits (GPUPhotons.get_flat_hits, reference photon.py:141-209) are
     gathered in rank order, which is ascending global photon order -- the same
-    order a single-GPU run returns;
+    order a single-GPU run returns -- to rank 0 (gather_rows), or to every
+    rank when each needs the events (allgather_rows);
   * the DAQ's per-channel words (reference daq.cu:78-80: atomicMin of the time
     bits, atomicAdd of the quantised charge, atomicOr of the history) are
     reduced with the same three operators: unsigned MIN, SUM (mod 2^32, as the
@@ -69,6 +70,19 @@ def _all_gather(parts, t, group):
         dist.all_gather(parts, t, group=group)
 
 
+def _gather(parts, t, dst, group):
+    """dist.gather of t into parts (on dst; parts is None elsewhere)."""
+    import torch.distributed as dist
+    if t.is_cuda and _host_backend(group):
+        host = [torch.empty_like(t, device='cpu') for _ in parts] if parts is not None else None
+        dist.gather(t.cpu(), host, dst=dst, group=group)
+        if parts is not None:
+            for p, h in zip(parts, host):
+                p.copy_(h)
+    else:
+        dist.gather(t, parts, dst=dst, group=group)
+
+
 def _all_reduce(t, op, group):
     import torch.distributed as dist
     if t.is_cuda and _host_backend(group):
@@ -97,6 +111,32 @@ def allgather_rows(local, group=None):
     padded[:local.shape[0]] = local
     parts = [torch.empty_like(padded) for _ in range(world)]
     _all_gather(parts, padded, group)
+    return torch.cat([parts[r][:counts[r]] for r in range(world)])
+
+
+def gather_rows(local, dst=0, group=None):
+    """Gather a (k_r, W) tensor from every rank to rank `dst` only: returns the
+    (sum k_r, W) concatenation in rank order on dst, None on the other ranks.
+    Only the row counts travel to every rank (W*8 bytes); the rows themselves
+    cross xGMI once, to dst (rows padded to max k_r for the collective)."""
+    import torch.distributed as dist
+    rank, world = dist_info(group)
+    if world == 1:
+        return local
+    k = torch.tensor([local.shape[0]], dtype=torch.int64, device=local.device)
+    ks = [torch.zeros_like(k) for _ in range(world)]
+    _all_gather(ks, k, group)
+    counts = [int(x.item()) for x in ks]
+    m = max(counts)
+    root = dist.get_global_rank(group, dst) if group is not None else dst
+    if m == 0:
+        return local[:0] if rank == dst else None
+    padded = torch.zeros((m,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+    padded[:local.shape[0]] = local
+    parts = [torch.empty_like(padded) for _ in range(world)] if rank == dst else None
+    _gather(parts, padded, root, group)
+    if rank != dst:
+        return None
     return torch.cat([parts[r][:counts[r]] for r in range(world)])
 
 

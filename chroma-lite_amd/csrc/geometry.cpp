@@ -7,6 +7,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <new>
 #include <string>
 #include <vector>
@@ -61,35 +62,50 @@ int dev_upload(chr_geometry *g, const void *host, size_t bytes, void **dptr) {
 extern "C" int chr_geometry_destroy(chr_geometry *g) {
     if (!g) return CHR_OK;
     int prev = 0;
-    hipGetDevice(&prev);
-    hipSetDevice(g->device);
-    for (int i = 0; i < g->nallocs; ++i) hipFree(g->allocs[i]);
-    hipSetDevice(prev);
+    (void)hipGetDevice(&prev);
+    (void)hipSetDevice(g->device);
+    for (int i = 0; i < g->nallocs; ++i) (void)hipFree(g->allocs[i]);
+    (void)hipSetDevice(prev);
     delete g->h_ref_nodes;
     delete g;
     return CHR_OK;
 }
 
+// The reference-order walk's data (16-B nodes, 48-B triangles), uploaded on
+// first use.  Callers on several host threads may reach it together, and from
+// a thread whose current device is not the geometry's: one lock for every
+// geometry (first use only), and the allocation on g->device.
 int chr::geometry_ref_nodes(const chr_geometry *cg) {
+    static std::mutex m;
+    std::lock_guard<std::mutex> lock(m);
     chr_geometry *g = const_cast<chr_geometry *>(cg);
     if (!g->h_ref_nodes && !g->ref_tri_pending) return CHR_OK;
-    void *p = nullptr;
-    int rc;
-    if (g->h_ref_nodes) {
-        if ((rc = dev_upload(g, g->h_ref_nodes->data(), g->h_ref_nodes->size() * sizeof(uint4), &p))) return rc;
-        g->dev.nodes = (const uint4 *)p;
-        delete g->h_ref_nodes;
-        g->h_ref_nodes = nullptr;
-    }
-    if (g->ref_tri_pending) {
-        if ((rc = dev_upload(g, nullptr, (size_t)g->dev.ntriangles * 48, &p))) return rc;
-        if ((rc = chr::build_ref_triangles(g->dev, (float4 *)p))) return rc;
-        g->dev.tri = (const float4 *)p;
-        g->ref_tri_pending = false;
-    }
-    const hipError_t e = hipMemcpy(g->d_dev, &g->dev, sizeof(g->dev), hipMemcpyHostToDevice);
-    if (e != hipSuccess) return chr::fail(CHR_ERR_HIP, "hipMemcpy H2D failed: %s", hipGetErrorString(e));
-    return CHR_OK;
+    int prev = 0;
+    hipError_t e = hipGetDevice(&prev);
+    if (e == hipSuccess && prev != g->device) e = hipSetDevice(g->device);
+    if (e != hipSuccess) return chr::fail(CHR_ERR_HIP, "geometry_ref_nodes: device %d: %s", g->device, hipGetErrorString(e));
+    auto run = [&]() -> int {
+        void *p = nullptr;
+        int rc;
+        if (g->h_ref_nodes) {
+            if ((rc = dev_upload(g, g->h_ref_nodes->data(), g->h_ref_nodes->size() * sizeof(uint4), &p))) return rc;
+            g->dev.nodes = (const uint4 *)p;
+            delete g->h_ref_nodes;
+            g->h_ref_nodes = nullptr;
+        }
+        if (g->ref_tri_pending) {
+            if ((rc = dev_upload(g, nullptr, (size_t)g->dev.ntriangles * 48, &p))) return rc;
+            if ((rc = chr::build_ref_triangles(g->dev, (float4 *)p))) return rc;
+            g->dev.tri = (const float4 *)p;
+            g->ref_tri_pending = false;
+        }
+        const hipError_t e2 = hipMemcpy(g->d_dev, &g->dev, sizeof(g->dev), hipMemcpyHostToDevice);
+        if (e2 != hipSuccess) return chr::fail(CHR_ERR_HIP, "hipMemcpy H2D failed: %s", hipGetErrorString(e2));
+        return CHR_OK;
+    };
+    const int rc = run();
+    if (prev != g->device) (void)hipSetDevice(prev);
+    return rc;
 }
 
 extern "C" int chr_geometry_device_bytes(const chr_geometry *g, uint64_t *bytes) {
@@ -129,7 +145,7 @@ extern "C" int chr_geometry_create(const chr_geometry_desc *d, chr_geometry **ou
     chr_geometry *g = new (std::nothrow) chr_geometry();
     if (!g) return chr::fail(CHR_ERR_NOMEM, "chr_geometry_create: host allocation failed");
     std::memset(g, 0, sizeof(*g));
-    hipGetDevice(&g->device);
+    (void)hipGetDevice(&g->device);
     int rc = CHR_OK;
     try {
         chr::DevGeom &dg = g->dev;

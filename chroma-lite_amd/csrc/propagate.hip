@@ -3895,9 +3895,11 @@ static void counter_stats(chr_propagate_stats &st, const PropBufs &b) {
 
 static int check_propagate_args(const char *fn, const chr_geometry *g, const chr_photons *ph, uint32_t nphotons,
                                 uint32_t true_nphotons, uint32_t ncopies, const uint32_t *d_rng_states,
-                                uint32_t rng_nslots, int32_t ntpb, int32_t max_blocks) {
+                                uint32_t rng_nslots, int32_t ntpb, int32_t max_blocks, int32_t max_steps) {
     if (!g || !photons_ok(ph) || !d_rng_states) return chr::fail(CHR_ERR_INVALID, "%s: null argument", fn);
     if (ntpb <= 0 || max_blocks <= 0) return chr::fail(CHR_ERR_INVALID, "%s: bad launch shape", fn);
+    // the slot-control words are sized by max_steps (device_slots, queue_prefix)
+    if (max_steps < 0) return chr::fail(CHR_ERR_INVALID, "%s: max_steps must be >= 0 (got %d)", fn, max_steps);
     if ((uint64_t)ntpb * (uint64_t)max_blocks > rng_nslots)
         return chr::fail(CHR_ERR_INVALID, "%s: rng_states must hold nthreads_per_block*max_blocks=%lld states (have %u)",
                          fn, (long long)ntpb * max_blocks, rng_nslots);
@@ -3916,11 +3918,16 @@ extern "C" int chr_propagate(const chr_geometry *g, const chr_photons *ph, uint3
                              int32_t max_blocks, int32_t max_steps, int32_t use_weights, int32_t scatter_first,
                              chr_propagate_stats *stats, void *vstream) {
     CHR_TRY(check_propagate_args("chr_propagate", g, ph, nphotons, true_nphotons, ncopies, d_rng_states, rng_nslots,
-                                 ntpb, max_blocks));
+                                 ntpb, max_blocks, max_steps));
+    chr_propagate_stats st{};
+    // max_steps == 0: the reference's step loop (photon.py:255) runs no launch
+    if (nphotons == 0 || max_steps == 0) {
+        st.final_alive = max_steps == 0 ? nphotons : 0u;
+        if (stats) *stats = st;
+        return CHR_OK;
+    }
     if (walks_reference_bvh(g)) CHR_TRY(chr::geometry_ref_nodes(g));
     hipStream_t stream = (hipStream_t)vstream;
-    chr_propagate_stats st{};
-    if (nphotons == 0) { if (stats) *stats = st; return CHR_OK; }
     if (int lrc = apply_node_layout(g, stream)) return lrc;
     PropBufs b;
     int rc = prop_bufs(nphotons, ntpb, max_blocks, 0, false, b);
@@ -4179,10 +4186,14 @@ static int propagate_batches(const chr_geometry *g, const chr_photons *phs, cons
         return chr::fail(CHR_ERR_INVALID, "chr_propagate_batches: null argument");
     for (uint32_t i = 0; i < nbatch; ++i)
         CHR_TRY(check_propagate_args("chr_propagate_batches", g, phs + i, nphotons[i], true_nphotons[i], ncopies[i],
-                                     d_rng_states, rng_nslots, ntpb, max_blocks));
+                                     d_rng_states, rng_nslots, ntpb, max_blocks, max_steps));
     hipStream_t stream = (hipStream_t)vstream;
     if (stats)
-        for (uint32_t i = 0; i < nbatch; ++i) stats[i] = chr_propagate_stats{};
+        for (uint32_t i = 0; i < nbatch; ++i) {
+            stats[i] = chr_propagate_stats{};
+            if (max_steps == 0) stats[i].final_alive = nphotons[i];
+        }
+    if (max_steps == 0) return CHR_OK;   // as max_steps == 0 propagate calls: no launch
     // the non-empty batches, in order
     std::vector<uint32_t> idx;
     uint32_t max_n = 0;

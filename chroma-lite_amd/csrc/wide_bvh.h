@@ -70,8 +70,11 @@ struct WideBVH {
 };
 
 // target number of sub-walks per decomposed walk (frontier size): the longest
-// sub-walk sets the launch time (32,768 items: ~1,200-node subtrees on the
-// 29k detector, one flat walk = a 15 ms launch, r02 rocprof)
+// sub-walk sets the launch time.  The BFS stops at the first level whose
+// frontier reaches the target, so a cut holds between 2^18 and 8 x 2^18 items
+// (one 8-wide level overshoots by up to 8x).  r02 rocprof: a 32,768-item cut
+// left ~1,200-node subtrees on the 29k detector and one flat walk made a 15 ms
+// launch; 2^18 items make each subtree about 8x smaller.
 constexpr uint32_t WIDE_CUT_TARGET = 1u << 18;
 
 // stack capacity of the wide traversal (entries); the builder marks a tree

@@ -190,3 +190,30 @@ def test_batches_c2_scale(cuda, tiny_geo):
         _same(a, b, 'C2 batch %d' % i)
     assert np.array_equal(rng_bat, rng_seq)
     assert all(s.trace_launches >= 1 and s.tail_photons > 0 for s in st)
+
+
+def test_max_steps_zero_and_negative(cuda, small_detector):
+    """max_steps=0 runs no launch (the reference's `while step < max_steps`
+    loop, photon.py:255) on both the sequential and the batched entry point:
+    photons and RNG states untouched.  A negative max_steps is rejected before
+    any device work (it would size the slot-control words)."""
+    from chroma import gpu
+    from chroma.gpu import _native
+    det = gpu.GPUDetector(small_detector)
+    src = _sources([3000, 2000], seed=41)
+    gps = [_gpu_photons(s) for s in src]
+    before = [gp.get() for gp in gps]
+    rng = gpu.get_rng_states(64 * 64, seed=6)
+    rng0 = rng.get()
+    gps[0].propagate(det, rng, nthreads_per_block=64, max_blocks=64, max_steps=0)
+    assert gps[0].last_stats.steps_run == 0 and gps[0].last_stats.final_alive == 3000
+    st = gpu.propagate_batches(gps, det, rng, nthreads_per_block=64, max_blocks=64, max_steps=0)
+    assert [s.steps_run for s in st] == [0, 0] and [s.final_alive for s in st] == [3000, 2000]
+    for a, b in zip(gps, before):
+        _same(a.get(), b, 'max_steps=0')
+    assert np.array_equal(rng.get(), rng0)
+    for call in (lambda: gps[0].propagate(det, rng, nthreads_per_block=64, max_blocks=64, max_steps=-1),
+                 lambda: gpu.propagate_batches(gps, det, rng, nthreads_per_block=64, max_blocks=64, max_steps=-3)):
+        with pytest.raises(_native.NativeError, match='max_steps'):
+            call()
+    assert np.array_equal(rng.get(), rng0)

@@ -37,20 +37,26 @@ def _photons():
     return isotropic(NEV * PER_EV, seed=41)
 
 
-def _worker(rank, world, port, out_dir):
+def _worker(rank, world, port, out_dir, hits):
     sys.path.insert(0, os.path.join(ROOT, 'chroma-lite_amd'))
     os.environ['LOCAL_RANK'] = '0'        # both ranks drive the box's one GPU
     import torch.distributed as dist
     dist.init_process_group('gloo', init_method='tcp://127.0.0.1:%d' % port, rank=rank, world_size=world)
     try:
         from chroma.sim import ShardedSimulation
-        sim = ShardedSimulation(_detector(), seed=1, nthreads_per_block=NTPB, max_blocks=MAXB)
+        sim = ShardedSimulation(_detector(), seed=1, nthreads_per_block=NTPB, max_blocks=MAXB, hits=hits)
         ph = _photons()
         evs = list(sim.simulate([ph[i * PER_EV:(i + 1) * PER_EV] for i in range(NEV)], run_daq=True,
                                 keep_hits=False))
         out = {}
         for i, ev in enumerate(evs):
             h = ev.flat_hits
+            if h is None:          # hits='root': only rank 0 receives the gathered hits
+                assert rank != 0 and hits == 'root'
+                out['ch_t_%d' % i] = ev.channels.t
+                out['ch_q_%d' % i] = ev.channels.q
+                out['ch_flags_%d' % i] = ev.channels.flags
+                continue
             out['flags_%d' % i] = h.flags
             out['last_hit_%d' % i] = h.last_hit_triangles
             out['channel_%d' % i] = h.channel
@@ -64,15 +70,19 @@ def _worker(rank, world, port, out_dir):
         dist.destroy_process_group()
 
 
-def test_sharded_simulation_two_ranks(tmp_path):
+@pytest.mark.parametrize('hits', ['root', 'all'])
+def test_sharded_simulation_two_ranks(tmp_path, hits):
+    """DAQ on: one propagate per batch (the DAQ draws from rng_states between
+    batches).  hits='root' gathers the hits to rank 0 only, 'all' to both."""
     import torch
     if not torch.cuda.is_available():
         pytest.skip('no HIP device')
     import torch.multiprocessing as mp
-    mp.spawn(_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    mp.spawn(_worker, args=(2, _free_port(), str(tmp_path), hits), nprocs=2, join=True)
     got = [np.load(os.path.join(str(tmp_path), 'rank%d.npz' % r)) for r in range(2)]
-    for k in got[0].files:                       # every rank yields the same events
+    for k in got[1].files:                       # every rank yields the same events (hits: where gathered)
         assert np.array_equal(got[0][k], got[1][k]), k
+    assert ('flags_0' in got[1].files) == (hits == 'all')
 
     from chroma.gpu.detector import cdf_arrays
     from chroma.gpu.packing import PackedGeometry

@@ -147,3 +147,36 @@ def test_seed_none_agrees_across_ranks(tmp_path):
     seed collective of the seed=None path)."""
     r0, r1 = _run('seed_agreement', tmp_path)
     assert r0[1] == r0[0] and r1[1] == r0[0] and r1[0] != r0[0]
+
+
+def gather_root(rank, world):
+    """hits to rank 0 only (ShardedSimulation(hits='root')): rank 1 gets None"""
+    from chroma.gpu import shard
+    f, ch = _local_hits(rank)
+    rows = shard.gather_rows(shard.pack_hits(f, ch), dst=0)
+    empty = shard.gather_rows(torch.zeros((0, 16), dtype=torch.int32), dst=0)
+    if rank != 0:
+        assert rows is None and empty is None
+        return np.zeros(0, np.int32)
+    assert empty.shape == (0, 16)
+    return rows.numpy()
+
+
+def test_gather_hits_to_root(tmp_path):
+    from chroma.gpu import shard
+    outs = _run('gather_root', tmp_path)
+    want = torch.cat([shard.pack_hits(*_local_hits(r)) for r in range(2)]).numpy()
+    assert np.array_equal(outs[0], want)
+    assert outs[1].size == 0
+
+
+def gather_root_world3(rank, world):
+    from chroma.gpu import shard
+    local = torch.full((rank, 3), rank, dtype=torch.int32)      # rank 0 contributes no rows
+    rows = shard.gather_rows(local, dst=0)
+    return rows.numpy() if rank == 0 else np.zeros(0, np.int32)
+
+
+def test_gather_to_root_world3_ragged(tmp_path):
+    outs = _run('gather_root_world3', tmp_path, world=3)
+    assert np.array_equal(outs[0], np.array([[1, 1, 1], [2, 2, 2], [2, 2, 2]], np.int32))

@@ -8,9 +8,12 @@ unknown).  Prints one JSON object."""
 import csv
 import re
 import glob
+import importlib.util
 import json
 import os
 import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def per_kernel(d, counter):
@@ -78,6 +81,26 @@ def main():
         res['by_kernel'][name] = {'launches': len(fetch.get(name, [])),
                                   'read_bytes_total': 2.0 * 1024.0 * sum(fetch.get(name, [])),
                                   'write_bytes_total': 1024.0 * sum(write.get(name, []))}
+    # L2 hit rate per kernel (TCC_HIT_sum / (HIT + MISS)) over the launches that
+    # did work (>= 1e5 L2 requests: the slots that exited at once are excluded)
+    hit = per_kernel(os.path.join(d, 'l2'), 'TCC_HIT_sum')
+    miss = per_kernel(os.path.join(d, 'l2'), 'TCC_MISS_sum')
+    if hit:
+        res['l2_hit_rate'] = {}
+        res['l2_requests'] = {}
+        for name in sorted(set(hit) & set(miss)):
+            pairs = [(h, m) for h, m in zip(hit[name], miss[name]) if h + m >= 1e5]
+            if not pairs:
+                continue
+            h, m = sum(p[0] for p in pairs), sum(p[1] for p in pairs)
+            res['l2_hit_rate'][name] = h / (h + m)
+            res['l2_requests'][name] = {'launches': len(pairs), 'hit': h, 'miss': m}
+    # the stamp: kernel sources of this tree (bench.py kernel_source_sha) and the commit
+    spec = importlib.util.spec_from_file_location('bench_stamp', os.path.join(ROOT, 'bench.py'))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    res['kernel_source_sha'] = mod.kernel_source_sha()
+    res['commit'] = os.environ.get('GIT_HEAD', 'unknown')
     # the workload the passes ran (bench.py only uses a summary of its own workload)
     try:
         with open(os.path.join(d, 'bench_fetch.json')) as f:
