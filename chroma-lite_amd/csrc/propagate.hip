@@ -2367,6 +2367,8 @@ struct TraceArgs {
     uint32_t *next;              // ray counter (zeroed by the host)
     uint32_t *counters;          // [0] overflows, [2..] u64 walk counters (COUNT)
     const uint32_t *order;       // fetch order: the j-th ray walked is queue position order[j] (nullptr: j)
+    const uint4 *rays;           // ray records in walk order (2 x uint4 per ray, ray_record; nullptr: gather
+                                 // queue -> flags / pos / dir / last_hit per refill instead)
     uint32_t *walk_hist;         // COUNT: [0..31] walks by log2(nodes + triangles), [32..33] u64 max (cost << 32 | photon)
     uint2 *spill;                // stack entries >= SL: (WIDE_STACK - SL) x gridDim.x*BLOCK, entry-major (HBM, no scratch)
     // flat walks of this step (walk_kind 2), enrolled before the launch:
@@ -2381,27 +2383,56 @@ struct TraceArgs {
     uint32_t drain_max;          // a wave drains its last <= drain_max walks whole-wave (0: never; at most 8)
 };
 
-// Enrol queue position p for the next trace launch if its walk is flat
-// (walk_kind 2): f = slot in the flat list, hits[p] = (FLAT_HIT, f).
-__device__ __forceinline__ void enrol_flat(const float *pos, const float *dir, uint32_t pid, uint32_t p, int2 *hits,
-                                           uint32_t *flat_q, uint32_t *flat_count, unsigned long long *flat_best) {
-    const V3 o = load3(pos, pid);
-    V3 d = load3(dir, pid);
-    d = d / norm(d);
-    if (walk_kind(o, d) != 2) return;
+// Enrol queue position p in the flat list of the next trace launch (its walk
+// is flat, walk_kind 2): f = slot in the flat list, hits[p] = (FLAT_HIT, f).
+__device__ __forceinline__ void enrol_flat_at(uint32_t p, int2 *hits, uint32_t *flat_q, uint32_t *flat_count,
+                                              unsigned long long *flat_best) {
     const uint32_t f = atomicAdd(flat_count, 1u);
     flat_q[f] = p;
     flat_best[f] = ~0ull;
     hits[p] = make_int2(FLAT_HIT, (int)f);
 }
 
+// Ray record of one queue position, the only thing trace_kernel's refill
+// reads: written in walk order by the kernel that builds the queue (the
+// previous step's scatter, or the first step's classification + permutation),
+// so a refill is one 32-byte load, contiguous across the refilling lanes,
+// instead of the dependent order -> queue -> flags / pos / dir / last_hit chain
+// of the photon arrays (propagate.cu:280-293).  Words: origin, the normalised
+// direction (propagate.cu:280-281, the same float operations as the walk
+// made), the photon's last hit, its queue position; bit 31 of the last word:
+// no ordinary walk here (dead on entry, NaN state, or flat: walked as sub-walks).
+constexpr uint32_t RAY_SKIP = 0x80000000u;
+__device__ __forceinline__ void put_ray(uint4 *rays, uint32_t j, V3 o, V3 d, int32_t last_hit, uint32_t q, bool walk) {
+    rays[2 * (size_t)j] = make_uint4(__float_as_uint(o.x), __float_as_uint(o.y), __float_as_uint(o.z),
+                                     __float_as_uint(d.x));
+    rays[2 * (size_t)j + 1] = make_uint4(__float_as_uint(d.y), __float_as_uint(d.z), (uint32_t)last_hit,
+                                         q | (walk ? 0u : RAY_SKIP));
+}
+
+// Enrol queue position p for the next trace launch if its walk is flat; with
+// rays, also write its ray record at walk position j.
+__device__ __forceinline__ void enrol_flat(const float *pos, const float *dir, uint32_t pid, uint32_t p, int2 *hits,
+                                           uint32_t *flat_q, uint32_t *flat_count, unsigned long long *flat_best,
+                                           uint4 *rays = nullptr, const int32_t *last_hit = nullptr,
+                                           uint32_t j = 0) {
+    const V3 o = load3(pos, pid);
+    V3 d = load3(dir, pid);
+    d = d / norm(d);
+    const int kind = walk_kind(o, d);
+    if (kind == 2) enrol_flat_at(p, hits, flat_q, flat_count, flat_best);
+    if (rays) put_ray(rays, j, o, d, last_hit[pid], p, kind == 1);
+}
+
 // first host step: enrol the flat walks of the initial queue; with keys, also
 // the direction-binning key of every queue position (bin_key_kernel's, one
-// pass over the photons instead of two)
+// pass over the photons instead of two), and with rays the ray record of every
+// queue position at its own index (binned: permuted into walk order after the sort)
 __global__ __launch_bounds__(BLOCK) void classify_kernel(const float *pos, const float *dir, const uint32_t *flags,
-                                                         const uint32_t *queue, uint32_t n, int2 *hits,
-                                                         uint32_t *flat_q, uint32_t *flat_count,
-                                                         unsigned long long *flat_best, uint32_t *keys, uint32_t *vals) {
+                                                         const int32_t *last_hit, const uint32_t *queue, uint32_t n,
+                                                         int2 *hits, uint32_t *flat_q, uint32_t *flat_count,
+                                                         unsigned long long *flat_best, uint32_t *keys, uint32_t *vals,
+                                                         uint4 *rays) {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     if (i >= n) return;
     const uint32_t pid = queue[i];
@@ -2409,8 +2440,22 @@ __global__ __launch_bounds__(BLOCK) void classify_kernel(const float *pos, const
         keys[i] = bin_key_of(v3(dir[3 * pid], dir[3 * pid + 1], dir[3 * pid + 2]));
         vals[i] = i;
     }
-    if ((flags[pid] & 0xFFFFu) & DEAD_MASK) return;
-    enrol_flat(pos, dir, pid, i, hits, flat_q, flat_count, flat_best);
+    if ((flags[pid] & 0xFFFFu) & DEAD_MASK) {
+        if (rays) put_ray(rays, i, v3(0.0f, 0.0f, 0.0f), v3(0.0f, 0.0f, 0.0f), -1, i, false);
+        return;
+    }
+    enrol_flat(pos, dir, pid, i, hits, flat_q, flat_count, flat_best, rays, last_hit, i);
+}
+
+// rays_out[j] = rays_in[order[j]]: the first step's records in the binned walk order
+__global__ __launch_bounds__(BLOCK) void permute_rays_kernel(const uint4 *rays_in, const uint32_t *order, uint32_t n,
+                                                             uint4 *rays_out) {
+    const uint32_t j = blockIdx.x * BLOCK + threadIdx.x;
+    if (j >= n) return;
+    const uint32_t q = order[j];
+    const uint4 r0 = rays_in[2 * (size_t)q], r1 = rays_in[2 * (size_t)q + 1];
+    rays_out[2 * (size_t)j] = r0;
+    rays_out[2 * (size_t)j + 1] = r1;
 }
 
 // COUNT: walk counters; F: triangle step once F/8 of the walking lanes have
@@ -2483,7 +2528,23 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
                 if (!has_ray) {
                     const uint32_t j = base + (uint32_t)__popcll(need & ((1ull << lane) - 1ull));
                     bool start = false;
-                    if (j < n) {
+                    if (j < n && a.rays) {
+                        // the ray record: one 32-B load (put_ray); skip bit: dead / NaN / flat
+                        const uint4 r0 = gld(a.rays + 2 * (size_t)j), r1 = gld(a.rays + 2 * (size_t)j + 1);
+                        q = r1.w & ~RAY_SKIP;
+                        if (!(r1.w & RAY_SKIP)) {
+                            o = v3(__uint_as_float(r0.x), __uint_as_float(r0.y), __uint_as_float(r0.z));
+                            d = v3(__uint_as_float(r0.w), __uint_as_float(r1.x), __uint_as_float(r1.y));
+                            last = r1.z;
+                            if constexpr (COUNT) pid = a.walk_hist ? a.queue[q] : q;
+                            start = true;
+                            flat_f = -1;
+                            node = 0;
+                            cmask = 0xFFu;
+                            best = __builtin_inff();
+                            best_rank = 0xFFFFFFFFu;
+                        }
+                    } else if (j < n) {
                         q = a.order ? a.order[j] : j;
                         pid = a.queue[q];
                         // dead on entry / NaN: no walk (the step kernel skips / aborts them);
@@ -2499,6 +2560,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
                                 cmask = 0xFFu;
                                 best = __builtin_inff();
                                 best_rank = 0xFFFFFFFFu;
+                                last = (uint32_t)a.last_hit[pid];
                             }
                         }
                     } else if (j < total) {                       // sub-walk k of flat walk f
@@ -2518,11 +2580,11 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
                         cmask = item.y;
                         best = key == ~0ull ? __builtin_inff() : __uint_as_float((uint32_t)(key >> 32));
                         best_rank = key == ~0ull ? 0xFFFFFFFFu : (uint32_t)key;
+                        last = (uint32_t)a.last_hit[pid];
                     }
                     if (start) {
                         slab = make_slab(v3(-o.x / d.x, -o.y / d.y, -o.z / d.z), v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z));
                         best_id = -1;
-                        last = (uint32_t)a.last_hit[pid];
                         sp = 0;
                         walk_done = false;
                         has_ray = true;
@@ -2804,6 +2866,8 @@ struct FlatEnrol {
     int2 *hits;
     uint32_t *flat_q, *flat_count;
     unsigned long long *flat_best;
+    uint4 *rays;                 // + the next step's ray records, in queue order (nullptr: off)
+    const int32_t *last_hit;
 };
 __global__ __launch_bounds__(BLOCK) void scatter_queue_kernel(const unsigned long long *masks, const uint32_t *word_offsets,
                                                                const uint32_t *block_prefix, const uint32_t *base,
@@ -2824,7 +2888,9 @@ __global__ __launch_bounds__(BLOCK) void scatter_queue_kernel(const unsigned lon
             const uint32_t pid = in_queue[first + id];
             out_queue[o] = pid;
             // out_queue[0] is the count header: position o - 1 of the next step's queue
-            if (fe.pos) enrol_flat(fe.pos, fe.dir, pid, o - 1u, fe.hits, fe.flat_q, fe.flat_count, fe.flat_best);
+            if (fe.pos)
+                enrol_flat(fe.pos, fe.dir, pid, o - 1u, fe.hits, fe.flat_q, fe.flat_count, fe.flat_best, fe.rays,
+                           fe.last_hit, o - 1u);
         }
     }
 }
@@ -3338,7 +3404,7 @@ static int launch_chunk(const chr_geometry *g, const chr_photons *ph, uint32_t *
     launch_mask_scan(masks, nwords, offsets, bsums, out_queue, counters + 1, nullptr, stream);
     hipLaunchKernelGGL(scatter_queue_kernel, dim3(grid_for(nthreads)), dim3(BLOCK), 0, stream, masks, offsets, bsums,
                        counters + 1, in_queue, first, nthreads, out_queue,
-                       FlatEnrol{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr}, (const uint32_t *)nullptr,
+                       FlatEnrol{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr}, (const uint32_t *)nullptr,
                        (const uint32_t *)nullptr, STEP_IDLE);
     CHR_HIP_CHECK(hipGetLastError());
     return CHR_OK;
@@ -3367,6 +3433,10 @@ struct FlatCtx {
     uint32_t *ctl;
     int cur;
     bool enrol_next;
+    // trace_kernel's ray records (put_ray): rays in queue order (the first
+    // step's classification, then every step's scatter for the next step),
+    // rays_walk the binned first step's records permuted into walk order
+    uint4 *rays = nullptr, *rays_walk = nullptr;
 };
 static int flat_get(uint32_t n, FlatCtx &fc, int ctx = 0) {
     static thread_local Scratch s[NCTX][16];
@@ -3389,6 +3459,12 @@ static int flat_get(uint32_t n, FlatCtx &fc, int ctx = 0) {
 }
 
 static bool trace_steps();
+// CHR_TRACE_RAYS=0: trace_kernel refills from the photon arrays through the
+// queue (the r02 path) instead of the ray records (A/B; read per launch)
+static bool trace_rays_enabled() {
+    const char *e = getenv("CHR_TRACE_RAYS");
+    return !(e && e[0] == '0');
+}
 // A device-driven step slot (chr_propagate without a host round trip per
 // step): the slot's kernels read the queue length from the input queue's
 // header and run by the mode step_head_kernel picks; n passed to launch_step
@@ -3481,13 +3557,18 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
         const bool bin_now = (sv.binned == 1 || (sv.binned == 2 && first_one_step && n >= kBinFirstMin)) &&
                              (!sc || first_one_step) && pre;
         uint32_t *keys = next + 16, *order = keys + n;
+        // ray records: the first step's from its classification, later steps' from
+        // the previous step's scatter (enrol_next)
+        const bool use_rays = fc->rays && trace_rays_enabled() && (first_one_step || fc->enrol_next);
         if (first_one_step && pre)   // flat walks of the initial queue (later steps: enrolled by the previous scatter)
             hipLaunchKernelGGL(classify_kernel, dim3(grid_for(n)), dim3(BLOCK), 0, stream, ph->d_pos, ph->d_dir,
-                               ph->d_flags, in_queue, n, hits, fc->flat_q, count_cur, fc->flat_best,
-                               bin_now ? keys : nullptr, bin_now ? order : nullptr);
+                               ph->d_flags, ph->d_last_hit_triangles, in_queue, n, hits, fc->flat_q, count_cur,
+                               fc->flat_best, bin_now ? keys : nullptr, bin_now ? order : nullptr,
+                               use_rays ? fc->rays : nullptr);
         TraceArgs ta;
         ta.pos = ph->d_pos; ta.dir = ph->d_dir; ta.flags = ph->d_flags; ta.last_hit = ph->d_last_hit_triangles;
         ta.queue = in_queue; ta.n = n; ta.hits = hits; ta.next = next; ta.counters = counters; ta.order = nullptr;
+        ta.rays = use_rays ? fc->rays : nullptr;
         ta.walk_hist = nullptr;
         ta.flat_q = fc->flat_q; ta.flat_count = count_cur; ta.flat_best = fc->flat_best; ta.diag = fc->ctl + 3;
         ta.dev_n = dev_n;
@@ -3496,7 +3577,8 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
         a.flat_best = fc->flat_best;
         a.zero_word = count_next;   // cleared by the shade pass, filled by this step's scatter
         if (fc->enrol_next)
-            fe = FlatEnrol{ph->d_pos, ph->d_dir, hits, fc->flat_q, count_next, fc->flat_best};
+            fe = FlatEnrol{ph->d_pos, ph->d_dir, hits, fc->flat_q, count_next, fc->flat_best,
+                           (fc->rays && trace_rays_enabled()) ? fc->rays : nullptr, ph->d_last_hit_triangles};
         if (trace_steps() && pre) {   // debugging: per-walk cost histogram (counting variants), printed per step
             ta.walk_hist = next + 16 + 2 * (size_t)(sc ? sc->n_layout : n);
             CHR_HIP_CHECK(hipMemsetAsync(ta.walk_hist, 0, 34 * 4, stream));
@@ -3512,6 +3594,11 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
                 CHR_HIP_CHECK(rocprim::radix_sort_pairs(temp, temp_bytes, keys, keys_out, order, vals_out, n, 0, 16,
                                                         stream));
                 ta.order = vals_out;
+                if (use_rays) {   // the records in the binned walk order
+                    hipLaunchKernelGGL(permute_rays_kernel, dim3(grid_for(n)), dim3(BLOCK), 0, stream, fc->rays,
+                                       vals_out, n, fc->rays_walk);
+                    ta.rays = fc->rays_walk;
+                }
             }
         }
         if (pre) {
@@ -3698,7 +3785,9 @@ static int prop_bufs(uint32_t nphotons, int32_t ntpb, int32_t max_blocks, int ct
     const size_t qbytes = ((size_t)nphotons + 1) * 4;
     // split path: hits, ray counter, binning keys/order/histogram
     const size_t hbytes = b.fused ? (size_t)nphotons * 24 + 128 + 256 + 512 + sort_temp_bytes16(nphotons) : 0;
-    const size_t base_bytes = 2 * qbytes + swords * 4 + 64 + hbytes;
+    // split path: ray records, queue order + walk order (FlatCtx::rays / rays_walk)
+    const size_t rbytes = b.fused ? (size_t)nphotons * 64 + 512 : 0;
+    const size_t base_bytes = 2 * qbytes + swords * 4 + 64 + hbytes + rbytes;
     const size_t mbytes = tail_masks ? ((size_t)nphotons + 63) / 64 * 8 + 512 : 0;
     void *buf = nullptr;
     int rc = scratch_get(base_bytes + mbytes, &buf, ctx);
@@ -3713,6 +3802,10 @@ static int prop_bufs(uint32_t nphotons, int32_t ntpb, int32_t max_blocks, int ct
     b.tail_masks = tail_masks ? (unsigned long long *)(((uintptr_t)buf + base_bytes + 255) & ~(uintptr_t)255) : nullptr;
     if ((rc = pinned_words(&b.pinned, ctx))) return rc;
     if (b.fused && (rc = flat_get(nphotons, b.fc, ctx))) return rc;
+    if (b.fused) {
+        b.fc.rays = (uint4 *)(((uintptr_t)buf + 2 * qbytes + swords * 4 + 64 + hbytes + 255) & ~(uintptr_t)255);
+        b.fc.rays_walk = b.fc.rays + 2 * (size_t)nphotons;
+    }
     return CHR_OK;
 }
 
