@@ -32,6 +32,24 @@ def _first_seen(objs):
     return out
 
 
+_NATIVE_UNIQUE_MIN = 1 << 16
+
+
+def _native_unique(v):
+    """(unique rows, inverse) from libchroma_amd's chr_unique_vertices, or None
+    when the rows hold a NaN or -0.0 (numpy then decides which duplicate stays)."""
+    import ctypes
+    from chroma.gpu import _native
+    out = np.empty_like(v)
+    inverse = np.empty(len(v), dtype=np.int64)
+    nu = ctypes.c_uint64()
+    rc = _native.lib().chr_unique_vertices(v.ctypes.data, len(v), out.ctypes.data, ctypes.byref(nu),
+                                           inverse.ctypes.data)
+    if rc != 0:
+        return None
+    return out[:nu.value].copy(), inverse
+
+
 class Mesh(object):
     """Vertices (V,3) float32 and triangles (T,3) vertex indices."""
 
@@ -67,10 +85,22 @@ class Mesh(object):
         return np.min(self.vertices, axis=0), np.max(self.vertices, axis=0)
 
     def remove_duplicate_vertices(self):
-        """Merge bit-identical vertices (lexicographically sorted, like np.unique)."""
-        rows = np.ascontiguousarray(self.vertices).view([('', self.vertices.dtype)] * 3)
+        """Merge equal vertices, rows sorted lexicographically: np.unique over
+        the (x, y, z) rows with return_inverse (reference geometry.py:71-81).
+        Large meshes without NaN / -0.0 (where equal rows are bit-identical, so
+        the choice of kept duplicate cannot matter) go to the parallel host sort
+        chr_unique_vertices: the 170M-triangle detector's flatten spent ~45 s in
+        numpy's structured argsort."""
+        v = np.ascontiguousarray(self.vertices, dtype=np.float32)
+        if len(v) >= _NATIVE_UNIQUE_MIN:
+            got = _native_unique(v)
+            if got is not None:
+                self.vertices, inverse = got
+                self.triangles = inverse[self.triangles]
+                return
+        rows = v.view([('', v.dtype)] * 3)
         uniq, inverse = np.unique(rows, return_inverse=True)
-        self.vertices = uniq.view(self.vertices.dtype).reshape((len(uniq), 3))
+        self.vertices = uniq.view(v.dtype).reshape((len(uniq), 3))
         tri = inverse.reshape(-1)[self.triangles]
         self.triangles = tri
 
@@ -272,11 +302,20 @@ class Geometry(object):
             else np.zeros(0, np.uint32)
         self.unique_materials = _first_seen([m for s in self.solids for m in s.unique_materials])
         mat_lookup = {id(m): i for i, m in enumerate(self.unique_materials)}
-        self.material1_index = np.concatenate([s.material1_indices(mat_lookup) for s in self.solids])
-        self.material2_index = np.concatenate([s.material2_indices(mat_lookup) for s in self.solids])
+        # a detector places the same Solid object many times (29,007 PMTs): its
+        # per-triangle index columns are computed once per distinct solid
+        memo = {}
+
+        def per_solid(s, which, lookup):
+            key = (id(s), which)
+            if key not in memo:
+                memo[key] = getattr(s, which)(lookup)
+            return memo[key]
+        self.material1_index = np.concatenate([per_solid(s, 'material1_indices', mat_lookup) for s in self.solids])
+        self.material2_index = np.concatenate([per_solid(s, 'material2_indices', mat_lookup) for s in self.solids])
         self.unique_surfaces = _first_seen([x for s in self.solids for x in s.unique_surfaces])
         surf_lookup = {id(x): i for i, x in enumerate(self.unique_surfaces)}
-        self.surface_index = np.concatenate([s.surface_indices(surf_lookup) for s in self.solids])
+        self.surface_index = np.concatenate([per_solid(s, 'surface_indices', surf_lookup) for s in self.solids])
         none_slot = [i for i, x in enumerate(self.unique_surfaces) if x is None]
         if none_slot:
             self.surface_index[self.surface_index == none_slot[0]] = -1

@@ -108,6 +108,7 @@ _SIGNATURES = {
     'chr_selftest_linalg': (c_i32, [c_i32, c_u32, c_vp, c_vp, c_f32, c_vp, c_vp]),
     'chr_selftest_rotate': (c_i32, [c_u32, c_vp, c_vp, c_f32, c_f32, c_f32, c_vp, c_vp]),
     'chr_selftest_sample_cdf': (c_i32, [c_u32, c_vp, c_u32, c_i32, c_vp, c_vp, c_f32, c_f32, c_i32, c_vp, c_vp]),
+    'chr_unique_vertices': (c_i32, [c_vp, c_u64, c_vp, ctypes.POINTER(c_u64), c_vp]),
     'chr_bvh_build_grid': (c_i32, [c_vp, c_u32, c_vp, c_u32, c_i32, ctypes.POINTER(c_vp)]),
     'chr_bvh_result_info': (c_i32, [c_vp, ctypes.POINTER(c_u32), ctypes.POINTER(c_u32), c_vp,
                                     ctypes.POINTER(c_f32)]),

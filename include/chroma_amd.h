@@ -278,6 +278,18 @@ int chr_bvh_result_copy(const chr_bvh_result *r, uint32_t *h_nodes /*[nnodes*4]*
                         uint32_t *h_layer_offsets /*[nlayers]*/);
 int chr_bvh_result_free(chr_bvh_result *r);
 
+/* ------------------------------------------------------------- flatten helper
+ * replaces: the np.unique(rows, return_inverse=True) of Mesh.remove_duplicate_vertices
+ * (chroma/geometry.py:71-81, called by Geometry.flatten, geometry.py:337-391)
+ * where every set of equal rows is bit-identical (so which duplicate numpy
+ * keeps cannot matter): rows sorted lexicographically by float value (x, then
+ * y, then z; -0.0 == +0.0), duplicates merged.  out_vertices (>= n rows)
+ * receives the unique rows, *nunique their count, inverse[i] the unique row of
+ * input row i.  Returns CHR_ERR_INVALID for a NaN, or a set of equal rows that
+ * mixes +0.0 and -0.0 (the caller then uses numpy). */
+int chr_unique_vertices(const float *h_vertices, uint64_t n, float *h_out_vertices, uint64_t *nunique,
+                        int64_t *h_inverse);
+
 /* ------------------------------------------------------------- traversal BVH
  * The layout the gfx950 walk uses (csrc/wide_bvh.h): an 8-wide SAH tree over
  * the reference BVH's own leaf boxes, each triangle carrying its reference DFS

@@ -103,3 +103,31 @@ def test_scintillator_detector_build():
     assert len(dp.angles) == len(dp.dichroic_reflect) == len(dp.dichroic_transmit)
     for r, t in zip(dp.dichroic_reflect, dp.dichroic_transmit):
         assert (r[:, 1] + t[:, 1] <= 1.0 + 1e-6).all()
+
+
+def test_native_vertex_unique_equals_numpy():
+    """Mesh.remove_duplicate_vertices through chr_unique_vertices (the flatten
+    of large meshes) == numpy's np.unique over the rows: same sorted unique
+    rows and inverse, with duplicates, negative values and -0.0 coordinates;
+    a set of equal rows mixing +0.0 and -0.0 (numpy's kept row then depends on
+    its sort) and NaN rows are refused and left to numpy."""
+    import numpy as np
+    from chroma import geometry
+    rng = np.random.default_rng(7)
+    v = (rng.integers(-40, 40, size=(200_000, 3)) * 0.25).astype(np.float32)
+    v[v == 0] = np.float32(-0.0)                      # every zero negative: no mixed run
+    t = rng.integers(0, len(v), size=(70_000, 3))
+    rows = v.view([('', np.float32)] * 3)
+    u, inv = np.unique(rows, return_inverse=True)
+    got = geometry._native_unique(v)
+    assert got is not None
+    assert np.array_equal(got[0].view(np.uint32), u.view(np.float32).reshape(-1, 3).view(np.uint32))
+    assert np.array_equal(got[1], inv.reshape(-1))
+    m = geometry.Mesh(v, t, remove_duplicate_vertices=True)
+    assert np.array_equal(m.triangles, inv.reshape(-1)[t])
+    mixed = v.copy()
+    mixed[:2] = [[0.0, 1.0, 2.0], [-0.0, 1.0, 2.0]]
+    assert geometry._native_unique(mixed) is None
+    nan = v.copy()
+    nan[5, 1] = np.nan
+    assert geometry._native_unique(nan) is None
