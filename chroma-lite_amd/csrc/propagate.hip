@@ -1526,7 +1526,8 @@ struct PropagateArgs {
     // and the launch runs only if *mode == want
     const uint32_t *dev_n;
     const uint32_t *mode;
-    uint32_t prio;                     // tail kernel: raise its waves' issue priority (s_setprio)
+    uint32_t prio;                     // tail kernel: bit 0 raise its waves' issue priority (s_setprio),
+                                       // bit 1 the whole-wave walk specialised for one walker (GS = 64)
     uint32_t want;
 };
 // modes of a device-driven step slot (step_head_kernel)
@@ -1941,10 +1942,14 @@ struct LdsRows {
 // best_id seed the walk with a hit already found (a trace_kernel walk handed
 // over mid-way): culling with it is conservative, and the result is the min
 // over the seed and every triangle this walk tests.
-template <class M>
-__device__ __forceinline__ int walk_segment(const DevGeom &g, bool act, V3 o, V3 d, uint32_t last, int Gs, M stk, int cap, M tlist,
+// GS > 0: the segment width as a compile-time constant (GS = 64: one walk on
+// the whole wave, the tail's lone long-lived photon -- segment masks and
+// offsets fold away); GS = 0: the width Gs_in at run time.
+template <int GS, class M>
+__device__ __forceinline__ int walk_segment(const DevGeom &g, bool act, V3 o, V3 d, uint32_t last, int Gs_in, M stk, int cap, M tlist,
                             uint32_t &overflow, float &min_distance, uint32_t &iters,
                             float best = __builtin_inff(), uint32_t best_rank = 0xFFFFFFFFu, int best_id = -1) {
+    const int Gs = GS ? GS : Gs_in;
     constexpr uint32_t INVALID = 0xFFFFFFFFu;
     constexpr unsigned long long NONE = ~0ull;
     const uint32_t lane = __lane_id();
@@ -2136,7 +2141,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_tail_kernel(const DevGe
     if (a.mode && *a.mode != a.want) return;
     // a tail overlapped by the next batch (chr_propagate_batches) is the critical
     // path: its waves win the SIMD's issue arbitration over that batch's walk
-    if (a.prio) __builtin_amdgcn_s_setprio(3);
+    if (a.prio & 1u) __builtin_amdgcn_s_setprio(3);
     const uint32_t slot = tid / 8, sub = tid & 7u;
     const uint32_t n = a.dev_n ? *a.dev_n - 1u : (uint32_t)a.nthreads;
     const uint32_t nslot = cap < n ? cap : n;
@@ -2245,8 +2250,11 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_tail_kernel(const DevGe
             const uint32_t seg0 = lane & ~(uint32_t)(Gs - 1);
             float sd;
             uint32_t it;
-            const int st = walk_segment(g, act, o, dd, last, Gs, LdsFlat{wstack + seg0 / 8 * TAIL_STACK * 2},
-                                        TAIL_STACK * Gs / 8, LdsFlat{wtris + 4 * seg0}, overflow, sd, it);
+            const int st = (Gs == 64 && (a.prio & 2u))
+                               ? walk_segment<64>(g, act, o, dd, last, 64, LdsFlat{wstack}, TAIL_STACK * 8, LdsFlat{wtris},
+                                                  overflow, sd, it)
+                               : walk_segment<0>(g, act, o, dd, last, Gs, LdsFlat{wstack + seg0 / 8 * TAIL_STACK * 2},
+                                                 TAIL_STACK * Gs / 8, LdsFlat{wtris + 4 * seg0}, overflow, sd, it);
             const int mine = __popcll(wm & ((1ull << (lane & ~7u)) - 1ull)) * Gs;   // my group's segment
             tri = __shfl(st, mine);
             dist = __shfl(sd, mine);
@@ -2711,7 +2719,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
             CHR_LDS uint32_t *wbase = (CHR_LDS uint32_t *)(lds + (threadIdx.x & ~63u));
             float sdist;
             uint32_t sit;
-            const int tri = walk_segment(g, act, so, sdir, slast, Gs, LdsRows{wbase, seg0 / 8 * TAIL_STACK * 2},
+            const int tri = walk_segment<0>(g, act, so, sdir, slast, Gs, LdsRows{wbase, seg0 / 8 * TAIL_STACK * 2},
                                          TAIL_STACK * Gs / 8, LdsRows{wbase, 8 * TAIL_STACK * 2 + 4 * seg0}, overflow,
                                          sdist, sit, sbest, srank, sid);
             const int mine = (__popcll(rm & ((1ull << lane) - 1ull)) * Gs) & 63;   // my segment's first lane
@@ -3270,6 +3278,12 @@ static uint32_t trace_drain_max() {
     const int k = e ? atoi(e) : 8;
     return (uint32_t)(k < 0 ? 0 : (k > 8 ? 8 : k));
 }
+// CHR_TAIL_GS64=0: the tail's lone-walker walks through the generic segment
+// walk (run-time width) instead of its GS = 64 specialisation (A/B)
+static bool tail_gs64() {
+    const char *e = getenv("CHR_TAIL_GS64");
+    return !(e && e[0] == '0');
+}
 // CHR_TAIL_PRIO=0: the batches' overlapped tail kernel at normal wave priority (A/B)
 static bool tail_prio() {
     const char *e = getenv("CHR_TAIL_PRIO");
@@ -3312,6 +3326,12 @@ struct StepVariant {
 // (demo.detector(), 4M photons: first-step walk 2.65 -> 2.21 ms for 0.11 ms of
 // sorting; second step unchanged).
 static constexpr uint32_t kBinFirstMin = 1u << 20;
+// CHR_TRACE_R=16|32|48: trace_kernel refills once that many of a wave's 64
+// lanes are without a ray (default 32; A/B)
+static int trace_refill_r() {
+    const char *e = getenv("CHR_TRACE_R");
+    return e ? atoi(e) : 32;
+}
 static StepVariant select_step_variant(const chr_geometry *g) {
     const char *e = getenv("CHR_PROPAGATE_VARIANT");
     int v = e ? atoi(e) : 0;
@@ -3336,7 +3356,8 @@ static StepVariant select_step_variant(const chr_geometry *g) {
             break;
         default:   // 0, 7, 8
             sv.fn = propagate_step_kernel<8, 4, kWalk>;
-            sv.trace = trace_kernel<false, 6, 12, 4, 32>;
+            sv.trace = trace_refill_r() == 16 ? trace_kernel<false, 6, 12, 4, 16>
+                       : (trace_refill_r() == 48 ? trace_kernel<false, 6, 12, 4, 48> : trace_kernel<false, 6, 12, 4, 32>);
             sv.shade = shade_kernel<3>;
             sv.tail = tail_group_walk() ? propagate_group_kernel<8, kGroupWaves>
                       : (tail_waves() == 4 ? propagate_tail_kernel<4>
@@ -3632,7 +3653,7 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
         hipLaunchKernelGGL(clear_masks_kernel, dim3(std::min<uint32_t>(1024u, grid_for(nwords))), dim3(BLOCK), 0, ts,
                            sc->tail_masks, dev_n, mode);
         PropagateArgs at = a;
-        at.prio = tail_prio() ? 1u : 0u;
+        at.prio = (tail_prio() ? 1u : 0u) | (tail_gs64() ? 2u : 0u);
         at.alive_masks = sc->tail_masks;
         at.max_steps = sc->remaining;
         at.want = STEP_TAIL;
@@ -3652,6 +3673,7 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
         else CHR_HIP_CHECK(hipMemsetAsync(masks, 0, (size_t)nwords * 8, stream));
         a.max_steps = sc ? sc->remaining : max_steps;
         a.want = STEP_TAIL;
+        a.prio = tail_gs64() ? 2u : 0u;
         hipLaunchKernelGGL(sv.tail, dim3(grid_for((uint64_t)threads * sv.tail_group)), dim3(BLOCK), 0, stream,
                            (const DevGeom *)g->d_dev, a, cap);
     } else if (!split) {
