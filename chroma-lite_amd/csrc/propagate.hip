@@ -1948,7 +1948,8 @@ struct LdsRows {
 template <int GS, class M>
 __device__ __forceinline__ int walk_segment(const DevGeom &g, bool act, V3 o, V3 d, uint32_t last, int Gs_in, M stk, int cap, M tlist,
                             uint32_t &overflow, float &min_distance, uint32_t &iters,
-                            float best = __builtin_inff(), uint32_t best_rank = 0xFFFFFFFFu, int best_id = -1) {
+                            float best = __builtin_inff(), uint32_t best_rank = 0xFFFFFFFFu, int best_id = -1,
+                            uint32_t *rank_out = nullptr) {
     const int Gs = GS ? GS : Gs_in;
     constexpr uint32_t INVALID = 0xFFFFFFFFu;
     constexpr unsigned long long NONE = ~0ull;
@@ -2128,6 +2129,7 @@ __device__ __forceinline__ int walk_segment(const DevGeom &g, bool act, V3 o, V3
         if (cur != INVALID && cur_t > best) cur = INVALID;
     }
     min_distance = best_id == -1 ? -1.0f : best;
+    if (rank_out) *rank_out = best_rank;
     return best_id;
 }
 
@@ -2389,7 +2391,21 @@ struct TraceArgs {
     const uint32_t *dev_n;
     const uint32_t *mode;
     uint32_t drain_max;          // a wave drains its last <= drain_max walks whole-wave (0: never; at most 8)
+    // Long-walk help (trace_help_after): once the ray counter is exhausted, a
+    // walk past help_after node + triangle steps is published (help_entries);
+    // waves left without rays walk published walks with the whole wave
+    // (walk_segment, 8 cursors) and join their results as flat walks do.
+    // help_ctl: [0] published, [1] claimed, [2] this launch's serial, [3] join
+    // slots taken (all reset by the step head kernel); a published walk joins
+    // flat-list slot flat_cap - 1 - k (enrolled flat walks fill the list from
+    // 0: a walk is one or the other, so they never meet); help_after 0: off.
+    uint32_t help_after;
+    uint32_t flat_cap;
+    uint32_t *help_ctl;
+    uint32_t *help_entries;      // HELP_CAP x 12 words: o, d, last hit, flat slot, ready serial, done serial
 };
+constexpr uint32_t HELP_CAP = 8192;
+constexpr uint32_t HELP_WORDS = 12;
 
 // Enrol queue position p in the flat list of the next trace launch (its walk
 // is flat, walk_kind 2): f = slot in the flat list, hits[p] = (FLAT_HIT, f).
@@ -2507,6 +2523,12 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
     bool walk_done = true, drain = false;
     uint32_t qh = 0, qt = 0, pcur = 0, pleft = 0;
     constexpr uint32_t INVALID = 0xFFFFFFFFu;
+    // long-walk help (TraceArgs::help_after): this lane's walk was published as
+    // help entry hidx (its result then joins flat slot flat_f, like a sub-walk)
+    const bool help_on = !COUNT && a.help_after != 0u && a.help_ctl != nullptr;
+    const uint32_t serial = help_on ? a.help_ctl[2] : 0u;
+    bool handed = false, helping = false;
+    uint32_t hidx = 0, wsteps = 0;
     enum { P_NODE, P_TRI, P_REFILL, P_IDLE, P_DRAIN, P_BOX = 3 };   // regions (calls: P_REFILL = walks, P_BOX = boxes)
     Prof<5> pf;
     pf.start(P_REFILL);
@@ -2593,6 +2615,8 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
                     if (start) {
                         slab = make_slab(v3(-o.x / d.x, -o.y / d.y, -o.z / d.z), v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z));
                         best_id = -1;
+                        handed = false;
+                        wsteps = 0;
                         sp = 0;
                         walk_done = false;
                         has_ray = true;
@@ -2604,6 +2628,38 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
             }
         }
         if constexpr (!COUNT) {
+            if (help_on && exhausted && has_ray && !walk_done) {
+                if (handed) {
+                    // a helper finished this walk (its result is in flat_best): drop it
+                    // (polled every 16 steps: the load stalls the wave)
+                    if ((wsteps & 15u) == 0u &&
+                        __hip_atomic_load(a.help_entries + HELP_WORDS * hidx + 9, __ATOMIC_ACQUIRE,
+                                          __HIP_MEMORY_SCOPE_AGENT) == serial) {
+                        has_ray = false;
+                        pleft = 0;
+                        qh = qt;
+                    }
+                } else if (flat_f < 0 && wsteps > a.help_after) {
+                    const uint32_t idx = atomicAdd(a.help_ctl, 1u);
+                    if (idx < HELP_CAP) {
+                        // join point: a flat-list slot seeded with this walk's best so far
+                        const uint32_t f = a.flat_cap - 1u - atomicAdd(a.help_ctl + 3, 1u);
+                        a.flat_best[f] = best_id == -1 ? ~0ull
+                                                       : (((unsigned long long)__float_as_uint(best) << 32) | best_rank);
+                        a.hits[q] = make_int2(FLAT_HIT, (int)f);
+                        uint32_t *e = a.help_entries + HELP_WORDS * idx;
+                        e[0] = __float_as_uint(o.x); e[1] = __float_as_uint(o.y); e[2] = __float_as_uint(o.z);
+                        e[3] = __float_as_uint(d.x); e[4] = __float_as_uint(d.y); e[5] = __float_as_uint(d.z);
+                        e[6] = last;
+                        e[7] = f;
+                        e[9] = 0u;
+                        __hip_atomic_store(e + 8, serial, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                        flat_f = (int)f;
+                        handed = true;
+                        hidx = idx;
+                    }
+                }
+            }
             // Drain: once the ray counter is exhausted and at most 8 ordinary walks
             // are left in the wave, the whole wave finishes them together
             // (walk_segment: 8..64 lanes per walk, Gs/8 cursors each, a dependent
@@ -2614,7 +2670,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
             // best so far (conservative culling, the same nearest hit); the
             // lanes' stacks are abandoned and their LDS rows reused.
             if (exhausted && __ballot(has_ray) != 0 && (uint32_t)__popcll(__ballot(has_ray)) <= a.drain_max &&
-                __ballot(has_ray && flat_f >= 0) == 0) {
+                __ballot(has_ray && flat_f >= 0 && !handed) == 0) {   // no cut-item sub-walks (they start mid-tree)
                 drain = true;   // after the loop, where the walk state below is no longer live
                 break;
             }
@@ -2625,7 +2681,12 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
         const unsigned long long mw = __ballot(can_walk);
         const unsigned long long mt = __ballot(has_work);
         if ((mw | mt) == 0) {
-            if (exhausted && __ballot(has_ray) == 0) break;
+            if (exhausted && __ballot(has_ray) == 0) {
+                if constexpr (!COUNT) {
+                    if (help_on) helping = true;
+                }
+                break;
+            }
             continue;                                    // walks ended: publish + refill
         }
         if (mw != 0 && 8 * __popcll(mt) < F * __popcll(mw | mt)) {
@@ -2643,6 +2704,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
                 if (!found) { walk_done = true; continue; }
             }
             if constexpr (COUNT) { cnt.nodes++; walk_cost++; if (wave_leader()) cnt.wave_nodes++; }
+            wsteps++;
             const uint4 *np = g.wnodes + (size_t)g.wstride * node;
             const uint4 h = gld(np), a1 = gld(np + 1), a2 = gld(np + 2), a3 = gld(np + 3), a4 = gld(np + 4),
                         a5 = gld(np + 5);
@@ -2677,6 +2739,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
                 pleft = (e >> 30) + 1u;
             }
             if constexpr (COUNT) { cnt.tris++; walk_cost++; if (wave_leader()) cnt.wave_tris++; }
+            wsteps++;
             const float4 *r = g.wtri + 4 * (size_t)pcur;
             const float4 r0 = gld(r), r1 = gld(r + 1), r2 = gld(r + 2);
             pcur++;
@@ -2718,16 +2781,58 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
             const int seg0 = (int)lane & ~(Gs - 1);
             CHR_LDS uint32_t *wbase = (CHR_LDS uint32_t *)(lds + (threadIdx.x & ~63u));
             float sdist;
-            uint32_t sit;
+            uint32_t sit, srank_out = 0;
             const int tri = walk_segment<0>(g, act, so, sdir, slast, Gs, LdsRows{wbase, seg0 / 8 * TAIL_STACK * 2},
                                          TAIL_STACK * Gs / 8, LdsRows{wbase, 8 * TAIL_STACK * 2 + 4 * seg0}, overflow,
-                                         sdist, sit, sbest, srank, sid);
+                                         sdist, sit, sbest, srank, sid, &srank_out);
             const int mine = (__popcll(rm & ((1ull << lane) - 1ull)) * Gs) & 63;   // my segment's first lane
             const int rt = __shfl(tri, mine);
             const float rd = __shfl(sdist, mine);
+            const uint32_t rr = (uint32_t)__shfl((int)srank_out, mine);
             if (has_ray) {                                        // publish (mesh.h:123-125)
-                a.hits[q] = make_int2(rt, __float_as_int(rt == -1 ? -1.0f : rd));
+                if (handed) {   // a published walk: its result joins the flat slot
+                    if (rt != -1)
+                        atomicMin(a.flat_best + flat_f, ((unsigned long long)__float_as_uint(rd) << 32) | rr);
+                } else {
+                    a.hits[q] = make_int2(rt, __float_as_int(rt == -1 ? -1.0f : rd));
+                }
                 pf.call(P_DRAIN);
+            }
+            pf.tick(P_IDLE);
+            helping = help_on;   // then help the other waves' long walks
+        }
+        if (helping) {
+            // Help: walk published long walks with the whole wave (8 cursors),
+            // one claim at a time until none is left; each claim is a fresh index,
+            // so the loop ends.  A claimed entry not yet visible is left to its owner.
+            pf.tick(P_DRAIN);
+            CHR_LDS uint32_t *wbase = (CHR_LDS uint32_t *)(lds + (threadIdx.x & ~63u));
+            while (true) {
+                uint32_t i = 0;
+                if (lane == 0) i = atomicAdd(a.help_ctl + 1, 1u);
+                i = (uint32_t)__shfl((int)i, 0);
+                const uint32_t pub = __hip_atomic_load(a.help_ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (i >= pub || i >= HELP_CAP) break;
+                uint32_t *e = a.help_entries + HELP_WORDS * i;
+                if (__hip_atomic_load(e + 8, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != serial) continue;
+                const V3 ho = v3(__uint_as_float(e[0]), __uint_as_float(e[1]), __uint_as_float(e[2]));
+                const V3 hd = v3(__uint_as_float(e[3]), __uint_as_float(e[4]), __uint_as_float(e[5]));
+                const uint32_t hlast = e[6], hf = e[7];
+                if (hf >= a.flat_cap) continue;   // (defensive: entries are written before their ready word)
+                const unsigned long long seed = __hip_atomic_load(a.flat_best + hf, __ATOMIC_RELAXED,
+                                                                  __HIP_MEMORY_SCOPE_AGENT);
+                const float sb = seed == ~0ull ? __builtin_inff() : __uint_as_float((uint32_t)(seed >> 32));
+                const uint32_t sr = seed == ~0ull ? 0xFFFFFFFFu : (uint32_t)seed;
+                float hdist;
+                uint32_t hit_iters, hrank = 0;
+                const int ht = walk_segment<64>(g, true, ho, hd, hlast, 64, LdsRows{wbase, 0}, TAIL_STACK * 8,
+                                                LdsRows{wbase, 8 * TAIL_STACK * 2}, overflow, hdist, hit_iters, sb, sr,
+                                                -1, &hrank);
+                if (lane == 0) {
+                    if (ht != -1)
+                        atomicMin(a.flat_best + hf, ((unsigned long long)__float_as_uint(hdist) << 32) | hrank);
+                    __hip_atomic_store(e + 9, serial, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                }
             }
             pf.tick(P_IDLE);
         }
@@ -2924,6 +3029,11 @@ __global__ void step_head_kernel(const uint32_t *in_hdr, uint32_t *out_hdr, uint
     if (m != STEP_IDLE) {
         out_hdr[0] = 1u;
         ray_counter[0] = 0u;
+        // trace_kernel's long-walk help words (TraceArgs::help_ctl = ray_counter + 4)
+        ray_counter[4] = 0u;
+        ray_counter[5] = 0u;
+        ray_counter[6] += 1u;
+        ray_counter[7] = 0u;
     }
 }
 
@@ -3326,6 +3436,14 @@ struct StepVariant {
 // (demo.detector(), 4M photons: first-step walk 2.65 -> 2.21 ms for 0.11 ms of
 // sorting; second step unchanged).
 static constexpr uint32_t kBinFirstMin = 1u << 20;
+// CHR_TRACE_HELP=k: after the ray counter is exhausted, trace_kernel publishes
+// walks past k node + triangle steps for waves without rays to finish
+// (whole-wave walk); 0: off (A/B).  Default 64 (a mean 29k walk is ~30 steps).
+static uint32_t trace_help_after() {
+    const char *e = getenv("CHR_TRACE_HELP");
+    const int k = e ? atoi(e) : 64;
+    return (uint32_t)(k < 0 ? 0 : k);
+}
 // CHR_TRACE_R=16|32|48: trace_kernel refills once that many of a wave's 64
 // lanes are without a ray (default 32; A/B)
 static int trace_refill_r() {
@@ -3458,6 +3576,8 @@ struct FlatCtx {
     // step's classification, then every step's scatter for the next step),
     // rays_walk the binned first step's records permuted into walk order
     uint4 *rays = nullptr, *rays_walk = nullptr;
+    uint32_t *help_entries = nullptr;   // trace_kernel's long-walk help entries (HELP_CAP x HELP_WORDS)
+    uint32_t cap = 0;                   // entries of flat_q / flat_best
 };
 static int flat_get(uint32_t n, FlatCtx &fc, int ctx = 0) {
     static thread_local Scratch s[NCTX][16];
@@ -3476,6 +3596,7 @@ static int flat_get(uint32_t n, FlatCtx &fc, int ctx = 0) {
     fc.flat_q = (uint32_t *)(fc.flat_best + n);
     fc.cur = 0;
     fc.enrol_next = false;
+    fc.cap = n;
     return CHR_OK;
 }
 
@@ -3595,6 +3716,11 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
         ta.dev_n = dev_n;
         ta.mode = mode;
         ta.drain_max = trace_drain_max();
+        // long-walk help: device-driven slots only (the head kernel resets its words)
+        ta.help_after = (sc && fc->help_entries) ? trace_help_after() : 0u;
+        ta.help_ctl = next + 4;
+        ta.help_entries = fc->help_entries;
+        ta.flat_cap = fc->cap;
         a.flat_best = fc->flat_best;
         a.zero_word = count_next;   // cleared by the shade pass, filled by this step's scatter
         if (fc->enrol_next)
@@ -3808,7 +3934,7 @@ static int prop_bufs(uint32_t nphotons, int32_t ntpb, int32_t max_blocks, int ct
     // split path: hits, ray counter, binning keys/order/histogram
     const size_t hbytes = b.fused ? (size_t)nphotons * 24 + 128 + 256 + 512 + sort_temp_bytes16(nphotons) : 0;
     // split path: ray records, queue order + walk order (FlatCtx::rays / rays_walk)
-    const size_t rbytes = b.fused ? (size_t)nphotons * 64 + 512 : 0;
+    const size_t rbytes = b.fused ? (size_t)nphotons * 64 + 512 + HELP_CAP * HELP_WORDS * 4 + 256 : 0;
     const size_t base_bytes = 2 * qbytes + swords * 4 + 64 + hbytes + rbytes;
     const size_t mbytes = tail_masks ? ((size_t)nphotons + 63) / 64 * 8 + 512 : 0;
     void *buf = nullptr;
@@ -3827,6 +3953,7 @@ static int prop_bufs(uint32_t nphotons, int32_t ntpb, int32_t max_blocks, int ct
     if (b.fused) {
         b.fc.rays = (uint4 *)(((uintptr_t)buf + 2 * qbytes + swords * 4 + 64 + hbytes + 255) & ~(uintptr_t)255);
         b.fc.rays_walk = b.fc.rays + 2 * (size_t)nphotons;
+        b.fc.help_entries = (uint32_t *)(((uintptr_t)(b.fc.rays_walk + 2 * (size_t)nphotons) + 255) & ~(uintptr_t)255);
     }
     return CHR_OK;
 }
@@ -3839,6 +3966,9 @@ static int prop_start(const PropBufs &b, uint32_t nphotons, uint32_t true_nphoto
     hipLaunchKernelGGL(init_queue_kernel, dim3(grid_for(nphotons)), dim3(BLOCK), 0, stream, b.q[0], b.q[1], nphotons,
                        true_nphotons, ncopies, z);
     CHR_HIP_CHECK(hipGetLastError());
+    // long-walk help entries: ready words of an earlier buffer use are launch serials;
+    // a fresh allocation is cleared so no stale word can match one
+    if (b.fc.help_entries) CHR_HIP_CHECK(hipMemsetAsync(b.fc.help_entries, 0, HELP_CAP * HELP_WORDS * 4, stream));
     return CHR_OK;
 }
 
