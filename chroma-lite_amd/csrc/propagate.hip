@@ -2399,12 +2399,21 @@ struct TraceArgs {
     // slots taken (all reset by the step head kernel); a published walk joins
     // flat-list slot flat_cap - 1 - k (enrolled flat walks fill the list from
     // 0: a walk is one or the other, so they never meet); help_after 0: off.
+    // No fences: a published entry is HELP_DATA 64-bit words, each the launch
+    // serial above one data word (o, d, last hit, flat slot, seed key hi/lo),
+    // written with plain device-coherent atomic stores after the slot's seed
+    // exchange has completed; a helper takes an entry only when all its words
+    // carry this launch's serial (else its owner finishes the walk alone).
+    // Word HELP_DATA: the serial once a helper has joined its result.  (An
+    // agent-scope release/acquire would write back / invalidate the XCD's L2
+    // at every publish and poll: measured 16.0 -> 21.7 ms of trace per step.)
     uint32_t help_after;
     uint32_t flat_cap;
     uint32_t *help_ctl;
-    uint32_t *help_entries;      // HELP_CAP x 12 words: o, d, last hit, flat slot, ready serial, done serial
+    unsigned long long *help_entries;   // HELP_CAP x HELP_WORDS
 };
 constexpr uint32_t HELP_CAP = 8192;
+constexpr uint32_t HELP_DATA = 10;
 constexpr uint32_t HELP_WORDS = 12;
 
 // Enrol queue position p in the flat list of the next trace launch (its walk
@@ -2529,6 +2538,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
     const uint32_t serial = help_on ? a.help_ctl[2] : 0u;
     bool handed = false, helping = false;
     uint32_t hidx = 0, wsteps = 0;
+    unsigned long long poll = 0;   // the handed walk's done word, read one iteration ahead of its use
     enum { P_NODE, P_TRI, P_REFILL, P_IDLE, P_DRAIN, P_BOX = 3 };   // regions (calls: P_REFILL = walks, P_BOX = boxes)
     Prof<5> pf;
     pf.start(P_REFILL);
@@ -2630,33 +2640,38 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
         if constexpr (!COUNT) {
             if (help_on && exhausted && has_ray && !walk_done) {
                 if (handed) {
-                    // a helper finished this walk (its result is in flat_best): drop it
-                    // (polled every 16 steps: the load stalls the wave)
-                    if ((wsteps & 15u) == 0u &&
-                        __hip_atomic_load(a.help_entries + HELP_WORDS * hidx + 9, __ATOMIC_ACQUIRE,
-                                          __HIP_MEMORY_SCOPE_AGENT) == serial) {
+                    // a helper joined this walk's result into its slot: drop it
+                    if ((uint32_t)poll == serial) {
                         has_ray = false;
                         pleft = 0;
                         qh = qt;
+                    } else {
+                        poll = __hip_atomic_load(a.help_entries + HELP_WORDS * hidx + HELP_DATA, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
                     }
                 } else if (flat_f < 0 && wsteps > a.help_after) {
                     const uint32_t idx = atomicAdd(a.help_ctl, 1u);
                     if (idx < HELP_CAP) {
                         // join point: a flat-list slot seeded with this walk's best so far
                         const uint32_t f = a.flat_cap - 1u - atomicAdd(a.help_ctl + 3, 1u);
-                        a.flat_best[f] = best_id == -1 ? ~0ull
-                                                       : (((unsigned long long)__float_as_uint(best) << 32) | best_rank);
+                        const unsigned long long seed =
+                            best_id == -1 ? ~0ull : (((unsigned long long)__float_as_uint(best) << 32) | best_rank);
+                        const unsigned long long prev = atomicExch(a.flat_best + f, seed);
                         a.hits[q] = make_int2(FLAT_HIT, (int)f);
-                        uint32_t *e = a.help_entries + HELP_WORDS * idx;
-                        e[0] = __float_as_uint(o.x); e[1] = __float_as_uint(o.y); e[2] = __float_as_uint(o.z);
-                        e[3] = __float_as_uint(d.x); e[4] = __float_as_uint(d.y); e[5] = __float_as_uint(d.z);
-                        e[6] = last;
-                        e[7] = f;
-                        e[9] = 0u;
-                        __hip_atomic_store(e + 8, serial, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                        // the entry only after the exchange has completed (its result is an
+                        // operand here): a helper's atomicMin can never precede the seed
+                        asm volatile("" ::"v"((uint32_t)prev), "v"((uint32_t)(prev >> 32)) : "memory");
+                        const uint32_t w[HELP_DATA] = {__float_as_uint(o.x), __float_as_uint(o.y), __float_as_uint(o.z),
+                                                       __float_as_uint(d.x), __float_as_uint(d.y), __float_as_uint(d.z),
+                                                       last, f, (uint32_t)(seed >> 32), (uint32_t)seed};
+                        unsigned long long *e = a.help_entries + HELP_WORDS * idx;
+                        for (uint32_t k = 0; k < HELP_DATA; ++k)
+                            __hip_atomic_store(e + k, ((unsigned long long)serial << 32) | w[k], __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
                         flat_f = (int)f;
                         handed = true;
                         hidx = idx;
+                        poll = 0;
                     }
                 }
             }
@@ -2813,14 +2828,19 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
                 i = (uint32_t)__shfl((int)i, 0);
                 const uint32_t pub = __hip_atomic_load(a.help_ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 if (i >= pub || i >= HELP_CAP) break;
-                uint32_t *e = a.help_entries + HELP_WORDS * i;
-                if (__hip_atomic_load(e + 8, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != serial) continue;
-                const V3 ho = v3(__uint_as_float(e[0]), __uint_as_float(e[1]), __uint_as_float(e[2]));
-                const V3 hd = v3(__uint_as_float(e[3]), __uint_as_float(e[4]), __uint_as_float(e[5]));
-                const uint32_t hlast = e[6], hf = e[7];
-                if (hf >= a.flat_cap) continue;   // (defensive: entries are written before their ready word)
-                const unsigned long long seed = __hip_atomic_load(a.flat_best + hf, __ATOMIC_RELAXED,
-                                                                  __HIP_MEMORY_SCOPE_AGENT);
+                unsigned long long *e = a.help_entries + HELP_WORDS * i;
+                // lane k reads data word k; the entry is whole when every word carries the serial
+                unsigned long long wk = 0;
+                if (lane < HELP_DATA) wk = __hip_atomic_load(e + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const unsigned long long okm = __ballot(lane < HELP_DATA && (uint32_t)(wk >> 32) == serial);
+                if (okm != (1ull << HELP_DATA) - 1ull) continue;
+                const uint32_t lo = (uint32_t)wk;
+                auto word = [&](int k) { return (uint32_t)__shfl((int)lo, k); };
+                const V3 ho = v3(__uint_as_float(word(0)), __uint_as_float(word(1)), __uint_as_float(word(2)));
+                const V3 hd = v3(__uint_as_float(word(3)), __uint_as_float(word(4)), __uint_as_float(word(5)));
+                const uint32_t hlast = word(6), hf = word(7);
+                if (hf >= a.flat_cap) continue;   // (defensive)
+                const unsigned long long seed = ((unsigned long long)word(8) << 32) | word(9);
                 const float sb = seed == ~0ull ? __builtin_inff() : __uint_as_float((uint32_t)(seed >> 32));
                 const uint32_t sr = seed == ~0ull ? 0xFFFFFFFFu : (uint32_t)seed;
                 float hdist;
@@ -2831,7 +2851,8 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
                 if (lane == 0) {
                     if (ht != -1)
                         atomicMin(a.flat_best + hf, ((unsigned long long)__float_as_uint(hdist) << 32) | hrank);
-                    __hip_atomic_store(e + 9, serial, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(e + HELP_DATA, (unsigned long long)serial, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
                 }
             }
             pf.tick(P_IDLE);
@@ -3032,7 +3053,7 @@ __global__ void step_head_kernel(const uint32_t *in_hdr, uint32_t *out_hdr, uint
         // trace_kernel's long-walk help words (TraceArgs::help_ctl = ray_counter + 4)
         ray_counter[4] = 0u;
         ray_counter[5] = 0u;
-        ray_counter[6] += 1u;
+        ray_counter[6] = ray_counter[6] + 1u == 0u ? 1u : ray_counter[6] + 1u;   // never 0 (cleared entries)
         ray_counter[7] = 0u;
     }
 }
@@ -3576,7 +3597,7 @@ struct FlatCtx {
     // step's classification, then every step's scatter for the next step),
     // rays_walk the binned first step's records permuted into walk order
     uint4 *rays = nullptr, *rays_walk = nullptr;
-    uint32_t *help_entries = nullptr;   // trace_kernel's long-walk help entries (HELP_CAP x HELP_WORDS)
+    unsigned long long *help_entries = nullptr;   // trace_kernel's long-walk help entries (HELP_CAP x HELP_WORDS)
     uint32_t cap = 0;                   // entries of flat_q / flat_best
 };
 static int flat_get(uint32_t n, FlatCtx &fc, int ctx = 0) {
@@ -3934,7 +3955,7 @@ static int prop_bufs(uint32_t nphotons, int32_t ntpb, int32_t max_blocks, int ct
     // split path: hits, ray counter, binning keys/order/histogram
     const size_t hbytes = b.fused ? (size_t)nphotons * 24 + 128 + 256 + 512 + sort_temp_bytes16(nphotons) : 0;
     // split path: ray records, queue order + walk order (FlatCtx::rays / rays_walk)
-    const size_t rbytes = b.fused ? (size_t)nphotons * 64 + 512 + HELP_CAP * HELP_WORDS * 4 + 256 : 0;
+    const size_t rbytes = b.fused ? (size_t)nphotons * 64 + 512 + HELP_CAP * HELP_WORDS * 8 + 256 : 0;
     const size_t base_bytes = 2 * qbytes + swords * 4 + 64 + hbytes + rbytes;
     const size_t mbytes = tail_masks ? ((size_t)nphotons + 63) / 64 * 8 + 512 : 0;
     void *buf = nullptr;
@@ -3953,7 +3974,8 @@ static int prop_bufs(uint32_t nphotons, int32_t ntpb, int32_t max_blocks, int ct
     if (b.fused) {
         b.fc.rays = (uint4 *)(((uintptr_t)buf + 2 * qbytes + swords * 4 + 64 + hbytes + 255) & ~(uintptr_t)255);
         b.fc.rays_walk = b.fc.rays + 2 * (size_t)nphotons;
-        b.fc.help_entries = (uint32_t *)(((uintptr_t)(b.fc.rays_walk + 2 * (size_t)nphotons) + 255) & ~(uintptr_t)255);
+        b.fc.help_entries =
+            (unsigned long long *)(((uintptr_t)(b.fc.rays_walk + 2 * (size_t)nphotons) + 255) & ~(uintptr_t)255);
     }
     return CHR_OK;
 }
@@ -3968,7 +3990,7 @@ static int prop_start(const PropBufs &b, uint32_t nphotons, uint32_t true_nphoto
     CHR_HIP_CHECK(hipGetLastError());
     // long-walk help entries: ready words of an earlier buffer use are launch serials;
     // a fresh allocation is cleared so no stale word can match one
-    if (b.fc.help_entries) CHR_HIP_CHECK(hipMemsetAsync(b.fc.help_entries, 0, HELP_CAP * HELP_WORDS * 4, stream));
+    if (b.fc.help_entries) CHR_HIP_CHECK(hipMemsetAsync(b.fc.help_entries, 0, HELP_CAP * HELP_WORDS * 8, stream));
     return CHR_OK;
 }
 

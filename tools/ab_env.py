@@ -62,6 +62,8 @@ def main():
     for r in range(rounds):
         for name, env in parsed:
             apply(env)
+            # the same RNG start for every configuration: identical batches, tails and walks
+            wl.rng = gpu.get_rng_states(wl.nslots, seed=args.seed)
             elapsed, per_step, stats = bench.timed_loop(wl.run, args.steps, max(2, args.warmup), None, wl.sync,
                                                         wl.group)
             rep = wl.rank_report(stats)
