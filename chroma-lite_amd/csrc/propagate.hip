@@ -3459,10 +3459,13 @@ struct StepVariant {
 static constexpr uint32_t kBinFirstMin = 1u << 20;
 // CHR_TRACE_HELP=k: after the ray counter is exhausted, trace_kernel publishes
 // walks past k node + triangle steps for waves without rays to finish
-// (whole-wave walk); 0: off (A/B).  Default 64 (a mean 29k walk is ~30 steps).
+// (whole-wave walk); 0: off.  Off by default: on the 29k bench it costs more
+// than it saves (trace ms per step 16.1 off, 19.8 at 64, 30.9 at 32, 16.8 at
+// 128; profiles/r03/ab2): every hand-off stalls its wave on three dependent
+// atomics, and helpers only find walks published before they look.
 static uint32_t trace_help_after() {
     const char *e = getenv("CHR_TRACE_HELP");
-    const int k = e ? atoi(e) : 64;
+    const int k = e ? atoi(e) : 0;
     return (uint32_t)(k < 0 ? 0 : k);
 }
 // CHR_TRACE_R=16|32|48: trace_kernel refills once that many of a wave's 64
