@@ -3392,9 +3392,12 @@ static constexpr int kExactVariant = 1;
 // launch lasts as long as its longest-lived photon, so fewer resident waves
 // means more rounds of waves behind it)
 static constexpr int kGroupWaves = 4;
-// propagate_tail_kernel (wave-adaptive walk) at 3 waves/SIMD: 168 VGPRs, no
-// VGPR spills (at 4: 64 spilled; r02 A/B on the 29k bench: 380.4 vs 376.9 M/s)
-static constexpr int kTailWaves = 3;
+// propagate_tail_kernel (wave-adaptive walk) at 2 waves/SIMD: ~200 VGPRs, no
+// spills, no private segment.  r03 A/B on the 29k bench (profiles/r03/ab3, same
+// batches and RNG for every configuration): the long-lived photon's step 26.7 ->
+// 21.5 us, mean tail 7.31 -> 6.64 ms against 3 waves/SIMD (168 VGPRs, 51 spilled
+// once the GS = 64 walk was added); r02 measured 3 waves ahead of 4 (64 spills).
+static constexpr int kTailWaves = 2;
 static int tail_waves() {              // CHR_TAIL_WAVES=4: the tail kernel at 4 waves/SIMD (A/B)
     const char *e = getenv("CHR_TAIL_WAVES");
     return e ? atoi(e) : kTailWaves;
@@ -3403,10 +3406,12 @@ static bool tail_group_walk() {        // CHR_TAIL=group: the fixed 8-lane group
     const char *e = getenv("CHR_TAIL");
     return e && std::strcmp(e, "group") == 0;
 }
-// CHR_TRACE_DRAIN=k: trace_kernel waves drain their last <= k walks whole-wave (default 8, 0 = off; A/B)
+// CHR_TRACE_DRAIN=k: trace_kernel waves drain their last <= k walks whole-wave
+// (0 = off; A/B).  Default 4 (r03 ab3: trace ms per step 16.23 at 8, 15.92 at 2,
+// 15.90 at 4, 16.33 off): with <= 4 walks each gets >= 2 cursors.
 static uint32_t trace_drain_max() {
     const char *e = getenv("CHR_TRACE_DRAIN");
-    const int k = e ? atoi(e) : 8;
+    const int k = e ? atoi(e) : 4;
     return (uint32_t)(k < 0 ? 0 : (k > 8 ? 8 : k));
 }
 // CHR_TAIL_GS64=0: the tail's lone-walker walks through the generic segment
@@ -3468,11 +3473,19 @@ static uint32_t trace_help_after() {
     const int k = e ? atoi(e) : 0;
     return (uint32_t)(k < 0 ? 0 : k);
 }
+// CHR_PREFIX_GRID=k: the prefix walk's persistent grid is 1/k of the full one (default 1; A/B)
+static uint32_t prefix_grid_div() {
+    const char *e = getenv("CHR_PREFIX_GRID");
+    const int k = e ? atoi(e) : 1;
+    return (uint32_t)(k < 1 ? 1 : (k > 16 ? 16 : k));
+}
 // CHR_TRACE_R=16|32|48: trace_kernel refills once that many of a wave's 64
-// lanes are without a ray (default 32; A/B)
+// lanes are without a ray (A/B).  Default 48 (r03 ab3: trace ms per step 17.87 at
+// 16, 16.25 at 32, 15.81 at 48; the binned first launch 5.74 -> 5.33 ms: its
+// coherent rays walk in phase, and fewer, larger refills keep them so).
 static int trace_refill_r() {
     const char *e = getenv("CHR_TRACE_R");
-    return e ? atoi(e) : 32;
+    return e ? atoi(e) : 48;
 }
 static StepVariant select_step_variant(const chr_geometry *g) {
     const char *e = getenv("CHR_PROPAGATE_VARIANT");
@@ -3499,11 +3512,11 @@ static StepVariant select_step_variant(const chr_geometry *g) {
         default:   // 0, 7, 8
             sv.fn = propagate_step_kernel<8, 4, kWalk>;
             sv.trace = trace_refill_r() == 16 ? trace_kernel<false, 6, 12, 4, 16>
-                       : (trace_refill_r() == 48 ? trace_kernel<false, 6, 12, 4, 48> : trace_kernel<false, 6, 12, 4, 32>);
+                       : (trace_refill_r() == 32 ? trace_kernel<false, 6, 12, 4, 32> : trace_kernel<false, 6, 12, 4, 48>);
             sv.shade = shade_kernel<3>;
             sv.tail = tail_group_walk() ? propagate_group_kernel<8, kGroupWaves>
                       : (tail_waves() == 4 ? propagate_tail_kernel<4>
-                         : (tail_waves() == 2 ? propagate_tail_kernel<2> : propagate_tail_kernel<kTailWaves>));
+                         : (tail_waves() == 3 ? propagate_tail_kernel<3> : propagate_tail_kernel<kTailWaves>));
             sv.tail_group = 8;
             sv.binned = v == 7 ? 1 : (v == 8 ? 0 : 2);
             break;
@@ -3775,7 +3788,10 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
         if (pre) {
             const int cus = device_cus();
             if (cus <= 0) return chr::fail(CHR_ERR_HIP, "launch_step: no compute units");
-            const uint64_t resident = (uint64_t)cus * 4 * sv.trace_waves * 64 / BLOCK;   // persistent grid
+            uint64_t resident = (uint64_t)cus * 4 * sv.trace_waves * 64 / BLOCK;   // persistent grid
+            // a batch's prefix walk (chr_propagate_batches) runs beside the previous
+            // batch's kernels: CHR_PREFIX_GRID=1/k of the grid leaves them CUs (A/B)
+            if (sc && sc->phase == PHASE_PREFIX) resident = std::max<uint64_t>(1, resident / prefix_grid_div());
             const uint32_t blocks = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(resident, grid_for(n)));
             if (int rc = walk_stack_get((size_t)WIDE_STACK * blocks * BLOCK * sizeof(uint2), &ta.spill, sc ? sc->ctx : 0))
                 return rc;
@@ -4668,9 +4684,9 @@ extern "C" int chr_kernel_info(int32_t which, chr_kernel_attr *out) {
     const void *fn = nullptr;
     const char *name = nullptr;
     switch (which) {
-        case 0: fn = (const void *)trace_kernel<false, 6, 12, 4, 32>; name = "chr::trace_kernel<false,6,12,4,32>"; break;
+        case 0: fn = (const void *)trace_kernel<false, 6, 12, 4, 48>; name = "chr::trace_kernel<false,6,12,4,48>"; break;
         case 1: fn = (const void *)shade_kernel<3>; name = "chr::shade_kernel<3>"; break;
-        case 2: fn = (const void *)propagate_tail_kernel<kTailWaves>; name = "chr::propagate_tail_kernel<3>"; break;
+        case 2: fn = (const void *)propagate_tail_kernel<kTailWaves>; name = "chr::propagate_tail_kernel<2>"; break;
         case 3: fn = (const void *)propagate_step_kernel<8, 4, kWalk>; name = "chr::propagate_step_kernel<8,4,2006>"; break;
         default: return chr::fail(CHR_ERR_INVALID, "chr_kernel_info: unknown kernel %d", which);
     }
@@ -4747,3 +4763,24 @@ extern "C" int chr_device_profile_fetch(uint64_t *h_calls, uint64_t *h_cycles, i
 // The renderer (render.cu, hybrid_render.cu, transform.cu): same translation
 // unit, it walks the same BVH and runs the same photon physics.
 #include "render.hip"
+
+#ifdef CHR_WALK_PROBE
+// ISA inspection only (make probe): walk_segment alone, whole wave, GS = 64 / run-time width
+namespace chr {
+__global__ __launch_bounds__(BLOCK) void walk_probe_kernel(const DevGeom *__restrict__ gdev, const float *od,
+                                                           int *out, int gs) {
+    __shared__ uint32_t stacks[(BLOCK / 8) * TAIL_STACK * 2];
+    __shared__ uint32_t tris[(BLOCK / 64) * 2 * TAIL_TRI];
+    CHR_LDS uint32_t *wstack = (CHR_LDS uint32_t *)stacks + (threadIdx.x >> 6) * 8 * TAIL_STACK * 2;
+    CHR_LDS uint32_t *wtris = (CHR_LDS uint32_t *)tris + (threadIdx.x >> 6) * 2 * TAIL_TRI;
+    uint32_t overflow = 0, it = 0;
+    float sd;
+    const V3 o = v3(od[0], od[1], od[2]), d = v3(od[3], od[4], od[5]);
+    const int st = gs == 64 ? walk_segment<64>(*gdev, true, o, d, 7u, 64, LdsFlat{wstack}, TAIL_STACK * 8, LdsFlat{wtris},
+                                               overflow, sd, it)
+                            : walk_segment<0>(*gdev, true, o, d, 7u, gs, LdsFlat{wstack}, TAIL_STACK * gs / 8,
+                                              LdsFlat{wtris}, overflow, sd, it);
+    out[threadIdx.x] = st + (int)overflow + (int)it + (int)sd;
+}
+}  // namespace chr
+#endif
