@@ -80,3 +80,39 @@ def test_xorwow_subsequences_differ():
     rows = st.reshape(6, 64)
     assert len({tuple(rows[:, s]) for s in range(64)}) == 64
     assert (rows[0] == rows[0, 0]).all()     # d is not moved by a 2^67 jump
+
+
+def _first_uniforms(states, nslots):
+    """The first curand_uniform of every slot, vectorised from the SoA states
+    (d, v0..v4; chroma_rng.h chr_xorwow_next / chr_uniform01)."""
+    st = states.reshape(6, nslots).astype(np.uint64)
+    d, v0, v4 = st[0], st[1], st[5]
+    m = np.uint64(0xFFFFFFFF)
+    t = (v0 ^ (v0 >> np.uint64(2))) & m
+    v4n = ((v4 ^ (v4 << np.uint64(4))) ^ (t ^ (t << np.uint64(1)))) & m
+    x = (v4n + ((d + np.uint64(362437)) & m)) & m
+    return (x.astype(np.float32) * np.float32(2.3283064365386963e-10) + np.float32(1.1641532182693481e-10))
+
+
+def test_xorwow_seed0_pooled_ks_is_a_stream_property():
+    """The reference's sample_cdf pin (test_sample_cdf.py: 128x128 slots,
+    curand_init(0, slot, offset=rep), 50 reps) is judged on MI355X by per-rep
+    KS uniformity plus a chi-square (tests/test_gpu_device_math.py), because
+    the pooled continuous KS of its 819,200 draws is low at seed 0.  That low
+    value belongs to the XORWOW stream itself, before any sampler: the first
+    uniforms of the CPU restatement (oracle rng_init, the same generator the
+    HIP path matches bit for bit) give the same p ~ 0.005 at seed 0 and
+    unremarkable values at other seeds."""
+    from scipy import stats
+    n = 128 * 128
+
+    def pooled(seed):
+        u = np.concatenate([_first_uniforms(oracle.rng_init(n, seed=seed, offset=rep), n) for rep in range(50)])
+        return stats.kstest(u.astype(np.float64), 'uniform').pvalue
+    p0 = pooled(0)
+    assert p0 < 0.02, p0
+    assert all(pooled(s) > 0.05 for s in (1, 2)), [pooled(s) for s in (1, 2)]
+    # the vectorised first draw is the generator's own
+    st = oracle.rng_init(64, seed=0, offset=3)
+    want = np.array([oracle.uniforms(st.copy(), 64, s, 1)[0] for s in range(64)], np.float32)
+    assert np.array_equal(_first_uniforms(st, 64), want)
