@@ -26,8 +26,12 @@ if [ "$MODE" = tests ] || [ "$MODE" = all ]; then
     tail -3 "$O/pytest_gpu.log"
 fi
 if [ "$MODE" = prof ]; then
+    # kernel trace + FETCH/WRITE/L2 passes of the bench workload, stamped (GIT_HEAD from the caller)
     bash "$R/tools/rocprof_bench.sh" "gpurun_out/$TAG/prof" --steps 3 --warmup 1 || exit $?
     cp "$O/prof/pmc_traffic.json" "$R/profiles/latest_pmc.json" || exit $?
+    # device region profile (libchroma_amd_prof.so)
+    ( cd /tmp && export TMPDIR=/tmp && CHROMA_DEVICE_PROFILE=1 timeout -k 10 600 python3 "$R/bench.py" --steps 3 --warmup 1 \
+        --no-cpu-baseline --no-count > "$O/devprof.json" 2> "$O/devprof.log" ) || { tail -5 "$O/devprof.log"; exit 1; }
 fi
 if [ "$MODE" = bench ] || [ "$MODE" = all ] || [ "$MODE" = prof ]; then
     cd /tmp && export TMPDIR=/tmp
