@@ -1953,6 +1953,20 @@ __device__ __forceinline__ int walk_segment(const DevGeom &g, bool act, V3 o, V3
     const int Gs = GS ? GS : Gs_in;
     constexpr uint32_t INVALID = 0xFFFFFFFFu;
     constexpr unsigned long long NONE = ~0ull;
+    // GS = 64: one ray for the whole wave -- the ray, its best hit and the loop
+    // state are wave-uniform; saying so (readfirstlane) lets them live in SGPRs
+    // and the loop branch on scalar conditions instead of exec masks
+    auto ufl = [](float x) { return GS == 64 ? __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(x))) : x; };
+    auto uu = [](uint32_t x) { return GS == 64 ? (uint32_t)__builtin_amdgcn_readfirstlane((int)x) : x; };
+    if (GS == 64) {
+        act = uu(act ? 1u : 0u) != 0u;
+        o = v3(ufl(o.x), ufl(o.y), ufl(o.z));
+        d = v3(ufl(d.x), ufl(d.y), ufl(d.z));
+        last = uu(last);
+        best = ufl(best);
+        best_rank = uu(best_rank);
+        best_id = (int)uu((uint32_t)best_id);
+    }
     const uint32_t lane = __lane_id();
     const uint32_t seg0 = lane & ~(uint32_t)(Gs - 1);
     const uint32_t L = lane - seg0;                   // lane within the segment
@@ -2120,9 +2134,9 @@ __device__ __forceinline__ int walk_segment(const DevGeom &g, bool act, V3 o, V3
                     if (ok < lkey) { lkey = ok; lid = oid; }
                 }
             }
-            best = __uint_as_float((uint32_t)(lkey >> 32));
-            best_rank = (uint32_t)lkey;
-            best_id = lid;
+            best = ufl(__uint_as_float((uint32_t)(lkey >> 32)));
+            best_rank = uu((uint32_t)lkey);
+            best_id = (int)uu((uint32_t)lid);
         }
         Tp = Tn;
         pb ^= 1;
@@ -2409,10 +2423,12 @@ struct TraceArgs {
     // at every publish and poll: measured 16.0 -> 21.7 ms of trace per step.)
     uint32_t help_after;
     uint32_t flat_cap;
+    uint32_t claim_ahead;        // refills from claimed chunks, the next claim in flight (trace_claim_ahead)
     uint32_t *help_ctl;
     unsigned long long *help_entries;   // HELP_CAP x HELP_WORDS
 };
 constexpr uint32_t HELP_CAP = 8192;
+constexpr uint32_t CLAIM = 64;   // ray-counter chunk of trace_kernel's claim-ahead refill
 constexpr uint32_t HELP_DATA = 10;
 constexpr uint32_t HELP_WORDS = 12;
 
@@ -2536,6 +2552,10 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
     // help entry hidx (its result then joins flat slot flat_f, like a sub-walk)
     const bool help_on = !COUNT && a.help_after != 0u && a.help_ctl != nullptr;
     const uint32_t serial = help_on ? a.help_ctl[2] : 0u;
+    // claimed ray-counter chunk (claim_ahead): next index cb, cn left; pend: the
+    // next chunk's base, claimed ahead (valid in lane 0 once have_pend)
+    uint32_t cb = 0, cn = 0, pend = 0;
+    bool have_pend = false;
     bool handed = false, helping = false;
     uint32_t hidx = 0, wsteps = 0;
     unsigned long long poll = 0;   // the handed walk's done word, read one iteration ahead of its use
@@ -2560,13 +2580,45 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
         if (!exhausted) {
             const unsigned long long need = __ballot(!has_ray);
             if (need != 0 && (__popcll(need) >= R || need == __ballot(1))) {
-                const int leader = __ffsll((long long)need) - 1;
-                uint32_t base = 0;
-                if ((int)lane == leader) base = atomicAdd(a.next, (uint32_t)__popcll(need));
-                base = __shfl(base, leader);
-                if (base + (uint32_t)__popcll(need) >= total) exhausted = true;
+                const uint32_t want = (uint32_t)__popcll(need);
+                const uint32_t rank = (uint32_t)__popcll(need & ((1ull << lane) - 1ull));
+                uint32_t j;
+                if (a.claim_ahead) {
+                    // Rays come from the wave's claimed chunk (CLAIM indices of the ray
+                    // counter); the next chunk's atomic is issued while the wave still
+                    // walks, so a refill does not wait on the counter's round trip.  Near
+                    // the end of a launch (fewer rays left than two grids of lanes) chunks
+                    // are claimed when needed, so no wave sits on rays others could walk.
+                    uint32_t b0 = cb, g0 = want < cn ? want : cn;
+                    cb += g0;
+                    cn -= g0;
+                    uint32_t b1 = 0, g1 = 0;
+                    if (g0 < want) {   // this chunk is used up: the pending one, or a claim now
+                        uint32_t nb = 0;
+                        if (have_pend) nb = (uint32_t)__shfl((int)pend, 0);
+                        else if (lane == 0) nb = atomicAdd(a.next, CLAIM);
+                        nb = have_pend ? nb : (uint32_t)__shfl((int)nb, 0);
+                        have_pend = false;
+                        b1 = nb;
+                        g1 = want - g0 < CLAIM ? want - g0 : CLAIM;
+                        cb = nb + g1;
+                        cn = CLAIM - g1;
+                    }
+                    j = rank < g0 ? b0 + rank : b1 + (rank - g0);
+                    if (cb >= total) exhausted = true;     // later claims lie beyond the last item
+                    else if (!have_pend && cb + 2u * gridDim.x * BLOCK < total) {
+                        if (lane == 0) pend = atomicAdd(a.next, CLAIM);
+                        have_pend = true;
+                    }
+                } else {
+                    const int leader = __ffsll((long long)need) - 1;
+                    uint32_t base = 0;
+                    if ((int)lane == leader) base = atomicAdd(a.next, want);
+                    base = __shfl(base, leader);
+                    if (base + want >= total) exhausted = true;
+                    j = base + rank;
+                }
                 if (!has_ray) {
-                    const uint32_t j = base + (uint32_t)__popcll(need & ((1ull << lane) - 1ull));
                     bool start = false;
                     if (j < n && a.rays) {
                         // the ray record: one 32-B load (put_ray); skip bit: dead / NaN / flat
@@ -3059,6 +3111,7 @@ __global__ void step_head_kernel(const uint32_t *in_hdr, uint32_t *out_hdr, uint
 }
 
 // alive-mask words of a tail slot (OR-ed by its kernel) zeroed, for the slot's queue length
+constexpr uint32_t kClearBlocks = 4;
 __global__ __launch_bounds__(BLOCK) void clear_masks_kernel(unsigned long long *masks, const uint32_t *dev_n,
                                                             const uint32_t *mode) {
     if (*mode != STEP_TAIL) return;
@@ -3473,6 +3526,12 @@ static uint32_t trace_help_after() {
     const int k = e ? atoi(e) : 0;
     return (uint32_t)(k < 0 ? 0 : k);
 }
+// CHR_TRACE_AHEAD=0: trace_kernel claims rays per refill with a blocking
+// atomic (r02 scheme) instead of from chunks claimed ahead (A/B)
+static bool trace_claim_ahead() {
+    const char *e = getenv("CHR_TRACE_AHEAD");
+    return !(e && e[0] == '0');
+}
 // CHR_PREFIX_GRID=k: the prefix walk's persistent grid is 1/k of the full one (default 1; A/B)
 static uint32_t prefix_grid_div() {
     const char *e = getenv("CHR_PREFIX_GRID");
@@ -3758,6 +3817,7 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
         ta.help_ctl = next + 4;
         ta.help_entries = fc->help_entries;
         ta.flat_cap = fc->cap;
+        ta.claim_ahead = trace_claim_ahead() ? 1u : 0u;
         a.flat_best = fc->flat_best;
         a.zero_word = count_next;   // cleared by the shade pass, filled by this step's scatter
         if (fc->enrol_next)
@@ -3816,7 +3876,11 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
         CHR_HIP_CHECK(hipEventRecord(ev1, stream));
         CHR_HIP_CHECK(hipStreamWaitEvent(ts, ev1, 0));
         if (sc->evt_tail0) CHR_HIP_CHECK(hipEventRecord(sc->evt_tail0, ts));
-        hipLaunchKernelGGL(clear_masks_kernel, dim3(std::min<uint32_t>(1024u, grid_for(nwords))), dim3(BLOCK), 0, ts,
+        // few workgroups (grid-stride): a tail holds < nthreads_per_block * 128 photons
+        // unless use_weights, and this launch waits for free CU slots beside the
+        // next batch's persistent walk grid -- a 1024-workgroup clear measured
+        // 125 us per slot (r03 rocprof), every slot's on the tail's stream
+        hipLaunchKernelGGL(clear_masks_kernel, dim3(std::min<uint32_t>(kClearBlocks, grid_for(nwords))), dim3(BLOCK), 0, ts,
                            sc->tail_masks, dev_n, mode);
         PropagateArgs at = a;
         at.prio = (tail_prio() ? 1u : 0u) | (tail_gs64() ? 2u : 0u);
@@ -3834,7 +3898,7 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
         return CHR_OK;
     }
     if (tail) {   // group / wave-adaptive walk, alive bits OR-ed into zeroed words
-        if (sc) hipLaunchKernelGGL(clear_masks_kernel, dim3(std::min<uint32_t>(1024u, grid_for(nwords))), dim3(BLOCK), 0,
+        if (sc) hipLaunchKernelGGL(clear_masks_kernel, dim3(std::min<uint32_t>(kClearBlocks, grid_for(nwords))), dim3(BLOCK), 0,
                                    stream, masks, dev_n, mode);
         else CHR_HIP_CHECK(hipMemsetAsync(masks, 0, (size_t)nwords * 8, stream));
         a.max_steps = sc ? sc->remaining : max_steps;
