@@ -3727,11 +3727,15 @@ struct SlotCtl {
     // (head, flat-walk classification, binning, the BVH walk: no random numbers)
     // on the prefix stream, ending with prefix_done; PHASE_REST (shade pass on)
     // on the batch stream after prefix_done, starting with ev_rest0
+    // The prefix itself may be queued in two parts (PHASE_BIN: head, classification,
+    // binning; PHASE_TRACE: the walk), the binning early, while the previous batch
+    // still runs its one-step slots (the binning's sort otherwise waits behind the
+    // previous tail's first waves for CUs).  ev_bin_end: after the binning.
     int phase = 0;
     int ctx = 0;                      // buffer context (walk-stack column)
-    hipEvent_t prefix_done = nullptr, ev_rest0 = nullptr;
+    hipEvent_t prefix_done = nullptr, ev_rest0 = nullptr, ev_bin_end = nullptr;
 };
-constexpr int PHASE_ALL = 0, PHASE_PREFIX = 1, PHASE_REST = 2;
+constexpr int PHASE_ALL = 0, PHASE_PREFIX = 1, PHASE_REST = 2, PHASE_BIN = 3, PHASE_TRACE = 4;
 
 // hits: n (triangle, distance) slots + a ray counter word, for the split path
 static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *rng, uint32_t nslots, uint32_t cap,
@@ -3772,19 +3776,21 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
     // the first step's length and mode are known on the host (binning, flat-walk enrolment)
     const bool first_one_step = first_step && (!sc || !((n < sc->tail_below || use_weights) && sc->remaining > 1));
     uint32_t *next = split ? (uint32_t *)(hits + (sc ? sc->n_layout : n)) : nullptr;
-    const bool pre = !sc || sc->phase != PHASE_REST, rest = !sc || sc->phase != PHASE_PREFIX;
-    if (sc && sc->phase != PHASE_ALL && (!split || !sc->prefix_done))
+    const int phase = sc ? sc->phase : PHASE_ALL;
+    const bool pre = phase != PHASE_REST, rest = phase == PHASE_ALL || phase == PHASE_REST;
+    const bool do_bin = pre && phase != PHASE_TRACE, do_trace = pre && phase != PHASE_BIN;
+    if (phase != PHASE_ALL && (!split || (phase != PHASE_BIN && !sc->prefix_done)))
         return chr::fail(CHR_ERR_INVALID, "launch_step: a split slot needs the split path and its prefix event");
-    if (ev0 && pre) CHR_HIP_CHECK(hipEventRecord(ev0, stream));
+    if (ev0 && do_bin) CHR_HIP_CHECK(hipEventRecord(ev0, stream));
     if (!pre) {
         CHR_HIP_CHECK(hipStreamWaitEvent(stream, sc->prefix_done, 0));
         if (sc->ev_rest0) CHR_HIP_CHECK(hipEventRecord(sc->ev_rest0, stream));
     }
-    if (sc && pre) {
+    if (sc && do_bin) {
         if (!next) return chr::fail(CHR_ERR_INVALID, "launch_step: device-driven steps need the split path");
         hipLaunchKernelGGL(step_head_kernel, dim3(1), dim3(64), 0, stream, in_queue - 1, out_queue, sc->mode, sc->nk,
                            sc->done, next, sc->tail_below, sc->remaining, use_weights, sc->n_layout);
-    } else if (split) {
+    } else if (split && !sc) {
         CHR_HIP_CHECK(hipMemsetAsync(next, 0, 4, stream));
     }
     if (split) {
@@ -3792,13 +3798,14 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
         // direction binning: 16-bit radix sort of (direction cell, queue position); hits region:
         // [hits n x int2][next + pad, 16 words][keys n][values n][walk hist 64 words]
         // (device-driven slots bin only the first step, whose length the host knows)
-        const bool bin_now = (sv.binned == 1 || (sv.binned == 2 && first_one_step && n >= kBinFirstMin)) &&
-                             (!sc || first_one_step) && pre;
+        const bool binned = (sv.binned == 1 || (sv.binned == 2 && first_one_step && n >= kBinFirstMin)) &&
+                            (!sc || first_one_step);
+        const bool bin_now = binned && do_bin;
         uint32_t *keys = next + 16, *order = keys + n;
         // ray records: the first step's from its classification, later steps' from
         // the previous step's scatter (enrol_next)
         const bool use_rays = fc->rays && trace_rays_enabled() && (first_one_step || fc->enrol_next);
-        if (first_one_step && pre)   // flat walks of the initial queue (later steps: enrolled by the previous scatter)
+        if (first_one_step && do_bin)   // flat walks of the initial queue (later steps: enrolled by the previous scatter)
             hipLaunchKernelGGL(classify_kernel, dim3(grid_for(n)), dim3(BLOCK), 0, stream, ph->d_pos, ph->d_dir,
                                ph->d_flags, ph->d_last_hit_triangles, in_queue, n, hits, fc->flat_q, count_cur,
                                fc->flat_best, bin_now ? keys : nullptr, bin_now ? order : nullptr,
@@ -3823,35 +3830,40 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
         if (fc->enrol_next)
             fe = FlatEnrol{ph->d_pos, ph->d_dir, hits, fc->flat_q, count_next, fc->flat_best,
                            (fc->rays && trace_rays_enabled()) ? fc->rays : nullptr, ph->d_last_hit_triangles};
-        if (trace_steps() && pre) {   // debugging: per-walk cost histogram (counting variants), printed per step
+        if (trace_steps() && do_trace) {   // debugging: per-walk cost histogram (counting variants), printed per step
             ta.walk_hist = next + 16 + 2 * (size_t)(sc ? sc->n_layout : n);
             CHR_HIP_CHECK(hipMemsetAsync(ta.walk_hist, 0, 34 * 4, stream));
         }
-        if (bin_now) {
-            {
+        if (binned) {
+            uint32_t *keys_out = sort_space, *vals_out = keys_out + n;
+            if (bin_now) {
                 if (!first_one_step)   // the first step's keys came with its classification
                     hipLaunchKernelGGL(bin_key_kernel, dim3(grid_for(n)), dim3(BLOCK), 0, stream, ph->d_dir, in_queue,
                                        n, keys, order);
-                uint32_t *keys_out = sort_space, *vals_out = keys_out + n;
                 void *temp = (void *)(((uintptr_t)(vals_out + n) + 255) & ~(uintptr_t)255);
                 size_t temp_bytes = sort_temp_bytes16(n);
                 CHR_HIP_CHECK(rocprim::radix_sort_pairs(temp, temp_bytes, keys, keys_out, order, vals_out, n, 0, 16,
                                                         stream));
-                ta.order = vals_out;
-                if (use_rays) {   // the records in the binned walk order
+                if (use_rays)   // the records in the binned walk order
                     hipLaunchKernelGGL(permute_rays_kernel, dim3(grid_for(n)), dim3(BLOCK), 0, stream, fc->rays,
                                        vals_out, n, fc->rays_walk);
-                    ta.rays = fc->rays_walk;
-                }
             }
+            ta.order = vals_out;
+            if (use_rays) ta.rays = fc->rays_walk;
         }
-        if (pre) {
+        if (do_bin && sc && sc->ev_bin_end) CHR_HIP_CHECK(hipEventRecord(sc->ev_bin_end, stream));
+        if (phase == PHASE_BIN) {
+            CHR_HIP_CHECK(hipGetLastError());
+            return CHR_OK;
+        }
+        if (do_trace) {
             const int cus = device_cus();
             if (cus <= 0) return chr::fail(CHR_ERR_HIP, "launch_step: no compute units");
             uint64_t resident = (uint64_t)cus * 4 * sv.trace_waves * 64 / BLOCK;   // persistent grid
             // a batch's prefix walk (chr_propagate_batches) runs beside the previous
             // batch's kernels: CHR_PREFIX_GRID=1/k of the grid leaves them CUs (A/B)
-            if (sc && sc->phase == PHASE_PREFIX) resident = std::max<uint64_t>(1, resident / prefix_grid_div());
+            if (phase == PHASE_PREFIX || phase == PHASE_TRACE)
+                resident = std::max<uint64_t>(1, resident / prefix_grid_div());
             const uint32_t blocks = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(resident, grid_for(n)));
             if (int rc = walk_stack_get((size_t)WIDE_STACK * blocks * BLOCK * sizeof(uint2), &ta.spill, sc ? sc->ctx : 0))
                 return rc;
@@ -4010,7 +4022,7 @@ static int slot_ctl_get(size_t words, uint32_t **out, int ctx = 0) {
 // [2,3] around trace_kernel, [4] slot done (ring copied), [5,6] around the tail
 // kernel when it runs on the tail stream, [7] start of the rest of a slot whose
 // prefix ran on the prefix stream (chr_propagate_batches)
-constexpr int SLOT_EVENTS = 8;
+constexpr int SLOT_EVENTS = 9;   // [8]: end of a split prefix's binning part
 
 // Device buffers of one propagate (context ctx of the calling thread):
 // queues, step scratch, the split path's hits / binning region, the flat-walk
@@ -4171,11 +4183,12 @@ static int slot_stats(chr_propagate_stats &st, const uint32_t *h, int k, const s
         const uint32_t m = h[2 * j], nj = h[2 * j + 1];
         const hipEvent_t *ev = events.data() + SLOT_EVENTS * (size_t)j;
         float ms = 0.0f;
-        if (j == 0 && prefixed) {   // the prefix on its stream, the rest after it on the batch stream
-            float ms2 = 0.0f;
-            CHR_HIP_CHECK(hipEventElapsedTime(&ms, ev[0], ev[3]));
-            CHR_HIP_CHECK(hipEventElapsedTime(&ms2, ev[7], ev[1]));
-            ms += ms2;
+        if (j == 0 && prefixed) {   // the prefix on its stream (binning, walk), the rest after it on the batch stream
+            float ms2 = 0.0f, ms3 = 0.0f;
+            CHR_HIP_CHECK(hipEventElapsedTime(&ms, ev[0], ev[8]));
+            CHR_HIP_CHECK(hipEventElapsedTime(&ms2, ev[2], ev[3]));
+            CHR_HIP_CHECK(hipEventElapsedTime(&ms3, ev[7], ev[1]));
+            ms += ms2 + ms3;
         } else {
             CHR_HIP_CHECK(hipEventElapsedTime(&ms, ev[0], ev[1]));
         }
@@ -4495,6 +4508,13 @@ static size_t batch_lookahead() {
     return (size_t)(k < 0 ? 0 : (k > NCTX - 1 ? NCTX - 1 : k));
 }
 
+// CHR_BATCH_EARLY_BIN=0: a batch's binning part is queued with its walk (at the
+// previous batch's tail) instead of right after the previous batch's walk (A/B)
+static bool batch_early_bin() {
+    const char *e = getenv("CHR_BATCH_EARLY_BIN");
+    return !(e && e[0] == '0');
+}
+
 // CHR_BATCH_PREFIX_BELOW=n: queue the next batch's prefix once a step of the
 // running batch leaves fewer than n survivors (n = nthreads_per_block * 128:
 // as soon as the next slot is known to be the tail); 0 (default): when the
@@ -4505,23 +4525,25 @@ static uint32_t batch_prefix_below() {
 }
 
 // The RNG-free part of a propagate's first slot on stream ps: queues, counters,
-// the head kernel, flat-walk classification, direction binning and the BVH
-// walk (launch_step PHASE_PREFIX), ending with prefix_done.
+// the head kernel, flat-walk classification, direction binning (part 1) and the
+// BVH walk (part 2) -- launch_step PHASE_BIN / PHASE_TRACE, or both at once
+// (PHASE_PREFIX) -- ending with prefix_done.
 static int queue_prefix(const chr_geometry *g, const chr_photons *ph, uint32_t nphotons, uint32_t true_nphotons,
                         uint32_t ncopies, uint32_t *rng, uint32_t nslots, int32_t ntpb, int32_t max_steps,
                         int32_t use_weights, int32_t scatter_first, PropBufs &b, int ctx,
-                        std::vector<hipEvent_t> &events, hipEvent_t prefix_done, hipStream_t ps) {
+                        std::vector<hipEvent_t> &events, hipEvent_t prefix_done, hipStream_t ps, int parts = 3) {
     uint32_t *ctl = nullptr;
     CHR_TRY(slot_ctl_get(2 * (size_t)max_steps + 8, &ctl, ctx));
     uint32_t *done = ctl + 2 * (size_t)max_steps;
-    CHR_TRY(prop_start(b, nphotons, true_nphotons, ncopies, ps, done));
+    if (parts & 1) CHR_TRY(prop_start(b, nphotons, true_nphotons, ncopies, ps, done));
     b.fc.enrol_next = true;
     CHR_TRY(grow_events(events, SLOT_EVENTS));
     SlotCtl sc{ctl, ctl + 1, done, nphotons, max_steps, (uint32_t)ntpb * 16 * 8};
-    sc.phase = PHASE_PREFIX;
+    sc.phase = parts == 1 ? PHASE_BIN : (parts == 2 ? PHASE_TRACE : PHASE_PREFIX);
     sc.ctx = ctx;
     sc.prefix_done = prefix_done;
     hipEvent_t *ev = events.data();
+    sc.ev_bin_end = ev[8];
     return launch_step(g, ph, rng, nslots, (uint32_t)b.cap, nphotons, b.q[0] + 1, b.q[1], 1, use_weights,
                        scatter_first, b.scratch, ps, ev[0], ev[1], b.hits, b.sort_space, true, ev[2], ev[3], nullptr,
                        &b.fc, &sc);
@@ -4592,30 +4614,48 @@ static int propagate_batches(const chr_geometry *g, const chr_photons *phs, cons
             if (photons_alias(phs + idx[j], nphotons[idx[j]], phs + idx[e], nphotons[idx[e]])) return true;
         return false;
     };
-    size_t queued = 0;   // batches whose prefix is queued
+    // prefixes: qbin batches have their binning part queued, qtrace their walk too
+    size_t qbin = 0, qtrace = 0;
     const size_t lookahead = batch_lookahead();
     const uint32_t prefix_below = batch_prefix_below();
-    auto prefix = [&](size_t j) -> int {
+    const bool early_bin = batch_early_bin();
+    // parts: 1 binning, 2 walk, 3 both (queue_prefix)
+    auto prefix = [&](size_t j, int parts) -> int {
         const uint32_t i = idx[j];
         const int c = (int)(j % NCTX);
-        if (j >= (size_t)NCTX) CHR_HIP_CHECK(hipStreamWaitEvent(ps, bh[j - NCTX].done, 0));   // the context is free
-        for (size_t e = j >= (size_t)NCTX ? j - NCTX + 1 : 0; e < j; ++e)   // shared photon arrays: after that batch
-            if (photons_alias(phs + i, nphotons[i], phs + idx[e], nphotons[idx[e]]))
-                CHR_HIP_CHECK(hipStreamWaitEvent(ps, bh[e].done, 0));
-        CHR_TRY(prop_bufs(nphotons[i], ntpb, max_blocks, c, true, bufs[c]));
-        bufs[c].pinned = bh[j].pinned;
+        if (parts & 1) {
+            if (j >= (size_t)NCTX) CHR_HIP_CHECK(hipStreamWaitEvent(ps, bh[j - NCTX].done, 0));   // the context is free
+            for (size_t e = j >= (size_t)NCTX ? j - NCTX + 1 : 0; e < j; ++e)   // shared photon arrays: after that batch
+                if (photons_alias(phs + i, nphotons[i], phs + idx[e], nphotons[idx[e]]))
+                    CHR_HIP_CHECK(hipStreamWaitEvent(ps, bh[e].done, 0));
+            CHR_TRY(prop_bufs(nphotons[i], ntpb, max_blocks, c, true, bufs[c]));
+            bufs[c].pinned = bh[j].pinned;
+        }
         return queue_prefix(g, phs + i, nphotons[i], true_nphotons[i], ncopies[i], d_rng_states, rng_nslots, ntpb,
-                            max_steps, use_weights, scatter_first, bufs[c], c, bh[j].ev, bh[j].prefix_done, ps);
+                            max_steps, use_weights, scatter_first, bufs[c], c, bh[j].ev, bh[j].prefix_done, ps, parts);
+    };
+    auto queue_walk = [&](size_t j) -> int {   // batch j's walk (and its binning, unless queued early)
+        const int parts = qbin > j ? 2 : 3;
+        CHR_TRY(prefix(j, parts));
+        if (parts == 3) qbin = j + 1;
+        qtrace = j + 1;
+        return CHR_OK;
     };
     std::vector<int> slots(nb, 0);
     for (size_t j = 0; j < nb; ++j) {
         // queue the prefixes of the batches ahead (as many as there are free
         // contexts); one sharing photon arrays with a batch not yet queued in
         // full waits until that batch's done event exists
-        while (queued < nb && queued < j + 1 + lookahead) {
-            if (queued > j && aliases_earlier(queued, j)) break;
-            CHR_TRY(prefix(queued));
-            queued++;
+        while (qtrace < nb && qtrace < j + 1 + lookahead) {
+            if (qtrace > j && aliases_earlier(qtrace, j)) break;
+            CHR_TRY(queue_walk(qtrace));
+        }
+        // the next batch's binning now: on the prefix stream behind this batch's
+        // walk, so it runs beside this batch's one-step slots instead of behind
+        // this batch's tail (CHR_BATCH_EARLY_BIN=0: with its walk, as in r02)
+        if (early_bin && qbin == j + 1 && qtrace == j + 1 && qbin < nb && !aliases_earlier(qbin, j)) {
+            CHR_TRY(prefix(qbin, 1));
+            qbin++;
         }
         const uint32_t i = idx[j];
         const int c = (int)(j % NCTX);
@@ -4628,13 +4668,10 @@ static int propagate_batches(const chr_geometry *g, const chr_photons *phs, cons
         run.ctx = c;
         // the next batch's prefix as soon as this batch is down to its late,
         // under-occupied steps (CHR_BATCH_PREFIX_BELOW photons; 0: at the next batch's start)
-        if (prefix_below && queued == j + 1 && queued < nb && !aliases_earlier(queued, j)) {
+        if (prefix_below && qtrace == j + 1 && qtrace < nb && !aliases_earlier(qtrace, j)) {
             run.out_ring = bh[j].pinned + 128 + 2 * (size_t)max_steps + 8;
             run.on_length = [&, j](uint32_t n) -> int {
-                if (queued == j + 1 && queued < nb && n < prefix_below) {
-                    CHR_TRY(prefix(queued));
-                    queued++;
-                }
+                if (qtrace == j + 1 && qtrace < nb && n < prefix_below) CHR_TRY(queue_walk(qtrace));
                 return CHR_OK;
             };
         }
