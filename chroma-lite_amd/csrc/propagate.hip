@@ -1993,27 +1993,39 @@ __device__ __forceinline__ int walk_segment(const DevGeom &g, bool act, V3 o, V3
         const bool refill = em != 0 && sp > 0;
         while (em != 0 && sp > 0) {
             const int W = sp < 8 ? sp : 8;
-            uint32_t et = 0;
+            uint32_t en = 0, et = 0;
             bool ok = false;
             if (L < (uint32_t)W) {
+                en = stk[2 * (sp - 1 - (int)L)];
                 et = stk[2 * (sp - 1 - (int)L) + 1];
                 ok = !(__uint_as_float(et) > best);           // mesh.h:94-96
             }
-            const unsigned long long vm = (__ballot(ok) & segmask) >> seg0;
-            const int need = __popcll(em), nv = __popcll(vm);
+            const unsigned long long okm = __ballot(ok) & segmask;
+            const int need = __popcll(em), nv = __popcll(okm);
             const int take = need < nv ? need : nv;
-            const int consumed = take == nv ? W : nth_bit(vm, take);   // entries above the first kept one
-            if (k == 0u && cur == INVALID) {
-                const int rnk = __popcll(em & below);
-                if (rnk < take) {
-                    const int src = nth_bit(vm, rnk);
-                    cur = stk[2 * (sp - 1 - src)];
-                    cur_t = __uint_as_float(stk[2 * (sp - 1 - src) + 1]);
-                }
+            // window lane L's rank among the unculled entries (from the top); the
+            // first unculled entry not taken bounds what is consumed (all above it)
+            const int rho = __popcll(okm & below);
+            const unsigned long long stopm = __ballot(ok && rho == take) & segmask;
+            const int consumed = stopm ? (__ffsll((long long)stopm) - 1 - (int)seg0) : W;
+            // the r-th empty cursor takes the r-th unculled entry, through the
+            // segment's free triangle-list buffer (written two iterations ago,
+            // tested one ago): no per-lane bit searches
+            if (ok && rho < take) {
+                tlist[(pb ^ 1) * TAIL_TRI + 2 * rho] = en;
+                tlist[(pb ^ 1) * TAIL_TRI + 2 * rho + 1] = et;
             }
+            __builtin_amdgcn_wave_barrier();
+            const bool empty = k == 0u && cur == INVALID;
+            const int rnk = __popcll(em & below);
+            const unsigned long long taken = __ballot(empty && rnk < take) & segmask;
+            if (empty && rnk < take) {
+                cur = tlist[(pb ^ 1) * TAIL_TRI + 2 * rnk];
+                cur_t = __uint_as_float(tlist[(pb ^ 1) * TAIL_TRI + 2 * rnk + 1]);
+            }
+            __builtin_amdgcn_wave_barrier();
             sp -= consumed;
-            for (int i = 0; i < take; ++i) em &= em - 1;
-            if (take == 0 && consumed == 0) break;
+            em &= ~taken;
         }
         if (refill) {   // the sub-group's cursor, from its leader lane
             cur = (uint32_t)__shfl((int)cur, (int)(lane & ~7u));
@@ -2091,7 +2103,11 @@ __device__ __forceinline__ int walk_segment(const DevGeom &g, bool act, V3 o, V3
                                  b2 = __ballot(cnt & 4u) & segmask;
         const uint32_t pre = __popcll(b0 & below) + 2u * __popcll(b1 & below) + 4u * __popcll(b2 & below);
         const uint32_t Tn = __popcll(b0) + 2u * __popcll(b1) + 4u * __popcll(b2);
-        for (uint32_t t = 0; t < cnt; ++t) tlist[(pb ^ 1) * TAIL_TRI + pre + t] = first + t;
+        // (a leaf holds at most 4 triangles)
+        if (cnt > 0u) tlist[(pb ^ 1) * TAIL_TRI + pre] = first;
+        if (cnt > 1u) tlist[(pb ^ 1) * TAIL_TRI + pre + 1] = first + 1u;
+        if (cnt > 2u) tlist[(pb ^ 1) * TAIL_TRI + pre + 2] = first + 2u;
+        if (cnt > 3u) tlist[(pb ^ 1) * TAIL_TRI + pre + 3] = first + 3u;
         // test the previous iteration's triangles (entries beyond the segment's
         // lanes, rare, are fetched now)
         float lbest = best;
