@@ -3542,11 +3542,13 @@ static uint32_t trace_help_after() {
     const int k = e ? atoi(e) : 0;
     return (uint32_t)(k < 0 ? 0 : k);
 }
-// CHR_TRACE_AHEAD=0: trace_kernel claims rays per refill with a blocking
-// atomic (r02 scheme) instead of from chunks claimed ahead (A/B)
+// CHR_TRACE_AHEAD=1: trace_kernel takes rays from chunks of the ray counter
+// claimed ahead (the next chunk's atomic in flight while the wave walks) instead
+// of one blocking atomic per refill.  Off: measured slower (r03 ab5: trace 17.63
+// -> 18.36 ms per step; the binned first launch 5.33 -> 5.60 ms).
 static bool trace_claim_ahead() {
     const char *e = getenv("CHR_TRACE_AHEAD");
-    return !(e && e[0] == '0');
+    return e && e[0] == '1';
 }
 // CHR_PREFIX_GRID=k: the prefix walk's persistent grid is 1/k of the full one (default 1; A/B)
 static uint32_t prefix_grid_div() {
@@ -4524,11 +4526,13 @@ static size_t batch_lookahead() {
     return (size_t)(k < 0 ? 0 : (k > NCTX - 1 ? NCTX - 1 : k));
 }
 
-// CHR_BATCH_EARLY_BIN=0: a batch's binning part is queued with its walk (at the
-// previous batch's tail) instead of right after the previous batch's walk (A/B)
+// CHR_BATCH_EARLY_BIN=1: a batch's binning part is queued right after the
+// previous batch's walk instead of with its own walk at the previous batch's
+// tail.  Off: measured slower (r03 ab5: 425.1 -> 412.0 M/s; the walk then starts
+// with the tail and slows its first, chip-wide phase: mean tail 6.53 -> 9.99 ms).
 static bool batch_early_bin() {
     const char *e = getenv("CHR_BATCH_EARLY_BIN");
-    return !(e && e[0] == '0');
+    return e && e[0] == '1';
 }
 
 // CHR_BATCH_PREFIX_BELOW=n: queue the next batch's prefix once a step of the
@@ -4666,9 +4670,9 @@ static int propagate_batches(const chr_geometry *g, const chr_photons *phs, cons
             if (qtrace > j && aliases_earlier(qtrace, j)) break;
             CHR_TRY(queue_walk(qtrace));
         }
-        // the next batch's binning now: on the prefix stream behind this batch's
-        // walk, so it runs beside this batch's one-step slots instead of behind
-        // this batch's tail (CHR_BATCH_EARLY_BIN=0: with its walk, as in r02)
+        // CHR_BATCH_EARLY_BIN=1: the next batch's binning now, on the prefix stream
+        // behind this batch's walk (beside this batch's one-step slots); default:
+        // with its walk, at this batch's tail
         if (early_bin && qbin == j + 1 && qtrace == j + 1 && qbin < nb && !aliases_earlier(qbin, j)) {
             CHR_TRY(prefix(qbin, 1));
             qbin++;
