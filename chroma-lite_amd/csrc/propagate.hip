@@ -2422,21 +2422,23 @@ struct TraceArgs {
     const uint32_t *mode;
     uint32_t drain_max;          // a wave drains its last <= drain_max walks whole-wave (0: never; at most 8)
     // Long-walk help (trace_help_after): once the ray counter is exhausted, a
-    // walk past help_after node + triangle steps is published (help_entries);
-    // waves left without rays walk published walks with the whole wave
-    // (walk_segment, 8 cursors) and join their results as flat walks do.
-    // help_ctl: [0] published, [1] claimed, [2] this launch's serial, [3] join
-    // slots taken (all reset by the step head kernel); a published walk joins
-    // flat-list slot flat_cap - 1 - k (enrolled flat walks fill the list from
-    // 0: a walk is one or the other, so they never meet); help_after 0: off.
-    // No fences: a published entry is HELP_DATA 64-bit words, each the launch
-    // serial above one data word (o, d, last hit, flat slot, seed key hi/lo),
-    // written with plain device-coherent atomic stores after the slot's seed
-    // exchange has completed; a helper takes an entry only when all its words
-    // carry this launch's serial (else its owner finishes the walk alone).
-    // Word HELP_DATA: the serial once a helper has joined its result.  (An
-    // agent-scope release/acquire would write back / invalidate the XCD's L2
-    // at every publish and poll: measured 16.0 -> 21.7 ms of trace per step.)
+    // lane whose walk passes help_after node + triangle steps publishes it
+    // (help_entries) and drops it; waves left without rays claim published walks
+    // one at a time and walk each with the whole wave (walk_segment, 8 cursors)
+    // from the root, seeded with the owner's best so far, then store the result
+    // in the walk's flat-list slot flat_cap - 1 - k (enrolled flat walks fill the
+    // list from 0: a walk is one or the other, so they never meet).  Every
+    // published walk is walked by exactly one wave: claims advance only below the
+    // published count (compare-and-swap), and a publisher claims what is left
+    // before it exits.  help_ctl: [0] published, [1] claimed, [2] this launch's
+    // serial (all reset by the step head kernel); help_after 0: off.
+    // No fences: an entry is HELP_DATA 64-bit words, each the launch serial above
+    // one data word (o, d, last hit, flat slot, seed key hi/lo), written with
+    // device-coherent relaxed atomic stores; a claimer reads it once every word
+    // carries this launch's serial (its publisher reserved the index and is
+    // writing it, nothing else).  (Agent-scope release/acquire would write back /
+    // invalidate the XCD's L2 at every publish: measured 16.0 -> 21.7 ms of trace
+    // per step in a first version.)
     uint32_t help_after;
     uint32_t flat_cap;
     uint32_t claim_ahead;        // refills from claimed chunks, the next claim in flight (trace_claim_ahead)
@@ -2564,17 +2566,15 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
     bool walk_done = true, drain = false;
     uint32_t qh = 0, qt = 0, pcur = 0, pleft = 0;
     constexpr uint32_t INVALID = 0xFFFFFFFFu;
-    // long-walk help (TraceArgs::help_after): this lane's walk was published as
-    // help entry hidx (its result then joins flat slot flat_f, like a sub-walk)
+    // long-walk help (TraceArgs::help_after)
     const bool help_on = !COUNT && a.help_after != 0u && a.help_ctl != nullptr;
     const uint32_t serial = help_on ? a.help_ctl[2] : 0u;
     // claimed ray-counter chunk (claim_ahead): next index cb, cn left; pend: the
     // next chunk's base, claimed ahead (valid in lane 0 once have_pend)
     uint32_t cb = 0, cn = 0, pend = 0;
     bool have_pend = false;
-    bool handed = false, helping = false;
-    uint32_t hidx = 0, wsteps = 0;
-    unsigned long long poll = 0;   // the handed walk's done word, read one iteration ahead of its use
+    bool helping = false;
+    uint32_t wsteps = 0;
     enum { P_NODE, P_TRI, P_REFILL, P_IDLE, P_DRAIN, P_BOX = 3 };   // regions (calls: P_REFILL = walks, P_BOX = boxes)
     Prof<5> pf;
     pf.start(P_REFILL);
@@ -2693,7 +2693,6 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
                     if (start) {
                         slab = make_slab(v3(-o.x / d.x, -o.y / d.y, -o.z / d.z), v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z));
                         best_id = -1;
-                        handed = false;
                         wsteps = 0;
                         sp = 0;
                         walk_done = false;
@@ -2706,41 +2705,25 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
             }
         }
         if constexpr (!COUNT) {
-            if (help_on && exhausted && has_ray && !walk_done) {
-                if (handed) {
-                    // a helper joined this walk's result into its slot: drop it
-                    if ((uint32_t)poll == serial) {
-                        has_ray = false;
-                        pleft = 0;
-                        qh = qt;
-                    } else {
-                        poll = __hip_atomic_load(a.help_entries + HELP_WORDS * hidx + HELP_DATA, __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT);
-                    }
-                } else if (flat_f < 0 && wsteps > a.help_after) {
-                    const uint32_t idx = atomicAdd(a.help_ctl, 1u);
-                    if (idx < HELP_CAP) {
-                        // join point: a flat-list slot seeded with this walk's best so far
-                        const uint32_t f = a.flat_cap - 1u - atomicAdd(a.help_ctl + 3, 1u);
-                        const unsigned long long seed =
-                            best_id == -1 ? ~0ull : (((unsigned long long)__float_as_uint(best) << 32) | best_rank);
-                        const unsigned long long prev = atomicExch(a.flat_best + f, seed);
-                        a.hits[q] = make_int2(FLAT_HIT, (int)f);
-                        // the entry only after the exchange has completed (its result is an
-                        // operand here): a helper's atomicMin can never precede the seed
-                        asm volatile("" ::"v"((uint32_t)prev), "v"((uint32_t)(prev >> 32)) : "memory");
-                        const uint32_t w[HELP_DATA] = {__float_as_uint(o.x), __float_as_uint(o.y), __float_as_uint(o.z),
-                                                       __float_as_uint(d.x), __float_as_uint(d.y), __float_as_uint(d.z),
-                                                       last, f, (uint32_t)(seed >> 32), (uint32_t)seed};
-                        unsigned long long *e = a.help_entries + HELP_WORDS * idx;
-                        for (uint32_t k = 0; k < HELP_DATA; ++k)
-                            __hip_atomic_store(e + k, ((unsigned long long)serial << 32) | w[k], __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_AGENT);
-                        flat_f = (int)f;
-                        handed = true;
-                        hidx = idx;
-                        poll = 0;
-                    }
+            if (help_on && exhausted && has_ray && !walk_done && flat_f < 0 && wsteps > a.help_after) {
+                const uint32_t idx = atomicAdd(a.help_ctl, 1u);
+                if (idx < HELP_CAP) {
+                    // publish and drop: the claimer walks it again from the root, seeded
+                    // with this walk's best so far, and stores the result in slot f
+                    const uint32_t f = a.flat_cap - 1u - idx;
+                    const unsigned long long seed =
+                        best_id == -1 ? ~0ull : (((unsigned long long)__float_as_uint(best) << 32) | best_rank);
+                    a.hits[q] = make_int2(FLAT_HIT, (int)f);
+                    const uint32_t w[HELP_DATA] = {__float_as_uint(o.x), __float_as_uint(o.y), __float_as_uint(o.z),
+                                                   __float_as_uint(d.x), __float_as_uint(d.y), __float_as_uint(d.z),
+                                                   last, f, (uint32_t)(seed >> 32), (uint32_t)seed};
+                    unsigned long long *e = a.help_entries + HELP_WORDS * idx;
+                    for (uint32_t k = 0; k < HELP_DATA; ++k)
+                        __hip_atomic_store(e + k, ((unsigned long long)serial << 32) | w[k], __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+                    has_ray = false;
+                    pleft = 0;
+                    qh = qt;
                 }
             }
             // Drain: once the ray counter is exhausted and at most 8 ordinary walks
@@ -2753,7 +2736,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
             // best so far (conservative culling, the same nearest hit); the
             // lanes' stacks are abandoned and their LDS rows reused.
             if (exhausted && __ballot(has_ray) != 0 && (uint32_t)__popcll(__ballot(has_ray)) <= a.drain_max &&
-                __ballot(has_ray && flat_f >= 0 && !handed) == 0) {   // no cut-item sub-walks (they start mid-tree)
+                __ballot(has_ray && flat_f >= 0) == 0) {   // no cut-item sub-walks (they start mid-tree)
                 drain = true;   // after the loop, where the walk state below is no longer live
                 break;
             }
@@ -2864,50 +2847,59 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
             const int seg0 = (int)lane & ~(Gs - 1);
             CHR_LDS uint32_t *wbase = (CHR_LDS uint32_t *)(lds + (threadIdx.x & ~63u));
             float sdist;
-            uint32_t sit, srank_out = 0;
+            uint32_t sit;
             const int tri = walk_segment<0>(g, act, so, sdir, slast, Gs, LdsRows{wbase, seg0 / 8 * TAIL_STACK * 2},
                                          TAIL_STACK * Gs / 8, LdsRows{wbase, 8 * TAIL_STACK * 2 + 4 * seg0}, overflow,
-                                         sdist, sit, sbest, srank, sid, &srank_out);
+                                         sdist, sit, sbest, srank, sid);
             const int mine = (__popcll(rm & ((1ull << lane) - 1ull)) * Gs) & 63;   // my segment's first lane
             const int rt = __shfl(tri, mine);
             const float rd = __shfl(sdist, mine);
-            const uint32_t rr = (uint32_t)__shfl((int)srank_out, mine);
             if (has_ray) {                                        // publish (mesh.h:123-125)
-                if (handed) {   // a published walk: its result joins the flat slot
-                    if (rt != -1)
-                        atomicMin(a.flat_best + flat_f, ((unsigned long long)__float_as_uint(rd) << 32) | rr);
-                } else {
-                    a.hits[q] = make_int2(rt, __float_as_int(rt == -1 ? -1.0f : rd));
-                }
+                a.hits[q] = make_int2(rt, __float_as_int(rt == -1 ? -1.0f : rd));
                 pf.call(P_DRAIN);
             }
             pf.tick(P_IDLE);
             helping = help_on;   // then help the other waves' long walks
         }
         if (helping) {
-            // Help: walk published long walks with the whole wave (8 cursors),
-            // one claim at a time until none is left; each claim is a fresh index,
-            // so the loop ends.  A claimed entry not yet visible is left to its owner.
+            // Help: claim published walks while any is unclaimed, walk each with the
+            // whole wave.  Claims: compare-and-swap below the published count, so
+            // every published walk is claimed exactly once (a wave that exits has
+            // seen all published walks claimed; the rest are published later, by
+            // waves that will claim them themselves).
             pf.tick(P_DRAIN);
             CHR_LDS uint32_t *wbase = (CHR_LDS uint32_t *)(lds + (threadIdx.x & ~63u));
             while (true) {
-                uint32_t i = 0;
-                if (lane == 0) i = atomicAdd(a.help_ctl + 1, 1u);
-                i = (uint32_t)__shfl((int)i, 0);
-                const uint32_t pub = __hip_atomic_load(a.help_ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (i >= pub || i >= HELP_CAP) break;
-                unsigned long long *e = a.help_entries + HELP_WORDS * i;
-                // lane k reads data word k; the entry is whole when every word carries the serial
+                uint32_t c = 0xFFFFFFFFu;
+                if (lane == 0) {
+                    uint32_t cl = __hip_atomic_load(a.help_ctl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    while (true) {
+                        uint32_t pub = __hip_atomic_load(a.help_ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        if (pub > HELP_CAP) pub = HELP_CAP;
+                        if (cl >= pub) break;
+                        const uint32_t prev = atomicCAS(a.help_ctl + 1, cl, cl + 1u);
+                        if (prev == cl) { c = cl; break; }
+                        cl = prev;
+                    }
+                }
+                c = (uint32_t)__shfl((int)c, 0);
+                if (c == 0xFFFFFFFFu) break;
+                unsigned long long *e = a.help_entries + HELP_WORDS * c;
+                // lane k reads data word k until all carry the serial (the publisher has
+                // reserved c and is storing it; bounded, counted if it ever runs out)
                 unsigned long long wk = 0;
-                if (lane < HELP_DATA) wk = __hip_atomic_load(e + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                const unsigned long long okm = __ballot(lane < HELP_DATA && (uint32_t)(wk >> 32) == serial);
-                if (okm != (1ull << HELP_DATA) - 1ull) continue;
+                bool whole = false;
+                for (uint32_t tries = 0; tries < (1u << 20) && !whole; ++tries) {
+                    if (lane < HELP_DATA) wk = __hip_atomic_load(e + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    whole = __ballot(lane < HELP_DATA && (uint32_t)(wk >> 32) == serial) == (1ull << HELP_DATA) - 1ull;
+                    if (!whole) __builtin_amdgcn_s_sleep(2);
+                }
+                if (!whole) { if (lane == 0) overflow++; continue; }
                 const uint32_t lo = (uint32_t)wk;
                 auto word = [&](int k) { return (uint32_t)__shfl((int)lo, k); };
                 const V3 ho = v3(__uint_as_float(word(0)), __uint_as_float(word(1)), __uint_as_float(word(2)));
                 const V3 hd = v3(__uint_as_float(word(3)), __uint_as_float(word(4)), __uint_as_float(word(5)));
                 const uint32_t hlast = word(6), hf = word(7);
-                if (hf >= a.flat_cap) continue;   // (defensive)
                 const unsigned long long seed = ((unsigned long long)word(8) << 32) | word(9);
                 const float sb = seed == ~0ull ? __builtin_inff() : __uint_as_float((uint32_t)(seed >> 32));
                 const uint32_t sr = seed == ~0ull ? 0xFFFFFFFFu : (uint32_t)seed;
@@ -2916,12 +2908,10 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
                 const int ht = walk_segment<64>(g, true, ho, hd, hlast, 64, LdsRows{wbase, 0}, TAIL_STACK * 8,
                                                 LdsRows{wbase, 8 * TAIL_STACK * 2}, overflow, hdist, hit_iters, sb, sr,
                                                 -1, &hrank);
-                if (lane == 0) {
-                    if (ht != -1)
-                        atomicMin(a.flat_best + hf, ((unsigned long long)__float_as_uint(hdist) << 32) | hrank);
-                    __hip_atomic_store(e + HELP_DATA, (unsigned long long)serial, __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-                }
+                // the walk's one writer: min(seed, this walk) -- the walk never returns
+                // a key above its seed, so its own result is that minimum
+                if (lane == 0 && hf < a.flat_cap)
+                    a.flat_best[hf] = ht == -1 ? seed : (((unsigned long long)__float_as_uint(hdist) << 32) | hrank);
             }
             pf.tick(P_IDLE);
         }
