@@ -2433,12 +2433,15 @@ struct TraceArgs {
     // before it exits.  help_ctl: [0] published, [1] claimed, [2] this launch's
     // serial (all reset by the step head kernel); help_after 0: off.
     // No fences: an entry is HELP_DATA 64-bit words, each the launch serial above
-    // one data word (o, d, last hit, flat slot, seed key hi/lo), written with
-    // device-coherent relaxed atomic stores; a claimer reads it once every word
-    // carries this launch's serial (its publisher reserved the index and is
-    // writing it, nothing else).  (Agent-scope release/acquire would write back /
-    // invalidate the XCD's L2 at every publish: measured 16.0 -> 21.7 ms of trace
-    // per step in a first version.)
+    // one data word (o, d, last hit, flat slot, seed key hi/lo), every access a
+    // device-scope read-modify-write (atomicExch to write, atomicOr 0 to read,
+    // performed at the coherence point, as the flat walks' atomicMin across the
+    // grid); a claimer reads it once every word carries this launch's serial
+    // (its publisher reserved the index and is writing it, nothing else).  Plain
+    // or relaxed-atomic loads and stores are not enough across XCDs: a reader's
+    // L2 kept a stale copy of an entry line and spun on it (r03 ab6), and an
+    // agent-scope release/acquire writes back / invalidates the XCD's L2 at every
+    // publish (trace 16.0 -> 21.7 ms per step in a first version).
     uint32_t help_after;
     uint32_t flat_cap;
     uint32_t claim_ahead;        // refills from claimed chunks, the next claim in flight (trace_claim_ahead)
@@ -2718,9 +2721,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
                                                    __float_as_uint(d.x), __float_as_uint(d.y), __float_as_uint(d.z),
                                                    last, f, (uint32_t)(seed >> 32), (uint32_t)seed};
                     unsigned long long *e = a.help_entries + HELP_WORDS * idx;
-                    for (uint32_t k = 0; k < HELP_DATA; ++k)
-                        __hip_atomic_store(e + k, ((unsigned long long)serial << 32) | w[k], __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT);
+                    for (uint32_t k = 0; k < HELP_DATA; ++k) atomicExch(e + k, ((unsigned long long)serial << 32) | w[k]);
                     has_ray = false;
                     pleft = 0;
                     qh = qt;
@@ -2872,9 +2873,9 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
             while (true) {
                 uint32_t c = 0xFFFFFFFFu;
                 if (lane == 0) {
-                    uint32_t cl = __hip_atomic_load(a.help_ctl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    uint32_t cl = atomicAdd(a.help_ctl + 1, 0u);
                     while (true) {
-                        uint32_t pub = __hip_atomic_load(a.help_ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        uint32_t pub = atomicAdd(a.help_ctl, 0u);
                         if (pub > HELP_CAP) pub = HELP_CAP;
                         if (cl >= pub) break;
                         const uint32_t prev = atomicCAS(a.help_ctl + 1, cl, cl + 1u);
@@ -2890,7 +2891,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
                 unsigned long long wk = 0;
                 bool whole = false;
                 for (uint32_t tries = 0; tries < (1u << 20) && !whole; ++tries) {
-                    if (lane < HELP_DATA) wk = __hip_atomic_load(e + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (lane < HELP_DATA) wk = atomicOr(e + lane, 0ull);
                     whole = __ballot(lane < HELP_DATA && (uint32_t)(wk >> 32) == serial) == (1ull << HELP_DATA) - 1ull;
                     if (!whole) __builtin_amdgcn_s_sleep(2);
                 }
@@ -2911,7 +2912,8 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
                 // the walk's one writer: min(seed, this walk) -- the walk never returns
                 // a key above its seed, so its own result is that minimum
                 if (lane == 0 && hf < a.flat_cap)
-                    a.flat_best[hf] = ht == -1 ? seed : (((unsigned long long)__float_as_uint(hdist) << 32) | hrank);
+                    atomicExch(a.flat_best + hf,
+                               ht == -1 ? seed : (((unsigned long long)__float_as_uint(hdist) << 32) | hrank));
             }
             pf.tick(P_IDLE);
         }

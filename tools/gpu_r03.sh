@@ -33,6 +33,16 @@ if [ "$MODE" = prof ]; then
     ( cd /tmp && export TMPDIR=/tmp && CHROMA_DEVICE_PROFILE=1 timeout -k 10 600 python3 "$R/bench.py" --steps 3 --warmup 1 \
         --no-cpu-baseline --no-count > "$O/devprof.json" 2> "$O/devprof.log" ) || { tail -5 "$O/devprof.log"; exit 1; }
 fi
+if [ "$MODE" = configs ]; then
+    # the other BASELINE configs on one GPU (C3 primary geometry, C2, C5), 3 timed / 1 warm-up as in r02
+    cd /tmp && export TMPDIR=/tmp
+    for spec in "demo 10000000" "tiny 1000000" "scint 10000000"; do
+        set -- $spec
+        timeout -k 10 900 python3 "$R/bench.py" --detector $1 --photons $2 --steps 3 --warmup 1 \
+            > "$O/bench_$1.json" 2> "$O/bench_$1.log" || { tail -20 "$O/bench_$1.log"; exit 1; }
+        cut -c1-200 "$O/bench_$1.json"
+    done
+fi
 if [ "$MODE" = bench ] || [ "$MODE" = all ] || [ "$MODE" = prof ]; then
     cd /tmp && export TMPDIR=/tmp
     timeout -k 10 900 python3 "$R/bench.py" --gpus 1 --steps 20 --warmup 5 > "$O/bench.json" 2> "$O/bench.log" || { tail -20 "$O/bench.log"; exit 1; }
