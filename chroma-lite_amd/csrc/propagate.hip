@@ -1948,8 +1948,7 @@ struct LdsRows {
 template <int GS, class M>
 __device__ __forceinline__ int walk_segment(const DevGeom &g, bool act, V3 o, V3 d, uint32_t last, int Gs_in, M stk, int cap, M tlist,
                             uint32_t &overflow, float &min_distance, uint32_t &iters,
-                            float best = __builtin_inff(), uint32_t best_rank = 0xFFFFFFFFu, int best_id = -1,
-                            uint32_t *rank_out = nullptr) {
+                            float best = __builtin_inff(), uint32_t best_rank = 0xFFFFFFFFu, int best_id = -1) {
     const int Gs = GS ? GS : Gs_in;
     constexpr uint32_t INVALID = 0xFFFFFFFFu;
     constexpr unsigned long long NONE = ~0ull;
@@ -2159,7 +2158,6 @@ __device__ __forceinline__ int walk_segment(const DevGeom &g, bool act, V3 o, V3
         if (cur != INVALID && cur_t > best) cur = INVALID;
     }
     min_distance = best_id == -1 ? -1.0f : best;
-    if (rank_out) *rank_out = best_rank;
     return best_id;
 }
 
@@ -2421,37 +2419,9 @@ struct TraceArgs {
     const uint32_t *dev_n;
     const uint32_t *mode;
     uint32_t drain_max;          // a wave drains its last <= drain_max walks whole-wave (0: never; at most 8)
-    // Long-walk help (trace_help_after): once the ray counter is exhausted, a
-    // lane whose walk passes help_after node + triangle steps publishes it
-    // (help_entries) and drops it; waves left without rays claim published walks
-    // one at a time and walk each with the whole wave (walk_segment, 8 cursors)
-    // from the root, seeded with the owner's best so far, then store the result
-    // in the walk's flat-list slot flat_cap - 1 - k (enrolled flat walks fill the
-    // list from 0: a walk is one or the other, so they never meet).  Every
-    // published walk is walked by exactly one wave: claims advance only below the
-    // published count (compare-and-swap), and a publisher claims what is left
-    // before it exits.  help_ctl: [0] published, [1] claimed, [2] this launch's
-    // serial (all reset by the step head kernel); help_after 0: off.
-    // No fences: an entry is HELP_DATA 64-bit words, each the launch serial above
-    // one data word (o, d, last hit, flat slot, seed key hi/lo), every access a
-    // device-scope read-modify-write (atomicExch to write, atomicOr 0 to read,
-    // performed at the coherence point, as the flat walks' atomicMin across the
-    // grid); a claimer reads it once every word carries this launch's serial
-    // (its publisher reserved the index and is writing it, nothing else).  Plain
-    // or relaxed-atomic loads and stores are not enough across XCDs: a reader's
-    // L2 kept a stale copy of an entry line and spun on it (r03 ab6), and an
-    // agent-scope release/acquire writes back / invalidates the XCD's L2 at every
-    // publish (trace 16.0 -> 21.7 ms per step in a first version).
-    uint32_t help_after;
-    uint32_t flat_cap;
     uint32_t claim_ahead;        // refills from claimed chunks, the next claim in flight (trace_claim_ahead)
-    uint32_t *help_ctl;
-    unsigned long long *help_entries;   // HELP_CAP x HELP_WORDS
 };
-constexpr uint32_t HELP_CAP = 8192;
 constexpr uint32_t CLAIM = 64;   // ray-counter chunk of trace_kernel's claim-ahead refill
-constexpr uint32_t HELP_DATA = 10;
-constexpr uint32_t HELP_WORDS = 12;
 
 // Enrol queue position p in the flat list of the next trace launch (its walk
 // is flat, walk_kind 2): f = slot in the flat list, hits[p] = (FLAT_HIT, f).
@@ -2569,15 +2539,10 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
     bool walk_done = true, drain = false;
     uint32_t qh = 0, qt = 0, pcur = 0, pleft = 0;
     constexpr uint32_t INVALID = 0xFFFFFFFFu;
-    // long-walk help (TraceArgs::help_after)
-    const bool help_on = !COUNT && a.help_after != 0u && a.help_ctl != nullptr;
-    const uint32_t serial = help_on ? a.help_ctl[2] : 0u;
     // claimed ray-counter chunk (claim_ahead): next index cb, cn left; pend: the
     // next chunk's base, claimed ahead (valid in lane 0 once have_pend)
     uint32_t cb = 0, cn = 0, pend = 0;
     bool have_pend = false;
-    bool helping = false;
-    uint32_t wsteps = 0;
     enum { P_NODE, P_TRI, P_REFILL, P_IDLE, P_DRAIN, P_BOX = 3 };   // regions (calls: P_REFILL = walks, P_BOX = boxes)
     Prof<5> pf;
     pf.start(P_REFILL);
@@ -2696,7 +2661,6 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
                     if (start) {
                         slab = make_slab(v3(-o.x / d.x, -o.y / d.y, -o.z / d.z), v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z));
                         best_id = -1;
-                        wsteps = 0;
                         sp = 0;
                         walk_done = false;
                         has_ray = true;
@@ -2708,25 +2672,6 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
             }
         }
         if constexpr (!COUNT) {
-            if (help_on && exhausted && has_ray && !walk_done && flat_f < 0 && wsteps > a.help_after) {
-                const uint32_t idx = atomicAdd(a.help_ctl, 1u);
-                if (idx < HELP_CAP) {
-                    // publish and drop: the claimer walks it again from the root, seeded
-                    // with this walk's best so far, and stores the result in slot f
-                    const uint32_t f = a.flat_cap - 1u - idx;
-                    const unsigned long long seed =
-                        best_id == -1 ? ~0ull : (((unsigned long long)__float_as_uint(best) << 32) | best_rank);
-                    a.hits[q] = make_int2(FLAT_HIT, (int)f);
-                    const uint32_t w[HELP_DATA] = {__float_as_uint(o.x), __float_as_uint(o.y), __float_as_uint(o.z),
-                                                   __float_as_uint(d.x), __float_as_uint(d.y), __float_as_uint(d.z),
-                                                   last, f, (uint32_t)(seed >> 32), (uint32_t)seed};
-                    unsigned long long *e = a.help_entries + HELP_WORDS * idx;
-                    for (uint32_t k = 0; k < HELP_DATA; ++k) atomicExch(e + k, ((unsigned long long)serial << 32) | w[k]);
-                    has_ray = false;
-                    pleft = 0;
-                    qh = qt;
-                }
-            }
             // Drain: once the ray counter is exhausted and at most 8 ordinary walks
             // are left in the wave, the whole wave finishes them together
             // (walk_segment: 8..64 lanes per walk, Gs/8 cursors each, a dependent
@@ -2749,9 +2694,6 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
         const unsigned long long mt = __ballot(has_work);
         if ((mw | mt) == 0) {
             if (exhausted && __ballot(has_ray) == 0) {
-                if constexpr (!COUNT) {
-                    if (help_on) helping = true;
-                }
                 break;
             }
             continue;                                    // walks ended: publish + refill
@@ -2771,7 +2713,6 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
                 if (!found) { walk_done = true; continue; }
             }
             if constexpr (COUNT) { cnt.nodes++; walk_cost++; if (wave_leader()) cnt.wave_nodes++; }
-            wsteps++;
             const uint4 *np = g.wnodes + (size_t)g.wstride * node;
             const uint4 h = gld(np), a1 = gld(np + 1), a2 = gld(np + 2), a3 = gld(np + 3), a4 = gld(np + 4),
                         a5 = gld(np + 5);
@@ -2806,7 +2747,6 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
                 pleft = (e >> 30) + 1u;
             }
             if constexpr (COUNT) { cnt.tris++; walk_cost++; if (wave_leader()) cnt.wave_tris++; }
-            wsteps++;
             const float4 *r = g.wtri + 4 * (size_t)pcur;
             const float4 r0 = gld(r), r1 = gld(r + 1), r2 = gld(r + 2);
             pcur++;
@@ -2858,62 +2798,6 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
             if (has_ray) {                                        // publish (mesh.h:123-125)
                 a.hits[q] = make_int2(rt, __float_as_int(rt == -1 ? -1.0f : rd));
                 pf.call(P_DRAIN);
-            }
-            pf.tick(P_IDLE);
-            helping = help_on;   // then help the other waves' long walks
-        }
-        if (helping) {
-            // Help: claim published walks while any is unclaimed, walk each with the
-            // whole wave.  Claims: compare-and-swap below the published count, so
-            // every published walk is claimed exactly once (a wave that exits has
-            // seen all published walks claimed; the rest are published later, by
-            // waves that will claim them themselves).
-            pf.tick(P_DRAIN);
-            CHR_LDS uint32_t *wbase = (CHR_LDS uint32_t *)(lds + (threadIdx.x & ~63u));
-            while (true) {
-                uint32_t c = 0xFFFFFFFFu;
-                if (lane == 0) {
-                    uint32_t cl = atomicAdd(a.help_ctl + 1, 0u);
-                    while (true) {
-                        uint32_t pub = atomicAdd(a.help_ctl, 0u);
-                        if (pub > HELP_CAP) pub = HELP_CAP;
-                        if (cl >= pub) break;
-                        const uint32_t prev = atomicCAS(a.help_ctl + 1, cl, cl + 1u);
-                        if (prev == cl) { c = cl; break; }
-                        cl = prev;
-                    }
-                }
-                c = (uint32_t)__shfl((int)c, 0);
-                if (c == 0xFFFFFFFFu) break;
-                unsigned long long *e = a.help_entries + HELP_WORDS * c;
-                // lane k reads data word k until all carry the serial (the publisher has
-                // reserved c and is storing it; bounded, counted if it ever runs out)
-                unsigned long long wk = 0;
-                bool whole = false;
-                for (uint32_t tries = 0; tries < (1u << 20) && !whole; ++tries) {
-                    if (lane < HELP_DATA) wk = atomicOr(e + lane, 0ull);
-                    whole = __ballot(lane < HELP_DATA && (uint32_t)(wk >> 32) == serial) == (1ull << HELP_DATA) - 1ull;
-                    if (!whole) __builtin_amdgcn_s_sleep(2);
-                }
-                if (!whole) { if (lane == 0) overflow++; continue; }
-                const uint32_t lo = (uint32_t)wk;
-                auto word = [&](int k) { return (uint32_t)__shfl((int)lo, k); };
-                const V3 ho = v3(__uint_as_float(word(0)), __uint_as_float(word(1)), __uint_as_float(word(2)));
-                const V3 hd = v3(__uint_as_float(word(3)), __uint_as_float(word(4)), __uint_as_float(word(5)));
-                const uint32_t hlast = word(6), hf = word(7);
-                const unsigned long long seed = ((unsigned long long)word(8) << 32) | word(9);
-                const float sb = seed == ~0ull ? __builtin_inff() : __uint_as_float((uint32_t)(seed >> 32));
-                const uint32_t sr = seed == ~0ull ? 0xFFFFFFFFu : (uint32_t)seed;
-                float hdist;
-                uint32_t hit_iters, hrank = 0;
-                const int ht = walk_segment<64>(g, true, ho, hd, hlast, 64, LdsRows{wbase, 0}, TAIL_STACK * 8,
-                                                LdsRows{wbase, 8 * TAIL_STACK * 2}, overflow, hdist, hit_iters, sb, sr,
-                                                -1, &hrank);
-                // the walk's one writer: min(seed, this walk) -- the walk never returns
-                // a key above its seed, so its own result is that minimum
-                if (lane == 0 && hf < a.flat_cap)
-                    atomicExch(a.flat_best + hf,
-                               ht == -1 ? seed : (((unsigned long long)__float_as_uint(hdist) << 32) | hrank));
             }
             pf.tick(P_IDLE);
         }
@@ -3110,11 +2994,6 @@ __global__ void step_head_kernel(const uint32_t *in_hdr, uint32_t *out_hdr, uint
     if (m != STEP_IDLE) {
         out_hdr[0] = 1u;
         ray_counter[0] = 0u;
-        // trace_kernel's long-walk help words (TraceArgs::help_ctl = ray_counter + 4)
-        ray_counter[4] = 0u;
-        ray_counter[5] = 0u;
-        ray_counter[6] = ray_counter[6] + 1u == 0u ? 1u : ray_counter[6] + 1u;   // never 0 (cleared entries)
-        ray_counter[7] = 0u;
     }
 }
 
@@ -3523,17 +3402,6 @@ struct StepVariant {
 // (demo.detector(), 4M photons: first-step walk 2.65 -> 2.21 ms for 0.11 ms of
 // sorting; second step unchanged).
 static constexpr uint32_t kBinFirstMin = 1u << 20;
-// CHR_TRACE_HELP=k: after the ray counter is exhausted, trace_kernel publishes
-// walks past k node + triangle steps for waves without rays to finish
-// (whole-wave walk); 0: off.  Off by default: on the 29k bench it costs more
-// than it saves (trace ms per step 16.1 off, 19.8 at 64, 30.9 at 32, 16.8 at
-// 128; profiles/r03/ab2): every hand-off stalls its wave on three dependent
-// atomics, and helpers only find walks published before they look.
-static uint32_t trace_help_after() {
-    const char *e = getenv("CHR_TRACE_HELP");
-    const int k = e ? atoi(e) : 0;
-    return (uint32_t)(k < 0 ? 0 : k);
-}
 // CHR_TRACE_AHEAD=1: trace_kernel takes rays from chunks of the ray counter
 // claimed ahead (the next chunk's atomic in flight while the wave walks) instead
 // of one blocking atomic per refill.  Off: measured slower (r03 ab5: trace 17.63
@@ -3682,7 +3550,6 @@ struct FlatCtx {
     // step's classification, then every step's scatter for the next step),
     // rays_walk the binned first step's records permuted into walk order
     uint4 *rays = nullptr, *rays_walk = nullptr;
-    unsigned long long *help_entries = nullptr;   // trace_kernel's long-walk help entries (HELP_CAP x HELP_WORDS)
     uint32_t cap = 0;                   // entries of flat_q / flat_best
 };
 static int flat_get(uint32_t n, FlatCtx &fc, int ctx = 0) {
@@ -3829,11 +3696,6 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
         ta.dev_n = dev_n;
         ta.mode = mode;
         ta.drain_max = trace_drain_max();
-        // long-walk help: device-driven slots only (the head kernel resets its words)
-        ta.help_after = (sc && fc->help_entries) ? trace_help_after() : 0u;
-        ta.help_ctl = next + 4;
-        ta.help_entries = fc->help_entries;
-        ta.flat_cap = fc->cap;
         ta.claim_ahead = trace_claim_ahead() ? 1u : 0u;
         a.flat_best = fc->flat_best;
         a.zero_word = count_next;   // cleared by the shade pass, filled by this step's scatter
@@ -4060,7 +3922,7 @@ static int prop_bufs(uint32_t nphotons, int32_t ntpb, int32_t max_blocks, int ct
     // split path: hits, ray counter, binning keys/order/histogram
     const size_t hbytes = b.fused ? (size_t)nphotons * 24 + 128 + 256 + 512 + sort_temp_bytes16(nphotons) : 0;
     // split path: ray records, queue order + walk order (FlatCtx::rays / rays_walk)
-    const size_t rbytes = b.fused ? (size_t)nphotons * 64 + 512 + HELP_CAP * HELP_WORDS * 8 + 256 : 0;
+    const size_t rbytes = b.fused ? (size_t)nphotons * 64 + 512 : 0;
     const size_t base_bytes = 2 * qbytes + swords * 4 + 64 + hbytes + rbytes;
     const size_t mbytes = tail_masks ? ((size_t)nphotons + 63) / 64 * 8 + 512 : 0;
     void *buf = nullptr;
@@ -4079,8 +3941,6 @@ static int prop_bufs(uint32_t nphotons, int32_t ntpb, int32_t max_blocks, int ct
     if (b.fused) {
         b.fc.rays = (uint4 *)(((uintptr_t)buf + 2 * qbytes + swords * 4 + 64 + hbytes + 255) & ~(uintptr_t)255);
         b.fc.rays_walk = b.fc.rays + 2 * (size_t)nphotons;
-        b.fc.help_entries =
-            (unsigned long long *)(((uintptr_t)(b.fc.rays_walk + 2 * (size_t)nphotons) + 255) & ~(uintptr_t)255);
     }
     return CHR_OK;
 }
@@ -4093,9 +3953,6 @@ static int prop_start(const PropBufs &b, uint32_t nphotons, uint32_t true_nphoto
     hipLaunchKernelGGL(init_queue_kernel, dim3(grid_for(nphotons)), dim3(BLOCK), 0, stream, b.q[0], b.q[1], nphotons,
                        true_nphotons, ncopies, z);
     CHR_HIP_CHECK(hipGetLastError());
-    // long-walk help entries: ready words of an earlier buffer use are launch serials;
-    // a fresh allocation is cleared so no stale word can match one
-    if (b.fc.help_entries) CHR_HIP_CHECK(hipMemsetAsync(b.fc.help_entries, 0, HELP_CAP * HELP_WORDS * 8, stream));
     return CHR_OK;
 }
 
