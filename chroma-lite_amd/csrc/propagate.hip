@@ -2973,6 +2973,60 @@ __global__ __launch_bounds__(BLOCK) void scatter_queue_kernel(const unsigned lon
     }
 }
 
+// Walk-order carry (CHR_WALK_CARRY; fc->walk): the next step's ray records
+// follow THIS step's walk order restricted to the survivors, instead of the
+// next queue's order.  The binned first step walks rays of one direction cell
+// together; those photons hit the same patch of the detector and leave it in
+// similar directions, so the order stays coherent for the steps after it,
+// while the queue (photon.py:242-250 order, which fixes each photon's RNG slot)
+// stays as it is.  walk[j]: the queue position walked j-th (nullptr: j).
+// walk_masks_kernel: bit j of wmasks = photon at queue position walk[j] alive.
+__global__ __launch_bounds__(BLOCK) void walk_masks_kernel(const unsigned long long *masks, const uint32_t *walk,
+                                                            uint32_t n, unsigned long long *wmasks,
+                                                            const uint32_t *dev_n, const uint32_t *mode, uint32_t skip) {
+    if (mode && (*mode == STEP_IDLE || *mode == skip)) return;
+    if (dev_n) n = *dev_n - 1u;
+    const uint32_t nj = (n + 63u) & ~63u;   // whole words: the wave's loop trip count is uniform
+    for (uint32_t j = blockIdx.x * BLOCK + threadIdx.x; j < nj; j += gridDim.x * BLOCK) {
+        bool alive = false;
+        if (j < n) {
+            const uint32_t p = walk ? walk[j] : j;
+            alive = ((masks[p >> 6] >> (p & 63u)) & 1ull) != 0ull;
+        }
+        const unsigned long long b = __ballot(alive);
+        if ((threadIdx.x & 63u) == 0u) wmasks[j >> 6] = b;
+    }
+}
+
+// Per walk position j of a survivor: its next queue position (the queue scan,
+// as scatter_queue_kernel computes it) and its next walk position (the
+// walk-order scan); writes the next step's ray record there, the flat-walk
+// enrolment, and walk_next = the next step's walk order.
+__global__ __launch_bounds__(BLOCK) void scatter_walk_kernel(const unsigned long long *masks, const uint32_t *word_offsets,
+                                                              const uint32_t *block_prefix, const uint32_t *base,
+                                                              const unsigned long long *wmasks, const uint32_t *woffsets,
+                                                              const uint32_t *wprefix, const uint32_t *walk,
+                                                              const uint32_t *in_queue, uint32_t n, uint32_t *walk_next,
+                                                              FlatEnrol fe, const uint32_t *dev_n, const uint32_t *mode,
+                                                              uint32_t skip) {
+    if (mode && (*mode == STEP_IDLE || *mode == skip)) return;
+    if (dev_n) n = *dev_n - 1u;
+    for (uint32_t j = blockIdx.x * BLOCK + threadIdx.x; j < n; j += gridDim.x * BLOCK) {
+        const unsigned long long wm = wmasks[j >> 6];
+        const uint32_t lj = j & 63u;
+        if (!((wm >> lj) & 1ull)) continue;
+        const uint32_t jn = word_offset(woffsets, wprefix, j >> 6) + (uint32_t)__popcll(wm & ((1ull << lj) - 1ull));
+        const uint32_t p = walk ? walk[j] : j;
+        const unsigned long long m = masks[p >> 6];
+        const uint32_t o = base[0] + word_offset(word_offsets, block_prefix, p >> 6) +
+                           (uint32_t)__popcll(m & ((1ull << (p & 63u)) - 1ull));
+        const uint32_t pid = in_queue[p];
+        walk_next[jn] = o - 1u;   // out_queue[0] is the count header: queue position o - 1
+        enrol_flat(fe.pos, fe.dir, pid, o - 1u, fe.hits, fe.flat_q, fe.flat_count, fe.flat_best, fe.rays, fe.last_hit,
+                   jn);
+    }
+}
+
 // Head of a device-driven step slot: the input queue's length picks the slot's
 // mode -- the nsteps policy of photon.py:261-264 (one-step launch; the
 // multi-step tail below `tail_below` photons or with use_weights, when more
@@ -3551,6 +3605,12 @@ struct FlatCtx {
     // rays_walk the binned first step's records permuted into walk order
     uint4 *rays = nullptr, *rays_walk = nullptr;
     uint32_t cap = 0;                   // entries of flat_q / flat_best
+    // walk-order carry (walk_carry_enabled): walk[cur] the step's walk order
+    // (steps after the first), walk[cur ^ 1] the next step's; the walk-order
+    // survivor masks and their scan
+    uint32_t *walk[2] = {nullptr, nullptr};
+    unsigned long long *wmasks = nullptr;
+    uint32_t *woffsets = nullptr, *wprefix = nullptr;
 };
 static int flat_get(uint32_t n, FlatCtx &fc, int ctx = 0) {
     static thread_local Scratch s[NCTX][16];
@@ -3574,6 +3634,13 @@ static int flat_get(uint32_t n, FlatCtx &fc, int ctx = 0) {
 }
 
 static bool trace_steps();
+// CHR_WALK_CARRY=1: later steps walk their rays in the previous step's walk
+// order (the binned first step's, restricted to survivors) instead of queue
+// order (walk_masks_kernel / scatter_walk_kernel; A/B, read per launch)
+static bool walk_carry_enabled() {
+    const char *e = getenv("CHR_WALK_CARRY");
+    return e && e[0] == '1';
+}
 // CHR_TRACE_RAYS=0: trace_kernel refills from the photon arrays through the
 // queue (the r02 path) instead of the ray records (A/B; read per launch)
 static bool trace_rays_enabled() {
@@ -3614,6 +3681,22 @@ struct SlotCtl {
 };
 constexpr int PHASE_ALL = 0, PHASE_PREFIX = 1, PHASE_REST = 2, PHASE_BIN = 3, PHASE_TRACE = 4;
 
+// The walk-order carry's end-of-step pass (after the queue scan): survivor
+// masks in walk order, their scan, and the records of the next step in that
+// order (scatter_walk_kernel).  skip: the mode that leaves no queue.
+static void launch_walk_scatter(const FlatCtx *fc, const unsigned long long *masks, const uint32_t *offsets,
+                                const uint32_t *bsums, const uint32_t *base, const uint32_t *in_queue, uint32_t n,
+                                const uint32_t *walk_cur, uint32_t *walk_next, const FlatEnrol &fe, hipStream_t stream,
+                                const uint32_t *dev_n, const uint32_t *mode, uint32_t skip, bool grid_stride) {
+    const uint32_t nwords = (n + 63) / 64;
+    const unsigned grid = grid_stride ? std::min<uint32_t>(4096u, grid_for(n)) : grid_for(n);
+    hipLaunchKernelGGL(walk_masks_kernel, dim3(std::max(1u, grid)), dim3(BLOCK), 0, stream, masks, walk_cur, n,
+                       fc->wmasks, dev_n, mode, skip);
+    launch_mask_scan(fc->wmasks, nwords, fc->woffsets, fc->wprefix, nullptr, nullptr, nullptr, stream, dev_n, mode, skip);
+    hipLaunchKernelGGL(scatter_walk_kernel, dim3(std::max(1u, grid)), dim3(BLOCK), 0, stream, masks, offsets, bsums, base,
+                       fc->wmasks, fc->woffsets, fc->wprefix, walk_cur, in_queue, n, walk_next, fe, dev_n, mode, skip);
+}
+
 // hits: n (triangle, distance) slots + a ray counter word, for the split path
 static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *rng, uint32_t nslots, uint32_t cap,
                        uint32_t n, const uint32_t *in_queue, uint32_t *out_queue, int32_t max_steps,
@@ -3644,6 +3727,10 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
     a.want = STEP_ONE;
     a.prio = 0;
     FlatEnrol fe{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+    // walk-order carry: this step's walk order (nullptr: queue order) and the next step's
+    bool carry = false;
+    const uint32_t *walk_cur = nullptr;
+    uint32_t *walk_next = nullptr;
     const uint32_t threads = std::min(cap, (n + 63u) & ~63u);
     const StepVariant sv = select_step_variant(g);
     // host-driven: the split when this launch is one step; device-driven: the
@@ -3682,6 +3769,8 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
         // ray records: the first step's from its classification, later steps' from
         // the previous step's scatter (enrol_next)
         const bool use_rays = fc->rays && trace_rays_enabled() && (first_one_step || fc->enrol_next);
+        // the carry needs records for this step and the next (they hold the queue positions)
+        carry = use_rays && fc->enrol_next && fc->walk[0] && walk_carry_enabled();
         if (first_one_step && do_bin)   // flat walks of the initial queue (later steps: enrolled by the previous scatter)
             hipLaunchKernelGGL(classify_kernel, dim3(grid_for(n)), dim3(BLOCK), 0, stream, ph->d_pos, ph->d_dir,
                                ph->d_flags, ph->d_last_hit_triangles, in_queue, n, hits, fc->flat_q, count_cur,
@@ -3722,6 +3811,14 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
             }
             ta.order = vals_out;
             if (use_rays) ta.rays = fc->rays_walk;
+        }
+        if (carry) {
+            // the first step's walk order: the binning's (queue order unbinned); later
+            // steps' (steps after the first): the previous step's scatter_walk_kernel output.  A first
+            // step that is the multi-step tail (host-driven propagate: it is compacted too)
+            // walked in queue order
+            walk_cur = first_step ? (first_one_step && binned ? ta.order : nullptr) : fc->walk[fc->cur];
+            walk_next = fc->walk[fc->cur ^ 1];
         }
         if (do_bin && sc && sc->ev_bin_end) CHR_HIP_CHECK(hipEventRecord(sc->ev_bin_end, stream));
         if (phase == PHASE_BIN) {
@@ -3776,8 +3873,11 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
         if (sc->evt_tail1) CHR_HIP_CHECK(hipEventRecord(sc->evt_tail1, ts));
         launch_mask_scan(masks, nwords, offsets, bsums, out_queue, counters + 1, nullptr, stream, dev_n, mode, STEP_TAIL);
         hipLaunchKernelGGL(scatter_queue_kernel, dim3(std::min<uint32_t>(4096u, grid_for(n))), dim3(BLOCK), 0, stream,
-                           masks, offsets, bsums, counters + 1, in_queue, 0, (int32_t)n, out_queue, fe, dev_n, mode,
+                           masks, offsets, bsums, counters + 1, in_queue, 0, (int32_t)n, out_queue,
+                           carry ? FlatEnrol{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr} : fe, dev_n, mode,
                            STEP_TAIL);
+        if (carry) launch_walk_scatter(fc, masks, offsets, bsums, counters + 1, in_queue, n, walk_cur, walk_next, fe,
+                                       stream, dev_n, mode, STEP_TAIL, true);
         CHR_HIP_CHECK(hipGetLastError());
         return CHR_OK;
     }
@@ -3796,8 +3896,11 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
     if (ev1) CHR_HIP_CHECK(hipEventRecord(ev1, stream));
     launch_mask_scan(masks, nwords, offsets, bsums, out_queue, counters + 1, nullptr, stream, dev_n, mode);
     hipLaunchKernelGGL(scatter_queue_kernel, dim3(sc ? std::min<uint32_t>(4096u, grid_for(n)) : grid_for(n)), dim3(BLOCK),
-                       0, stream, masks, offsets, bsums, counters + 1, in_queue, 0, (int32_t)n, out_queue, fe, dev_n,
-                       mode, STEP_IDLE);
+                       0, stream, masks, offsets, bsums, counters + 1, in_queue, 0, (int32_t)n, out_queue,
+                       carry ? FlatEnrol{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr} : fe, dev_n, mode,
+                       STEP_IDLE);
+    if (carry) launch_walk_scatter(fc, masks, offsets, bsums, counters + 1, in_queue, n, walk_cur, walk_next, fe, stream,
+                                   dev_n, mode, STEP_IDLE, sc != nullptr);
     CHR_HIP_CHECK(hipGetLastError());
     return CHR_OK;
 }
@@ -3922,7 +4025,11 @@ static int prop_bufs(uint32_t nphotons, int32_t ntpb, int32_t max_blocks, int ct
     // split path: hits, ray counter, binning keys/order/histogram
     const size_t hbytes = b.fused ? (size_t)nphotons * 24 + 128 + 256 + 512 + sort_temp_bytes16(nphotons) : 0;
     // split path: ray records, queue order + walk order (FlatCtx::rays / rays_walk)
-    const size_t rbytes = b.fused ? (size_t)nphotons * 64 + 512 : 0;
+    // + the walk-order carry: two walk orders, survivor masks in walk order and their scan
+    const size_t cwords = ((size_t)nphotons + 63) / 64;
+    const size_t rbytes = b.fused ? (size_t)nphotons * 64 + 512 + (size_t)nphotons * 8 + cwords * 12 +
+                                        (size_t)scan_blocks((uint32_t)cwords) * 4 + 1024
+                                  : 0;
     const size_t base_bytes = 2 * qbytes + swords * 4 + 64 + hbytes + rbytes;
     const size_t mbytes = tail_masks ? ((size_t)nphotons + 63) / 64 * 8 + 512 : 0;
     void *buf = nullptr;
@@ -3941,6 +4048,11 @@ static int prop_bufs(uint32_t nphotons, int32_t ntpb, int32_t max_blocks, int ct
     if (b.fused) {
         b.fc.rays = (uint4 *)(((uintptr_t)buf + 2 * qbytes + swords * 4 + 64 + hbytes + 255) & ~(uintptr_t)255);
         b.fc.rays_walk = b.fc.rays + 2 * (size_t)nphotons;
+        b.fc.walk[0] = (uint32_t *)(b.fc.rays_walk + 2 * (size_t)nphotons);
+        b.fc.walk[1] = b.fc.walk[0] + nphotons;
+        b.fc.wmasks = (unsigned long long *)(((uintptr_t)(b.fc.walk[1] + nphotons) + 255) & ~(uintptr_t)255);
+        b.fc.woffsets = (uint32_t *)(b.fc.wmasks + cwords);
+        b.fc.wprefix = b.fc.woffsets + cwords;
     }
     return CHR_OK;
 }
