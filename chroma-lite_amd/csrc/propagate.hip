@@ -1529,6 +1529,10 @@ struct PropagateArgs {
     uint32_t prio;                     // tail kernel: bit 0 raise its waves' issue priority (s_setprio),
                                        // bit 1 the whole-wave walk specialised for one walker (GS = 64)
     uint32_t want;
+    // tail kernel, work-queue mode (nullptr: group g runs queue positions g, g + cap, ...): a
+    // zeroed counter the photon groups take queue positions from, for queues no longer than
+    // the slot count (each position then its own RNG slot, loaded and stored per photon)
+    uint32_t *work;
 };
 // modes of a device-driven step slot (step_head_kernel)
 constexpr uint32_t STEP_IDLE = 0, STEP_ONE = 1, STEP_TAIL = 2;
@@ -2175,7 +2179,16 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_tail_kernel(const DevGe
     const uint32_t slot = tid / 8, sub = tid & 7u;
     const uint32_t n = a.dev_n ? *a.dev_n - 1u : (uint32_t)a.nthreads;
     const uint32_t nslot = cap < n ? cap : n;
-    if ((tid & ~63u) / 8 >= nslot) return;             // whole waves: the others help walk
+    // work-queue mode: groups take the next queue position when their photon ends, so the
+    // launch is one resident grid (no waves waiting for dispatch behind the first ones,
+    // no wave held by its slowest photon while its other groups idle)
+    const bool wq = a.work != nullptr && n <= cap;
+    if (!wq && (tid & ~63u) / 8 >= nslot) return;      // whole waves: the others help walk
+    auto next_q = [&]() -> uint32_t {   // the group's next queue position (group-uniform)
+        uint32_t v = 0;
+        if (sub == 0) v = atomicAdd(a.work, 1u);
+        return (uint32_t)__shfl((int)v, (int)(lane & ~7u));
+    };
     CHR_LDS uint32_t *wstack = (CHR_LDS uint32_t *)stacks + (threadIdx.x >> 6) * 8 * TAIL_STACK * 2;
     CHR_LDS uint32_t *wtris = (CHR_LDS uint32_t *)tris + (threadIdx.x >> 6) * 2 * TAIL_TRI;
     const DevGeom &g = *gdev;
@@ -2185,8 +2198,8 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_tail_kernel(const DevGe
     Photon p;
     State s;
     int steps = 0, scatter_first = 0;
-    uint32_t q = slot, pid = 0, iters = 0;
-    bool live = false, exhausted = slot >= nslot;
+    uint32_t q = wq ? next_q() : slot, pid = 0, iters = 0;
+    bool live = false, exhausted = wq ? q >= n : slot >= nslot;
     unsigned long long t0 = 0, walk_ticks = 0;
     enum { P_WALK, P_PHYS, P_OTHER };
     Prof<3> pf;
@@ -2202,6 +2215,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_tail_kernel(const DevGe
         a.last_hit[pid] = p.last_hit;
         a.weights[pid] = p.weight;
         if (sub == 0) {
+            if (wq) store_rng(a, q, rng);   // this photon's own slot
             if ((p.history & DEAD_MASK) == 0) atomicOr(a.alive_masks + (q >> 6), 1ull << (q & 63u));
             if (a.diag) {   // the tail's serial chain: longest photon in steps and in time
                 const unsigned long long cyc = __builtin_amdgcn_s_memrealtime() - t0;
@@ -2219,15 +2233,16 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_tail_kernel(const DevGe
             }
         }
         live = false;
-        q += cap;
+        q = wq ? next_q() : q + cap;
     };
     while (true) {
         if (!live && !exhausted) {   // the slot's next queued photon (dead on entry: skipped, no write-back)
             while (q < n) {
                 pid = a.input_queue[q];
                 const uint32_t history = a.flags[pid] & 0xFFFFu;   // photon.h:29
-                if (history & DEAD_MASK) { q += cap; continue; }
-                if (!have_rng) { load_rng(a, slot, rng); have_rng = true; }
+                if (history & DEAD_MASK) { q = wq ? next_q() : q + cap; continue; }
+                if (wq) load_rng(a, q, rng);
+                else if (!have_rng) { load_rng(a, slot, rng); have_rng = true; }
                 p.history = history;
                 p.pos = load3(a.pos, pid);
                 p.dir = load3(a.dir, pid);
@@ -2323,7 +2338,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_tail_kernel(const DevGe
             if (stop) finish();
         }
     }
-    if (have_rng && sub == 0) store_rng(a, slot, rng);
+    if (!wq && have_rng && sub == 0) store_rng(a, slot, rng);
     if (sub == 0 && overflow) atomicAdd(a.counters, overflow);
     if (sub == 0 && flat && a.diag) atomicAdd(a.diag, flat);
 #ifdef CHR_DEVICE_PROFILE
@@ -3034,7 +3049,7 @@ __global__ __launch_bounds__(BLOCK) void scatter_walk_kernel(const unsigned long
 // and the slot's bookkeeping is reset: output queue header, trace ray counter.
 __global__ void step_head_kernel(const uint32_t *in_hdr, uint32_t *out_hdr, uint32_t *mode, uint32_t *n_out,
                                  uint32_t *done, uint32_t *ray_counter, uint32_t tail_below, int32_t remaining,
-                                 int32_t use_weights, uint32_t max_n) {
+                                 int32_t use_weights, uint32_t max_n, uint32_t *host_ring) {
     if (threadIdx.x != 0) return;
     const uint32_t n = in_hdr[0] - 1u;
     uint32_t m = STEP_IDLE;
@@ -3045,6 +3060,9 @@ __global__ void step_head_kernel(const uint32_t *in_hdr, uint32_t *out_hdr, uint
     }
     mode[0] = m;
     n_out[0] = n;
+    // the host's copy of (mode, length), in pinned host memory: read once the
+    // slot's end event has completed (no copy dispatch per slot)
+    if (host_ring) { host_ring[0] = m; host_ring[1] = n; }
     if (m != STEP_IDLE) {
         out_hdr[0] = 1u;
         ray_counter[0] = 0u;
@@ -3547,6 +3565,7 @@ static int launch_chunk(const chr_geometry *g, const chr_photons *ph, uint32_t *
     a.dev_n = nullptr;
     a.mode = nullptr;
     a.want = STEP_ONE;
+    a.work = nullptr;
     a.prio = 0;
     if (sort_enabled() && nthreads >= kSortMin) {
         // coherence order (sort_key_kernel): rays that start close together in
@@ -3677,9 +3696,31 @@ struct SlotCtl {
     // previous tail's first waves for CUs).  ev_bin_end: after the binning.
     int phase = 0;
     int ctx = 0;                      // buffer context (walk-stack column)
+    uint32_t *host_ring = nullptr;    // pinned (mode, length) words the head kernel writes (nullptr: none)
     hipEvent_t prefix_done = nullptr, ev_rest0 = nullptr, ev_bin_end = nullptr;
 };
 constexpr int PHASE_ALL = 0, PHASE_PREFIX = 1, PHASE_REST = 2, PHASE_BIN = 3, PHASE_TRACE = 4;
+
+// The wave-adaptive tail kernel as one resident grid whose photon groups take
+// queue positions from a counter (PropagateArgs::work; the slot's ray counter,
+// zeroed by the head kernel) -- where every queued photon has its own RNG slot
+// (the tail starts below nthreads_per_block * 128 photons and that is at most
+// the slot count; not use_weights, whose tail takes any length).  r03 ab11, 29k
+// bench: 440.4 -> 450.3 M/s (mean tail 6.93 -> 6.65 ms, kernel time per step
+// 29.98 -> 28.37 ms).  CHR_TAIL_WQ=0: one group per slot, as many waves as
+// photons / 8 (A/B).
+static bool tail_work_queue(const StepVariant &sv, const SlotCtl *sc, int32_t use_weights, uint32_t cap) {
+    const char *e = getenv("CHR_TAIL_WQ");
+    return !(e && e[0] == '0') && sv.tail_group == 8 && sc && !use_weights && sc->tail_below <= cap;
+}
+// blocks of a tail launch: every slot's group, or (work queue) the resident grid
+static unsigned tail_grid(const StepVariant &sv, uint32_t threads, bool work_queue) {
+    const unsigned full = grid_for((uint64_t)threads * sv.tail_group);
+    if (!work_queue) return full;
+    const int cus = device_cus();
+    const unsigned resident = (unsigned)std::max(1, cus) * (unsigned)tail_waves() * 4u * 64u / BLOCK;
+    return std::max(1u, std::min(full, resident));
+}
 
 // The walk-order carry's end-of-step pass (after the queue scan): survivor
 // masks in walk order, their scan, and the records of the next step in that
@@ -3725,6 +3766,7 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
     a.dev_n = dev_n;
     a.mode = mode;
     a.want = STEP_ONE;
+    a.work = nullptr;
     a.prio = 0;
     FlatEnrol fe{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
     // walk-order carry: this step's walk order (nullptr: queue order) and the next step's
@@ -3753,7 +3795,7 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
     if (sc && do_bin) {
         if (!next) return chr::fail(CHR_ERR_INVALID, "launch_step: device-driven steps need the split path");
         hipLaunchKernelGGL(step_head_kernel, dim3(1), dim3(64), 0, stream, in_queue - 1, out_queue, sc->mode, sc->nk,
-                           sc->done, next, sc->tail_below, sc->remaining, use_weights, sc->n_layout);
+                           sc->done, next, sc->tail_below, sc->remaining, use_weights, sc->n_layout, sc->host_ring);
     } else if (split && !sc) {
         CHR_HIP_CHECK(hipMemsetAsync(next, 0, 4, stream));
     }
@@ -3868,7 +3910,8 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
         at.alive_masks = sc->tail_masks;
         at.max_steps = sc->remaining;
         at.want = STEP_TAIL;
-        hipLaunchKernelGGL(sv.tail, dim3(grid_for((uint64_t)threads * sv.tail_group)), dim3(BLOCK), 0, ts,
+        at.work = tail_work_queue(sv, sc, use_weights, cap) ? next : nullptr;
+        hipLaunchKernelGGL(sv.tail, dim3(tail_grid(sv, threads, at.work != nullptr)), dim3(BLOCK), 0, ts,
                            (const DevGeom *)g->d_dev, at, cap);
         if (sc->evt_tail1) CHR_HIP_CHECK(hipEventRecord(sc->evt_tail1, ts));
         launch_mask_scan(masks, nwords, offsets, bsums, out_queue, counters + 1, nullptr, stream, dev_n, mode, STEP_TAIL);
@@ -3888,7 +3931,8 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
         a.max_steps = sc ? sc->remaining : max_steps;
         a.want = STEP_TAIL;
         a.prio = tail_gs64() ? 2u : 0u;
-        hipLaunchKernelGGL(sv.tail, dim3(grid_for((uint64_t)threads * sv.tail_group)), dim3(BLOCK), 0, stream,
+        a.work = (sc && next && tail_work_queue(sv, sc, use_weights, cap)) ? next : nullptr;
+        hipLaunchKernelGGL(sv.tail, dim3(tail_grid(sv, threads, a.work != nullptr)), dim3(BLOCK), 0, stream,
                            (const DevGeom *)g->d_dev, a, cap);
     } else if (!split) {
         hipLaunchKernelGGL(sv.fn, dim3(grid_for(threads)), dim3(BLOCK), 0, stream, (const DevGeom *)g->d_dev, a, cap);
@@ -4108,7 +4152,7 @@ static int device_slots(const chr_geometry *g, const chr_photons *ph, uint32_t n
     uint32_t *done = ctl + 2 * (size_t)max_steps;
     if (!run.prefix_done) CHR_HIP_CHECK(hipMemsetAsync(done, 0, 4, stream));
     b.fc.enrol_next = true;
-    uint32_t *ring = b.pinned + 64;   // (mode, n) of recent slots, 32 entries (copied after each slot)
+    uint32_t *ring = b.pinned + 64;   // (mode, n) of recent slots, 32 entries (written by each slot's head kernel)
     std::vector<hipEvent_t> &events = *run.events;
     uint32_t n_ub = nphotons;
     int k = 0, cur = 0;
@@ -4123,6 +4167,7 @@ static int device_slots(const chr_geometry *g, const chr_photons *ph, uint32_t n
         sc.evt_tail1 = ev[6];
         sc.rng_ready = k == 0 ? run.rng_ready : nullptr;
         sc.ctx = run.ctx;
+        sc.host_ring = ring + 2 * (k % 32);   // written by the slot's head kernel (slot 0 of a batch: its prefix's)
         if (k == 0 && run.prefix_done) {
             sc.phase = PHASE_REST;
             sc.prefix_done = run.prefix_done;
@@ -4133,7 +4178,6 @@ static int device_slots(const chr_geometry *g, const chr_photons *ph, uint32_t n
                          scatter_first, b.scratch, stream, ev[0], ev[1], b.hits, b.sort_space, k == 0, ev[2], ev[3],
                          &split, &b.fc, &sc);
         if (rc) return rc;
-        CHR_HIP_CHECK(hipMemcpyAsync(ring + 2 * (k % 32), ctl + 2 * (size_t)k, 8, hipMemcpyDeviceToHost, stream));
         if (run.on_length)   // the output queue's count header (+1)
             CHR_HIP_CHECK(hipMemcpyAsync(run.out_ring + k % 32, b.q[cur ^ 1], 4, hipMemcpyDeviceToHost, stream));
         CHR_HIP_CHECK(hipEventRecord(ev[4], stream));
@@ -4523,6 +4567,7 @@ static int queue_prefix(const chr_geometry *g, const chr_photons *ph, uint32_t n
     sc.phase = parts == 1 ? PHASE_BIN : (parts == 2 ? PHASE_TRACE : PHASE_PREFIX);
     sc.ctx = ctx;
     sc.prefix_done = prefix_done;
+    sc.host_ring = b.pinned + 64;   // ring entry 0 (device_slots' slot 0): this head is slot 0's
     hipEvent_t *ev = events.data();
     sc.ev_bin_end = ev[8];
     return launch_step(g, ph, rng, nslots, (uint32_t)b.cap, nphotons, b.q[0] + 1, b.q[1], 1, use_weights,

@@ -53,7 +53,7 @@ def _same(a, b, label):
         assert np.array_equal(getattr(a, f), getattr(b, f)), '%s: %s differs' % (label, f)
 
 
-@pytest.mark.parametrize('ntpb,max_blocks', [(64, 64), (256, 64)])
+@pytest.mark.parametrize('ntpb,max_blocks', [(64, 64), (256, 64), (64, 256)])
 def test_batches_equal_sequential_and_oracle(cuda, small_detector, small_packed, ntpb, max_blocks):
     """Batches of 30k / 70k / 5k / 120k photons (one-step slots, then tails of
     < ntpb*128 photons) on the 2-PMT detector: batched == sequential GPU ==
