@@ -1533,6 +1533,9 @@ struct PropagateArgs {
     // zeroed counter the photon groups take queue positions from, for queues no longer than
     // the slot count (each position then its own RNG slot, loaded and stored per photon)
     uint32_t *work;
+    // shade kernel, walk-order carry (nullptr: off): walive[winv[q]] = survival of queue position q
+    const uint32_t *winv;
+    uint8_t *walive;
 };
 // modes of a device-driven step slot (step_head_kernel)
 constexpr uint32_t STEP_IDLE = 0, STEP_ONE = 1, STEP_TAIL = 2;
@@ -1737,7 +1740,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_step_kernel(const DevGe
 // share only the RNG state, so the next photon's queue entry, state and walk
 // result are loaded while the current one's physics runs.
 struct QueuedPhoton {
-    uint32_t pid, history;
+    uint32_t pid, history, walk;
     V3 pos, dir, pol;
     float wavelength, time, weight;
     int last_hit;
@@ -1754,6 +1757,7 @@ __device__ __forceinline__ void fetch_queued(const PropagateArgs &a, uint32_t q,
     f.weight = a.weights[f.pid];
     f.last_hit = a.last_hit[f.pid];
     f.hit = a.hits[q];
+    f.walk = a.winv ? a.winv[q] : 0u;
 }
 template <int MINW>
 __global__ __launch_bounds__(BLOCK, MINW) void shade_kernel(const DevGeom *__restrict__ gdev, PropagateArgs a,
@@ -1823,6 +1827,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void shade_kernel(const DevGeom *__res
             a.weights[pid] = p.weight;
             alive = (p.history & DEAD_MASK) == 0;
         }
+        if (a.walive && pos < n) a.walive[cur.walk] = alive ? 1u : 0u;   // dead on entry: 0 too
         const unsigned long long mask = __ballot(alive);
         if ((slot & 63u) == 0) a.alive_masks[qb >> 6] = mask;
     }
@@ -2433,6 +2438,7 @@ struct TraceArgs {
     // (the input queue's count header) and the launch runs only if *mode is STEP_ONE
     const uint32_t *dev_n;
     const uint32_t *mode;
+    uint32_t *winv;              // walk-order carry: winv[queue position] = its walk position (nullptr: off)
     uint32_t drain_max;          // a wave drains its last <= drain_max walks whole-wave (0: never; at most 8)
     uint32_t claim_ahead;        // refills from claimed chunks, the next claim in flight (trace_claim_ahead)
 };
@@ -2623,6 +2629,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
                         // the ray record: one 32-B load (put_ray); skip bit: dead / NaN / flat
                         const uint4 r0 = gld(a.rays + 2 * (size_t)j), r1 = gld(a.rays + 2 * (size_t)j + 1);
                         q = r1.w & ~RAY_SKIP;
+                        if (a.winv) a.winv[q] = j;
                         if (!(r1.w & RAY_SKIP)) {
                             o = v3(__uint_as_float(r0.x), __uint_as_float(r0.y), __uint_as_float(r0.z));
                             d = v3(__uint_as_float(r0.w), __uint_as_float(r1.x), __uint_as_float(r1.y));
@@ -2994,51 +3001,127 @@ __global__ __launch_bounds__(BLOCK) void scatter_queue_kernel(const unsigned lon
 // together; those photons hit the same patch of the detector and leave it in
 // similar directions, so the order stays coherent for the steps after it,
 // while the queue (photon.py:242-250 order, which fixes each photon's RNG slot)
-// stays as it is.  walk[j]: the queue position walked j-th (nullptr: j).
-// walk_masks_kernel: bit j of wmasks = photon at queue position walk[j] alive.
-__global__ __launch_bounds__(BLOCK) void walk_masks_kernel(const unsigned long long *masks, const uint32_t *walk,
-                                                            uint32_t n, unsigned long long *wmasks,
-                                                            const uint32_t *dev_n, const uint32_t *mode, uint32_t skip) {
+// stays as it is.  Same dispatches as without it: trace_kernel records each
+// queue position's walk position (winv), shade_kernel each walk position's
+// survival (walive, one byte), and the end-of-step scan and scatter below run
+// over both orders at once.  walk[j]: the queue position walked j-th (nullptr: j).
+__device__ __forceinline__ unsigned long long bytes_to_bits(uint4 v0, uint4 v1) {   // 16 bytes (0 / 1) -> 16 bits
+    const unsigned long long m = 0x0102040810204080ull;   // byte k (0 / 1) of x -> bit 56 + k of x * m
+    const unsigned long long a = ((unsigned long long)v0.y << 32) | v0.x, b = ((unsigned long long)v0.w << 32) | v0.z;
+    const unsigned long long c = ((unsigned long long)v1.y << 32) | v1.x, d = ((unsigned long long)v1.w << 32) | v1.z;
+    return ((a * m) >> 56) | (((b * m) >> 56) << 8) | (((c * m) >> 56) << 16) | (((d * m) >> 56) << 24);
+}
+// mask_block_scan_kernel over the queue masks and, from walive, the walk-order
+// survivor masks (wmasks) with their own word offsets / block sums
+__global__ __launch_bounds__(SCAN_WORDS) void mask_block_scan2_kernel(const unsigned long long *masks,
+                                                                      const uint8_t *walive, uint32_t n,
+                                                                      uint32_t *word_offsets, uint32_t *block_sums,
+                                                                      unsigned long long *wmasks, uint32_t *woffsets,
+                                                                      uint32_t *wsums, const uint32_t *dev_n,
+                                                                      const uint32_t *mode, uint32_t skip) {
+    __shared__ uint32_t tot[2][SCAN_WORDS / 64];
     if (mode && (*mode == STEP_IDLE || *mode == skip)) return;
     if (dev_n) n = *dev_n - 1u;
-    const uint32_t nj = (n + 63u) & ~63u;   // whole words: the wave's loop trip count is uniform
-    for (uint32_t j = blockIdx.x * BLOCK + threadIdx.x; j < nj; j += gridDim.x * BLOCK) {
-        bool alive = false;
-        if (j < n) {
-            const uint32_t p = walk ? walk[j] : j;
-            alive = ((masks[p >> 6] >> (p & 63u)) & 1ull) != 0ull;
-        }
-        const unsigned long long b = __ballot(alive);
-        if ((threadIdx.x & 63u) == 0u) wmasks[j >> 6] = b;
+    const uint32_t nwords = (n + 63u) / 64u;
+    const uint32_t w = blockIdx.x * SCAN_WORDS + threadIdx.x;
+    const uint32_t c = w < nwords ? (uint32_t)__popcll(masks[w]) : 0u;
+    unsigned long long wm = 0ull;
+    if (w < nwords) {   // 64 survival bytes (the last word's bytes past n: cleared)
+        const uint4 *src = reinterpret_cast<const uint4 *>(walive + 64 * (size_t)w);
+        wm = bytes_to_bits(src[0], src[1]) | (bytes_to_bits(src[2], src[3]) << 32);
+        if (64u * w + 64u > n) wm &= (1ull << (n - 64u * w)) - 1ull;
+        wmasks[w] = wm;
+    }
+    const uint32_t cw = (uint32_t)__popcll(wm);
+    uint32_t x = c, y = cw;
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t xu = __shfl_up(x, off, 64), yu = __shfl_up(y, off, 64);
+        if (lane >= off) { x += xu; y += yu; }
+    }
+    const int wid = threadIdx.x >> 6;
+    if (lane == 63) { tot[0][wid] = x; tot[1][wid] = y; }
+    __syncthreads();
+    uint32_t bx = 0, by = 0;
+    for (int k = 0; k < wid; ++k) { bx += tot[0][k]; by += tot[1][k]; }
+    if (w < nwords) { word_offsets[w] = bx + x - c; woffsets[w] = by + y - cw; }
+    if (threadIdx.x == SCAN_WORDS - 1) { block_sums[blockIdx.x] = bx + x; wsums[blockIdx.x] = by + y; }
+}
+// exclusive prefix of one block-sum array by a 1024-thread block (scan_block_sums_kernel's)
+__device__ __forceinline__ uint32_t block_prefix_1024(uint32_t *sums, uint32_t nblocks, uint32_t *partial) {
+    const uint32_t tid = threadIdx.x;
+    const uint32_t per = (nblocks + 1023) / 1024;
+    const uint32_t b0 = tid * per;
+    uint32_t sum = 0;
+    for (uint32_t k = 0; k < per && b0 + k < nblocks; ++k) sum += sums[b0 + k];
+    partial[tid] = sum;
+    __syncthreads();
+    for (uint32_t off = 1; off < 1024; off <<= 1) {
+        const uint32_t v = (tid >= off) ? partial[tid - off] : 0;
+        __syncthreads();
+        partial[tid] += v;
+        __syncthreads();
+    }
+    uint32_t run = partial[tid] - sum;
+    for (uint32_t k = 0; k < per && b0 + k < nblocks; ++k) {
+        const uint32_t v = sums[b0 + k];
+        sums[b0 + k] = run;
+        run += v;
+    }
+    const uint32_t total = partial[1023];
+    __syncthreads();
+    return total;
+}
+__global__ __launch_bounds__(1024) void scan_block_sums2_kernel(uint32_t *block_sums, uint32_t *wsums, uint32_t nblocks,
+                                                                uint32_t *out_counter, uint32_t *base, const uint32_t *mode,
+                                                                uint32_t skip) {
+    __shared__ uint32_t partial[1024];
+    if (mode && (*mode == STEP_IDLE || *mode == skip)) return;
+    const uint32_t total = block_prefix_1024(block_sums, nblocks, partial);
+    block_prefix_1024(wsums, nblocks, partial);
+    if (threadIdx.x == 1023) {
+        base[0] = out_counter[0];
+        out_counter[0] += total;
     }
 }
 
-// Per walk position j of a survivor: its next queue position (the queue scan,
-// as scatter_queue_kernel computes it) and its next walk position (the
-// walk-order scan); writes the next step's ray record there, the flat-walk
-// enrolment, and walk_next = the next step's walk order.
+// The end-of-step scatter over both orders: per walk position j of a survivor,
+// its next queue position (the queue scan; out_queue[o] = photon id, as
+// scatter_queue_kernel writes it) and its next walk position jn (the walk
+// scan): the next step's ray record and flat-walk enrolment, walk_next[jn].
+// A multi-step tail slot (its alive bits are the tail kernel's; no walk order)
+// scatters in queue order as scatter_queue_kernel does.
 __global__ __launch_bounds__(BLOCK) void scatter_walk_kernel(const unsigned long long *masks, const uint32_t *word_offsets,
                                                               const uint32_t *block_prefix, const uint32_t *base,
                                                               const unsigned long long *wmasks, const uint32_t *woffsets,
                                                               const uint32_t *wprefix, const uint32_t *walk,
-                                                              const uint32_t *in_queue, uint32_t n, uint32_t *walk_next,
-                                                              FlatEnrol fe, const uint32_t *dev_n, const uint32_t *mode,
-                                                              uint32_t skip) {
+                                                              const uint32_t *in_queue, uint32_t n, uint32_t *out_queue,
+                                                              uint32_t *walk_next, FlatEnrol fe, const uint32_t *dev_n,
+                                                              const uint32_t *mode, uint32_t skip) {
     if (mode && (*mode == STEP_IDLE || *mode == skip)) return;
     if (dev_n) n = *dev_n - 1u;
+    const bool by_walk = !mode || *mode == STEP_ONE;
     for (uint32_t j = blockIdx.x * BLOCK + threadIdx.x; j < n; j += gridDim.x * BLOCK) {
-        const unsigned long long wm = wmasks[j >> 6];
-        const uint32_t lj = j & 63u;
-        if (!((wm >> lj) & 1ull)) continue;
-        const uint32_t jn = word_offset(woffsets, wprefix, j >> 6) + (uint32_t)__popcll(wm & ((1ull << lj) - 1ull));
-        const uint32_t p = walk ? walk[j] : j;
+        uint32_t p = j, jn = 0;
+        if (by_walk) {
+            const unsigned long long wm = wmasks[j >> 6];
+            const uint32_t lj = j & 63u;
+            if (!((wm >> lj) & 1ull)) continue;
+            jn = word_offset(woffsets, wprefix, j >> 6) + (uint32_t)__popcll(wm & ((1ull << lj) - 1ull));
+            p = walk ? walk[j] : j;
+        }
         const unsigned long long m = masks[p >> 6];
+        if (!by_walk && !((m >> (p & 63u)) & 1ull)) continue;
         const uint32_t o = base[0] + word_offset(word_offsets, block_prefix, p >> 6) +
                            (uint32_t)__popcll(m & ((1ull << (p & 63u)) - 1ull));
         const uint32_t pid = in_queue[p];
-        walk_next[jn] = o - 1u;   // out_queue[0] is the count header: queue position o - 1
-        enrol_flat(fe.pos, fe.dir, pid, o - 1u, fe.hits, fe.flat_q, fe.flat_count, fe.flat_best, fe.rays, fe.last_hit,
-                   jn);
+        out_queue[o] = pid;
+        // out_queue[0] is the count header: queue position o - 1
+        if (by_walk) walk_next[jn] = o - 1u;
+        if (fe.pos)
+            enrol_flat(fe.pos, fe.dir, pid, o - 1u, fe.hits, fe.flat_q, fe.flat_count, fe.flat_best, fe.rays, fe.last_hit,
+                       by_walk ? jn : o - 1u);
     }
 }
 
@@ -3414,6 +3497,10 @@ static int tail_waves() {              // CHR_TAIL_WAVES=4: the tail kernel at 4
     const char *e = getenv("CHR_TAIL_WAVES");
     return e ? atoi(e) : kTailWaves;
 }
+static int shade_waves() {             // CHR_SHADE_WAVES=2|4: the shade kernel at 2 / 4 waves per SIMD (A/B)
+    const char *e = getenv("CHR_SHADE_WAVES");
+    return e ? atoi(e) : 3;
+}
 static bool tail_group_walk() {        // CHR_TAIL=group: the fixed 8-lane group kernel (A/B)
     const char *e = getenv("CHR_TAIL");
     return e && std::strcmp(e, "group") == 0;
@@ -3522,7 +3609,7 @@ static StepVariant select_step_variant(const chr_geometry *g) {
             sv.fn = propagate_step_kernel<8, 4, kWalk>;
             sv.trace = trace_refill_r() == 16 ? trace_kernel<false, 6, 12, 4, 16>
                        : (trace_refill_r() == 32 ? trace_kernel<false, 6, 12, 4, 32> : trace_kernel<false, 6, 12, 4, 48>);
-            sv.shade = shade_kernel<3>;
+            sv.shade = shade_waves() == 4 ? shade_kernel<4> : (shade_waves() == 2 ? shade_kernel<2> : shade_kernel<3>);
             sv.tail = tail_group_walk() ? propagate_group_kernel<8, kGroupWaves>
                       : (tail_waves() == 4 ? propagate_tail_kernel<4>
                          : (tail_waves() == 3 ? propagate_tail_kernel<3> : propagate_tail_kernel<kTailWaves>));
@@ -3566,6 +3653,8 @@ static int launch_chunk(const chr_geometry *g, const chr_photons *ph, uint32_t *
     a.mode = nullptr;
     a.want = STEP_ONE;
     a.work = nullptr;
+    a.winv = nullptr;
+    a.walive = nullptr;
     a.prio = 0;
     if (sort_enabled() && nthreads >= kSortMin) {
         // coherence order (sort_key_kernel): rays that start close together in
@@ -3630,6 +3719,8 @@ struct FlatCtx {
     uint32_t *walk[2] = {nullptr, nullptr};
     unsigned long long *wmasks = nullptr;
     uint32_t *woffsets = nullptr, *wprefix = nullptr;
+    uint32_t *winv = nullptr;   // queue position -> walk position (trace_kernel)
+    uint8_t *walive = nullptr;  // walk position -> survived the step (shade_kernel)
 };
 static int flat_get(uint32_t n, FlatCtx &fc, int ctx = 0) {
     static thread_local Scratch s[NCTX][16];
@@ -3722,20 +3813,24 @@ static unsigned tail_grid(const StepVariant &sv, uint32_t threads, bool work_que
     return std::max(1u, std::min(full, resident));
 }
 
-// The walk-order carry's end-of-step pass (after the queue scan): survivor
-// masks in walk order, their scan, and the records of the next step in that
-// order (scatter_walk_kernel).  skip: the mode that leaves no queue.
-static void launch_walk_scatter(const FlatCtx *fc, const unsigned long long *masks, const uint32_t *offsets,
-                                const uint32_t *bsums, const uint32_t *base, const uint32_t *in_queue, uint32_t n,
-                                const uint32_t *walk_cur, uint32_t *walk_next, const FlatEnrol &fe, hipStream_t stream,
-                                const uint32_t *dev_n, const uint32_t *mode, uint32_t skip, bool grid_stride) {
-    const uint32_t nwords = (n + 63) / 64;
+// The walk-order carry's end of step: the survivor scan of both orders and the
+// scatter in walk order (mask_block_scan2 / scan_block_sums2 / scatter_walk,
+// the same three dispatches as launch_mask_scan + scatter_queue_kernel).
+// skip: the mode that leaves no queue.
+static void launch_carry_scatter(const FlatCtx *fc, const unsigned long long *masks, uint32_t *offsets, uint32_t *bsums,
+                                 uint32_t *out_queue, uint32_t *base, const uint32_t *in_queue, uint32_t n,
+                                 const uint32_t *walk_cur, uint32_t *walk_next, const FlatEnrol &fe, hipStream_t stream,
+                                 const uint32_t *dev_n, const uint32_t *mode, uint32_t skip, bool grid_stride) {
+    const uint32_t nb = scan_blocks((n + 63) / 64);
+    if (nb)
+        hipLaunchKernelGGL(mask_block_scan2_kernel, dim3(nb), dim3(SCAN_WORDS), 0, stream, masks, fc->walive, n, offsets,
+                           bsums, fc->wmasks, fc->woffsets, fc->wprefix, dev_n, mode, skip);
+    hipLaunchKernelGGL(scan_block_sums2_kernel, dim3(1), dim3(1024), 0, stream, bsums, fc->wprefix, nb, out_queue, base,
+                       mode, skip);
     const unsigned grid = grid_stride ? std::min<uint32_t>(4096u, grid_for(n)) : grid_for(n);
-    hipLaunchKernelGGL(walk_masks_kernel, dim3(std::max(1u, grid)), dim3(BLOCK), 0, stream, masks, walk_cur, n,
-                       fc->wmasks, dev_n, mode, skip);
-    launch_mask_scan(fc->wmasks, nwords, fc->woffsets, fc->wprefix, nullptr, nullptr, nullptr, stream, dev_n, mode, skip);
     hipLaunchKernelGGL(scatter_walk_kernel, dim3(std::max(1u, grid)), dim3(BLOCK), 0, stream, masks, offsets, bsums, base,
-                       fc->wmasks, fc->woffsets, fc->wprefix, walk_cur, in_queue, n, walk_next, fe, dev_n, mode, skip);
+                       fc->wmasks, fc->woffsets, fc->wprefix, walk_cur, in_queue, n, out_queue, walk_next, fe, dev_n,
+                       mode, skip);
 }
 
 // hits: n (triangle, distance) slots + a ray counter word, for the split path
@@ -3767,6 +3862,8 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
     a.mode = mode;
     a.want = STEP_ONE;
     a.work = nullptr;
+    a.winv = nullptr;
+    a.walive = nullptr;
     a.prio = 0;
     FlatEnrol fe{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
     // walk-order carry: this step's walk order (nullptr: queue order) and the next step's
@@ -3812,7 +3909,7 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
         // the previous step's scatter (enrol_next)
         const bool use_rays = fc->rays && trace_rays_enabled() && (first_one_step || fc->enrol_next);
         // the carry needs records for this step and the next (they hold the queue positions)
-        carry = use_rays && fc->enrol_next && fc->walk[0] && walk_carry_enabled();
+        carry = use_rays && fc->enrol_next && fc->walk[0] && fc->winv && walk_carry_enabled();
         if (first_one_step && do_bin)   // flat walks of the initial queue (later steps: enrolled by the previous scatter)
             hipLaunchKernelGGL(classify_kernel, dim3(grid_for(n)), dim3(BLOCK), 0, stream, ph->d_pos, ph->d_dir,
                                ph->d_flags, ph->d_last_hit_triangles, in_queue, n, hits, fc->flat_q, count_cur,
@@ -3828,6 +3925,9 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
         ta.mode = mode;
         ta.drain_max = trace_drain_max();
         ta.claim_ahead = trace_claim_ahead() ? 1u : 0u;
+        ta.winv = carry ? fc->winv : nullptr;
+        a.winv = carry ? fc->winv : nullptr;
+        a.walive = carry ? fc->walive : nullptr;
         a.flat_best = fc->flat_best;
         a.zero_word = count_next;   // cleared by the shade pass, filled by this step's scatter
         if (fc->enrol_next)
@@ -3914,13 +4014,16 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
         hipLaunchKernelGGL(sv.tail, dim3(tail_grid(sv, threads, at.work != nullptr)), dim3(BLOCK), 0, ts,
                            (const DevGeom *)g->d_dev, at, cap);
         if (sc->evt_tail1) CHR_HIP_CHECK(hipEventRecord(sc->evt_tail1, ts));
-        launch_mask_scan(masks, nwords, offsets, bsums, out_queue, counters + 1, nullptr, stream, dev_n, mode, STEP_TAIL);
-        hipLaunchKernelGGL(scatter_queue_kernel, dim3(std::min<uint32_t>(4096u, grid_for(n))), dim3(BLOCK), 0, stream,
-                           masks, offsets, bsums, counters + 1, in_queue, 0, (int32_t)n, out_queue,
-                           carry ? FlatEnrol{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr} : fe, dev_n, mode,
-                           STEP_TAIL);
-        if (carry) launch_walk_scatter(fc, masks, offsets, bsums, counters + 1, in_queue, n, walk_cur, walk_next, fe,
-                                       stream, dev_n, mode, STEP_TAIL, true);
+        if (carry) {
+            launch_carry_scatter(fc, masks, offsets, bsums, out_queue, counters + 1, in_queue, n, walk_cur, walk_next, fe,
+                                 stream, dev_n, mode, STEP_TAIL, true);
+        } else {
+            launch_mask_scan(masks, nwords, offsets, bsums, out_queue, counters + 1, nullptr, stream, dev_n, mode,
+                             STEP_TAIL);
+            hipLaunchKernelGGL(scatter_queue_kernel, dim3(std::min<uint32_t>(4096u, grid_for(n))), dim3(BLOCK), 0,
+                               stream, masks, offsets, bsums, counters + 1, in_queue, 0, (int32_t)n, out_queue, fe,
+                               dev_n, mode, STEP_TAIL);
+        }
         CHR_HIP_CHECK(hipGetLastError());
         return CHR_OK;
     }
@@ -3938,13 +4041,15 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
         hipLaunchKernelGGL(sv.fn, dim3(grid_for(threads)), dim3(BLOCK), 0, stream, (const DevGeom *)g->d_dev, a, cap);
     }
     if (ev1) CHR_HIP_CHECK(hipEventRecord(ev1, stream));
-    launch_mask_scan(masks, nwords, offsets, bsums, out_queue, counters + 1, nullptr, stream, dev_n, mode);
-    hipLaunchKernelGGL(scatter_queue_kernel, dim3(sc ? std::min<uint32_t>(4096u, grid_for(n)) : grid_for(n)), dim3(BLOCK),
-                       0, stream, masks, offsets, bsums, counters + 1, in_queue, 0, (int32_t)n, out_queue,
-                       carry ? FlatEnrol{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr} : fe, dev_n, mode,
-                       STEP_IDLE);
-    if (carry) launch_walk_scatter(fc, masks, offsets, bsums, counters + 1, in_queue, n, walk_cur, walk_next, fe, stream,
-                                   dev_n, mode, STEP_IDLE, sc != nullptr);
+    if (carry) {
+        launch_carry_scatter(fc, masks, offsets, bsums, out_queue, counters + 1, in_queue, n, walk_cur, walk_next, fe,
+                             stream, dev_n, mode, STEP_IDLE, sc != nullptr);
+    } else {
+        launch_mask_scan(masks, nwords, offsets, bsums, out_queue, counters + 1, nullptr, stream, dev_n, mode);
+        hipLaunchKernelGGL(scatter_queue_kernel, dim3(sc ? std::min<uint32_t>(4096u, grid_for(n)) : grid_for(n)),
+                           dim3(BLOCK), 0, stream, masks, offsets, bsums, counters + 1, in_queue, 0, (int32_t)n,
+                           out_queue, fe, dev_n, mode, STEP_IDLE);
+    }
     CHR_HIP_CHECK(hipGetLastError());
     return CHR_OK;
 }
@@ -4071,8 +4176,8 @@ static int prop_bufs(uint32_t nphotons, int32_t ntpb, int32_t max_blocks, int ct
     // split path: ray records, queue order + walk order (FlatCtx::rays / rays_walk)
     // + the walk-order carry: two walk orders, survivor masks in walk order and their scan
     const size_t cwords = ((size_t)nphotons + 63) / 64;
-    const size_t rbytes = b.fused ? (size_t)nphotons * 64 + 512 + (size_t)nphotons * 8 + cwords * 12 +
-                                        (size_t)scan_blocks((uint32_t)cwords) * 4 + 1024
+    const size_t rbytes = b.fused ? (size_t)nphotons * 64 + 512 + (size_t)nphotons * 13 + cwords * 12 +
+                                        (size_t)scan_blocks((uint32_t)cwords) * 4 + 2048
                                   : 0;
     const size_t base_bytes = 2 * qbytes + swords * 4 + 64 + hbytes + rbytes;
     const size_t mbytes = tail_masks ? ((size_t)nphotons + 63) / 64 * 8 + 512 : 0;
@@ -4097,6 +4202,8 @@ static int prop_bufs(uint32_t nphotons, int32_t ntpb, int32_t max_blocks, int ct
         b.fc.wmasks = (unsigned long long *)(((uintptr_t)(b.fc.walk[1] + nphotons) + 255) & ~(uintptr_t)255);
         b.fc.woffsets = (uint32_t *)(b.fc.wmasks + cwords);
         b.fc.wprefix = b.fc.woffsets + cwords;
+        b.fc.winv = (uint32_t *)(((uintptr_t)(b.fc.wprefix + scan_blocks((uint32_t)cwords)) + 255) & ~(uintptr_t)255);
+        b.fc.walive = (uint8_t *)(((uintptr_t)(b.fc.winv + nphotons) + 255) & ~(uintptr_t)255);   // + 64 B read slack
     }
     return CHR_OK;
 }
