@@ -644,6 +644,9 @@ def parse_args(argv=None):
                     help='one synchronous propagate per step (no tail / next-batch overlap)')
     ap.add_argument('--pipeline-depth', type=int, default=32,
                     help='steps per pipelined call (each holds its own copy of the batch in HBM)')
+    ap.add_argument('--timing-steps', type=int, default=5,
+                    help='untimed pipelined steps with every per-slot timing event recorded, after the timed '
+                         'steps (detail.slot_timing_pass, detail.kernel_ms_per_step; 0: skip)')
     ap.add_argument('--sequential-steps', type=int, default=5,
                     help='after the pipelined headline: this many one-call-per-step steps, timed the same way '
                          '(detail.sequential; 0: skip)')
@@ -735,6 +738,28 @@ def run_rank(args):
                'ms_per_step': 1e3 * s_el / args.sequential_steps,
                'path': 'one GPUPhotons.propagate call per step (the reference caller\'s loop)'}
     wl.reduced.pop('gp', None)
+    # per-slot timing events (kernel time per step, tail launch times) cost ~0.6% of the
+    # step when recorded (CHR_SLOT_TIMING): the timed steps record only the
+    # trace launches' pair (the roofline's launch times); a short untimed pass with every
+    # slot's events reports the rest
+    timing_pass = None
+    tsteps = min(args.timing_steps, len(getattr(wl, 'pool', [])) or args.timing_steps)
+    if tsteps > 0:
+        prev = os.environ.get('CHR_SLOT_TIMING')
+        os.environ['CHR_SLOT_TIMING'] = '1'
+        t_el, _, t_stats = timed_loop(wl.run, tsteps, 0, dist, wl.sync, min(wl.group, tsteps))
+        t_rep = wl.rank_report(t_stats)
+        wl.reduced.pop('gp', None)
+        if prev is None:
+            del os.environ['CHR_SLOT_TIMING']
+        else:
+            os.environ['CHR_SLOT_TIMING'] = prev
+        timing_pass = {'steps': tsteps, 'ms_per_step': 1e3 * t_el / tsteps,
+                       'kernel_ms_per_step': t_rep['kernel_ms'] / tsteps,
+                       'trace_ms_per_step': t_rep['trace_ms'] / tsteps,
+                       'tail_ms': [t['ms'] for t in t_rep['tail']],
+                       'note': 'untimed pass after the timed steps with every slot event recorded '
+                               '(CHR_SLOT_TIMING=1); the timed steps record only the trace launch pairs'}
     extra = wl.untimed_passes()
 
     # oracle checks: ranks > 0 check a sample of their own shard first (small,
@@ -760,7 +785,7 @@ def run_rank(args):
                   'ranks_seen': len(reports), 'ranks': [{k: rep[k] for k in ('rank', 'local_rank', 'host', 'device',
                                                                              'photons_per_step')}
                                                         for rep in reports],
-                  'kernel_ms_per_step': r0['kernel_ms'] / steps,
+                  'kernel_ms_per_step': (timing_pass['kernel_ms_per_step'] if timing_pass else r0['kernel_ms'] / steps),
                   'trace_ms_per_step': r0['trace_ms'] / steps,
                   'launches_per_step': r0['launches'] / steps,
                   'host_steps_per_propagate': r0['host_steps'] / steps,
@@ -773,7 +798,7 @@ def run_rank(args):
                                                      zip(r0['launch_rays'], r0['launch_ms'][:len(r0['launch_rays'])])],
                   'detected_fraction': r0['detected_last_step'] / max(1, nphotons),
                   'channel_hits_all_ranks': r0['channel_hits_all_ranks'],
-                  'sequential': seq}
+                  'sequential': seq, 'slot_timing_pass': timing_pass}
         detail.update(wl.device_info())
         detail.update(extra)
         result = result_line(args, world, elapsed, per_step, total_photons, wl.detector_info(), detail)

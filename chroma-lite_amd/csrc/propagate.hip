@@ -3744,6 +3744,20 @@ static int flat_get(uint32_t n, FlatCtx &fc, int ctx = 0) {
 }
 
 static bool trace_steps();
+// CHR_SLOT_TIMING: which per-slot timing events a device-driven propagate
+// records.  Each hipEventRecord between two dependent dispatches of a step's
+// chain adds a gap (r03 ab15, 29k bench: all 449.9, trace pair only 452.6,
+// none 454.7 M/s).  Default "trace": only the pair around each trace launch
+// (the stats' trace_ms / trace_launch_ms, which the bench's roofline uses);
+// "1" every slot's events as well (kernel_ms, tail_ms, the prefix split);
+// "0" only the events the streams and the host synchronise on.  Times not
+// recorded read 0 in chr_propagate_stats.
+static int slot_timing() {
+    const char *e = getenv("CHR_SLOT_TIMING");
+    if (!e || e[0] == 't') return 1;
+    if (e[0] == '0') return 0;
+    return 2;
+}
 // CHR_WALK_CARRY=1: later steps walk their rays in the previous step's walk
 // order (the binned first step's, restricted to survivors) instead of queue
 // order (walk_masks_kernel / scatter_walk_kernel; A/B, read per launch)
@@ -4270,19 +4284,21 @@ static int device_slots(const chr_geometry *g, const chr_photons *ph, uint32_t n
         SlotCtl sc{ctl + 2 * (size_t)k, ctl + 2 * (size_t)k + 1, done, nphotons, max_steps - k, tail_below};
         sc.tail_stream = run.tstream;
         sc.tail_masks = b.tail_masks;
-        sc.evt_tail0 = ev[5];
-        sc.evt_tail1 = ev[6];
+        const int timing = slot_timing();
+        sc.evt_tail0 = timing == 2 ? ev[5] : nullptr;
+        sc.evt_tail1 = timing == 2 ? ev[6] : nullptr;
         sc.rng_ready = k == 0 ? run.rng_ready : nullptr;
         sc.ctx = run.ctx;
         sc.host_ring = ring + 2 * (k % 32);   // written by the slot's head kernel (slot 0 of a batch: its prefix's)
         if (k == 0 && run.prefix_done) {
             sc.phase = PHASE_REST;
             sc.prefix_done = run.prefix_done;
-            sc.ev_rest0 = ev[7];
+            sc.ev_rest0 = timing == 2 ? ev[7] : nullptr;
         }
         bool split = false;
         rc = launch_step(g, ph, rng, nslots, (uint32_t)b.cap, n_ub, b.q[cur] + 1, b.q[cur ^ 1], 1, use_weights,
-                         scatter_first, b.scratch, stream, ev[0], ev[1], b.hits, b.sort_space, k == 0, ev[2], ev[3],
+                         scatter_first, b.scratch, stream, timing == 2 ? ev[0] : nullptr, ev[1], b.hits, b.sort_space,
+                         k == 0, timing ? ev[2] : nullptr, timing ? ev[3] : nullptr,
                          &split, &b.fc, &sc);
         if (rc) return rc;
         if (run.on_length)   // the output queue's count header (+1)
@@ -4309,10 +4325,29 @@ static int device_slots(const chr_geometry *g, const chr_photons *ph, uint32_t n
 // per slot); prefixed: slot 0 ran as prefix + rest (chr_propagate_batches)
 static int slot_stats(chr_propagate_stats &st, const uint32_t *h, int k, const std::vector<hipEvent_t> &events,
                       bool tail_stream, bool prefixed = false) {
+    const int timing = slot_timing();
     for (int j = 0; j < k; ++j) {
         const uint32_t m = h[2 * j], nj = h[2 * j + 1];
         const hipEvent_t *ev = events.data() + SLOT_EVENTS * (size_t)j;
         float ms = 0.0f;
+        if (timing < 2) {   // (CHR_SLOT_TIMING) counts only, and the trace launches' times
+            if (m == STEP_IDLE) continue;
+            st.launches++;
+            st.steps_run++;
+            if (m == STEP_ONE) {
+                if (timing == 1) CHR_HIP_CHECK(hipEventElapsedTime(&ms, ev[2], ev[3]));
+                st.trace_ms += ms;
+                if (st.trace_ms_n < CHR_TRACE_MS_MAX) {
+                    st.trace_launch_rays[st.trace_ms_n] = nj;
+                    st.trace_launch_ms[st.trace_ms_n++] = ms;
+                }
+                st.trace_launches++;
+                st.trace_rays += nj;
+            } else {
+                st.tail_photons += nj;
+            }
+            continue;
+        }
         if (j == 0 && prefixed) {   // the prefix on its stream (binning, walk), the rest after it on the batch stream
             float ms2 = 0.0f, ms3 = 0.0f;
             CHR_HIP_CHECK(hipEventElapsedTime(&ms, ev[0], ev[8]));
@@ -4676,9 +4711,11 @@ static int queue_prefix(const chr_geometry *g, const chr_photons *ph, uint32_t n
     sc.prefix_done = prefix_done;
     sc.host_ring = b.pinned + 64;   // ring entry 0 (device_slots' slot 0): this head is slot 0's
     hipEvent_t *ev = events.data();
-    sc.ev_bin_end = ev[8];
+    const int timing = slot_timing();
+    sc.ev_bin_end = timing == 2 ? ev[8] : nullptr;
     return launch_step(g, ph, rng, nslots, (uint32_t)b.cap, nphotons, b.q[0] + 1, b.q[1], 1, use_weights,
-                       scatter_first, b.scratch, ps, ev[0], ev[1], b.hits, b.sort_space, true, ev[2], ev[3], nullptr,
+                       scatter_first, b.scratch, ps, timing == 2 ? ev[0] : nullptr, ev[1], b.hits, b.sort_space, true,
+                       timing ? ev[2] : nullptr, timing ? ev[3] : nullptr, nullptr,
                        &b.fc, &sc);
 }
 

@@ -158,7 +158,8 @@ typedef struct chr_propagate_stats {
     uint32_t launches;          /* chunk launches */
     uint32_t final_alive;       /* photons still in the queue at exit */
     uint32_t stack_overflows;   /* traversals that exceeded the 1000-entry stack */
-    double kernel_ms;           /* summed device time of the propagate kernels (HIP events) */
+    double kernel_ms;           /* summed device time of the propagate kernels (HIP events; device-driven
+                                   propagates record them only with CHR_SLOT_TIMING=1, else 0) */
     uint64_t nodes_visited;     /* BVH nodes / triangles / walks: filled only by the counting */
     uint64_t triangles_tested;  /* kernel variant (CHR_PROPAGATE_VARIANT=5), zero otherwise */
     uint64_t traversals;
@@ -176,7 +177,7 @@ typedef struct chr_propagate_stats {
                                      slab test then skips that axis): split into sub-walks by trace_kernel */
     uint32_t flat_walks_whole;    /* such walks done whole by the multi-step (tail) kernel */
     uint32_t tail_photons;        /* photons handed to the multi-step (tail) launch (nsteps policy) */
-    double tail_ms;               /* device time of that launch (HIP events) */
+    double tail_ms;               /* device time of that launch (HIP events; CHR_SLOT_TIMING=1, else 0) */
     uint32_t tail_max_steps;      /* most steps one photon ran in the tail launch */
     uint32_t tail_slowest_steps;  /* steps of the photon that took longest in the tail launch */
     uint64_t tail_max_cycles;     /* that photon's time in ticks of the 100 MHz s_memrealtime clock */

@@ -74,7 +74,8 @@ def main():
                 'ms_per_step': 1e3 * elapsed / args.steps,
                 'trace_ms_per_step': rep['trace_ms'] / args.steps,
                 'kernel_ms_per_step': rep['kernel_ms'] / args.steps,
-                'tail_ms_mean': sum(t['ms'] for t in rep['tail']) / max(1, len(rep['tail'])),
+                # tail launch times need CHR_SLOT_TIMING=1; otherwise the slowest photon's time
+                'tail_ms_mean': sum(t['ms'] or t['slowest_photon_ms'] for t in rep['tail']) / max(1, len(rep['tail'])),
                 'long_us_per_step': [t['long_us_per_step'] for t in tails],
                 'long_walk_us_per_step': [t['long_walk_us_per_step'] for t in tails],
                 'first_trace_launches_ms': [round(x, 3) for x in rep['launch_ms'][:10]],
