@@ -72,6 +72,12 @@ struct DevGeom {
     float wl_start, wl_step;
     uint32_t t_n;
     float t_start, t_step;
+    // the physics tables as one allocation, [tables | materials | surfaces]: tables ==
+    // phys, materials == phys + mat_off, surfaces == phys + surf_off (words), phys_words
+    // in all -- small enough on the usual detectors (demo: 25 KB) for the shade and
+    // tail kernels to keep a copy in LDS (chr::PhysCache)
+    const uint32_t *phys;
+    uint32_t phys_words, mat_off, surf_off;
 };
 
 }  // namespace chr

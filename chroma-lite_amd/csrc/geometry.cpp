@@ -288,12 +288,27 @@ extern "C" int chr_geometry_create(const chr_geometry_desc *d, chr_geometry **ou
                 o.angular_reflect_diffuse = blob.add(s.angular_reflect_diffuse, s.angular_nangles);
             }
         }
-        if ((rc = dev_upload(g, blob.data.data(), blob.data.size() * 4, &p))) throw rc;
-        dg.tables = (const float *)p;
-        if ((rc = dev_upload(g, mats.data(), mats.size() * sizeof(chr::DevMaterial), &p))) throw rc;
-        dg.materials = (const chr::DevMaterial *)p;
-        if ((rc = dev_upload(g, surfs.data(), surfs.size() * sizeof(chr::DevSurface), &p))) throw rc;
-        dg.surfaces = (const chr::DevSurface *)p;
+        {   // one allocation [tables | materials | surfaces], 16-byte aligned parts (DevGeom::phys)
+            std::vector<uint32_t> phys(blob.data.size());
+            std::memcpy(phys.data(), blob.data.data(), blob.data.size() * 4);
+            phys.resize((phys.size() + 3) & ~(size_t)3, 0u);
+            const uint32_t mat_off = (uint32_t)phys.size();
+            phys.resize(phys.size() + mats.size() * sizeof(chr::DevMaterial) / 4);
+            std::memcpy(phys.data() + mat_off, mats.data(), mats.size() * sizeof(chr::DevMaterial));
+            phys.resize((phys.size() + 3) & ~(size_t)3, 0u);
+            const uint32_t surf_off = (uint32_t)phys.size();
+            phys.resize(phys.size() + surfs.size() * sizeof(chr::DevSurface) / 4);
+            std::memcpy(phys.data() + surf_off, surfs.data(), surfs.size() * sizeof(chr::DevSurface));
+            phys.resize((phys.size() + 3) & ~(size_t)3, 0u);
+            if ((rc = dev_upload(g, phys.data(), phys.size() * 4, &p))) throw rc;
+            dg.phys = (const uint32_t *)p;
+            dg.phys_words = (uint32_t)phys.size();
+            dg.mat_off = mat_off;
+            dg.surf_off = surf_off;
+            dg.tables = (const float *)p;
+            dg.materials = (const chr::DevMaterial *)(dg.phys + mat_off);
+            dg.surfaces = (const chr::DevSurface *)(dg.phys + surf_off);
+        }
         if (d->nwireplanes) {
             if ((rc = dev_upload(g, d->wireplanes, (size_t)d->nwireplanes * sizeof(chr_wireplane_desc), &p))) throw rc;
             dg.wireplanes = (const chr_wireplane_desc *)p;

@@ -111,14 +111,19 @@ __device__ __forceinline__ void node_bounds(const DevGeom &g, uint4 n, V3 &lo, V
             __builtin_fmaf((float)(n.z >> 16), g.scale, g.oz));
 }
 
+// a table word: from LDS when the tables were copied there (phys_cache), else a global load
+__device__ __forceinline__ float tab(const float *p) {
+    return __builtin_amdgcn_is_shared((const __attribute__((address_space(0))) void *)p) ? *(const CHR_LDS float *)p
+                                                                                         : gld(p);
+}
 __device__ __forceinline__ float interp_property(const DevGeom &g, float x, const float *fp) {
     const float start = g.wl_start, step = g.wl_step;
     const int n = (int)g.wl_n;
-    if (x < start) return gld(fp);
-    if (x > __builtin_fmaf((float)(n - 1), step, start)) return gld(fp + n - 1);
+    if (x < start) return tab(fp);
+    if (x > __builtin_fmaf((float)(n - 1), step, start)) return tab(fp + n - 1);
     const int jl = (int)((x - start) / step);
     const float base = __builtin_fmaf((float)jl, step, start);
-    const float f0 = gld(fp + jl), f1 = gld(fp + jl + 1);
+    const float f0 = tab(fp + jl), f1 = tab(fp + jl + 1);
     return f0 + ((x - base) * (f1 - f0)) / step;
 }
 
@@ -1536,6 +1541,7 @@ struct PropagateArgs {
     // shade kernel, walk-order carry (nullptr: off): walive[winv[q]] = survival of queue position q
     const uint32_t *winv;
     uint8_t *walive;
+    uint32_t phys_lds;                 // shade / tail kernels: keep the physics tables in LDS (phys_cache)
 };
 // modes of a device-driven step slot (step_head_kernel)
 constexpr uint32_t STEP_IDLE = 0, STEP_ONE = 1, STEP_TAIL = 2;
@@ -1739,6 +1745,28 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_step_kernel(const DevGe
 // 64 queue positions.  A slot's photons (queue positions slot, slot + cap, ...)
 // share only the RNG state, so the next photon's queue entry, state and walk
 // result are loaded while the current one's physics runs.
+// LDS copy of the physics tables (DevGeom::phys: property tables, material and
+// surface records) for the kernels that run the step physics: fill_state's and
+// the surface models' table reads then cost an LDS round trip instead of a
+// dependent L2 one.  All threads of the workgroup call it; returns the geometry
+// to use -- tables / materials / surfaces pointing into LDS when they fit in
+// cap_words, else g unchanged.
+constexpr uint32_t SHADE_PHYS_WORDS = 12288;   // 48 KB: 3 workgroups of shade_kernel<3> per CU
+constexpr uint32_t TAIL_PHYS_WORDS = 8192;     // 32 KB: 2 tail workgroups (+ 40 KB of walk stacks each)
+__device__ __forceinline__ DevGeom phys_cache(const DevGeom &g, uint4 *lds, uint32_t cap_words) {
+    DevGeom gl = g;
+    if (g.phys && g.phys_words <= cap_words) {   // workgroup-uniform
+        const uint4 *src = reinterpret_cast<const uint4 *>(g.phys);
+        for (uint32_t i = threadIdx.x; i < g.phys_words / 4u; i += BLOCK) lds[i] = src[i];
+        __syncthreads();
+        const uint32_t *base = reinterpret_cast<const uint32_t *>(lds);
+        gl.tables = reinterpret_cast<const float *>(base);
+        gl.materials = reinterpret_cast<const DevMaterial *>(base + g.mat_off);
+        gl.surfaces = reinterpret_cast<const DevSurface *>(base + g.surf_off);
+    }
+    return gl;
+}
+
 struct QueuedPhoton {
     uint32_t pid, history, walk;
     V3 pos, dir, pol;
@@ -1763,11 +1791,12 @@ template <int MINW>
 __global__ __launch_bounds__(BLOCK, MINW) void shade_kernel(const DevGeom *__restrict__ gdev, PropagateArgs a,
                                                             uint32_t cap) {
     if (a.mode && *a.mode != a.want) return;
+    __shared__ uint4 phys_lds[SHADE_PHYS_WORDS / 4];
+    const DevGeom g = phys_cache(*gdev, phys_lds, a.phys_lds ? SHADE_PHYS_WORDS : 0u);
     const uint32_t slot = blockIdx.x * BLOCK + threadIdx.x;
     const uint32_t n = a.dev_n ? *a.dev_n - 1u : (uint32_t)a.nthreads;
     if (slot == 0 && a.zero_word) *a.zero_word = 0u;
     if (slot >= cap || (slot & ~63u) >= n) return;   // whole waves (cap % 64 == 0)
-    const DevGeom &g = *gdev;
     chr_xorwow rng;
     bool have_rng = false;
     enum { P_FILL, P_PHYS, P_OTHER };
@@ -2181,6 +2210,8 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_tail_kernel(const DevGe
     // a tail overlapped by the next batch (chr_propagate_batches) is the critical
     // path: its waves win the SIMD's issue arbitration over that batch's walk
     if (a.prio & 1u) __builtin_amdgcn_s_setprio(3);
+    __shared__ uint4 phys_lds[TAIL_PHYS_WORDS / 4];
+    const DevGeom g = phys_cache(*gdev, phys_lds, a.phys_lds ? TAIL_PHYS_WORDS : 0u);
     const uint32_t slot = tid / 8, sub = tid & 7u;
     const uint32_t n = a.dev_n ? *a.dev_n - 1u : (uint32_t)a.nthreads;
     const uint32_t nslot = cap < n ? cap : n;
@@ -2196,7 +2227,6 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_tail_kernel(const DevGe
     };
     CHR_LDS uint32_t *wstack = (CHR_LDS uint32_t *)stacks + (threadIdx.x >> 6) * 8 * TAIL_STACK * 2;
     CHR_LDS uint32_t *wtris = (CHR_LDS uint32_t *)tris + (threadIdx.x >> 6) * 2 * TAIL_TRI;
-    const DevGeom &g = *gdev;
     chr_xorwow rng;
     bool have_rng = false;
     uint32_t overflow = 0, flat = 0;
@@ -3497,6 +3527,13 @@ static int tail_waves() {              // CHR_TAIL_WAVES=4: the tail kernel at 4
     const char *e = getenv("CHR_TAIL_WAVES");
     return e ? atoi(e) : kTailWaves;
 }
+// The shade and tail kernels copy the physics tables into LDS (phys_cache): r03
+// ab16, 29k bench, 450.7 -> 461.7 M/s, mean tail 6.36 -> 6.06 ms.  CHR_PHYS_LDS=0:
+// the tables read from global memory (A/B).
+static bool phys_lds_enabled() {
+    const char *e = getenv("CHR_PHYS_LDS");
+    return !(e && e[0] == '0');
+}
 static int shade_waves() {             // CHR_SHADE_WAVES=2|4: the shade kernel at 2 / 4 waves per SIMD (A/B)
     const char *e = getenv("CHR_SHADE_WAVES");
     return e ? atoi(e) : 3;
@@ -3655,6 +3692,7 @@ static int launch_chunk(const chr_geometry *g, const chr_photons *ph, uint32_t *
     a.work = nullptr;
     a.winv = nullptr;
     a.walive = nullptr;
+    a.phys_lds = phys_lds_enabled() ? 1u : 0u;
     a.prio = 0;
     if (sort_enabled() && nthreads >= kSortMin) {
         // coherence order (sort_key_kernel): rays that start close together in
@@ -3878,6 +3916,7 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
     a.work = nullptr;
     a.winv = nullptr;
     a.walive = nullptr;
+    a.phys_lds = phys_lds_enabled() ? 1u : 0u;
     a.prio = 0;
     FlatEnrol fe{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
     // walk-order carry: this step's walk order (nullptr: queue order) and the next step's
