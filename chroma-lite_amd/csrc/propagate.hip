@@ -2952,12 +2952,45 @@ __global__ __launch_bounds__(SCAN_WORDS) void mask_block_scan_kernel(const unsig
     if (threadIdx.x == SCAN_WORDS - 1) block_sums[blockIdx.x] = before + x;
 }
 
+// The head of a device-driven step slot (step_head_kernel, or folded into the
+// previous slot's scan_block_sums_kernel): the queue length n picks the slot's
+// mode -- the nsteps policy of photon.py:261-264 (one-step launch; the multi-step
+// tail below `tail_below` photons or with use_weights, when more than one step
+// remains; nothing once the queue is empty or the tail ran) -- and resets the
+// trace ray counter.  Returns the mode.
+struct HeadNext {                      // the next slot's head words (mode == nullptr: no fold)
+    uint32_t *mode, *n_out, *done, *ray_counter, *host_ring;
+    uint32_t tail_below, max_n;
+    int32_t remaining, use_weights;
+};
+__device__ __forceinline__ uint32_t slot_head(uint32_t n, const HeadNext &h) {
+    uint32_t m = STEP_IDLE;
+    if (!h.done[0]) {
+        if (n == 0 || n > h.max_n) h.done[0] = 1u;   // empty (or a corrupt header: run nothing)
+        else if ((n < h.tail_below || h.use_weights) && h.remaining > 1) { m = STEP_TAIL; h.done[0] = 1u; }
+        else m = STEP_ONE;
+    }
+    h.mode[0] = m;
+    h.n_out[0] = n;
+    // the host's copy of (mode, length), in pinned host memory: read once the
+    // slot's end event has completed (no copy dispatch per slot)
+    if (h.host_ring) { h.host_ring[0] = m; h.host_ring[1] = n; }
+    if (m != STEP_IDLE) h.ray_counter[0] = 0u;
+    return m;
+}
+
+// fresh: the output queue starts empty (device-driven slots: base 1, header 1 + total,
+// no reset of the header needed); hn: the next slot's head, folded in (one dispatch
+// fewer per slot) -- run even when this slot's scan is skipped (its mode then IDLE)
 __global__ __launch_bounds__(1024) void scan_block_sums_kernel(uint32_t *block_sums, uint32_t nblocks,
                                                                uint32_t *out_counter, uint32_t *base,
                                                                uint32_t *total_out, const uint32_t *mode,
-                                                               uint32_t skip) {
+                                                               uint32_t skip, uint32_t fresh, HeadNext hn) {
     __shared__ uint32_t partial[1024];
-    if (mode && (*mode == STEP_IDLE || *mode == skip)) return;
+    if (mode && (*mode == STEP_IDLE || *mode == skip)) {
+        if (hn.mode && threadIdx.x == 0) slot_head(0u, hn);
+        return;
+    }
     const uint32_t tid = threadIdx.x;
     const uint32_t per = (nblocks + 1023) / 1024;
     const uint32_t b0 = tid * per;
@@ -2979,9 +3012,15 @@ __global__ __launch_bounds__(1024) void scan_block_sums_kernel(uint32_t *block_s
     }
     if (tid == 1023) {
         const uint32_t total = partial[1023];
-        if (base) base[0] = out_counter ? out_counter[0] : 0u;
-        if (out_counter) out_counter[0] += total;
+        if (fresh) {
+            if (base) base[0] = 1u;
+            if (out_counter) out_counter[0] = 1u + total;
+        } else {
+            if (base) base[0] = out_counter ? out_counter[0] : 0u;
+            if (out_counter) out_counter[0] += total;
+        }
         if (total_out) total_out[0] = total;
+        if (hn.mode) slot_head(total, hn);   // the next slot's queue is this slot's survivors
     }
 }
 
@@ -3164,22 +3203,8 @@ __global__ void step_head_kernel(const uint32_t *in_hdr, uint32_t *out_hdr, uint
                                  uint32_t *done, uint32_t *ray_counter, uint32_t tail_below, int32_t remaining,
                                  int32_t use_weights, uint32_t max_n, uint32_t *host_ring) {
     if (threadIdx.x != 0) return;
-    const uint32_t n = in_hdr[0] - 1u;
-    uint32_t m = STEP_IDLE;
-    if (!done[0]) {
-        if (n == 0 || n > max_n) done[0] = 1u;   // empty (or a corrupt header: run nothing)
-        else if ((n < tail_below || use_weights) && remaining > 1) { m = STEP_TAIL; done[0] = 1u; }
-        else m = STEP_ONE;
-    }
-    mode[0] = m;
-    n_out[0] = n;
-    // the host's copy of (mode, length), in pinned host memory: read once the
-    // slot's end event has completed (no copy dispatch per slot)
-    if (host_ring) { host_ring[0] = m; host_ring[1] = n; }
-    if (m != STEP_IDLE) {
-        out_hdr[0] = 1u;
-        ray_counter[0] = 0u;
-    }
+    const HeadNext h{mode, n_out, done, ray_counter, host_ring, tail_below, max_n, remaining, use_weights};
+    if (slot_head(in_hdr[0] - 1u, h) != STEP_IDLE) out_hdr[0] = 1u;
 }
 
 // alive-mask words of a tail slot (OR-ed by its kernel) zeroed, for the slot's queue length
@@ -3345,12 +3370,14 @@ inline uint32_t scan_blocks(uint32_t nwords) { return (nwords + SCAN_WORDS - 1) 
 // word_offsets (nwords) + block prefixes (scan_blocks(nwords)) of the masks
 void launch_mask_scan(const unsigned long long *masks, uint32_t nwords, uint32_t *word_offsets, uint32_t *block_sums,
                       uint32_t *out_counter, uint32_t *base, uint32_t *total_out, hipStream_t stream,
-                      const uint32_t *dev_n = nullptr, const uint32_t *mode = nullptr, uint32_t skip = STEP_IDLE) {
+                      const uint32_t *dev_n = nullptr, const uint32_t *mode = nullptr, uint32_t skip = STEP_IDLE,
+                      const HeadNext *hn = nullptr) {
     const uint32_t nb = scan_blocks(nwords);   // device-driven: nwords is an upper bound
     if (nb) hipLaunchKernelGGL(mask_block_scan_kernel, dim3(nb), dim3(SCAN_WORDS), 0, stream, masks, nwords, word_offsets,
                                block_sums, dev_n, mode, skip);
     hipLaunchKernelGGL(scan_block_sums_kernel, dim3(1), dim3(1024), 0, stream, block_sums, nb, out_counter, base,
-                       total_out, mode, skip);
+                       total_out, mode, skip, dev_n ? 1u : 0u,
+                       hn ? *hn : HeadNext{nullptr, nullptr, nullptr, nullptr, nullptr, 0u, 0u, 0, 0});
 }
 
 PhotonPtrs to_ptrs(const chr_photons *p) {
@@ -3790,6 +3817,12 @@ static bool trace_steps();
 // "1" every slot's events as well (kernel_ms, tail_ms, the prefix split);
 // "0" only the events the streams and the host synchronise on.  Times not
 // recorded read 0 in chr_propagate_stats.
+// CHR_HEAD_FOLD=0: every device-driven slot launches its own head kernel instead of
+// the previous slot's block-sum scan running it (A/B)
+static bool head_fold_enabled() {
+    const char *e = getenv("CHR_HEAD_FOLD");
+    return !(e && e[0] == '0');
+}
 static int slot_timing() {
     const char *e = getenv("CHR_SLOT_TIMING");
     if (!e || e[0] == 't') return 1;
@@ -3840,6 +3873,11 @@ struct SlotCtl {
     int phase = 0;
     int ctx = 0;                      // buffer context (walk-stack column)
     uint32_t *host_ring = nullptr;    // pinned (mode, length) words the head kernel writes (nullptr: none)
+    // the next slot's head folded into this slot's block-sum scan (fold_head: every slot
+    // after the first then launches no head kernel of its own); next_head.ray_counter is
+    // filled by launch_step
+    bool fold_head = false;
+    HeadNext next_head{nullptr, nullptr, nullptr, nullptr, nullptr, 0u, 0u, 0, 0};
     hipEvent_t prefix_done = nullptr, ev_rest0 = nullptr, ev_bin_end = nullptr;
 };
 constexpr int PHASE_ALL = 0, PHASE_PREFIX = 1, PHASE_REST = 2, PHASE_BIN = 3, PHASE_TRACE = 4;
@@ -3942,7 +3980,14 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
         CHR_HIP_CHECK(hipStreamWaitEvent(stream, sc->prefix_done, 0));
         if (sc->ev_rest0) CHR_HIP_CHECK(hipEventRecord(sc->ev_rest0, stream));
     }
-    if (sc && do_bin) {
+    // the next slot's head, folded into this slot's scan (SlotCtl::fold_head)
+    HeadNext hn{nullptr, nullptr, nullptr, nullptr, nullptr, 0u, 0u, 0, 0};
+    if (sc && sc->fold_head && sc->next_head.mode && next) {
+        hn = sc->next_head;
+        hn.ray_counter = next;
+    }
+    const HeadNext *hnp = hn.mode ? &hn : nullptr;
+    if (sc && do_bin && !(sc->fold_head && !first_step)) {
         if (!next) return chr::fail(CHR_ERR_INVALID, "launch_step: device-driven steps need the split path");
         hipLaunchKernelGGL(step_head_kernel, dim3(1), dim3(64), 0, stream, in_queue - 1, out_queue, sc->mode, sc->nk,
                            sc->done, next, sc->tail_below, sc->remaining, use_weights, sc->n_layout, sc->host_ring);
@@ -4072,7 +4117,7 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
                                  stream, dev_n, mode, STEP_TAIL, true);
         } else {
             launch_mask_scan(masks, nwords, offsets, bsums, out_queue, counters + 1, nullptr, stream, dev_n, mode,
-                             STEP_TAIL);
+                             STEP_TAIL, hnp);
             hipLaunchKernelGGL(scatter_queue_kernel, dim3(std::min<uint32_t>(4096u, grid_for(n))), dim3(BLOCK), 0,
                                stream, masks, offsets, bsums, counters + 1, in_queue, 0, (int32_t)n, out_queue, fe,
                                dev_n, mode, STEP_TAIL);
@@ -4098,7 +4143,8 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
         launch_carry_scatter(fc, masks, offsets, bsums, out_queue, counters + 1, in_queue, n, walk_cur, walk_next, fe,
                              stream, dev_n, mode, STEP_IDLE, sc != nullptr);
     } else {
-        launch_mask_scan(masks, nwords, offsets, bsums, out_queue, counters + 1, nullptr, stream, dev_n, mode);
+        launch_mask_scan(masks, nwords, offsets, bsums, out_queue, counters + 1, nullptr, stream, dev_n, mode, STEP_IDLE,
+                         hnp);
         hipLaunchKernelGGL(scatter_queue_kernel, dim3(sc ? std::min<uint32_t>(4096u, grid_for(n)) : grid_for(n)),
                            dim3(BLOCK), 0, stream, masks, offsets, bsums, counters + 1, in_queue, 0, (int32_t)n,
                            out_queue, fe, dev_n, mode, STEP_IDLE);
@@ -4313,6 +4359,9 @@ static int device_slots(const chr_geometry *g, const chr_photons *ph, uint32_t n
     if (!run.prefix_done) CHR_HIP_CHECK(hipMemsetAsync(done, 0, 4, stream));
     b.fc.enrol_next = true;
     uint32_t *ring = b.pinned + 64;   // (mode, n) of recent slots, 32 entries (written by each slot's head kernel)
+    // slot k + 1's head runs at the end of slot k's scan (no head dispatch per slot);
+    // not with the walk-order carry, whose scan is its own kernel
+    const bool fold = head_fold_enabled() && !walk_carry_enabled();
     std::vector<hipEvent_t> &events = *run.events;
     uint32_t n_ub = nphotons;
     int k = 0, cur = 0;
@@ -4329,6 +4378,10 @@ static int device_slots(const chr_geometry *g, const chr_photons *ph, uint32_t n
         sc.rng_ready = k == 0 ? run.rng_ready : nullptr;
         sc.ctx = run.ctx;
         sc.host_ring = ring + 2 * (k % 32);   // written by the slot's head kernel (slot 0 of a batch: its prefix's)
+        sc.fold_head = fold;
+        if (fold && k + 1 < max_steps)
+            sc.next_head = HeadNext{ctl + 2 * (size_t)(k + 1), ctl + 2 * (size_t)(k + 1) + 1, done, nullptr,
+                                    ring + 2 * ((k + 1) % 32), tail_below, nphotons, max_steps - k - 1, use_weights};
         if (k == 0 && run.prefix_done) {
             sc.phase = PHASE_REST;
             sc.prefix_done = run.prefix_done;
