@@ -4092,10 +4092,14 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
     }
     if (split_out) *split_out = split;
     if (tail && sc && sc->tail_stream) {   // the tail on its own stream (chr_propagate_batches)
-        if (!ev1) return chr::fail(CHR_ERR_INVALID, "launch_step: a tail stream needs the slot's end event");
+        // the tail kernel needs the slot's head (its mode) and the previous slot's scatter (its
+        // queue): both come before the slot's trace-start event; with every slot event
+        // recorded (CHR_SLOT_TIMING=1) it waits for the slot's one-step part as before
+        hipEvent_t dep = ev1 ? ev1 : evt0;
+        if (!dep) return chr::fail(CHR_ERR_INVALID, "launch_step: a tail stream needs a slot event");
         hipStream_t ts = sc->tail_stream;
-        CHR_HIP_CHECK(hipEventRecord(ev1, stream));
-        CHR_HIP_CHECK(hipStreamWaitEvent(ts, ev1, 0));
+        if (ev1) CHR_HIP_CHECK(hipEventRecord(ev1, stream));
+        CHR_HIP_CHECK(hipStreamWaitEvent(ts, dep, 0));
         if (sc->evt_tail0) CHR_HIP_CHECK(hipEventRecord(sc->evt_tail0, ts));
         // few workgroups (grid-stride): a tail holds < nthreads_per_block * 128 photons
         // unless use_weights, and this launch waits for free CU slots beside the
@@ -4388,19 +4392,21 @@ static int device_slots(const chr_geometry *g, const chr_photons *ph, uint32_t n
             sc.ev_rest0 = timing == 2 ? ev[7] : nullptr;
         }
         bool split = false;
+        // ev[2] (before the slot's trace) is always recorded: the host's and the tail
+        // stream's sync point for the slot (its head has run); the end-of-slot event ev[4]
+        // only with every slot event (CHR_SLOT_TIMING=1), else once after the last slot
         rc = launch_step(g, ph, rng, nslots, (uint32_t)b.cap, n_ub, b.q[cur] + 1, b.q[cur ^ 1], 1, use_weights,
-                         scatter_first, b.scratch, stream, timing == 2 ? ev[0] : nullptr, ev[1], b.hits, b.sort_space,
-                         k == 0, timing ? ev[2] : nullptr, timing ? ev[3] : nullptr,
-                         &split, &b.fc, &sc);
+                         scatter_first, b.scratch, stream, timing == 2 ? ev[0] : nullptr, timing == 2 ? ev[1] : nullptr,
+                         b.hits, b.sort_space, k == 0, ev[2], timing ? ev[3] : nullptr, &split, &b.fc, &sc);
         if (rc) return rc;
         if (run.on_length)   // the output queue's count header (+1)
             CHR_HIP_CHECK(hipMemcpyAsync(run.out_ring + k % 32, b.q[cur ^ 1], 4, hipMemcpyDeviceToHost, stream));
-        CHR_HIP_CHECK(hipEventRecord(ev[4], stream));
+        if (timing == 2) CHR_HIP_CHECK(hipEventRecord(ev[4], stream));
         b.fc.cur ^= 1;   // the step's scatter enrolled the next step's flat walks in the other list
         cur ^= 1;
         scatter_first = 0;
-        if (k >= 1) {   // slot k - 1 finished before slot k started: is there a slot k + 1?
-            CHR_HIP_CHECK(hipEventSynchronize(events[SLOT_EVENTS * (size_t)(k - 1) + 4]));
+        if (k >= 1) {   // slot k - 1's head has run (its mode is known): is there a slot k + 1?
+            CHR_HIP_CHECK(hipEventSynchronize(events[SLOT_EVENTS * (size_t)(k - 1) + (timing == 2 ? 4 : 2)]));
             const uint32_t m = ring[2 * ((k - 1) % 32)], nk = ring[2 * ((k - 1) % 32) + 1];
             if (m != STEP_ONE) stop = true;   // the tail ran or the queue emptied: slot k is idle
             else n_ub = nk;                   // later queues are no longer
@@ -4408,6 +4414,8 @@ static int device_slots(const chr_geometry *g, const chr_photons *ph, uint32_t n
         }
         k++;
     }
+    if (k > 0 && slot_timing() != 2)   // the end of the last slot (the batch's read-back waits for it)
+        CHR_HIP_CHECK(hipEventRecord(events[SLOT_EVENTS * (size_t)(k - 1) + 4], stream));
     *ctl_out = ctl;
     *k_out = k;
     return CHR_OK;
@@ -4807,7 +4815,7 @@ static int queue_prefix(const chr_geometry *g, const chr_photons *ph, uint32_t n
     sc.ev_bin_end = timing == 2 ? ev[8] : nullptr;
     return launch_step(g, ph, rng, nslots, (uint32_t)b.cap, nphotons, b.q[0] + 1, b.q[1], 1, use_weights,
                        scatter_first, b.scratch, ps, timing == 2 ? ev[0] : nullptr, ev[1], b.hits, b.sort_space, true,
-                       timing ? ev[2] : nullptr, timing ? ev[3] : nullptr, nullptr,
+                       ev[2], timing ? ev[3] : nullptr, nullptr,
                        &b.fc, &sc);
 }
 
