@@ -160,22 +160,24 @@ extern "C" int chr_geometry_create(const chr_geometry_desc *d, chr_geometry **ou
             chr::WideBVH wb;
             if ((rc = chr::build_wide_bvh(d, wb))) throw rc;
             if (wb.usable && !std::getenv("CHR_EXACT_ORDER_ONLY")) {
-                // nodes padded to 128 bytes: one node = one cache line (a 96-byte
-                // node at a 96-byte stride straddles two lines half the time)
-                // (measured r01: no gain over the packed 96-byte stride, which is the default)
+                // nodes padded to 128 bytes: one node = one cache line (a 96-byte node at a
+                // 96-byte stride straddles two lines half the time).  r01: no gain over the
+                // packed stride; r03 ab21, where the later steps' walks are line-bound:
+                // 463.7 -> 467.1 M/s, so the padded slots are the default (the packed ones
+                // kept beside them with CHR_NODE_LAYOUT_AB, selected by CHR_NODE_LAYOUT=96)
                 const bool ab = std::getenv("CHR_NODE_LAYOUT_AB") != nullptr;
-                std::vector<uint8_t> padded(ab ? wb.nodes.size() * 128 : 0, 0);
-                for (size_t i = 0; ab && i < wb.nodes.size(); ++i)
+                std::vector<uint8_t> padded(wb.nodes.size() * 128, 0);
+                for (size_t i = 0; i < wb.nodes.size(); ++i)
                     std::memcpy(padded.data() + 128 * i, &wb.nodes[i], sizeof(chr::WideNode));
-                if ((rc = dev_upload(g, wb.nodes.data(), wb.nodes.size() * sizeof(chr::WideNode), &p))) throw rc;
+                if ((rc = dev_upload(g, padded.data(), std::max<size_t>(128, padded.size()), &p))) throw rc;
                 dg.wnodes = (const uint4 *)p;
-                dg.wstride = 6;
-                if (ab) {
-                    if ((rc = dev_upload(g, padded.data(), padded.size(), &p))) throw rc;
-                    g->wnodes_alt = (const uint4 *)p;
-                    g->wstride_alt = 8;
-                }
+                dg.wstride = 8;
                 std::vector<uint8_t>().swap(padded);
+                if (ab) {
+                    if ((rc = dev_upload(g, wb.nodes.data(), wb.nodes.size() * sizeof(chr::WideNode), &p))) throw rc;
+                    g->wnodes_alt = (const uint4 *)p;
+                    g->wstride_alt = 6;
+                }
                 if ((rc = dev_upload(g, wb.tri.data(), std::max<size_t>(1, wb.tri.size()) * sizeof(chr::WideTri), &p)))
                     throw rc;
                 dg.wtri = (const float4 *)p;

@@ -4203,7 +4203,7 @@ static int apply_node_layout(const chr_geometry *cg, hipStream_t stream) {
     chr_geometry *g = const_cast<chr_geometry *>(cg);
     if (!g->wnodes_alt) return CHR_OK;
     const char *e = getenv("CHR_NODE_LAYOUT");
-    const uint32_t want = (e && atoi(e) == 128) ? 8u : 6u;
+    const uint32_t want = (e && atoi(e) == 96) ? 6u : 8u;
     if (g->dev.wstride == want) return CHR_OK;
     std::swap(g->dev.wnodes, g->wnodes_alt);
     std::swap(g->dev.wstride, g->wstride_alt);
