@@ -78,6 +78,11 @@ struct DevGeom {
     // tail kernels to keep a copy in LDS (chr::PhysCache)
     const uint32_t *phys;
     uint32_t phys_words, mat_off, surf_off;
+    // [0, phys_hot_words): the tables and records the step physics reads on every step;
+    // after it the materials' component tables (bulk re-emission), read through tables_g
+    // (== tables in global memory; phys_cache points tables into LDS, tables_g stays)
+    uint32_t phys_hot_words;
+    const float *tables_g;
 };
 
 }  // namespace chr

@@ -227,7 +227,7 @@ extern "C" int chr_geometry_create(const chr_geometry_desc *d, chr_geometry **ou
         if ((rc = dev_upload(g, d->h_material_codes, (size_t)d->ntriangles * 4, &p))) throw rc;
         dg.material_codes = (const uint32_t *)p;
 
-        Blob blob;
+        Blob blob, comp;
         const uint32_t W1 = d->wavelength_n + 1, T1 = d->time_n + 1;
         std::vector<chr::DevMaterial> mats(d->nmaterials);
         for (uint32_t i = 0; i < d->nmaterials; ++i) {
@@ -241,14 +241,16 @@ extern "C" int chr_geometry_create(const chr_geometry_desc *d, chr_geometry **ou
             o.refractive_index = blob.add(m.refractive_index, W1);
             o.absorption_length = blob.add(m.absorption_length, W1);
             o.scattering_length = blob.add(m.scattering_length, W1);
-            o.comp_reemission_prob = (uint32_t)blob.data.size();
-            for (uint32_t c = 0; c < m.num_comp; ++c) blob.add(m.comp_reemission_prob + c * W1, W1);
-            o.comp_reemission_wvl_cdf = (uint32_t)blob.data.size();
-            for (uint32_t c = 0; c < m.num_comp; ++c) blob.add(m.comp_reemission_wvl_cdf + c * W1, W1);
-            o.comp_reemission_time_cdf = (uint32_t)blob.data.size();
-            for (uint32_t c = 0; c < m.num_comp; ++c) blob.add(m.comp_reemission_time_cdf + c * T1, T1);
-            o.comp_absorption_length = (uint32_t)blob.data.size();
-            for (uint32_t c = 0; c < m.num_comp; ++c) blob.add(m.comp_absorption_length + c * W1, W1);
+            // the components' tables (bulk re-emission, 20,000-entry time CDFs) go in a
+            // second blob after the records: the hot part before them fits in LDS
+            o.comp_reemission_prob = (uint32_t)comp.data.size();
+            for (uint32_t c = 0; c < m.num_comp; ++c) comp.add(m.comp_reemission_prob + c * W1, W1);
+            o.comp_reemission_wvl_cdf = (uint32_t)comp.data.size();
+            for (uint32_t c = 0; c < m.num_comp; ++c) comp.add(m.comp_reemission_wvl_cdf + c * W1, W1);
+            o.comp_reemission_time_cdf = (uint32_t)comp.data.size();
+            for (uint32_t c = 0; c < m.num_comp; ++c) comp.add(m.comp_reemission_time_cdf + c * T1, T1);
+            o.comp_absorption_length = (uint32_t)comp.data.size();
+            for (uint32_t c = 0; c < m.num_comp; ++c) comp.add(m.comp_absorption_length + c * W1, W1);
         }
         std::vector<chr::DevSurface> surfs(d->nsurfaces > 0 ? d->nsurfaces : 1);
         std::memset(surfs.data(), 0, surfs.size() * sizeof(chr::DevSurface));
@@ -302,12 +304,26 @@ extern "C" int chr_geometry_create(const chr_geometry_desc *d, chr_geometry **ou
             phys.resize(phys.size() + surfs.size() * sizeof(chr::DevSurface) / 4);
             std::memcpy(phys.data() + surf_off, surfs.data(), surfs.size() * sizeof(chr::DevSurface));
             phys.resize((phys.size() + 3) & ~(size_t)3, 0u);
+            const uint32_t hot = (uint32_t)phys.size();
+            // material component offsets: relative to the phys base, past the records
+            for (auto &m : mats) {
+                m.comp_reemission_prob += hot;
+                m.comp_reemission_wvl_cdf += hot;
+                m.comp_reemission_time_cdf += hot;
+                m.comp_absorption_length += hot;
+            }
+            std::memcpy(phys.data() + mat_off, mats.data(), mats.size() * sizeof(chr::DevMaterial));
+            phys.resize(phys.size() + comp.data.size());
+            std::memcpy(phys.data() + hot, comp.data.data(), comp.data.size() * 4);
+            phys.resize((phys.size() + 3) & ~(size_t)3, 0u);
             if ((rc = dev_upload(g, phys.data(), phys.size() * 4, &p))) throw rc;
             dg.phys = (const uint32_t *)p;
             dg.phys_words = (uint32_t)phys.size();
+            dg.phys_hot_words = hot;
             dg.mat_off = mat_off;
             dg.surf_off = surf_off;
             dg.tables = (const float *)p;
+            dg.tables_g = (const float *)p;
             dg.materials = (const chr::DevMaterial *)(dg.phys + mat_off);
             dg.surfaces = (const chr::DevSurface *)(dg.phys + surf_off);
         }

@@ -1159,16 +1159,16 @@ __device__ __forceinline__ int propagate_to_boundary(const DevGeom &g, Photon &p
             float prob = 0.0f;
             uint32_t comp;
             for (comp = 0;; comp++) {
-                const float comp_abs = interp_property(g, p.wavelength, g.tables + m.comp_absorption_length + comp * W1);
+                const float comp_abs = interp_property(g, p.wavelength, g.tables_g + m.comp_absorption_length + comp * W1);
                 prob += s.absorption_length / comp_abs;
                 if (usc < prob || comp + 1 == m.num_comp) break;
             }
             const float usr = chr_uniform01(&rng);
-            const float crp = interp_property(g, p.wavelength, g.tables + m.comp_reemission_prob + comp * W1);
+            const float crp = interp_property(g, p.wavelength, g.tables_g + m.comp_reemission_prob + comp * W1);
             if (usr < crp) {
                 p.wavelength = sample_cdf(rng, (int)g.wl_n, g.wl_start, g.wl_step,
-                                          g.tables + m.comp_reemission_wvl_cdf + comp * W1);
-                p.time += sample_cdf(rng, (int)g.t_n, g.t_start, g.t_step, g.tables + m.comp_reemission_time_cdf + comp * T1);
+                                          g.tables_g + m.comp_reemission_wvl_cdf + comp * W1);
+                p.time += sample_cdf(rng, (int)g.t_n, g.t_start, g.t_step, g.tables_g + m.comp_reemission_time_cdf + comp * T1);
                 p.dir = uniform_sphere(rng);
                 p.pol = cross(uniform_sphere(rng), p.dir);
                 p.pol = p.pol / norm(p.pol);
@@ -1752,12 +1752,14 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_step_kernel(const DevGe
 // to use -- tables / materials / surfaces pointing into LDS when they fit in
 // cap_words, else g unchanged.
 constexpr uint32_t SHADE_PHYS_WORDS = 12288;   // 48 KB: 3 workgroups of shade_kernel<3> per CU
+// (only DevGeom::phys_hot_words are copied: the materials' component tables stay in HBM)
 constexpr uint32_t TAIL_PHYS_WORDS = 8192;     // 32 KB: 2 tail workgroups (+ 40 KB of walk stacks each)
 __device__ __forceinline__ DevGeom phys_cache(const DevGeom &g, uint4 *lds, uint32_t cap_words) {
     DevGeom gl = g;
-    if (g.phys && g.phys_words <= cap_words) {   // workgroup-uniform
+    if (g.phys && g.phys_hot_words <= cap_words) {   // workgroup-uniform
+        // the hot part: tables and records; the component tables stay global (tables_g)
         const uint4 *src = reinterpret_cast<const uint4 *>(g.phys);
-        for (uint32_t i = threadIdx.x; i < g.phys_words / 4u; i += BLOCK) lds[i] = src[i];
+        for (uint32_t i = threadIdx.x; i < g.phys_hot_words / 4u; i += BLOCK) lds[i] = src[i];
         __syncthreads();
         const uint32_t *base = reinterpret_cast<const uint32_t *>(lds);
         gl.tables = reinterpret_cast<const float *>(base);
