@@ -2473,6 +2473,7 @@ struct TraceArgs {
     uint32_t *winv;              // walk-order carry: winv[queue position] = its walk position (nullptr: off)
     uint32_t drain_max;          // a wave drains its last <= drain_max walks whole-wave (0: never; at most 8)
     uint32_t claim_ahead;        // refills from claimed chunks, the next claim in flight (trace_claim_ahead)
+    uint32_t spread;             // launches with fewer rays than lanes: each wave claims its share (trace_spread)
 };
 constexpr uint32_t CLAIM = 64;   // ray-counter chunk of trace_kernel's claim-ahead refill
 
@@ -2596,6 +2597,14 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
     // next chunk's base, claimed ahead (valid in lane 0 once have_pend)
     uint32_t cb = 0, cn = 0, pend = 0;
     bool have_pend = false;
+    // claim size: CLAIM, or with spread a wave's share of a launch smaller than the
+    // grid's lanes (every wave then walks a few rays and reaches its drain sooner)
+    uint32_t claim = CLAIM;
+    if (a.spread) {
+        const uint32_t waves = gridDim.x * (BLOCK / 64);
+        const uint32_t share = (total + waves - 1u) / waves;
+        claim = share < 1u ? 1u : (share < CLAIM ? share : CLAIM);
+    }
     enum { P_NODE, P_TRI, P_REFILL, P_IDLE, P_DRAIN, P_BOX = 3 };   // regions (calls: P_REFILL = walks, P_BOX = boxes)
     Prof<5> pf;
     pf.start(P_REFILL);
@@ -2617,7 +2626,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
         if (!exhausted) {
             const unsigned long long need = __ballot(!has_ray);
             if (need != 0 && (__popcll(need) >= R || need == __ballot(1))) {
-                const uint32_t want = (uint32_t)__popcll(need);
+                const uint32_t want = (uint32_t)__popcll(need) < claim ? (uint32_t)__popcll(need) : claim;
                 const uint32_t rank = (uint32_t)__popcll(need & ((1ull << lane) - 1ull));
                 uint32_t j;
                 if (a.claim_ahead) {
@@ -2633,18 +2642,18 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
                     if (g0 < want) {   // this chunk is used up: the pending one, or a claim now
                         uint32_t nb = 0;
                         if (have_pend) nb = (uint32_t)__shfl((int)pend, 0);
-                        else if (lane == 0) nb = atomicAdd(a.next, CLAIM);
+                        else if (lane == 0) nb = atomicAdd(a.next, claim);
                         nb = have_pend ? nb : (uint32_t)__shfl((int)nb, 0);
                         have_pend = false;
                         b1 = nb;
-                        g1 = want - g0 < CLAIM ? want - g0 : CLAIM;
+                        g1 = want - g0 < claim ? want - g0 : claim;
                         cb = nb + g1;
-                        cn = CLAIM - g1;
+                        cn = claim - g1;
                     }
                     j = rank < g0 ? b0 + rank : b1 + (rank - g0);
                     if (cb >= total) exhausted = true;     // later claims lie beyond the last item
                     else if (!have_pend && cb + 2u * gridDim.x * BLOCK < total) {
-                        if (lane == 0) pend = atomicAdd(a.next, CLAIM);
+                        if (lane == 0) pend = atomicAdd(a.next, claim);
                         have_pend = true;
                     }
                 } else {
@@ -2655,7 +2664,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
                     if (base + want >= total) exhausted = true;
                     j = base + rank;
                 }
-                if (!has_ray) {
+                if (!has_ray && rank < want) {
                     bool start = false;
                     if (j < n && a.rays) {
                         // the ray record: one 32-B load (put_ray); skip bit: dead / NaN / flat
@@ -3631,6 +3640,15 @@ static constexpr uint32_t kBinFirstMin = 1u << 20;
 // claimed ahead (the next chunk's atomic in flight while the wave walks) instead
 // of one blocking atomic per refill.  Off: measured slower (r03 ab5: trace 17.63
 // -> 18.36 ms per step; the binned first launch 5.33 -> 5.60 ms).
+// A trace launch with fewer rays than the grid's lanes hands each wave its share
+// (ceil(rays / waves)) instead of 64 rays: the small late launches spread their
+// walks over every wave and reach the drain sooner.  r03 ab24/ab25 (same batches,
+// photons identical): trace 14.40 -> 14.32 ms per step, the last launches 0.39 -> 0.37
+// ms.  CHR_TRACE_SPREAD=0: 64 per wave (A/B).
+static bool trace_spread() {
+    const char *e = getenv("CHR_TRACE_SPREAD");
+    return !(e && e[0] == '0');
+}
 static bool trace_claim_ahead() {
     const char *e = getenv("CHR_TRACE_AHEAD");
     return e && e[0] == '1';
@@ -4025,6 +4043,7 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
         ta.mode = mode;
         ta.drain_max = trace_drain_max();
         ta.claim_ahead = trace_claim_ahead() ? 1u : 0u;
+        ta.spread = trace_spread() ? 1u : 0u;
         ta.winv = carry ? fc->winv : nullptr;
         a.winv = carry ? fc->winv : nullptr;
         a.walive = carry ? fc->walive : nullptr;
