@@ -104,6 +104,42 @@ __device__ __forceinline__ float4 gld(const float4 *p) {
 }
 
 // ---------------------------------------------------------------- geometry.h
+// The top of the wide BVH in LDS (north_star: "BVH nodes ... staged through
+// LDS").  The builder numbers nodes level by level (wide_bvh.cpp), so nodes
+// [0, TOP_NODES) are the root and the two levels below it of the 8-wide tree:
+// every walk starts there and re-enters them from its stack.  A workgroup copies
+// them once (96 B each: the node without its slot pad); a walk reads node i < n
+// from LDS, every other node from global memory.  Same bytes, same results.
+constexpr uint32_t TOP_NODES = 73;   // 1 + 8 + 64: 7,008 B
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));   // (HIP's uint4 has no LDS assignment)
+struct TopNodes {
+    const CHR_LDS u32x4 *p;          // 6 x 16 B per node
+    uint32_t n;                      // nodes held (0: none)
+};
+template <int TB>
+__device__ __forceinline__ TopNodes stage_top(const DevGeom &g, CHR_LDS u32x4 *lds, uint32_t want) {
+    const uint32_t n = want < g.nwnodes ? want : g.nwnodes;   // workgroup-uniform
+    for (uint32_t i = threadIdx.x; i < 6u * n; i += TB) {
+        const uint4 v = gld(g.wnodes + (size_t)g.wstride * (i / 6u) + i % 6u);
+        u32x4 w;
+        w.x = v.x; w.y = v.y; w.z = v.z; w.w = v.w;
+        lds[i] = w;
+    }
+    __syncthreads();
+    return TopNodes{lds, n};
+}
+__device__ __forceinline__ uint4 u4(u32x4 v) { return make_uint4(v.x, v.y, v.z, v.w); }
+__device__ __forceinline__ void load_node(const DevGeom &g, const TopNodes &top, uint32_t node, uint4 &h, uint4 &a1,
+                                          uint4 &a2, uint4 &a3, uint4 &a4, uint4 &a5) {
+    if (node < top.n) {
+        const CHR_LDS u32x4 *tp = top.p + 6u * node;
+        h = u4(tp[0]); a1 = u4(tp[1]); a2 = u4(tp[2]); a3 = u4(tp[3]); a4 = u4(tp[4]); a5 = u4(tp[5]);
+    } else {
+        const uint4 *np = g.wnodes + (size_t)g.wstride * node;
+        h = gld(np); a1 = gld(np + 1); a2 = gld(np + 2); a3 = gld(np + 3); a4 = gld(np + 4); a5 = gld(np + 5);
+    }
+}
+
 __device__ __forceinline__ void node_bounds(const DevGeom &g, uint4 n, V3 &lo, V3 &hi) {
     lo = v3(__builtin_fmaf((float)(n.x & 0xFFFFu), g.scale, g.ox), __builtin_fmaf((float)(n.y & 0xFFFFu), g.scale, g.oy),
             __builtin_fmaf((float)(n.z & 0xFFFFu), g.scale, g.oz));
@@ -281,14 +317,16 @@ struct WStack {
     CHR_LDS uint32_t *group;  // group walk: the group's shared stack, entry i = (node, entry distance) at [2i, 2i+1]
 };
 // SL: stack entries kept in LDS (the rest spill to scratch)
-template <int SL = WIDE_LDS>
+// TB: the LDS column stride (threads of the workgroup: trace_kernel may run
+// wider workgroups than BLOCK, so its per-CU top-of-tree copy is shared by more waves)
+template <int SL = WIDE_LDS, int TB = BLOCK>
 __device__ __forceinline__ void wpush(WStack &s, int i, uint32_t n, float t) {
-    if (i < SL) { s.node[i * BLOCK] = n; s.dist[i * BLOCK] = t; }
+    if (i < SL) { s.node[i * TB] = n; s.dist[i * TB] = t; }
     else s.spill[(size_t)(i - SL) * s.sstride] = make_uint2(n, __float_as_uint(t));
 }
-template <int SL = WIDE_LDS>
+template <int SL = WIDE_LDS, int TB = BLOCK>
 __device__ __forceinline__ void wpop(const WStack &s, int i, uint32_t &n, float &t) {
-    if (i < SL) { n = s.node[i * BLOCK]; t = s.dist[i * BLOCK]; }
+    if (i < SL) { n = s.node[i * TB]; t = s.dist[i * TB]; }
     else { const uint2 e = s.spill[(size_t)(i - SL) * s.sstride]; n = e.x; t = __uint_as_float(e.y); }
 }
 
@@ -371,7 +409,7 @@ __device__ __forceinline__ int walk_kind(V3 o, V3 d) {
 // each and divide the wave anyway): all 8 slab tests, the near child as the
 // first of the smallest entry distance, then one predicated push per child at
 // its prefix position.
-template <int SL = WIDE_LDS>
+template <int SL = WIDE_LDS, int TB = BLOCK>
 __device__ __forceinline__ uint32_t expand_node(const uint4 h, const uint4 a1, const uint4 a2, const uint4 a3,
                                                 const uint4 a4, const uint4 a5, const RaySlab &r, float best,
                                                 uint32_t &near_node, float &near_t, WStack &st, int &sp,
@@ -438,15 +476,15 @@ __device__ __forceinline__ uint32_t expand_node(const uint4 h, const uint4 a1, c
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
                 const int pos = ((push >> k) & 1u) ? sp + __builtin_popcount(push & ((1u << k) - 1u)) : sp + npush;
-                st.node[pos * BLOCK] = a4.x + (((k < 4 ? a5.x : a5.y) >> (8 * (k & 3))) & 0xFFu);
-                st.dist[pos * BLOCK] = tk[k];
+                st.node[pos * TB] = a4.x + (((k < 4 ? a5.x : a5.y) >> (8 * (k & 3))) & 0xFFu);
+                st.dist[pos * TB] = tk[k];
             }
         } else {
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
                 const int pos = sp + __builtin_popcount(push & ((1u << k) - 1u));
                 if (((push >> k) & 1u) && pos < WIDE_STACK)
-                    wpush<SL>(st, pos, a4.x + (((k < 4 ? a5.x : a5.y) >> (8 * (k & 3))) & 0xFFu), tk[k]);
+                    wpush<SL, TB>(st, pos, a4.x + (((k < 4 ? a5.x : a5.y) >> (8 * (k & 3))) & 0xFFu), tk[k]);
             }
         }
         if (sp + npush > WIDE_STACK) {
@@ -1542,6 +1580,7 @@ struct PropagateArgs {
     const uint32_t *winv;
     uint8_t *walive;
     uint32_t phys_lds;                 // shade / tail kernels: keep the physics tables in LDS (phys_cache)
+    uint32_t top_nodes;                // tail kernel: the first nodes of the wide BVH held in LDS (stage_top)
 };
 // modes of a device-driven step slot (step_head_kernel)
 constexpr uint32_t STEP_IDLE = 0, STEP_ONE = 1, STEP_TAIL = 2;
@@ -1965,13 +2004,15 @@ struct LdsFlat {
     CHR_LDS uint32_t *p;
     __device__ __forceinline__ CHR_LDS uint32_t &operator[](int i) const { return p[i]; }
 };
-struct LdsRows {
+template <int TB>
+struct LdsRowsT {
     CHR_LDS uint32_t *p;   // the wave's word 0 (row 0, its first lane)
     int off;
     __device__ __forceinline__ CHR_LDS uint32_t &operator[](int i) const {
-        return p[((i + off) >> 6) * BLOCK + ((i + off) & 63)];
+        return p[((i + off) >> 6) * TB + ((i + off) & 63)];
     }
 };
+typedef LdsRowsT<BLOCK> LdsRows;
 
 // All 64 lanes call this (converged).  act: the segment has a ray (segment-
 // uniform).  Returns the nearest triangle (-1: none) and its distance in
@@ -1987,7 +2028,7 @@ struct LdsRows {
 // offsets fold away); GS = 0: the width Gs_in at run time.
 template <int GS, class M>
 __device__ __forceinline__ int walk_segment(const DevGeom &g, bool act, V3 o, V3 d, uint32_t last, int Gs_in, M stk, int cap, M tlist,
-                            uint32_t &overflow, float &min_distance, uint32_t &iters,
+                            const TopNodes &top, uint32_t &overflow, float &min_distance, uint32_t &iters,
                             float best = __builtin_inff(), uint32_t best_rank = 0xFFFFFFFFu, int best_id = -1) {
     const int Gs = GS ? GS : Gs_in;
     constexpr uint32_t INVALID = 0xFFFFFFFFu;
@@ -2074,10 +2115,7 @@ __device__ __forceinline__ int walk_segment(const DevGeom &g, bool act, V3 o, V3
         if (!walking && Tp == 0) { done = true; continue; }
         // fetch: this iteration's nodes and the previous iteration's triangles together
         uint4 h = make_uint4(0u, 0u, 0u, 0u), a1 = h, a2 = h, a3 = h, a4 = h, a5 = h;
-        if (cur != INVALID) {
-            const uint4 *np = g.wnodes + (size_t)g.wstride * cur;
-            h = gld(np); a1 = gld(np + 1); a2 = gld(np + 2); a3 = gld(np + 3); a4 = gld(np + 4); a5 = gld(np + 5);
-        }
+        if (cur != INVALID) load_node(g, top, cur, h, a1, a2, a3, a4, a5);
         const bool has_tri = L < Tp;
         float4 r0 = make_float4(0.0f, 0.0f, 0.0f, 0.0f), r1 = r0, r2 = r0, r3 = r0;
         const float4 *rr = nullptr;
@@ -2214,6 +2252,8 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_tail_kernel(const DevGe
     if (a.prio & 1u) __builtin_amdgcn_s_setprio(3);
     __shared__ uint4 phys_lds[TAIL_PHYS_WORDS / 4];
     const DevGeom g = phys_cache(*gdev, phys_lds, a.phys_lds ? TAIL_PHYS_WORDS : 0u);
+    __shared__ uint4 top_lds[6 * TOP_NODES];   // 7 KB: 2 workgroups per CU hold 2 x 79 KB
+    const TopNodes top = stage_top<BLOCK>(g, (CHR_LDS u32x4 *)top_lds, a.top_nodes);
     const uint32_t slot = tid / 8, sub = tid & 7u;
     const uint32_t n = a.dev_n ? *a.dev_n - 1u : (uint32_t)a.nthreads;
     const uint32_t nslot = cap < n ? cap : n;
@@ -2334,9 +2374,9 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_tail_kernel(const DevGe
             uint32_t it;
             const int st = (Gs == 64 && (a.prio & 2u))
                                ? walk_segment<64>(g, act, o, dd, last, 64, LdsFlat{wstack}, TAIL_STACK * 8, LdsFlat{wtris},
-                                                  overflow, sd, it)
+                                                  top, overflow, sd, it)
                                : walk_segment<0>(g, act, o, dd, last, Gs, LdsFlat{wstack + seg0 / 8 * TAIL_STACK * 2},
-                                                 TAIL_STACK * Gs / 8, LdsFlat{wtris + 4 * seg0}, overflow, sd, it);
+                                                 TAIL_STACK * Gs / 8, LdsFlat{wtris + 4 * seg0}, top, overflow, sd, it);
             const int mine = __popcll(wm & ((1ull << (lane & ~7u)) - 1ull)) * Gs;   // my group's segment
             tri = __shfl(st, mine);
             dist = __shfl(sd, mine);
@@ -2555,24 +2595,29 @@ __global__ __launch_bounds__(BLOCK) void permute_rays_kernel(const uint4 *rays_i
 // COUNT: walk counters; F: triangle step once F/8 of the walking lanes have
 // parked leaves (intersect_wide_spec); SL: stack entries in LDS; MINW: waves
 // per SIMD; R: refill once R of the 64 lanes are without a ray.
-template <bool COUNT, int F, int SL, int MINW, int R>
-__global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__restrict__ gdev, TraceArgs a) {
-    __shared__ uint32_t lds[(2 * SL + LEAFQ) * BLOCK];
-    // a draining wave's walk_segment stacks (8 x TAIL_STACK entries) + triangle lists in its LDS rows
-    static_assert((2 * SL + LEAFQ) * 64 >= 8 * TAIL_STACK * 2 + 2 * TAIL_TRI, "drain needs the wave's LDS rows");
+template <bool COUNT, int F, int SL, int MINW, int R, int TB = BLOCK, int TOPN = 0>
+__global__ __launch_bounds__(TB, MINW) void trace_kernel(const DevGeom *__restrict__ gdev, TraceArgs a) {
+    __shared__ uint32_t lds[(2 * SL + LEAFQ) * TB];
+    // the top of the tree (stage_top): TB = 1024 makes one copy per CU serve its 16 waves
+    __shared__ uint4 top_lds[TOPN > 0 ? 6 * TOPN : 1];
+    // a draining wave's walk_segment stacks (8 x DSTK entries, DSTK per 8 lanes) + triangle
+    // lists in its LDS rows
+    constexpr int DSTK = ((2 * SL + LEAFQ) * 64 - 2 * TAIL_TRI) / 16;
+    static_assert(DSTK >= 112, "drain needs the wave's LDS rows");
     WStack st;
     // Deep stack entries live in a lane-strided HBM column sized for this
     // persistent grid, not in private scratch: a kernel with a private segment
     // depends on the runtime's scratch allocation, which can throttle the waves
     // a dispatch keeps resident (the persistent grid then drains on a few waves).
-    st.spill = a.spill + (blockIdx.x * BLOCK + threadIdx.x);
-    st.sstride = gridDim.x * BLOCK;
+    st.spill = a.spill + (blockIdx.x * TB + threadIdx.x);
+    st.sstride = gridDim.x * TB;
     st.node = (CHR_LDS uint32_t *)(lds + threadIdx.x);
-    st.dist = (CHR_LDS float *)(lds + SL * BLOCK + threadIdx.x);
-    st.leafq = (CHR_LDS uint32_t *)(lds + 2 * SL * BLOCK + threadIdx.x);
+    st.dist = (CHR_LDS float *)(lds + SL * TB + threadIdx.x);
+    st.leafq = (CHR_LDS uint32_t *)(lds + 2 * SL * TB + threadIdx.x);
     if (a.mode && *a.mode != STEP_ONE) return;
     const uint32_t n = a.dev_n ? *a.dev_n - 1u : a.n;
     const DevGeom &g = *gdev;
+    const TopNodes top = TOPN > 0 ? stage_top<TB>(g, (CHR_LDS u32x4 *)top_lds, (uint32_t)TOPN) : TopNodes{nullptr, 0u};
     const uint32_t lane = __lane_id();
     uint32_t overflow = 0;
     WalkCounts cnt{0u, 0u, 0u, 0u, 0u, 0ull, 0ull, 0u};
@@ -2601,7 +2646,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
     // grid's lanes (every wave then walks a few rays and reaches its drain sooner)
     uint32_t claim = CLAIM;
     if (a.spread) {
-        const uint32_t waves = gridDim.x * (BLOCK / 64);
+        const uint32_t waves = gridDim.x * (TB / 64);
         const uint32_t share = (total + waves - 1u) / waves;
         claim = share < 1u ? 1u : (share < CLAIM ? share : CLAIM);
     }
@@ -2652,7 +2697,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
                     }
                     j = rank < g0 ? b0 + rank : b1 + (rank - g0);
                     if (cb >= total) exhausted = true;     // later claims lie beyond the last item
-                    else if (!have_pend && cb + 2u * gridDim.x * BLOCK < total) {
+                    else if (!have_pend && cb + 2u * gridDim.x * TB < total) {
                         if (lane == 0) pend = atomicAdd(a.next, claim);
                         have_pend = true;
                     }
@@ -2770,15 +2815,19 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
                 while (sp > 0) {
                     sp--;
                     float t;
-                    wpop<SL>(st, sp, node, t);
+                    wpop<SL, TB>(st, sp, node, t);
                     if (!(t > best)) { found = true; break; }
                 }
                 if (!found) { walk_done = true; continue; }
             }
             if constexpr (COUNT) { cnt.nodes++; walk_cost++; if (wave_leader()) cnt.wave_nodes++; }
-            const uint4 *np = g.wnodes + (size_t)g.wstride * node;
-            const uint4 h = gld(np), a1 = gld(np + 1), a2 = gld(np + 2), a3 = gld(np + 3), a4 = gld(np + 4),
-                        a5 = gld(np + 5);
+            uint4 h, a1, a2, a3, a4, a5;
+            if constexpr (TOPN > 0) {
+                load_node(g, top, node, h, a1, a2, a3, a4, a5);
+            } else {
+                const uint4 *np = g.wnodes + (size_t)g.wstride * node;
+                h = gld(np); a1 = gld(np + 1); a2 = gld(np + 2); a3 = gld(np + 3); a4 = gld(np + 4); a5 = gld(np + 5);
+            }
 #ifdef CHR_DEVICE_PROFILE
             pf.call(P_NODE);
             for (int k = 0; k < 8; ++k)
@@ -2787,7 +2836,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
             uint32_t near_node;
             float near_t;
             uint32_t leaf_mask =
-                expand_node<SL>(h, a1, a2, a3, a4, a5, slab, best, near_node, near_t, st, sp, overflow, cmask);
+                expand_node<SL, TB>(h, a1, a2, a3, a4, a5, slab, best, near_node, near_t, st, sp, overflow, cmask);
             cmask = 0xFFu;
             node = near_node;
             while (leaf_mask) {
@@ -2795,7 +2844,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
                 leaf_mask &= leaf_mask - 1;
                 const uint32_t kind = ((k < 4 ? a4.z : a4.w) >> (8 * (k & 3))) & 0xFFu;
                 const uint32_t first = a4.y + (((k < 4 ? a5.x : a5.y) >> (8 * (k & 3))) & 0xFFu);
-                st.leafq[(qt % LEAFQ) * BLOCK] = first | ((kind - 1u) << 30);
+                st.leafq[(qt % LEAFQ) * TB] = first | ((kind - 1u) << 30);
                 qt++;
             }
         } else {
@@ -2804,7 +2853,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
             pf.set(P_TRI);
             pf.call(P_TRI);
             if (pleft == 0) {
-                const uint32_t e = st.leafq[(qh % LEAFQ) * BLOCK];
+                const uint32_t e = st.leafq[(qh % LEAFQ) * TB];
                 qh++;
                 pcur = e & 0x3FFFFFFFu;
                 pleft = (e >> 30) + 1u;
@@ -2852,8 +2901,8 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
             CHR_LDS uint32_t *wbase = (CHR_LDS uint32_t *)(lds + (threadIdx.x & ~63u));
             float sdist;
             uint32_t sit;
-            const int tri = walk_segment<0>(g, act, so, sdir, slast, Gs, LdsRows{wbase, seg0 / 8 * TAIL_STACK * 2},
-                                         TAIL_STACK * Gs / 8, LdsRows{wbase, 8 * TAIL_STACK * 2 + 4 * seg0}, overflow,
+            const int tri = walk_segment<0>(g, act, so, sdir, slast, Gs, LdsRowsT<TB>{wbase, seg0 / 8 * DSTK * 2},
+                                         DSTK * Gs / 8, LdsRowsT<TB>{wbase, 8 * DSTK * 2 + 4 * seg0}, top, overflow,
                                          sdist, sit, sbest, srank, sid);
             const int mine = (__popcll(rm & ((1ull << lane) - 1ull)) * Gs) & 63;   // my segment's first lane
             const int rt = __shfl(tri, mine);
@@ -3572,6 +3621,12 @@ static bool phys_lds_enabled() {
     const char *e = getenv("CHR_PHYS_LDS");
     return !(e && e[0] == '0');
 }
+// CHR_TAIL_TOP=0: the tail's walks read every node from global memory instead of
+// the top of the tree from LDS (stage_top; A/B)
+static uint32_t tail_top_nodes() {
+    const char *e = getenv("CHR_TAIL_TOP");
+    return (e && e[0] == '0') ? 0u : TOP_NODES;
+}
 static int shade_waves() {             // CHR_SHADE_WAVES=2|4: the shade kernel at 2 / 4 waves per SIMD (A/B)
     const char *e = getenv("CHR_SHADE_WAVES");
     return e ? atoi(e) : 3;
@@ -3627,6 +3682,7 @@ struct StepVariant {
     trace_fn trace = nullptr;       // one-step launches: trace_kernel + shade (nullptr: fn)
     propagate_step_fn shade = nullptr;
     int trace_waves = 4;            // waves per SIMD of the trace kernel (persistent grid size)
+    int trace_block = BLOCK;        // its workgroup size
     propagate_step_fn tail = nullptr;   // multi-step launches: group-walk kernel (nullptr: fn)
     int tail_group = 0;                 // its lanes per photon
     int binned = 0;                 // trace order binned by direction: 1 every step, 2 first host step only
@@ -3667,6 +3723,13 @@ static int trace_refill_r() {
     const char *e = getenv("CHR_TRACE_R");
     return e ? atoi(e) : 48;
 }
+// CHR_TRACE_LAYOUT (A/B): 0 256-thread workgroups, 12 LDS stack entries per lane;
+// 1 1024-thread workgroups (one per CU), 11 entries, the top TOP_NODES nodes of
+// the tree in LDS (stage_top); 2 the same without the top nodes (control)
+static int trace_layout() {
+    const char *e = getenv("CHR_TRACE_LAYOUT");
+    return e ? atoi(e) : 0;
+}
 static StepVariant select_step_variant(const chr_geometry *g) {
     const char *e = getenv("CHR_PROPAGATE_VARIANT");
     int v = e ? atoi(e) : 0;
@@ -3693,6 +3756,13 @@ static StepVariant select_step_variant(const chr_geometry *g) {
             sv.fn = propagate_step_kernel<8, 4, kWalk>;
             sv.trace = trace_refill_r() == 16 ? trace_kernel<false, 6, 12, 4, 16>
                        : (trace_refill_r() == 32 ? trace_kernel<false, 6, 12, 4, 32> : trace_kernel<false, 6, 12, 4, 48>);
+            if (trace_refill_r() == 48) {
+                switch (trace_layout()) {
+                    case 1: sv.trace = trace_kernel<false, 6, 11, 4, 48, 1024, TOP_NODES>; sv.trace_block = 1024; break;
+                    case 2: sv.trace = trace_kernel<false, 6, 11, 4, 48, 1024, 0>; sv.trace_block = 1024; break;
+                    default: break;
+                }
+            }
             sv.shade = shade_waves() == 4 ? shade_kernel<4> : (shade_waves() == 2 ? shade_kernel<2> : shade_kernel<3>);
             sv.tail = tail_group_walk() ? propagate_group_kernel<8, kGroupWaves>
                       : (tail_waves() == 4 ? propagate_tail_kernel<4>
@@ -3740,6 +3810,7 @@ static int launch_chunk(const chr_geometry *g, const chr_photons *ph, uint32_t *
     a.winv = nullptr;
     a.walive = nullptr;
     a.phys_lds = phys_lds_enabled() ? 1u : 0u;
+    a.top_nodes = tail_top_nodes();
     a.prio = 0;
     if (sort_enabled() && nthreads >= kSortMin) {
         // coherence order (sort_key_kernel): rays that start close together in
@@ -3975,6 +4046,7 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
     a.winv = nullptr;
     a.walive = nullptr;
     a.phys_lds = phys_lds_enabled() ? 1u : 0u;
+    a.top_nodes = tail_top_nodes();
     a.prio = 0;
     FlatEnrol fe{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
     // walk-order carry: this step's walk order (nullptr: queue order) and the next step's
@@ -4089,16 +4161,17 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
         if (do_trace) {
             const int cus = device_cus();
             if (cus <= 0) return chr::fail(CHR_ERR_HIP, "launch_step: no compute units");
-            uint64_t resident = (uint64_t)cus * 4 * sv.trace_waves * 64 / BLOCK;   // persistent grid
+            const int tb = sv.trace_block;
+            uint64_t resident = (uint64_t)cus * 4 * sv.trace_waves * 64 / tb;   // persistent grid
             // a batch's prefix walk (chr_propagate_batches) runs beside the previous
             // batch's kernels: CHR_PREFIX_GRID=1/k of the grid leaves them CUs (A/B)
             if (phase == PHASE_PREFIX || phase == PHASE_TRACE)
                 resident = std::max<uint64_t>(1, resident / prefix_grid_div());
-            const uint32_t blocks = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(resident, grid_for(n)));
-            if (int rc = walk_stack_get((size_t)WIDE_STACK * blocks * BLOCK * sizeof(uint2), &ta.spill, sc ? sc->ctx : 0))
+            const uint32_t blocks = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(resident, ((uint64_t)n + tb - 1) / tb));
+            if (int rc = walk_stack_get((size_t)WIDE_STACK * blocks * tb * sizeof(uint2), &ta.spill, sc ? sc->ctx : 0))
                 return rc;
             if (evt0) CHR_HIP_CHECK(hipEventRecord(evt0, stream));
-            hipLaunchKernelGGL(sv.trace, dim3(blocks), dim3(BLOCK), 0, stream, (const DevGeom *)g->d_dev, ta);
+            hipLaunchKernelGGL(sv.trace, dim3(blocks), dim3(tb), 0, stream, (const DevGeom *)g->d_dev, ta);
             if (evt1) CHR_HIP_CHECK(hipEventRecord(evt1, stream));
         }
         if (!rest) {
@@ -4890,10 +4963,11 @@ static int propagate_batches(const chr_geometry *g, const chr_photons *phs, cons
         CHR_TRY(slot_ctl_get(2 * (size_t)max_steps + 8, &ctl, c));
         const int cus = device_cus();
         const StepVariant sv = select_step_variant(g);
-        const uint64_t blocks = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)cus * 4 * sv.trace_waves * 64 / BLOCK,
-                                                                          grid_for(max_n)));
+        const uint64_t tb = (uint64_t)sv.trace_block;
+        const uint64_t blocks = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)cus * 4 * sv.trace_waves * 64 / tb,
+                                                                          ((uint64_t)max_n + tb - 1) / tb));
         uint2 *spill = nullptr;
-        CHR_TRY(walk_stack_get((size_t)WIDE_STACK * blocks * BLOCK * sizeof(uint2), &spill, c));
+        CHR_TRY(walk_stack_get((size_t)WIDE_STACK * blocks * tb * sizeof(uint2), &spill, c));
     }
     // the photon inputs were written on the caller's stream
     std::vector<hipEvent_t> *entry_ev = nullptr;
@@ -5168,10 +5242,11 @@ __global__ __launch_bounds__(BLOCK) void walk_probe_kernel(const DevGeom *__rest
     uint32_t overflow = 0, it = 0;
     float sd;
     const V3 o = v3(od[0], od[1], od[2]), d = v3(od[3], od[4], od[5]);
+    const TopNodes top{nullptr, 0u};
     const int st = gs == 64 ? walk_segment<64>(*gdev, true, o, d, 7u, 64, LdsFlat{wstack}, TAIL_STACK * 8, LdsFlat{wtris},
-                                               overflow, sd, it)
+                                               top, overflow, sd, it)
                             : walk_segment<0>(*gdev, true, o, d, 7u, gs, LdsFlat{wstack}, TAIL_STACK * gs / 8,
-                                              LdsFlat{wtris}, overflow, sd, it);
+                                              LdsFlat{wtris}, top, overflow, sd, it);
     out[threadIdx.x] = st + (int)overflow + (int)it + (int)sd;
 }
 }  // namespace chr
