@@ -39,8 +39,11 @@ initialisation, as two batches in order, then propagates the SAME two batches
 on the GPU through the path the headline used (pipelined or sequential) and
 compares photon by photon (history flags, last-hit triangles and channels
 bit-exact; positions, directions, polarisations, times and wavelengths as a
-max relative difference).  Ranks > 0 check a smaller sample of their own shard
-(their own photon seed and RNG subsequences): parity.per_rank.
+max relative difference).  Ranks > 0 propagate a smaller sample of their own
+shard (their own photon seed and RNG subsequences) on their GPU and send the
+photons to rank 0, which runs the oracle for them: parity.per_rank (only rank
+0 holds the oracle's host copy of the geometry).  detail.ranks carries each
+rank's setup times (geometry build / cache load, upload) and host memory.
 
 Roofline: the dominant kernel is trace_kernel, the
 BVH walk of every one-step launch.  It is bound by HBM/L2 latency-bandwidth on
@@ -121,20 +124,39 @@ def usable_cpus():
     return n
 
 
+def host_memory():
+    """This process's host memory: resident now and its peak (GB), from
+    /proc/self/status (a replicated 29k geometry is ~15 GB of host memory per rank)."""
+    out = {}
+    try:
+        with open('/proc/self/status') as f:
+            for line in f:
+                k, _, v = line.partition(':')
+                if k in ('VmRSS', 'VmHWM'):
+                    out['host_rss_gb' if k == 'VmRSS' else 'host_peak_rss_gb'] = round(int(v.split()[0]) / 1e6, 3)
+    except (OSError, ValueError):
+        pass
+    return out
+
+
 def kernel_source_sha():
-    """sha256 (16 hex) of the sources libchroma_amd.so is built from: the stamp
-    that ties a committed PMC record to the kernels it measured."""
-    h = hashlib.sha256()
-    csrc = os.path.join(ROOT, 'chroma-lite_amd', 'csrc')
-    inc = os.path.join(ROOT, 'include')
-    files = sorted(os.path.join(csrc, f) for f in os.listdir(csrc)
-                   if f.endswith(('.hip', '.h', '.cpp')) or f == 'Makefile')
-    files += sorted(os.path.join(inc, f) for f in os.listdir(inc) if f.endswith('.h'))
-    for p in files:
-        h.update(os.path.relpath(p, ROOT).encode())
-        with open(p, 'rb') as f:
-            h.update(f.read())
-    return h.hexdigest()[:16]
+    """sha256 (16 hex) of the sources libchroma_amd.so is built from
+    (tools/source_sha.py): the stamp that ties a committed PMC record to the
+    kernels it measured."""
+    sys.path.insert(0, os.path.join(ROOT, 'tools'))
+    from source_sha import kernel_source_sha as sha
+    return sha(ROOT)
+
+
+def so_source_sha():
+    """The sha compiled into the loaded libchroma_amd.so (chr_source_sha): the
+    library travels prebuilt with the tree, so the line says whether it was
+    built from these sources."""
+    from chroma.gpu import _native
+    try:
+        return _native.lib().chr_source_sha().decode()
+    except (AttributeError, OSError, _native.NativeError) as e:   # an older library
+        return 'unavailable: %s' % e
 
 
 def build_geometry(name, cache_dir):
@@ -328,6 +350,8 @@ def roofline(args, reports, ref):
     pmc, note = pmc_record(args)
     sha = kernel_source_sha()
     rl['kernel_source_sha'] = sha
+    rl['so_source_sha'] = so_source_sha()
+    rl['so_built_from_these_sources'] = rl['so_source_sha'] == sha
     if pmc is None:
         rl['traffic_source'] = note
         return rl
@@ -360,9 +384,11 @@ class PropagateWorkload(object):
         from types import SimpleNamespace
         self.args, self.rank, self.world, self.local, self.nphotons = args, rank, world, local, nphotons
         self.torch = torch
+        t_setup = time.time()
         self.det = shared_geometry(args.detector, args.cache_dir, rank, dist)
         t0 = time.time()
         self.gdet = gpu.GPUDetector(self.det)
+        self.setup = {'geometry_s': round(t0 - t_setup, 2), 'upload_s': round(time.time() - t0, 2)}
         log('rank %d: geometry on device in %.1fs (%.2f GB)' % (rank, time.time() - t0,
                                                                self.gdet.device_bytes() / 1e9))
         self.nslots = args.nthreads_per_block * args.max_blocks
@@ -375,6 +401,7 @@ class PropagateWorkload(object):
             pol=ga.to_gpu(gpu.to_float3(ph.pol)), wavelengths=ga.to_gpu(ph.wavelengths),
             t=ga.to_gpu(ph.t), flags=ga.to_gpu(ph.flags), evidx=ga.to_gpu(ph.evidx), true_nphotons=nphotons)
         torch.cuda.synchronize()
+        self.setup['setup_s'] = round(time.time() - t_setup, 2)
         self.counts = ga.zeros(self.gdet.nchannels, np.uint32)
         self.reduced = {}
         self.group = max(1, min(args.steps, args.pipeline_depth)) if args.pipeline else 1
@@ -457,6 +484,7 @@ class PropagateWorkload(object):
                 'detected_last_step': int(((gp.flags.get() & 4) != 0).sum()) if gp is not None else 0,
                 'channel_hits_all_ranks': int(self.reduced['counts'].sum().item()) if 'counts' in self.reduced
                 else 0,
+                'setup': dict(self.setup, **host_memory()),
                 'tail': [{'ms': round(s.tail_ms, 3), 'photons': int(s.tail_photons),
                           'max_steps': int(s.tail_max_steps),
                           'slowest_photon_ms': round(s.tail_max_cycles / 1e5, 3),
@@ -519,10 +547,19 @@ class PropagateWorkload(object):
                 'channels': self.det.num_channels()}
 
     # ------------------------------------------------------------ oracle checks
-    def _oracle_batches(self, n, threads):
-        """The oracle on this rank's first n photons as two batches in order
-        (the RNG states carried from one to the next, as two propagate calls),
-        from the rank's own RNG subsequences.  Returns (hosts, walk stats, seconds)."""
+    def photons_of_rank(self, r):
+        """Rank r's photon source: its own seed and shard size (rank 0 regenerates
+        another rank's photons to check that rank's GPU sample against the oracle)."""
+        if r == self.rank:
+            return self.photons
+        from chroma.photon_source import isotropic
+        return isotropic(photons_for_rank(self.args, r, self.world), seed=PHOTON_SEED + r)
+
+    def _oracle_batches(self, n, threads, rank=None):
+        """The oracle on rank `rank`'s first n photons (default: this rank's) as two
+        batches in order (the RNG states carried from one to the next, as two
+        propagate calls), from that rank's own RNG subsequences.  Returns (hosts,
+        walk stats, seconds)."""
         sys.path.insert(0, os.path.join(ROOT, 'oracle'))
         import oracle
         from chroma.event import Photons
@@ -530,11 +567,12 @@ class PropagateWorkload(object):
         if not hasattr(self, '_packed'):
             self._packed = PackedGeometry(self.det)
         a = self.args
-        ph = self.photons
+        rank = self.rank if rank is None else rank
+        ph = self.photons_of_rank(rank)
         cuts = [0, n // 2, n]
         hosts = [oracle.HostPhotons(Photons(ph.pos[lo:hi], ph.dir[lo:hi], ph.pol[lo:hi], ph.wavelengths[lo:hi]))
                  for lo, hi in zip(cuts[:-1], cuts[1:])]
-        st = oracle.rng_init(self.nslots, seed=a.seed, first_subsequence=rng_first_subsequence(self.rank, self.nslots))
+        st = oracle.rng_init(self.nslots, seed=a.seed, first_subsequence=rng_first_subsequence(rank, self.nslots))
         tot = {}
         t0 = time.time()
         for h in hosts:
@@ -561,10 +599,14 @@ class PropagateWorkload(object):
                               n, n // 2, n - n // 2, self.args.max_steps, dt, threads, os.cpu_count() or 0))
         return cpu, stats, n, hosts
 
-    def gpu_parity(self, n, hosts, pipeline):
-        """Propagate the oracle's two batches on the GPU (same RNG initialisation,
-        same launch shape) -- through propagate_batches when the headline is
-        pipelined, one propagate call each otherwise -- and compare photon by photon."""
+    PARITY_FIELDS = ('flags', 'last_hit_triangles', 'pos', 'dir', 'pol', 't', 'wavelengths')
+
+    def gpu_sample(self, n, pipeline):
+        """This rank's first n photons propagated on its GPU as two batches (same
+        RNG initialisation and launch shape as the oracle's) -- through
+        propagate_batches when the headline is pipelined, one propagate call each
+        otherwise.  Returns the photons' fields (host arrays) and the run's facts:
+        what a rank > 0 sends to rank 0, which runs the oracle for every rank."""
         from chroma import gpu
         from chroma.event import Photons
         a = self.args
@@ -584,6 +626,16 @@ class PropagateWorkload(object):
                 gp.propagate(self.gdet, rng, **kw)
                 sts.append(gp.last_stats)
         got = [gp.get() for gp in gps]
+        return {'rank': self.rank, 'n': int(n), 'batches': [int(c) for c in np.diff(cuts)],
+                'path': 'propagate_batches (pipelined)' if pipeline else 'propagate (sequential)',
+                'stack_overflows': int(sum(s.stack_overflows for s in sts)),
+                'photons': {f: np.concatenate([getattr(o, f) for o in got]) for f in self.PARITY_FIELDS}}
+
+    def compare(self, sample, hosts):
+        """Parity of a rank's GPU sample against the oracle's photons (hosts):
+        flags, last-hit triangles and channels bit-exact, floats as max relative."""
+        got = sample['photons']
+        rank = sample['rank']
         solid_map = np.asarray(self.det.solid_id, np.int64)
         s2c = np.asarray(self.det.solid_id_to_channel_index, np.int64)
 
@@ -601,25 +653,25 @@ class PropagateWorkload(object):
             y = np.asarray(y, np.float64)
             return float(np.max(np.abs(x - y) / np.maximum(np.abs(y), 1e-30))) if x.size else 0.0
 
-        gf, hf = cat(got, 'flags'), cat(hosts, 'flags')
-        gl, hl = cat(got, 'last_hit_triangles'), cat(hosts, 'last_hit_triangles')
+        n = sample['n']
+        gf, hf = got['flags'], cat(hosts, 'flags')
+        gl, hl = got['last_hit_triangles'], cat(hosts, 'last_hit_triangles')
         ch_gpu, ch_ref = channel(gf, gl), channel(hf, hl)
-        rel = max(max_rel(cat(got, f), cat(hosts, f)) for f in ('pos', 't', 'wavelengths'))
-        dp = max(float(np.max(np.abs(cat(got, f) - cat(hosts, f)))) if n else 0.0 for f in ('dir', 'pol'))
-        return {'rank': self.rank, 'n': int(n), 'batches': [int(c) for c in np.diff(cuts)],
-                'path': 'propagate_batches (pipelined)' if pipeline else 'propagate (sequential)',
-                'rng_first_subsequence': rng_first_subsequence(self.rank, self.nslots),
-                'photon_seed': PHOTON_SEED + self.rank,
+        rel = max(max_rel(got[f], cat(hosts, f)) for f in ('pos', 't', 'wavelengths'))
+        dp = max(float(np.max(np.abs(got[f] - cat(hosts, f)))) if n else 0.0 for f in ('dir', 'pol'))
+        return {'rank': rank, 'n': int(n), 'batches': sample['batches'], 'path': sample['path'],
+                'rng_first_subsequence': rng_first_subsequence(rank, self.nslots),
+                'photon_seed': PHOTON_SEED + rank,
                 'flags_equal': bool(np.array_equal(gf, hf)), 'last_hit_equal': bool(np.array_equal(gl, hl)),
                 'channel_equal': bool(np.array_equal(ch_gpu, ch_ref)),
                 'flags_mismatches': int(np.count_nonzero(gf != hf)),
                 'detected': int(np.count_nonzero(ch_ref >= 0)), 'max_rel': rel, 'dir_pol_max_abs': dp,
                 'binned_first_step': bool(n // 2 >= (1 << 20)),
-                'stack_overflows': int(sum(s.stack_overflows for s in sts))}
+                'stack_overflows': sample['stack_overflows'], 'oracle_on_rank': self.rank}
 
     def check(self, full, budget_s, threads, sample):
-        """Rank 0 (full): cpu_baseline + parity on the adaptive sample.  Other
-        ranks: parity on `sample` photons of their own shard.  Returns
+        """Rank 0 (full): cpu_baseline + parity on the adaptive sample.  Otherwise
+        parity on `sample` photons of this rank's shard, oracle run here.  Returns
         (cpu_baseline or None, oracle walk stats, parity)."""
         if full:
             cpu, stats, n, hosts = self.cpu_baseline(budget_s, threads)
@@ -627,7 +679,14 @@ class PropagateWorkload(object):
             n = min(self.nphotons, sample)
             hosts, stats, _ = self._oracle_batches(n, threads)
             cpu = None
-        return cpu, stats, self.gpu_parity(n, hosts, self.args.pipeline)
+        return cpu, stats, self.compare(self.gpu_sample(n, self.args.pipeline), hosts)
+
+    def check_rank(self, sample, threads):
+        """On rank 0: the oracle for another rank's GPU sample (that rank's photon
+        seed and RNG subsequences; only they differ, the geometry is rank 0's),
+        compared photon by photon.  The other ranks build no host geometry copy."""
+        hosts, _, _ = self._oracle_batches(sample['n'], threads, rank=sample['rank'])
+        return self.compare(sample, hosts)
 
 
 WORKLOAD = PropagateWorkload     # replaced by tests/bench_stub_main.py (CPU rehearsal of the rank logic)
@@ -660,7 +719,7 @@ def parse_args(argv=None):
     ap.add_argument('--timing-steps', type=int, default=5,
                     help='untimed pipelined steps with every per-slot timing event recorded, after the timed '
                          'steps (detail.slot_timing_pass, detail.kernel_ms_per_step; 0: skip)')
-    ap.add_argument('--sequential-steps', type=int, default=5,
+    ap.add_argument('--sequential-steps', type=int, default=20,
                     help='after the pipelined headline: this many one-call-per-step steps, timed the same way '
                          '(detail.sequential; 0: skip)')
     ap.add_argument('--cache-dir', default=os.environ.get('CHROMA_BENCH_CACHE', '/tmp/chroma_bench_cache'))
@@ -744,11 +803,13 @@ def run_rank(args):
     report = wl.rank_report(stats)
     seq = None
     if args.pipeline and args.sequential_steps > 0:
-        s_el, _, _ = timed_loop(wl.run_sequential, args.sequential_steps, 0, dist, wl.sync, 1)
+        # warm-up first: a propagate call uses its own buffer context, whose first use
+        # allocates it (r03's 5-step figure, 350.7 M/s, timed that allocation)
+        s_el, _, _ = timed_loop(wl.run_sequential, args.sequential_steps, 2, dist, wl.sync, 1)
         s_total = nphotons * args.sequential_steps
         if dist is not None:
             s_total = _allreduce(dist, float(s_total), 'sum')
-        seq = {'photons_per_s': s_total / s_el, 'steps': args.sequential_steps,
+        seq = {'photons_per_s': s_total / s_el, 'steps': args.sequential_steps, 'warmup': 2,
                'ms_per_step': 1e3 * s_el / args.sequential_steps,
                'path': 'one GPUPhotons.propagate call per step (the reference caller\'s loop)'}
     wl.reduced.pop('gp', None)
@@ -776,16 +837,23 @@ def run_rank(args):
                                '(CHR_SLOT_TIMING=1); the timed steps record only the trace launch pairs'}
     extra = wl.untimed_passes()
 
-    # oracle checks: ranks > 0 check a sample of their own shard first (small,
-    # concurrently), then rank 0 runs the timed cpu_baseline alone on the host
-    check = None
-    if not args.no_cpu_baseline and rank > 0:
-        check = wl.check(False, args.cpu_budget, max(1, usable_cpus() // world), args.rank_parity_photons)
-    if dist is not None:
-        dist.barrier()
-    if not args.no_cpu_baseline and rank == 0:
-        check = wl.check(True, args.cpu_budget, usable_cpus(), 0)
-    report['parity'] = check[2] if check else None
+    # oracle checks: ranks > 0 propagate a sample of their own shard on their GPU and
+    # send the photons to rank 0; rank 0 runs the timed cpu_baseline alone on the host
+    # (its own parity), then the oracle for every other rank's sample -- only rank 0
+    # holds a host copy of the geometry's packed tables (PackedGeometry)
+    check, samples = None, None
+    if not args.no_cpu_baseline:
+        mine = None
+        if rank > 0:
+            mine = wl.gpu_sample(min(nphotons, args.rank_parity_photons), args.pipeline)
+        if dist is not None:
+            samples = [None] * world if rank == 0 else None
+            dist.gather_object(mine, samples, dst=0)
+        if rank == 0:
+            check = wl.check(True, args.cpu_budget, usable_cpus(), 0)
+            per_rank = [check[2]] + [wl.check_rank(smp, usable_cpus()) for smp in (samples or [None])[1:]]
+            check = (check[0], check[1], check[2], per_rank)
+    report.update(host_memory())
     if dist is not None:
         reports = [None] * world
         dist.all_gather_object(reports, report)
@@ -796,9 +864,14 @@ def run_rank(args):
         steps = max(1, args.steps)
         r0 = reports[0]
         detail = {'pipelined_steps_per_call': wl.group, 'warmup_steps_run': warmup,
-                  'ranks_seen': len(reports), 'ranks': [{k: rep[k] for k in ('rank', 'local_rank', 'host', 'device',
-                                                                             'photons_per_step')}
-                                                        for rep in reports],
+                  # the timed steps' input batches were filled before t0 (timed_loop's prepare;
+                  # bench.py since 40b6d98) rather than restored inside the timed region
+                  'inputs_prefilled': getattr(wl, 'prepare', None) is not None and wl.group >= args.steps,
+                  'ranks_seen': len(reports),
+                  'ranks': [dict({k: rep[k] for k in ('rank', 'local_rank', 'host', 'device', 'photons_per_step')},
+                                 setup=rep.get('setup'), host_rss_gb=rep.get('host_rss_gb'),
+                                 host_peak_rss_gb=rep.get('host_peak_rss_gb'))
+                            for rep in reports],
                   'kernel_ms_per_step': (timing_pass['kernel_ms_per_step'] if timing_pass else r0['kernel_ms'] / steps),
                   'trace_ms_per_step': r0['trace_ms'] / steps,
                   'launches_per_step': r0['launches'] / steps,
@@ -817,7 +890,7 @@ def run_rank(args):
         detail.update(extra)
         result = result_line(args, world, elapsed, per_step, total_photons, wl.detector_info(), detail)
         if check is not None:
-            cpu, ostats, par = check
+            cpu, ostats, par, per_rank = check
             result['cpu_baseline'] = cpu
             nsample = par['n']
             detail['reference_bvh_nodes_per_photon'] = ostats['nodes_visited'] / nsample
@@ -826,7 +899,7 @@ def run_rank(args):
                                                          4.0 * ostats['traversals']) / nsample
             parity = dict(par)
             if world > 1:
-                parity['per_rank'] = [r['parity'] for r in reports]
+                parity['per_rank'] = per_rank
                 parity['all_ranks_equal'] = all(p is not None and p['flags_equal'] and p['last_hit_equal'] and
                                                 p['channel_equal'] for p in parity['per_rank'])
             result['parity'] = parity

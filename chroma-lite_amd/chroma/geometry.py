@@ -37,13 +37,19 @@ _NATIVE_UNIQUE_MIN = 1 << 16
 
 def _native_unique(v):
     """(unique rows, inverse) from libchroma_amd's chr_unique_vertices, or None
-    when the rows hold a NaN or -0.0 (numpy then decides which duplicate stays)."""
+    when the rows hold a NaN or -0.0 (numpy then decides which duplicate stays)
+    or the library cannot be loaded here (a host-only install: this host-side
+    merge is the reference's np.unique either way, geometry.py:337-391)."""
     import ctypes
-    from chroma.gpu import _native
+    try:
+        from chroma.gpu import _native
+        lib = _native.lib()
+    except (ImportError, OSError):
+        return None
     out = np.empty_like(v)
     inverse = np.empty(len(v), dtype=np.int64)
     nu = ctypes.c_uint64()
-    rc = _native.lib().chr_unique_vertices(v.ctypes.data, len(v), out.ctypes.data, ctypes.byref(nu),
+    rc = lib.chr_unique_vertices(v.ctypes.data, len(v), out.ctypes.data, ctypes.byref(nu),
                                            inverse.ctypes.data)
     if rc != 0:
         return None

@@ -149,6 +149,7 @@ _SIGNATURES = {
     'chr_device_profile_fetch': (c_i32, [c_vp, c_vp, c_i32, ctypes.POINTER(c_u32)]),
     'chr_last_error': (ctypes.c_char_p, []),
     'chr_version': (c_i32, []),
+    'chr_source_sha': (ctypes.c_char_p, []),
 }
 
 EXPORTED = tuple(_SIGNATURES)

@@ -329,7 +329,9 @@ class ShardedSimulation(Simulation):
         daq.channel_history_gpu.tensor.copy_(h)
         return daq.end_acquire().get()
 
-    def _emit(self, b, keep_photons_end=False, **kw):
+    def simulate(self, iterable, keep_photons_end=False, **kw):
+        """Simulation.simulate on this rank's shards.  keep_photons_end is refused
+        here, before any batch is read or uploaded (the photons are not gathered)."""
         if keep_photons_end:
             raise NotImplementedError('ShardedSimulation: keep_photons_end is not gathered; use Simulation')
-        yield from Simulation._emit(self, b, **kw)
+        return Simulation.simulate(self, iterable, **kw)

@@ -25,7 +25,6 @@ std::string &last_error() {
 }  // namespace chr
 
 extern "C" const char *chr_last_error(void) { return chr::last_error().c_str(); }
-extern "C" int chr_version(void) { return 1; }
 
 namespace {
 

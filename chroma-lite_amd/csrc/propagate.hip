@@ -3033,7 +3033,8 @@ __device__ __forceinline__ uint32_t slot_head(uint32_t n, const HeadNext &h) {
     h.mode[0] = m;
     h.n_out[0] = n;
     // the host's copy of (mode, length), in pinned host memory: read once the
-    // slot's end event has completed (no copy dispatch per slot)
+    // slot's trace-start event (ev[2] of device_slots, recorded after this head)
+    // has completed (no copy dispatch per slot)
     if (h.host_ring) { h.host_ring[0] = m; h.host_ring[1] = n; }
     if (m != STEP_IDLE) h.ray_counter[0] = 0u;
     return m;
@@ -3945,7 +3946,8 @@ struct SlotCtl {
     int32_t remaining;     // steps left (max_steps - step)
     uint32_t tail_below;   // the nsteps policy's threshold, nthreads_per_block * 128
     // chr_propagate_batches: the slot's tail kernel runs on its own stream
-    // (after the slot's one-step kernels, ev1), so the caller's stream moves on
+    // (after the slot's trace-start event, or its one-step kernels' ev1 with every
+    // slot event recorded), so the caller's stream moves on
     // to the next batch while a tail's long-lived photons finish.  The tail
     // leaves no queue (it runs every remaining step): its alive bits go to
     // tail_masks and the slot's scan / scatter skip the tail mode.
@@ -4188,7 +4190,14 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
     if (tail && sc && sc->tail_stream) {   // the tail on its own stream (chr_propagate_batches)
         // the tail kernel needs the slot's head (its mode) and the previous slot's scatter (its
         // queue): both come before the slot's trace-start event; with every slot event
-        // recorded (CHR_SLOT_TIMING=1) it waits for the slot's one-step part as before
+        // recorded (CHR_SLOT_TIMING=1) it waits for the slot's one-step part as before.
+        // Invariant that makes the earlier event enough: every kernel queued on `stream`
+        // for this slot (classify / binning, trace, shade, scan, scatter) exits at once
+        // when the slot's mode is STEP_TAIL (their mode / want checks), so none of them
+        // touches the photons, queues or RNG slots the tail works on; and the RNG slot
+        // states the tail reads were last written by kernels ordered before ev0 on
+        // `stream`, or by the previous batch's tail, earlier on this same tail stream.
+        // tests/test_gpu_batches.py checks CHR_SLOT_TIMING=0 / 1 give identical photons.
         hipEvent_t dep = ev1 ? ev1 : evt0;
         if (!dep) return chr::fail(CHR_ERR_INVALID, "launch_step: a tail stream needs a slot event");
         hipStream_t ts = sc->tail_stream;

@@ -495,6 +495,10 @@ int chr_device_profile_fetch(uint64_t *h_calls, uint64_t *h_cycles, int32_t n, u
 /* ------------------------------------------------------------- misc */
 const char *chr_last_error(void);
 int chr_version(void);
+/* sha256 (16 hex) of the sources this library was built from (tools/source_sha.py:
+ * csrc/ and include/), compiled in by the Makefile; bench.py compares it with the
+ * tree's own (so_source_sha vs kernel_source_sha) */
+const char *chr_source_sha(void);
 
 #ifdef __cplusplus
 }

@@ -65,6 +65,7 @@ class StubWorkload(object):
                 'launch_ms': [x for s in stats for x in s.trace_launch_ms], 'launch_rays': [700, 300],
                 'overflows': 0, 'flat': 0, 'flat_whole': 0, 'detected_last_step': 0,
                 'channel_hits_all_ranks': int(self.reduced['counts'].sum().item()), 'tail': [],
+                'setup': dict({'geometry_s': 0.0, 'upload_s': 0.0, 'setup_s': 0.0}, **bench.host_memory()),
                 'calls': self.calls}
 
     def untimed_passes(self):
@@ -76,14 +77,27 @@ class StubWorkload(object):
     def detector_info(self):
         return {'triangles': 0, 'bvh_nodes': 0, 'channels': 4}
 
+    def _parity(self, rank, n, full, threads):
+        return {'rank': rank, 'n': n, 'flags_equal': True, 'last_hit_equal': True, 'channel_equal': True,
+                'threads': threads, 'full': full, 'oracle_on_rank': self.rank,
+                'rng_first_subsequence': bench.rng_first_subsequence(rank, self.args.nthreads_per_block *
+                                                                     self.args.max_blocks)}
+
+    def gpu_sample(self, n, pipeline):
+        # what a rank > 0 sends to rank 0: its photons (here a stand-in array) and the run's facts
+        import numpy as np
+        return {'rank': self.rank, 'n': int(n), 'path': 'stub', 'stack_overflows': 0,
+                'photons': {'flags': np.full(n, self.rank, np.uint32)}}
+
     def check(self, full, budget_s, threads, sample):
-        par = {'rank': self.rank, 'n': 100 if full else min(self.nphotons, sample), 'flags_equal': True,
-               'last_hit_equal': True, 'channel_equal': True, 'threads': threads, 'full': full,
-               'rng_first_subsequence': bench.rng_first_subsequence(self.rank, self.args.nthreads_per_block *
-                                                                    self.args.max_blocks)}
         stats = {'nodes_visited': 1000, 'tris_tested': 100, 'traversals': 10}
         cpu = {'value': 1.0, 'unit': 'photons/s', 'cores': threads, 'kind': 'port', 'sample': 'stub'} if full else None
-        return cpu, stats, par
+        return cpu, stats, self._parity(self.rank, 100 if full else min(self.nphotons, sample), full, threads)
+
+    def check_rank(self, sample, threads):
+        # rank 0 checks another rank's sample: the sample must be that rank's own
+        assert self.rank == 0 and (sample['photons']['flags'] == sample['rank']).all()
+        return self._parity(sample['rank'], sample['n'], False, threads)
 
 
 bench.WORKLOAD = StubWorkload

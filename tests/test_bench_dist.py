@@ -107,11 +107,41 @@ def test_bench_gpus2_spawns_two_ranks():
     assert par['all_ranks_equal'] and [p['rank'] for p in par['per_rank']] == [0, 1]
     assert par['per_rank'][0]['full'] and not par['per_rank'][1]['full']
     assert par['per_rank'][1]['rng_first_subsequence'] == 524288
+    # rank 1's sample went to rank 0, which ran its oracle check
+    assert par['per_rank'][1]['oracle_on_rank'] == 0 and par['per_rank'][1]['n'] == 1000
+    for r in d['ranks']:
+        assert r['host_rss_gb'] > 0 and r['host_peak_rss_gb'] >= r['host_rss_gb'] - 1e-3
+        assert set(r['setup']) >= {'geometry_s', 'upload_s', 'setup_s', 'host_rss_gb'}
     rl = line['roofline']
     assert [r['rank'] for r in rl['per_rank']] == [0, 1]
     # rank 1's launches: 2 ms+1 over 2 launches of 1000 rays / step -> its own frac
     assert rl['per_rank'][1]['avg_launch_ms'] == pytest.approx(1.5)
     assert line['cpu_baseline']['cores'] >= 1
+
+
+def test_bench_gpus8_line():
+    """The driver's 8-GPU command (`bench.py --gpus 8`), rehearsed with 8 gloo ranks:
+    8 ranks seen, the max-over-ranks time, every rank's parity (ranks 1-7 checked by
+    rank 0's oracle on their own RNG subsequences), roofline and host memory /
+    setup fields -- what a first 8-GPU run needs to be diagnosable."""
+    rc, line, err = _stub_bench(['--gpus', '8', '--steps', '2', '--warmup', '1', '--photons', '1000',
+                                 '--pipeline-depth', '2', '--sequential-steps', '1', '--detector', 'small',
+                                 '--rank-parity-photons', '500'], timeout=300)
+    assert rc == 0, err
+    assert line['n_gpus'] == 8
+    d = line['detail']
+    assert d['ranks_seen'] == 8 and [r['rank'] for r in d['ranks']] == list(range(8))
+    assert line['ms_per_step'] >= 80.0                  # rank 7 sleeps 80 ms per step: the max over ranks
+    assert line['value'] == pytest.approx(8 * 1000 * 2 / (line['ms_per_step'] * 2 / 1e3))
+    assert d['channel_hits_all_ranks'] == sum(1 + r for r in range(8))
+    par = line['parity']
+    assert par['all_ranks_equal'] and [p['rank'] for p in par['per_rank']] == list(range(8))
+    for r, p in enumerate(par['per_rank']):
+        assert p['rng_first_subsequence'] == r * 524288 and p['oracle_on_rank'] == 0
+        assert p['n'] == (100 if r == 0 else 500)
+    assert [r['rank'] for r in line['roofline']['per_rank']] == list(range(8))
+    for r in d['ranks']:
+        assert r['host_rss_gb'] > 0 and 'setup_s' in r['setup']
 
 
 def test_bench_total_photons_is_strong_scaling():

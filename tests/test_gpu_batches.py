@@ -217,3 +217,22 @@ def test_max_steps_zero_and_negative(cuda, small_detector):
         with pytest.raises(_native.NativeError, match='max_steps'):
             call()
     assert np.array_equal(rng.get(), rng0)
+
+
+def test_batches_slot_timing_modes_identical(cuda, small_detector, monkeypatch):
+    """The tail stream's dependency on a slot: its trace-start event by default,
+    the end of the slot's one-step kernels with every slot event recorded
+    (CHR_SLOT_TIMING=1).  Every kernel of a tail-mode slot on the caller's
+    stream exits at once, so both give the same photons and RNG states."""
+    from chroma import gpu
+    det = gpu.GPUDetector(small_detector)
+    sources = _sources([30000, 70000, 5000, 120000], seed=17)
+    out = {}
+    for mode in ('t', '0', '1'):    # the default (trace launch pairs), none, every slot event
+        monkeypatch.setenv('CHR_SLOT_TIMING', mode)
+        out[mode] = _run(det, sources, 64, 256, 1000, batched=True)
+    for mode in ('0', '1'):
+        for i, (a, b) in enumerate(zip(out['t'][0], out[mode][0])):
+            _same(a, b, 'CHR_SLOT_TIMING=%s batch %d' % (mode, i))
+        assert np.array_equal(out['t'][1], out[mode][1])
+    assert sum(s.tail_photons for s in out['t'][2]) > 0

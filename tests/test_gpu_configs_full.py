@@ -10,6 +10,8 @@ round 3, at their own sizes and launch shape (512 x 1024
 * C4: the shard rank 7 of an 8-GPU run propagates (photon seed 20260102+7,
   RNG subsequences 7*524288 + slot, bench.py rng_first_subsequence) on
   demo.detector(), 1.1M photons, sequential and pipelined (two batches);
+* C4's rank 7 on the 29k-PMT geometry with a first batch of 2^20 + 50,000
+  photons: the binned first step under first_subsequence = 7*524288;
 * C3 29k-PMT variant (the headline geometry, 169.9M triangles) at 1.1M photons.
 
 Bit-exact on history flags, last-hit triangles and channels; floats within
@@ -150,13 +152,43 @@ def test_c4_rank7_shard(cuda, demo_geo, pipelined):
     assert all(s.trace_launches >= 1 for s in stats)
 
 
+@pytest.fixture(scope='module')
+def geo29k():
+    return _geometry('29k')
+
+
 @pytest.mark.timeout(1200)
-def test_c3_29k_detector_parity(cuda):
+@pytest.mark.parametrize('pipelined', [False, True])
+def test_c4_rank7_shard_29k(cuda, geo29k, pipelined):
+    """C4's rank 7 on the headline geometry (29,007 PMTs): its own photon seed
+    and RNG subsequences from 7*524288, a first batch of 2^20 + 50,000 photons
+    -- so the direction-binned first step runs under the rank's non-zero
+    first_subsequence -- then a second batch of 200,000 continuing its RNG
+    states; one propagate call each or pipelined; HIP == oracle."""
+    from chroma import gpu
+    from chroma.photon_source import isotropic
+    rank = 7
+    first = _bench().rng_first_subsequence(rank, NSLOTS)
+    assert first == 7 * 524288
+    n0 = (1 << 20) + 50_000
+    photons = isotropic(n0 + 200_000, seed=PHOTON_SEED + rank)
+    batches = [photons[:n0], photons[n0:]]
+    got, rng, stats = _gpu(gpu.GPUDetector(geo29k), batches, first, pipelined)
+    hosts, st = _oracle(geo29k, batches, first)
+    for i in range(2):
+        _check(got[i], hosts[i], geo29k, 'C4 29k rank 7 batch %d (%s)' % (i, 'pipelined' if pipelined else 'sequential'))
+    assert np.array_equal(rng.reshape(-1), st.reshape(-1))
+    assert stats[0].trace_launches >= 1 and all(s.stack_overflows == 0 for s in stats)
+    assert ((hosts[0].flags & 4) != 0).sum() > 10000
+
+
+@pytest.mark.timeout(1200)
+def test_c3_29k_detector_parity(cuda, geo29k):
     """The headline geometry (29,007 PMTs, 169.9M triangles) at 1.1M photons
     of the bench source: HIP == oracle."""
     from chroma import gpu
     from chroma.photon_source import isotropic
-    geo = _geometry('29k')
+    geo = geo29k
     assert geo.num_channels() == 29007
     photons = isotropic(1_100_000, seed=PHOTON_SEED)
     got, rng, stats = _gpu(gpu.GPUDetector(geo), [photons], 0, pipelined=False)

@@ -135,3 +135,70 @@ def test_sharded_simulation_two_ranks(tmp_path, hits):
         assert np.array_equal(got[0]['ch_q_%d' % e], (q.astype(np.float32) * unit).astype(np.float32))
         assert np.array_equal(got[0]['ch_flags_%d' % e], fl)
     assert len(gidx) > 100
+
+
+SIZES = (5000, 1, 4000, 3000)   # photons_per_batch=1: one batch per event; the 1-photon batch leaves rank 0 empty
+
+
+def _pipe_worker(rank, world, port, out_dir, hits):
+    sys.path.insert(0, os.path.join(ROOT, 'chroma-lite_amd'))
+    os.environ['LOCAL_RANK'] = '0'
+    import torch.distributed as dist
+    dist.init_process_group('gloo', init_method='tcp://127.0.0.1:%d' % port, rank=rank, world_size=world)
+    try:
+        from chroma.photon_source import isotropic
+        from chroma.sim import ShardedSimulation
+        ph = isotropic(sum(SIZES), seed=43)
+        cuts = np.cumsum((0,) + SIZES)
+        out = {}
+        for depth in (8, 1):
+            sim = ShardedSimulation(_detector(), seed=5, nthreads_per_block=NTPB, max_blocks=MAXB, hits=hits)
+            sim.pipeline_batches = depth
+            evs = list(sim.simulate([ph[cuts[i]:cuts[i + 1]] for i in range(len(SIZES))], run_daq=False,
+                                    keep_hits=False, photons_per_batch=1))
+            out['pipeline_%d' % depth] = np.array(sim.last_pipeline)
+            for i, ev in enumerate(evs):
+                if ev.flat_hits is None:
+                    assert rank != 0 and hits == 'root'
+                    continue
+                for f in ('flags', 'last_hit_triangles', 'channel', 't'):
+                    out['%s_%d_%d' % (f, depth, i)] = getattr(ev.flat_hits, f)
+                out['pos_%d_%d' % (depth, i)] = ev.flat_hits.pos
+            if depth == 8:   # keep_photons_end is refused before any batch is uploaded
+                try:
+                    sim.simulate([ph[:10]], keep_photons_end=True)
+                    out['refused'] = np.array(0)
+                except NotImplementedError:
+                    out['refused'] = np.array(1)
+        np.savez(os.path.join(out_dir, 'rank%d.npz' % rank), **out)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('hits', ['root', 'all'])
+def test_sharded_simulation_pipelined(tmp_path, hits):
+    """DAQ off: each rank propagates its shards of all batches in ONE pipelined
+    propagate_batches call (empty shards left out of it: rank 0 holds nothing of
+    the 1-photon batch), then the hits of every batch are gathered in batch
+    order.  The events equal the depth-1 run's (one propagate per batch)."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip('no HIP device')
+    import torch.multiprocessing as mp
+    mp.spawn(_pipe_worker, args=(2, _free_port(), str(tmp_path), hits), nprocs=2, join=True)
+    got = [np.load(os.path.join(str(tmp_path), 'rank%d.npz' % r)) for r in range(2)]
+    for g in got:
+        assert tuple(g['pipeline_8']) == (len(SIZES), 1) and tuple(g['pipeline_1']) == (len(SIZES), 0)
+        assert int(g['refused']) == 1
+    ranks_with_hits = (0, 1) if hits == 'all' else (0,)
+    nhits = 0
+    for r in ranks_with_hits:
+        for i in range(len(SIZES)):
+            for f in ('flags', 'last_hit_triangles', 'channel', 't', 'pos'):
+                a, b = got[r]['%s_8_%d' % (f, i)], got[r]['%s_1_%d' % (f, i)]
+                assert np.array_equal(a, b), (r, i, f)
+                assert np.array_equal(a, got[0]['%s_8_%d' % (f, i)]), (r, i, f)
+            nhits += len(got[r]['flags_8_%d' % i])
+    if hits == 'root':
+        assert 'flags_8_0' not in got[1].files
+    assert nhits > 50

@@ -30,6 +30,17 @@ def test_version_and_error_string():
     assert isinstance(l.chr_last_error(), bytes)
 
 
+def test_library_built_from_this_tree():
+    """The .so travels prebuilt with the tree (the GPU box does not rebuild it):
+    the source sha compiled into it (chr_source_sha, csrc/Makefile) must be
+    the sha of the sources beside it (tools/source_sha.py)."""
+    import sys
+    from chroma.gpu import _native
+    sys.path.insert(0, os.path.join(ROOT, 'tools'))
+    from source_sha import kernel_source_sha
+    assert _native.lib().chr_source_sha().decode() == kernel_source_sha(ROOT)
+
+
 def test_invalid_arguments_fail_loudly():
     import pytest
     from chroma.gpu import _native
