@@ -50,8 +50,13 @@ DEVICE_REGION_NAMES = {
     14: 'shade_kernel',
     15: 'tail_kernel',
     16: 'trace_drain',
+    17: 'lone_refill',
+    18: 'lone_fetch',
+    19: 'lone_expand',
+    20: 'lone_tris',
+    21: 'lone_walk',
 }
-NREGIONS = 17        # CHR_PROF_NREGIONS
+NREGIONS = 22        # CHR_PROF_NREGIONS
 COUNTERS = 64        # CHR_PROF_COUNT (profile.h:16)
 
 

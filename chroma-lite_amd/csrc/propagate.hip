@@ -2014,6 +2014,39 @@ struct LdsRowsT {
 };
 typedef LdsRowsT<BLOCK> LdsRows;
 
+// Where the lone walker's iteration goes (walk_segment<64>, the tail's
+// long-lived photon; device profile build only): wave-cycles of its stack
+// refill, its fetch (the loads issued and waited for at once, so the expansion
+// after it is compute only), the children's slab tests + near child + pushes +
+// triangle list, and the triangle tests + hit reduction; calls = iterations.
+template <bool ON>
+struct LoneProf {
+    __device__ __forceinline__ void begin() {}
+    __device__ __forceinline__ void tick(int) {}
+    __device__ __forceinline__ void wait_loads() {}
+    __device__ __forceinline__ void flush() {}
+};
+#ifdef CHR_DEVICE_PROFILE
+template <>
+struct LoneProf<true> {
+    unsigned long long cyc[4] = {0ull, 0ull, 0ull, 0ull}, iters = 0ull, t = 0ull;
+    __device__ __forceinline__ void begin() { t = __builtin_amdgcn_s_memtime(); iters++; }
+    __device__ __forceinline__ void tick(int i) {
+        const unsigned long long now = __builtin_amdgcn_s_memtime();
+        cyc[i] += now - t;
+        t = now;
+    }
+    __device__ __forceinline__ void wait_loads() { __builtin_amdgcn_s_waitcnt(0); }
+    __device__ __forceinline__ void flush() {
+        if (__lane_id() == 0) {
+            for (int i = 0; i < 4; ++i) atomicAdd(&chr_prof_cycles[CHR_PROF_LONE_REFILL + i], cyc[i]);
+            atomicAdd(&chr_prof_calls[CHR_PROF_LONE_WALK], iters);
+            atomicAdd(&chr_prof_cycles[CHR_PROF_LONE_WALK], cyc[0] + cyc[1] + cyc[2] + cyc[3]);
+        }
+    }
+};
+#endif
+
 // All 64 lanes call this (converged).  act: the segment has a ray (segment-
 // uniform).  Returns the nearest triangle (-1: none) and its distance in
 // every lane of the segment.  One dependent global fetch per iteration: the
@@ -2063,13 +2096,24 @@ __device__ __forceinline__ int walk_segment(const DevGeom &g, bool act, V3 o, V3
     int pb = 0;                                       // their list buffer (double-buffered)
     bool done = !act;
     iters = 0;
-    while (__ballot(!done) != 0) {
-        if (done) continue;
+    LoneProf<GS == 64> lp;
+    // GS = 64: the loop state (done, the stack depth, the listed triangles) is
+    // wave-uniform, said explicitly (uu) so the loop branches on scalars instead of
+    // exec masks
+    while (true) {
+        if constexpr (GS == 64) {
+            if (done) break;
+        } else {
+            if (__ballot(!done) == 0) break;
+            if (done) continue;
+        }
         iters++;
+        lp.begin();
         // cursors without a node take the topmost unculled stack entries: a
         // window of up to 8 entries read at once, the r-th empty cursor (in
         // sub-group order) taking the r-th unculled entry (from the top)
         unsigned long long em = __ballot(k == 0u && cur == INVALID) & segmask;
+        const uint32_t lead = lane & ~7u;                 // my sub-group's leader lane
         const bool refill = em != 0 && sp > 0;
         while (em != 0 && sp > 0) {
             const int W = sp < 8 ? sp : 8;
@@ -2096,32 +2140,57 @@ __device__ __forceinline__ int walk_segment(const DevGeom &g, bool act, V3 o, V3
                 tlist[(pb ^ 1) * TAIL_TRI + 2 * rho + 1] = et;
             }
             __builtin_amdgcn_wave_barrier();
-            const bool empty = k == 0u && cur == INVALID;
-            const int rnk = __popcll(em & below);
-            const unsigned long long taken = __ballot(empty && rnk < take) & segmask;
+            // GS = 64: all 8 lanes of an empty cursor's sub-group read the entry it
+            // takes (an LDS broadcast), no shuffle from the leader follows; otherwise
+            // the leader takes it and its sub-group reads it by shuffle below
+            const bool empty = GS == 64 ? ((em >> lead) & 1ull) != 0 : (k == 0u && cur == INVALID);
+            const int rnk = __popcll(em & (GS == 64 ? ((1ull << lead) - 1ull) : below));
+            const unsigned long long taken = __ballot(k == 0u && empty && rnk < take) & segmask;
             if (empty && rnk < take) {
                 cur = tlist[(pb ^ 1) * TAIL_TRI + 2 * rnk];
                 cur_t = __uint_as_float(tlist[(pb ^ 1) * TAIL_TRI + 2 * rnk + 1]);
             }
             __builtin_amdgcn_wave_barrier();
-            sp -= consumed;
+            sp = (int)uu((uint32_t)(sp - consumed));
             em &= ~taken;
         }
-        if (refill) {   // the sub-group's cursor, from its leader lane
-            cur = (uint32_t)__shfl((int)cur, (int)(lane & ~7u));
-            cur_t = __shfl(cur_t, (int)(lane & ~7u));
+        if (GS != 64 && refill) {   // the sub-group's cursor, from its leader lane
+            cur = (uint32_t)__shfl((int)cur, (int)lead);
+            cur_t = __shfl(cur_t, (int)lead);
         }
+        lp.tick(0);
         const bool walking = (__ballot(cur != INVALID) & segmask) != 0;
-        if (!walking && Tp == 0) { done = true; continue; }
-        // fetch: this iteration's nodes and the previous iteration's triangles together
-        uint4 h = make_uint4(0u, 0u, 0u, 0u), a1 = h, a2 = h, a3 = h, a4 = h, a5 = h;
-        if (cur != INVALID) load_node(g, top, cur, h, a1, a2, a3, a4, a5);
+        if (!walking && Tp == 0) {
+            done = true;
+            continue;
+        }
+        // fetch: this iteration's nodes and the previous iteration's triangles together,
+        // one dependent round trip.  The triangle list is read first, and the load
+        // registers stay undefined where a lane has no node / triangle (nothing reads
+        // them there): zero-filling them let the compiler reuse a register still owed
+        // by a node load, so it waited for the nodes before issuing the triangles.
+        // (GS = 64 only: in the run-time-width walk, trace_kernel's drain, the
+        // zero-filled form keeps its register allocation without spills)
         const bool has_tri = L < Tp;
-        float4 r0 = make_float4(0.0f, 0.0f, 0.0f, 0.0f), r1 = r0, r2 = r0, r3 = r0;
-        const float4 *rr = nullptr;
-        if (has_tri) {
-            rr = g.wtri + 4 * (size_t)tlist[pb * TAIL_TRI + L];
-            r0 = gld(rr); r1 = gld(rr + 1); r2 = gld(rr + 2); r3 = gld(rr + 3);
+        uint4 h, a1, a2, a3, a4, a5;
+        float4 r0, r1, r2, r3;
+        const float4 *rr;
+        if constexpr (GS == 64) {
+            const uint32_t trec = has_tri ? tlist[pb * TAIL_TRI + L] : 0u;
+            if (cur != INVALID) load_node(g, top, cur, h, a1, a2, a3, a4, a5);
+            rr = g.wtri + 4 * (size_t)trec;
+            if (has_tri) { r0 = gld(rr); r1 = gld(rr + 1); r2 = gld(rr + 2); r3 = gld(rr + 3); }
+            lp.wait_loads();
+            lp.tick(1);
+        } else {
+            h = make_uint4(0u, 0u, 0u, 0u); a1 = h; a2 = h; a3 = h; a4 = h; a5 = h;
+            if (cur != INVALID) load_node(g, top, cur, h, a1, a2, a3, a4, a5);
+            r0 = make_float4(0.0f, 0.0f, 0.0f, 0.0f); r1 = r0; r2 = r0; r3 = r0;
+            rr = nullptr;
+            if (has_tri) {
+                rr = g.wtri + 4 * (size_t)tlist[pb * TAIL_TRI + L];
+                r0 = gld(rr); r1 = gld(rr + 1); r2 = gld(rr + 2); r3 = gld(rr + 3);
+            }
         }
         // expand: sub-group j's 8 lanes slab-test the 8 children of its node
         bool inner = false, leafhit = false;
@@ -2185,6 +2254,7 @@ __device__ __forceinline__ int walk_segment(const DevGeom &g, bool act, V3 o, V3
         if (cnt > 1u) tlist[(pb ^ 1) * TAIL_TRI + pre + 1] = first + 1u;
         if (cnt > 2u) tlist[(pb ^ 1) * TAIL_TRI + pre + 2] = first + 2u;
         if (cnt > 3u) tlist[(pb ^ 1) * TAIL_TRI + pre + 3] = first + 3u;
+        lp.tick(2);
         // test the previous iteration's triangles (entries beyond the segment's
         // lanes, rare, are fetched now)
         float lbest = best;
@@ -2217,9 +2287,16 @@ __device__ __forceinline__ int walk_segment(const DevGeom &g, bool act, V3 o, V3
             unsigned long long lkey = lid == -1 ? NONE : (((unsigned long long)__float_as_uint(lbest) << 32) | lrank);
             if ((hm & (hm - 1)) == 0) {
                 const int src = __ffsll((long long)hm) - 1;
-                lkey = ((unsigned long long)(uint32_t)__shfl((int)(uint32_t)(lkey >> 32), src) << 32) |
-                       (uint32_t)__shfl((int)(uint32_t)lkey, src);
-                lid = __shfl(lid, src);
+                if (GS == 64) {   // src is wave-uniform: scalar reads of the winning lane
+                    lkey = ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(lkey >> 32), src)
+                            << 32) |
+                           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)lkey, src);
+                    lid = __builtin_amdgcn_readlane(lid, src);
+                } else {
+                    lkey = ((unsigned long long)(uint32_t)__shfl((int)(uint32_t)(lkey >> 32), src) << 32) |
+                           (uint32_t)__shfl((int)(uint32_t)lkey, src);
+                    lid = __shfl(lid, src);
+                }
             } else {
                 for (int off = 1; off < Gs; off <<= 1) {
                     const unsigned long long ok = __shfl_xor(lkey, off);
@@ -2231,10 +2308,13 @@ __device__ __forceinline__ int walk_segment(const DevGeom &g, bool act, V3 o, V3
             best_rank = uu((uint32_t)lkey);
             best_id = (int)uu((uint32_t)lid);
         }
-        Tp = Tn;
+        Tp = uu(Tn);
+        sp = (int)uu((uint32_t)sp);
         pb ^= 1;
+        lp.tick(3);
         if (cur != INVALID && cur_t > best) cur = INVALID;
     }
+    lp.flush();
     min_distance = best_id == -1 ? -1.0f : best;
     return best_id;
 }
@@ -2366,9 +2446,19 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_tail_kernel(const DevGe
             for (int i = 0; i < si && m != 0; ++i) m &= m - 1;
             const int src = m != 0 ? __ffsll((long long)m) - 1 : (int)(lane & ~7u);
             const bool act = m != 0;
-            const V3 o = v3(__shfl(p.pos.x, src), __shfl(p.pos.y, src), __shfl(p.pos.z, src));
-            const V3 dd = v3(__shfl(p.dir.x, src), __shfl(p.dir.y, src), __shfl(p.dir.z, src));
-            const uint32_t last = (uint32_t)__shfl(p.last_hit, src);
+            V3 o, dd;
+            uint32_t last;
+            if (w == 1) {   // one walker: its lane is wave-uniform, scalar reads instead of LDS shuffles
+                const int s1 = __ffsll((long long)wm) - 1;
+                auto rl = [s1](float x) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), s1)); };
+                o = v3(rl(p.pos.x), rl(p.pos.y), rl(p.pos.z));
+                dd = v3(rl(p.dir.x), rl(p.dir.y), rl(p.dir.z));
+                last = (uint32_t)__builtin_amdgcn_readlane(p.last_hit, s1);
+            } else {
+                o = v3(__shfl(p.pos.x, src), __shfl(p.pos.y, src), __shfl(p.pos.z, src));
+                dd = v3(__shfl(p.dir.x, src), __shfl(p.dir.y, src), __shfl(p.dir.z, src));
+                last = (uint32_t)__shfl(p.last_hit, src);
+            }
             const uint32_t seg0 = lane & ~(uint32_t)(Gs - 1);
             float sd;
             uint32_t it;
@@ -2377,10 +2467,15 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_tail_kernel(const DevGe
                                                   top, overflow, sd, it)
                                : walk_segment<0>(g, act, o, dd, last, Gs, LdsFlat{wstack + seg0 / 8 * TAIL_STACK * 2},
                                                  TAIL_STACK * Gs / 8, LdsFlat{wtris + 4 * seg0}, top, overflow, sd, it);
-            const int mine = __popcll(wm & ((1ull << (lane & ~7u)) - 1ull)) * Gs;   // my group's segment
-            tri = __shfl(st, mine);
-            dist = __shfl(sd, mine);
-            it = (uint32_t)__shfl((int)it, mine);
+            if (Gs == 64) {   // one segment: every lane already holds the result
+                tri = st;
+                dist = sd;
+            } else {
+                const int mine = __popcll(wm & ((1ull << (lane & ~7u)) - 1ull)) * Gs;   // my group's segment
+                tri = __shfl(st, mine);
+                dist = __shfl(sd, mine);
+                it = (uint32_t)__shfl((int)it, mine);
+            }
             if (walk) {
                 iters += it;
                 walk_ticks += __builtin_amdgcn_s_memrealtime() - tw0;
@@ -3726,7 +3821,10 @@ static int trace_refill_r() {
 }
 // CHR_TRACE_LAYOUT (A/B): 0 256-thread workgroups, 12 LDS stack entries per lane;
 // 1 1024-thread workgroups (one per CU), 11 entries, the top TOP_NODES nodes of
-// the tree in LDS (stage_top); 2 the same without the top nodes (control)
+// the tree in LDS (stage_top); 2 the same without the top nodes (control).
+// (r04 ab3, removed: a combined step -- every lane fetching its node AND its next
+// parked triangle each iteration -- ran trace 38.8 ms/step at 4 waves/SIMD (200 B
+// of spills) and 17.2 at 3, against 14.35 for the wave-wide node / triangle choice)
 static int trace_layout() {
     const char *e = getenv("CHR_TRACE_LAYOUT");
     return e ? atoi(e) : 0;
@@ -5090,10 +5188,13 @@ extern "C" int chr_propagate_batches(const chr_geometry *g, const chr_photons *p
 static int select_common(const chr_photons *ph, int32_t start, int32_t n, uint32_t state, const uint32_t *solid_map,
                          const int32_t *s2c, int mode, const chr_photons *out, int32_t *channels, uint32_t *count,
                          hipStream_t stream) {
-    if (!photons_ok(ph) || !count) return chr::fail(CHR_ERR_INVALID, "selection: null argument");
-    if (mode == 0 && (!solid_map || !s2c)) return chr::fail(CHR_ERR_INVALID, "hits: solid map / channel map missing");
+    if (!count) return chr::fail(CHR_ERR_INVALID, "selection: null count");
     *count = 0;
-    if (n <= 0) return CHR_OK;
+    // an empty selection needs no photon arrays (a GPUPhotons of 0 photons, e.g. a
+    // rank's empty shard of a batch, has none)
+    if (n <= 0 && ph) return CHR_OK;
+    if (!photons_ok(ph)) return chr::fail(CHR_ERR_INVALID, "selection: null argument");
+    if (mode == 0 && (!solid_map || !s2c)) return chr::fail(CHR_ERR_INVALID, "hits: solid map / channel map missing");
     const uint32_t nwords = (uint32_t)((n + 63) / 64);
     void *buf;
     int rc = scratch_get((mask_scan_words((uint64_t)n) + 8) * 4 + 64, &buf);

@@ -481,7 +481,13 @@ enum {
     CHR_PROF_SHADE_KERNEL = 14,       /* whole shade_kernel */
     CHR_PROF_TAIL_KERNEL = 15,        /* whole propagate_tail_kernel */
     CHR_PROF_TRACE_DRAIN = 16,        /* trace_kernel: a wave's last <= 8 walks, whole-wave (calls = walks) */
-    CHR_PROF_NREGIONS = 17,
+    /* the tail's lone walker (walk_segment<64>), wave-cycles per phase of its iterations: */
+    CHR_PROF_LONE_REFILL = 17,        /* cursors refilled from the shared stack */
+    CHR_PROF_LONE_FETCH = 18,         /* nodes + triangles loaded (issued and waited for) */
+    CHR_PROF_LONE_EXPAND = 19,        /* children slab-tested, near child, pushes, triangle list */
+    CHR_PROF_LONE_TRIS = 20,          /* triangles tested, nearest hit reduced */
+    CHR_PROF_LONE_WALK = 21,          /* all of the above (calls = iterations) */
+    CHR_PROF_NREGIONS = 22,
     CHR_PROF_COUNT = 64               /* counter array length (profile.h:16) */
 };
 /* 1 when this library was built with the device profile, else 0 */

@@ -65,4 +65,5 @@ def test_profile_library_exports():
     assert lib.chr_device_profile_enabled() == 1
     assert lib.chr_version() == 1
     names = __import__('chroma.gpu.profiler', fromlist=['x']).DEVICE_REGION_NAMES
-    assert len(names) == 17 and names[0] == 'intersect_mesh' and names[3] == 'intersect_box'
+    assert len(names) == 22 and names[0] == 'intersect_mesh' and names[3] == 'intersect_box'
+    assert names[21] == 'lone_walk'
