@@ -102,6 +102,11 @@ __device__ __forceinline__ float4 gld(const float4 *p) {
     const chr_f32x4 v = *(const CHR_GLOBAL chr_f32x4 *)p;
     return make_float4(v.x, v.y, v.z, v.w);
 }
+typedef uint32_t chr_u32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint2 gld_lo2(const void *p) {   // the first 8 bytes at p (global_load_dwordx2)
+    const chr_u32x2 v = *(const CHR_GLOBAL chr_u32x2 *)p;
+    return make_uint2(v.x, v.y);
+}
 
 // ---------------------------------------------------------------- geometry.h
 // The top of the wide BVH in LDS (north_star: "BVH nodes ... staged through
@@ -1570,7 +1575,8 @@ struct PropagateArgs {
     const uint32_t *dev_n;
     const uint32_t *mode;
     uint32_t prio;                     // tail kernel: bit 0 raise its waves' issue priority (s_setprio),
-                                       // bit 1 the whole-wave walk specialised for one walker (GS = 64)
+                                       // bit 1 the whole-wave walk specialised for one walker (GS = 64),
+                                       // bit 2 that walker software-pipelined (walk_lone)
     uint32_t want;
     // tail kernel, work-queue mode (nullptr: group g runs queue positions g, g + cap, ...): a
     // zeroed counter the photon groups take queue positions from, for queues no longer than
@@ -1815,8 +1821,11 @@ struct QueuedPhoton {
     int last_hit;
     int2 hit;
 };
-__device__ __forceinline__ void fetch_queued(const PropagateArgs &a, uint32_t q, QueuedPhoton &f) {
-    f.pid = a.input_queue[q];
+// the photon at queue position q; pid: its queue entry when already loaded (the
+// shade kernel's two-ahead prefetch), else read here first (a dependent load)
+__device__ __forceinline__ void fetch_queued(const PropagateArgs &a, uint32_t q, QueuedPhoton &f,
+                                             uint32_t pid = 0xFFFFFFFFu) {
+    f.pid = pid != 0xFFFFFFFFu ? pid : a.input_queue[q];
     f.history = a.flags[f.pid] & 0xFFFFu;   // photon.h:29
     f.pos = load3(a.pos, f.pid);
     f.dir = load3(a.dir, f.pid);
@@ -1828,7 +1837,10 @@ __device__ __forceinline__ void fetch_queued(const PropagateArgs &a, uint32_t q,
     f.hit = a.hits[q];
     f.walk = a.winv ? a.winv[q] : 0u;
 }
-template <int MINW>
+// P2: the queue entry of the photon two positions ahead is loaded one iteration
+// early, so the next photon's state loads go out without first waiting for its
+// queue entry (a dependent round trip per photon otherwise)
+template <int MINW, bool P2 = false>
 __global__ __launch_bounds__(BLOCK, MINW) void shade_kernel(const DevGeom *__restrict__ gdev, PropagateArgs a,
                                                             uint32_t cap) {
     if (a.mode && *a.mode != a.want) return;
@@ -1845,10 +1857,13 @@ __global__ __launch_bounds__(BLOCK, MINW) void shade_kernel(const DevGeom *__res
     pf.start(P_OTHER);
     QueuedPhoton nx;
     if (slot < n) fetch_queued(a, slot, nx);
+    uint32_t pid2 = 0xFFFFFFFFu;                       // P2: queue entry of position pos + cap
+    if (P2 && slot + cap < n) pid2 = a.input_queue[slot + cap];
     uint32_t pos = slot;
     for (uint32_t qb = slot & ~63u; qb < n; qb += cap, pos += cap) {   // wave-uniform trip count
         const QueuedPhoton cur = nx;
-        if (pos + cap < n) fetch_queued(a, pos + cap, nx);
+        if (pos + cap < n) fetch_queued(a, pos + cap, nx, P2 ? pid2 : 0xFFFFFFFFu);
+        if (P2 && pos + 2 * cap < n) pid2 = a.input_queue[pos + 2 * cap];
         bool alive = false;
         if (pos < n && !(cur.history & DEAD_MASK)) {
             if (!have_rng) { load_rng(a, slot, rng); have_rng = true; }
@@ -2319,6 +2334,263 @@ __device__ __forceinline__ int walk_segment(const DevGeom &g, bool act, V3 o, V3
     return best_id;
 }
 
+// The tail's lone long-lived photon: one walk on the whole wave, 8 cursors of 8
+// lanes (lane k of a cursor's sub-group slab-tests child k), software-pipelined.
+// walk_segment<64> spends each iteration in sequence: refill the empty cursors
+// from the stack, fetch (nodes + the previous iteration's triangles, one round
+// trip), expand, test the triangles -- measured (profile build, r04 dp1): 13% /
+// 40% / 29% / 18% of 3,244 cycles.  Here the loads of the next iteration are
+// issued as soon as they are known -- the nodes of the cursors that descend
+// (near child) and the triangles just listed -- and the previous triangles'
+// tests, the hit reduction, the culling and the stack refill run while they are
+// in flight; only a cursor refilled from the stack issues its node load after
+// them.  Same culling rule (a best never below the final one, strict '>'), same
+// (distance, reference rank) minimum: the result is walk_segment's.
+// Also cheaper per iteration: 32-bit near-child keys (the entry distance's bits
+// with the child slot in the low 3 bits: the pick among children whose entries
+// differ in those bits only may change, the culling distance is rounded down),
+// byte extraction with v_perm, branch-free triangle-list writes.
+__device__ __forceinline__ uint32_t byte8(uint32_t lo4, uint32_t hi4, uint32_t k) {   // byte k of (hi4:lo4)
+    return __builtin_amdgcn_perm(hi4, lo4, 0x0c0c0c00u | k);
+}
+// walk_lone loads only the first 8 bytes of a node's last 16 (its slot offsets;
+// the rest is pad), and of a triangle record's last 16 the 8 the leaf box needs:
+// registers written by an in-flight load but never read are reused by the register
+// allocator as temporaries, and the compiler then waits for the load first.
+template <class M>
+__device__ __forceinline__ int walk_lone(const DevGeom &g, V3 o, V3 d, uint32_t last, M stk, int cap, M tlist,
+                                         uint32_t &overflow, float &min_distance,
+                                         uint32_t &iters) {
+    constexpr uint32_t INVALID = 0xFFFFFFFFu;
+    auto ufl = [](float x) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(x))); };
+    auto uu = [](uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); };
+    o = v3(ufl(o.x), ufl(o.y), ufl(o.z));
+    d = v3(ufl(d.x), ufl(d.y), ufl(d.z));
+    last = uu(last);
+    float best = __builtin_inff();
+    uint32_t best_rank = 0xFFFFFFFFu;
+    int best_id = -1;
+    const uint32_t lane = __lane_id();
+    const uint32_t k = lane & 7u;                     // child slot of this lane
+    const uint32_t lead = lane & ~7u;                 // its sub-group's first lane
+    const unsigned long long below = (1ull << lane) - 1ull;
+    const V3 noid = v3(-o.x / d.x, -o.y / d.y, -o.z / d.z);
+    const V3 inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    const RaySlab r = make_slab(noid, inv);
+    uint32_t cur = lane < 8u ? 0u : INVALID;          // cursor 0 starts at the root
+    float cur_t = 0.0f;
+    int sp = 0;
+    uint32_t Tp = 0;                                  // triangles in flight (listed by the last expansion)
+    int pb = 0;                                       // the list buffer they were read from
+    iters = 0;
+    LoneProf<true> lp;
+    uint4 h, a1, a2, a3, a4;                          // the cursor's node (in flight at the loop top)
+    uint2 a5;
+    float4 r0, r1, r2;                                // this lane's listed triangle (in flight)
+    float2 r3;
+    const float4 *rr = g.wtri;
+    // Every lane issues the same number of loads every iteration (a lane without a
+    // cursor loads the root, one without a listed triangle record 0): with a fixed
+    // count of younger loads the compiler waits for exactly the older ones
+    // (vmcnt(N) instead of vmcnt(0)), so a node fetch overlaps the triangle tests and
+    // a triangle fetch the next expansion.  (No LDS copy of the tree top here: a
+    // lane-divergent LDS / global choice makes that count unknown.)
+    auto fetch_node = [&](uint32_t node) {
+        const uint4 *np = g.wnodes + (size_t)g.wstride * (node == INVALID ? 0u : node);
+        h = gld(np); a1 = gld(np + 1); a2 = gld(np + 2); a3 = gld(np + 3); a4 = gld(np + 4);
+        a5 = gld_lo2(np + 5);
+    };
+    auto fetch_tri = [&](uint32_t trec) {
+        rr = g.wtri + 4 * (size_t)trec;
+        r0 = gld(rr); r1 = gld(rr + 1); r2 = gld(rr + 2);
+        const uint2 w = gld_lo2(rr + 3);
+        r3 = make_float2(__uint_as_float(w.x), __uint_as_float(w.y));
+    };
+    fetch_node(cur);
+    __builtin_amdgcn_sched_barrier(0);   // nodes before triangles, as in the loop (one wait pattern)
+    fetch_tri(0u);   // (none listed yet: the same load pattern as every iteration's end)
+    while (true) {
+        iters++;
+        lp.begin();
+        // expand: sub-group j's 8 lanes slab-test the 8 children of its node
+        bool inner = false, leafhit = false;
+        float tk = 0.0f;
+        uint32_t kind = 0, child = 0, first = 0;
+        if (cur != INVALID) {
+            const V3 org = v3(__uint_as_float(h.x), __uint_as_float(h.y), __uint_as_float(h.z));
+            const float sx = exp_scale(h.w), sy = exp_scale(h.w >> 8), sz = exp_scale(h.w >> 16);
+            kind = byte8(a4.z, a4.w, k);
+            auto q = [k](uint32_t lo4, uint32_t hi4) { return (float)byte8(lo4, hi4, k); };
+            const float tnx = __builtin_fmaf(__builtin_fmaf(q(r.negx ? a2.z : a1.x, r.negx ? a2.w : a1.y), sx, org.x), r.inx, r.onx);
+            const float tfx = __builtin_fmaf(__builtin_fmaf(q(r.negx ? a1.x : a2.z, r.negx ? a1.y : a2.w), sx, org.x), r.inx, r.ofx);
+            const float tny = __builtin_fmaf(__builtin_fmaf(q(r.negy ? a3.x : a1.z, r.negy ? a3.y : a1.w), sy, org.y), r.iny, r.ony);
+            const float tfy = __builtin_fmaf(__builtin_fmaf(q(r.negy ? a1.z : a3.x, r.negy ? a1.w : a3.y), sy, org.y), r.iny, r.ofy);
+            const float tnz = __builtin_fmaf(__builtin_fmaf(q(r.negz ? a3.z : a2.x, r.negz ? a3.w : a2.y), sz, org.z), r.inz, r.onz);
+            const float tfz = __builtin_fmaf(__builtin_fmaf(q(r.negz ? a2.x : a3.z, r.negz ? a2.y : a3.w), sz, org.z), r.inz, r.ofz);
+            const float tmin = __builtin_fmaxf(__builtin_fmaxf(__builtin_fmaxf(tnx, tny), tnz), 0.0f);
+            const float tmax = __builtin_fminf(__builtin_fminf(tfx, tfy), tfz);
+            const bool hit = (kind != 0u) & !(tmin > tmax) & !(tmin > best);
+            inner = hit & (kind == WIDE_INNER);
+            leafhit = hit & (kind != WIDE_INNER);
+            tk = tmin;
+            const uint32_t off = byte8(a5.x, a5.y, k);
+            child = a4.x + off;
+            first = a4.y + off;
+        }
+        // each sub-group continues with its nearest inner child and pushes the others;
+        // key: the entry distance's bits (>= 0: ordered as unsigned) with the slot in the
+        // low 3 bits, min over the sub-group by DPP
+        uint32_t key = inner ? ((__float_as_uint(tk) & ~7u) | k) : INVALID;
+        auto dmin = [](uint32_t v, auto ctrl) {
+            const uint32_t o2 = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, decltype(ctrl)::value, 0xF, 0xF, true);
+            return o2 < v ? o2 : v;
+        };
+        key = dmin(key, std::integral_constant<int, 0xB1>());    // quad_perm [1,0,3,2]
+        key = dmin(key, std::integral_constant<int, 0x4E>());    // quad_perm [2,3,0,1]
+        key = dmin(key, std::integral_constant<int, 0x141>());   // row_half_mirror
+        uint32_t near = INVALID;
+        if (key != INVALID) near = a4.x + byte8(a5.x, a5.y, key & 7u);
+        const bool push = inner && (key & 7u) != k;
+        const unsigned long long pm = __ballot(push);
+        const int pos = sp + __popcll(pm & below);
+        if (push && pos < cap) {
+            stk[2 * pos] = child;
+            stk[2 * pos + 1] = __float_as_uint(tk);
+        }
+        const int npush = __popcll(pm);
+        if (sp + npush > cap) {
+            if (lane == 0) overflow += (uint32_t)(sp + npush - cap);
+            sp = cap;
+        } else {
+            sp += npush;
+        }
+        cur = near;
+        cur_t = __uint_as_float(key & ~7u);           // <= the child's entry distance
+        // this expansion's hit-leaf triangles, listed in lane order.  A lane with
+        // triangles writes its 4 slots from the last down: a slot beyond its count
+        // lands on a later lane's entry, which that lane writes afterwards (a lower
+        // slot index), and slot indices are clamped to the buffer.
+        const uint32_t cnt = leafhit ? kind : 0u;
+        const unsigned long long b0 = __ballot(cnt & 1u), b1 = __ballot(cnt & 2u), b2 = __ballot(cnt & 4u);
+        const uint32_t pre = __popcll(b0 & below) + 2u * __popcll(b1 & below) + 4u * __popcll(b2 & below);
+        const uint32_t Tn = uu(__popcll(b0) + 2u * __popcll(b1) + 4u * __popcll(b2));
+        const int nb = (pb ^ 1) * TAIL_TRI;
+        if (cnt > 0u) {
+#pragma unroll
+            for (int i = 3; i >= 0; --i)
+                tlist[nb + (int)min(pre + (uint32_t)i, (uint32_t)(TAIL_TRI - 1))] = first + (uint32_t)i;
+        }
+        lp.tick(2);
+        // cursors without a node take the topmost unculled stack entries (walk_segment's
+        // window refill; culled with the best before this iteration's triangle tests --
+        // conservative), passed through the previous list's buffer (entries 0..15: its
+        // triangles are loaded, only entries >= 64 are still read, below)
+        unsigned long long em = __ballot(k == 0u && cur == INVALID);
+        while (em != 0 && sp > 0) {
+            const int W = sp < 8 ? sp : 8;
+            uint32_t en = 0, et = 0;
+            bool ok = false;
+            if (lane < (uint32_t)W) {
+                en = stk[2 * (sp - 1 - (int)lane)];
+                et = stk[2 * (sp - 1 - (int)lane) + 1];
+                ok = !(__uint_as_float(et) > best);           // mesh.h:94-96
+            }
+            const unsigned long long okm = __ballot(ok);
+            const int need = __popcll(em), nv = __popcll(okm);
+            const int take = need < nv ? need : nv;
+            const int rho = __popcll(okm & below);
+            const unsigned long long stopm = __ballot(ok && rho == take);
+            const int consumed = stopm ? (__ffsll((long long)stopm) - 1) : W;
+            if (ok && rho < take) {
+                tlist[pb * TAIL_TRI + 2 * rho] = en;
+                tlist[pb * TAIL_TRI + 2 * rho + 1] = et;
+            }
+            __builtin_amdgcn_wave_barrier();
+            const bool empty = ((em >> lead) & 1ull) != 0;
+            const int rnk = __popcll(em & ((1ull << lead) - 1ull));
+            const unsigned long long taken = __ballot(k == 0u && empty && rnk < take);
+            if (empty && rnk < take) {
+                cur = tlist[pb * TAIL_TRI + 2 * rnk];
+                cur_t = __uint_as_float(tlist[pb * TAIL_TRI + 2 * rnk + 1]);
+            }
+            __builtin_amdgcn_wave_barrier();
+            sp = (int)uu((uint32_t)(sp - consumed));
+            em &= ~taken;
+        }
+        sp = (int)uu((uint32_t)sp);
+        // every cursor's next node, in flight during the triangle tests below
+        fetch_node(cur);
+        lp.tick(0);
+        // test the previous list's triangles: each lane its own (loaded last
+        // iteration); entries beyond the 64 lanes (rare) are fetched in a loop of their
+        // own, so the common test waits for nothing in flight
+        float lbest = best;
+        uint32_t lrank = best_rank;
+        int lid = -1;
+        // (t3 = nullptr: the leaf-box words are loaded for a candidate only)
+        auto test = [&](const float4 &t0, const float4 &t1, const float4 &t2, const float2 *t3, const float4 *tr) {
+            const uint32_t id = __float_as_uint(t2.y);
+            float dist;
+            if (id == last || !intersect_record(o, d, t0, t1, t2, dist)) return;
+            const uint32_t rank = __float_as_uint(t2.z);
+            if (!(dist < lbest || (dist == lbest && rank < lrank))) return;
+            uint2 w;
+            if (t3) w = make_uint2(__float_as_uint(t3->x), __float_as_uint(t3->y));
+            else w = gld_lo2(tr + 3);
+            V3 lo, hi;
+            node_bounds(g, make_uint4(__float_as_uint(t2.w), w.x, w.y, 0u), lo, hi);
+            float bd;
+            if (!intersect_box(noid, inv, lo, hi, bd) || bd > lbest) return;   // mesh.h:94-96
+            lbest = dist;
+            lrank = rank;
+            lid = rec_of(g, tr);
+        };
+        if (lane < Tp) {
+            // every word of the lane's triangle waited for here, with the node loads
+            // above still in flight: a register the allocator reuses later is then
+            // no longer owed by a load (the compiler would wait for everything there)
+            asm volatile("" :: "v"(r3.x), "v"(r3.y));
+            test(r0, r1, r2, &r3, rr);
+        }
+        for (uint32_t i = lane + 64u; i < Tp; i += 64u) {
+            const float4 *tr = g.wtri + 4 * (size_t)tlist[pb * TAIL_TRI + (int)i];
+            test(gld(tr), gld(tr + 1), gld(tr + 2), nullptr, tr);
+        }
+        // wave min over (distance, rank): usually no lane or one lane has a hit
+        const unsigned long long hm = __ballot(lid != -1);
+        if (hm != 0) {
+            unsigned long long lkey = lid == -1 ? ~0ull : (((unsigned long long)__float_as_uint(lbest) << 32) | lrank);
+            if ((hm & (hm - 1)) == 0) {
+                const int src = __ffsll((long long)hm) - 1;
+                lkey = ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(lkey >> 32), src) << 32) |
+                       (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)lkey, src);
+                lid = __builtin_amdgcn_readlane(lid, src);
+            } else {
+                for (int off = 1; off < 64; off <<= 1) {
+                    const unsigned long long ok = __shfl_xor(lkey, off);
+                    const int oid = __shfl_xor(lid, off);
+                    if (ok < lkey) { lkey = ok; lid = oid; }
+                }
+            }
+            best = ufl(__uint_as_float((uint32_t)(lkey >> 32)));
+            best_rank = uu((uint32_t)lkey);
+            best_id = (int)uu((uint32_t)lid);
+        }
+        // this expansion's triangles, in flight during the stack refill and the next
+        // expansion (the registers of the ones just tested are free)
+        __builtin_amdgcn_wave_barrier();
+        fetch_tri(lane < Tn ? tlist[nb + (int)lane] : 0u);
+        Tp = Tn;
+        pb ^= 1;
+        if (cur != INVALID && cur_t > best) cur = INVALID;   // its node load is in flight: ignored
+        lp.tick(3);
+        if (__ballot(cur != INVALID) == 0 && Tp == 0 && sp == 0) break;
+    }
+    lp.flush();
+    min_distance = best_id == -1 ? -1.0f : best;
+    return best_id;
+}
+
 template <int MINW>
 __global__ __launch_bounds__(BLOCK, MINW) void propagate_tail_kernel(const DevGeom *__restrict__ gdev, PropagateArgs a,
                                                                      uint32_t cap) {
@@ -2462,7 +2734,9 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_tail_kernel(const DevGe
             const uint32_t seg0 = lane & ~(uint32_t)(Gs - 1);
             float sd;
             uint32_t it;
-            const int st = (Gs == 64 && (a.prio & 2u))
+            const int st = (Gs == 64 && (a.prio & 4u))
+                               ? walk_lone(g, o, dd, last, LdsFlat{wstack}, TAIL_STACK * 8, LdsFlat{wtris}, overflow, sd, it)
+                           : (Gs == 64 && (a.prio & 2u))
                                ? walk_segment<64>(g, act, o, dd, last, 64, LdsFlat{wstack}, TAIL_STACK * 8, LdsFlat{wtris},
                                                   top, overflow, sd, it)
                                : walk_segment<0>(g, act, o, dd, last, Gs, LdsFlat{wstack + seg0 / 8 * TAIL_STACK * 2},
@@ -3723,6 +3997,13 @@ static uint32_t tail_top_nodes() {
     const char *e = getenv("CHR_TAIL_TOP");
     return (e && e[0] == '0') ? 0u : TOP_NODES;
 }
+// CHR_SHADE_PREFETCH2=0: the shade kernel reads the next photon's queue entry
+// right before its state (one dependent load per photon) instead of an iteration
+// ahead (A/B)
+static bool shade_prefetch2() {
+    const char *e = getenv("CHR_SHADE_PREFETCH2");
+    return !(e && e[0] == '0');
+}
 static int shade_waves() {             // CHR_SHADE_WAVES=2|4: the shade kernel at 2 / 4 waves per SIMD (A/B)
     const char *e = getenv("CHR_SHADE_WAVES");
     return e ? atoi(e) : 3;
@@ -3743,6 +4024,12 @@ static uint32_t trace_drain_max() {
 // walk (run-time width) instead of its GS = 64 specialisation (A/B)
 static bool tail_gs64() {
     const char *e = getenv("CHR_TAIL_GS64");
+    return !(e && e[0] == '0');
+}
+// CHR_TAIL_LONE=0: the lone walker walks with walk_segment<64> instead of the
+// software-pipelined walk_lone (A/B)
+static bool tail_lone() {
+    const char *e = getenv("CHR_TAIL_LONE");
     return !(e && e[0] == '0');
 }
 // CHR_TAIL_PRIO=0: the batches' overlapped tail kernel at normal wave priority (A/B)
@@ -3862,7 +4149,8 @@ static StepVariant select_step_variant(const chr_geometry *g) {
                     default: break;
                 }
             }
-            sv.shade = shade_waves() == 4 ? shade_kernel<4> : (shade_waves() == 2 ? shade_kernel<2> : shade_kernel<3>);
+            sv.shade = shade_waves() == 4 ? shade_kernel<4>
+                       : (shade_waves() == 2 ? shade_kernel<2> : (shade_prefetch2() ? shade_kernel<3, true> : shade_kernel<3>));
             sv.tail = tail_group_walk() ? propagate_group_kernel<8, kGroupWaves>
                       : (tail_waves() == 4 ? propagate_tail_kernel<4>
                          : (tail_waves() == 3 ? propagate_tail_kernel<3> : propagate_tail_kernel<kTailWaves>));
@@ -4309,7 +4597,7 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
         hipLaunchKernelGGL(clear_masks_kernel, dim3(std::min<uint32_t>(kClearBlocks, grid_for(nwords))), dim3(BLOCK), 0, ts,
                            sc->tail_masks, dev_n, mode);
         PropagateArgs at = a;
-        at.prio = (tail_prio() ? 1u : 0u) | (tail_gs64() ? 2u : 0u);
+        at.prio = (tail_prio() ? 1u : 0u) | (tail_gs64() ? 2u : 0u) | (tail_lone() ? 4u : 0u);
         at.alive_masks = sc->tail_masks;
         at.max_steps = sc->remaining;
         at.want = STEP_TAIL;
@@ -4336,7 +4624,7 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
         else CHR_HIP_CHECK(hipMemsetAsync(masks, 0, (size_t)nwords * 8, stream));
         a.max_steps = sc ? sc->remaining : max_steps;
         a.want = STEP_TAIL;
-        a.prio = tail_gs64() ? 2u : 0u;
+        a.prio = (tail_gs64() ? 2u : 0u) | (tail_lone() ? 4u : 0u);
         a.work = (sc && next && tail_work_queue(sv, sc, use_weights, cap)) ? next : nullptr;
         hipLaunchKernelGGL(sv.tail, dim3(tail_grid(sv, threads, a.work != nullptr)), dim3(BLOCK), 0, stream,
                            (const DevGeom *)g->d_dev, a, cap);
@@ -5261,7 +5549,7 @@ extern "C" int chr_kernel_info(int32_t which, chr_kernel_attr *out) {
     const char *name = nullptr;
     switch (which) {
         case 0: fn = (const void *)trace_kernel<false, 6, 12, 4, 48>; name = "chr::trace_kernel<false,6,12,4,48>"; break;
-        case 1: fn = (const void *)shade_kernel<3>; name = "chr::shade_kernel<3>"; break;
+        case 1: fn = (const void *)shade_kernel<3, true>; name = "chr::shade_kernel<3,true>"; break;
         case 2: fn = (const void *)propagate_tail_kernel<kTailWaves>; name = "chr::propagate_tail_kernel<2>"; break;
         case 3: fn = (const void *)propagate_step_kernel<8, 4, kWalk>; name = "chr::propagate_step_kernel<8,4,2006>"; break;
         default: return chr::fail(CHR_ERR_INVALID, "chr_kernel_info: unknown kernel %d", which);
