@@ -2357,19 +2357,22 @@ __device__ __forceinline__ uint32_t byte8(uint32_t lo4, uint32_t hi4, uint32_t k
 // the rest is pad), and of a triangle record's last 16 the 8 the leaf box needs:
 // registers written by an in-flight load but never read are reused by the register
 // allocator as temporaries, and the compiler then waits for the load first.
+// best / best_rank / best_id: a hit already found seeds the walk (trace_kernel's
+// drain of a walk begun lane by lane), as in walk_segment.
 template <class M>
 __device__ __forceinline__ int walk_lone(const DevGeom &g, V3 o, V3 d, uint32_t last, M stk, int cap, M tlist,
-                                         uint32_t &overflow, float &min_distance,
-                                         uint32_t &iters) {
+                                         uint32_t &overflow, float &min_distance, uint32_t &iters,
+                                         float best = __builtin_inff(), uint32_t best_rank = 0xFFFFFFFFu,
+                                         int best_id = -1) {
     constexpr uint32_t INVALID = 0xFFFFFFFFu;
     auto ufl = [](float x) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(x))); };
     auto uu = [](uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); };
     o = v3(ufl(o.x), ufl(o.y), ufl(o.z));
     d = v3(ufl(d.x), ufl(d.y), ufl(d.z));
     last = uu(last);
-    float best = __builtin_inff();
-    uint32_t best_rank = 0xFFFFFFFFu;
-    int best_id = -1;
+    best = ufl(best);
+    best_rank = uu(best_rank);
+    best_id = (int)uu((uint32_t)best_id);
     const uint32_t lane = __lane_id();
     const uint32_t k = lane & 7u;                     // child slot of this lane
     const uint32_t lead = lane & ~7u;                 // its sub-group's first lane
@@ -2883,6 +2886,7 @@ struct TraceArgs {
     uint32_t drain_max;          // a wave drains its last <= drain_max walks whole-wave (0: never; at most 8)
     uint32_t claim_ahead;        // refills from claimed chunks, the next claim in flight (trace_claim_ahead)
     uint32_t spread;             // launches with fewer rays than lanes: each wave claims its share (trace_spread)
+    uint32_t drain_lone;         // a wave draining ONE walk walks it with walk_lone (trace_drain_lone)
 };
 constexpr uint32_t CLAIM = 64;   // ray-counter chunk of trace_kernel's claim-ahead refill
 
@@ -3270,9 +3274,12 @@ __global__ __launch_bounds__(TB, MINW) void trace_kernel(const DevGeom *__restri
             CHR_LDS uint32_t *wbase = (CHR_LDS uint32_t *)(lds + (threadIdx.x & ~63u));
             float sdist;
             uint32_t sit;
-            const int tri = walk_segment<0>(g, act, so, sdir, slast, Gs, LdsRowsT<TB>{wbase, seg0 / 8 * DSTK * 2},
-                                         DSTK * Gs / 8, LdsRowsT<TB>{wbase, 8 * DSTK * 2 + 4 * seg0}, top, overflow,
-                                         sdist, sit, sbest, srank, sid);
+            const int tri = (w == 1 && a.drain_lone)
+                                ? walk_lone(g, so, sdir, slast, LdsRowsT<TB>{wbase, 0}, DSTK * 8,
+                                            LdsRowsT<TB>{wbase, 8 * DSTK * 2}, overflow, sdist, sit, sbest, srank, sid)
+                                : walk_segment<0>(g, act, so, sdir, slast, Gs, LdsRowsT<TB>{wbase, seg0 / 8 * DSTK * 2},
+                                                  DSTK * Gs / 8, LdsRowsT<TB>{wbase, 8 * DSTK * 2 + 4 * seg0}, top,
+                                                  overflow, sdist, sit, sbest, srank, sid);
             const int mine = (__popcll(rm & ((1ull << lane) - 1ull)) * Gs) & 63;   // my segment's first lane
             const int rt = __shfl(tri, mine);
             const float rd = __shfl(sdist, mine);
@@ -4088,6 +4095,11 @@ static bool trace_spread() {
     const char *e = getenv("CHR_TRACE_SPREAD");
     return !(e && e[0] == '0');
 }
+// CHR_TRACE_DRAIN_LONE=0: a wave draining one walk uses walk_segment<0> (A/B)
+static bool trace_drain_lone() {
+    const char *e = getenv("CHR_TRACE_DRAIN_LONE");
+    return !(e && e[0] == '0');
+}
 static bool trace_claim_ahead() {
     const char *e = getenv("CHR_TRACE_AHEAD");
     return e && e[0] == '1';
@@ -4504,6 +4516,7 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
         ta.drain_max = trace_drain_max();
         ta.claim_ahead = trace_claim_ahead() ? 1u : 0u;
         ta.spread = trace_spread() ? 1u : 0u;
+        ta.drain_lone = trace_drain_lone() ? 1u : 0u;
         ta.winv = carry ? fc->winv : nullptr;
         a.winv = carry ? fc->winv : nullptr;
         a.walive = carry ? fc->walive : nullptr;

@@ -46,6 +46,12 @@ inline uint32_t leaf_max_env() {
     return (uint32_t)std::min(LEAF_MAX, std::max(1, v));
 }
 constexpr int NBINS = 32;
+// CHR_WIDE_SWEEP=n: ranges of <= n triangles split by an exact SAH sweep instead of
+// NBINS bins (build-time A/B; default 0: binned everywhere)
+inline uint32_t sweep_max_env() {
+    const char *e = std::getenv("CHR_WIDE_SWEEP");
+    return e ? (uint32_t)std::max(0, std::atoi(e)) : 0u;
+}
 
 struct Box {
     float lo[3], hi[3];
@@ -72,6 +78,7 @@ struct Cluster {
 struct Builder {
     bool fill_leaves;
     uint32_t leaf_max;
+    uint32_t sweep_max;   // ranges of at most this many triangles split by an exact SAH sweep
     const std::vector<Box> &tri_box;
     const std::vector<float> &centroid;   // 3 per triangle
     std::vector<uint32_t> &idx;
@@ -95,8 +102,41 @@ struct Builder {
         return r;
     }
 
+    // exact SAH split of a small range [b,e): every split position of the
+    // centroid order on each axis (the binned split below approximates this)
+    uint32_t split_sweep(uint32_t b, uint32_t e) {
+        const uint32_t n = e - b;
+        std::vector<uint32_t> ord[3];
+        std::vector<double> right(n);
+        double best_cost = INFINITY;
+        int best_axis = -1;
+        uint32_t best_m = 0;
+        for (int a = 0; a < 3; ++a) {
+            ord[a].assign(idx.begin() + b, idx.begin() + e);
+            std::stable_sort(ord[a].begin(), ord[a].end(), [&](uint32_t x, uint32_t y) {
+                return centroid[3 * (size_t)x + a] < centroid[3 * (size_t)y + a];
+            });
+            Box acc;
+            acc.empty();
+            for (uint32_t i = n; i-- > 1;) {
+                acc.grow(tri_box[ord[a][i]]);
+                right[i] = acc.area() * (double)(n - i);
+            }
+            acc.empty();
+            for (uint32_t i = 1; i < n; ++i) {
+                acc.grow(tri_box[ord[a][i - 1]]);
+                const double cost = acc.area() * (double)i + right[i];
+                if (cost < best_cost) { best_cost = cost; best_axis = a; best_m = i; }
+            }
+        }
+        if (best_axis < 0) return b + n / 2;
+        std::copy(ord[best_axis].begin(), ord[best_axis].end(), idx.begin() + b);
+        return b + best_m;
+    }
+
     // binned SAH split of [b,e); returns split point (b < m < e)
     uint32_t split(uint32_t b, uint32_t e, bool par) {
+        if (e - b <= sweep_max) return split_sweep(b, e);
         Box cb;
         cb.empty();
         for (uint32_t i = b; i < e; ++i) cb.grow(&centroid[3 * (size_t)idx[i]]);   // cheap relative to binning
@@ -293,7 +333,7 @@ int build_wide_bvh(const chr_geometry_desc *d, WideBVH &out) {
     for (int64_t t = 0; t < (int64_t)ntri; ++t)
         for (int a = 0; a < 3; ++a) centroid[3 * t + a] = 0.5f * (tri_box[t].lo[a] + tri_box[t].hi[a]);
 
-    Builder B{!std::getenv("CHR_WIDE_NO_FILL"), leaf_max_env(), tri_box, centroid, idx};
+    Builder B{!std::getenv("CHR_WIDE_NO_FILL"), leaf_max_env(), sweep_max_env(), tri_box, centroid, idx};
     out.nodes.clear();
     out.tri.clear();
     out.nodes.resize(1);
