@@ -236,3 +236,55 @@ def test_batches_slot_timing_modes_identical(cuda, small_detector, monkeypatch):
             _same(a, b, 'CHR_SLOT_TIMING=%s batch %d' % (mode, i))
         assert np.array_equal(out['t'][1], out[mode][1])
     assert sum(s.tail_photons for s in out['t'][2]) > 0
+
+
+@pytest.mark.parametrize('switch', ['CHR_TAIL_LONE', 'CHR_TRACE_DRAIN_LONE', 'CHR_SHADE_PREFETCH2', 'CHR_TAIL_GS64'])
+def test_batches_walker_switches_identical(cuda, small_detector, monkeypatch, switch):
+    """The walkers are interchangeable: the tail's lone photon walked by the
+    software-pipelined walk_lone (default) or walk_segment<64>
+    (CHR_TAIL_LONE=0) or the run-time-width segment walk (CHR_TAIL_GS64=0); a
+    trace wave draining one walk through walk_lone or walk_segment<0>
+    (CHR_TRACE_DRAIN_LONE=0); the shade kernel's two-ahead queue prefetch on or
+    off.  Same photons, same RNG states."""
+    sources = _sources([30000, 70000, 5000, 120000], seed=29)
+    from chroma import gpu
+    det = gpu.GPUDetector(small_detector)
+    monkeypatch.delenv(switch, raising=False)
+    base = _run(det, sources, 64, 256, 1000, batched=True)
+    monkeypatch.setenv(switch, '0')
+    alt = _run(det, sources, 64, 256, 1000, batched=True)
+    for i, (a, b) in enumerate(zip(base[0], alt[0])):
+        _same(a, b, '%s=0 batch %d' % (switch, i))
+    assert np.array_equal(base[1], alt[1])
+    assert sum(s.tail_photons for s in base[2]) > 0
+    assert sum(s.trace_launches for s in base[2]) > 0
+
+
+@pytest.mark.parametrize('lone', ['1', '0'])
+def test_mirror_scene_long_tail_parity(cuda, monkeypatch, lone):
+    """The physics scene (97% specular mirror plate, wire planes, every surface
+    model) at 4000 photons over 64 x 64 slots, 1000 steps: every step after the
+    first runs in the tail kernel, whose waves thin out to one walking photon
+    (the lone walker).  HIP == oracle with either lone walker."""
+    import scenes
+    from chroma import gpu, loader
+    from chroma.gpu.packing import PackedGeometry
+    monkeypatch.setenv('CHR_TAIL_LONE', lone)
+    geo = loader.create_geometry_from_obj(scenes.physics_scene())
+    det = gpu.GPUDetector(geo)
+    src = scenes.photon_sources(4000, seed=41)
+    got, rng, stats = _run(det, [src], 64, 64, 1000, batched=False, seed=5)
+    nslots = 64 * 64
+    states = oracle.rng_init(nslots, seed=5)
+    host = oracle.HostPhotons(src)
+    host.last_hit_triangles[:] = -1
+    host.weights[:] = 1.0
+    oracle.propagate(PackedGeometry(geo), host, states, nslots, 64, 64, 1000)
+    for f in ('flags', 'last_hit_triangles'):
+        assert np.array_equal(getattr(got[0], f), getattr(host, f)), 'mirror scene lone=%s: %s' % (lone, f)
+    for f in ('pos', 'dir', 'pol', 't', 'wavelengths'):
+        a = getattr(got[0], f).astype(np.float64)
+        b = getattr(host, f).astype(np.float64)
+        assert np.all(np.abs(a - b) <= 1e-5 * np.maximum(np.abs(b), 1.0)), 'mirror scene lone=%s: %s' % (lone, f)
+    assert np.array_equal(rng, states.reshape(6, nslots))
+    assert stats[0].tail_photons > 0
