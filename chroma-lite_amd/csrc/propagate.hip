@@ -2976,7 +2976,10 @@ __global__ __launch_bounds__(TB, MINW) void trace_kernel(const DevGeom *__restri
     // a draining wave's walk_segment stacks (8 x DSTK entries, DSTK per 8 lanes) + triangle
     // lists in its LDS rows
     constexpr int DSTK = ((2 * SL + LEAFQ) * 64 - 2 * TAIL_TRI) / 16;
-    static_assert(DSTK >= 112, "drain needs the wave's LDS rows");
+    // a walk's stack holds >= 112 entries: 8 lanes per walk (drains of 5..8 walks) need
+    // DSTK >= 112, 16 lanes (<= 4 walks, the default) 2 * DSTK
+    static_assert(2 * DSTK >= 112, "drain needs the wave's LDS rows");
+    const uint32_t drain_max = DSTK >= 112 ? a.drain_max : (a.drain_max < 4u ? a.drain_max : 4u);
     WStack st;
     // Deep stack entries live in a lane-strided HBM column sized for this
     // persistent grid, not in private scratch: a kernel with a private segment
@@ -3162,7 +3165,7 @@ __global__ __launch_bounds__(TB, MINW) void trace_kernel(const DevGeom *__restri
             // every small launch).  Each restarts from the root seeded with its
             // best so far (conservative culling, the same nearest hit); the
             // lanes' stacks are abandoned and their LDS rows reused.
-            if (exhausted && __ballot(has_ray) != 0 && (uint32_t)__popcll(__ballot(has_ray)) <= a.drain_max &&
+            if (exhausted && __ballot(has_ray) != 0 && (uint32_t)__popcll(__ballot(has_ray)) <= drain_max &&
                 __ballot(has_ray && flat_f >= 0) == 0) {   // no cut-item sub-walks (they start mid-tree)
                 drain = true;   // after the loop, where the walk state below is no longer live
                 break;
@@ -4121,6 +4124,12 @@ static int trace_refill_r() {
 // CHR_TRACE_LAYOUT (A/B): 0 256-thread workgroups, 12 LDS stack entries per lane;
 // 1 1024-thread workgroups (one per CU), 11 entries, the top TOP_NODES nodes of
 // the tree in LDS (stage_top); 2 the same without the top nodes (control).
+// (r04 ab7, removed: the per-child offsets derived from the kind bytes by byte-wise
+// prefix sums instead of loaded -- five 16-byte node loads per node step, not six:
+// trace 14.16 vs 14.18 ms per step, 492.2 vs 491.7 M/s: the walk is not bound by
+// its load instruction count.)
+// (r04 ab6, removed: 5 waves per SIMD with 8 LDS stack entries per lane, 8 KB of LDS
+// per wave: trace 14.14 -> 14.97 ms per step, 492.8 -> 474 M/s.)
 // (r04 ab3, removed: a combined step -- every lane fetching its node AND its next
 // parked triangle each iteration -- ran trace 38.8 ms/step at 4 waves/SIMD (200 B
 // of spills) and 17.2 at 3, against 14.35 for the wave-wide node / triangle choice)
