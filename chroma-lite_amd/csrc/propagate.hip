@@ -1823,9 +1823,11 @@ struct QueuedPhoton {
 };
 // the photon at queue position q; pid: its queue entry when already loaded (the
 // shade kernel's two-ahead prefetch), else read here first (a dependent load)
+// (KNOWN: pid is the queue entry, no fallback load -- no branch holding a load)
+template <bool KNOWN = false>
 __device__ __forceinline__ void fetch_queued(const PropagateArgs &a, uint32_t q, QueuedPhoton &f,
                                              uint32_t pid = 0xFFFFFFFFu) {
-    f.pid = pid != 0xFFFFFFFFu ? pid : a.input_queue[q];
+    f.pid = (KNOWN || pid != 0xFFFFFFFFu) ? pid : a.input_queue[q];
     f.history = a.flags[f.pid] & 0xFFFFu;   // photon.h:29
     f.pos = load3(a.pos, f.pid);
     f.dir = load3(a.dir, f.pid);
@@ -1840,7 +1842,19 @@ __device__ __forceinline__ void fetch_queued(const PropagateArgs &a, uint32_t q,
 // P2: the queue entry of the photon two positions ahead is loaded one iteration
 // early, so the next photon's state loads go out without first waiting for its
 // queue entry (a dependent round trip per photon otherwise)
-template <int MINW, bool P2 = false>
+// SC: no wait for the write-back.  On gfx9 stores count in vmcnt with the loads,
+// in issue order, and the compiler waits for a prefetched value with the count of
+// the path into its use with the fewest younger operations.  Without SC the loop's
+// back edge copied the prefetched photon after this iteration's stores with
+// `s_waitcnt vmcnt(0)` (the prefetch under `if (pos + cap < n)`, the entry path from
+// the prologue, the queue entry's fallback load all leave paths with none younger),
+// so every iteration waited for its own stores to be acknowledged.  With SC every
+// lane issues the prefetch (position clamped into the queue), the queue entry two
+// ahead is always the one loaded (no fallback load), and the first iteration is
+// peeled, so every path into the loop has the write-back behind the prefetch: the
+// prefetch is waited for at the physics' join, before the stores, and nothing waits
+// for the stores.
+template <int MINW, bool P2 = false, bool SC = false>
 __global__ __launch_bounds__(BLOCK, MINW) void shade_kernel(const DevGeom *__restrict__ gdev, PropagateArgs a,
                                                             uint32_t cap) {
     if (a.mode && *a.mode != a.want) return;
@@ -1855,19 +1869,26 @@ __global__ __launch_bounds__(BLOCK, MINW) void shade_kernel(const DevGeom *__res
     enum { P_FILL, P_PHYS, P_OTHER };
     Prof<3> pf;
     pf.start(P_OTHER);
+    auto clampq = [n](uint32_t q) { return q < n ? q : n - 1u; };
     QueuedPhoton nx;
-    if (slot < n) fetch_queued(a, slot, nx);
+    if (SC) fetch_queued(a, clampq(slot), nx);
+    else if (slot < n) fetch_queued(a, slot, nx);
     uint32_t pid2 = 0xFFFFFFFFu;                       // P2: queue entry of position pos + cap
-    if (P2 && slot + cap < n) pid2 = a.input_queue[slot + cap];
+    if (SC && P2) pid2 = a.input_queue[clampq(slot + cap)];
+    else if (P2 && slot + cap < n) pid2 = a.input_queue[slot + cap];
     uint32_t pos = slot;
-    for (uint32_t qb = slot & ~63u; qb < n; qb += cap, pos += cap) {   // wave-uniform trip count
+    auto body = [&](uint32_t qb) __attribute__((always_inline)) {
         const QueuedPhoton cur = nx;
-        if (pos + cap < n) fetch_queued(a, pos + cap, nx, P2 ? pid2 : 0xFFFFFFFFu);
-        if (P2 && pos + 2 * cap < n) pid2 = a.input_queue[pos + 2 * cap];
+        if (SC && P2) fetch_queued<true>(a, clampq(pos + cap), nx, pid2);
+        else if (SC) fetch_queued(a, clampq(pos + cap), nx);
+        else if (pos + cap < n) fetch_queued(a, pos + cap, nx, P2 ? pid2 : 0xFFFFFFFFu);
+        if (SC && P2) pid2 = a.input_queue[clampq(pos + 2 * cap)];
+        else if (P2 && pos + 2 * cap < n) pid2 = a.input_queue[pos + 2 * cap];
         bool alive = false;
-        if (pos < n && !(cur.history & DEAD_MASK)) {
+        const bool valid = pos < n && !(cur.history & DEAD_MASK);
+        Photon p;
+        if (valid) {
             if (!have_rng) { load_rng(a, slot, rng); have_rng = true; }
-            Photon p;
             p.history = cur.history;
             p.pos = cur.pos;
             p.dir = cur.dir / norm(cur.dir);
@@ -1901,6 +1922,17 @@ __global__ __launch_bounds__(BLOCK, MINW) void shade_kernel(const DevGeom *__res
                 }
                 pf.tick(P_OTHER);
             }
+            alive = (p.history & DEAD_MASK) == 0;
+        }
+        if constexpr (SC) {
+            // the prefetched photon and queue entry waited for here, on every path and
+            // before the write-back (see SC above)
+            asm volatile("" ::"v"(nx.pid), "v"(nx.history), "v"(nx.pos.x), "v"(nx.pos.y), "v"(nx.pos.z), "v"(nx.dir.x),
+                         "v"(nx.dir.y), "v"(nx.dir.z), "v"(nx.pol.x), "v"(nx.pol.y), "v"(nx.pol.z));
+            asm volatile("" ::"v"(nx.wavelength), "v"(nx.time), "v"(nx.weight), "v"(nx.last_hit), "v"(nx.hit.x),
+                         "v"(nx.hit.y), "v"(nx.walk), "v"(pid2));
+        }
+        if (valid) {
             const uint32_t pid = cur.pid;
             store3(a.pos, pid, p.pos);
             store3(a.dir, pid, p.dir);
@@ -1910,12 +1942,21 @@ __global__ __launch_bounds__(BLOCK, MINW) void shade_kernel(const DevGeom *__res
             a.flags[pid] = p.history;
             a.last_hit[pid] = p.last_hit;
             a.weights[pid] = p.weight;
-            alive = (p.history & DEAD_MASK) == 0;
         }
         if (a.walive && pos < n) a.walive[cur.walk] = alive ? 1u : 0u;   // dead on entry: 0 too
         const unsigned long long mask = __ballot(alive);
         if ((slot & 63u) == 0) a.alive_masks[qb >> 6] = mask;
+    };
+    uint32_t qb = slot & ~63u;                         // wave-uniform trip count
+    if (SC && qb < n) {
+        // the first iteration peeled: the loop's first wait for the prefetched queue
+        // entry and state then has this iteration's write-back behind it on every
+        // path into the loop (from the prologue it would be the youngest load: vmcnt(0))
+        body(qb);
+        qb += cap;
+        pos += cap;
     }
+    for (; qb < n; qb += cap, pos += cap) body(qb);
     if (have_rng) store_rng(a, slot, rng);
 #ifdef CHR_DEVICE_PROFILE
     pf.tick(P_OTHER);
@@ -2968,7 +3009,10 @@ __global__ __launch_bounds__(BLOCK) void permute_rays_kernel(const uint4 *rays_i
 // COUNT: walk counters; F: triangle step once F/8 of the walking lanes have
 // parked leaves (intersect_wide_spec); SL: stack entries in LDS; MINW: waves
 // per SIMD; R: refill once R of the 64 lanes are without a ray.
-template <bool COUNT, int F, int SL, int MINW, int R, int TB = BLOCK, int TOPN = 0>
+// PF: each lane holds its next ray's record in registers (prefetched): a lane whose
+// walk ends starts that ray at once, and the wave claims and loads new records once
+// R lanes have used theirs (the loads land while the walks go on).
+template <bool COUNT, int F, int SL, int MINW, int R, int TB = BLOCK, int TOPN = 0, bool PF = false>
 __global__ __launch_bounds__(TB, MINW) void trace_kernel(const DevGeom *__restrict__ gdev, TraceArgs a) {
     __shared__ uint32_t lds[(2 * SL + LEAFQ) * TB];
     // the top of the tree (stage_top): TB = 1024 makes one copy per CU serve its 16 waves
@@ -3018,6 +3062,10 @@ __global__ __launch_bounds__(TB, MINW) void trace_kernel(const DevGeom *__restri
     // next chunk's base, claimed ahead (valid in lane 0 once have_pend)
     uint32_t cb = 0, cn = 0, pend = 0;
     bool have_pend = false;
+    // PF: this lane's prefetched work item pj (pv) and, for a queued ray, its record
+    bool pv = false;
+    uint32_t pj = 0;
+    uint4 pr0 = make_uint4(0u, 0u, 0u, 0u), pr1 = make_uint4(0u, 0u, 0u, 0u);
     // claim size: CLAIM, or with spread a wave's share of a launch smaller than the
     // grid's lanes (every wave then walks a few rays and reaches its drain sooner)
     uint32_t claim = CLAIM;
@@ -3044,7 +3092,94 @@ __global__ __launch_bounds__(TB, MINW) void trace_kernel(const DevGeom *__restri
                 }
             }
         }
-        if (!exhausted) {
+        if constexpr (PF) {
+            // a lane without a walk starts its prefetched ray (no round trip)
+            if (!has_ray && pv) {
+                pv = false;
+                bool start = false;
+                if (pj < n && !a.rays) {                  // no ray records: from the photon arrays
+                    q = a.order ? a.order[pj] : pj;
+                    pid = a.queue[q];
+                    if (!((a.flags[pid] & 0xFFFFu) & DEAD_MASK)) {
+                        o = load3(a.pos, pid);
+                        d = load3(a.dir, pid);
+                        d = d / norm(d);                        // propagate.cu:280-281
+                        if (walk_kind(o, d) == 1) {
+                            start = true;
+                            flat_f = -1;
+                            node = 0;
+                            cmask = 0xFFu;
+                            best = __builtin_inff();
+                            best_rank = 0xFFFFFFFFu;
+                            last = (uint32_t)a.last_hit[pid];
+                        }
+                    }
+                } else if (pj < n) {
+                    q = pr1.w & ~RAY_SKIP;
+                    if (a.winv) a.winv[q] = pj;
+                    if (!(pr1.w & RAY_SKIP)) {
+                        o = v3(__uint_as_float(pr0.x), __uint_as_float(pr0.y), __uint_as_float(pr0.z));
+                        d = v3(__uint_as_float(pr0.w), __uint_as_float(pr1.x), __uint_as_float(pr1.y));
+                        last = pr1.z;
+                        if constexpr (COUNT) pid = a.walk_hist ? a.queue[q] : q;
+                        start = true;
+                        flat_f = -1;
+                        node = 0;
+                        cmask = 0xFFu;
+                        best = __builtin_inff();
+                        best_rank = 0xFFFFFFFFu;
+                    }
+                } else {                                  // sub-walk k of flat walk f
+                    const uint32_t it = pj - n, f = it / K, k = it - f * K;
+                    q = a.flat_q[f];
+                    pid = a.queue[q];
+                    o = load3(a.pos, pid);
+                    d = load3(a.dir, pid);
+                    d = d / norm(d);
+                    const uint2 item = K == 1u ? make_uint2(0u, 0xFFu) : g.wcut[k];
+                    const unsigned long long key = a.flat_best[f];
+                    start = true;
+                    flat_f = (int)f;
+                    node = item.x;
+                    cmask = item.y;
+                    best = key == ~0ull ? __builtin_inff() : __uint_as_float((uint32_t)(key >> 32));
+                    best_rank = key == ~0ull ? 0xFFFFFFFFu : (uint32_t)key;
+                    last = (uint32_t)a.last_hit[pid];
+                }
+                if (start) {
+                    slab = make_slab(v3(-o.x / d.x, -o.y / d.y, -o.z / d.z), v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z));
+                    best_id = -1;
+                    sp = 0;
+                    walk_done = false;
+                    has_ray = true;
+                    walk_cost = 0;
+                    pf.call(P_REFILL);
+                    if constexpr (COUNT) cnt.walks++;
+                }
+            }
+            // the wave claims new rays for R lanes without a prefetched one and loads
+            // their records; nothing waits for the loads until a lane starts the ray
+            if (!exhausted) {
+                const unsigned long long need = __ballot(!pv);
+                if (need != 0 && (__popcll(need) >= R || need == __ballot(1))) {
+                    const uint32_t want = (uint32_t)__popcll(need) < claim ? (uint32_t)__popcll(need) : claim;
+                    const uint32_t rank = (uint32_t)__popcll(need & ((1ull << lane) - 1ull));
+                    const int leader = __ffsll((long long)need) - 1;
+                    uint32_t base = 0;
+                    if ((int)lane == leader) base = atomicAdd(a.next, want);
+                    base = __shfl(base, leader);
+                    if (base + want >= total) exhausted = true;
+                    if (!pv && rank < want && base + rank < total) {
+                        pj = base + rank;
+                        pv = true;
+                        if (pj < n && a.rays) {
+                            pr0 = gld(a.rays + 2 * (size_t)pj);
+                            pr1 = gld(a.rays + 2 * (size_t)pj + 1);
+                        }
+                    }
+                }
+            }
+        } else if (!exhausted) {
             const unsigned long long need = __ballot(!has_ray);
             if (need != 0 && (__popcll(need) >= R || need == __ballot(1))) {
                 const uint32_t want = (uint32_t)__popcll(need) < claim ? (uint32_t)__popcll(need) : claim;
@@ -3165,7 +3300,8 @@ __global__ __launch_bounds__(TB, MINW) void trace_kernel(const DevGeom *__restri
             // every small launch).  Each restarts from the root seeded with its
             // best so far (conservative culling, the same nearest hit); the
             // lanes' stacks are abandoned and their LDS rows reused.
-            if (exhausted && __ballot(has_ray) != 0 && (uint32_t)__popcll(__ballot(has_ray)) <= drain_max &&
+            if (exhausted && (!PF || __ballot(pv) == 0) && __ballot(has_ray) != 0 &&
+                (uint32_t)__popcll(__ballot(has_ray)) <= drain_max &&
                 __ballot(has_ray && flat_f >= 0) == 0) {   // no cut-item sub-walks (they start mid-tree)
                 drain = true;   // after the loop, where the walk state below is no longer live
                 break;
@@ -3177,7 +3313,7 @@ __global__ __launch_bounds__(TB, MINW) void trace_kernel(const DevGeom *__restri
         const unsigned long long mw = __ballot(can_walk);
         const unsigned long long mt = __ballot(has_work);
         if ((mw | mt) == 0) {
-            if (exhausted && __ballot(has_ray) == 0) {
+            if (exhausted && __ballot(has_ray || (PF && pv)) == 0) {
                 break;
             }
             continue;                                    // walks ended: publish + refill
@@ -4014,6 +4150,12 @@ static bool shade_prefetch2() {
     const char *e = getenv("CHR_SHADE_PREFETCH2");
     return !(e && e[0] == '0');
 }
+// CHR_SHADE_SC=0: the shade kernel's prefetch and write-back under branches (the
+// per-iteration wait for its own stores, shade_kernel SC) (A/B)
+static bool shade_static_counts() {
+    const char *e = getenv("CHR_SHADE_SC");
+    return !(e && e[0] == '0');
+}
 static int shade_waves() {             // CHR_SHADE_WAVES=2|4: the shade kernel at 2 / 4 waves per SIMD (A/B)
     const char *e = getenv("CHR_SHADE_WAVES");
     return e ? atoi(e) : 3;
@@ -4133,6 +4275,12 @@ static int trace_refill_r() {
 // (r04 ab3, removed: a combined step -- every lane fetching its node AND its next
 // parked triangle each iteration -- ran trace 38.8 ms/step at 4 waves/SIMD (200 B
 // of spills) and 17.2 at 3, against 14.35 for the wave-wide node / triangle choice)
+// CHR_TRACE_PF=48|32|16: trace_kernel with prefetched ray records (PF), new records
+// claimed once that many lanes have used theirs (A/B; 0: off)
+static int trace_pf() {
+    const char *e = getenv("CHR_TRACE_PF");
+    return e ? atoi(e) : 0;
+}
 static int trace_layout() {
     const char *e = getenv("CHR_TRACE_LAYOUT");
     return e ? atoi(e) : 0;
@@ -4163,7 +4311,10 @@ static StepVariant select_step_variant(const chr_geometry *g) {
             sv.fn = propagate_step_kernel<8, 4, kWalk>;
             sv.trace = trace_refill_r() == 16 ? trace_kernel<false, 6, 12, 4, 16>
                        : (trace_refill_r() == 32 ? trace_kernel<false, 6, 12, 4, 32> : trace_kernel<false, 6, 12, 4, 48>);
-            if (trace_refill_r() == 48) {
+            if (trace_pf() == 48) sv.trace = trace_kernel<false, 6, 12, 4, 48, BLOCK, 0, true>;
+            else if (trace_pf() == 32) sv.trace = trace_kernel<false, 6, 12, 4, 32, BLOCK, 0, true>;
+            else if (trace_pf() == 16) sv.trace = trace_kernel<false, 6, 12, 4, 16, BLOCK, 0, true>;
+            else if (trace_refill_r() == 48) {
                 switch (trace_layout()) {
                     case 1: sv.trace = trace_kernel<false, 6, 11, 4, 48, 1024, TOP_NODES>; sv.trace_block = 1024; break;
                     case 2: sv.trace = trace_kernel<false, 6, 11, 4, 48, 1024, 0>; sv.trace_block = 1024; break;
@@ -4171,7 +4322,9 @@ static StepVariant select_step_variant(const chr_geometry *g) {
                 }
             }
             sv.shade = shade_waves() == 4 ? shade_kernel<4>
-                       : (shade_waves() == 2 ? shade_kernel<2> : (shade_prefetch2() ? shade_kernel<3, true> : shade_kernel<3>));
+                       : (shade_waves() == 2 ? shade_kernel<2>
+                          : (shade_prefetch2() ? (shade_static_counts() ? shade_kernel<3, true, true> : shade_kernel<3, true>)
+                                               : shade_kernel<3>));
             sv.tail = tail_group_walk() ? propagate_group_kernel<8, kGroupWaves>
                       : (tail_waves() == 4 ? propagate_tail_kernel<4>
                          : (tail_waves() == 3 ? propagate_tail_kernel<3> : propagate_tail_kernel<kTailWaves>));
@@ -5571,7 +5724,7 @@ extern "C" int chr_kernel_info(int32_t which, chr_kernel_attr *out) {
     const char *name = nullptr;
     switch (which) {
         case 0: fn = (const void *)trace_kernel<false, 6, 12, 4, 48>; name = "chr::trace_kernel<false,6,12,4,48>"; break;
-        case 1: fn = (const void *)shade_kernel<3, true>; name = "chr::shade_kernel<3,true>"; break;
+        case 1: fn = (const void *)shade_kernel<3, true, true>; name = "chr::shade_kernel<3,true,true>"; break;
         case 2: fn = (const void *)propagate_tail_kernel<kTailWaves>; name = "chr::propagate_tail_kernel<2>"; break;
         case 3: fn = (const void *)propagate_step_kernel<8, 4, kWalk>; name = "chr::propagate_step_kernel<8,4,2006>"; break;
         default: return chr::fail(CHR_ERR_INVALID, "chr_kernel_info: unknown kernel %d", which);
