@@ -3009,10 +3009,7 @@ __global__ __launch_bounds__(BLOCK) void permute_rays_kernel(const uint4 *rays_i
 // COUNT: walk counters; F: triangle step once F/8 of the walking lanes have
 // parked leaves (intersect_wide_spec); SL: stack entries in LDS; MINW: waves
 // per SIMD; R: refill once R of the 64 lanes are without a ray.
-// PF: each lane holds its next ray's record in registers (prefetched): a lane whose
-// walk ends starts that ray at once, and the wave claims and loads new records once
-// R lanes have used theirs (the loads land while the walks go on).
-template <bool COUNT, int F, int SL, int MINW, int R, int TB = BLOCK, int TOPN = 0, bool PF = false>
+template <bool COUNT, int F, int SL, int MINW, int R, int TB = BLOCK, int TOPN = 0>
 __global__ __launch_bounds__(TB, MINW) void trace_kernel(const DevGeom *__restrict__ gdev, TraceArgs a) {
     __shared__ uint32_t lds[(2 * SL + LEAFQ) * TB];
     // the top of the tree (stage_top): TB = 1024 makes one copy per CU serve its 16 waves
@@ -3062,10 +3059,6 @@ __global__ __launch_bounds__(TB, MINW) void trace_kernel(const DevGeom *__restri
     // next chunk's base, claimed ahead (valid in lane 0 once have_pend)
     uint32_t cb = 0, cn = 0, pend = 0;
     bool have_pend = false;
-    // PF: this lane's prefetched work item pj (pv) and, for a queued ray, its record
-    bool pv = false;
-    uint32_t pj = 0;
-    uint4 pr0 = make_uint4(0u, 0u, 0u, 0u), pr1 = make_uint4(0u, 0u, 0u, 0u);
     // claim size: CLAIM, or with spread a wave's share of a launch smaller than the
     // grid's lanes (every wave then walks a few rays and reaches its drain sooner)
     uint32_t claim = CLAIM;
@@ -3092,94 +3085,7 @@ __global__ __launch_bounds__(TB, MINW) void trace_kernel(const DevGeom *__restri
                 }
             }
         }
-        if constexpr (PF) {
-            // a lane without a walk starts its prefetched ray (no round trip)
-            if (!has_ray && pv) {
-                pv = false;
-                bool start = false;
-                if (pj < n && !a.rays) {                  // no ray records: from the photon arrays
-                    q = a.order ? a.order[pj] : pj;
-                    pid = a.queue[q];
-                    if (!((a.flags[pid] & 0xFFFFu) & DEAD_MASK)) {
-                        o = load3(a.pos, pid);
-                        d = load3(a.dir, pid);
-                        d = d / norm(d);                        // propagate.cu:280-281
-                        if (walk_kind(o, d) == 1) {
-                            start = true;
-                            flat_f = -1;
-                            node = 0;
-                            cmask = 0xFFu;
-                            best = __builtin_inff();
-                            best_rank = 0xFFFFFFFFu;
-                            last = (uint32_t)a.last_hit[pid];
-                        }
-                    }
-                } else if (pj < n) {
-                    q = pr1.w & ~RAY_SKIP;
-                    if (a.winv) a.winv[q] = pj;
-                    if (!(pr1.w & RAY_SKIP)) {
-                        o = v3(__uint_as_float(pr0.x), __uint_as_float(pr0.y), __uint_as_float(pr0.z));
-                        d = v3(__uint_as_float(pr0.w), __uint_as_float(pr1.x), __uint_as_float(pr1.y));
-                        last = pr1.z;
-                        if constexpr (COUNT) pid = a.walk_hist ? a.queue[q] : q;
-                        start = true;
-                        flat_f = -1;
-                        node = 0;
-                        cmask = 0xFFu;
-                        best = __builtin_inff();
-                        best_rank = 0xFFFFFFFFu;
-                    }
-                } else {                                  // sub-walk k of flat walk f
-                    const uint32_t it = pj - n, f = it / K, k = it - f * K;
-                    q = a.flat_q[f];
-                    pid = a.queue[q];
-                    o = load3(a.pos, pid);
-                    d = load3(a.dir, pid);
-                    d = d / norm(d);
-                    const uint2 item = K == 1u ? make_uint2(0u, 0xFFu) : g.wcut[k];
-                    const unsigned long long key = a.flat_best[f];
-                    start = true;
-                    flat_f = (int)f;
-                    node = item.x;
-                    cmask = item.y;
-                    best = key == ~0ull ? __builtin_inff() : __uint_as_float((uint32_t)(key >> 32));
-                    best_rank = key == ~0ull ? 0xFFFFFFFFu : (uint32_t)key;
-                    last = (uint32_t)a.last_hit[pid];
-                }
-                if (start) {
-                    slab = make_slab(v3(-o.x / d.x, -o.y / d.y, -o.z / d.z), v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z));
-                    best_id = -1;
-                    sp = 0;
-                    walk_done = false;
-                    has_ray = true;
-                    walk_cost = 0;
-                    pf.call(P_REFILL);
-                    if constexpr (COUNT) cnt.walks++;
-                }
-            }
-            // the wave claims new rays for R lanes without a prefetched one and loads
-            // their records; nothing waits for the loads until a lane starts the ray
-            if (!exhausted) {
-                const unsigned long long need = __ballot(!pv);
-                if (need != 0 && (__popcll(need) >= R || need == __ballot(1))) {
-                    const uint32_t want = (uint32_t)__popcll(need) < claim ? (uint32_t)__popcll(need) : claim;
-                    const uint32_t rank = (uint32_t)__popcll(need & ((1ull << lane) - 1ull));
-                    const int leader = __ffsll((long long)need) - 1;
-                    uint32_t base = 0;
-                    if ((int)lane == leader) base = atomicAdd(a.next, want);
-                    base = __shfl(base, leader);
-                    if (base + want >= total) exhausted = true;
-                    if (!pv && rank < want && base + rank < total) {
-                        pj = base + rank;
-                        pv = true;
-                        if (pj < n && a.rays) {
-                            pr0 = gld(a.rays + 2 * (size_t)pj);
-                            pr1 = gld(a.rays + 2 * (size_t)pj + 1);
-                        }
-                    }
-                }
-            }
-        } else if (!exhausted) {
+        if (!exhausted) {
             const unsigned long long need = __ballot(!has_ray);
             if (need != 0 && (__popcll(need) >= R || need == __ballot(1))) {
                 const uint32_t want = (uint32_t)__popcll(need) < claim ? (uint32_t)__popcll(need) : claim;
@@ -3300,8 +3206,7 @@ __global__ __launch_bounds__(TB, MINW) void trace_kernel(const DevGeom *__restri
             // every small launch).  Each restarts from the root seeded with its
             // best so far (conservative culling, the same nearest hit); the
             // lanes' stacks are abandoned and their LDS rows reused.
-            if (exhausted && (!PF || __ballot(pv) == 0) && __ballot(has_ray) != 0 &&
-                (uint32_t)__popcll(__ballot(has_ray)) <= drain_max &&
+            if (exhausted && __ballot(has_ray) != 0 && (uint32_t)__popcll(__ballot(has_ray)) <= drain_max &&
                 __ballot(has_ray && flat_f >= 0) == 0) {   // no cut-item sub-walks (they start mid-tree)
                 drain = true;   // after the loop, where the walk state below is no longer live
                 break;
@@ -3313,7 +3218,7 @@ __global__ __launch_bounds__(TB, MINW) void trace_kernel(const DevGeom *__restri
         const unsigned long long mw = __ballot(can_walk);
         const unsigned long long mt = __ballot(has_work);
         if ((mw | mt) == 0) {
-            if (exhausted && __ballot(has_ray || (PF && pv)) == 0) {
+            if (exhausted && __ballot(has_ray) == 0) {
                 break;
             }
             continue;                                    // walks ended: publish + refill
@@ -4266,6 +4171,10 @@ static int trace_refill_r() {
 // CHR_TRACE_LAYOUT (A/B): 0 256-thread workgroups, 12 LDS stack entries per lane;
 // 1 1024-thread workgroups (one per CU), 11 entries, the top TOP_NODES nodes of
 // the tree in LDS (stage_top); 2 the same without the top nodes (control).
+// (r04 ab11, removed: each lane holding its next ray's record in registers, started
+// as soon as its walk ends, records claimed and loaded for R lanes at a time: every
+// launch 30-40% longer, trace 14.0 -> 18.3 ms per step -- lanes restarting one by one
+// break the cohorts of neighbouring rays that start and walk together.)
 // (r04 ab7, removed: the per-child offsets derived from the kind bytes by byte-wise
 // prefix sums instead of loaded -- five 16-byte node loads per node step, not six:
 // trace 14.16 vs 14.18 ms per step, 492.2 vs 491.7 M/s: the walk is not bound by
@@ -4275,12 +4184,6 @@ static int trace_refill_r() {
 // (r04 ab3, removed: a combined step -- every lane fetching its node AND its next
 // parked triangle each iteration -- ran trace 38.8 ms/step at 4 waves/SIMD (200 B
 // of spills) and 17.2 at 3, against 14.35 for the wave-wide node / triangle choice)
-// CHR_TRACE_PF=48|32|16: trace_kernel with prefetched ray records (PF), new records
-// claimed once that many lanes have used theirs (A/B; 0: off)
-static int trace_pf() {
-    const char *e = getenv("CHR_TRACE_PF");
-    return e ? atoi(e) : 0;
-}
 static int trace_layout() {
     const char *e = getenv("CHR_TRACE_LAYOUT");
     return e ? atoi(e) : 0;
@@ -4311,10 +4214,7 @@ static StepVariant select_step_variant(const chr_geometry *g) {
             sv.fn = propagate_step_kernel<8, 4, kWalk>;
             sv.trace = trace_refill_r() == 16 ? trace_kernel<false, 6, 12, 4, 16>
                        : (trace_refill_r() == 32 ? trace_kernel<false, 6, 12, 4, 32> : trace_kernel<false, 6, 12, 4, 48>);
-            if (trace_pf() == 48) sv.trace = trace_kernel<false, 6, 12, 4, 48, BLOCK, 0, true>;
-            else if (trace_pf() == 32) sv.trace = trace_kernel<false, 6, 12, 4, 32, BLOCK, 0, true>;
-            else if (trace_pf() == 16) sv.trace = trace_kernel<false, 6, 12, 4, 16, BLOCK, 0, true>;
-            else if (trace_refill_r() == 48) {
+            if (trace_refill_r() == 48) {
                 switch (trace_layout()) {
                     case 1: sv.trace = trace_kernel<false, 6, 11, 4, 48, 1024, TOP_NODES>; sv.trace_block = 1024; break;
                     case 2: sv.trace = trace_kernel<false, 6, 11, 4, 48, 1024, 0>; sv.trace_block = 1024; break;
