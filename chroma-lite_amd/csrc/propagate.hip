@@ -4171,6 +4171,8 @@ static int trace_refill_r() {
 // CHR_TRACE_LAYOUT (A/B): 0 256-thread workgroups, 12 LDS stack entries per lane;
 // 1 1024-thread workgroups (one per CU), 11 entries, the top TOP_NODES nodes of
 // the tree in LDS (stage_top); 2 the same without the top nodes (control).
+// (r04 ab12: refill threshold R = 56 / 64 trace 14.45 / 17.36 ms per step against
+// 14.06 at 48; the node / triangle threshold F = 5 / 7 14.03 / 14.42 against 14.06 at 6)
 // (r04 ab11, removed: each lane holding its next ray's record in registers, started
 // as soon as its walk ends, records claimed and loaded for R lanes at a time: every
 // launch 30-40% longer, trace 14.0 -> 18.3 ms per step -- lanes restarting one by one
