@@ -2858,9 +2858,19 @@ __global__ __launch_bounds__(BLOCK) void ref_triangles_kernel(const float4 *wtri
 // ---------------------------------------------------------------- ray binning (trace order)
 // The order in which trace_kernel walks the queued rays does not change any
 // result (each walk's result is stored at its queue position), so rays are
-// binned by direction cell (16-bit radix sort, 65,536 octahedral cells) to make the
+// binned by direction cell (a 22-bit radix sort of 2^22 octahedral cells in Morton order
+// by default, bin_key_mode; round 1-3: 16 bits, 65,536 cells row-major) to make the
 // 64 rays of a wave walk the same subtrees: better L1/L2 reuse of nodes.
-__device__ __forceinline__ uint32_t octa_cell(V3 d) {   // octahedral map of a unit vector, 8 bits per axis
+// kmode (CHR_BIN_KEY, A/B): 0 row-major 8+8 bits; 1 the same cells in Morton order (2D-near
+// cells adjacent in walk order); 2 / 3 / 4 Morton order of 10+10 / 11+11 / 12+12-bit cells
+// (20 / 22 / 24-bit sorts)
+__device__ __forceinline__ uint32_t spread_bits(uint32_t x) {   // bit i -> bit 2i (x < 2^16)
+    x = (x | (x << 8)) & 0x00FF00FFu;
+    x = (x | (x << 4)) & 0x0F0F0F0Fu;
+    x = (x | (x << 2)) & 0x33333333u;
+    return (x | (x << 1)) & 0x55555555u;
+}
+__device__ __forceinline__ uint32_t octa_cell(V3 d, uint32_t kmode = 0) {   // octahedral map of a unit vector
     const float s = fabsf(d.x) + fabsf(d.y) + fabsf(d.z);
     float u = d.x / s, v = d.y / s;
     if (d.z < 0.0f) {
@@ -2868,21 +2878,27 @@ __device__ __forceinline__ uint32_t octa_cell(V3 d) {   // octahedral map of a u
         const float vv = (1.0f - fabsf(u)) * (v < 0.0f ? -1.0f : 1.0f);
         u = uu; v = vv;
     }
+    if (kmode >= 2) {   // b = 8 + kmode bits per axis
+        const float half = (float)(1u << (7u + kmode)), top = (float)((1u << (8u + kmode)) - 1u);
+        const uint32_t iu = (uint32_t)fminf(fmaxf((u + 1.0f) * half, 0.0f), top);
+        const uint32_t iv = (uint32_t)fminf(fmaxf((v + 1.0f) * half, 0.0f), top);
+        return (spread_bits(iv) << 1) | spread_bits(iu);
+    }
     const uint32_t iu = (uint32_t)fminf(fmaxf((u + 1.0f) * 128.0f, 0.0f), 255.0f);
     const uint32_t iv = (uint32_t)fminf(fmaxf((v + 1.0f) * 128.0f, 0.0f), 255.0f);
-    return (iv << 8) | iu;
+    return kmode == 1 ? ((spread_bits(iv) << 1) | spread_bits(iu)) : ((iv << 8) | iu);
 }
 // direction-binning key of a queued photon (0 for a zero / non-finite direction)
-__device__ __forceinline__ uint32_t bin_key_of(V3 d) {
+__device__ __forceinline__ uint32_t bin_key_of(V3 d, uint32_t kmode = 0) {
     const float l = sqrtf(d.x * d.x + d.y * d.y + d.z * d.z);
-    return (l > 0.0f && l < __builtin_inff()) ? octa_cell(v3(d.x / l, d.y / l, d.z / l)) : 0u;
+    return (l > 0.0f && l < __builtin_inff()) ? octa_cell(v3(d.x / l, d.y / l, d.z / l), kmode) : 0u;
 }
 __global__ __launch_bounds__(BLOCK) void bin_key_kernel(const float *dir, const uint32_t *queue, uint32_t n,
-                                                        uint32_t *keys, uint32_t *vals) {
+                                                        uint32_t *keys, uint32_t *vals, uint32_t kmode) {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     if (i >= n) return;
     const uint32_t pid = queue[i];
-    keys[i] = bin_key_of(v3(dir[3 * pid], dir[3 * pid + 1], dir[3 * pid + 2]));
+    keys[i] = bin_key_of(v3(dir[3 * pid], dir[3 * pid + 1], dir[3 * pid + 2]), kmode);
     vals[i] = i;
 }
 // ---------------------------------------------------------------- wavefront split
@@ -2980,12 +2996,12 @@ __global__ __launch_bounds__(BLOCK) void classify_kernel(const float *pos, const
                                                          const int32_t *last_hit, const uint32_t *queue, uint32_t n,
                                                          int2 *hits, uint32_t *flat_q, uint32_t *flat_count,
                                                          unsigned long long *flat_best, uint32_t *keys, uint32_t *vals,
-                                                         uint4 *rays) {
+                                                         uint4 *rays, uint32_t kmode) {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     if (i >= n) return;
     const uint32_t pid = queue[i];
     if (keys) {
-        keys[i] = bin_key_of(v3(dir[3 * pid], dir[3 * pid + 1], dir[3 * pid + 2]));
+        keys[i] = bin_key_of(v3(dir[3 * pid], dir[3 * pid + 1], dir[3 * pid + 2]), kmode);
         vals[i] = i;
     }
     if ((flags[pid] & 0xFFFFu) & DEAD_MASK) {
@@ -3976,11 +3992,23 @@ extern "C" int chr_rng_download(const uint32_t *d_states, uint32_t nslots, uint3
     return CHR_OK;
 }
 
-static size_t sort_temp_bytes16(uint32_t n) {
+// the direction-binning sort's temporary storage (allocated for 24-bit keys, the largest
+// CHR_BIN_KEY asks for; queried with the bits of the sort at hand)
+static size_t sort_temp_bytes16(uint32_t n, int bits = 24) {
     size_t bytes = 0;
     (void)rocprim::radix_sort_pairs((void *)nullptr, bytes, (const uint32_t *)nullptr, (uint32_t *)nullptr,
-                                    (const uint32_t *)nullptr, (uint32_t *)nullptr, n, 0, 16);
+                                    (const uint32_t *)nullptr, (uint32_t *)nullptr, n, 0, bits);
     return bytes;
+}
+// CHR_BIN_KEY=0..4: direction-binning keys of row-major 8+8-bit octahedral cells (0), or in
+// Morton order of 8+8 / 10+10 / 11+11 / 12+12-bit cells (1..4).  Default 3: the binned first
+// launch 5.0 -> 4.63 ms (10 M rays of the 29k bench), 490.3 -> 495.6 M/s (r04 ab15/ab16,
+// photons identical): a wave's 64 rays come from a compact patch of directions instead
+// of a 0.5-degree cell's ~150 rays in queue order.
+static uint32_t bin_key_mode() {
+    const char *e = getenv("CHR_BIN_KEY");
+    const int k = e ? atoi(e) : 3;
+    return (uint32_t)(k >= 0 && k <= 4 ? k : 3);
 }
 static size_t sort_temp_bytes(uint32_t n) {
     size_t bytes = 0;
@@ -4568,7 +4596,7 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
             hipLaunchKernelGGL(classify_kernel, dim3(grid_for(n)), dim3(BLOCK), 0, stream, ph->d_pos, ph->d_dir,
                                ph->d_flags, ph->d_last_hit_triangles, in_queue, n, hits, fc->flat_q, count_cur,
                                fc->flat_best, bin_now ? keys : nullptr, bin_now ? order : nullptr,
-                               use_rays ? fc->rays : nullptr);
+                               use_rays ? fc->rays : nullptr, bin_key_mode());
         TraceArgs ta;
         ta.pos = ph->d_pos; ta.dir = ph->d_dir; ta.flags = ph->d_flags; ta.last_hit = ph->d_last_hit_triangles;
         ta.queue = in_queue; ta.n = n; ta.hits = hits; ta.next = next; ta.counters = counters; ta.order = nullptr;
@@ -4598,10 +4626,11 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
             if (bin_now) {
                 if (!first_one_step)   // the first step's keys came with its classification
                     hipLaunchKernelGGL(bin_key_kernel, dim3(grid_for(n)), dim3(BLOCK), 0, stream, ph->d_dir, in_queue,
-                                       n, keys, order);
+                                       n, keys, order, bin_key_mode());
                 void *temp = (void *)(((uintptr_t)(vals_out + n) + 255) & ~(uintptr_t)255);
-                size_t temp_bytes = sort_temp_bytes16(n);
-                CHR_HIP_CHECK(rocprim::radix_sort_pairs(temp, temp_bytes, keys, keys_out, order, vals_out, n, 0, 16,
+                const int kbits = bin_key_mode() >= 2 ? 16 + 2 * (int)bin_key_mode() : 16;
+                size_t temp_bytes = sort_temp_bytes16(n, kbits);
+                CHR_HIP_CHECK(rocprim::radix_sort_pairs(temp, temp_bytes, keys, keys_out, order, vals_out, n, 0, kbits,
                                                         stream));
                 if (use_rays)   // the records in the binned walk order
                     hipLaunchKernelGGL(permute_rays_kernel, dim3(grid_for(n)), dim3(BLOCK), 0, stream, fc->rays,
