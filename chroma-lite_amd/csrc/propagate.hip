@@ -2858,12 +2858,12 @@ __global__ __launch_bounds__(BLOCK) void ref_triangles_kernel(const float4 *wtri
 // ---------------------------------------------------------------- ray binning (trace order)
 // The order in which trace_kernel walks the queued rays does not change any
 // result (each walk's result is stored at its queue position), so rays are
-// binned by direction cell (a 22-bit radix sort of 2^22 octahedral cells in Morton order
+// binned by direction cell (a 22-bit radix sort of 2^22 octahedral cells in Hilbert order
 // by default, bin_key_mode; round 1-3: 16 bits, 65,536 cells row-major) to make the
 // 64 rays of a wave walk the same subtrees: better L1/L2 reuse of nodes.
 // kmode (CHR_BIN_KEY, A/B): 0 row-major 8+8 bits; 1 the same cells in Morton order (2D-near
 // cells adjacent in walk order); 2 / 3 / 4 Morton order of 10+10 / 11+11 / 12+12-bit cells
-// (20 / 22 / 24-bit sorts)
+// (20 / 22 / 24-bit sorts); 5 11+11-bit cells in Hilbert order (22 bits)
 __device__ __forceinline__ uint32_t spread_bits(uint32_t x) {   // bit i -> bit 2i (x < 2^16)
     x = (x | (x << 8)) & 0x00FF00FFu;
     x = (x | (x << 4)) & 0x0F0F0F0Fu;
@@ -2877,6 +2877,20 @@ __device__ __forceinline__ uint32_t octa_cell(V3 d, uint32_t kmode = 0) {   // o
         const float uu = (1.0f - fabsf(v)) * (u < 0.0f ? -1.0f : 1.0f);
         const float vv = (1.0f - fabsf(u)) * (v < 0.0f ? -1.0f : 1.0f);
         u = uu; v = vv;
+    }
+    if (kmode == 5) {   // 11+11-bit cells in Hilbert order (no jumps between quadrants)
+        uint32_t x = (uint32_t)fminf(fmaxf((u + 1.0f) * 1024.0f, 0.0f), 2047.0f);
+        uint32_t y = (uint32_t)fminf(fmaxf((v + 1.0f) * 1024.0f, 0.0f), 2047.0f);
+        uint32_t dkey = 0;
+        for (uint32_t sq = 1024u; sq > 0u; sq >>= 1) {
+            const uint32_t rx = (x & sq) ? 1u : 0u, ry = (y & sq) ? 1u : 0u;
+            dkey += sq * sq * ((3u * rx) ^ ry);
+            if (ry == 0u) {   // rotate the quadrant
+                if (rx == 1u) { x = 2047u - x; y = 2047u - y; }
+                const uint32_t t = x; x = y; y = t;
+            }
+        }
+        return dkey;
     }
     if (kmode >= 2) {   // b = 8 + kmode bits per axis
         const float half = (float)(1u << (7u + kmode)), top = (float)((1u << (8u + kmode)) - 1u);
@@ -4000,15 +4014,16 @@ static size_t sort_temp_bytes16(uint32_t n, int bits = 24) {
                                     (const uint32_t *)nullptr, (uint32_t *)nullptr, n, 0, bits);
     return bytes;
 }
-// CHR_BIN_KEY=0..4: direction-binning keys of row-major 8+8-bit octahedral cells (0), or in
-// Morton order of 8+8 / 10+10 / 11+11 / 12+12-bit cells (1..4).  Default 3: the binned first
-// launch 5.0 -> 4.63 ms (10 M rays of the 29k bench), 490.3 -> 495.6 M/s (r04 ab15/ab16,
-// photons identical): a wave's 64 rays come from a compact patch of directions instead
-// of a 0.5-degree cell's ~150 rays in queue order.
+// CHR_BIN_KEY=0..5: direction-binning keys of row-major 8+8-bit octahedral cells (0), in
+// Morton order of 8+8 / 10+10 / 11+11 / 12+12-bit cells (1..4), or of 11+11-bit cells in
+// Hilbert order (5).  Morton 11+11: the binned first launch 5.0 -> 4.63 ms (10 M rays of the
+// 29k bench), 490.3 -> 495.6 M/s (r04 ab15/ab16): a wave's 64 rays come from a compact
+// patch of directions instead of a 0.5-degree cell's ~150 rays in queue order.  Hilbert
+// (default): 4.60 -> 4.55 ms, 498.8 -> 500.3 M/s (ab18).  Photons identical in all.
 static uint32_t bin_key_mode() {
     const char *e = getenv("CHR_BIN_KEY");
-    const int k = e ? atoi(e) : 3;
-    return (uint32_t)(k >= 0 && k <= 4 ? k : 3);
+    const int k = e ? atoi(e) : 5;
+    return (uint32_t)(k >= 0 && k <= 5 ? k : 5);
 }
 static size_t sort_temp_bytes(uint32_t n) {
     size_t bytes = 0;
@@ -4628,7 +4643,7 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
                     hipLaunchKernelGGL(bin_key_kernel, dim3(grid_for(n)), dim3(BLOCK), 0, stream, ph->d_dir, in_queue,
                                        n, keys, order, bin_key_mode());
                 void *temp = (void *)(((uintptr_t)(vals_out + n) + 255) & ~(uintptr_t)255);
-                const int kbits = bin_key_mode() >= 2 ? 16 + 2 * (int)bin_key_mode() : 16;
+                const int kbits = bin_key_mode() == 5 ? 22 : (bin_key_mode() >= 2 ? 16 + 2 * (int)bin_key_mode() : 16);
                 size_t temp_bytes = sort_temp_bytes16(n, kbits);
                 CHR_HIP_CHECK(rocprim::radix_sort_pairs(temp, temp_bytes, keys, keys_out, order, vals_out, n, 0, kbits,
                                                         stream));
