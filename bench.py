@@ -194,15 +194,34 @@ def build_geometry(name, cache_dir):
 
 def shared_geometry(name, cache_dir, rank, dist):
     """Rank 0 builds (flatten + BVH: minutes for the 29k detector) and fills
-    the node-local cache; the other ranks wait at a barrier, then load it."""
+    the node-local cache -- the reference BVH and the traversal BVH derived from
+    it (chroma.gpu.wide_bvh, 33-36 s of host build on the 29k detector) -- while
+    the other ranks wait at a barrier, then load both from the cache.  Returns
+    (geometry, setup phases: geometry_s, and on rank 0 of a multi-rank job
+    wide_bvh_prepare_s / wide_bvh_prepare_source)."""
+    t0 = time.time()
     if dist is None or not cache_dir:
-        return build_geometry(name, cache_dir)
+        return build_geometry(name, cache_dir), {'geometry_s': round(time.time() - t0, 2)}
+    setup = {}
     if rank == 0:
         det = build_geometry(name, cache_dir)
+        setup['geometry_s'] = round(time.time() - t0, 2)
+        from chroma.gpu import wide_bvh
+        t1 = time.time()
+        setup['wide_bvh_prepare_source'] = wide_bvh.prepare(det)
+        setup['wide_bvh_prepare_s'] = round(time.time() - t1, 2)
     dist.barrier()
     if rank != 0:
+        t1 = time.time()
         det = build_geometry(name, cache_dir)
-    return det
+        setup['geometry_s'] = round(time.time() - t1, 2)
+        setup['barrier_wait_s'] = round(t1 - t0, 2)
+    return det, setup
+
+
+def _native_host_threads():
+    from chroma.gpu import _native
+    return _native.host_threads()
 
 
 def rng_first_subsequence(rank, nslots):
@@ -385,12 +404,15 @@ class PropagateWorkload(object):
         self.args, self.rank, self.world, self.local, self.nphotons = args, rank, world, local, nphotons
         self.torch = torch
         t_setup = time.time()
-        self.det = shared_geometry(args.detector, args.cache_dir, rank, dist)
+        self.det, self.setup = shared_geometry(args.detector, args.cache_dir, rank, dist)
         t0 = time.time()
         self.gdet = gpu.GPUDetector(self.det)
-        self.setup = {'geometry_s': round(t0 - t_setup, 2), 'upload_s': round(time.time() - t0, 2)}
-        log('rank %d: geometry on device in %.1fs (%.2f GB)' % (rank, time.time() - t0,
-                                                               self.gdet.device_bytes() / 1e9))
+        # GPUDetector's phases: packing, traversal BVH (cache load or host build), H2D
+        self.setup['upload_s'] = round(time.time() - t0, 2)
+        self.setup.update(getattr(self.gdet, 'setup_times', {}))
+        self.setup['host_threads'] = _native_host_threads()
+        log('rank %d: geometry on device in %.1fs (%.2f GB; %s)' % (rank, time.time() - t0,
+                                                                   self.gdet.device_bytes() / 1e9, self.setup))
         self.nslots = args.nthreads_per_block * args.max_blocks
         self.rng = gpu.get_rng_states(self.nslots, seed=args.seed,
                                       first_subsequence=rng_first_subsequence(rank, self.nslots))
@@ -547,19 +569,11 @@ class PropagateWorkload(object):
                 'channels': self.det.num_channels()}
 
     # ------------------------------------------------------------ oracle checks
-    def photons_of_rank(self, r):
-        """Rank r's photon source: its own seed and shard size (rank 0 regenerates
-        another rank's photons to check that rank's GPU sample against the oracle)."""
-        if r == self.rank:
-            return self.photons
-        from chroma.photon_source import isotropic
-        return isotropic(photons_for_rank(self.args, r, self.world), seed=PHOTON_SEED + r)
-
-    def _oracle_batches(self, n, threads, rank=None):
-        """The oracle on rank `rank`'s first n photons (default: this rank's) as two
-        batches in order (the RNG states carried from one to the next, as two
-        propagate calls), from that rank's own RNG subsequences.  Returns (hosts,
-        walk stats, seconds)."""
+    def _oracle_batches(self, n, threads, rank=None, inputs=None):
+        """The oracle on rank `rank`'s first n photons (default: this rank's; another
+        rank's come as `inputs`, the arrays its gpu_sample sent) as two batches in
+        order (the RNG states carried from one to the next, as two propagate calls),
+        from that rank's own RNG subsequences.  Returns (hosts, walk stats, seconds)."""
         sys.path.insert(0, os.path.join(ROOT, 'oracle'))
         import oracle
         from chroma.event import Photons
@@ -568,7 +582,8 @@ class PropagateWorkload(object):
             self._packed = PackedGeometry(self.det)
         a = self.args
         rank = self.rank if rank is None else rank
-        ph = self.photons_of_rank(rank)
+        ph = self.photons if inputs is None else Photons(inputs['pos'], inputs['dir'], inputs['pol'],
+                                                         inputs['wavelengths'])
         cuts = [0, n // 2, n]
         hosts = [oracle.HostPhotons(Photons(ph.pos[lo:hi], ph.dir[lo:hi], ph.pol[lo:hi], ph.wavelengths[lo:hi]))
                  for lo, hi in zip(cuts[:-1], cuts[1:])]
@@ -626,7 +641,11 @@ class PropagateWorkload(object):
                 gp.propagate(self.gdet, rng, **kw)
                 sts.append(gp.last_stats)
         got = [gp.get() for gp in gps]
-        return {'rank': self.rank, 'n': int(n), 'batches': [int(c) for c in np.diff(cuts)],
+        # the inputs go with the photons: rank 0 runs the oracle on them (regenerating
+        # another rank's whole shard to take its first n photons would cost rank 0 the
+        # memory of every shard)
+        inputs = {f: np.ascontiguousarray(getattr(ph, f)[:n]) for f in ('pos', 'dir', 'pol', 'wavelengths')}
+        return {'rank': self.rank, 'n': int(n), 'batches': [int(c) for c in np.diff(cuts)], 'inputs': inputs,
                 'path': 'propagate_batches (pipelined)' if pipeline else 'propagate (sequential)',
                 'stack_overflows': int(sum(s.stack_overflows for s in sts)),
                 'photons': {f: np.concatenate([getattr(o, f) for o in got]) for f in self.PARITY_FIELDS}}
@@ -685,7 +704,7 @@ class PropagateWorkload(object):
         """On rank 0: the oracle for another rank's GPU sample (that rank's photon
         seed and RNG subsequences; only they differ, the geometry is rank 0's),
         compared photon by photon.  The other ranks build no host geometry copy."""
-        hosts, _, _ = self._oracle_batches(sample['n'], threads, rank=sample['rank'])
+        hosts, _, _ = self._oracle_batches(sample['n'], threads, rank=sample['rank'], inputs=sample['inputs'])
         return self.compare(sample, hosts)
 
 
@@ -790,6 +809,11 @@ def run_rank(args):
         if dist.get_world_size() != args.gpus:
             raise SystemExit('bench.py: process group has %d ranks, --gpus %d' % (dist.get_world_size(), args.gpus))
     nphotons = photons_for_rank(args, rank, world)
+    # libchroma_amd's host-side builds use this rank's share of the job's cores
+    # (the box's cgroup quota, not nproc), not a full team per rank
+    local_world = int(os.environ.get('LOCAL_WORLD_SIZE', str(world)))
+    from chroma.gpu import _native
+    _native.set_host_threads(max(1, usable_cpus() // max(1, local_world)))
     wl = WORKLOAD(args, rank, world, local, dist, nphotons)
 
     # pipelined runs warm up with at least 2 steps: a 1-batch call does not use
@@ -841,6 +865,9 @@ def run_rank(args):
     # send the photons to rank 0; rank 0 runs the timed cpu_baseline alone on the host
     # (its own parity), then the oracle for every other rank's sample -- only rank 0
     # holds a host copy of the geometry's packed tables (PackedGeometry)
+    # this rank's memory before the oracle checks (rank 0's checks hold the oracle's
+    # host copy of the geometry and every rank's sample: reported apart)
+    report.update(host_memory())
     check, samples = None, None
     if not args.no_cpu_baseline:
         mine = None
@@ -853,7 +880,7 @@ def run_rank(args):
             check = wl.check(True, args.cpu_budget, usable_cpus(), 0)
             per_rank = [check[2]] + [wl.check_rank(smp, usable_cpus()) for smp in (samples or [None])[1:]]
             check = (check[0], check[1], check[2], per_rank)
-    report.update(host_memory())
+    report['host_peak_rss_gb_after_checks'] = host_memory().get('host_peak_rss_gb')
     if dist is not None:
         reports = [None] * world
         dist.all_gather_object(reports, report)
@@ -870,7 +897,8 @@ def run_rank(args):
                   'ranks_seen': len(reports),
                   'ranks': [dict({k: rep[k] for k in ('rank', 'local_rank', 'host', 'device', 'photons_per_step')},
                                  setup=rep.get('setup'), host_rss_gb=rep.get('host_rss_gb'),
-                                 host_peak_rss_gb=rep.get('host_peak_rss_gb'))
+                                 host_peak_rss_gb=rep.get('host_peak_rss_gb'),
+                                 host_peak_rss_gb_after_checks=rep.get('host_peak_rss_gb_after_checks'))
                             for rep in reports],
                   'kernel_ms_per_step': (timing_pass['kernel_ms_per_step'] if timing_pass else r0['kernel_ms'] / steps),
                   'trace_ms_per_step': r0['trace_ms'] / steps,

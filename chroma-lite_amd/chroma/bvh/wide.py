@@ -1,8 +1,9 @@
 """Host view of the traversal BVH the gfx950 kernel walks (csrc/wide_bvh.h).
 
-chr_geometry_create builds this tree itself; this module exposes the same
-build so tests can check its invariants (containment after the kernel's
-float decode, every reachable triangle exactly once, reference DFS ranks).
+GPUGeometry obtains this tree through chroma.gpu.wide_bvh (cached compact
+form, or a build); this module exposes the full build, records included, so
+tests can check its invariants (containment after the kernel's float decode,
+every reachable triangle exactly once, reference DFS ranks).
 No reference counterpart: it is derived from the reference BVH
 (chroma/bvh/grid.py) and never replaces it in the Python API.
 """

@@ -10,7 +10,10 @@ arrays the propagator consumes (vertices, triangles, solid_id, colors,
 material/surface indices), every unique material and surface property table,
 the detector channel maps and time/charge CDFs, and the mesh MD5 (read alone
 by get_geometry_hash, as cache.py:141-151).  As in the reference, the BVH and
-the placed solids are not saved with a geometry (cache.py:105-110).
+the placed solids are not saved with a geometry (cache.py:105-110).  The
+traversal BVH the kernels walk is cached beside the reference BVH it was
+built from (``bvh/<md5>/<name>.wide/``, chroma.gpu.wide_bvh); a BVH loaded or
+saved here carries ``cache_ref`` to find it.
 """
 import json
 import os
@@ -321,7 +324,10 @@ class Cache(object):
         bvh_dir = self.get_bvh_directory(mesh_hash)
         if not os.path.isdir(bvh_dir):
             return []
-        return [n for n in os.listdir(bvh_dir) if not n.endswith('.tmp.npz')]
+        # BVH files only: the traversal BVHs cached beside them are directories
+        # (<name>.wide/, chroma.gpu.wide_bvh)
+        return [n for n in os.listdir(bvh_dir)
+                if not n.endswith('.tmp.npz') and os.path.isfile(os.path.join(bvh_dir, n))]
 
     def exist_bvh(self, mesh_hash, name='default'):
         return os.path.isfile(self.get_bvh_filename(mesh_hash, name))
@@ -334,6 +340,7 @@ class Cache(object):
                    {'nodes': bvh.nodes, 'layer_offsets': np.asarray(bvh.layer_offsets, dtype=np.int64),
                     'world_origin': np.asarray(bvh.world_coords.world_origin),
                     'world_scale': np.asarray(bvh.world_coords.world_scale)})
+        bvh.cache_ref = (self.cache_dir, mesh_hash, name)
 
     def load_bvh(self, mesh_hash, name='default'):
         from chroma.bvh import BVH, WorldCoords
@@ -341,10 +348,17 @@ class Cache(object):
         if not os.path.exists(bvh_file):
             raise BVHNotFoundError(mesh_hash + ':' + name)
         with np.load(bvh_file, allow_pickle=False) as z:
-            return BVH(WorldCoords(z['world_origin'], z['world_scale'][()]), z['nodes'],
-                       [int(x) for x in z['layer_offsets']])
+            bvh = BVH(WorldCoords(z['world_origin'], z['world_scale'][()]), z['nodes'],
+                      [int(x) for x in z['layer_offsets']])
+        # where the traversal BVH derived from this one is cached (chroma.gpu.wide_bvh)
+        bvh.cache_ref = (self.cache_dir, mesh_hash, name)
+        return bvh
 
     def remove_bvh(self, mesh_hash, name='default'):
         bvh_file = self.get_bvh_filename(mesh_hash, name)
         if os.path.exists(bvh_file):
             os.remove(bvh_file)
+        wide_dir = bvh_file + '.wide'      # the traversal BVHs derived from it
+        if os.path.isdir(wide_dir):
+            import shutil
+            shutil.rmtree(wide_dir, ignore_errors=True)

@@ -59,6 +59,12 @@ class GeometryDesc(ctypes.Structure):
                 ('wireplanes', ctypes.POINTER(WirePlaneDesc))]
 
 
+class WideBvhDesc(ctypes.Structure):
+    """chr_wide_bvh_desc: the traversal BVH in compact (cacheable) form."""
+    _fields_ = [('nnodes', c_u32), ('nrec', c_u32), ('ncut', c_u32), ('max_depth', c_u32), ('usable', c_i32),
+                ('leaf_max', c_u32), ('h_nodes', c_vp), ('h_rec_id', c_vp), ('h_rec_rank', c_vp), ('h_cut', c_vp)]
+
+
 class PhotonsDesc(ctypes.Structure):
     _fields_ = [('d_pos', c_vp), ('d_dir', c_vp), ('d_pol', c_vp), ('d_wavelengths', c_vp), ('d_t', c_vp),
                 ('d_weights', c_vp), ('d_flags', c_vp), ('d_last_hit_triangles', c_vp), ('d_evidx', c_vp)]
@@ -119,6 +125,14 @@ _SIGNATURES = {
                                   ctypes.POINTER(ctypes.c_int32)]),
     'chr_wide_bvh_copy': (c_i32, [c_vp, c_vp, c_vp]),
     'chr_wide_bvh_free': (c_i32, [c_vp]),
+    'chr_wide_bvh_describe': (c_i32, [c_vp, ctypes.POINTER(WideBvhDesc)]),
+    'chr_wide_bvh_export': (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp]),
+    'chr_wide_bvh_key': (c_i32, [ctypes.c_char_p, c_u32]),
+    'chr_wide_bvh_records': (c_i32, [ctypes.POINTER(GeometryDesc), ctypes.POINTER(WideBvhDesc), c_u32, c_u32, c_vp]),
+    'chr_geometry_create_wide': (c_i32, [ctypes.POINTER(GeometryDesc), ctypes.POINTER(WideBvhDesc),
+                                         ctypes.POINTER(c_vp)]),
+    'chr_set_host_threads': (c_i32, [c_i32]),
+    'chr_get_host_threads': (c_i32, []),
     'chr_daq_begin': (c_i32, [c_vp, c_vp, c_vp, c_u32, c_f32, c_vp]),
     'chr_daq_acquire': (c_i32, [ctypes.POINTER(PhotonsDesc), c_vp, c_u32, c_vp, c_u32, c_i32, c_i32, c_vp, c_vp,
                                 c_vp, c_vp, c_vp, c_i32, c_i32, c_f32, c_i32, c_i32, c_vp]),
@@ -212,3 +226,13 @@ def kernel_info():
         out.append(dict(name=a.name.decode(), private_bytes=int(a.private_bytes), lds_bytes=int(a.lds_bytes),
                         vgprs=int(a.vgprs), max_threads=int(a.max_threads)))
     return out
+
+
+def set_host_threads(n):
+    """Threads of the library's host-side parallel regions (chr_set_host_threads;
+    0 restores the default: usable cores / $LOCAL_WORLD_SIZE)."""
+    call('chr_set_host_threads', int(n))
+
+
+def host_threads():
+    return int(lib().chr_get_host_threads())

@@ -1,17 +1,20 @@
 """GPUGeometry (drop-in for reference chroma/gpu/geometry.py:13-565).
 
-Packs the geometry (chroma.gpu.packing) and uploads it with
-chr_geometry_create, which lays it out for the gfx950 traversal kernel
+Packs the geometry (chroma.gpu.packing), obtains the traversal BVH
+(chroma.gpu.wide_bvh: cached next to the reference BVH, as the reference
+caches the BVH its kernel walks) and uploads both with
+chr_geometry_create_wide, which lays them out for the gfx950 traversal kernel
 (csrc/device_geometry.h).  `gpudata` is the opaque device-geometry handle the
 kernels take.  There is no host-mapped split of the BVH (the reference's
 min_free_gpu_mem path, geometry.py:409-439): 288 GB of HBM holds even the
 ~170 M-triangle 29k-PMT detector many times over.
 """
 import ctypes
+import time
 
 import numpy as np
 
-from chroma.gpu import _native
+from chroma.gpu import _native, wide_bvh
 from chroma.gpu import gpuarray as ga
 from chroma.gpu.packing import PackedGeometry
 from chroma.gpu.tools import format_size
@@ -20,17 +23,28 @@ from chroma.log import logger
 
 class GPUGeometry(object):
     def __init__(self, geometry, wavelengths=None, times=None, print_usage=False, min_free_gpu_mem=300e6):
+        t0 = time.time()
         if getattr(geometry, 'bvh', None) is None:
             from chroma.loader import load_bvh
             geometry.bvh = load_bvh(geometry)
         self.packed = PackedGeometry(geometry, wavelengths=wavelengths, times=times)
+        t1 = time.time()
+        # the traversal BVH: attached to the BVH, from the cache next to it, or
+        # built on the host (chroma.gpu.wide_bvh); uploaded without a rebuild
+        wide, source = wide_bvh.obtain(geometry.bvh, self.packed)
+        t2 = time.time()
         handle = ctypes.c_void_p()
-        _native.call('chr_geometry_create', ctypes.byref(self.packed.desc()), ctypes.byref(handle))
+        _native.call('chr_geometry_create_wide', ctypes.byref(self.packed.desc()), ctypes.byref(wide.desc()),
+                     ctypes.byref(handle))
         self._handle = handle
         self.geometry = geometry
         self.solid_id_map = ga.to_gpu(np.asarray(geometry.solid_id, dtype=np.uint32))
         self.world_origin = self.packed.world_origin
         self.world_scale = self.packed.world_scale
+        # setup phases (bench.py detail.ranks[r].setup): packing the tables / codes,
+        # the traversal BVH (cache load or build), the device upload
+        self.setup_times = {'pack_s': round(t1 - t0, 3), 'wide_bvh_s': round(t2 - t1, 3), 'wide_bvh_source': source,
+                            'h2d_s': round(time.time() - t2, 3)}
         if print_usage:
             self.print_device_usage()
         logger.info(self.device_usage_str())

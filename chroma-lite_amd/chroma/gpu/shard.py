@@ -16,7 +16,9 @@ path has a reduction step:
     reduced with the same three operators: unsigned MIN, SUM (mod 2^32, as the
     u32 atomics wrap) and OR (RCCL has no bitwise reduction: the per-rank words
     are all-gathered -- 8 x 116 KB for 29k channels -- and OR-ed on device);
-  * per-channel hit counts (chr_channel_hit_counts) are SUM-reduced.
+  * per-channel hit counts (chr_channel_hit_counts) are SUM-reduced;
+  * the end photons (keep_photons_end) are gathered like the hits, in global
+    photon order (pack_photons).
 
 RNG streams: rank r of a world of W initialises its S slot states as
 curand_init(seed, r*S + slot) (get_rng_states(first_subsequence=r*S)), so no
@@ -195,6 +197,36 @@ def pack_hits(fields, channels):
                       f32(fields['wavelengths'], 1), f32(fields['t'], 1), f32(fields['weights'], 1),
                       i32(fields['last_hit_triangles']), i32(fields['flags']), i32(fields['evidx']),
                       i32(channels)], dim=1)
+
+
+# one gathered photon (keep_photons_end): the hit record without the channel -> 15 words
+PHOTON_WORDS = 15
+
+
+def pack_photons(gp):
+    """(n, 15) int32 tensor of every photon of a GPUPhotons (or any object with
+    the nine photon GPUArrays), in photon order: the end photons a sharded run
+    gathers for keep_photons_end (reference sim.py:72-75 downloads them whole)."""
+    k = gp.wavelengths.tensor.numel()
+    if k == 0:
+        return torch.zeros((0, PHOTON_WORDS), dtype=torch.int32, device=gp.wavelengths.tensor.device)
+
+    def f32(a, w):
+        return a.tensor.view(torch.int32).reshape(k, w)
+
+    def i32(a):
+        return a.tensor.view(torch.int32).reshape(k, 1)
+    return torch.cat([f32(gp.pos, 3), f32(gp.dir, 3), f32(gp.pol, 3), f32(gp.wavelengths, 1), f32(gp.t, 1),
+                      f32(gp.weights, 1), i32(gp.last_hit_triangles), i32(gp.flags), i32(gp.evidx)], dim=1)
+
+
+def unpack_photons(rows):
+    """event.Photons from gathered (K, 15) photon records."""
+    a = rows.cpu().numpy()
+    f = a.view(np.float32)
+    return event.Photons(f[:, 0:3].copy(), f[:, 3:6].copy(), f[:, 6:9].copy(), f[:, 9].copy(), f[:, 10].copy(),
+                         a[:, 12].copy(), a[:, 13].view(np.uint32).copy(), f[:, 11].copy(),
+                         a[:, 14].view(np.uint32).copy())
 
 
 def unpack_hits(rows):

@@ -107,6 +107,10 @@ class Simulation(object):
     def _batch_hits(self, b):
         return b.gpu_photons.get_flat_hits(self.gpu_geometry)
 
+    def _photons_end(self, b):
+        """The batch's photons after propagation, batch order (sim.py:72-75)."""
+        return b.gpu_photons.get()
+
     def _acquire(self, b, start, end):
         """DAQ of one event (sim.py:143-152)."""
         self.gpu_daq.begin_acquire()
@@ -118,7 +122,7 @@ class Simulation(object):
               run_daq=False):
         """Split a propagated batch back into its events (sim.py:72-110)."""
         if keep_photons_end:
-            photons_end = b.gpu_photons.get()
+            photons_end = self._photons_end(b)
         has_channels = hasattr(self.detector, 'num_channels')
         batch_hits = None
         if has_channels and (keep_hits or keep_flat_hits):
@@ -139,7 +143,7 @@ class Simulation(object):
                 ev.photon_tracks = [event.Photons.join(t, concatenate=False) if t else event.Photons()
                                     for t in tracks]
             if keep_photons_end:
-                ev.photons_end = photons_end[start:end]
+                ev.photons_end = photons_end[start:end] if photons_end is not None else None
             if batch_hits is not None:
                 ev_hits = batch_hits[batch_hits.evidx == i]
                 if keep_hits:
@@ -266,8 +270,10 @@ class ShardedSimulation(Simulation):
     events carry hits/flat_hits None) or to every rank (hits='all') -- and the
     per-event DAQ channels are reduced on every rank (chroma.gpu.shard).  The
     events equal a single-GPU run's except for the RNG streams of ranks > 0
-    (rank r draws from curand subsequences r*S .. r*S+S-1).
-    photon_tracking and keep_photons_end are not sharded (use Simulation)."""
+    (rank r draws from curand subsequences r*S .. r*S+S-1).  keep_photons_end
+    gathers the end photons the same way as the hits (to rank 0, or to every
+    rank with hits='all'; None elsewhere).  photon_tracking is not sharded (use
+    Simulation)."""
 
     def __init__(self, detector, seed=None, group=None, nthreads_per_block=512, max_blocks=1024, hits='root'):
         import torch
@@ -314,6 +320,17 @@ class ShardedSimulation(Simulation):
         rows = shard.gather_rows(rows, 0, self.group)
         return shard.unpack_hits(rows) if rows is not None else None
 
+    def _photons_end(self, b):
+        """Every rank's shard of the batch's end photons, concatenated in rank
+        (= global photon) order on rank 0 (hits='root'; None on the others) or on
+        every rank (hits='all')."""
+        from chroma.gpu import shard
+        rows = shard.pack_photons(b.gpu_photons)
+        if self.hits_to == 'all':
+            return shard.unpack_photons(shard.allgather_rows(rows, self.group))
+        rows = shard.gather_rows(rows, 0, self.group)
+        return shard.unpack_photons(rows) if rows is not None else None
+
     def _acquire(self, b, start, end):
         from chroma.gpu import shard
         daq = self.gpu_daq
@@ -328,10 +345,3 @@ class ShardedSimulation(Simulation):
         daq.channel_q_int_gpu.tensor.copy_(q)
         daq.channel_history_gpu.tensor.copy_(h)
         return daq.end_acquire().get()
-
-    def simulate(self, iterable, keep_photons_end=False, **kw):
-        """Simulation.simulate on this rank's shards.  keep_photons_end is refused
-        here, before any batch is read or uploaded (the photons are not gathered)."""
-        if keep_photons_end:
-            raise NotImplementedError('ShardedSimulation: keep_photons_end is not gathered; use Simulation')
-        return Simulation.simulate(self, iterable, **kw)

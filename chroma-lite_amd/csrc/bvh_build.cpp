@@ -110,7 +110,7 @@ extern "C" int chr_bvh_build_grid(const float *h_vertices, uint32_t nvertices, c
         const size_t n = ntriangles;
         std::vector<U4> leaves(n);
         std::vector<uint64_t> morton(n);
-#pragma omp parallel for schedule(static)
+#pragma omp parallel for num_threads(chr::host_threads()) schedule(static)
         for (int64_t t = 0; t < (int64_t)n; ++t) {
             const uint32_t *tri = h_triangles + 3 * t;
             const float *p0 = h_vertices + 3 * (size_t)tri[0];
@@ -180,7 +180,7 @@ extern "C" int chr_bvh_build_grid(const float *h_vertices, uint32_t nvertices, c
             for (size_t p = 0; p < np; ++p)
                 nchild[p] = (uint32_t)((p + 1 < np ? first_child[p + 1] : nnodes) - first_child[p]);
             std::vector<U4> parents(np);
-#pragma omp parallel for schedule(static)
+#pragma omp parallel for num_threads(chr::host_threads()) schedule(static)
             for (int64_t p = 0; p < (int64_t)np; ++p) {
                 U4 b = box_union(&top[first_child[p]], nchild[p]);
                 b.w = (nchild[p] << CHILD_BITS) | first_child[p];
@@ -199,7 +199,7 @@ extern "C" int chr_bvh_build_grid(const float *h_vertices, uint32_t nvertices, c
             const std::vector<U4> &src = layers[nlayers - 1 - l];
             const uint32_t off = (l + 1 == nlayers) ? 0u : (uint32_t)bounds[l + 1];
             U4 *dst = res->nodes.data() + bounds[l];
-#pragma omp parallel for schedule(static)
+#pragma omp parallel for num_threads(chr::host_threads()) schedule(static)
             for (int64_t i = 0; i < (int64_t)src.size(); ++i) {
                 U4 v = src[i];
                 const uint32_t nc = v.w >> CHILD_BITS, child = v.w & ~(0xFFFFu << CHILD_BITS);
@@ -212,7 +212,7 @@ extern "C" int chr_bvh_build_grid(const float *h_vertices, uint32_t nvertices, c
         // collapse single-child chains, deepest internal layer first (gpu/bvh.py:114-130)
         for (size_t l = nlayers - 1; l-- > 0;) {
             U4 *nodes = res->nodes.data();
-#pragma omp parallel for schedule(static)
+#pragma omp parallel for num_threads(chr::host_threads()) schedule(static)
             for (int64_t i = (int64_t)bounds[l]; i < (int64_t)bounds[l + 1]; ++i) {
                 const U4 v = nodes[i];
                 if ((v.w >> CHILD_BITS) == 1) nodes[i] = nodes[v.w & ~(0xFFFFu << CHILD_BITS)];

@@ -12,6 +12,9 @@ namespace chr {
 // thread-local last-error message (chr_last_error)
 std::string &last_error();
 
+// threads of the library's host OpenMP regions (host.cpp, chr_set_host_threads)
+int host_threads();
+
 inline int fail(int code, const char *fmt, ...) {
     char buf[1024];
     va_list ap;

@@ -65,7 +65,7 @@ struct DevGeom {
     const uint32_t *wrank_rec;       // reference DFS rank -> triangle record (wtri index)
     uint32_t nwcut;
     uint32_t nwnodes, nwtri;
-    uint32_t wstride;                // uint4 per node slot: 8 (96-byte node padded to one 128-byte line) or 6
+    uint32_t wstride;                // uint4 per node slot: 8 (each 96-byte node padded to one 128-byte line)
     float ox, oy, oz, scale;         // world_origin, world_scale
     uint32_t nnodes, ntriangles, nwireplanes;
     uint32_t wl_n;
@@ -94,8 +94,6 @@ struct chr_geometry {
     uint64_t bytes;
     void *allocs[16];
     int nallocs;
-    const uint4 *wnodes_alt;   // the other node layout (only with CHR_NODE_LAYOUT_AB set at creation; A/B tooling)
-    uint32_t wstride_alt;
     // The reference BVH nodes (16 B each) are walked only by the exact-order
     // variant, the no-wide-BVH fallback and distance_to_mesh's exact form.  With a
     // wide BVH only the root stays in HBM (the renderer's world box) and the

@@ -113,7 +113,109 @@ extern "C" int chr_geometry_device_bytes(const chr_geometry *g, uint64_t *bytes)
     return CHR_OK;
 }
 
-extern "C" int chr_geometry_create(const chr_geometry_desc *d, chr_geometry **out) {
+// Host staging for the large uploads: records / node slots are filled chunk by
+// chunk into two pinned buffers while the previous chunk's copy runs, so the
+// 64-byte records (10.9 GB on the 29k detector) never exist whole in host memory.
+// Without pinned memory the chunks go through one pageable buffer, synchronously.
+struct Stager {
+    static constexpr size_t CHUNK = 64u << 20;
+    hipStream_t stream = nullptr;
+    void *buf[2] = {nullptr, nullptr};
+    hipEvent_t ev[2] = {nullptr, nullptr};
+    bool used[2] = {false, false};
+    std::vector<uint8_t> pageable;
+    int init() {
+        if (hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess) stream = nullptr;
+        for (int k = 0; k < 2 && stream; ++k) {
+            if (hipHostMalloc(&buf[k], CHUNK, hipHostMallocDefault) != hipSuccess ||
+                hipEventCreateWithFlags(&ev[k], hipEventDisableTiming) != hipSuccess) {
+                release();
+                break;
+            }
+        }
+        if (!buf[0]) pageable.resize(CHUNK);
+        return CHR_OK;
+    }
+    void release() {
+        if (stream) (void)hipStreamSynchronize(stream);
+        for (int k = 0; k < 2; ++k) {
+            if (buf[k]) (void)hipHostFree(buf[k]);
+            if (ev[k]) (void)hipEventDestroy(ev[k]);
+            buf[k] = nullptr;
+            ev[k] = nullptr;
+        }
+        if (stream) (void)hipStreamDestroy(stream);
+        stream = nullptr;
+    }
+    ~Stager() { release(); }
+    // buffer k (0/1) once its previous copy has finished
+    int acquire(int k, uint8_t **p) {
+        if (!buf[0]) { *p = pageable.data(); return CHR_OK; }
+        if (used[k]) CHR_HIP_CHECK(hipEventSynchronize(ev[k]));
+        *p = static_cast<uint8_t *>(buf[k]);
+        return CHR_OK;
+    }
+    int copy(int k, void *dst, size_t bytes) {
+        if (!buf[0]) {
+            CHR_HIP_CHECK(hipMemcpy(dst, pageable.data(), bytes, hipMemcpyHostToDevice));
+            return CHR_OK;
+        }
+        CHR_HIP_CHECK(hipMemcpyAsync(dst, buf[k], bytes, hipMemcpyHostToDevice, stream));
+        CHR_HIP_CHECK(hipEventRecord(ev[k], stream));
+        used[k] = true;
+        return CHR_OK;
+    }
+    int finish() {
+        if (stream) CHR_HIP_CHECK(hipStreamSynchronize(stream));
+        return CHR_OK;
+    }
+};
+
+// the traversal BVH (compact form w) into HBM: 96-byte nodes in 128-byte slots
+// (one line per node: r01 no gain over the packed stride; r03 ab21, where the
+// later steps' walks are line-bound, 463.7 -> 467.1 M/s), the 64-byte triangle
+// records rebuilt from the geometry, the sub-walk cut and the rank -> record map
+static int upload_wide(chr_geometry *g, const chr_geometry_desc *d, const chr_wide_bvh_desc *w) {
+    chr::WideCheck c;
+    CHR_TRY(chr::wide_validate(d, w, c));
+    chr::DevGeom &dg = g->dev;
+    Stager st;
+    CHR_TRY(st.init());
+    void *p = nullptr;
+    int k = 0;
+    CHR_TRY(dev_upload(g, nullptr, std::max<size_t>(128, (size_t)w->nnodes * 128), &p));
+    dg.wnodes = (const uint4 *)p;
+    dg.wstride = 8;
+    for (size_t i = 0, per = Stager::CHUNK / 128; i < w->nnodes; i += per, k ^= 1) {
+        const size_t n = std::min<size_t>(per, w->nnodes - i);
+        uint8_t *h;
+        CHR_TRY(st.acquire(k, &h));
+        chr::wide_fill_node_slots(w, i, n, h);
+        CHR_TRY(st.copy(k, static_cast<uint8_t *>(p) + 128 * i, n * 128));
+    }
+    CHR_TRY(dev_upload(g, nullptr, std::max<size_t>(1, w->nrec) * sizeof(chr::WideTri), &p));
+    dg.wtri = (const float4 *)p;
+    for (size_t i = 0, per = Stager::CHUNK / sizeof(chr::WideTri); i < w->nrec; i += per, k ^= 1) {
+        const size_t n = std::min<size_t>(per, w->nrec - i);
+        uint8_t *h;
+        CHR_TRY(st.acquire(k, &h));
+        chr::wide_fill_records(d, w, c, i, n, reinterpret_cast<chr::WideTri *>(h));
+        CHR_TRY(st.copy(k, static_cast<uint8_t *>(p) + sizeof(chr::WideTri) * i, n * sizeof(chr::WideTri)));
+    }
+    CHR_TRY(st.finish());
+    dg.nwnodes = w->nnodes;
+    dg.nwtri = w->nrec;
+    CHR_TRY(dev_upload(g, w->h_cut, (size_t)w->ncut * 8, &p));
+    dg.wcut = (const uint2 *)p;
+    dg.nwcut = w->ncut;
+    CHR_TRY(dev_upload(g, c.rank_rec.data(), c.rank_rec.size() * 4, &p));
+    dg.wrank_rec = (const uint32_t *)p;
+    return CHR_OK;
+}
+
+// create with the traversal BVH given in compact form (w, validated first), or
+// built here (w == NULL)
+static int geometry_create(const chr_geometry_desc *d, const chr_wide_bvh_desc *w, chr_geometry **out) {
     if (!d || !out) return chr::fail(CHR_ERR_INVALID, "chr_geometry_create: null argument");
     if (d->ntriangles == 0 || d->nnodes == 0 || !d->h_vertices || !d->h_triangles || !d->h_nodes ||
         !d->h_material_codes)
@@ -121,25 +223,32 @@ extern "C" int chr_geometry_create(const chr_geometry_desc *d, chr_geometry **ou
     if (d->nmaterials == 0 || !d->materials) return chr::fail(CHR_ERR_INVALID, "chr_geometry_create: no materials");
     if (d->nwireplanes && !d->wireplanes) return chr::fail(CHR_ERR_INVALID, "chr_geometry_create: wireplanes NULL");
     if (d->wavelength_n < 2 || d->time_n < 2) return chr::fail(CHR_ERR_INVALID, "chr_geometry_create: grids need >= 2 points");
-    // validate triangle indices / BVH child ranges up front: an out-of-range
-    // index would otherwise become an out-of-bounds read inside the kernel.
-    for (size_t i = 0; i < (size_t)d->ntriangles * 3; ++i)
-        if (d->h_triangles[i] >= d->nvertices)
-            return chr::fail(CHR_ERR_INVALID, "triangle %zu references vertex %u >= %u", i / 3, d->h_triangles[i], d->nvertices);
-    for (size_t i = 0; i < d->nnodes; ++i) {
+    // validate triangle indices / BVH child ranges / material codes up front: an
+    // out-of-range index would otherwise become an out-of-bounds read inside the kernel
+    int64_t bad_tri = -1, bad_node = -1, bad_code = -1;
+    const int64_t NT = d->ntriangles, NN = d->nnodes;
+#pragma omp parallel for num_threads(chr::host_threads()) schedule(static) reduction(max : bad_tri, bad_code)
+    for (int64_t t = 0; t < NT; ++t) {
+        const uint32_t *ix = d->h_triangles + 3 * t;
+        if (ix[0] >= d->nvertices || ix[1] >= d->nvertices || ix[2] >= d->nvertices) bad_tri = std::max(bad_tri, t);
+        const uint32_t c = d->h_material_codes[t];
+        const uint32_t m1 = (c >> 24) & 0xFF, m2 = (c >> 16) & 0xFF, sf = (c >> 8) & 0xFF;
+        if (m1 >= d->nmaterials || m2 >= d->nmaterials ||
+            (sf != 0xFF && (sf >= d->nsurfaces || !d->surfaces || !d->surfaces[sf].present)))
+            bad_code = std::max(bad_code, t);
+    }
+#pragma omp parallel for num_threads(chr::host_threads()) schedule(static) reduction(max : bad_node)
+    for (int64_t i = 0; i < NN; ++i) {
         const uint32_t w = d->h_nodes[4 * i + 3];
         const uint32_t nc = w >> 28, child = w & 0x0FFFFFFFu;
-        if (nc == 0 ? child >= d->ntriangles : (uint64_t)child + nc > d->nnodes)
-            return chr::fail(CHR_ERR_INVALID, "BVH node %zu has child %u nchild %u out of range", i, child, nc);
+        if (nc == 0 ? child >= d->ntriangles : (uint64_t)child + nc > d->nnodes) bad_node = std::max(bad_node, i);
     }
-    for (size_t t = 0; t < d->ntriangles; ++t) {
-        const uint32_t c = d->h_material_codes[t];
-        int m1 = (c >> 24) & 0xFF, m2 = (c >> 16) & 0xFF, s = (c >> 8) & 0xFF;
-        if (m1 >= (int)d->nmaterials || m2 >= (int)d->nmaterials)
-            return chr::fail(CHR_ERR_INVALID, "triangle %zu: material index out of range", t);
-        if (s != 0xFF && (s >= (int)d->nsurfaces || !d->surfaces || !d->surfaces[s].present))
-            return chr::fail(CHR_ERR_INVALID, "triangle %zu: surface %d missing", t, s);
-    }
+    if (bad_tri >= 0)
+        return chr::fail(CHR_ERR_INVALID, "triangle %lld references a vertex >= %u", (long long)bad_tri, d->nvertices);
+    if (bad_node >= 0)
+        return chr::fail(CHR_ERR_INVALID, "BVH node %lld has a child out of range", (long long)bad_node);
+    if (bad_code >= 0)
+        return chr::fail(CHR_ERR_INVALID, "triangle %lld: material index out of range or surface missing", (long long)bad_code);
 
     chr_geometry *g = new (std::nothrow) chr_geometry();
     if (!g) return chr::fail(CHR_ERR_NOMEM, "chr_geometry_create: host allocation failed");
@@ -156,37 +265,33 @@ extern "C" int chr_geometry_create(const chr_geometry_desc *d, chr_geometry **ou
 
         void *p;
         {
+            // the traversal BVH in compact form: given (a cache), or built now and
+            // compacted, so both paths upload through the same record fill
             chr::WideBVH wb;
-            if ((rc = chr::build_wide_bvh(d, wb))) throw rc;
-            if (wb.usable && !std::getenv("CHR_EXACT_ORDER_ONLY")) {
-                // nodes padded to 128 bytes: one node = one cache line (a 96-byte node at a
-                // 96-byte stride straddles two lines half the time).  r01: no gain over the
-                // packed stride; r03 ab21, where the later steps' walks are line-bound:
-                // 463.7 -> 467.1 M/s, so the padded slots are the default (the packed ones
-                // kept beside them with CHR_NODE_LAYOUT_AB, selected by CHR_NODE_LAYOUT=96)
-                const bool ab = std::getenv("CHR_NODE_LAYOUT_AB") != nullptr;
-                std::vector<uint8_t> padded(wb.nodes.size() * 128, 0);
-                for (size_t i = 0; i < wb.nodes.size(); ++i)
-                    std::memcpy(padded.data() + 128 * i, &wb.nodes[i], sizeof(chr::WideNode));
-                if ((rc = dev_upload(g, padded.data(), std::max<size_t>(128, padded.size()), &p))) throw rc;
-                dg.wnodes = (const uint4 *)p;
-                dg.wstride = 8;
-                std::vector<uint8_t>().swap(padded);
-                if (ab) {
-                    if ((rc = dev_upload(g, wb.nodes.data(), wb.nodes.size() * sizeof(chr::WideNode), &p))) throw rc;
-                    g->wnodes_alt = (const uint4 *)p;
-                    g->wstride_alt = 6;
-                }
-                if ((rc = dev_upload(g, wb.tri.data(), std::max<size_t>(1, wb.tri.size()) * sizeof(chr::WideTri), &p)))
-                    throw rc;
-                dg.wtri = (const float4 *)p;
-                dg.nwnodes = (uint32_t)wb.nodes.size();
-                dg.nwtri = (uint32_t)wb.tri.size();
-                if ((rc = dev_upload(g, wb.cut.data(), wb.cut.size() * 4, &p))) throw rc;
-                dg.wcut = (const uint2 *)p;
-                dg.nwcut = (uint32_t)(wb.cut.size() / 2);
-                if ((rc = dev_upload(g, wb.rank_rec.data(), wb.rank_rec.size() * 4, &p))) throw rc;
-                dg.wrank_rec = (const uint32_t *)p;
+            std::vector<uint32_t> rec_id, rec_rank;
+            chr_wide_bvh_desc built;
+            std::memset(&built, 0, sizeof(built));
+            const bool exact_only = std::getenv("CHR_EXACT_ORDER_ONLY") != nullptr;
+            if (w && (!w->usable || exact_only)) {
+                w = nullptr;       // a tree the wide walk cannot use: the exact-order walk, nothing built
+            } else if (!w) {
+                if ((rc = chr::build_wide_bvh(d, wb))) throw rc;
+                chr::wide_compact(wb, rec_id, rec_rank);
+                std::vector<chr::WideTri>().swap(wb.tri);
+                built.nnodes = (uint32_t)wb.nodes.size();
+                built.nrec = (uint32_t)rec_id.size();
+                built.ncut = (uint32_t)(wb.cut.size() / 2);
+                built.max_depth = wb.max_depth;
+                built.usable = wb.usable ? 1 : 0;
+                built.leaf_max = wb.leaf_max;
+                built.h_nodes = wb.nodes.data();
+                built.h_rec_id = rec_id.data();
+                built.h_rec_rank = rec_rank.data();
+                built.h_cut = wb.cut.data();
+                if (built.usable && !exact_only) w = &built;
+            }
+            if (w) {
+                if ((rc = upload_wide(g, d, w))) throw rc;
             }
         }
 
@@ -197,7 +302,7 @@ extern "C" int chr_geometry_create(const chr_geometry_desc *d, chr_geometry **ou
         if (dg.nwnodes == 0 || std::getenv("CHR_REF_NODES_RESIDENT")) {
             std::vector<float> tri((size_t)d->ntriangles * 12);
             const float *v = d->h_vertices;
-#pragma omp parallel for schedule(static)
+#pragma omp parallel for num_threads(chr::host_threads()) schedule(static)
             for (int64_t t = 0; t < (int64_t)d->ntriangles; ++t) {
                 const uint32_t *ix = d->h_triangles + 3 * t;
                 const float *a = v + 3 * (size_t)ix[0], *b = v + 3 * (size_t)ix[1], *c = v + 3 * (size_t)ix[2];
@@ -341,4 +446,13 @@ extern "C" int chr_geometry_create(const chr_geometry_desc *d, chr_geometry **ou
     }
     *out = g;
     return CHR_OK;
+}
+
+extern "C" int chr_geometry_create(const chr_geometry_desc *d, chr_geometry **out) {
+    return geometry_create(d, nullptr, out);
+}
+
+extern "C" int chr_geometry_create_wide(const chr_geometry_desc *d, const chr_wide_bvh_desc *w, chr_geometry **out) {
+    if (!w) return chr::fail(CHR_ERR_INVALID, "chr_geometry_create_wide: null traversal BVH");
+    return geometry_create(d, w, out);
 }

@@ -4807,21 +4807,6 @@ static int timing_events(size_t n, std::vector<hipEvent_t> **out, int ctx = 0) {
     return CHR_OK;
 }
 
-// A/B of the node layouts (CHR_NODE_LAYOUT=96|128, read per launch; only when
-// the geometry was created with CHR_NODE_LAYOUT_AB set): swap the live layout
-static int apply_node_layout(const chr_geometry *cg, hipStream_t stream) {
-    chr_geometry *g = const_cast<chr_geometry *>(cg);
-    if (!g->wnodes_alt) return CHR_OK;
-    const char *e = getenv("CHR_NODE_LAYOUT");
-    const uint32_t want = (e && atoi(e) == 96) ? 6u : 8u;
-    if (g->dev.wstride == want) return CHR_OK;
-    std::swap(g->dev.wnodes, g->wnodes_alt);
-    std::swap(g->dev.wstride, g->wstride_alt);
-    CHR_HIP_CHECK(hipMemcpyAsync(g->d_dev, &g->dev, sizeof(g->dev), hipMemcpyHostToDevice, stream));
-    CHR_HIP_CHECK(hipStreamSynchronize(stream));
-    return CHR_OK;
-}
-
 static bool trace_steps() {   // CHR_TRACE_STEPS=1: one stderr line per host step (debugging)
     const char *e = getenv("CHR_TRACE_STEPS");
     return e && e[0] == '1';
@@ -5166,7 +5151,6 @@ extern "C" int chr_propagate(const chr_geometry *g, const chr_photons *ph, uint3
     }
     if (walks_reference_bvh(g)) CHR_TRY(chr::geometry_ref_nodes(g));
     hipStream_t stream = (hipStream_t)vstream;
-    if (int lrc = apply_node_layout(g, stream)) return lrc;
     PropBufs b;
     int rc = prop_bufs(nphotons, ntpb, max_blocks, 0, false, b);
     if (rc) return rc;
@@ -5453,7 +5437,6 @@ static int propagate_batches(const chr_geometry *g, const chr_photons *phs, cons
         if (nphotons[i]) { idx.push_back(i); max_n = std::max(max_n, nphotons[i]); }
     if (idx.empty()) return CHR_OK;
     if (walks_reference_bvh(g)) CHR_TRY(chr::geometry_ref_nodes(g));
-    if (int lrc = apply_node_layout(g, stream)) return lrc;
     PropBufs probe;
     probe.cap = (uint64_t)ntpb * max_blocks;
     probe.fused = (probe.cap % 64 == 0) && probe.cap <= 0x7FFFFFFFull && step_launch_enabled() && !sort_enabled();

@@ -40,7 +40,7 @@ extern "C" int chr_unique_vertices(const float *v, uint64_t n, float *out, uint6
     const uint32_t *u = reinterpret_cast<const uint32_t *>(v);
     std::vector<Row> rows(n);
     int bad = 0;
-#pragma omp parallel for reduction(| : bad) schedule(static)
+#pragma omp parallel for num_threads(chr::host_threads()) reduction(| : bad) schedule(static)
     for (int64_t i = 0; i < (int64_t)n; ++i) {
         uint32_t k[3];
         for (int c = 0; c < 3; ++c) {
@@ -51,12 +51,12 @@ extern "C" int chr_unique_vertices(const float *v, uint64_t n, float *out, uint6
         rows[i] = Row{((uint64_t)k[0] << 32) | k[1], k[2], (uint32_t)i};
     }
     if (bad) return chr::fail(CHR_ERR_INVALID, "chr_unique_vertices: NaN present");
-    __gnu_parallel::sort(rows.begin(), rows.end());
+    __gnu_parallel::sort(rows.begin(), rows.end(), __gnu_parallel::default_parallel_tag(chr::host_threads()));
     // group starts -> unique row numbers (prefix count, in parallel blocks)
     const int64_t N = (int64_t)n;
     std::vector<uint8_t> start(n);
     int mixed = 0;
-#pragma omp parallel for reduction(| : mixed) schedule(static)
+#pragma omp parallel for num_threads(chr::host_threads()) reduction(| : mixed) schedule(static)
     for (int64_t j = 0; j < N; ++j) {
         start[j] = (j == 0 || !rows[j].same(rows[j - 1])) ? 1 : 0;
         // an equal run holding both zeros of a coordinate: which row numpy keeps
@@ -70,7 +70,7 @@ extern "C" int chr_unique_vertices(const float *v, uint64_t n, float *out, uint6
         g += start[j];
         gid[j] = g;
     }
-#pragma omp parallel for schedule(static)
+#pragma omp parallel for num_threads(chr::host_threads()) schedule(static)
     for (int64_t j = 0; j < N; ++j) {
         const uint32_t i = rows[j].idx;
         inverse[i] = gid[j];

@@ -26,6 +26,7 @@
 #include <atomic>
 #include <cmath>
 #include <cstdint>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <new>
@@ -56,6 +57,9 @@ inline uint32_t sweep_max_env() {
     const char *e = std::getenv("CHR_WIDE_SWEEP");
     return e ? (uint32_t)std::max(0, std::atoi(e)) : 0u;
 }
+
+// CHR_WIDE_NO_FILL: do not split multi-triangle leaves into free child slots (build-time A/B)
+inline bool fill_env() { return !std::getenv("CHR_WIDE_NO_FILL"); }
 
 struct Box {
     float lo[3], hi[3];
@@ -94,7 +98,7 @@ struct Builder {
             for (uint32_t i = b; i < e; ++i) r.grow(tri_box[idx[i]]);
             return r;
         }
-#pragma omp parallel
+#pragma omp parallel num_threads(chr::host_threads())
         {
             Box l;
             l.empty();
@@ -159,7 +163,7 @@ struct Builder {
                 return std::min(NBINS - 1, std::max(0, j));
             };
             if (par) {
-#pragma omp parallel
+#pragma omp parallel num_threads(chr::host_threads())
                 {
                     Box lb[NBINS];
                     uint32_t lc[NBINS];
@@ -333,11 +337,12 @@ int build_wide_bvh(const chr_geometry_desc *d, WideBVH &out) {
         if (rank[t] != 0xFFFFFFFFu) idx.push_back(t);
     const uint32_t nreach = (uint32_t)idx.size();
     std::vector<float> centroid((size_t)ntri * 3);
-#pragma omp parallel for schedule(static)
+#pragma omp parallel for num_threads(chr::host_threads()) schedule(static)
     for (int64_t t = 0; t < (int64_t)ntri; ++t)
         for (int a = 0; a < 3; ++a) centroid[3 * t + a] = 0.5f * (tri_box[t].lo[a] + tri_box[t].hi[a]);
 
-    Builder B{!std::getenv("CHR_WIDE_NO_FILL"), leaf_max_env(), sweep_max_env(), tri_box, centroid, idx};
+    Builder B{fill_env(), leaf_max_env(), sweep_max_env(), tri_box, centroid, idx};
+    out.leaf_max = B.leaf_max;
     out.nodes.clear();
     out.tri.clear();
     out.nodes.resize(1);
@@ -356,7 +361,7 @@ int build_wide_bvh(const chr_geometry_desc *d, WideBVH &out) {
         if (nt < 16) {
             for (size_t i = 0; i < nt; ++i) ncl[i] = B.clusters(level[i].begin, level[i].end, true, &cl[8 * i]);
         } else {
-#pragma omp parallel for schedule(dynamic, 1)
+#pragma omp parallel for num_threads(chr::host_threads()) schedule(dynamic, 1)
             for (int64_t i = 0; i < (int64_t)nt; ++i) ncl[i] = B.clusters(level[i].begin, level[i].end, false, &cl[8 * i]);
         }
         // deterministic allocation of child nodes / triangle slots
@@ -378,7 +383,7 @@ int build_wide_bvh(const chr_geometry_desc *d, WideBVH &out) {
             out.nodes.resize(out.nodes.size() + ninner);
         }
         int bad = 0;
-#pragma omp parallel for schedule(static) reduction(+:bad)
+#pragma omp parallel for num_threads(chr::host_threads()) schedule(static) reduction(+:bad)
         for (int64_t i = 0; i < (int64_t)nt; ++i) {
             WideNode &W = out.nodes[level[i].node];
             std::memset(&W, 0, sizeof(W));
@@ -458,6 +463,120 @@ int build_wide_bvh(const chr_geometry_desc *d, WideBVH &out) {
     return CHR_OK;
 }
 
+void wide_compact(const WideBVH &b, std::vector<uint32_t> &rec_id, std::vector<uint32_t> &rec_rank) {
+    const int64_t n = (int64_t)b.tri.size();
+    rec_id.resize(n);
+    rec_rank.resize(n);
+#pragma omp parallel for num_threads(chr::host_threads()) schedule(static)
+    for (int64_t i = 0; i < n; ++i) {
+        rec_id[i] = b.tri[i].id;
+        rec_rank[i] = b.tri[i].rank;
+    }
+}
+
+int wide_validate(const chr_geometry_desc *d, const chr_wide_bvh_desc *w, WideCheck &out) {
+    if (!w->h_nodes || w->nnodes == 0 || (w->nrec && (!w->h_rec_id || !w->h_rec_rank)) || (w->ncut && !w->h_cut))
+        return chr::fail(CHR_ERR_INVALID, "wide BVH: missing arrays");
+    if (!w->usable) return chr::fail(CHR_ERR_INVALID, "wide BVH: marked unusable (use chr_geometry_create)");
+    if (w->nrec > d->ntriangles) return chr::fail(CHR_ERR_INVALID, "wide BVH: %u records > %u triangles", w->nrec, d->ntriangles);
+    const WideNode *N = static_cast<const WideNode *>(w->h_nodes);
+    const uint32_t nn = w->nnodes, nrec = w->nrec;
+    // nodes: children in range and numbered after their parent (the builder allocates a
+    // level's children after the level), so one forward pass gives every node's depth
+    std::vector<uint16_t> depth(nn, 0);
+    uint32_t maxd = 0;
+    for (uint32_t i = 0; i < nn; ++i) {
+        const WideNode &W = N[i];
+        if (W.nchild > 8) return chr::fail(CHR_ERR_INVALID, "wide BVH: node %u has %u children", i, W.nchild);
+        for (int k = 0; k < 8; ++k) {
+            const uint8_t kind = W.kind[k];
+            if (kind == 0) continue;
+            if (kind == WIDE_INNER) {
+                const uint64_t c = (uint64_t)W.child_base + W.off[k];
+                if (c >= nn || c <= i) return chr::fail(CHR_ERR_INVALID, "wide BVH: node %u child %llu out of range", i, (unsigned long long)c);
+                const uint32_t dc = depth[i] + 1u;
+                if (dc > depth[c]) depth[c] = (uint16_t)std::min<uint32_t>(dc, 0xFFFFu);
+                maxd = std::max(maxd, dc);
+            } else if (kind <= LEAF_MAX) {
+                if ((uint64_t)W.tri_base + W.off[k] + kind > nrec)
+                    return chr::fail(CHR_ERR_INVALID, "wide BVH: node %u leaf records out of range", i);
+            } else {
+                return chr::fail(CHR_ERR_INVALID, "wide BVH: node %u has child kind %u", i, kind);
+            }
+        }
+    }
+    if (7 * (maxd + 1) + 1 > (uint32_t)WIDE_STACK)
+        return chr::fail(CHR_ERR_INVALID, "wide BVH: depth %u exceeds the walk's stack", maxd);
+    for (uint32_t i = 0; i < w->ncut; ++i)
+        if (w->h_cut[2 * i] >= nn) return chr::fail(CHR_ERR_INVALID, "wide BVH: cut item %u out of range", i);
+    // records: triangle ids in range, ranks a permutation of [0, nrec)
+    out.rank_rec.assign(nrec, 0xFFFFFFFFu);
+    int bad = 0;
+    uint32_t *rr = out.rank_rec.data();
+#pragma omp parallel for num_threads(chr::host_threads()) schedule(static) reduction(| : bad)
+    for (int64_t i = 0; i < (int64_t)nrec; ++i) {
+        const uint32_t r = w->h_rec_rank[i];
+        if (r >= nrec || w->h_rec_id[i] >= d->ntriangles) { bad = 1; continue; }
+        __atomic_store_n(rr + r, (uint32_t)i, __ATOMIC_RELAXED);
+    }
+#pragma omp parallel for num_threads(chr::host_threads()) schedule(static) reduction(| : bad)
+    for (int64_t r = 0; r < (int64_t)nrec; ++r)
+        if (rr[r] == 0xFFFFFFFFu) bad = 1;       // a rank missing: some other rank repeats
+    if (bad) return chr::fail(CHR_ERR_INVALID, "wide BVH: record ids out of range or ranks not a permutation");
+    // reference leaf words per triangle (a triangle under several leaves has the same
+    // words under each in a usable tree, wide_bvh.cpp build step 1)
+    const size_t nt = d->ntriangles;
+    out.leafq.assign(3 * nt, 0u);
+    std::vector<uint8_t> has(nt, 0);
+    uint32_t *lq = out.leafq.data();
+    uint8_t *hp = has.data();
+    const uint32_t *RN = d->h_nodes;
+#pragma omp parallel for num_threads(chr::host_threads()) schedule(static)
+    for (int64_t i = 0; i < (int64_t)d->nnodes; ++i) {
+        const uint32_t *n = RN + 4 * (size_t)i;
+        if ((n[3] >> 28) != 0) continue;
+        const uint32_t t = n[3] & 0x0FFFFFFFu;
+        if (t >= nt) continue;
+        for (int a = 0; a < 3; ++a) __atomic_store_n(lq + 3 * (size_t)t + a, n[a], __ATOMIC_RELAXED);
+        __atomic_store_n(hp + t, (uint8_t)1, __ATOMIC_RELAXED);
+    }
+#pragma omp parallel for num_threads(chr::host_threads()) schedule(static) reduction(| : bad)
+    for (int64_t i = 0; i < (int64_t)nrec; ++i)
+        if (!hp[w->h_rec_id[i]]) bad = 1;
+    if (bad) return chr::fail(CHR_ERR_INVALID, "wide BVH: a record's triangle is under no reference leaf");
+    return CHR_OK;
+}
+
+void wide_fill_records(const chr_geometry_desc *d, const chr_wide_bvh_desc *w, const WideCheck &c, size_t first,
+                       size_t n, WideTri *out) {
+#pragma omp parallel for num_threads(chr::host_threads()) schedule(static)
+    for (int64_t j = 0; j < (int64_t)n; ++j) {
+        const size_t i = first + (size_t)j;
+        const uint32_t t = w->h_rec_id[i];
+        const uint32_t *ix = d->h_triangles + 3 * (size_t)t;
+        WideTri &R = out[j];
+        for (int a = 0; a < 3; ++a) {
+            R.v0[a] = d->h_vertices[3 * (size_t)ix[0] + a];
+            R.v1[a] = d->h_vertices[3 * (size_t)ix[1] + a];
+            R.v2[a] = d->h_vertices[3 * (size_t)ix[2] + a];
+        }
+        R.id = t;
+        R.rank = w->h_rec_rank[i];
+        std::memcpy(R.leaf, &c.leafq[3 * (size_t)t], 12);
+        R.code = d->h_material_codes ? d->h_material_codes[t] : 0u;
+        R.pad = 0;
+    }
+}
+
+void wide_fill_node_slots(const chr_wide_bvh_desc *w, size_t first, size_t n, uint8_t *out) {
+    const WideNode *N = static_cast<const WideNode *>(w->h_nodes);
+#pragma omp parallel for num_threads(chr::host_threads()) schedule(static)
+    for (int64_t j = 0; j < (int64_t)n; ++j) {
+        std::memcpy(out + 128 * (size_t)j, N + first + (size_t)j, sizeof(WideNode));
+        std::memset(out + 128 * (size_t)j + sizeof(WideNode), 0, 128 - sizeof(WideNode));
+    }
+}
+
 }  // namespace chr
 
 struct chr_wide_result {
@@ -494,5 +613,56 @@ extern "C" int chr_wide_bvh_copy(const chr_wide_result *r, void *h_nodes, void *
 
 extern "C" int chr_wide_bvh_free(chr_wide_result *r) {
     delete r;
+    return CHR_OK;
+}
+
+extern "C" int chr_wide_bvh_describe(const chr_wide_result *r, chr_wide_bvh_desc *out) {
+    if (!r || !out) return chr::fail(CHR_ERR_INVALID, "chr_wide_bvh_describe: null argument");
+    std::memset(out, 0, sizeof(*out));
+    out->nnodes = (uint32_t)r->b.nodes.size();
+    out->nrec = (uint32_t)r->b.tri.size();
+    out->ncut = (uint32_t)(r->b.cut.size() / 2);
+    out->max_depth = r->b.max_depth;
+    out->usable = r->b.usable ? 1 : 0;
+    out->leaf_max = r->b.leaf_max;
+    return CHR_OK;
+}
+
+extern "C" int chr_wide_bvh_export(const chr_wide_result *r, void *h_nodes, uint32_t *h_rec_id, uint32_t *h_rec_rank,
+                                   uint32_t *h_cut) {
+    if (!r) return chr::fail(CHR_ERR_INVALID, "chr_wide_bvh_export: null handle");
+    if (h_nodes) std::memcpy(h_nodes, r->b.nodes.data(), r->b.nodes.size() * sizeof(chr::WideNode));
+    if (h_rec_id || h_rec_rank) {
+        const int64_t n = (int64_t)r->b.tri.size();
+#pragma omp parallel for num_threads(chr::host_threads()) schedule(static)
+        for (int64_t i = 0; i < n; ++i) {
+            if (h_rec_id) h_rec_id[i] = r->b.tri[i].id;
+            if (h_rec_rank) h_rec_rank[i] = r->b.tri[i].rank;
+        }
+    }
+    if (h_cut) std::memcpy(h_cut, r->b.cut.data(), r->b.cut.size() * 4);
+    return CHR_OK;
+}
+
+extern "C" int chr_wide_bvh_key(char *out, uint32_t n) {
+    if (!out || n == 0) return chr::fail(CHR_ERR_INVALID, "chr_wide_bvh_key: no buffer");
+    // bump the format number whenever the builder's output for the same inputs changes
+    const int len = std::snprintf(out, n, "w%d-l%u-s%u-f%d", chr::WIDE_FORMAT, chr::leaf_max_env(),
+                                  chr::sweep_max_env(), chr::fill_env() ? 1 : 0);
+    if (len < 0 || (uint32_t)len >= n) return chr::fail(CHR_ERR_INVALID, "chr_wide_bvh_key: buffer too small");
+    return CHR_OK;
+}
+
+extern "C" int chr_wide_bvh_records(const chr_geometry_desc *d, const chr_wide_bvh_desc *w, uint32_t first, uint32_t n,
+                                    void *h_tri) {
+    if (!d || !w || (n && !h_tri)) return chr::fail(CHR_ERR_INVALID, "chr_wide_bvh_records: null argument");
+    if ((uint64_t)first + n > w->nrec) return chr::fail(CHR_ERR_INVALID, "chr_wide_bvh_records: range past the records");
+    try {
+        chr::WideCheck c;
+        if (int rc = chr::wide_validate(d, w, c)) return rc;
+        chr::wide_fill_records(d, w, c, first, n, static_cast<chr::WideTri *>(h_tri));
+    } catch (const std::bad_alloc &) {
+        return chr::fail(CHR_ERR_NOMEM, "chr_wide_bvh_records: out of host memory");
+    }
     return CHR_OK;
 }

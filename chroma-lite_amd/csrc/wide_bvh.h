@@ -25,10 +25,15 @@
 #include <vector>
 
 struct chr_geometry_desc;
+struct chr_wide_bvh_desc;
 
 namespace chr {
 
 constexpr uint8_t WIDE_INNER = 0x80;
+
+// version of the builder's output (the traversal-BVH cache key, chr_wide_bvh_key):
+// bump it whenever the same inputs would build a different tree
+constexpr int WIDE_FORMAT = 1;
 
 struct alignas(16) WideNode {
     float origin[3];
@@ -60,6 +65,7 @@ struct WideBVH {
     std::vector<WideNode> nodes;   // node 0 is the root
     std::vector<WideTri> tri;      // leaf order
     uint32_t max_depth = 0;        // levels below the root
+    uint32_t leaf_max = 0;         // builder setting used
     bool usable = true;            // false: the exact-order traversal must be used
     // Decomposition of one walk into independent sub-walks (flat rays, see
     // propagate.hip trace_kernel): (node, child mask) pairs whose subtrees
@@ -83,5 +89,23 @@ constexpr int WIDE_STACK = 128;
 
 // Build from the descriptor's mesh and reference BVH (h_nodes).  Returns a chr_status.
 int build_wide_bvh(const chr_geometry_desc *d, WideBVH &out);
+
+// The compact form (chr_wide_bvh_desc): record ids / ranks split out of a build.
+void wide_compact(const WideBVH &b, std::vector<uint32_t> &rec_id, std::vector<uint32_t> &rec_rank);
+
+// A compact form checked against a geometry, ready to rebuild records from:
+// every node / record / cut index in range, the depth within WIDE_STACK, the
+// ranks a permutation (rank_rec = its inverse), each record's triangle under a
+// reference leaf (leafq: that leaf's x/y/z words per triangle).
+struct WideCheck {
+    std::vector<uint32_t> rank_rec;
+    std::vector<uint32_t> leafq;
+};
+int wide_validate(const chr_geometry_desc *d, const chr_wide_bvh_desc *w, WideCheck &out);
+// the 64-byte triangle records [first, first+n) of a validated compact form
+void wide_fill_records(const chr_geometry_desc *d, const chr_wide_bvh_desc *w, const WideCheck &c, size_t first,
+                       size_t n, WideTri *out);
+// 96-byte nodes [first, first+n) into 128-byte slots (the device layout)
+void wide_fill_node_slots(const chr_wide_bvh_desc *w, size_t first, size_t n, uint8_t *out);
 
 }  // namespace chr

@@ -306,6 +306,53 @@ int chr_wide_bvh_copy(const chr_wide_result *r, void *h_nodes /*[nnodes*96 B]*/,
                       void *h_tri /*[ntri*64 B]*/);
 int chr_wide_bvh_free(chr_wide_result *r);
 
+/* The traversal BVH in its compact, cacheable form.  The reference caches the
+ * BVH its kernel walks, keyed by mesh MD5 (chroma/cache.py:209-236, used by
+ * chroma/loader.py:131-160); here the structure the kernel walks is the wide
+ * BVH, a function of the mesh and the reference BVH only.  Its compact form
+ * keeps what the build decides -- the nodes, each triangle record's triangle
+ * id and reference DFS rank, the sub-walk cut -- and drops what the upload
+ * derives from the geometry descriptor (vertices, reference leaf words,
+ * material codes), so a cached copy cannot go stale against the materials. */
+typedef struct chr_wide_bvh_desc {
+    uint32_t nnodes;                /* 96-byte nodes (wide_bvh.h WideNode) */
+    uint32_t nrec;                  /* triangle records = triangles reachable in the reference BVH */
+    uint32_t ncut;                  /* sub-walk items, 2 words each */
+    uint32_t max_depth;             /* levels below the root */
+    int32_t usable;                 /* 0: the wide walk cannot be used (the exact-order walk is) */
+    uint32_t leaf_max;              /* builder setting it was built with */
+    const void *h_nodes;            /* [nnodes*96 B] */
+    const uint32_t *h_rec_id;       /* [nrec] triangle id of record i */
+    const uint32_t *h_rec_rank;     /* [nrec] its reference DFS rank (a permutation of [0, nrec)) */
+    const uint32_t *h_cut;          /* [ncut*2] (node, child mask) */
+} chr_wide_bvh_desc;
+/* sizes and settings of a built result (pointers left NULL) */
+int chr_wide_bvh_describe(const chr_wide_result *r, chr_wide_bvh_desc *out);
+/* copy the compact form into caller arrays sized by chr_wide_bvh_describe */
+int chr_wide_bvh_export(const chr_wide_result *r, void *h_nodes, uint32_t *h_rec_id, uint32_t *h_rec_rank,
+                        uint32_t *h_cut);
+/* the builder's settings as a short string ("w<format>-l<leaf max>-s<sweep>-f<fill>"):
+ * part of a cache key -- a compact form is reused only under the same settings */
+int chr_wide_bvh_key(char *out, uint32_t n);
+/* check a compact form against a geometry (every index in range, the ranks a
+ * permutation, the depth within the walk's stack) and rebuild its 64-byte
+ * triangle records [first, first+n) on the host (tests; the upload does the same) */
+int chr_wide_bvh_records(const chr_geometry_desc *desc, const chr_wide_bvh_desc *wide, uint32_t first,
+                         uint32_t n, void *h_tri /*[n*64 B]*/);
+/* chr_geometry_create with a prebuilt (e.g. cached) traversal BVH instead of
+ * building it: the same device layout and results, without the build.  The
+ * compact form is validated first (CHR_ERR_INVALID if it does not fit desc);
+ * one marked unusable selects the exact-order walk, as the build would. */
+int chr_geometry_create_wide(const chr_geometry_desc *desc, const chr_wide_bvh_desc *wide,
+                             chr_geometry **out);
+
+/* Threads of the library's host-side parallel regions (BVH builds, record
+ * fill, vertex merge).  Default: the usable cores (affinity mask capped by the
+ * cgroup CPU quota) divided by $LOCAL_WORLD_SIZE; n = 0 restores the default.
+ * No reference counterpart (the reference builds on the GPU). */
+int chr_set_host_threads(int32_t n);
+int32_t chr_get_host_threads(void);
+
 /* ------------------------------------------------------------------- DAQ
  * replaces: chroma/cuda/daq.cu + GPUDaq (chroma/gpu/daq.py:37-101) and the
  * Detector struct (chroma/cuda/detector.h:4-22, uploaded by

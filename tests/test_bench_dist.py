@@ -18,6 +18,12 @@ import torch.multiprocessing as mp
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+def bench_usable_cpus():
+    sys.path.insert(0, ROOT)
+    import bench
+    return bench.usable_cpus()
+
+
 def _free_port():
     with socket.socket() as s:
         s.bind(('127.0.0.1', 0))
@@ -33,7 +39,10 @@ def _worker(rank, world, port, out_dir):
         import bench
         from chroma.gpu import shard
         cache = os.path.join(out_dir, 'cache')
-        det = bench.shared_geometry('small', cache, rank, dist)
+        det, setup = bench.shared_geometry('small', cache, rank, dist)
+        from chroma.gpu import wide_bvh
+        from chroma.gpu.packing import PackedGeometry
+        src = wide_bvh.obtain(det.bvh, PackedGeometry(det))[1]
         md5 = int(det.mesh.md5()[:12], 16)
         nch = det.num_channels()
         counts = torch.zeros(nch, dtype=torch.int32)
@@ -52,7 +61,12 @@ def _worker(rank, world, port, out_dir):
         elapsed, per_step, results = bench.timed_loop(run, 3, 1, dist, lambda: None, group=2)
         c = reduced['c'].numpy()
         res = np.array([elapsed, sum(per_step), md5, nch, bench.rng_first_subsequence(rank, 524288),
-                        c[0], c[1 % nch], c.sum(), len(results)], dtype=np.float64)
+                        c[0], c[1 % nch], c.sum(), len(results),
+                        # rank 0 built the traversal BVH before the barrier (it is then in memory);
+                        # rank 1 loaded it from the cache rank 0 filled
+                        {'built': 1, 'memory': 2, 'cache': 3}[src],
+                        {'built': 1, 'cache': 3}.get(setup.get('wide_bvh_prepare_source'), 0)],
+                       dtype=np.float64)
         np.save(os.path.join(out_dir, 'r%d.npy' % rank), res, allow_pickle=False)
     finally:
         dist.destroy_process_group()
@@ -64,6 +78,8 @@ def test_bench_world2_scaffolding(tmp_path):
     # one geometry, built once by rank 0 into the shared cache, loaded by rank 1
     assert r0[2] == r1[2] and r0[3] == r1[3]
     assert os.path.isdir(os.path.join(str(tmp_path), 'cache'))
+    # the traversal BVH: built once by rank 0 before the barrier, loaded from the cache by rank 1
+    assert r0[10] == 1 and r0[9] == 2 and r1[9] == 3
     # timed region: max over ranks -> identical on both, at least the slow rank's 3 steps
     assert r0[0] == r1[0] and r0[0] >= 3 * 0.04 - 1e-3
     assert r1[1] >= 3 * 0.04 - 1e-3
@@ -76,9 +92,13 @@ def test_bench_world2_scaffolding(tmp_path):
 
 def _stub_bench(args, env_extra=None, timeout=120):
     """Run tests/bench_stub_main.py (bench.py with a CPU stand-in workload) as
-    the driver would run bench.py; returns (returncode, parsed line or None, stderr)."""
+    the driver would run bench.py, with a fresh node-local cache; returns
+    (returncode, parsed line or None, stderr)."""
     import json
     import subprocess
+    import tempfile
+    if '--cache-dir' not in args:
+        args = list(args) + ['--cache-dir', tempfile.mkdtemp(prefix='bench_stub_cache_')]
     env = {k: v for k, v in os.environ.items() if k not in ('WORLD_SIZE', 'RANK', 'LOCAL_RANK', 'MASTER_ADDR',
                                                             'MASTER_PORT')}
     env.update(env_extra or {})
@@ -142,6 +162,14 @@ def test_bench_gpus8_line():
     assert [r['rank'] for r in line['roofline']['per_rank']] == list(range(8))
     for r in d['ranks']:
         assert r['host_rss_gb'] > 0 and 'setup_s' in r['setup']
+    # a fresh cache: rank 0 builds the traversal BVH once before the barrier, ranks 1-7
+    # load it from the node-local cache (no 8 concurrent builds), each with its share
+    # of the job's cores
+    s0 = d['ranks'][0]['setup']
+    assert s0['wide_bvh_prepare_source'] == 'built' and s0['wide_bvh_source'] == 'memory'
+    for r in d['ranks'][1:]:
+        assert r['setup']['wide_bvh_source'] == 'cache' and 'wide_bvh_prepare_source' not in r['setup']
+    assert all(r['setup']['host_threads'] == max(1, bench_usable_cpus() // 8) for r in d['ranks'])
 
 
 def test_bench_total_photons_is_strong_scaling():

@@ -155,21 +155,18 @@ def _pipe_worker(rank, world, port, out_dir, hits):
             sim = ShardedSimulation(_detector(), seed=5, nthreads_per_block=NTPB, max_blocks=MAXB, hits=hits)
             sim.pipeline_batches = depth
             evs = list(sim.simulate([ph[cuts[i]:cuts[i + 1]] for i in range(len(SIZES))], run_daq=False,
-                                    keep_hits=False, photons_per_batch=1))
+                                    keep_hits=False, photons_per_batch=1, keep_photons_end=True))
             out['pipeline_%d' % depth] = np.array(sim.last_pipeline)
             for i, ev in enumerate(evs):
                 if ev.flat_hits is None:
-                    assert rank != 0 and hits == 'root'
+                    assert rank != 0 and hits == 'root' and ev.photons_end is None
                     continue
                 for f in ('flags', 'last_hit_triangles', 'channel', 't'):
                     out['%s_%d_%d' % (f, depth, i)] = getattr(ev.flat_hits, f)
                 out['pos_%d_%d' % (depth, i)] = ev.flat_hits.pos
-            if depth == 8:   # keep_photons_end is refused before any batch is uploaded
-                try:
-                    sim.simulate([ph[:10]], keep_photons_end=True)
-                    out['refused'] = np.array(0)
-                except NotImplementedError:
-                    out['refused'] = np.array(1)
+                # the end photons, gathered in global photon order
+                for f in ('pos', 'dir', 'pol', 'wavelengths', 't', 'flags', 'last_hit_triangles', 'weights', 'evidx'):
+                    out['end_%s_%d_%d' % (f, depth, i)] = getattr(ev.photons_end, f)
         np.savez(os.path.join(out_dir, 'rank%d.npz' % rank), **out)
     finally:
         dist.destroy_process_group()
@@ -179,8 +176,9 @@ def _pipe_worker(rank, world, port, out_dir, hits):
 def test_sharded_simulation_pipelined(tmp_path, hits):
     """DAQ off: each rank propagates its shards of all batches in ONE pipelined
     propagate_batches call (empty shards left out of it: rank 0 holds nothing of
-    the 1-photon batch), then the hits of every batch are gathered in batch
-    order.  The events equal the depth-1 run's (one propagate per batch)."""
+    the 1-photon batch), then the hits and the end photons of every batch are
+    gathered in batch order.  The events equal the depth-1 run's (one propagate
+    per batch), and the end photons equal the oracle's."""
     import torch
     if not torch.cuda.is_available():
         pytest.skip('no HIP device')
@@ -189,7 +187,6 @@ def test_sharded_simulation_pipelined(tmp_path, hits):
     got = [np.load(os.path.join(str(tmp_path), 'rank%d.npz' % r)) for r in range(2)]
     for g in got:
         assert tuple(g['pipeline_8']) == (len(SIZES), 1) and tuple(g['pipeline_1']) == (len(SIZES), 0)
-        assert int(g['refused']) == 1
     ranks_with_hits = (0, 1) if hits == 'all' else (0,)
     nhits = 0
     for r in ranks_with_hits:
@@ -200,5 +197,37 @@ def test_sharded_simulation_pipelined(tmp_path, hits):
                 assert np.array_equal(a, got[0]['%s_8_%d' % (f, i)]), (r, i, f)
             nhits += len(got[r]['flags_8_%d' % i])
     if hits == 'root':
-        assert 'flags_8_0' not in got[1].files
+        assert 'flags_8_0' not in got[1].files and 'end_flags_8_0' not in got[1].files
     assert nhits > 50
+
+    # keep_photons_end: each event's end photons == the oracle's for every rank's
+    # slice of each batch, in global photon order (rank r: RNG subsequences from
+    # r*S, one state set carried across the batches; empty shards not propagated)
+    from chroma.gpu.packing import PackedGeometry
+    from chroma.photon_source import isotropic
+    packed = PackedGeometry(_detector())
+    ph = isotropic(sum(SIZES), seed=43)
+    cuts = np.cumsum((0,) + SIZES)
+    S = NTPB * MAXB
+    states = [oracle.rng_init(S, seed=5, first_subsequence=r * S) for r in range(2)]
+    for i, n in enumerate(SIZES):
+        parts = []
+        for r in range(2):
+            lo, hi = n * r // 2, n * (r + 1) // 2
+            host = oracle.HostPhotons(ph[cuts[i] + lo:cuts[i] + hi])
+            host.flags[:] = 0
+            host.last_hit_triangles[:] = -1
+            host.weights[:] = 1
+            if hi > lo:
+                oracle.propagate(packed, host, states[r], S, NTPB, MAXB, 1000)
+            parts.append(host)
+        for r in ranks_with_hits:
+            for depth in (8, 1):
+                for f in ('flags', 'last_hit_triangles'):
+                    exp = np.concatenate([getattr(h, f) for h in parts])
+                    assert np.array_equal(got[r]['end_%s_%d_%d' % (f, depth, i)], exp), (r, depth, i, f)
+                for f in ('pos', 'dir', 'pol', 't', 'wavelengths'):
+                    exp = np.concatenate([np.asarray(getattr(h, f)).reshape(len(h.flags), -1) for h in parts])
+                    g = got[r]['end_%s_%d_%d' % (f, depth, i)].reshape(len(exp), -1)
+                    assert np.allclose(g, exp, rtol=1e-5, atol=1e-5), (r, depth, i, f)
+                assert (got[r]['end_evidx_%d_%d' % (depth, i)] == 0).all()

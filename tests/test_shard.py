@@ -88,6 +88,38 @@ def empty_rank_gather(rank, world):
     return shard.allgather_rows(local).numpy()
 
 
+def gather_photons_end(rank, world):
+    """keep_photons_end's gather (ShardedSimulation._photons_end): rank 1 holds
+    5 end photons, rank 0 none; gathered to rank 0 in rank order."""
+    from types import SimpleNamespace
+    from chroma.gpu import shard
+    f, _ = _local_hits(rank)
+    if rank == 0:
+        f = {k: _A(v.tensor[:0]) for k, v in f.items()}
+    rows = shard.gather_rows(shard.pack_photons(SimpleNamespace(**f)), 0)
+    if rows is None:
+        return np.zeros(0, np.uint32)
+    p = shard.unpack_photons(rows)
+    return np.concatenate([p.pos.ravel().view(np.uint32), p.dir.ravel().view(np.uint32),
+                           p.last_hit_triangles.view(np.uint32), p.flags, p.evidx, p.weights.view(np.uint32),
+                           p.t.view(np.uint32)])
+
+
+def test_gather_photons_end_to_root(tmp_path):
+    from types import SimpleNamespace
+    from chroma.gpu import shard
+    outs = _run('gather_photons_end', tmp_path)
+    assert outs[1].size == 0
+    f, _ = _local_hits(1)
+    p = shard.unpack_photons(shard.pack_photons(SimpleNamespace(**f)))
+    assert len(p) == 5 and p.flags[0] == np.uint32(4 | (1 << 31)) and (p.evidx == 1).all()
+    want = np.concatenate([p.pos.ravel().view(np.uint32), p.dir.ravel().view(np.uint32),
+                           p.last_hit_triangles.view(np.uint32), p.flags, p.evidx, p.weights.view(np.uint32),
+                           p.t.view(np.uint32)])
+    assert np.array_equal(outs[0], want)
+    assert np.array_equal(p.pos.ravel(), f['pos'].tensor.numpy()) and np.array_equal(p.t, f['t'].tensor.numpy())
+
+
 def test_gather_with_an_empty_rank(tmp_path):
     outs = _run('empty_rank_gather', tmp_path)
     assert np.array_equal(outs[0], np.arange(4, dtype=np.int32).reshape(2, 2))
