@@ -227,7 +227,7 @@ def test_sharded_simulation_pipelined(tmp_path, hits):
                     exp = np.concatenate([getattr(h, f) for h in parts])
                     assert np.array_equal(got[r]['end_%s_%d_%d' % (f, depth, i)], exp), (r, depth, i, f)
                 for f in ('pos', 'dir', 'pol', 't', 'wavelengths'):
-                    exp = np.concatenate([np.asarray(getattr(h, f)).reshape(len(h.flags), -1) for h in parts])
-                    g = got[r]['end_%s_%d_%d' % (f, depth, i)].reshape(len(exp), -1)
+                    exp = np.concatenate([np.asarray(getattr(h, f)) for h in parts]).reshape(n, -1)
+                    g = got[r]['end_%s_%d_%d' % (f, depth, i)].reshape(n, -1)
                     assert np.allclose(g, exp, rtol=1e-5, atol=1e-5), (r, depth, i, f)
                 assert (got[r]['end_evidx_%d_%d' % (depth, i)] == 0).all()
