@@ -49,7 +49,11 @@ def verify_or_create_dir(dirname, exception_msg, logger_msg=None):
             raise IOError(exception_msg)
         if logger_msg is not None:
             logger.info(logger_msg)
-        os.mkdir(dirname)
+        try:
+            os.mkdir(dirname)
+        except FileExistsError:     # another process (one per GPU) made it first
+            if not os.path.isdir(dirname):
+                raise IOError(exception_msg)
 
 
 # ------------------------------------------------------------ (de)serialisation
