@@ -297,9 +297,9 @@ static int geometry_create(const chr_geometry_desc *d, const chr_wide_bvh_desc *
 
         // de-indexed reference triangle records (v0, e1 = v1-v0, e2 = v2-v0,
         // e3 = v2-v1) for the reference walk: uploaded now only without a wide
-        // BVH (or with CHR_REF_NODES_RESIDENT); otherwise built on the device
-        // from the wide records the first time a call walks the reference BVH
-        if (dg.nwnodes == 0 || std::getenv("CHR_REF_NODES_RESIDENT")) {
+        // BVH; otherwise built on the device from the wide records the first
+        // time a call walks the reference BVH
+        if (dg.nwnodes == 0) {
             std::vector<float> tri((size_t)d->ntriangles * 12);
             const float *v = d->h_vertices;
 #pragma omp parallel for num_threads(chr::host_threads()) schedule(static)
@@ -318,9 +318,9 @@ static int geometry_create(const chr_geometry_desc *d, const chr_wide_bvh_desc *
             g->ref_tri_pending = true;
         }
 
-        // reference BVH nodes: all resident only without a wide BVH (or with
-        // CHR_REF_NODES_RESIDENT); otherwise the root, the rest on first use
-        if (dg.nwnodes == 0 || std::getenv("CHR_REF_NODES_RESIDENT")) {
+        // reference BVH nodes: all resident only without a wide BVH; otherwise
+        // the root, the rest on first use
+        if (dg.nwnodes == 0) {
             if ((rc = dev_upload(g, d->h_nodes, (size_t)d->nnodes * 16, &p))) throw rc;
         } else {
             g->h_ref_nodes = new std::vector<uint4>((const uint4 *)d->h_nodes, (const uint4 *)d->h_nodes + d->nnodes);

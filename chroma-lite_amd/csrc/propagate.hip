@@ -303,11 +303,7 @@ __device__ __forceinline__ int intersect_mesh(const DevGeom &g, V3 o, V3 d, floa
 constexpr int WIDE_LDS = 12;
 constexpr int LEAFQ = 16;          // per-lane parked-leaf queue (speculative walk), LDS
 // LDS words per work-item: traversal stack (node + entry distance) [+ leaf queue]
-constexpr int GROUP_MODE = 7000;   // group walk of G = WIDE - 7000 lanes per photon (propagate_group_kernel)
-constexpr int lds_words(int wide) {
-    return (wide >= GROUP_MODE && wide < GROUP_MODE + 16) ? 1
-           : (wide >= 2000 ? 2 * WIDE_LDS + LEAFQ : (wide ? 2 * WIDE_LDS : 0));
-}
+constexpr int lds_words(int wide) { return wide >= 2000 ? 2 * WIDE_LDS + LEAFQ : (wide ? 2 * WIDE_LDS : 0); }
 
 // The LDS column pointers are typed (ds_* ops) and the scratch spill array is
 // a separate object: an object holding both lives in scratch and its LDS
@@ -319,7 +315,6 @@ struct WStack {
     uint2 *spill;             // entries >= SL: private array (sstride 1) or a lane-strided HBM column
     uint32_t sstride;         // uint2 between consecutive spill entries of this work-item
     CHR_LDS uint32_t *leafq;  // parked leaves (speculative walk): entry i at leafq[i * BLOCK]
-    CHR_LDS uint32_t *group;  // group walk: the group's shared stack, entry i = (node, entry distance) at [2i, 2i+1]
 };
 // SL: stack entries kept in LDS (the rest spill to scratch)
 // TB: the LDS column stride (threads of the workgroup: trace_kernel may run
@@ -772,169 +767,8 @@ __device__ int intersect_wide_spec(const DevGeom &g, V3 o, V3 d, float &min_dist
     return best_id;
 }
 
-// Group walk: G lanes (G | 8) walk ONE ray of the wide BVH together, for
-// launches with few photons where the latency of each dependent step, not
-// throughput, sets the time (the multi-step tail launch of the nsteps policy).
-// Each lane slab-tests 8/G children of the current node; the nearest hit inner
-// child (first of the smallest entry distance, as expand_node) is found by an
-// in-group min over (distance, child) keys; the other hit inner children are
-// pushed in child order onto the group's LDS stack by the lanes that own them;
-// each lane tests the triangles of its own hit leaves and the group keeps the
-// min over (distance, reference rank) -- the nearest-hit rule of every other
-// walk, with the same reference leaf check and a running best that never
-// drops below the final one, so the result is unchanged.  All lanes of a group
-// hold identical walk state and take identical branches.
-constexpr int GROUP_STACK = WIDE_STACK;
 __device__ __forceinline__ uint32_t byte_of(uint32_t lo4, uint32_t hi4, int k) {
     return ((k < 4 ? lo4 : hi4) >> (8 * (k & 3))) & 0xFFu;
-}
-template <int G>
-__device__ int intersect_group(const DevGeom &g, V3 o, V3 d, float &min_distance, int last_hit,
-                               CHR_LDS uint32_t *stk, uint32_t &overflow, WalkCounts &cnt) {
-    static_assert(G == 2 || G == 4 || G == 8, "group size divides 8");
-    constexpr int C = 8 / G;                       // children per lane: k = sub + G * c
-    constexpr uint32_t INVALID = 0xFFFFFFFFu;
-    constexpr unsigned long long NONE = ~0ull;
-    const uint32_t lane = __lane_id();
-    const uint32_t sub = lane & (uint32_t)(G - 1), gbase = lane & ~(uint32_t)(G - 1);
-    const V3 noid = v3(-o.x / d.x, -o.y / d.y, -o.z / d.z);
-    const V3 inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
-    const RaySlab r = make_slab(noid, inv);
-    if (!(chr_isfinite(inv.x) && chr_isfinite(inv.y) && chr_isfinite(inv.z))) cnt.flat++;   // walk_kind 2
-    float best = __builtin_inff();
-    uint32_t best_rank = 0xFFFFFFFFu;
-    int best_id = -1;
-    const uint32_t last = (uint32_t)last_hit;
-    int sp = 0;
-    uint32_t node = 0;
-    while (true) {
-        if (node == INVALID) {                       // pop, culling against the best (mesh.h:94-96)
-            bool found = false;
-            while (sp > 0) {
-                sp--;
-                const uint32_t en = stk[2 * sp], et = stk[2 * sp + 1];
-                if (!(__uint_as_float(et) > best)) { node = en; found = true; break; }
-            }
-            if (!found) break;
-        }
-        const uint4 *np = g.wnodes + (size_t)g.wstride * node;
-        const uint4 h = gld(np), a1 = gld(np + 1), a2 = gld(np + 2), a3 = gld(np + 3), a4 = gld(np + 4),
-                    a5 = gld(np + 5);
-        const V3 org = v3(__uint_as_float(h.x), __uint_as_float(h.y), __uint_as_float(h.z));
-        const float sx = exp_scale(h.w), sy = exp_scale(h.w >> 8), sz = exp_scale(h.w >> 16);
-        const uint32_t nx0 = r.negx ? a2.z : a1.x, nx1 = r.negx ? a2.w : a1.y;
-        const uint32_t fx0 = r.negx ? a1.x : a2.z, fx1 = r.negx ? a1.y : a2.w;
-        const uint32_t ny0 = r.negy ? a3.x : a1.z, ny1 = r.negy ? a3.y : a1.w;
-        const uint32_t fy0 = r.negy ? a1.z : a3.x, fy1 = r.negy ? a1.w : a3.y;
-        const uint32_t nz0 = r.negz ? a3.z : a2.x, nz1 = r.negz ? a3.w : a2.y;
-        const uint32_t fz0 = r.negz ? a2.x : a3.z, fz1 = r.negz ? a2.y : a3.w;
-        float tk[C];
-        bool inner[C], leaf[C];
-        uint32_t kind_k[C];
-        unsigned long long key = NONE;
-#pragma unroll
-        for (int c = 0; c < C; ++c) {
-            const int k = (int)sub + G * c;
-            const uint32_t kind = byte_of(a4.z, a4.w, k);
-            const float tnx = __builtin_fmaf(__builtin_fmaf(byte_f(nx0, nx1, k), sx, org.x), r.inx, r.onx);
-            const float tfx = __builtin_fmaf(__builtin_fmaf(byte_f(fx0, fx1, k), sx, org.x), r.inx, r.ofx);
-            const float tny = __builtin_fmaf(__builtin_fmaf(byte_f(ny0, ny1, k), sy, org.y), r.iny, r.ony);
-            const float tfy = __builtin_fmaf(__builtin_fmaf(byte_f(fy0, fy1, k), sy, org.y), r.iny, r.ofy);
-            const float tnz = __builtin_fmaf(__builtin_fmaf(byte_f(nz0, nz1, k), sz, org.z), r.inz, r.onz);
-            const float tfz = __builtin_fmaf(__builtin_fmaf(byte_f(fz0, fz1, k), sz, org.z), r.inz, r.ofz);
-            const float tmin = __builtin_fmaxf(__builtin_fmaxf(__builtin_fmaxf(tnx, tny), tnz), 0.0f);
-            const float tmax = __builtin_fminf(__builtin_fminf(tfx, tfy), tfz);
-            const bool hit = (kind != 0u) & !(tmin > tmax) & !(tmin > best);
-            inner[c] = hit & (kind == WIDE_INNER);
-            leaf[c] = hit & (kind != WIDE_INNER);
-            tk[c] = tmin;
-            kind_k[c] = kind;
-            const unsigned long long cand = ((unsigned long long)__float_as_uint(tmin) << 32) | (uint32_t)k;
-            if (inner[c] && cand < key) key = cand;
-        }
-        uint32_t m_inner = 0;
-#pragma unroll
-        for (int c = 0; c < C; ++c)
-            m_inner |= (uint32_t)((__ballot(inner[c]) >> gbase) & ((1ull << G) - 1ull)) << (G * c);
-#pragma unroll
-        for (int off = 1; off < G; off <<= 1) {
-            const unsigned long long other = __shfl_xor(key, off, G);
-            key = other < key ? other : key;
-        }
-        uint32_t near = INVALID;
-        float near_t = 0.0f;
-        uint32_t m_push = m_inner;
-        if (key != NONE) {
-            const int nk = (int)(key & 7u);
-            near_t = __uint_as_float((uint32_t)(key >> 32));
-            near = a4.x + byte_of(a5.x, a5.y, nk);
-            m_push &= ~(1u << nk);
-        }
-        const int npush = __builtin_popcount(m_push);
-#pragma unroll
-        for (int c = 0; c < C; ++c) {
-            const int k = (int)sub + G * c;
-            if ((m_push >> k) & 1u) {
-                const int pos = sp + __builtin_popcount(m_push & ((1u << k) - 1u));
-                if (pos < GROUP_STACK) {
-                    stk[2 * pos] = a4.x + byte_of(a5.x, a5.y, k);
-                    stk[2 * pos + 1] = __float_as_uint(tk[c]);
-                }
-            }
-        }
-        if (sp + npush > GROUP_STACK) {
-            if (sub == 0) overflow += (uint32_t)(sp + npush - GROUP_STACK);
-            sp = GROUP_STACK;
-        } else {
-            sp += npush;
-        }
-        // this lane's hit leaves, each triangle in record order (intersect_wide_spec's test)
-        float lbest = best;
-        uint32_t lrank = best_rank;
-        int lid = -1;
-#pragma unroll
-        for (int c = 0; c < C; ++c) {
-            if (!leaf[c]) continue;
-            const int k = (int)sub + G * c;
-            const uint32_t first = a4.y + byte_of(a5.x, a5.y, k);
-            for (uint32_t j = 0; j < kind_k[c]; ++j) {
-                const float4 *rr = g.wtri + 4 * (size_t)(first + j);
-                const float4 r0 = gld(rr), r1 = gld(rr + 1), r2 = gld(rr + 2);
-                const uint32_t id = __float_as_uint(r2.y);
-                float dist;
-                if (id == last ||
-                    !intersect_record(o, d, r0, r1, r2, dist))
-                    continue;
-                const uint32_t rank = __float_as_uint(r2.z);
-                if (!(dist < lbest || (dist == lbest && rank < lrank))) continue;
-                const float4 r3 = gld(rr + 3);
-                V3 lo, hi;
-                node_bounds(g, make_uint4(__float_as_uint(r2.w), __float_as_uint(r3.x), __float_as_uint(r3.y), 0u),
-                            lo, hi);
-                float bd;
-                if (!intersect_box(noid, inv, lo, hi, bd) || bd > lbest) continue;   // mesh.h:94-96
-                lbest = dist;
-                lrank = rank;
-                lid = rec_of(g, rr);
-            }
-        }
-        unsigned long long lkey = lid == -1 ? NONE : (((unsigned long long)__float_as_uint(lbest) << 32) | lrank);
-#pragma unroll
-        for (int off = 1; off < G; off <<= 1) {
-            const unsigned long long ok = __shfl_xor(lkey, off, G);
-            const int oid = __shfl_xor(lid, off, G);
-            if (ok < lkey) { lkey = ok; lid = oid; }
-        }
-        if (lkey != NONE) {
-            best = __uint_as_float((uint32_t)(lkey >> 32));
-            best_rank = (uint32_t)lkey;
-            best_id = lid;
-        }
-        node = (near != INVALID && !(near_t > best)) ? near : INVALID;
-        __builtin_amdgcn_wave_barrier();             // pushes land before the group's next pop
-    }
-    min_distance = best_id == -1 ? -1.0f : best;
-    return best_id;
 }
 
 // ---------------------------------------------------------------- photon.h
@@ -1113,10 +947,7 @@ template <int BATCH, int WIDE, bool COUNT>
 __device__ __forceinline__ void fill_state(const DevGeom &g, State &s, Photon &p, Stack st, WStack &wst,
                                            uint32_t &overflow, WalkCounts &cnt) {
     int mesh_triangle;
-    if constexpr (WIDE >= GROUP_MODE && WIDE < GROUP_MODE + 16) {   // group walk, G = WIDE - GROUP_MODE
-        mesh_triangle =
-            intersect_group<WIDE - GROUP_MODE>(g, p.pos, p.dir, s.distance, p.last_hit, wst.group, overflow, cnt);
-    } else if constexpr (WIDE >= 2000)   // speculative walk, triangle-step threshold (WIDE - 2000)/8 of live lanes
+    if constexpr (WIDE >= 2000)   // speculative walk, triangle-step threshold (WIDE - 2000)/8 of live lanes
         mesh_triangle =
             intersect_wide_spec<COUNT, WIDE - 2000>(g, p.pos, p.dir, s.distance, p.last_hit, wst, overflow, cnt);
     else if constexpr (WIDE >= 1000)   // scheduled walk, triangle batch threshold WIDE - 1000
@@ -1574,19 +1405,13 @@ struct PropagateArgs {
     // and the launch runs only if *mode == want
     const uint32_t *dev_n;
     const uint32_t *mode;
-    uint32_t prio;                     // tail kernel: bit 0 raise its waves' issue priority (s_setprio),
-                                       // bit 1 the whole-wave walk specialised for one walker (GS = 64),
-                                       // bit 2 that walker software-pipelined (walk_lone)
+    uint32_t prio;                     // tail kernel: raise its waves' issue priority (s_setprio; the
+                                       // batches' tail, the critical path beside the next batch's walk)
     uint32_t want;
     // tail kernel, work-queue mode (nullptr: group g runs queue positions g, g + cap, ...): a
     // zeroed counter the photon groups take queue positions from, for queues no longer than
     // the slot count (each position then its own RNG slot, loaded and stored per photon)
     uint32_t *work;
-    // shade kernel, walk-order carry (nullptr: off): walive[winv[q]] = survival of queue position q
-    const uint32_t *winv;
-    uint8_t *walive;
-    uint32_t phys_lds;                 // shade / tail kernels: keep the physics tables in LDS (phys_cache)
-    uint32_t top_nodes;                // tail kernel: the first nodes of the wide BVH held in LDS (stage_top)
 };
 // modes of a device-driven step slot (step_head_kernel)
 constexpr uint32_t STEP_IDLE = 0, STEP_ONE = 1, STEP_TAIL = 2;
@@ -1815,7 +1640,7 @@ __device__ __forceinline__ DevGeom phys_cache(const DevGeom &g, uint4 *lds, uint
 }
 
 struct QueuedPhoton {
-    uint32_t pid, history, walk;
+    uint32_t pid, history;
     V3 pos, dir, pol;
     float wavelength, time, weight;
     int last_hit;
@@ -1837,29 +1662,28 @@ __device__ __forceinline__ void fetch_queued(const PropagateArgs &a, uint32_t q,
     f.weight = a.weights[f.pid];
     f.last_hit = a.last_hit[f.pid];
     f.hit = a.hits[q];
-    f.walk = a.winv ? a.winv[q] : 0u;
 }
-// P2: the queue entry of the photon two positions ahead is loaded one iteration
+// The queue entry of the photon two positions ahead is loaded one iteration
 // early, so the next photon's state loads go out without first waiting for its
-// queue entry (a dependent round trip per photon otherwise)
-// SC: no wait for the write-back.  On gfx9 stores count in vmcnt with the loads,
+// queue entry (a dependent round trip per photon otherwise; r04 ab5: 487.8-488.2 ->
+// 489.4 M/s).
+// No wait for the write-back (r04 ab9/ab10).  On gfx9 stores count in vmcnt with the loads,
 // in issue order, and the compiler waits for a prefetched value with the count of
-// the path into its use with the fewest younger operations.  Without SC the loop's
-// back edge copied the prefetched photon after this iteration's stores with
-// `s_waitcnt vmcnt(0)` (the prefetch under `if (pos + cap < n)`, the entry path from
-// the prologue, the queue entry's fallback load all leave paths with none younger),
-// so every iteration waited for its own stores to be acknowledged.  With SC every
-// lane issues the prefetch (position clamped into the queue), the queue entry two
+// the path into its use with the fewest younger operations.  With the prefetch under
+// `if (pos + cap < n)` the loop's back edge copied the prefetched photon after this
+// iteration's stores with `s_waitcnt vmcnt(0)` (the entry path from the prologue and
+// the queue entry's fallback load also leave paths with none younger), so every
+// iteration waited for its own stores to be acknowledged.  Here every lane issues the prefetch (position clamped into the queue), the queue entry two
 // ahead is always the one loaded (no fallback load), and the first iteration is
 // peeled, so every path into the loop has the write-back behind the prefetch: the
 // prefetch is waited for at the physics' join, before the stores, and nothing waits
 // for the stores.
-template <int MINW, bool P2 = false, bool SC = false>
+template <int MINW>
 __global__ __launch_bounds__(BLOCK, MINW) void shade_kernel(const DevGeom *__restrict__ gdev, PropagateArgs a,
                                                             uint32_t cap) {
     if (a.mode && *a.mode != a.want) return;
     __shared__ uint4 phys_lds[SHADE_PHYS_WORDS / 4];
-    const DevGeom g = phys_cache(*gdev, phys_lds, a.phys_lds ? SHADE_PHYS_WORDS : 0u);
+    const DevGeom g = phys_cache(*gdev, phys_lds, SHADE_PHYS_WORDS);
     const uint32_t slot = blockIdx.x * BLOCK + threadIdx.x;
     const uint32_t n = a.dev_n ? *a.dev_n - 1u : (uint32_t)a.nthreads;
     if (slot == 0 && a.zero_word) *a.zero_word = 0u;
@@ -1871,19 +1695,13 @@ __global__ __launch_bounds__(BLOCK, MINW) void shade_kernel(const DevGeom *__res
     pf.start(P_OTHER);
     auto clampq = [n](uint32_t q) { return q < n ? q : n - 1u; };
     QueuedPhoton nx;
-    if (SC) fetch_queued(a, clampq(slot), nx);
-    else if (slot < n) fetch_queued(a, slot, nx);
-    uint32_t pid2 = 0xFFFFFFFFu;                       // P2: queue entry of position pos + cap
-    if (SC && P2) pid2 = a.input_queue[clampq(slot + cap)];
-    else if (P2 && slot + cap < n) pid2 = a.input_queue[slot + cap];
+    fetch_queued(a, clampq(slot), nx);
+    uint32_t pid2 = a.input_queue[clampq(slot + cap)];   // queue entry of position pos + cap
     uint32_t pos = slot;
     auto body = [&](uint32_t qb) __attribute__((always_inline)) {
         const QueuedPhoton cur = nx;
-        if (SC && P2) fetch_queued<true>(a, clampq(pos + cap), nx, pid2);
-        else if (SC) fetch_queued(a, clampq(pos + cap), nx);
-        else if (pos + cap < n) fetch_queued(a, pos + cap, nx, P2 ? pid2 : 0xFFFFFFFFu);
-        if (SC && P2) pid2 = a.input_queue[clampq(pos + 2 * cap)];
-        else if (P2 && pos + 2 * cap < n) pid2 = a.input_queue[pos + 2 * cap];
+        fetch_queued<true>(a, clampq(pos + cap), nx, pid2);
+        pid2 = a.input_queue[clampq(pos + 2 * cap)];
         bool alive = false;
         const bool valid = pos < n && !(cur.history & DEAD_MASK);
         Photon p;
@@ -1924,14 +1742,12 @@ __global__ __launch_bounds__(BLOCK, MINW) void shade_kernel(const DevGeom *__res
             }
             alive = (p.history & DEAD_MASK) == 0;
         }
-        if constexpr (SC) {
-            // the prefetched photon and queue entry waited for here, on every path and
-            // before the write-back (see SC above)
-            asm volatile("" ::"v"(nx.pid), "v"(nx.history), "v"(nx.pos.x), "v"(nx.pos.y), "v"(nx.pos.z), "v"(nx.dir.x),
-                         "v"(nx.dir.y), "v"(nx.dir.z), "v"(nx.pol.x), "v"(nx.pol.y), "v"(nx.pol.z));
-            asm volatile("" ::"v"(nx.wavelength), "v"(nx.time), "v"(nx.weight), "v"(nx.last_hit), "v"(nx.hit.x),
-                         "v"(nx.hit.y), "v"(nx.walk), "v"(pid2));
-        }
+        // the prefetched photon and queue entry waited for here, on every path and
+        // before the write-back (see above)
+        asm volatile("" ::"v"(nx.pid), "v"(nx.history), "v"(nx.pos.x), "v"(nx.pos.y), "v"(nx.pos.z), "v"(nx.dir.x),
+                     "v"(nx.dir.y), "v"(nx.dir.z), "v"(nx.pol.x), "v"(nx.pol.y), "v"(nx.pol.z));
+        asm volatile("" ::"v"(nx.wavelength), "v"(nx.time), "v"(nx.weight), "v"(nx.last_hit), "v"(nx.hit.x),
+                     "v"(nx.hit.y), "v"(pid2));
         if (valid) {
             const uint32_t pid = cur.pid;
             store3(a.pos, pid, p.pos);
@@ -1943,12 +1759,11 @@ __global__ __launch_bounds__(BLOCK, MINW) void shade_kernel(const DevGeom *__res
             a.last_hit[pid] = p.last_hit;
             a.weights[pid] = p.weight;
         }
-        if (a.walive && pos < n) a.walive[cur.walk] = alive ? 1u : 0u;   // dead on entry: 0 too
         const unsigned long long mask = __ballot(alive);
         if ((slot & 63u) == 0) a.alive_masks[qb >> 6] = mask;
     };
     uint32_t qb = slot & ~63u;                         // wave-uniform trip count
-    if (SC && qb < n) {
+    if (qb < n) {
         // the first iteration peeled: the loop's first wait for the prefetched queue
         // entry and state then has this iteration's write-back behind it on every
         // path into the loop (from the prologue it would be the youngest load: vmcnt(0))
@@ -1967,52 +1782,6 @@ __global__ __launch_bounds__(BLOCK, MINW) void shade_kernel(const DevGeom *__res
 #endif
 }
 
-// Multi-step launches (the tail of the nsteps policy, photon.py:261-264): a
-// group of G work-items per RNG slot runs the slot's photons through
-// run_photon with the group walk; the group's lanes hold identical photon and
-// RNG state and compute identical results (every lane stores the same words),
-// so each photon computes exactly what the one-lane kernels compute.  Alive
-// bits are OR-ed per queue position into zeroed mask words.
-template <int G, int MINW>
-__global__ __launch_bounds__(BLOCK, MINW) void propagate_group_kernel(const DevGeom *__restrict__ gdev, PropagateArgs a,
-                                                                      uint32_t cap) {
-    __shared__ uint32_t group_stacks[(BLOCK / G) * GROUP_STACK * 2];
-    const uint32_t tid = blockIdx.x * BLOCK + threadIdx.x;
-    if (a.mode && *a.mode != a.want) return;
-    const uint32_t slot = tid / G, sub = tid & (uint32_t)(G - 1);
-    const uint32_t n = a.dev_n ? *a.dev_n - 1u : (uint32_t)a.nthreads;
-    if (slot >= cap || slot >= n) return;          // whole groups
-    Stack st;
-    st.lds = nullptr;
-    WStack wst;
-    wst.node = nullptr; wst.dist = nullptr; wst.spill = nullptr; wst.sstride = 1; wst.leafq = nullptr;
-    wst.group = (CHR_LDS uint32_t *)group_stacks + (threadIdx.x / G) * GROUP_STACK * 2;
-    uint32_t overflow = 0;
-    WalkCounts cnt{0u, 0u, 0u, 0u, 0u, 0ull, 0ull, 0u};
-    const DevGeom &g = *gdev;
-    chr_xorwow rng;
-    bool have_rng = false;
-    for (uint32_t q = slot; q < n; q += cap) {
-        const uint32_t photon_id = a.input_queue[q];
-        const uint32_t history = a.flags[photon_id] & 0xFFFFu;   // photon.h:29
-        if (history & DEAD_MASK) continue;
-        if (!have_rng) { load_rng(a, slot, rng); have_rng = true; }
-        int steps = 0;
-        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();   // 100 MHz
-        const bool alive = run_photon<8, GROUP_MODE + G, false>(g, a, photon_id, history, rng, st, wst, overflow, cnt,
-                                                                &steps);
-        if (alive && sub == 0) atomicOr(a.alive_masks + (q >> 6), 1ull << (q & 63u));
-        if (sub == 0 && a.diag) {   // the tail's serial chain: longest photon in steps and in time
-            const unsigned long long cyc = __builtin_amdgcn_s_memrealtime() - t0;
-            atomicMax(a.diag + 1, (uint32_t)steps);
-            atomicMax(reinterpret_cast<unsigned long long *>(a.diag + 2),
-                      (cyc << 16) | (unsigned long long)(steps > 0xFFFF ? 0xFFFF : steps));
-        }
-    }
-    if (have_rng && sub == 0) store_rng(a, slot, rng);
-    if (sub == 0 && overflow) atomicAdd(a.counters, overflow);
-    if (sub == 0 && cnt.flat && a.diag) atomicAdd(a.diag, cnt.flat);
-}
 
 // ---------------------------------------------------------------- wave-adaptive tail
 // The multi-step tail launch lasts as long as its longest-lived photon: on the
@@ -2645,11 +2414,11 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_tail_kernel(const DevGe
     if (a.mode && *a.mode != a.want) return;
     // a tail overlapped by the next batch (chr_propagate_batches) is the critical
     // path: its waves win the SIMD's issue arbitration over that batch's walk
-    if (a.prio & 1u) __builtin_amdgcn_s_setprio(3);
+    if (a.prio) __builtin_amdgcn_s_setprio(3);
     __shared__ uint4 phys_lds[TAIL_PHYS_WORDS / 4];
-    const DevGeom g = phys_cache(*gdev, phys_lds, a.phys_lds ? TAIL_PHYS_WORDS : 0u);
+    const DevGeom g = phys_cache(*gdev, phys_lds, TAIL_PHYS_WORDS);
     __shared__ uint4 top_lds[6 * TOP_NODES];   // 7 KB: 2 workgroups per CU hold 2 x 79 KB
-    const TopNodes top = stage_top<BLOCK>(g, (CHR_LDS u32x4 *)top_lds, a.top_nodes);
+    const TopNodes top = stage_top<BLOCK>(g, (CHR_LDS u32x4 *)top_lds, TOP_NODES);
     const uint32_t slot = tid / 8, sub = tid & 7u;
     const uint32_t n = a.dev_n ? *a.dev_n - 1u : (uint32_t)a.nthreads;
     const uint32_t nslot = cap < n ? cap : n;
@@ -2778,11 +2547,8 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_tail_kernel(const DevGe
             const uint32_t seg0 = lane & ~(uint32_t)(Gs - 1);
             float sd;
             uint32_t it;
-            const int st = (Gs == 64 && (a.prio & 4u))
+            const int st = Gs == 64
                                ? walk_lone(g, o, dd, last, LdsFlat{wstack}, TAIL_STACK * 8, LdsFlat{wtris}, overflow, sd, it)
-                           : (Gs == 64 && (a.prio & 2u))
-                               ? walk_segment<64>(g, act, o, dd, last, 64, LdsFlat{wstack}, TAIL_STACK * 8, LdsFlat{wtris},
-                                                  top, overflow, sd, it)
                                : walk_segment<0>(g, act, o, dd, last, Gs, LdsFlat{wstack + seg0 / 8 * TAIL_STACK * 2},
                                                  TAIL_STACK * Gs / 8, LdsFlat{wtris + 4 * seg0}, top, overflow, sd, it);
             if (Gs == 64) {   // one segment: every lane already holds the result
@@ -2857,20 +2623,11 @@ __global__ __launch_bounds__(BLOCK) void ref_triangles_kernel(const float4 *wtri
 
 // ---------------------------------------------------------------- ray binning (trace order)
 // The order in which trace_kernel walks the queued rays does not change any
-// result (each walk's result is stored at its queue position), so rays are
-// binned by direction cell (a 22-bit radix sort of 2^22 octahedral cells in Hilbert order
-// by default, bin_key_mode; round 1-3: 16 bits, 65,536 cells row-major) to make the
-// 64 rays of a wave walk the same subtrees: better L1/L2 reuse of nodes.
-// kmode (CHR_BIN_KEY, A/B): 0 row-major 8+8 bits; 1 the same cells in Morton order (2D-near
-// cells adjacent in walk order); 2 / 3 / 4 Morton order of 10+10 / 11+11 / 12+12-bit cells
-// (20 / 22 / 24-bit sorts); 5 11+11-bit cells in Hilbert order (22 bits)
-__device__ __forceinline__ uint32_t spread_bits(uint32_t x) {   // bit i -> bit 2i (x < 2^16)
-    x = (x | (x << 8)) & 0x00FF00FFu;
-    x = (x | (x << 4)) & 0x0F0F0F0Fu;
-    x = (x | (x << 2)) & 0x33333333u;
-    return (x | (x << 1)) & 0x55555555u;
-}
-__device__ __forceinline__ uint32_t octa_cell(V3 d, uint32_t kmode = 0) {   // octahedral map of a unit vector
+// result (each walk's result is stored at its queue position), so the first
+// step's rays are binned by direction cell (a 22-bit radix sort of 2^22
+// octahedral cells in Hilbert order; rounds 1-3: 16 bits, 65,536 cells row-major)
+// to make the 64 rays of a wave walk the same subtrees: better L1/L2 reuse of nodes.
+__device__ __forceinline__ uint32_t octa_cell(V3 d) {   // octahedral map of a unit vector, Hilbert order of 11+11-bit cells
     const float s = fabsf(d.x) + fabsf(d.y) + fabsf(d.z);
     float u = d.x / s, v = d.y / s;
     if (d.z < 0.0f) {
@@ -2878,41 +2635,30 @@ __device__ __forceinline__ uint32_t octa_cell(V3 d, uint32_t kmode = 0) {   // o
         const float vv = (1.0f - fabsf(u)) * (v < 0.0f ? -1.0f : 1.0f);
         u = uu; v = vv;
     }
-    if (kmode == 5) {   // 11+11-bit cells in Hilbert order (no jumps between quadrants)
-        uint32_t x = (uint32_t)fminf(fmaxf((u + 1.0f) * 1024.0f, 0.0f), 2047.0f);
-        uint32_t y = (uint32_t)fminf(fmaxf((v + 1.0f) * 1024.0f, 0.0f), 2047.0f);
-        uint32_t dkey = 0;
-        for (uint32_t sq = 1024u; sq > 0u; sq >>= 1) {
-            const uint32_t rx = (x & sq) ? 1u : 0u, ry = (y & sq) ? 1u : 0u;
-            dkey += sq * sq * ((3u * rx) ^ ry);
-            if (ry == 0u) {   // rotate the quadrant
-                if (rx == 1u) { x = 2047u - x; y = 2047u - y; }
-                const uint32_t t = x; x = y; y = t;
-            }
+    uint32_t x = (uint32_t)fminf(fmaxf((u + 1.0f) * 1024.0f, 0.0f), 2047.0f);
+    uint32_t y = (uint32_t)fminf(fmaxf((v + 1.0f) * 1024.0f, 0.0f), 2047.0f);
+    uint32_t dkey = 0;
+    for (uint32_t sq = 1024u; sq > 0u; sq >>= 1) {   // Hilbert order: no jumps between quadrants
+        const uint32_t rx = (x & sq) ? 1u : 0u, ry = (y & sq) ? 1u : 0u;
+        dkey += sq * sq * ((3u * rx) ^ ry);
+        if (ry == 0u) {   // rotate the quadrant
+            if (rx == 1u) { x = 2047u - x; y = 2047u - y; }
+            const uint32_t t = x; x = y; y = t;
         }
-        return dkey;
     }
-    if (kmode >= 2) {   // b = 8 + kmode bits per axis
-        const float half = (float)(1u << (7u + kmode)), top = (float)((1u << (8u + kmode)) - 1u);
-        const uint32_t iu = (uint32_t)fminf(fmaxf((u + 1.0f) * half, 0.0f), top);
-        const uint32_t iv = (uint32_t)fminf(fmaxf((v + 1.0f) * half, 0.0f), top);
-        return (spread_bits(iv) << 1) | spread_bits(iu);
-    }
-    const uint32_t iu = (uint32_t)fminf(fmaxf((u + 1.0f) * 128.0f, 0.0f), 255.0f);
-    const uint32_t iv = (uint32_t)fminf(fmaxf((v + 1.0f) * 128.0f, 0.0f), 255.0f);
-    return kmode == 1 ? ((spread_bits(iv) << 1) | spread_bits(iu)) : ((iv << 8) | iu);
+    return dkey;
 }
 // direction-binning key of a queued photon (0 for a zero / non-finite direction)
-__device__ __forceinline__ uint32_t bin_key_of(V3 d, uint32_t kmode = 0) {
+__device__ __forceinline__ uint32_t bin_key_of(V3 d) {
     const float l = sqrtf(d.x * d.x + d.y * d.y + d.z * d.z);
-    return (l > 0.0f && l < __builtin_inff()) ? octa_cell(v3(d.x / l, d.y / l, d.z / l), kmode) : 0u;
+    return (l > 0.0f && l < __builtin_inff()) ? octa_cell(v3(d.x / l, d.y / l, d.z / l)) : 0u;
 }
 __global__ __launch_bounds__(BLOCK) void bin_key_kernel(const float *dir, const uint32_t *queue, uint32_t n,
-                                                        uint32_t *keys, uint32_t *vals, uint32_t kmode) {
+                                                        uint32_t *keys, uint32_t *vals) {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     if (i >= n) return;
     const uint32_t pid = queue[i];
-    keys[i] = bin_key_of(v3(dir[3 * pid], dir[3 * pid + 1], dir[3 * pid + 2]), kmode);
+    keys[i] = bin_key_of(v3(dir[3 * pid], dir[3 * pid + 1], dir[3 * pid + 2]));
     vals[i] = i;
 }
 // ---------------------------------------------------------------- wavefront split
@@ -2953,13 +2699,9 @@ struct TraceArgs {
     // (the input queue's count header) and the launch runs only if *mode is STEP_ONE
     const uint32_t *dev_n;
     const uint32_t *mode;
-    uint32_t *winv;              // walk-order carry: winv[queue position] = its walk position (nullptr: off)
-    uint32_t drain_max;          // a wave drains its last <= drain_max walks whole-wave (0: never; at most 8)
-    uint32_t claim_ahead;        // refills from claimed chunks, the next claim in flight (trace_claim_ahead)
-    uint32_t spread;             // launches with fewer rays than lanes: each wave claims its share (trace_spread)
-    uint32_t drain_lone;         // a wave draining ONE walk walks it with walk_lone (trace_drain_lone)
 };
-constexpr uint32_t CLAIM = 64;   // ray-counter chunk of trace_kernel's claim-ahead refill
+constexpr uint32_t CLAIM = 64;       // rays a wave takes from the ray counter per refill (at most)
+constexpr uint32_t DRAIN_MAX = 4;    // a wave drains its last <= DRAIN_MAX walks whole-wave
 
 // Enrol queue position p in the flat list of the next trace launch (its walk
 // is flat, walk_kind 2): f = slot in the flat list, hits[p] = (FLAT_HIT, f).
@@ -3010,12 +2752,12 @@ __global__ __launch_bounds__(BLOCK) void classify_kernel(const float *pos, const
                                                          const int32_t *last_hit, const uint32_t *queue, uint32_t n,
                                                          int2 *hits, uint32_t *flat_q, uint32_t *flat_count,
                                                          unsigned long long *flat_best, uint32_t *keys, uint32_t *vals,
-                                                         uint4 *rays, uint32_t kmode) {
+                                                         uint4 *rays) {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     if (i >= n) return;
     const uint32_t pid = queue[i];
     if (keys) {
-        keys[i] = bin_key_of(v3(dir[3 * pid], dir[3 * pid + 1], dir[3 * pid + 2]), kmode);
+        keys[i] = bin_key_of(v3(dir[3 * pid], dir[3 * pid + 1], dir[3 * pid + 2]));
         vals[i] = i;
     }
     if ((flags[pid] & 0xFFFFu) & DEAD_MASK) {
@@ -3039,18 +2781,15 @@ __global__ __launch_bounds__(BLOCK) void permute_rays_kernel(const uint4 *rays_i
 // COUNT: walk counters; F: triangle step once F/8 of the walking lanes have
 // parked leaves (intersect_wide_spec); SL: stack entries in LDS; MINW: waves
 // per SIMD; R: refill once R of the 64 lanes are without a ray.
-template <bool COUNT, int F, int SL, int MINW, int R, int TB = BLOCK, int TOPN = 0>
-__global__ __launch_bounds__(TB, MINW) void trace_kernel(const DevGeom *__restrict__ gdev, TraceArgs a) {
+template <bool COUNT, int F, int SL, int MINW, int R>
+__global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__restrict__ gdev, TraceArgs a) {
+    constexpr int TB = BLOCK;
     __shared__ uint32_t lds[(2 * SL + LEAFQ) * TB];
-    // the top of the tree (stage_top): TB = 1024 makes one copy per CU serve its 16 waves
-    __shared__ uint4 top_lds[TOPN > 0 ? 6 * TOPN : 1];
     // a draining wave's walk_segment stacks (8 x DSTK entries, DSTK per 8 lanes) + triangle
     // lists in its LDS rows
     constexpr int DSTK = ((2 * SL + LEAFQ) * 64 - 2 * TAIL_TRI) / 16;
-    // a walk's stack holds >= 112 entries: 8 lanes per walk (drains of 5..8 walks) need
-    // DSTK >= 112, 16 lanes (<= 4 walks, the default) 2 * DSTK
+    // a walk's stack holds >= 112 entries: 16 lanes per walk (<= DRAIN_MAX = 4 walks) need 2 * DSTK
     static_assert(2 * DSTK >= 112, "drain needs the wave's LDS rows");
-    const uint32_t drain_max = DSTK >= 112 ? a.drain_max : (a.drain_max < 4u ? a.drain_max : 4u);
     WStack st;
     // Deep stack entries live in a lane-strided HBM column sized for this
     // persistent grid, not in private scratch: a kernel with a private segment
@@ -3064,7 +2803,7 @@ __global__ __launch_bounds__(TB, MINW) void trace_kernel(const DevGeom *__restri
     if (a.mode && *a.mode != STEP_ONE) return;
     const uint32_t n = a.dev_n ? *a.dev_n - 1u : a.n;
     const DevGeom &g = *gdev;
-    const TopNodes top = TOPN > 0 ? stage_top<TB>(g, (CHR_LDS u32x4 *)top_lds, (uint32_t)TOPN) : TopNodes{nullptr, 0u};
+    const TopNodes top{nullptr, 0u};
     const uint32_t lane = __lane_id();
     uint32_t overflow = 0;
     WalkCounts cnt{0u, 0u, 0u, 0u, 0u, 0ull, 0ull, 0u};
@@ -3085,14 +2824,11 @@ __global__ __launch_bounds__(TB, MINW) void trace_kernel(const DevGeom *__restri
     bool walk_done = true, drain = false;
     uint32_t qh = 0, qt = 0, pcur = 0, pleft = 0;
     constexpr uint32_t INVALID = 0xFFFFFFFFu;
-    // claimed ray-counter chunk (claim_ahead): next index cb, cn left; pend: the
-    // next chunk's base, claimed ahead (valid in lane 0 once have_pend)
-    uint32_t cb = 0, cn = 0, pend = 0;
-    bool have_pend = false;
-    // claim size: CLAIM, or with spread a wave's share of a launch smaller than the
-    // grid's lanes (every wave then walks a few rays and reaches its drain sooner)
+    // claim size: CLAIM, or a wave's share of a launch smaller than the grid's lanes
+    // (every wave then walks a few rays and reaches its drain sooner; r03 ab24/ab25:
+    // trace 14.40 -> 14.32 ms per step, the last launches 0.39 -> 0.37 ms)
     uint32_t claim = CLAIM;
-    if (a.spread) {
+    {
         const uint32_t waves = gridDim.x * (TB / 64);
         const uint32_t share = (total + waves - 1u) / waves;
         claim = share < 1u ? 1u : (share < CLAIM ? share : CLAIM);
@@ -3120,49 +2856,18 @@ __global__ __launch_bounds__(TB, MINW) void trace_kernel(const DevGeom *__restri
             if (need != 0 && (__popcll(need) >= R || need == __ballot(1))) {
                 const uint32_t want = (uint32_t)__popcll(need) < claim ? (uint32_t)__popcll(need) : claim;
                 const uint32_t rank = (uint32_t)__popcll(need & ((1ull << lane) - 1ull));
-                uint32_t j;
-                if (a.claim_ahead) {
-                    // Rays come from the wave's claimed chunk (CLAIM indices of the ray
-                    // counter); the next chunk's atomic is issued while the wave still
-                    // walks, so a refill does not wait on the counter's round trip.  Near
-                    // the end of a launch (fewer rays left than two grids of lanes) chunks
-                    // are claimed when needed, so no wave sits on rays others could walk.
-                    uint32_t b0 = cb, g0 = want < cn ? want : cn;
-                    cb += g0;
-                    cn -= g0;
-                    uint32_t b1 = 0, g1 = 0;
-                    if (g0 < want) {   // this chunk is used up: the pending one, or a claim now
-                        uint32_t nb = 0;
-                        if (have_pend) nb = (uint32_t)__shfl((int)pend, 0);
-                        else if (lane == 0) nb = atomicAdd(a.next, claim);
-                        nb = have_pend ? nb : (uint32_t)__shfl((int)nb, 0);
-                        have_pend = false;
-                        b1 = nb;
-                        g1 = want - g0 < claim ? want - g0 : claim;
-                        cb = nb + g1;
-                        cn = claim - g1;
-                    }
-                    j = rank < g0 ? b0 + rank : b1 + (rank - g0);
-                    if (cb >= total) exhausted = true;     // later claims lie beyond the last item
-                    else if (!have_pend && cb + 2u * gridDim.x * TB < total) {
-                        if (lane == 0) pend = atomicAdd(a.next, claim);
-                        have_pend = true;
-                    }
-                } else {
-                    const int leader = __ffsll((long long)need) - 1;
-                    uint32_t base = 0;
-                    if ((int)lane == leader) base = atomicAdd(a.next, want);
-                    base = __shfl(base, leader);
-                    if (base + want >= total) exhausted = true;
-                    j = base + rank;
-                }
+                const int leader = __ffsll((long long)need) - 1;
+                uint32_t base = 0;
+                if ((int)lane == leader) base = atomicAdd(a.next, want);
+                base = __shfl(base, leader);
+                if (base + want >= total) exhausted = true;
+                const uint32_t j = base + rank;
                 if (!has_ray && rank < want) {
                     bool start = false;
                     if (j < n && a.rays) {
                         // the ray record: one 32-B load (put_ray); skip bit: dead / NaN / flat
                         const uint4 r0 = gld(a.rays + 2 * (size_t)j), r1 = gld(a.rays + 2 * (size_t)j + 1);
                         q = r1.w & ~RAY_SKIP;
-                        if (a.winv) a.winv[q] = j;
                         if (!(r1.w & RAY_SKIP)) {
                             o = v3(__uint_as_float(r0.x), __uint_as_float(r0.y), __uint_as_float(r0.z));
                             d = v3(__uint_as_float(r0.w), __uint_as_float(r1.x), __uint_as_float(r1.y));
@@ -3236,7 +2941,7 @@ __global__ __launch_bounds__(TB, MINW) void trace_kernel(const DevGeom *__restri
             // every small launch).  Each restarts from the root seeded with its
             // best so far (conservative culling, the same nearest hit); the
             // lanes' stacks are abandoned and their LDS rows reused.
-            if (exhausted && __ballot(has_ray) != 0 && (uint32_t)__popcll(__ballot(has_ray)) <= drain_max &&
+            if (exhausted && __ballot(has_ray) != 0 && (uint32_t)__popcll(__ballot(has_ray)) <= DRAIN_MAX &&
                 __ballot(has_ray && flat_f >= 0) == 0) {   // no cut-item sub-walks (they start mid-tree)
                 drain = true;   // after the loop, where the walk state below is no longer live
                 break;
@@ -3269,9 +2974,7 @@ __global__ __launch_bounds__(TB, MINW) void trace_kernel(const DevGeom *__restri
             }
             if constexpr (COUNT) { cnt.nodes++; walk_cost++; if (wave_leader()) cnt.wave_nodes++; }
             uint4 h, a1, a2, a3, a4, a5;
-            if constexpr (TOPN > 0) {
-                load_node(g, top, node, h, a1, a2, a3, a4, a5);
-            } else {
+            {
                 const uint4 *np = g.wnodes + (size_t)g.wstride * node;
                 h = gld(np); a1 = gld(np + 1); a2 = gld(np + 2); a3 = gld(np + 3); a4 = gld(np + 4); a5 = gld(np + 5);
             }
@@ -3332,7 +3035,7 @@ __global__ __launch_bounds__(TB, MINW) void trace_kernel(const DevGeom *__restri
             pf.tick(P_DRAIN);
             const unsigned long long rm = __ballot(has_ray);
             const int w = __popcll(rm);
-            const int Gs = w == 1 ? 64 : (w == 2 ? 32 : (w <= 4 ? 16 : 8));
+            const int Gs = w == 1 ? 64 : (w == 2 ? 32 : 16);
             const int si = (int)lane / Gs;
             unsigned long long m = rm;
             for (int i = 0; i < si && m != 0; ++i) m &= m - 1;
@@ -3348,7 +3051,7 @@ __global__ __launch_bounds__(TB, MINW) void trace_kernel(const DevGeom *__restri
             CHR_LDS uint32_t *wbase = (CHR_LDS uint32_t *)(lds + (threadIdx.x & ~63u));
             float sdist;
             uint32_t sit;
-            const int tri = (w == 1 && a.drain_lone)
+            const int tri = w == 1
                                 ? walk_lone(g, so, sdir, slast, LdsRowsT<TB>{wbase, 0}, DSTK * 8,
                                             LdsRowsT<TB>{wbase, 8 * DSTK * 2}, overflow, sdist, sit, sbest, srank, sid)
                                 : walk_segment<0>(g, act, so, sdir, slast, Gs, LdsRowsT<TB>{wbase, seg0 / 8 * DSTK * 2},
@@ -3385,48 +3088,6 @@ __global__ __launch_bounds__(TB, MINW) void trace_kernel(const DevGeom *__restri
         atomicAdd(c64 + 3, (unsigned long long)cnt.wave_nodes);
         atomicAdd(c64 + 4, (unsigned long long)cnt.wave_tris);
     }
-}
-
-// Coherence key of a queued photon: 18-bit Morton code of its position in the
-// world box (6 bits/axis) above a 12-bit octahedral direction cell.  Photons
-// already dead sort last (their work-items exit at once).
-__device__ __forceinline__ uint32_t spread3_6(uint32_t x) {   // 6 bits -> every third bit
-    x &= 0x3Fu;
-    x = (x | (x << 8)) & 0x0000F00Fu;
-    x = (x | (x << 4)) & 0x000C30C3u;
-    x = (x | (x << 2)) & 0x00249249u;
-    return x;
-}
-
-__global__ __launch_bounds__(BLOCK) void sort_key_kernel(const float *pos, const float *dir, const uint32_t *flags,
-                                                         const uint32_t *queue, int32_t first, int32_t n,
-                                                         float ox, float oy, float oz, float inv_extent,
-                                                         uint32_t *keys, uint32_t *vals) {
-    const int t = blockIdx.x * BLOCK + threadIdx.x;
-    if (t >= n) return;
-    const uint32_t ph = queue[first + t];
-    uint32_t key = 0xFFFFFFFFu;
-    if (!((flags[ph] & 0xFFFFu) & DEAD_MASK)) {
-        const V3 p = load3(pos, ph), d = load3(dir, ph);
-        auto cell = [&](float x, float o) {
-            const float u = (x - o) * inv_extent * 64.0f;
-            return (uint32_t)fminf(63.0f, fmaxf(0.0f, u));
-        };
-        const uint32_t m = spread3_6(cell(p.x, ox)) | (spread3_6(cell(p.y, oy)) << 1) | (spread3_6(cell(p.z, oz)) << 2);
-        // octahedral map of the direction to [0,1]^2, 6 bits each
-        const float l1 = fabsf(d.x) + fabsf(d.y) + fabsf(d.z);
-        float u = d.x / l1, v = d.y / l1;
-        if (d.z < 0.0f) {
-            const float uu = (1.0f - fabsf(v)) * (u >= 0.0f ? 1.0f : -1.0f);
-            const float vv = (1.0f - fabsf(u)) * (v >= 0.0f ? 1.0f : -1.0f);
-            u = uu; v = vv;
-        }
-        const uint32_t du = (uint32_t)fminf(63.0f, fmaxf(0.0f, (u * 0.5f + 0.5f) * 64.0f));
-        const uint32_t dv = (uint32_t)fminf(63.0f, fmaxf(0.0f, (v * 0.5f + 0.5f) * 64.0f));
-        key = (m << 12) | (du << 6) | dv;   // < 2^30 (NaN inputs land in some cell: harmless)
-    }
-    keys[t] = key;
-    vals[t] = (uint32_t)t;
 }
 
 // Two-level exclusive scan of the popcounts of nwords alive/selection masks.
@@ -3572,136 +3233,6 @@ __global__ __launch_bounds__(BLOCK) void scatter_queue_kernel(const unsigned lon
                 enrol_flat(fe.pos, fe.dir, pid, o - 1u, fe.hits, fe.flat_q, fe.flat_count, fe.flat_best, fe.rays,
                            fe.last_hit, o - 1u);
         }
-    }
-}
-
-// Walk-order carry (CHR_WALK_CARRY; fc->walk): the next step's ray records
-// follow THIS step's walk order restricted to the survivors, instead of the
-// next queue's order.  The binned first step walks rays of one direction cell
-// together; those photons hit the same patch of the detector and leave it in
-// similar directions, so the order stays coherent for the steps after it,
-// while the queue (photon.py:242-250 order, which fixes each photon's RNG slot)
-// stays as it is.  Same dispatches as without it: trace_kernel records each
-// queue position's walk position (winv), shade_kernel each walk position's
-// survival (walive, one byte), and the end-of-step scan and scatter below run
-// over both orders at once.  walk[j]: the queue position walked j-th (nullptr: j).
-__device__ __forceinline__ unsigned long long bytes_to_bits(uint4 v0, uint4 v1) {   // 16 bytes (0 / 1) -> 16 bits
-    const unsigned long long m = 0x0102040810204080ull;   // byte k (0 / 1) of x -> bit 56 + k of x * m
-    const unsigned long long a = ((unsigned long long)v0.y << 32) | v0.x, b = ((unsigned long long)v0.w << 32) | v0.z;
-    const unsigned long long c = ((unsigned long long)v1.y << 32) | v1.x, d = ((unsigned long long)v1.w << 32) | v1.z;
-    return ((a * m) >> 56) | (((b * m) >> 56) << 8) | (((c * m) >> 56) << 16) | (((d * m) >> 56) << 24);
-}
-// mask_block_scan_kernel over the queue masks and, from walive, the walk-order
-// survivor masks (wmasks) with their own word offsets / block sums
-__global__ __launch_bounds__(SCAN_WORDS) void mask_block_scan2_kernel(const unsigned long long *masks,
-                                                                      const uint8_t *walive, uint32_t n,
-                                                                      uint32_t *word_offsets, uint32_t *block_sums,
-                                                                      unsigned long long *wmasks, uint32_t *woffsets,
-                                                                      uint32_t *wsums, const uint32_t *dev_n,
-                                                                      const uint32_t *mode, uint32_t skip) {
-    __shared__ uint32_t tot[2][SCAN_WORDS / 64];
-    if (mode && (*mode == STEP_IDLE || *mode == skip)) return;
-    if (dev_n) n = *dev_n - 1u;
-    const uint32_t nwords = (n + 63u) / 64u;
-    const uint32_t w = blockIdx.x * SCAN_WORDS + threadIdx.x;
-    const uint32_t c = w < nwords ? (uint32_t)__popcll(masks[w]) : 0u;
-    unsigned long long wm = 0ull;
-    if (w < nwords) {   // 64 survival bytes (the last word's bytes past n: cleared)
-        const uint4 *src = reinterpret_cast<const uint4 *>(walive + 64 * (size_t)w);
-        wm = bytes_to_bits(src[0], src[1]) | (bytes_to_bits(src[2], src[3]) << 32);
-        if (64u * w + 64u > n) wm &= (1ull << (n - 64u * w)) - 1ull;
-        wmasks[w] = wm;
-    }
-    const uint32_t cw = (uint32_t)__popcll(wm);
-    uint32_t x = c, y = cw;
-    const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const uint32_t xu = __shfl_up(x, off, 64), yu = __shfl_up(y, off, 64);
-        if (lane >= off) { x += xu; y += yu; }
-    }
-    const int wid = threadIdx.x >> 6;
-    if (lane == 63) { tot[0][wid] = x; tot[1][wid] = y; }
-    __syncthreads();
-    uint32_t bx = 0, by = 0;
-    for (int k = 0; k < wid; ++k) { bx += tot[0][k]; by += tot[1][k]; }
-    if (w < nwords) { word_offsets[w] = bx + x - c; woffsets[w] = by + y - cw; }
-    if (threadIdx.x == SCAN_WORDS - 1) { block_sums[blockIdx.x] = bx + x; wsums[blockIdx.x] = by + y; }
-}
-// exclusive prefix of one block-sum array by a 1024-thread block (scan_block_sums_kernel's)
-__device__ __forceinline__ uint32_t block_prefix_1024(uint32_t *sums, uint32_t nblocks, uint32_t *partial) {
-    const uint32_t tid = threadIdx.x;
-    const uint32_t per = (nblocks + 1023) / 1024;
-    const uint32_t b0 = tid * per;
-    uint32_t sum = 0;
-    for (uint32_t k = 0; k < per && b0 + k < nblocks; ++k) sum += sums[b0 + k];
-    partial[tid] = sum;
-    __syncthreads();
-    for (uint32_t off = 1; off < 1024; off <<= 1) {
-        const uint32_t v = (tid >= off) ? partial[tid - off] : 0;
-        __syncthreads();
-        partial[tid] += v;
-        __syncthreads();
-    }
-    uint32_t run = partial[tid] - sum;
-    for (uint32_t k = 0; k < per && b0 + k < nblocks; ++k) {
-        const uint32_t v = sums[b0 + k];
-        sums[b0 + k] = run;
-        run += v;
-    }
-    const uint32_t total = partial[1023];
-    __syncthreads();
-    return total;
-}
-__global__ __launch_bounds__(1024) void scan_block_sums2_kernel(uint32_t *block_sums, uint32_t *wsums, uint32_t nblocks,
-                                                                uint32_t *out_counter, uint32_t *base, const uint32_t *mode,
-                                                                uint32_t skip) {
-    __shared__ uint32_t partial[1024];
-    if (mode && (*mode == STEP_IDLE || *mode == skip)) return;
-    const uint32_t total = block_prefix_1024(block_sums, nblocks, partial);
-    block_prefix_1024(wsums, nblocks, partial);
-    if (threadIdx.x == 1023) {
-        base[0] = out_counter[0];
-        out_counter[0] += total;
-    }
-}
-
-// The end-of-step scatter over both orders: per walk position j of a survivor,
-// its next queue position (the queue scan; out_queue[o] = photon id, as
-// scatter_queue_kernel writes it) and its next walk position jn (the walk
-// scan): the next step's ray record and flat-walk enrolment, walk_next[jn].
-// A multi-step tail slot (its alive bits are the tail kernel's; no walk order)
-// scatters in queue order as scatter_queue_kernel does.
-__global__ __launch_bounds__(BLOCK) void scatter_walk_kernel(const unsigned long long *masks, const uint32_t *word_offsets,
-                                                              const uint32_t *block_prefix, const uint32_t *base,
-                                                              const unsigned long long *wmasks, const uint32_t *woffsets,
-                                                              const uint32_t *wprefix, const uint32_t *walk,
-                                                              const uint32_t *in_queue, uint32_t n, uint32_t *out_queue,
-                                                              uint32_t *walk_next, FlatEnrol fe, const uint32_t *dev_n,
-                                                              const uint32_t *mode, uint32_t skip) {
-    if (mode && (*mode == STEP_IDLE || *mode == skip)) return;
-    if (dev_n) n = *dev_n - 1u;
-    const bool by_walk = !mode || *mode == STEP_ONE;
-    for (uint32_t j = blockIdx.x * BLOCK + threadIdx.x; j < n; j += gridDim.x * BLOCK) {
-        uint32_t p = j, jn = 0;
-        if (by_walk) {
-            const unsigned long long wm = wmasks[j >> 6];
-            const uint32_t lj = j & 63u;
-            if (!((wm >> lj) & 1ull)) continue;
-            jn = word_offset(woffsets, wprefix, j >> 6) + (uint32_t)__popcll(wm & ((1ull << lj) - 1ull));
-            p = walk ? walk[j] : j;
-        }
-        const unsigned long long m = masks[p >> 6];
-        if (!by_walk && !((m >> (p & 63u)) & 1ull)) continue;
-        const uint32_t o = base[0] + word_offset(word_offsets, block_prefix, p >> 6) +
-                           (uint32_t)__popcll(m & ((1ull << (p & 63u)) - 1ull));
-        const uint32_t pid = in_queue[p];
-        out_queue[o] = pid;
-        // out_queue[0] is the count header: queue position o - 1
-        if (by_walk) walk_next[jn] = o - 1u;
-        if (fe.pos)
-            enrol_flat(fe.pos, fe.dir, pid, o - 1u, fe.hits, fe.flat_q, fe.flat_count, fe.flat_best, fe.rays, fe.last_hit,
-                       by_walk ? jn : o - 1u);
     }
 }
 
@@ -4014,33 +3545,19 @@ static size_t sort_temp_bytes16(uint32_t n, int bits = 24) {
                                     (const uint32_t *)nullptr, (uint32_t *)nullptr, n, 0, bits);
     return bytes;
 }
-// CHR_BIN_KEY=0..5: direction-binning keys of row-major 8+8-bit octahedral cells (0), in
-// Morton order of 8+8 / 10+10 / 11+11 / 12+12-bit cells (1..4), or of 11+11-bit cells in
-// Hilbert order (5).  Morton 11+11: the binned first launch 5.0 -> 4.63 ms (10 M rays of the
-// 29k bench), 490.3 -> 495.6 M/s (r04 ab15/ab16): a wave's 64 rays come from a compact
-// patch of directions instead of a 0.5-degree cell's ~150 rays in queue order.  Hilbert
-// (default): 4.60 -> 4.55 ms, 498.8 -> 500.3 M/s (ab18).  Photons identical in all.
-static uint32_t bin_key_mode() {
-    const char *e = getenv("CHR_BIN_KEY");
-    const int k = e ? atoi(e) : 5;
-    return (uint32_t)(k >= 0 && k <= 5 ? k : 5);
-}
-static size_t sort_temp_bytes(uint32_t n) {
-    size_t bytes = 0;
-    (void)rocprim::radix_sort_pairs((void *)nullptr, bytes, (const uint32_t *)nullptr, (uint32_t *)nullptr,
-                              (const uint32_t *)nullptr, (uint32_t *)nullptr, n, 0, 30);
-    return bytes;
-}
-
+// The first step's direction-binning sort: keys of 11+11-bit octahedral cells in
+// Hilbert order (octa_cell).  r04 ab15/ab16/ab18 (29k bench, 10 M rays): the binned
+// first launch 5.01 ms with r01-r03's 8+8-bit row-major cells, 4.63 with 11+11-bit
+// Morton cells, 4.55 with Hilbert order (490.3 -> 500.3 M/s); photons identical.
+constexpr int BIN_KEY_BITS = 22;
 // u32 words: [0..15] counters | masks (2 per 64 slots) | offsets (1 per 64) |
-// block prefixes (1 per 256 words, +2) | sort keys in/out + order in/out (n each) |
-// rocprim sort temporary storage
+// block prefixes (1 per 256 words, +2)
 static uint64_t mask_scan_words(uint64_t n) {   // masks + offsets + block prefixes for n positions
     const uint64_t nwords = (n + 63) / 64;
     return 2 * nwords + nwords + scan_blocks((uint32_t)nwords) + 2;
 }
 extern "C" uint64_t chr_propagate_scratch_words(uint32_t nthreads) {
-    return 16 + mask_scan_words(nthreads) + 4 * (uint64_t)nthreads + 64 + (sort_temp_bytes(nthreads) + 3) / 4;
+    return 16 + mask_scan_words(nthreads) + 64;
 }
 
 // Kernel variants (CHR_PROPAGATE_VARIANT=<n>, read per launch so one process
@@ -4049,7 +3566,7 @@ extern "C" uint64_t chr_propagate_scratch_words(uint32_t nthreads) {
 // section 5 and profiles/r01/ab_*.log.
 //   0  default.  One-step launches: trace_kernel (BVH walk, first step's rays
 //      binned by direction) + shade_kernel<3>; multi-step launches (the tail):
-//      propagate_group_kernel (8 lanes per photon).
+//      propagate_tail_kernel (wave-adaptive walk, 8 lanes of physics per photon).
 //   5  counting form of 0 (bench: node/triangle counts of the walk); its
 //      multi-step launches run the counting fused kernel.
 //   1  exact-order walk of the reference BVH (fused step kernel).
@@ -4062,85 +3579,23 @@ typedef void (*propagate_fn)(const DevGeom *, PropagateArgs);
 static constexpr int kWalk = 2006;        // speculative wide walk, triangle steps at 6/8 of the live lanes
 static constexpr int kWalkSched = 1002;   // scheduled wide walk, triangle batch 2
 static constexpr int kExactVariant = 1;
-// the tail's group kernel at 4 waves/SIMD: it spills ~67 VGPRs to scratch
-// there, but at 2 waves/SIMD (no spills) the tail ran 2-3x longer (r02 rocprof:
-// a tail launch is up to 65,536 photons x 8 lanes = 8,192 waves, and the
-// launch lasts as long as its longest-lived photon, so fewer resident waves
-// means more rounds of waves behind it)
-static constexpr int kGroupWaves = 4;
 // propagate_tail_kernel (wave-adaptive walk) at 2 waves/SIMD: ~200 VGPRs, no
 // spills, no private segment.  r03 A/B on the 29k bench (profiles/r03/ab3, same
 // batches and RNG for every configuration): the long-lived photon's step 26.7 ->
 // 21.5 us, mean tail 7.31 -> 6.64 ms against 3 waves/SIMD (168 VGPRs, 51 spilled
 // once the GS = 64 walk was added); r02 measured 3 waves ahead of 4 (64 spills).
 static constexpr int kTailWaves = 2;
-static int tail_waves() {              // CHR_TAIL_WAVES=4: the tail kernel at 4 waves/SIMD (A/B)
-    const char *e = getenv("CHR_TAIL_WAVES");
-    return e ? atoi(e) : kTailWaves;
-}
 // The shade and tail kernels copy the physics tables into LDS (phys_cache): r03
-// ab16, 29k bench, 450.7 -> 461.7 M/s, mean tail 6.36 -> 6.06 ms.  CHR_PHYS_LDS=0:
-// the tables read from global memory (A/B).
-static bool phys_lds_enabled() {
-    const char *e = getenv("CHR_PHYS_LDS");
-    return !(e && e[0] == '0');
-}
-// CHR_TAIL_TOP=0: the tail's walks read every node from global memory instead of
-// the top of the tree from LDS (stage_top; A/B)
-static uint32_t tail_top_nodes() {
-    const char *e = getenv("CHR_TAIL_TOP");
-    return (e && e[0] == '0') ? 0u : TOP_NODES;
-}
-// CHR_SHADE_PREFETCH2=0: the shade kernel reads the next photon's queue entry
-// right before its state (one dependent load per photon) instead of an iteration
-// ahead (A/B)
-static bool shade_prefetch2() {
-    const char *e = getenv("CHR_SHADE_PREFETCH2");
-    return !(e && e[0] == '0');
-}
-// CHR_SHADE_SC=0: the shade kernel's prefetch and write-back under branches (the
-// per-iteration wait for its own stores, shade_kernel SC) (A/B)
-static bool shade_static_counts() {
-    const char *e = getenv("CHR_SHADE_SC");
-    return !(e && e[0] == '0');
-}
-static int shade_waves() {             // CHR_SHADE_WAVES=2|4: the shade kernel at 2 / 4 waves per SIMD (A/B)
-    const char *e = getenv("CHR_SHADE_WAVES");
-    return e ? atoi(e) : 3;
-}
-static bool tail_group_walk() {        // CHR_TAIL=group: the fixed 8-lane group kernel (A/B)
-    const char *e = getenv("CHR_TAIL");
-    return e && std::strcmp(e, "group") == 0;
-}
-// CHR_TRACE_DRAIN=k: trace_kernel waves drain their last <= k walks whole-wave
-// (0 = off; A/B).  Default 4 (r03 ab3: trace ms per step 16.23 at 8, 15.92 at 2,
-// 15.90 at 4, 16.33 off): with <= 4 walks each gets >= 2 cursors.
-static uint32_t trace_drain_max() {
-    const char *e = getenv("CHR_TRACE_DRAIN");
-    const int k = e ? atoi(e) : 4;
-    return (uint32_t)(k < 0 ? 0 : (k > 8 ? 8 : k));
-}
-// CHR_TAIL_GS64=0: the tail's lone-walker walks through the generic segment
-// walk (run-time width) instead of its GS = 64 specialisation (A/B)
-static bool tail_gs64() {
-    const char *e = getenv("CHR_TAIL_GS64");
-    return !(e && e[0] == '0');
-}
-// CHR_TAIL_LONE=0: the lone walker walks with walk_segment<64> instead of the
-// software-pipelined walk_lone (A/B)
-static bool tail_lone() {
-    const char *e = getenv("CHR_TAIL_LONE");
-    return !(e && e[0] == '0');
-}
-// CHR_TAIL_PRIO=0: the batches' overlapped tail kernel at normal wave priority (A/B)
-static bool tail_prio() {
-    const char *e = getenv("CHR_TAIL_PRIO");
-    return !(e && e[0] == '0');
-}
+// ab16, 29k bench, 450.7 -> 461.7 M/s, mean tail 6.36 -> 6.06 ms.  The tail kernel's
+// walks read the top of the tree from LDS (stage_top): walk 16.4 -> 16.0 us per step
+// of the long-lived photon (r04 ab1).  The shade kernel reads queue entries two ahead
+// and never waits for its own write-back (shade_kernel, r04 ab9/ab10).  A wave of the
+// tail kernel with one walking photon walks it with walk_lone (r04 §10.1: 474.6 ->
+// 489.4 M/s against walk_segment<64>), as does a trace wave draining one walk.
+// trace_kernel waves drain their last <= 4 walks whole-wave (r03 ab3: trace ms per
+// step 16.23 at 8, 15.92 at 2, 15.90 at 4, 16.33 off): each then has >= 2 cursors.
 static bool wide_queue_ok(const chr_geometry *g) { return g->dev.nwtri < (1u << 30); }   // 30-bit leaf queue entries
 
-// one launch per chunk (the reference's launch structure: slot counts that are
-// not a multiple of 64, or CHR_STEP_LAUNCH=0)
 // whether this call's kernels walk the reference BVH (its nodes must be resident)
 static bool walks_reference_bvh(const chr_geometry *g) {
     const char *e = getenv("CHR_PROPAGATE_VARIANT");
@@ -4175,64 +3630,14 @@ struct StepVariant {
 // (demo.detector(), 4M photons: first-step walk 2.65 -> 2.21 ms for 0.11 ms of
 // sorting; second step unchanged).
 static constexpr uint32_t kBinFirstMin = 1u << 20;
-// CHR_TRACE_AHEAD=1: trace_kernel takes rays from chunks of the ray counter
-// claimed ahead (the next chunk's atomic in flight while the wave walks) instead
-// of one blocking atomic per refill.  Off: measured slower (r03 ab5: trace 17.63
-// -> 18.36 ms per step; the binned first launch 5.33 -> 5.60 ms).
-// A trace launch with fewer rays than the grid's lanes hands each wave its share
-// (ceil(rays / waves)) instead of 64 rays: the small late launches spread their
-// walks over every wave and reach the drain sooner.  r03 ab24/ab25 (same batches,
-// photons identical): trace 14.40 -> 14.32 ms per step, the last launches 0.39 -> 0.37
-// ms.  CHR_TRACE_SPREAD=0: 64 per wave (A/B).
-static bool trace_spread() {
-    const char *e = getenv("CHR_TRACE_SPREAD");
-    return !(e && e[0] == '0');
-}
-// CHR_TRACE_DRAIN_LONE=0: a wave draining one walk uses walk_segment<0> (A/B)
-static bool trace_drain_lone() {
-    const char *e = getenv("CHR_TRACE_DRAIN_LONE");
-    return !(e && e[0] == '0');
-}
-static bool trace_claim_ahead() {
-    const char *e = getenv("CHR_TRACE_AHEAD");
-    return e && e[0] == '1';
-}
-// CHR_PREFIX_GRID=k: the prefix walk's persistent grid is 1/k of the full one (default 1; A/B)
-static uint32_t prefix_grid_div() {
-    const char *e = getenv("CHR_PREFIX_GRID");
-    const int k = e ? atoi(e) : 1;
-    return (uint32_t)(k < 1 ? 1 : (k > 16 ? 16 : k));
-}
-// CHR_TRACE_R=16|32|48: trace_kernel refills once that many of a wave's 64
-// lanes are without a ray (A/B).  Default 48 (r03 ab3: trace ms per step 17.87 at
-// 16, 16.25 at 32, 15.81 at 48; the binned first launch 5.74 -> 5.33 ms: its
-// coherent rays walk in phase, and fewer, larger refills keep them so).
-static int trace_refill_r() {
-    const char *e = getenv("CHR_TRACE_R");
-    return e ? atoi(e) : 48;
-}
-// CHR_TRACE_LAYOUT (A/B): 0 256-thread workgroups, 12 LDS stack entries per lane;
-// 1 1024-thread workgroups (one per CU), 11 entries, the top TOP_NODES nodes of
-// the tree in LDS (stage_top); 2 the same without the top nodes (control).
-// (r04 ab12: refill threshold R = 56 / 64 trace 14.45 / 17.36 ms per step against
-// 14.06 at 48; the node / triangle threshold F = 5 / 7 14.03 / 14.42 against 14.06 at 6)
-// (r04 ab11, removed: each lane holding its next ray's record in registers, started
-// as soon as its walk ends, records claimed and loaded for R lanes at a time: every
-// launch 30-40% longer, trace 14.0 -> 18.3 ms per step -- lanes restarting one by one
-// break the cohorts of neighbouring rays that start and walk together.)
-// (r04 ab7, removed: the per-child offsets derived from the kind bytes by byte-wise
-// prefix sums instead of loaded -- five 16-byte node loads per node step, not six:
-// trace 14.16 vs 14.18 ms per step, 492.2 vs 491.7 M/s: the walk is not bound by
-// its load instruction count.)
-// (r04 ab6, removed: 5 waves per SIMD with 8 LDS stack entries per lane, 8 KB of LDS
-// per wave: trace 14.14 -> 14.97 ms per step, 492.8 -> 474 M/s.)
-// (r04 ab3, removed: a combined step -- every lane fetching its node AND its next
-// parked triangle each iteration -- ran trace 38.8 ms/step at 4 waves/SIMD (200 B
-// of spills) and 17.2 at 3, against 14.35 for the wave-wide node / triangle choice)
-static int trace_layout() {
-    const char *e = getenv("CHR_TRACE_LAYOUT");
-    return e ? atoi(e) : 0;
-}
+// Measured and removed (records in DESIGN 9-10): claim-ahead ray-counter chunks (r03
+// ab5, r04 ab14: slower, the counter is not contended), a 1024-thread trace layout with
+// the top of the tree in LDS (r04 ab1: no gain), refill thresholds other than 48 (r03
+// ab3: 17.87 at 16, 16.25 at 32, 15.81 ms per step at 48; r04 ab12: 14.45 at 56, 17.36
+// at 64), prefetched rays per lane (r04 ab11: every launch 30-40% longer), five node
+// loads instead of six (r04 ab7), 5 waves per SIMD (r04 ab6), a combined node + triangle
+// step (r04 ab3), the walk-order carry (r03 ab10/ab14, r04 ab17: the walk-order scatter
+// cost more than the walks gained), a coherence sort of every launch (r01).
 static StepVariant select_step_variant(const chr_geometry *g) {
     const char *e = getenv("CHR_PROPAGATE_VARIANT");
     int v = e ? atoi(e) : 0;
@@ -4257,35 +3662,14 @@ static StepVariant select_step_variant(const chr_geometry *g) {
             break;
         default:   // 0, 7, 8
             sv.fn = propagate_step_kernel<8, 4, kWalk>;
-            sv.trace = trace_refill_r() == 16 ? trace_kernel<false, 6, 12, 4, 16>
-                       : (trace_refill_r() == 32 ? trace_kernel<false, 6, 12, 4, 32> : trace_kernel<false, 6, 12, 4, 48>);
-            if (trace_refill_r() == 48) {
-                switch (trace_layout()) {
-                    case 1: sv.trace = trace_kernel<false, 6, 11, 4, 48, 1024, TOP_NODES>; sv.trace_block = 1024; break;
-                    case 2: sv.trace = trace_kernel<false, 6, 11, 4, 48, 1024, 0>; sv.trace_block = 1024; break;
-                    default: break;
-                }
-            }
-            sv.shade = shade_waves() == 4 ? shade_kernel<4>
-                       : (shade_waves() == 2 ? shade_kernel<2>
-                          : (shade_prefetch2() ? (shade_static_counts() ? shade_kernel<3, true, true> : shade_kernel<3, true>)
-                                               : shade_kernel<3>));
-            sv.tail = tail_group_walk() ? propagate_group_kernel<8, kGroupWaves>
-                      : (tail_waves() == 4 ? propagate_tail_kernel<4>
-                         : (tail_waves() == 3 ? propagate_tail_kernel<3> : propagate_tail_kernel<kTailWaves>));
+            sv.trace = trace_kernel<false, 6, 12, 4, 48>;
+            sv.shade = shade_kernel<3>;
+            sv.tail = propagate_tail_kernel<kTailWaves>;
             sv.tail_group = 8;
             sv.binned = v == 7 ? 1 : (v == 8 ? 0 : 2);
             break;
     }
     return sv;
-}
-
-static constexpr int32_t kSortMin = 16384;   // below this a launch is a few waves: no reordering
-static bool sort_enabled() {
-    // read per launch (A/B).  Default off: on demo.detector() the reordered
-    // walk was not faster and the sort costs ~3 ms per 4M photons (r01 A/B).
-    const char *e = getenv("CHR_SORT");
-    return e && e[0] == '1';
 }
 
 // scratch layout (u32 words): [0] overflows [1] queue base [2..11] u64 walk counters [12..15] pad; masks (u64, 8-aligned); offsets
@@ -4313,27 +3697,7 @@ static int launch_chunk(const chr_geometry *g, const chr_photons *ph, uint32_t *
     a.mode = nullptr;
     a.want = STEP_ONE;
     a.work = nullptr;
-    a.winv = nullptr;
-    a.walive = nullptr;
-    a.phys_lds = phys_lds_enabled() ? 1u : 0u;
-    a.top_nodes = tail_top_nodes();
     a.prio = 0;
-    if (sort_enabled() && nthreads >= kSortMin) {
-        // coherence order (sort_key_kernel): rays that start close together in
-        // similar directions share a wave
-        uint32_t *keys = bsums + scan_blocks(nwords) + 2;
-        uint32_t *keys_out = keys + nthreads, *vals = keys_out + nthreads, *vals_out = vals + nthreads;
-        void *temp = (void *)(((uintptr_t)(vals_out + nthreads) + 255) & ~(uintptr_t)255);
-        size_t temp_bytes = sort_temp_bytes((uint32_t)nthreads);
-        const float inv_extent = 1.0f / (g->dev.scale * 65536.0f);
-        hipLaunchKernelGGL(sort_key_kernel, dim3(grid_for(nthreads)), dim3(BLOCK), 0, stream, ph->d_pos, ph->d_dir,
-                           ph->d_flags, in_queue, first, nthreads, g->dev.ox, g->dev.oy, g->dev.oz, inv_extent, keys,
-                           vals);
-        CHR_HIP_CHECK(rocprim::radix_sort_pairs(temp, temp_bytes, keys, keys_out, vals, vals_out, (uint32_t)nthreads,
-                                                0, 30, stream));
-        CHR_HIP_CHECK(hipMemsetAsync(masks, 0, (size_t)nwords * 8, stream));
-        a.order = vals_out;
-    }
     if (ev0) CHR_HIP_CHECK(hipEventRecord(ev0, stream));
     hipLaunchKernelGGL(select_variant(g), dim3(grid_for(nthreads)), dim3(BLOCK), 0, stream,
                        (const DevGeom *)g->d_dev, a);
@@ -4375,14 +3739,6 @@ struct FlatCtx {
     // rays_walk the binned first step's records permuted into walk order
     uint4 *rays = nullptr, *rays_walk = nullptr;
     uint32_t cap = 0;                   // entries of flat_q / flat_best
-    // walk-order carry (walk_carry_enabled): walk[cur] the step's walk order
-    // (steps after the first), walk[cur ^ 1] the next step's; the walk-order
-    // survivor masks and their scan
-    uint32_t *walk[2] = {nullptr, nullptr};
-    unsigned long long *wmasks = nullptr;
-    uint32_t *woffsets = nullptr, *wprefix = nullptr;
-    uint32_t *winv = nullptr;   // queue position -> walk position (trace_kernel)
-    uint8_t *walive = nullptr;  // walk position -> survived the step (shade_kernel)
 };
 static int flat_get(uint32_t n, FlatCtx &fc, int ctx = 0) {
     static thread_local Scratch s[NCTX][16];
@@ -4414,30 +3770,11 @@ static bool trace_steps();
 // "1" every slot's events as well (kernel_ms, tail_ms, the prefix split);
 // "0" only the events the streams and the host synchronise on.  Times not
 // recorded read 0 in chr_propagate_stats.
-// CHR_HEAD_FOLD=0: every device-driven slot launches its own head kernel instead of
-// the previous slot's block-sum scan running it (A/B)
-static bool head_fold_enabled() {
-    const char *e = getenv("CHR_HEAD_FOLD");
-    return !(e && e[0] == '0');
-}
 static int slot_timing() {
     const char *e = getenv("CHR_SLOT_TIMING");
     if (!e || e[0] == 't') return 1;
     if (e[0] == '0') return 0;
     return 2;
-}
-// CHR_WALK_CARRY=1: later steps walk their rays in the previous step's walk
-// order (the binned first step's, restricted to survivors) instead of queue
-// order (walk_masks_kernel / scatter_walk_kernel; A/B, read per launch)
-static bool walk_carry_enabled() {
-    const char *e = getenv("CHR_WALK_CARRY");
-    return e && e[0] == '1';
-}
-// CHR_TRACE_RAYS=0: trace_kernel refills from the photon arrays through the
-// queue (the r02 path) instead of the ray records (A/B; read per launch)
-static bool trace_rays_enabled() {
-    const char *e = getenv("CHR_TRACE_RAYS");
-    return !(e && e[0] == '0');
 }
 // A device-driven step slot (chr_propagate without a host round trip per
 // step): the slot's kernels read the queue length from the input queue's
@@ -4464,10 +3801,6 @@ struct SlotCtl {
     // (head, flat-walk classification, binning, the BVH walk: no random numbers)
     // on the prefix stream, ending with prefix_done; PHASE_REST (shade pass on)
     // on the batch stream after prefix_done, starting with ev_rest0
-    // The prefix itself may be queued in two parts (PHASE_BIN: head, classification,
-    // binning; PHASE_TRACE: the walk), the binning early, while the previous batch
-    // still runs its one-step slots (the binning's sort otherwise waits behind the
-    // previous tail's first waves for CUs).  ev_bin_end: after the binning.
     int phase = 0;
     int ctx = 0;                      // buffer context (walk-stack column)
     uint32_t *host_ring = nullptr;    // pinned (mode, length) words the head kernel writes (nullptr: none)
@@ -4476,9 +3809,9 @@ struct SlotCtl {
     // filled by launch_step
     bool fold_head = false;
     HeadNext next_head{nullptr, nullptr, nullptr, nullptr, nullptr, 0u, 0u, 0, 0};
-    hipEvent_t prefix_done = nullptr, ev_rest0 = nullptr, ev_bin_end = nullptr;
+    hipEvent_t prefix_done = nullptr, ev_rest0 = nullptr;
 };
-constexpr int PHASE_ALL = 0, PHASE_PREFIX = 1, PHASE_REST = 2, PHASE_BIN = 3, PHASE_TRACE = 4;
+constexpr int PHASE_ALL = 0, PHASE_PREFIX = 1, PHASE_REST = 2;
 
 // The wave-adaptive tail kernel as one resident grid whose photon groups take
 // queue positions from a counter (PropagateArgs::work; the slot's ray counter,
@@ -4487,41 +3820,19 @@ constexpr int PHASE_ALL = 0, PHASE_PREFIX = 1, PHASE_REST = 2, PHASE_BIN = 3, PH
 // the slot count; not use_weights, whose tail takes any length).  r03 ab11, 29k
 // bench: 440.4 -> 450.3 M/s (mean tail 6.93 -> 6.65 ms, kernel time per step
 // 29.98 -> 28.37 ms).  CHR_TAIL_WQ=0: one group per slot, as many waves as
-// photons / 8 (A/B).
+// photons / 8.
 static bool tail_work_queue(const StepVariant &sv, const SlotCtl *sc, int32_t use_weights, uint32_t cap) {
-    const char *e = getenv("CHR_TAIL_WQ");
-    return !(e && e[0] == '0') && sv.tail_group == 8 && sc && !use_weights && sc->tail_below <= cap;
+    return sv.tail_group == 8 && sc && !use_weights && sc->tail_below <= cap;
 }
 // blocks of a tail launch: every slot's group, or (work queue) the resident grid
 static unsigned tail_grid(const StepVariant &sv, uint32_t threads, bool work_queue) {
     const unsigned full = grid_for((uint64_t)threads * sv.tail_group);
     if (!work_queue) return full;
     const int cus = device_cus();
-    const unsigned resident = (unsigned)std::max(1, cus) * (unsigned)tail_waves() * 4u * 64u / BLOCK;
+    const unsigned resident = (unsigned)std::max(1, cus) * (unsigned)kTailWaves * 4u * 64u / BLOCK;
     return std::max(1u, std::min(full, resident));
 }
 
-// The walk-order carry's end of step: the survivor scan of both orders and the
-// scatter in walk order (mask_block_scan2 / scan_block_sums2 / scatter_walk,
-// the same three dispatches as launch_mask_scan + scatter_queue_kernel).
-// skip: the mode that leaves no queue.
-static void launch_carry_scatter(const FlatCtx *fc, const unsigned long long *masks, uint32_t *offsets, uint32_t *bsums,
-                                 uint32_t *out_queue, uint32_t *base, const uint32_t *in_queue, uint32_t n,
-                                 const uint32_t *walk_cur, uint32_t *walk_next, const FlatEnrol &fe, hipStream_t stream,
-                                 const uint32_t *dev_n, const uint32_t *mode, uint32_t skip, bool grid_stride) {
-    const uint32_t nb = scan_blocks((n + 63) / 64);
-    if (nb)
-        hipLaunchKernelGGL(mask_block_scan2_kernel, dim3(nb), dim3(SCAN_WORDS), 0, stream, masks, fc->walive, n, offsets,
-                           bsums, fc->wmasks, fc->woffsets, fc->wprefix, dev_n, mode, skip);
-    hipLaunchKernelGGL(scan_block_sums2_kernel, dim3(1), dim3(1024), 0, stream, bsums, fc->wprefix, nb, out_queue, base,
-                       mode, skip);
-    const unsigned grid = grid_stride ? std::min<uint32_t>(4096u, grid_for(n)) : grid_for(n);
-    hipLaunchKernelGGL(scatter_walk_kernel, dim3(std::max(1u, grid)), dim3(BLOCK), 0, stream, masks, offsets, bsums, base,
-                       fc->wmasks, fc->woffsets, fc->wprefix, walk_cur, in_queue, n, out_queue, walk_next, fe, dev_n,
-                       mode, skip);
-}
-
-// hits: n (triangle, distance) slots + a ray counter word, for the split path
 static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *rng, uint32_t nslots, uint32_t cap,
                        uint32_t n, const uint32_t *in_queue, uint32_t *out_queue, int32_t max_steps,
                        int32_t use_weights, int32_t scatter_first, uint32_t *scratch, hipStream_t stream,
@@ -4550,16 +3861,8 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
     a.mode = mode;
     a.want = STEP_ONE;
     a.work = nullptr;
-    a.winv = nullptr;
-    a.walive = nullptr;
-    a.phys_lds = phys_lds_enabled() ? 1u : 0u;
-    a.top_nodes = tail_top_nodes();
     a.prio = 0;
     FlatEnrol fe{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
-    // walk-order carry: this step's walk order (nullptr: queue order) and the next step's
-    bool carry = false;
-    const uint32_t *walk_cur = nullptr;
-    uint32_t *walk_next = nullptr;
     const uint32_t threads = std::min(cap, (n + 63u) & ~63u);
     const StepVariant sv = select_step_variant(g);
     // host-driven: the split when this launch is one step; device-driven: the
@@ -4571,10 +3874,9 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
     uint32_t *next = split ? (uint32_t *)(hits + (sc ? sc->n_layout : n)) : nullptr;
     const int phase = sc ? sc->phase : PHASE_ALL;
     const bool pre = phase != PHASE_REST, rest = phase == PHASE_ALL || phase == PHASE_REST;
-    const bool do_bin = pre && phase != PHASE_TRACE, do_trace = pre && phase != PHASE_BIN;
-    if (phase != PHASE_ALL && (!split || (phase != PHASE_BIN && !sc->prefix_done)))
+    if (phase != PHASE_ALL && (!split || !sc->prefix_done))
         return chr::fail(CHR_ERR_INVALID, "launch_step: a split slot needs the split path and its prefix event");
-    if (ev0 && do_bin) CHR_HIP_CHECK(hipEventRecord(ev0, stream));
+    if (ev0 && pre) CHR_HIP_CHECK(hipEventRecord(ev0, stream));
     if (!pre) {
         CHR_HIP_CHECK(hipStreamWaitEvent(stream, sc->prefix_done, 0));
         if (sc->ev_rest0) CHR_HIP_CHECK(hipEventRecord(sc->ev_rest0, stream));
@@ -4586,7 +3888,7 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
         hn.ray_counter = next;
     }
     const HeadNext *hnp = hn.mode ? &hn : nullptr;
-    if (sc && do_bin && !(sc->fold_head && !first_step)) {
+    if (sc && pre && !(sc->fold_head && !first_step)) {
         if (!next) return chr::fail(CHR_ERR_INVALID, "launch_step: device-driven steps need the split path");
         hipLaunchKernelGGL(step_head_kernel, dim3(1), dim3(64), 0, stream, in_queue - 1, out_queue, sc->mode, sc->nk,
                            sc->done, next, sc->tail_below, sc->remaining, use_weights, sc->n_layout, sc->host_ring);
@@ -4600,18 +3902,16 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
         // (device-driven slots bin only the first step, whose length the host knows)
         const bool binned = (sv.binned == 1 || (sv.binned == 2 && first_one_step && n >= kBinFirstMin)) &&
                             (!sc || first_one_step);
-        const bool bin_now = binned && do_bin;
+        const bool bin_now = binned && pre;
         uint32_t *keys = next + 16, *order = keys + n;
         // ray records: the first step's from its classification, later steps' from
         // the previous step's scatter (enrol_next)
-        const bool use_rays = fc->rays && trace_rays_enabled() && (first_one_step || fc->enrol_next);
-        // the carry needs records for this step and the next (they hold the queue positions)
-        carry = use_rays && fc->enrol_next && fc->walk[0] && fc->winv && walk_carry_enabled();
-        if (first_one_step && do_bin)   // flat walks of the initial queue (later steps: enrolled by the previous scatter)
+        const bool use_rays = fc->rays && (first_one_step || fc->enrol_next);
+        if (first_one_step && pre)   // flat walks of the initial queue (later steps: enrolled by the previous scatter)
             hipLaunchKernelGGL(classify_kernel, dim3(grid_for(n)), dim3(BLOCK), 0, stream, ph->d_pos, ph->d_dir,
                                ph->d_flags, ph->d_last_hit_triangles, in_queue, n, hits, fc->flat_q, count_cur,
                                fc->flat_best, bin_now ? keys : nullptr, bin_now ? order : nullptr,
-                               use_rays ? fc->rays : nullptr, bin_key_mode());
+                               use_rays ? fc->rays : nullptr);
         TraceArgs ta;
         ta.pos = ph->d_pos; ta.dir = ph->d_dir; ta.flags = ph->d_flags; ta.last_hit = ph->d_last_hit_triangles;
         ta.queue = in_queue; ta.n = n; ta.hits = hits; ta.next = next; ta.counters = counters; ta.order = nullptr;
@@ -4620,19 +3920,12 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
         ta.flat_q = fc->flat_q; ta.flat_count = count_cur; ta.flat_best = fc->flat_best; ta.diag = fc->ctl + 3;
         ta.dev_n = dev_n;
         ta.mode = mode;
-        ta.drain_max = trace_drain_max();
-        ta.claim_ahead = trace_claim_ahead() ? 1u : 0u;
-        ta.spread = trace_spread() ? 1u : 0u;
-        ta.drain_lone = trace_drain_lone() ? 1u : 0u;
-        ta.winv = carry ? fc->winv : nullptr;
-        a.winv = carry ? fc->winv : nullptr;
-        a.walive = carry ? fc->walive : nullptr;
         a.flat_best = fc->flat_best;
         a.zero_word = count_next;   // cleared by the shade pass, filled by this step's scatter
         if (fc->enrol_next)
-            fe = FlatEnrol{ph->d_pos, ph->d_dir, hits, fc->flat_q, count_next, fc->flat_best,
-                           (fc->rays && trace_rays_enabled()) ? fc->rays : nullptr, ph->d_last_hit_triangles};
-        if (trace_steps() && do_trace) {   // debugging: per-walk cost histogram (counting variants), printed per step
+            fe = FlatEnrol{ph->d_pos, ph->d_dir, hits, fc->flat_q, count_next, fc->flat_best, fc->rays,
+                           ph->d_last_hit_triangles};
+        if (trace_steps() && pre) {   // debugging: per-walk cost histogram (counting variants), printed per step
             ta.walk_hist = next + 16 + 2 * (size_t)(sc ? sc->n_layout : n);
             CHR_HIP_CHECK(hipMemsetAsync(ta.walk_hist, 0, 34 * 4, stream));
         }
@@ -4641,12 +3934,11 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
             if (bin_now) {
                 if (!first_one_step)   // the first step's keys came with its classification
                     hipLaunchKernelGGL(bin_key_kernel, dim3(grid_for(n)), dim3(BLOCK), 0, stream, ph->d_dir, in_queue,
-                                       n, keys, order, bin_key_mode());
+                                       n, keys, order);
                 void *temp = (void *)(((uintptr_t)(vals_out + n) + 255) & ~(uintptr_t)255);
-                const int kbits = bin_key_mode() == 5 ? 22 : (bin_key_mode() >= 2 ? 16 + 2 * (int)bin_key_mode() : 16);
-                size_t temp_bytes = sort_temp_bytes16(n, kbits);
-                CHR_HIP_CHECK(rocprim::radix_sort_pairs(temp, temp_bytes, keys, keys_out, order, vals_out, n, 0, kbits,
-                                                        stream));
+                size_t temp_bytes = sort_temp_bytes16(n, BIN_KEY_BITS);
+                CHR_HIP_CHECK(rocprim::radix_sort_pairs(temp, temp_bytes, keys, keys_out, order, vals_out, n, 0,
+                                                        BIN_KEY_BITS, stream));
                 if (use_rays)   // the records in the binned walk order
                     hipLaunchKernelGGL(permute_rays_kernel, dim3(grid_for(n)), dim3(BLOCK), 0, stream, fc->rays,
                                        vals_out, n, fc->rays_walk);
@@ -4654,28 +3946,11 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
             ta.order = vals_out;
             if (use_rays) ta.rays = fc->rays_walk;
         }
-        if (carry) {
-            // the first step's walk order: the binning's (queue order unbinned); later
-            // steps' (steps after the first): the previous step's scatter_walk_kernel output.  A first
-            // step that is the multi-step tail (host-driven propagate: it is compacted too)
-            // walked in queue order
-            walk_cur = first_step ? (first_one_step && binned ? ta.order : nullptr) : fc->walk[fc->cur];
-            walk_next = fc->walk[fc->cur ^ 1];
-        }
-        if (do_bin && sc && sc->ev_bin_end) CHR_HIP_CHECK(hipEventRecord(sc->ev_bin_end, stream));
-        if (phase == PHASE_BIN) {
-            CHR_HIP_CHECK(hipGetLastError());
-            return CHR_OK;
-        }
-        if (do_trace) {
+        if (pre) {
             const int cus = device_cus();
             if (cus <= 0) return chr::fail(CHR_ERR_HIP, "launch_step: no compute units");
             const int tb = sv.trace_block;
-            uint64_t resident = (uint64_t)cus * 4 * sv.trace_waves * 64 / tb;   // persistent grid
-            // a batch's prefix walk (chr_propagate_batches) runs beside the previous
-            // batch's kernels: CHR_PREFIX_GRID=1/k of the grid leaves them CUs (A/B)
-            if (phase == PHASE_PREFIX || phase == PHASE_TRACE)
-                resident = std::max<uint64_t>(1, resident / prefix_grid_div());
+            const uint64_t resident = (uint64_t)cus * 4 * sv.trace_waves * 64 / tb;   // persistent grid
             const uint32_t blocks = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(resident, ((uint64_t)n + tb - 1) / tb));
             if (int rc = walk_stack_get((size_t)WIDE_STACK * blocks * tb * sizeof(uint2), &ta.spill, sc ? sc->ctx : 0))
                 return rc;
@@ -4718,7 +3993,7 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
         hipLaunchKernelGGL(clear_masks_kernel, dim3(std::min<uint32_t>(kClearBlocks, grid_for(nwords))), dim3(BLOCK), 0, ts,
                            sc->tail_masks, dev_n, mode);
         PropagateArgs at = a;
-        at.prio = (tail_prio() ? 1u : 0u) | (tail_gs64() ? 2u : 0u) | (tail_lone() ? 4u : 0u);
+        at.prio = 1u;
         at.alive_masks = sc->tail_masks;
         at.max_steps = sc->remaining;
         at.want = STEP_TAIL;
@@ -4726,16 +4001,11 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
         hipLaunchKernelGGL(sv.tail, dim3(tail_grid(sv, threads, at.work != nullptr)), dim3(BLOCK), 0, ts,
                            (const DevGeom *)g->d_dev, at, cap);
         if (sc->evt_tail1) CHR_HIP_CHECK(hipEventRecord(sc->evt_tail1, ts));
-        if (carry) {
-            launch_carry_scatter(fc, masks, offsets, bsums, out_queue, counters + 1, in_queue, n, walk_cur, walk_next, fe,
-                                 stream, dev_n, mode, STEP_TAIL, true);
-        } else {
-            launch_mask_scan(masks, nwords, offsets, bsums, out_queue, counters + 1, nullptr, stream, dev_n, mode,
-                             STEP_TAIL, hnp);
-            hipLaunchKernelGGL(scatter_queue_kernel, dim3(std::min<uint32_t>(4096u, grid_for(n))), dim3(BLOCK), 0,
-                               stream, masks, offsets, bsums, counters + 1, in_queue, 0, (int32_t)n, out_queue, fe,
-                               dev_n, mode, STEP_TAIL);
-        }
+        launch_mask_scan(masks, nwords, offsets, bsums, out_queue, counters + 1, nullptr, stream, dev_n, mode, STEP_TAIL,
+                         hnp);
+        hipLaunchKernelGGL(scatter_queue_kernel, dim3(std::min<uint32_t>(4096u, grid_for(n))), dim3(BLOCK), 0, stream,
+                           masks, offsets, bsums, counters + 1, in_queue, 0, (int32_t)n, out_queue, fe, dev_n, mode,
+                           STEP_TAIL);
         CHR_HIP_CHECK(hipGetLastError());
         return CHR_OK;
     }
@@ -4745,7 +4015,6 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
         else CHR_HIP_CHECK(hipMemsetAsync(masks, 0, (size_t)nwords * 8, stream));
         a.max_steps = sc ? sc->remaining : max_steps;
         a.want = STEP_TAIL;
-        a.prio = (tail_gs64() ? 2u : 0u) | (tail_lone() ? 4u : 0u);
         a.work = (sc && next && tail_work_queue(sv, sc, use_weights, cap)) ? next : nullptr;
         hipLaunchKernelGGL(sv.tail, dim3(tail_grid(sv, threads, a.work != nullptr)), dim3(BLOCK), 0, stream,
                            (const DevGeom *)g->d_dev, a, cap);
@@ -4753,16 +4022,10 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
         hipLaunchKernelGGL(sv.fn, dim3(grid_for(threads)), dim3(BLOCK), 0, stream, (const DevGeom *)g->d_dev, a, cap);
     }
     if (ev1) CHR_HIP_CHECK(hipEventRecord(ev1, stream));
-    if (carry) {
-        launch_carry_scatter(fc, masks, offsets, bsums, out_queue, counters + 1, in_queue, n, walk_cur, walk_next, fe,
-                             stream, dev_n, mode, STEP_IDLE, sc != nullptr);
-    } else {
-        launch_mask_scan(masks, nwords, offsets, bsums, out_queue, counters + 1, nullptr, stream, dev_n, mode, STEP_IDLE,
-                         hnp);
-        hipLaunchKernelGGL(scatter_queue_kernel, dim3(sc ? std::min<uint32_t>(4096u, grid_for(n)) : grid_for(n)),
-                           dim3(BLOCK), 0, stream, masks, offsets, bsums, counters + 1, in_queue, 0, (int32_t)n,
-                           out_queue, fe, dev_n, mode, STEP_IDLE);
-    }
+    launch_mask_scan(masks, nwords, offsets, bsums, out_queue, counters + 1, nullptr, stream, dev_n, mode, STEP_IDLE, hnp);
+    hipLaunchKernelGGL(scatter_queue_kernel, dim3(sc ? std::min<uint32_t>(4096u, grid_for(n)) : grid_for(n)), dim3(BLOCK),
+                       0, stream, masks, offsets, bsums, counters + 1, in_queue, 0, (int32_t)n, out_queue, fe, dev_n,
+                       mode, STEP_IDLE);
     CHR_HIP_CHECK(hipGetLastError());
     return CHR_OK;
 }
@@ -4865,18 +4128,14 @@ static int prop_bufs(uint32_t nphotons, int32_t ntpb, int32_t max_blocks, int ct
     b.cap = (uint64_t)ntpb * max_blocks;   // slots of one chunk (chunk_iterator)
     const uint32_t chunk_cap = (uint32_t)std::min<uint64_t>(b.cap, nphotons);
     // one launch per step when a wave's 64 slots map to whole mask words
-    b.fused = (b.cap % 64 == 0) && b.cap <= 0x7FFFFFFFull && step_launch_enabled() && !sort_enabled();
+    b.fused = (b.cap % 64 == 0) && b.cap <= 0x7FFFFFFFull && step_launch_enabled();
     uint64_t swords = chr_propagate_scratch_words(chunk_cap);
     if (b.fused) swords = std::max<uint64_t>(swords, 16 + mask_scan_words(nphotons) + 16);
     const size_t qbytes = ((size_t)nphotons + 1) * 4;
     // split path: hits, ray counter, binning keys/order/histogram
     const size_t hbytes = b.fused ? (size_t)nphotons * 24 + 128 + 256 + 512 + sort_temp_bytes16(nphotons) : 0;
     // split path: ray records, queue order + walk order (FlatCtx::rays / rays_walk)
-    // + the walk-order carry: two walk orders, survivor masks in walk order and their scan
-    const size_t cwords = ((size_t)nphotons + 63) / 64;
-    const size_t rbytes = b.fused ? (size_t)nphotons * 64 + 512 + (size_t)nphotons * 13 + cwords * 12 +
-                                        (size_t)scan_blocks((uint32_t)cwords) * 4 + 2048
-                                  : 0;
+    const size_t rbytes = b.fused ? (size_t)nphotons * 64 + 512 : 0;
     const size_t base_bytes = 2 * qbytes + swords * 4 + 64 + hbytes + rbytes;
     const size_t mbytes = tail_masks ? ((size_t)nphotons + 63) / 64 * 8 + 512 : 0;
     void *buf = nullptr;
@@ -4895,13 +4154,6 @@ static int prop_bufs(uint32_t nphotons, int32_t ntpb, int32_t max_blocks, int ct
     if (b.fused) {
         b.fc.rays = (uint4 *)(((uintptr_t)buf + 2 * qbytes + swords * 4 + 64 + hbytes + 255) & ~(uintptr_t)255);
         b.fc.rays_walk = b.fc.rays + 2 * (size_t)nphotons;
-        b.fc.walk[0] = (uint32_t *)(b.fc.rays_walk + 2 * (size_t)nphotons);
-        b.fc.walk[1] = b.fc.walk[0] + nphotons;
-        b.fc.wmasks = (unsigned long long *)(((uintptr_t)(b.fc.walk[1] + nphotons) + 255) & ~(uintptr_t)255);
-        b.fc.woffsets = (uint32_t *)(b.fc.wmasks + cwords);
-        b.fc.wprefix = b.fc.woffsets + cwords;
-        b.fc.winv = (uint32_t *)(((uintptr_t)(b.fc.wprefix + scan_blocks((uint32_t)cwords)) + 255) & ~(uintptr_t)255);
-        b.fc.walive = (uint8_t *)(((uintptr_t)(b.fc.winv + nphotons) + 255) & ~(uintptr_t)255);   // + 64 B read slack
     }
     return CHR_OK;
 }
@@ -4934,11 +4186,6 @@ struct SlotRun {
     hipEvent_t rng_ready = nullptr;    // the first RNG use waits for it
     hipEvent_t prefix_done = nullptr;  // slot 0's prefix was queued by queue_prefix and ends with this event
     int ctx = 0;
-    // called with each one-step slot's survivor count (the next slot's queue
-    // length) as the host learns it, read through out_ring (32 pinned words)
-    // (chr_propagate_batches: queue the next batch's prefix once few photons remain)
-    std::function<int(uint32_t)> on_length;
-    uint32_t *out_ring = nullptr;
 };
 
 // Device-driven steps: every slot's kernels read the queue length from the
@@ -4958,9 +4205,8 @@ static int device_slots(const chr_geometry *g, const chr_photons *ph, uint32_t n
     if (!run.prefix_done) CHR_HIP_CHECK(hipMemsetAsync(done, 0, 4, stream));
     b.fc.enrol_next = true;
     uint32_t *ring = b.pinned + 64;   // (mode, n) of recent slots, 32 entries (written by each slot's head kernel)
-    // slot k + 1's head runs at the end of slot k's scan (no head dispatch per slot);
-    // not with the walk-order carry, whose scan is its own kernel
-    const bool fold = head_fold_enabled() && !walk_carry_enabled();
+    // slot k + 1's head runs at the end of slot k's scan (no head dispatch per slot)
+    const bool fold = true;
     std::vector<hipEvent_t> &events = *run.events;
     uint32_t n_ub = nphotons;
     int k = 0, cur = 0;
@@ -4994,8 +4240,6 @@ static int device_slots(const chr_geometry *g, const chr_photons *ph, uint32_t n
                          scatter_first, b.scratch, stream, timing == 2 ? ev[0] : nullptr, timing == 2 ? ev[1] : nullptr,
                          b.hits, b.sort_space, k == 0, ev[2], timing ? ev[3] : nullptr, &split, &b.fc, &sc);
         if (rc) return rc;
-        if (run.on_length)   // the output queue's count header (+1)
-            CHR_HIP_CHECK(hipMemcpyAsync(run.out_ring + k % 32, b.q[cur ^ 1], 4, hipMemcpyDeviceToHost, stream));
         if (timing == 2) CHR_HIP_CHECK(hipEventRecord(ev[4], stream));
         b.fc.cur ^= 1;   // the step's scatter enrolled the next step's flat walks in the other list
         cur ^= 1;
@@ -5005,7 +4249,6 @@ static int device_slots(const chr_geometry *g, const chr_photons *ph, uint32_t n
             const uint32_t m = ring[2 * ((k - 1) % 32)], nk = ring[2 * ((k - 1) % 32) + 1];
             if (m != STEP_ONE) stop = true;   // the tail ran or the queue emptied: slot k is idle
             else n_ub = nk;                   // later queues are no longer
-            if (run.on_length) CHR_TRY(run.on_length(m == STEP_ONE ? run.out_ring[(k - 1) % 32] - 1u : 0u));
         }
         k++;
     }
@@ -5356,57 +4599,33 @@ static bool photons_alias(const chr_photons *a, uint32_t na, const chr_photons *
     return false;
 }
 
-// CHR_BATCH_LOOKAHEAD=k (0..NCTX-1, default 0): prefixes queued for the k
-// batches after the running one as well.  Measured on the 29k bench (r02,
-// profiles/r02/ab_lookahead): 0 416.8, 1 417.3, 2 378.2 M photons/s -- a second
-// batch's walk queued early competes with the running batch's walks (two
-// persistent grids, twice the node working set) and the step loses the overlap.
-static size_t batch_lookahead() {
-    const char *e = getenv("CHR_BATCH_LOOKAHEAD");
-    const int k = e ? atoi(e) : 0;
-    return (size_t)(k < 0 ? 0 : (k > NCTX - 1 ? NCTX - 1 : k));
-}
-
-// CHR_BATCH_EARLY_BIN=1: a batch's binning part is queued right after the
-// previous batch's walk instead of with its own walk at the previous batch's
-// tail.  Off: measured slower (r03 ab5: 425.1 -> 412.0 M/s; the walk then starts
-// with the tail and slows its first, chip-wide phase: mean tail 6.53 -> 9.99 ms).
-static bool batch_early_bin() {
-    const char *e = getenv("CHR_BATCH_EARLY_BIN");
-    return e && e[0] == '1';
-}
-
-// CHR_BATCH_PREFIX_BELOW=n: queue the next batch's prefix once a step of the
-// running batch leaves fewer than n survivors (n = nthreads_per_block * 128:
-// as soon as the next slot is known to be the tail); 0 (default): when the
-// next batch starts, i.e. once the host has seen the tail slot start
-static uint32_t batch_prefix_below() {
-    const char *e = getenv("CHR_BATCH_PREFIX_BELOW");
-    return e ? (uint32_t)strtoul(e, nullptr, 10) : 0u;
-}
-
 // The RNG-free part of a propagate's first slot on stream ps: queues, counters,
-// the head kernel, flat-walk classification, direction binning (part 1) and the
-// BVH walk (part 2) -- launch_step PHASE_BIN / PHASE_TRACE, or both at once
-// (PHASE_PREFIX) -- ending with prefix_done.
+// the head kernel, flat-walk classification, direction binning and the BVH walk
+// (launch_step PHASE_PREFIX), ending with prefix_done.
+// Measured and removed: queueing the prefixes of later batches
+// earlier (r02 ab_lookahead: one batch ahead 417.3, two 378.2 against 416.8 M/s),
+// the next batch's prefix once the running one is down to few photons (r02
+// ab_prefix_trigger, 392 against 428 M/s), its binning early (r03 ab5, 412.0
+// against 425.1 M/s), and the prefix walk on a fraction of the grid (r03 ab4):
+// a walk started beside the running batch's late steps or its tail slows them
+// more than the overlap gains.
 static int queue_prefix(const chr_geometry *g, const chr_photons *ph, uint32_t nphotons, uint32_t true_nphotons,
                         uint32_t ncopies, uint32_t *rng, uint32_t nslots, int32_t ntpb, int32_t max_steps,
                         int32_t use_weights, int32_t scatter_first, PropBufs &b, int ctx,
-                        std::vector<hipEvent_t> &events, hipEvent_t prefix_done, hipStream_t ps, int parts = 3) {
+                        std::vector<hipEvent_t> &events, hipEvent_t prefix_done, hipStream_t ps) {
     uint32_t *ctl = nullptr;
     CHR_TRY(slot_ctl_get(2 * (size_t)max_steps + 8, &ctl, ctx));
     uint32_t *done = ctl + 2 * (size_t)max_steps;
-    if (parts & 1) CHR_TRY(prop_start(b, nphotons, true_nphotons, ncopies, ps, done));
+    CHR_TRY(prop_start(b, nphotons, true_nphotons, ncopies, ps, done));
     b.fc.enrol_next = true;
     CHR_TRY(grow_events(events, SLOT_EVENTS));
     SlotCtl sc{ctl, ctl + 1, done, nphotons, max_steps, (uint32_t)ntpb * 16 * 8};
-    sc.phase = parts == 1 ? PHASE_BIN : (parts == 2 ? PHASE_TRACE : PHASE_PREFIX);
+    sc.phase = PHASE_PREFIX;
     sc.ctx = ctx;
     sc.prefix_done = prefix_done;
     sc.host_ring = b.pinned + 64;   // ring entry 0 (device_slots' slot 0): this head is slot 0's
     hipEvent_t *ev = events.data();
     const int timing = slot_timing();
-    sc.ev_bin_end = timing == 2 ? ev[8] : nullptr;
     return launch_step(g, ph, rng, nslots, (uint32_t)b.cap, nphotons, b.q[0] + 1, b.q[1], 1, use_weights,
                        scatter_first, b.scratch, ps, timing == 2 ? ev[0] : nullptr, ev[1], b.hits, b.sort_space, true,
                        ev[2], timing ? ev[3] : nullptr, nullptr,
@@ -5439,7 +4658,7 @@ static int propagate_batches(const chr_geometry *g, const chr_photons *phs, cons
     if (walks_reference_bvh(g)) CHR_TRY(chr::geometry_ref_nodes(g));
     PropBufs probe;
     probe.cap = (uint64_t)ntpb * max_blocks;
-    probe.fused = (probe.cap % 64 == 0) && probe.cap <= 0x7FFFFFFFull && step_launch_enabled() && !sort_enabled();
+    probe.fused = (probe.cap % 64 == 0) && probe.cap <= 0x7FFFFFFFull && step_launch_enabled();
     if (idx.size() == 1 || !device_steps_ok(g, probe)) {   // nothing to overlap: one propagate after the other
         for (uint32_t i : idx)
             CHR_TRY(chr_propagate(g, phs + i, nphotons[i], true_nphotons[i], ncopies[i], d_rng_states, rng_nslots,
@@ -5451,7 +4670,7 @@ static int propagate_batches(const chr_geometry *g, const chr_photons *phs, cons
     CHR_TRY(batch_streams_get(&ts, &ps));
     const size_t nb = idx.size();
     std::vector<BatchHost> *pool = nullptr;
-    CHR_TRY(batch_host_get(nb, 128 + 2 * (size_t)max_steps + 8 + 32, &pool));   // + the survivor-count ring
+    CHR_TRY(batch_host_get(nb, 128 + 2 * (size_t)max_steps + 8, &pool));
     std::vector<BatchHost> &bh = *pool;
     // every context sized for the largest batch up front: no buffer is
     // reallocated while an earlier batch may still use it
@@ -5473,54 +4692,23 @@ static int propagate_batches(const chr_geometry *g, const chr_photons *phs, cons
     CHR_TRY(timing_events(1, &entry_ev, 1));
     CHR_HIP_CHECK(hipEventRecord((*entry_ev)[0], stream));
     CHR_HIP_CHECK(hipStreamWaitEvent(ps, (*entry_ev)[0], 0));
-    auto aliases_earlier = [&](size_t j, size_t from) {   // batch j shares arrays with one of batches [from, j)
-        for (size_t e = from; e < j; ++e)
-            if (photons_alias(phs + idx[j], nphotons[idx[j]], phs + idx[e], nphotons[idx[e]])) return true;
-        return false;
-    };
-    // prefixes: qbin batches have their binning part queued, qtrace their walk too
-    size_t qbin = 0, qtrace = 0;
-    const size_t lookahead = batch_lookahead();
-    const uint32_t prefix_below = batch_prefix_below();
-    const bool early_bin = batch_early_bin();
-    // parts: 1 binning, 2 walk, 3 both (queue_prefix)
-    auto prefix = [&](size_t j, int parts) -> int {
+    // batch j's prefix is queued when batch j starts (after batch j - 1's slots, so
+    // it runs beside that batch's tail)
+    auto prefix = [&](size_t j) -> int {
         const uint32_t i = idx[j];
         const int c = (int)(j % NCTX);
-        if (parts & 1) {
-            if (j >= (size_t)NCTX) CHR_HIP_CHECK(hipStreamWaitEvent(ps, bh[j - NCTX].done, 0));   // the context is free
-            for (size_t e = j >= (size_t)NCTX ? j - NCTX + 1 : 0; e < j; ++e)   // shared photon arrays: after that batch
-                if (photons_alias(phs + i, nphotons[i], phs + idx[e], nphotons[idx[e]]))
-                    CHR_HIP_CHECK(hipStreamWaitEvent(ps, bh[e].done, 0));
-            CHR_TRY(prop_bufs(nphotons[i], ntpb, max_blocks, c, true, bufs[c]));
-            bufs[c].pinned = bh[j].pinned;
-        }
+        if (j >= (size_t)NCTX) CHR_HIP_CHECK(hipStreamWaitEvent(ps, bh[j - NCTX].done, 0));   // the context is free
+        for (size_t e = j >= (size_t)NCTX ? j - NCTX + 1 : 0; e < j; ++e)   // shared photon arrays: after that batch
+            if (photons_alias(phs + i, nphotons[i], phs + idx[e], nphotons[idx[e]]))
+                CHR_HIP_CHECK(hipStreamWaitEvent(ps, bh[e].done, 0));
+        CHR_TRY(prop_bufs(nphotons[i], ntpb, max_blocks, c, true, bufs[c]));
+        bufs[c].pinned = bh[j].pinned;
         return queue_prefix(g, phs + i, nphotons[i], true_nphotons[i], ncopies[i], d_rng_states, rng_nslots, ntpb,
-                            max_steps, use_weights, scatter_first, bufs[c], c, bh[j].ev, bh[j].prefix_done, ps, parts);
-    };
-    auto queue_walk = [&](size_t j) -> int {   // batch j's walk (and its binning, unless queued early)
-        const int parts = qbin > j ? 2 : 3;
-        CHR_TRY(prefix(j, parts));
-        if (parts == 3) qbin = j + 1;
-        qtrace = j + 1;
-        return CHR_OK;
+                            max_steps, use_weights, scatter_first, bufs[c], c, bh[j].ev, bh[j].prefix_done, ps);
     };
     std::vector<int> slots(nb, 0);
     for (size_t j = 0; j < nb; ++j) {
-        // queue the prefixes of the batches ahead (as many as there are free
-        // contexts); one sharing photon arrays with a batch not yet queued in
-        // full waits until that batch's done event exists
-        while (qtrace < nb && qtrace < j + 1 + lookahead) {
-            if (qtrace > j && aliases_earlier(qtrace, j)) break;
-            CHR_TRY(queue_walk(qtrace));
-        }
-        // CHR_BATCH_EARLY_BIN=1: the next batch's binning now, on the prefix stream
-        // behind this batch's walk (beside this batch's one-step slots); default:
-        // with its walk, at this batch's tail
-        if (early_bin && qbin == j + 1 && qtrace == j + 1 && qbin < nb && !aliases_earlier(qbin, j)) {
-            CHR_TRY(prefix(qbin, 1));
-            qbin++;
-        }
+        CHR_TRY(prefix(j));
         const uint32_t i = idx[j];
         const int c = (int)(j % NCTX);
         PropBufs &b = bufs[c];
@@ -5530,15 +4718,6 @@ static int propagate_batches(const chr_geometry *g, const chr_photons *phs, cons
         run.rng_ready = j > 0 ? bh[j - 1].done : nullptr;   // the previous batch's tail advances the RNG slots
         run.prefix_done = bh[j].prefix_done;
         run.ctx = c;
-        // the next batch's prefix as soon as this batch is down to its late,
-        // under-occupied steps (CHR_BATCH_PREFIX_BELOW photons; 0: at the next batch's start)
-        if (prefix_below && qtrace == j + 1 && qtrace < nb && !aliases_earlier(qtrace, j)) {
-            run.out_ring = bh[j].pinned + 128 + 2 * (size_t)max_steps + 8;
-            run.on_length = [&, j](uint32_t n) -> int {
-                if (qtrace == j + 1 && qtrace < nb && n < prefix_below) CHR_TRY(queue_walk(qtrace));
-                return CHR_OK;
-            };
-        }
         uint32_t *ctl = nullptr;
         CHR_TRY(device_slots(g, phs + i, nphotons[i], d_rng_states, rng_nslots, ntpb, max_steps, use_weights,
                              scatter_first, b, run, stream, &ctl, &slots[j]));
@@ -5653,7 +4832,7 @@ extern "C" int chr_kernel_info(int32_t which, chr_kernel_attr *out) {
     const char *name = nullptr;
     switch (which) {
         case 0: fn = (const void *)trace_kernel<false, 6, 12, 4, 48>; name = "chr::trace_kernel<false,6,12,4,48>"; break;
-        case 1: fn = (const void *)shade_kernel<3, true, true>; name = "chr::shade_kernel<3,true,true>"; break;
+        case 1: fn = (const void *)shade_kernel<3>; name = "chr::shade_kernel<3>"; break;
         case 2: fn = (const void *)propagate_tail_kernel<kTailWaves>; name = "chr::propagate_tail_kernel<2>"; break;
         case 3: fn = (const void *)propagate_step_kernel<8, 4, kWalk>; name = "chr::propagate_step_kernel<8,4,2006>"; break;
         default: return chr::fail(CHR_ERR_INVALID, "chr_kernel_info: unknown kernel %d", which);

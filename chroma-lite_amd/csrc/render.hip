@@ -205,8 +205,7 @@ __device__ void to_diffuse(const DevGeom &g, Photon &p, State &s, chr_xorwow &rn
     wst.sstride = 1;                                                               \
     wst.node = (CHR_LDS uint32_t *)(lds_stack + threadIdx.x);                      \
     wst.dist = (CHR_LDS float *)(lds_stack + WIDE_LDS * BLOCK + threadIdx.x);      \
-    wst.leafq = nullptr;                                                           \
-    wst.group = nullptr
+    wst.leafq = nullptr
 
 // float adds of the per-triangle lookup (the reference's fAtomicAdd loop)
 __device__ __forceinline__ void lookup_add(float *base, uint32_t tri, V3 v) {

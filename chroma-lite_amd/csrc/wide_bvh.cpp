@@ -50,16 +50,10 @@ inline uint32_t leaf_max_env() {
     const int v = e ? std::atoi(e) : LEAF_DEFAULT;
     return (uint32_t)std::min(LEAF_MAX, std::max(1, v));
 }
+// SAH bins per axis.  An exact SAH sweep over every split position of ranges of up
+// to 64 triangles found no better tree on these meshes (r04 bvh5: trace 14.35 vs
+// 14.41 ms per step, removed).
 constexpr int NBINS = 32;
-// CHR_WIDE_SWEEP=n: ranges of <= n triangles split by an exact SAH sweep instead of
-// NBINS bins (build-time A/B; default 0: binned everywhere)
-inline uint32_t sweep_max_env() {
-    const char *e = std::getenv("CHR_WIDE_SWEEP");
-    return e ? (uint32_t)std::max(0, std::atoi(e)) : 0u;
-}
-
-// CHR_WIDE_NO_FILL: do not split multi-triangle leaves into free child slots (build-time A/B)
-inline bool fill_env() { return !std::getenv("CHR_WIDE_NO_FILL"); }
 
 struct Box {
     float lo[3], hi[3];
@@ -84,9 +78,7 @@ struct Cluster {
 };
 
 struct Builder {
-    bool fill_leaves;
     uint32_t leaf_max;
-    uint32_t sweep_max;   // ranges of at most this many triangles split by an exact SAH sweep
     const std::vector<Box> &tri_box;
     const std::vector<float> &centroid;   // 3 per triangle
     std::vector<uint32_t> &idx;
@@ -110,41 +102,8 @@ struct Builder {
         return r;
     }
 
-    // exact SAH split of a small range [b,e): every split position of the
-    // centroid order on each axis (the binned split below approximates this)
-    uint32_t split_sweep(uint32_t b, uint32_t e) {
-        const uint32_t n = e - b;
-        std::vector<uint32_t> ord[3];
-        std::vector<double> right(n);
-        double best_cost = INFINITY;
-        int best_axis = -1;
-        uint32_t best_m = 0;
-        for (int a = 0; a < 3; ++a) {
-            ord[a].assign(idx.begin() + b, idx.begin() + e);
-            std::stable_sort(ord[a].begin(), ord[a].end(), [&](uint32_t x, uint32_t y) {
-                return centroid[3 * (size_t)x + a] < centroid[3 * (size_t)y + a];
-            });
-            Box acc;
-            acc.empty();
-            for (uint32_t i = n; i-- > 1;) {
-                acc.grow(tri_box[ord[a][i]]);
-                right[i] = acc.area() * (double)(n - i);
-            }
-            acc.empty();
-            for (uint32_t i = 1; i < n; ++i) {
-                acc.grow(tri_box[ord[a][i - 1]]);
-                const double cost = acc.area() * (double)i + right[i];
-                if (cost < best_cost) { best_cost = cost; best_axis = a; best_m = i; }
-            }
-        }
-        if (best_axis < 0) return b + n / 2;
-        std::copy(ord[best_axis].begin(), ord[best_axis].end(), idx.begin() + b);
-        return b + best_m;
-    }
-
     // binned SAH split of [b,e); returns split point (b < m < e)
     uint32_t split(uint32_t b, uint32_t e, bool par) {
-        if (e - b <= sweep_max) return split_sweep(b, e);
         Box cb;
         cb.empty();
         for (uint32_t i = b; i < e; ++i) cb.grow(&centroid[3 * (size_t)idx[i]]);   // cheap relative to binning
@@ -233,7 +192,7 @@ struct Builder {
             double best = -1.0;
             for (int i = 0; i < n; ++i)
                 if (out[i].count() > leaf_max && out[i].box.area() > best) { best = out[i].box.area(); pick = i; }
-            if (pick < 0 && fill_leaves)
+            if (pick < 0)
                 for (int i = 0; i < n; ++i)
                     if (out[i].count() > 1 && out[i].box.area() > best) { best = out[i].box.area(); pick = i; }
             if (pick < 0) break;
@@ -341,7 +300,7 @@ int build_wide_bvh(const chr_geometry_desc *d, WideBVH &out) {
     for (int64_t t = 0; t < (int64_t)ntri; ++t)
         for (int a = 0; a < 3; ++a) centroid[3 * t + a] = 0.5f * (tri_box[t].lo[a] + tri_box[t].hi[a]);
 
-    Builder B{fill_env(), leaf_max_env(), sweep_max_env(), tri_box, centroid, idx};
+    Builder B{leaf_max_env(), tri_box, centroid, idx};
     out.leaf_max = B.leaf_max;
     out.nodes.clear();
     out.tri.clear();
@@ -647,8 +606,7 @@ extern "C" int chr_wide_bvh_export(const chr_wide_result *r, void *h_nodes, uint
 extern "C" int chr_wide_bvh_key(char *out, uint32_t n) {
     if (!out || n == 0) return chr::fail(CHR_ERR_INVALID, "chr_wide_bvh_key: no buffer");
     // bump the format number whenever the builder's output for the same inputs changes
-    const int len = std::snprintf(out, n, "w%d-l%u-s%u-f%d", chr::WIDE_FORMAT, chr::leaf_max_env(),
-                                  chr::sweep_max_env(), chr::fill_env() ? 1 : 0);
+    const int len = std::snprintf(out, n, "w%d-l%u", chr::WIDE_FORMAT, chr::leaf_max_env());
     if (len < 0 || (uint32_t)len >= n) return chr::fail(CHR_ERR_INVALID, "chr_wide_bvh_key: buffer too small");
     return CHR_OK;
 }

@@ -331,7 +331,7 @@ int chr_wide_bvh_describe(const chr_wide_result *r, chr_wide_bvh_desc *out);
 /* copy the compact form into caller arrays sized by chr_wide_bvh_describe */
 int chr_wide_bvh_export(const chr_wide_result *r, void *h_nodes, uint32_t *h_rec_id, uint32_t *h_rec_rank,
                         uint32_t *h_cut);
-/* the builder's settings as a short string ("w<format>-l<leaf max>-s<sweep>-f<fill>"):
+/* the builder's settings as a short string ("w<format>-l<leaf max>"):
  * part of a cache key -- a compact form is reused only under the same settings */
 int chr_wide_bvh_key(char *out, uint32_t n);
 /* check a compact form against a geometry (every index in range, the ranks a

@@ -112,24 +112,6 @@ def test_batches_shared_photons(cuda, small_detector, pattern):
     assert np.array_equal(out[True][1], out[False][1])
 
 
-@pytest.mark.parametrize('env', [('CHR_BATCH_LOOKAHEAD', '0'), ('CHR_BATCH_LOOKAHEAD', '1'),
-                                 ('CHR_BATCH_PREFIX_BELOW', '20000')])
-def test_batches_lookahead_settings(cuda, small_detector, monkeypatch, env):
-    """When the next batches' prefixes are queued (CHR_BATCH_LOOKAHEAD: that
-    many batches ahead; CHR_BATCH_PREFIX_BELOW: once the running batch is down
-    to that many photons) changes nothing in the results."""
-    from chroma import gpu
-    monkeypatch.setenv(*env)
-    lookahead = '%s=%s' % env
-    det = gpu.GPUDetector(small_detector)
-    sources = _sources([30000, 50000, 20000, 60000], seed=17)
-    seq, rng_seq, _ = _run(det, sources, 64, 64, 1000, batched=False)
-    bat, rng_bat, _ = _run(det, sources, 64, 64, 1000, batched=True)
-    for i, (a, b) in enumerate(zip(bat, seq)):
-        _same(a, b, 'lookahead %s batch %d' % (lookahead, i))
-    assert np.array_equal(rng_bat, rng_seq)
-
-
 def test_batches_with_copies_and_weights(cuda, small_detector):
     """Batches of GPUPhotons with ncopies > 1 (clones interleaved in the queue,
     photon.py:242-250), and use_weights (every slot a multi-step tail) ==
@@ -238,38 +220,65 @@ def test_batches_slot_timing_modes_identical(cuda, small_detector, monkeypatch):
     assert sum(s.tail_photons for s in out['t'][2]) > 0
 
 
-@pytest.mark.parametrize('switch', ['CHR_TAIL_LONE', 'CHR_TRACE_DRAIN_LONE', 'CHR_SHADE_PREFETCH2', 'CHR_TAIL_GS64'])
-def test_batches_walker_switches_identical(cuda, small_detector, monkeypatch, switch):
-    """The walkers are interchangeable: the tail's lone photon walked by the
-    software-pipelined walk_lone (default) or walk_segment<64>
-    (CHR_TAIL_LONE=0) or the run-time-width segment walk (CHR_TAIL_GS64=0); a
-    trace wave draining one walk through walk_lone or walk_segment<0>
-    (CHR_TRACE_DRAIN_LONE=0); the shade kernel's two-ahead queue prefetch on or
-    off.  Same photons, same RNG states."""
+# Every run-time switch the library reads (include/chroma_amd.h lists them)
+# gives the same photons and RNG states as the default, sequential and batched:
+#   CHR_HOST_STEPS=1        the host reads the survivor count every step
+#   CHR_STEP_LAUNCH=0       one launch per chunk (the reference's launch structure)
+#   CHR_TRACE_STEPS=1       per-step stderr lines (debugging)
+#   CHR_PROPAGATE_VARIANT   2/4 fused step kernels, 7/8 binning every / no step, 1 the
+#                           exact-order walk of the reference BVH, 5 the counting form
+#   CHR_SLOT_TIMING         test_batches_slot_timing_modes_identical
+#   CHR_WIDE_LEAF_MAX / CHR_EXACT_ORDER_ONLY: test_geometry_build_switches_identical
+SWITCHES = [('CHR_HOST_STEPS', '1'), ('CHR_STEP_LAUNCH', '0'), ('CHR_TRACE_STEPS', '1'),
+            ('CHR_PROPAGATE_VARIANT', '2'), ('CHR_PROPAGATE_VARIANT', '4'), ('CHR_PROPAGATE_VARIANT', '7'),
+            ('CHR_PROPAGATE_VARIANT', '8'), ('CHR_PROPAGATE_VARIANT', '1'), ('CHR_PROPAGATE_VARIANT', '5')]
+
+
+@pytest.mark.parametrize('switch,value', SWITCHES)
+def test_switches_identical(cuda, small_detector, monkeypatch, switch, value):
     sources = _sources([30000, 70000, 5000, 120000], seed=29)
     from chroma import gpu
     det = gpu.GPUDetector(small_detector)
     monkeypatch.delenv(switch, raising=False)
-    base = _run(det, sources, 64, 256, 1000, batched=True)
-    monkeypatch.setenv(switch, '0')
+    base = {b: _run(det, sources, 64, 256, 1000, batched=b) for b in (False, True)}
+    monkeypatch.setenv(switch, value)
+    for batched in (False, True):
+        alt = _run(det, sources, 64, 256, 1000, batched=batched)
+        for i, (a, b) in enumerate(zip(base[batched][0], alt[0])):
+            _same(a, b, '%s=%s batched=%s batch %d' % (switch, value, batched, i))
+        assert np.array_equal(base[batched][1], alt[1])
+    assert sum(s.tail_photons for s in base[True][2]) > 0
+    assert sum(s.trace_launches for s in base[True][2]) > 0
+
+
+@pytest.mark.parametrize('switch,value', [('CHR_WIDE_LEAF_MAX', '4'), ('CHR_WIDE_LEAF_MAX', '1'),
+                                          ('CHR_EXACT_ORDER_ONLY', '1')])
+def test_geometry_build_switches_identical(cuda, small_detector, monkeypatch, switch, value):
+    """The traversal BVH's leaf size (a build-time setting, part of its cache key)
+    and the exact-order walk only (no traversal BVH uploaded): same photons."""
+    import copy
+    from chroma import gpu
+    sources = _sources([30000, 70000], seed=37)
+    base = _run(gpu.GPUDetector(small_detector), sources, 64, 256, 1000, batched=True)
+    monkeypatch.setenv(switch, value)
+    geo = copy.copy(small_detector)
+    geo.bvh = copy.copy(small_detector.bvh)
+    geo.bvh.wide = None
+    det = gpu.GPUDetector(geo)
     alt = _run(det, sources, 64, 256, 1000, batched=True)
     for i, (a, b) in enumerate(zip(base[0], alt[0])):
-        _same(a, b, '%s=0 batch %d' % (switch, i))
+        _same(a, b, '%s=%s batch %d' % (switch, value, i))
     assert np.array_equal(base[1], alt[1])
-    assert sum(s.tail_photons for s in base[2]) > 0
-    assert sum(s.trace_launches for s in base[2]) > 0
 
 
-@pytest.mark.parametrize('lone', ['1', '0'])
-def test_mirror_scene_long_tail_parity(cuda, monkeypatch, lone):
+def test_mirror_scene_long_tail_parity(cuda):
     """The physics scene (97% specular mirror plate, wire planes, every surface
     model) at 4000 photons over 64 x 64 slots, 1000 steps: every step after the
-    first runs in the tail kernel, whose waves thin out to one walking photon
-    (the lone walker).  HIP == oracle with either lone walker."""
+    first runs in the tail kernel, whose waves thin out to a few walking photons
+    (walk_lone for one, the segment walk for several).  HIP == oracle."""
     import scenes
     from chroma import gpu, loader
     from chroma.gpu.packing import PackedGeometry
-    monkeypatch.setenv('CHR_TAIL_LONE', lone)
     geo = loader.create_geometry_from_obj(scenes.physics_scene())
     det = gpu.GPUDetector(geo)
     src = scenes.photon_sources(4000, seed=41)
@@ -281,10 +290,10 @@ def test_mirror_scene_long_tail_parity(cuda, monkeypatch, lone):
     host.weights[:] = 1.0
     oracle.propagate(PackedGeometry(geo), host, states, nslots, 64, 64, 1000)
     for f in ('flags', 'last_hit_triangles'):
-        assert np.array_equal(getattr(got[0], f), getattr(host, f)), 'mirror scene lone=%s: %s' % (lone, f)
+        assert np.array_equal(getattr(got[0], f), getattr(host, f)), 'mirror scene: %s' % f
     for f in ('pos', 'dir', 'pol', 't', 'wavelengths'):
         a = getattr(got[0], f).astype(np.float64)
         b = getattr(host, f).astype(np.float64)
-        assert np.all(np.abs(a - b) <= 1e-5 * np.maximum(np.abs(b), 1.0)), 'mirror scene lone=%s: %s' % (lone, f)
+        assert np.all(np.abs(a - b) <= 1e-5 * np.maximum(np.abs(b), 1.0)), 'mirror scene: %s' % f
     assert np.array_equal(rng, states.reshape(6, nslots))
     assert stats[0].tail_photons > 0

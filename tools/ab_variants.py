@@ -29,7 +29,6 @@ def main():
     from chroma.photon_source import isotropic
     from types import SimpleNamespace
     torch.cuda.set_device(0)
-    os.environ['CHR_NODE_LAYOUT_AB'] = '1'      # keep both node layouts on the device (":n128" variants)
     det = bench.build_geometry(args.detector, '/tmp/chroma_bench_cache')
     t0 = time.time()
     gdet = gpu.GPUDetector(det)
@@ -39,7 +38,7 @@ def main():
                                pol=ga.to_gpu(gpu.to_float3(photons.pol)), wavelengths=ga.to_gpu(photons.wavelengths),
                                t=ga.to_gpu(photons.t), flags=ga.to_gpu(photons.flags), evidx=ga.to_gpu(photons.evidx),
                                true_nphotons=args.photons)
-    variants = args.variants.split(',')   # "<n>[:sort][:n128][:chunked]"
+    variants = args.variants.split(',')   # "<n>[:chunked]"
     times = {v: [] for v in variants}
     kms = {v: [] for v in variants}
     ref_flags = None
@@ -47,8 +46,6 @@ def main():
         for v in variants:
             opts = v.split(':')
             os.environ['CHR_PROPAGATE_VARIANT'] = opts[0]
-            os.environ['CHR_SORT'] = '1' if 'sort' in opts[1:] else '0'
-            os.environ['CHR_NODE_LAYOUT'] = '128' if 'n128' in opts[1:] else '96'
             os.environ['CHR_STEP_LAUNCH'] = '0' if 'chunked' in opts[1:] else '1'
             rng = gpu.get_rng_states(512 * 1024, seed=1)
             gp = gpu.GPUPhotons(pristine, copy_flags=True, copy_triangles=False, copy_weights=False)
