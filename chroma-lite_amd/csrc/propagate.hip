@@ -2211,7 +2211,11 @@ __device__ __forceinline__ int walk_segment(const DevGeom &g, bool act, V3 o, V3
 // Also cheaper per iteration: 32-bit near-child keys (the entry distance's bits
 // with the child slot in the low 3 bits: the pick among children whose entries
 // differ in those bits only may change, the culling distance is rounded down),
-// byte extraction with v_perm, branch-free triangle-list writes.
+// byte extraction with v_perm.
+// Device profile (CHR_PROF_LONE_*): walk_lone ticks REFILL (the stack refill and the
+// next nodes' issue), EXPAND (the expansion, including the wait for its nodes) and
+// TRIS (the tests, including the wait for their records); FETCH stays 0 -- its loads
+// are waited for inside EXPAND and TRIS.  walk_segment ticks all four in sequence.
 __device__ __forceinline__ uint32_t byte8(uint32_t lo4, uint32_t hi4, uint32_t k) {   // byte k of (hi4:lo4)
     return __builtin_amdgcn_perm(hi4, lo4, 0x0c0c0c00u | k);
 }
@@ -2331,20 +2335,16 @@ __device__ __forceinline__ int walk_lone(const DevGeom &g, V3 o, V3 d, uint32_t 
         }
         cur = near;
         cur_t = __uint_as_float(key & ~7u);           // <= the child's entry distance
-        // this expansion's hit-leaf triangles, listed in lane order.  A lane with
-        // triangles writes its 4 slots from the last down: a slot beyond its count
-        // lands on a later lane's entry, which that lane writes afterwards (a lower
-        // slot index), and slot indices are clamped to the buffer.
+        // this expansion's hit-leaf triangles, listed in lane order: each lane writes
+        // exactly its own entries [pre, pre + cnt) (slot indices clamped to the buffer)
         const uint32_t cnt = leafhit ? kind : 0u;
         const unsigned long long b0 = __ballot(cnt & 1u), b1 = __ballot(cnt & 2u), b2 = __ballot(cnt & 4u);
         const uint32_t pre = __popcll(b0 & below) + 2u * __popcll(b1 & below) + 4u * __popcll(b2 & below);
         const uint32_t Tn = uu(__popcll(b0) + 2u * __popcll(b1) + 4u * __popcll(b2));
         const int nb = (pb ^ 1) * TAIL_TRI;
-        if (cnt > 0u) {
 #pragma unroll
-            for (int i = 3; i >= 0; --i)
-                tlist[nb + (int)min(pre + (uint32_t)i, (uint32_t)(TAIL_TRI - 1))] = first + (uint32_t)i;
-        }
+        for (int i = 0; i < 4; ++i)
+            if ((uint32_t)i < cnt) tlist[nb + (int)min(pre + (uint32_t)i, (uint32_t)(TAIL_TRI - 1))] = first + (uint32_t)i;
         lp.tick(2);
         // cursors without a node take the topmost unculled stack entries (walk_segment's
         // window refill; culled with the best before this iteration's triangle tests --

@@ -528,7 +528,8 @@ enum {
     CHR_PROF_SHADE_KERNEL = 14,       /* whole shade_kernel */
     CHR_PROF_TAIL_KERNEL = 15,        /* whole propagate_tail_kernel */
     CHR_PROF_TRACE_DRAIN = 16,        /* trace_kernel: a wave's last <= 8 walks, whole-wave (calls = walks) */
-    /* the tail's lone walker (walk_segment<64>), wave-cycles per phase of its iterations: */
+    /* the lone walker's wave-cycles per phase of its iterations (walk_lone, the default, has no
+       separate fetch phase: its node / record loads are waited for inside EXPAND / TRIS): */
     CHR_PROF_LONE_REFILL = 17,        /* cursors refilled from the shared stack */
     CHR_PROF_LONE_FETCH = 18,         /* nodes + triangles loaded (issued and waited for) */
     CHR_PROF_LONE_EXPAND = 19,        /* children slab-tested, near child, pushes, triangle list */
