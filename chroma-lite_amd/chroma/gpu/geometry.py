@@ -84,6 +84,14 @@ class GPUGeometry(object):
         _native.call('chr_geometry_device_bytes', self._handle, ctypes.byref(b))
         return b.value
 
+    def phys_words(self):
+        """(hot, total) 4-byte words of the physics tables and records
+        (chr_geometry_phys_words): the step kernels keep the hot part in LDS
+        when it fits (propagate.hip SHADE_PHYS_WORDS / TAIL_PHYS_WORDS)."""
+        hot, total = ctypes.c_uint32(), ctypes.c_uint32()
+        _native.call('chr_geometry_phys_words', self._handle, ctypes.byref(hot), ctypes.byref(total))
+        return hot.value, total.value
+
     def device_usage_str(self):
         return 'device usage: geometry %s (%d triangles, %d BVH nodes)' % (
             format_size(self.device_bytes()), len(self.packed.triangles), len(self.packed.nodes))

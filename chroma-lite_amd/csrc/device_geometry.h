@@ -35,11 +35,16 @@
 
 namespace chr {
 
+// buckets of a re-emission time CDF's index (geometry.cpp time_cdf_index)
+constexpr uint32_t TIME_INDEX_BUCKETS = 4096;
+
 struct DevMaterial {
     uint32_t num_comp;
     uint32_t refractive_index, absorption_length, scattering_length;       // blob offsets
-    uint32_t comp_reemission_prob, comp_reemission_wvl_cdf, comp_reemission_time_cdf,
-        comp_absorption_length;                                            // first component
+    // first component; component c at + c * (wl_n + 1) (time CDF: + c * (t_n + 1))
+    uint32_t comp_reemission_prob, comp_reemission_wvl_cdf, comp_absorption_length;   // hot
+    uint32_t comp_reemission_time_cdf;                                     // cold (tables_g)
+    uint32_t comp_time_index;   // cold: (TIME_INDEX_BUCKETS + 1) words per component, ~0u: none
 };
 
 struct DevSurface {
@@ -78,8 +83,8 @@ struct DevGeom {
     // tail kernels to keep a copy in LDS (chr::PhysCache)
     const uint32_t *phys;
     uint32_t phys_words, mat_off, surf_off;
-    // [0, phys_hot_words): the tables and records the step physics reads on every step;
-    // after it the materials' component tables (bulk re-emission), read through tables_g
+    // [0, phys_hot_words): the tables (identical ones stored once) and records; after it
+    // the materials' re-emission time CDFs and their bucket indexes, read through tables_g
     // (== tables in global memory; phys_cache points tables into LDS, tables_g stays)
     uint32_t phys_hot_words;
     const float *tables_g;
@@ -102,6 +107,10 @@ struct chr_geometry {
     bool ref_tri_pending;   // the 48-byte reference triangle records are built on first use
 };
 namespace chr {
+// the bucket index of ncomp CDFs of n entries (CDF c at cdf0 + c * stride):
+// (TIME_INDEX_BUCKETS + 1) words per CDF (sample_cdf_indexed, sampling.h); false
+// when one is not >= 2 finite non-decreasing entries (no index: plain bisection)
+bool time_cdf_index(const float *cdf0, uint32_t ncomp, uint32_t n, uint32_t stride, std::vector<uint32_t> &idx);
 // make every reference node and the reference triangle records resident in
 // HBM (no-op when they are); CHR_OK or an error
 int geometry_ref_nodes(const chr_geometry *g);

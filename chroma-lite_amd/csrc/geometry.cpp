@@ -5,11 +5,13 @@
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <new>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/chroma_amd.h"
@@ -28,13 +30,24 @@ extern "C" const char *chr_last_error(void) { return chr::last_error().c_str(); 
 
 namespace {
 
+// Physics tables as 32-bit words.  add() appends a block (a table with its pad
+// element, or a group of tables addressed from one offset) and returns its
+// offset; a block identical to one already added shares that copy (detectors
+// repeat the same tables across materials and surfaces, and the hot part has
+// to fit LDS, PhysCache in propagate.hip).
 struct Blob {
-    std::vector<float> data;
-    // append n+1 floats (table + its pad element) and return the offset
-    uint32_t add(const float *p, uint32_t n_with_pad) {
-        uint32_t off = (uint32_t)data.size();
-        if (p) data.insert(data.end(), p, p + n_with_pad);
-        else data.insert(data.end(), n_with_pad, 0.0f);
+    std::vector<uint32_t> data;
+    std::unordered_map<std::string, uint32_t> seen;
+    uint32_t add(const void *p, size_t nwords) {
+        if (nwords == 0) return (uint32_t)data.size();
+        std::string key(nwords * 4, '\0');
+        if (p) std::memcpy(&key[0], p, nwords * 4);
+        auto it = seen.find(key);
+        if (it != seen.end()) return it->second;
+        const uint32_t off = (uint32_t)data.size();
+        data.resize(data.size() + nwords);
+        std::memcpy(data.data() + off, key.data(), nwords * 4);
+        seen.emplace(std::move(key), off);
         return off;
     }
 };
@@ -57,6 +70,31 @@ int dev_upload(chr_geometry *g, const void *host, size_t bytes, void **dptr) {
 }
 
 }  // namespace
+
+// The bucket index of a re-emission time CDF (sample_cdf_indexed, sampling.h):
+// per component TIME_INDEX_BUCKETS+1 words, word b = the largest j with
+// cdf[j] <= b/TIME_INDEX_BUCKETS clamped to [0, n-2].  Only for CDFs of >= 2
+// finite non-decreasing entries (false otherwise: the kernel bisects the whole
+// table as the reference does, random.h:34-55).
+bool chr::time_cdf_index(const float *cdf0, uint32_t ncomp, uint32_t n, uint32_t stride, std::vector<uint32_t> &idx) {
+    if (n < 2 || ncomp == 0) return false;
+    for (uint32_t c = 0; c < ncomp; ++c) {
+        const float *cdf = cdf0 + (size_t)c * stride;
+        for (uint32_t j = 0; j < n; ++j)
+            if (!std::isfinite(cdf[j]) || (j + 1 < n && !(cdf[j] <= cdf[j + 1]))) return false;
+    }
+    const uint32_t NB = chr::TIME_INDEX_BUCKETS;
+    idx.assign((size_t)ncomp * (NB + 1), 0u);
+    for (uint32_t c = 0; c < ncomp; ++c) {
+        const float *cdf = cdf0 + (size_t)c * stride;
+        for (uint32_t b = 0; b <= NB; ++b) {
+            const float x = (float)b / (float)NB;          // exact: NB is a power of two
+            const int64_t cnt = std::upper_bound(cdf, cdf + n, x) - cdf;
+            idx[(size_t)c * (NB + 1) + b] = (uint32_t)std::min<int64_t>(std::max<int64_t>(cnt - 1, 0), n - 2);
+        }
+    }
+    return true;
+}
 
 extern "C" int chr_geometry_destroy(chr_geometry *g) {
     if (!g) return CHR_OK;
@@ -110,6 +148,13 @@ int chr::geometry_ref_nodes(const chr_geometry *cg) {
 extern "C" int chr_geometry_device_bytes(const chr_geometry *g, uint64_t *bytes) {
     if (!g || !bytes) return chr::fail(CHR_ERR_INVALID, "chr_geometry_device_bytes: null argument");
     *bytes = g->bytes;
+    return CHR_OK;
+}
+
+extern "C" int chr_geometry_phys_words(const chr_geometry *g, uint32_t *hot_words, uint32_t *total_words) {
+    if (!g || !hot_words || !total_words) return chr::fail(CHR_ERR_INVALID, "chr_geometry_phys_words: null argument");
+    *hot_words = g->dev.phys_hot_words;
+    *total_words = g->dev.phys_words;
     return CHR_OK;
 }
 
@@ -345,16 +390,18 @@ static int geometry_create(const chr_geometry_desc *d, const chr_wide_bvh_desc *
             o.refractive_index = blob.add(m.refractive_index, W1);
             o.absorption_length = blob.add(m.absorption_length, W1);
             o.scattering_length = blob.add(m.scattering_length, W1);
-            // the components' tables (bulk re-emission, 20,000-entry time CDFs) go in a
-            // second blob after the records: the hot part before them fits in LDS
-            o.comp_reemission_prob = (uint32_t)comp.data.size();
-            for (uint32_t c = 0; c < m.num_comp; ++c) comp.add(m.comp_reemission_prob + c * W1, W1);
-            o.comp_reemission_wvl_cdf = (uint32_t)comp.data.size();
-            for (uint32_t c = 0; c < m.num_comp; ++c) comp.add(m.comp_reemission_wvl_cdf + c * W1, W1);
-            o.comp_reemission_time_cdf = (uint32_t)comp.data.size();
-            for (uint32_t c = 0; c < m.num_comp; ++c) comp.add(m.comp_reemission_time_cdf + c * T1, T1);
-            o.comp_absorption_length = (uint32_t)comp.data.size();
-            for (uint32_t c = 0; c < m.num_comp; ++c) comp.add(m.comp_absorption_length + c * W1, W1);
+            // the components' wavelength tables (a group each, component c at + c*W1) stay
+            // with the hot tables; the 20,000-entry time CDFs and their bucket index go in a
+            // second blob after the records (read from HBM: the hot part fits LDS)
+            const size_t nc = m.num_comp;
+            o.comp_reemission_prob = blob.add(m.comp_reemission_prob, nc * W1);
+            o.comp_reemission_wvl_cdf = blob.add(m.comp_reemission_wvl_cdf, nc * W1);
+            o.comp_absorption_length = blob.add(m.comp_absorption_length, nc * W1);
+            o.comp_reemission_time_cdf = comp.add(m.comp_reemission_time_cdf, nc * T1);
+            o.comp_time_index = ~0u;
+            std::vector<uint32_t> idx;
+            if (nc && chr::time_cdf_index(m.comp_reemission_time_cdf, m.num_comp, d->time_n, T1, idx))
+                o.comp_time_index = comp.add(idx.data(), idx.size());
         }
         std::vector<chr::DevSurface> surfs(d->nsurfaces > 0 ? d->nsurfaces : 1);
         std::memset(surfs.data(), 0, surfs.size() * sizeof(chr::DevSurface));
@@ -383,10 +430,8 @@ static int geometry_create(const chr_geometry_desc *d, const chr_wide_bvh_desc *
             o.dichroic_nangles = s.dichroic_nangles;
             if (s.dichroic_nangles) {
                 o.dichroic_angles = blob.add(s.dichroic_angles, s.dichroic_nangles);
-                o.dichroic_reflect = (uint32_t)blob.data.size();
-                blob.data.insert(blob.data.end(), s.dichroic_reflect, s.dichroic_reflect + (size_t)s.dichroic_nangles * W1);
-                o.dichroic_transmit = (uint32_t)blob.data.size();
-                blob.data.insert(blob.data.end(), s.dichroic_transmit, s.dichroic_transmit + (size_t)s.dichroic_nangles * W1);
+                o.dichroic_reflect = blob.add(s.dichroic_reflect, (size_t)s.dichroic_nangles * W1);
+                o.dichroic_transmit = blob.add(s.dichroic_transmit, (size_t)s.dichroic_nangles * W1);
             }
             o.angular_nangles = s.angular_nangles;
             if (s.angular_nangles) {
@@ -397,8 +442,7 @@ static int geometry_create(const chr_geometry_desc *d, const chr_wide_bvh_desc *
             }
         }
         {   // one allocation [tables | materials | surfaces], 16-byte aligned parts (DevGeom::phys)
-            std::vector<uint32_t> phys(blob.data.size());
-            std::memcpy(phys.data(), blob.data.data(), blob.data.size() * 4);
+            std::vector<uint32_t> phys(blob.data);
             phys.resize((phys.size() + 3) & ~(size_t)3, 0u);
             const uint32_t mat_off = (uint32_t)phys.size();
             phys.resize(phys.size() + mats.size() * sizeof(chr::DevMaterial) / 4);
@@ -409,12 +453,10 @@ static int geometry_create(const chr_geometry_desc *d, const chr_wide_bvh_desc *
             std::memcpy(phys.data() + surf_off, surfs.data(), surfs.size() * sizeof(chr::DevSurface));
             phys.resize((phys.size() + 3) & ~(size_t)3, 0u);
             const uint32_t hot = (uint32_t)phys.size();
-            // material component offsets: relative to the phys base, past the records
+            // the cold offsets: relative to the phys base, past the records
             for (auto &m : mats) {
-                m.comp_reemission_prob += hot;
-                m.comp_reemission_wvl_cdf += hot;
                 m.comp_reemission_time_cdf += hot;
-                m.comp_absorption_length += hot;
+                if (m.comp_time_index != ~0u) m.comp_time_index += hot;
             }
             std::memcpy(phys.data() + mat_off, mats.data(), mats.size() * sizeof(chr::DevMaterial));
             phys.resize(phys.size() + comp.data.size());

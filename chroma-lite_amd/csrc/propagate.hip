@@ -1033,16 +1033,23 @@ __device__ __forceinline__ int propagate_to_boundary(const DevGeom &g, Photon &p
             float prob = 0.0f;
             uint32_t comp;
             for (comp = 0;; comp++) {
-                const float comp_abs = interp_property(g, p.wavelength, g.tables_g + m.comp_absorption_length + comp * W1);
+                const float comp_abs = interp_property(g, p.wavelength, g.tables + m.comp_absorption_length + comp * W1);
                 prob += s.absorption_length / comp_abs;
                 if (usc < prob || comp + 1 == m.num_comp) break;
             }
             const float usr = chr_uniform01(&rng);
-            const float crp = interp_property(g, p.wavelength, g.tables_g + m.comp_reemission_prob + comp * W1);
+            const float crp = interp_property(g, p.wavelength, g.tables + m.comp_reemission_prob + comp * W1);
             if (usr < crp) {
                 p.wavelength = sample_cdf(rng, (int)g.wl_n, g.wl_start, g.wl_step,
-                                          g.tables_g + m.comp_reemission_wvl_cdf + comp * W1);
-                p.time += sample_cdf(rng, (int)g.t_n, g.t_start, g.t_step, g.tables_g + m.comp_reemission_time_cdf + comp * T1);
+                                          g.tables + m.comp_reemission_wvl_cdf + comp * W1);
+                const float *tcdf = g.tables_g + m.comp_reemission_time_cdf + comp * T1;
+                if (m.comp_time_index != ~0u)
+                    p.time += sample_cdf_indexed(rng, g.t_start, g.t_step, tcdf,
+                                                 (const uint32_t *)g.tables_g + m.comp_time_index +
+                                                     comp * (TIME_INDEX_BUCKETS + 1),
+                                                 TIME_INDEX_BUCKETS);
+                else
+                    p.time += sample_cdf(rng, (int)g.t_n, g.t_start, g.t_step, tcdf);
                 p.dir = uniform_sphere(rng);
                 p.pol = cross(uniform_sphere(rng), p.dir);
                 p.pol = p.pol / norm(p.pol);
@@ -1625,12 +1632,12 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_step_kernel(const DevGe
 // to use -- tables / materials / surfaces pointing into LDS when they fit in
 // cap_words, else g unchanged.
 constexpr uint32_t SHADE_PHYS_WORDS = 12288;   // 48 KB: 3 workgroups of shade_kernel<3> per CU
-// (only DevGeom::phys_hot_words are copied: the materials' component tables stay in HBM)
+// (only DevGeom::phys_hot_words are copied: the re-emission time CDFs stay in HBM)
 constexpr uint32_t TAIL_PHYS_WORDS = 8192;     // 32 KB: 2 tail workgroups (+ 40 KB of walk stacks each)
 __device__ __forceinline__ DevGeom phys_cache(const DevGeom &g, uint4 *lds, uint32_t cap_words) {
     DevGeom gl = g;
     if (g.phys && g.phys_hot_words <= cap_words) {   // workgroup-uniform
-        // the hot part: tables and records; the component tables stay global (tables_g)
+        // the hot part: tables and records; the time CDFs stay global (tables_g)
         const uint4 *src = reinterpret_cast<const uint4 *>(g.phys);
         for (uint32_t i = threadIdx.x; i < g.phys_hot_words / 4u; i += BLOCK) lds[i] = src[i];
         __syncthreads();
@@ -4184,7 +4191,7 @@ static int slot_ctl_get(size_t words, uint32_t **out, int ctx = 0) {
 // [2,3] around trace_kernel, [4] slot done (ring copied), [5,6] around the tail
 // kernel when it runs on the tail stream, [7] start of the rest of a slot whose
 // prefix ran on the prefix stream (chr_propagate_batches)
-constexpr int SLOT_EVENTS = 9;   // [8]: end of a split prefix's binning part
+constexpr int SLOT_EVENTS = 8;
 
 // Device buffers of one propagate (context ctx of the calling thread):
 // queues, step scratch, the split path's hits / binning region, the flat-walk
@@ -4370,11 +4377,10 @@ static int slot_stats(chr_propagate_stats &st, const uint32_t *h, int k, const s
             continue;
         }
         if (j == 0 && prefixed) {   // the prefix on its stream (binning, walk), the rest after it on the batch stream
-            float ms2 = 0.0f, ms3 = 0.0f;
-            CHR_HIP_CHECK(hipEventElapsedTime(&ms, ev[0], ev[8]));
-            CHR_HIP_CHECK(hipEventElapsedTime(&ms2, ev[2], ev[3]));
-            CHR_HIP_CHECK(hipEventElapsedTime(&ms3, ev[7], ev[1]));
-            ms += ms2 + ms3;
+            float ms2 = 0.0f;
+            CHR_HIP_CHECK(hipEventElapsedTime(&ms, ev[0], ev[3]));    // head, binning, trace
+            CHR_HIP_CHECK(hipEventElapsedTime(&ms2, ev[7], ev[1]));   // shade, scan, scatter
+            ms += ms2;
         } else {
             CHR_HIP_CHECK(hipEventElapsedTime(&ms, ev[0], ev[1]));
         }

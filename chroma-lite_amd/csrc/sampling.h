@@ -64,4 +64,24 @@ __device__ float sample_cdf(chr_xorwow &rng, int ncdf, float x0, float delta, co
     return __builtin_fmaf(delta, (float)lower, x0) + (delta * (u - cdf_y[lower])) / dcy;
 }
 
+// random.h:34-55 over a non-decreasing CDF of >= 2 entries with a bucket index
+// (index[b] = the largest j with cdf_y[j] <= b/nb clamped to [0, ncdf-2], nb a
+// power of two; geometry.cpp time_cdf_index).  The reference's bisection ends on
+// lower = the largest j with cdf_y[j] <= u clamped to [0, ncdf-2]; u lies in
+// [b/nb, (b+1)/nb] for b = min(floor(u*nb), nb-1), so that j lies in
+// [index[b], index[b+1]] and a bisection of that range finds the same lower: the
+// same sample, from ~log2(ncdf/nb) probes instead of log2(ncdf).
+__device__ float sample_cdf_indexed(chr_xorwow &rng, float x0, float delta, const float *cdf_y,
+                                    const uint32_t *index, uint32_t nb) {
+    const float u = chr_uniform01(&rng);
+    const uint32_t b = min((uint32_t)(u * (float)nb), nb - 1u);
+    int lower = (int)index[b], upper = (int)index[b + 1];
+    while (lower < upper) {                 // the largest j in [lower, upper] with cdf_y[j] <= u, else lower
+        const int half = (lower + upper + 1) >> 1;
+        if (cdf_y[half] <= u) lower = half; else upper = half - 1;
+    }
+    const float dcy = cdf_y[lower + 1] - cdf_y[lower];
+    return __builtin_fmaf(delta, (float)lower, x0) + (delta * (u - cdf_y[lower])) / dcy;
+}
+
 }  // namespace chr

@@ -7,11 +7,13 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <vector>
 
 #include "../../include/chroma_amd.h"
 #include "common.h"
 #include "device_math.h"
 #include "sampling.h"
+#include "device_geometry.h"
 
 namespace chr {
 namespace {
@@ -63,13 +65,15 @@ __global__ __launch_bounds__(TB) void rotate_kernel(uint32_t n, const float *A, 
 // test/test_sample_cdf.cu: one draw per slot from its (curand_init-ed) state
 __global__ __launch_bounds__(TB) void sample_cdf_kernel(uint32_t n, const uint32_t *states, uint32_t nslots, int ncdf,
                                                         const float *cdf_x, const float *cdf_y, float x0, float delta,
-                                                        int uniform_grid, float *out) {
+                                                        int uniform_grid, const uint32_t *index, float *out) {
     const uint32_t i = blockIdx.x * TB + threadIdx.x;
     if (i >= n) return;
     chr_xorwow s;
     s.d = states[i]; s.v0 = states[nslots + i]; s.v1 = states[2 * nslots + i];
     s.v2 = states[3 * nslots + i]; s.v3 = states[4 * nslots + i]; s.v4 = states[5 * nslots + i];
-    out[i] = uniform_grid ? sample_cdf(s, ncdf, x0, delta, cdf_y) : sample_cdf(s, ncdf, cdf_x, cdf_y);
+    out[i] = uniform_grid == 2 ? sample_cdf_indexed(s, x0, delta, cdf_y, index, TIME_INDEX_BUCKETS)
+             : uniform_grid  ? sample_cdf(s, ncdf, x0, delta, cdf_y)
+                             : sample_cdf(s, ncdf, cdf_x, cdf_y);
 }
 
 inline unsigned blocks(uint32_t n) { return (n + TB - 1) / TB; }
@@ -102,10 +106,27 @@ extern "C" int chr_selftest_sample_cdf(uint32_t n, const uint32_t *d_states, uin
                                        const float *d_cdf_x, const float *d_cdf_y, float x0, float delta,
                                        int32_t uniform_grid, float *d_out, void *stream) {
     if (n == 0) return CHR_OK;
-    if (!d_states || !d_cdf_y || !d_out || (!uniform_grid && !d_cdf_x) || n > nslots || ncdf < 2)
+    if (!d_states || !d_cdf_y || !d_out || (!uniform_grid && !d_cdf_x) || n > nslots || ncdf < 2 || uniform_grid < 0 ||
+        uniform_grid > 2)
         return chr::fail(CHR_ERR_INVALID, "chr_selftest_sample_cdf: bad argument");
+    uint32_t *d_index = nullptr;
+    if (uniform_grid == 2) {   // the geometry upload's bucket index of the CDF (synchronous)
+        std::vector<float> h((size_t)ncdf);
+        std::vector<uint32_t> idx;
+        CHR_HIP_CHECK(hipStreamSynchronize((hipStream_t)stream));
+        CHR_HIP_CHECK(hipMemcpy(h.data(), d_cdf_y, h.size() * 4, hipMemcpyDeviceToHost));
+        if (!chr::time_cdf_index(h.data(), 1, (uint32_t)ncdf, (uint32_t)ncdf, idx))
+            return chr::fail(CHR_ERR_INVALID, "chr_selftest_sample_cdf: CDF not indexable (non-finite or decreasing)");
+        CHR_HIP_CHECK(hipMalloc(&d_index, idx.size() * 4));
+        CHR_HIP_CHECK(hipMemcpy(d_index, idx.data(), idx.size() * 4, hipMemcpyHostToDevice));
+    }
     hipLaunchKernelGGL(chr::sample_cdf_kernel, dim3(chr::blocks(n)), dim3(chr::TB), 0, (hipStream_t)stream, n, d_states,
-                       nslots, ncdf, d_cdf_x, d_cdf_y, x0, delta, uniform_grid, d_out);
-    CHR_HIP_CHECK(hipGetLastError());
+                       nslots, ncdf, d_cdf_x, d_cdf_y, x0, delta, uniform_grid, d_index, d_out);
+    hipError_t e = hipGetLastError();
+    if (d_index) {
+        if (e == hipSuccess) e = hipStreamSynchronize((hipStream_t)stream);
+        (void)hipFree(d_index);
+    }
+    if (e != hipSuccess) return chr::fail(CHR_ERR_HIP, "chr_selftest_sample_cdf: %s", hipGetErrorString(e));
     return CHR_OK;
 }

@@ -117,6 +117,11 @@ int chr_geometry_create(const chr_geometry_desc *desc, chr_geometry **out);
 int chr_geometry_destroy(chr_geometry *g);
 /* bytes of HBM held by the geometry (reference: GPUGeometry.device_usage_str) */
 int chr_geometry_device_bytes(const chr_geometry *g, uint64_t *bytes);
+/* words (4 B) of the physics tables and records: the hot part the step kernels
+ * copy to LDS when it fits (property tables, identical tables stored once, the
+ * material / surface records) and the whole (+ re-emission time CDFs and their
+ * bucket indexes, read from HBM).  No reference counterpart (diagnostic). */
+int chr_geometry_phys_words(const chr_geometry *g, uint32_t *hot_words, uint32_t *total_words);
 
 /* ----------------------------------------------------------------- photons */
 typedef struct chr_photons {               /* reference GPUPhotons arrays, photon.py:46-62 */
@@ -496,7 +501,9 @@ int chr_selftest_rotate(uint32_t n, const float *d_a, const float *d_phi, float 
                         float *d_out, void *stream);
 /* replaces: test/test_sample_cdf.cu (random.h:27-55): one draw per slot i < n from
  * RNG slot state i (SoA, chr_init_rng layout; states are not written back);
- * uniform_grid = 0: sample_cdf(cdf_x, cdf_y), 1: sample_cdf(x0, delta, cdf_y) */
+ * uniform_grid = 0: sample_cdf(cdf_x, cdf_y), 1: sample_cdf(x0, delta, cdf_y),
+ * 2: the bucket-indexed form of 1 the propagate kernels use for re-emission time
+ * CDFs (index built as chr_geometry_create builds it; synchronous) */
 int chr_selftest_sample_cdf(uint32_t n, const uint32_t *d_states, uint32_t nslots, int32_t ncdf,
                             const float *d_cdf_x, const float *d_cdf_y, float x0, float delta,
                             int32_t uniform_grid, float *d_out, void *stream);

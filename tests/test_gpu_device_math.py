@@ -185,3 +185,49 @@ def test_sample_cdf_uniform_grid():
     cdf = lambda v: np.interp(v, cdf_x, cdf_y)
     reps = [stats.kstest(s.astype(np.float64), cdf).pvalue for s in samples]
     assert stats.kstest(reps, 'uniform').pvalue > 0.01, reps
+
+
+def _cdfs(u_hit):
+    """CDFs for the indexed sampler: Gaussian, an exponential decay time CDF of
+    20,000 entries (long flat tail), steps with repeated values, entries exactly
+    at bucket edges and at the draws' own uniforms, a CDF starting above 0 and
+    one ending below 1, and the 2- and 3-entry minimum."""
+    g = _gaussian_cdf_tables()[1]
+    t = np.arange(20000, dtype=np.float64) * 0.05
+    expo = (1 - np.exp(-t / 40.0)).astype(np.float32)
+    steps = np.repeat(np.linspace(0, 1, 9, dtype=np.float32), 7)
+    edges = (np.arange(4097, dtype=np.float32) / 4096).astype(np.float32)
+    hits = np.sort(np.concatenate([u_hit, u_hit[::3], [0.0, 1.0]]).astype(np.float32))
+    return {'gauss': g, 'expo': expo, 'steps': steps, 'edges': edges, 'hits': hits,
+            'above0': np.linspace(0.3, 1, 50, dtype=np.float32), 'below1': np.linspace(0, 0.6, 50, dtype=np.float32),
+            'n2': np.array([0, 1], np.float32), 'n3': np.array([0.2, 0.2, 0.9], np.float32)}
+
+
+def test_sample_cdf_indexed_same_samples():
+    """The bucket-indexed sampler the kernels use for re-emission time CDFs
+    (sampling.h sample_cdf_indexed, index from chr_geometry_create) draws
+    exactly the sample of the reference's bisection (random.h:34-55) -- bit
+    for bit, flat stretches, exact-edge and exact-uniform entries included --
+    and a decreasing CDF is refused (the kernel then bisects the whole table)."""
+    import oracle
+    from chroma import gpu
+    from chroma.gpu import _native
+    from chroma.gpu import gpuarray as ga
+    n = 1 << 16
+    st = gpu.get_rng_states(n, seed=5)
+    host = oracle.rng_init(n, seed=5)
+    u_hit = np.array([oracle.uniforms(host, n, s, 1)[0] for s in range(0, n, 31)], np.float32)
+    out1, out2 = ga.empty(n, np.float32), ga.empty(n, np.float32)
+    for name, cdf in _cdfs(u_hit).items():
+        dy = _dev(cdf)
+        _call('chr_selftest_sample_cdf', n, st.gpudata, n, len(cdf), None, dy.gpudata, ctypes.c_float(-1.5),
+              ctypes.c_float(0.05), 1, out1.gpudata)
+        _call('chr_selftest_sample_cdf', n, st.gpudata, n, len(cdf), None, dy.gpudata, ctypes.c_float(-1.5),
+              ctypes.c_float(0.05), 2, out2.gpudata)
+        a, b = out1.get(), out2.get()
+        assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), (name, np.flatnonzero(a.view(np.uint32) !=
+                                                                                          b.view(np.uint32))[:5])
+    bad = _dev(np.array([0, 0.5, 0.4, 1], np.float32))
+    with pytest.raises(_native.NativeError, match='not indexable'):
+        _call('chr_selftest_sample_cdf', n, st.gpudata, n, 4, None, bad.gpudata, ctypes.c_float(0), ctypes.c_float(1),
+              2, out2.gpudata)

@@ -203,3 +203,16 @@ def test_scintillator_detector_parity(cuda):
     hits = gp.get_flat_hits(gpu.GPUDetector(geo))
     idx, ch = oracle.hits(host, geo.solid_id, geo.solid_id_to_channel_index)
     assert np.array_equal(hits.channel.astype(np.int64), ch.astype(np.int64))
+
+
+def test_scintillator_physics_tables_fit_lds(cuda):
+    """The scintillator geometry's hot physics tables (identical tables stored
+    once; the components' wavelength tables included) fit the tail kernel's
+    LDS copy (propagate.hip TAIL_PHYS_WORDS = 8192 words); the 20,000-entry
+    time CDFs and their bucket indexes stay in HBM."""
+    from chroma import gpu, loader
+    from chroma.demo import scint
+    geo = loader.create_geometry_from_obj(scint.tiny())
+    hot, total = gpu.GPUGeometry(geo).phys_words()
+    assert hot <= 8192, hot
+    assert total - hot >= 2 * 20000, (hot, total)
