@@ -3716,10 +3716,12 @@ static StepVariant select_step_variant(const chr_geometry *g) {
     switch (v) {
         case 2: sv.fn = propagate_step_kernel<8, 4, kWalk>; break;
         case 3: sv.fn = propagate_step_kernel<8, 4, kWalk, true>; break;
-        case 5:
+        case 5:   // walk counters of the one-step launches' trace kernel; the tail as variant 0
             sv.fn = propagate_step_kernel<8, 4, kWalk, true>;
             sv.trace = trace_kernel<true, 6, 12, 4, 32>;
             sv.shade = shade_kernel<3>;
+            sv.tail = propagate_tail_kernel<kTailWaves>;
+            sv.tail_group = 8;
             sv.binned = 2;
             break;
         default:   // 0, 7, 8
@@ -4465,7 +4467,8 @@ static int check_propagate_args(const char *fn, const chr_geometry *g, const chr
 }
 
 static bool device_steps_ok(const chr_geometry *g, const PropBufs &b) {
-    return b.fused && !trace_steps() && !host_steps_forced() && select_step_variant(g).trace != nullptr;
+    const StepVariant sv = select_step_variant(g);
+    return b.fused && !trace_steps() && !host_steps_forced() && sv.trace && sv.tail;   // a slot queues both
 }
 
 extern "C" int chr_propagate(const chr_geometry *g, const chr_photons *ph, uint32_t nphotons, uint32_t true_nphotons,
