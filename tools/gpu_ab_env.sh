@@ -19,7 +19,7 @@ if [ "$TESTS" != "-" ]; then
   tail -2 "$O/pytest.log"
 fi
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 900 python3 -u "$R/tools/ab_env.py" --steps 20 --warmup 5 -- "$@" > "$O/ab.jsonl" 2> "$O/ab.log" \
+timeout -k 10 900 python3 -u "$R/tools/ab_env.py" --steps 20 --warmup 5 ${AB_ARGS:-} -- "$@" > "$O/ab.jsonl" 2> "$O/ab.log" \
     || { tail -20 "$O/ab.log"; exit 1; }
 python3 - "$O/ab.jsonl" <<'PY'
 import json, sys, collections
