@@ -1419,9 +1419,6 @@ struct PropagateArgs {
     // zeroed counter the photon groups take queue positions from, for queues no longer than
     // the slot count (each position then its own RNG slot, loaded and stored per photon)
     uint32_t *work;
-    // shade kernel, walk order of the next step (nullptr: off): each survivor's bucket
-    // (walk_key) at its queue position, and the buckets' histogram
-    uint32_t *wkey, *whist;
 };
 // modes of a device-driven step slot (step_head_kernel)
 constexpr uint32_t STEP_IDLE = 0, STEP_ONE = 1, STEP_TAIL = 2;
@@ -1649,50 +1646,6 @@ __device__ __forceinline__ DevGeom phys_cache(const DevGeom &g, uint4 *lds, uint
     return gl;
 }
 
-constexpr int BIN_KEY_BITS_DEV = 22;   // octa_cell keys: 11 + 11 bits
-__device__ __forceinline__ uint32_t octa_cell(V3 d) {   // octahedral map of a unit vector, Hilbert order of 11+11-bit cells
-    const float s = fabsf(d.x) + fabsf(d.y) + fabsf(d.z);
-    float u = d.x / s, v = d.y / s;
-    if (d.z < 0.0f) {
-        const float uu = (1.0f - fabsf(v)) * (u < 0.0f ? -1.0f : 1.0f);
-        const float vv = (1.0f - fabsf(u)) * (v < 0.0f ? -1.0f : 1.0f);
-        u = uu; v = vv;
-    }
-    uint32_t x = (uint32_t)fminf(fmaxf((u + 1.0f) * 1024.0f, 0.0f), 2047.0f);
-    uint32_t y = (uint32_t)fminf(fmaxf((v + 1.0f) * 1024.0f, 0.0f), 2047.0f);
-    uint32_t dkey = 0;
-    for (uint32_t sq = 1024u; sq > 0u; sq >>= 1) {   // Hilbert order: no jumps between quadrants
-        const uint32_t rx = (x & sq) ? 1u : 0u, ry = (y & sq) ? 1u : 0u;
-        dkey += sq * sq * ((3u * rx) ^ ry);
-        if (ry == 0u) {   // rotate the quadrant
-            if (rx == 1u) { x = 2047u - x; y = 2047u - y; }
-            const uint32_t t = x; x = y; y = t;
-        }
-    }
-    return dkey;
-}
-// direction-binning key of a queued photon (0 for a zero / non-finite direction)
-__device__ __forceinline__ uint32_t bin_key_of(V3 d) {
-    const float l = sqrtf(d.x * d.x + d.y * d.y + d.z * d.z);
-    return (l > 0.0f && l < __builtin_inff()) ? octa_cell(v3(d.x / l, d.y / l, d.z / l)) : 0u;
-}
-// Walk order of the steps after the first (CHR_WALK_ORDER): trace_kernel walks the
-// next step's rays bucket by bucket instead of in queue order -- a photon's next walk
-// starts on the triangle it just hit, so rays leaving one PMT walk together (its
-// subtree's nodes and triangles in L1/L2 for the whole bucket).  Buckets [0, 2^15):
-// the hit triangle's id scaled over the mesh (Geometry.flatten numbers a solid's
-// triangles together, and the spiral of PMTs puts neighbours next to each other);
-// [2^15, 2^16): photons without a hit (bulk scatter / re-emission) by direction cell.
-// The key is computed once, by the shade pass (wkey), and the scatter places each
-// survivor's ray record at its bucket's next slot; the order of the walks never
-// changes a result.
-constexpr uint32_t WALK_BUCKETS = 1u << 16;
-__device__ __forceinline__ uint32_t walk_key(const DevGeom &g, int last_hit, V3 dir) {
-    if (last_hit >= 0 && (uint32_t)last_hit < g.ntriangles)
-        return (uint32_t)(((unsigned long long)last_hit * (WALK_BUCKETS / 2)) / g.ntriangles);
-    return WALK_BUCKETS / 2 + (bin_key_of(dir) >> (BIN_KEY_BITS_DEV - 15));
-}
-
 struct QueuedPhoton {
     uint32_t pid, history;
     V3 pos, dir, pol;
@@ -1795,11 +1748,6 @@ __global__ __launch_bounds__(BLOCK, MINW) void shade_kernel(const DevGeom *__res
                 pf.tick(P_OTHER);
             }
             alive = (p.history & DEAD_MASK) == 0;
-            if (alive && a.wkey) {   // the next step's walk bucket (scatter_queue_kernel places the ray by it)
-                const uint32_t k = walk_key(g, p.last_hit, p.dir);
-                a.wkey[pos] = k;
-                atomicAdd(a.whist + k, 1u);
-            }
         }
         // the prefetched photon and queue entry waited for here, on every path and
         // before the write-back (see above)
@@ -2686,6 +2634,32 @@ __global__ __launch_bounds__(BLOCK) void ref_triangles_kernel(const float4 *wtri
 // step's rays are binned by direction cell (a 22-bit radix sort of 2^22
 // octahedral cells in Hilbert order; rounds 1-3: 16 bits, 65,536 cells row-major)
 // to make the 64 rays of a wave walk the same subtrees: better L1/L2 reuse of nodes.
+__device__ __forceinline__ uint32_t octa_cell(V3 d) {   // octahedral map of a unit vector, Hilbert order of 11+11-bit cells
+    const float s = fabsf(d.x) + fabsf(d.y) + fabsf(d.z);
+    float u = d.x / s, v = d.y / s;
+    if (d.z < 0.0f) {
+        const float uu = (1.0f - fabsf(v)) * (u < 0.0f ? -1.0f : 1.0f);
+        const float vv = (1.0f - fabsf(u)) * (v < 0.0f ? -1.0f : 1.0f);
+        u = uu; v = vv;
+    }
+    uint32_t x = (uint32_t)fminf(fmaxf((u + 1.0f) * 1024.0f, 0.0f), 2047.0f);
+    uint32_t y = (uint32_t)fminf(fmaxf((v + 1.0f) * 1024.0f, 0.0f), 2047.0f);
+    uint32_t dkey = 0;
+    for (uint32_t sq = 1024u; sq > 0u; sq >>= 1) {   // Hilbert order: no jumps between quadrants
+        const uint32_t rx = (x & sq) ? 1u : 0u, ry = (y & sq) ? 1u : 0u;
+        dkey += sq * sq * ((3u * rx) ^ ry);
+        if (ry == 0u) {   // rotate the quadrant
+            if (rx == 1u) { x = 2047u - x; y = 2047u - y; }
+            const uint32_t t = x; x = y; y = t;
+        }
+    }
+    return dkey;
+}
+// direction-binning key of a queued photon (0 for a zero / non-finite direction)
+__device__ __forceinline__ uint32_t bin_key_of(V3 d) {
+    const float l = sqrtf(d.x * d.x + d.y * d.y + d.z * d.z);
+    return (l > 0.0f && l < __builtin_inff()) ? octa_cell(v3(d.x / l, d.y / l, d.z / l)) : 0u;
+}
 __global__ __launch_bounds__(BLOCK) void bin_key_kernel(const float *dir, const uint32_t *queue, uint32_t n,
                                                         uint32_t *keys, uint32_t *vals) {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
@@ -3190,10 +3164,8 @@ __device__ __forceinline__ uint32_t slot_head(uint32_t n, const HeadNext &h) {
 __global__ __launch_bounds__(1024) void scan_block_sums_kernel(uint32_t *block_sums, uint32_t nblocks,
                                                                uint32_t *out_counter, uint32_t *base,
                                                                uint32_t *total_out, const uint32_t *mode,
-                                                               uint32_t skip, uint32_t fresh, HeadNext hn,
-                                                               uint32_t *whist, uint32_t *wcursor) {
+                                                               uint32_t skip, uint32_t fresh, HeadNext hn) {
     __shared__ uint32_t partial[1024];
-    __shared__ uint32_t wpartial[1024];
     if (mode && (*mode == STEP_IDLE || *mode == skip)) {
         if (hn.mode && threadIdx.x == 0) slot_head(0u, hn);
         return;
@@ -3229,26 +3201,6 @@ __global__ __launch_bounds__(1024) void scan_block_sums_kernel(uint32_t *block_s
         if (total_out) total_out[0] = total;
         if (hn.mode) slot_head(total, hn);   // the next slot's queue is this slot's survivors
     }
-    if (whist) {   // the next step's walk buckets: exclusive prefix -> wcursor, histogram cleared
-        constexpr uint32_t PER = WALK_BUCKETS / 1024;
-        uint32_t wsum = 0;
-        for (uint32_t k = 0; k < PER; ++k) wsum += whist[tid * PER + k];
-        wpartial[tid] = wsum;
-        __syncthreads();
-        for (uint32_t off = 1; off < 1024; off <<= 1) {
-            const uint32_t v = (tid >= off) ? wpartial[tid - off] : 0;
-            __syncthreads();
-            wpartial[tid] += v;
-            __syncthreads();
-        }
-        uint32_t wrun = wpartial[tid] - wsum;
-        for (uint32_t k = 0; k < PER; ++k) {
-            const uint32_t v = whist[tid * PER + k];
-            wcursor[tid * PER + k] = wrun;
-            whist[tid * PER + k] = 0u;
-            wrun += v;
-        }
-    }
 }
 
 __device__ __forceinline__ uint32_t word_offset(const uint32_t *word_offsets, const uint32_t *block_prefix, uint32_t w) {
@@ -3264,10 +3216,6 @@ struct FlatEnrol {
     unsigned long long *flat_best;
     uint4 *rays;                 // + the next step's ray records, in queue order (nullptr: off)
     const int32_t *last_hit;
-    // walk order (nullptr: queue order): a survivor's record goes to the next free slot
-    // of its bucket (wkey[queue position], cursors from scan_block_sums_kernel)
-    const uint32_t *wkey;
-    uint32_t *wcursor;
 };
 __global__ __launch_bounds__(BLOCK) void scatter_queue_kernel(const unsigned long long *masks, const uint32_t *word_offsets,
                                                                const uint32_t *block_prefix, const uint32_t *base,
@@ -3288,12 +3236,9 @@ __global__ __launch_bounds__(BLOCK) void scatter_queue_kernel(const unsigned lon
             const uint32_t pid = in_queue[first + id];
             out_queue[o] = pid;
             // out_queue[0] is the count header: position o - 1 of the next step's queue
-            if (fe.pos) {
-                uint32_t j = o - 1u;   // the record's walk position
-                if (fe.wcursor && (!mode || *mode == STEP_ONE)) j = atomicAdd(fe.wcursor + fe.wkey[first + id], 1u);
+            if (fe.pos)
                 enrol_flat(fe.pos, fe.dir, pid, o - 1u, fe.hits, fe.flat_q, fe.flat_count, fe.flat_best, fe.rays,
-                           fe.last_hit, j);
-            }
+                           fe.last_hit, o - 1u);
         }
     }
 }
@@ -3475,13 +3420,13 @@ inline uint32_t scan_blocks(uint32_t nwords) { return (nwords + SCAN_WORDS - 1) 
 void launch_mask_scan(const unsigned long long *masks, uint32_t nwords, uint32_t *word_offsets, uint32_t *block_sums,
                       uint32_t *out_counter, uint32_t *base, uint32_t *total_out, hipStream_t stream,
                       const uint32_t *dev_n = nullptr, const uint32_t *mode = nullptr, uint32_t skip = STEP_IDLE,
-                      const HeadNext *hn = nullptr, uint32_t *whist = nullptr, uint32_t *wcursor = nullptr) {
+                      const HeadNext *hn = nullptr) {
     const uint32_t nb = scan_blocks(nwords);   // device-driven: nwords is an upper bound
     if (nb) hipLaunchKernelGGL(mask_block_scan_kernel, dim3(nb), dim3(SCAN_WORDS), 0, stream, masks, nwords, word_offsets,
                                block_sums, dev_n, mode, skip);
     hipLaunchKernelGGL(scan_block_sums_kernel, dim3(1), dim3(1024), 0, stream, block_sums, nb, out_counter, base,
                        total_out, mode, skip, dev_n ? 1u : 0u,
-                       hn ? *hn : HeadNext{nullptr, nullptr, nullptr, nullptr, nullptr, 0u, 0u, 0, 0}, whist, wcursor);
+                       hn ? *hn : HeadNext{nullptr, nullptr, nullptr, nullptr, nullptr, 0u, 0u, 0, 0});
 }
 
 PhotonPtrs to_ptrs(const chr_photons *p) {
@@ -3611,7 +3556,7 @@ static size_t sort_temp_bytes16(uint32_t n, int bits = 24) {
 // Hilbert order (octa_cell).  r04 ab15/ab16/ab18 (29k bench, 10 M rays): the binned
 // first launch 5.01 ms with r01-r03's 8+8-bit row-major cells, 4.63 with 11+11-bit
 // Morton cells, 4.55 with Hilbert order (490.3 -> 500.3 M/s); photons identical.
-constexpr int BIN_KEY_BITS = BIN_KEY_BITS_DEV;
+constexpr int BIN_KEY_BITS = 22;
 // u32 words: [0..15] counters | masks (2 per 64 slots) | offsets (1 per 64) |
 // block prefixes (1 per 256 words, +2)
 static uint64_t mask_scan_words(uint64_t n) {   // masks + offsets + block prefixes for n positions
@@ -3761,8 +3706,6 @@ static int launch_chunk(const chr_geometry *g, const chr_photons *ph, uint32_t *
     a.mode = nullptr;
     a.want = STEP_ONE;
     a.work = nullptr;
-    a.wkey = nullptr;
-    a.whist = nullptr;
     a.prio = 0;
     if (ev0) CHR_HIP_CHECK(hipEventRecord(ev0, stream));
     hipLaunchKernelGGL(select_variant(g), dim3(grid_for(nthreads)), dim3(BLOCK), 0, stream,
@@ -3771,8 +3714,7 @@ static int launch_chunk(const chr_geometry *g, const chr_photons *ph, uint32_t *
     launch_mask_scan(masks, nwords, offsets, bsums, out_queue, counters + 1, nullptr, stream);
     hipLaunchKernelGGL(scatter_queue_kernel, dim3(grid_for(nthreads)), dim3(BLOCK), 0, stream, masks, offsets, bsums,
                        counters + 1, in_queue, first, nthreads, out_queue,
-                       FlatEnrol{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr},
-                       (const uint32_t *)nullptr,
+                       FlatEnrol{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr}, (const uint32_t *)nullptr,
                        (const uint32_t *)nullptr, STEP_IDLE);
     CHR_HIP_CHECK(hipGetLastError());
     return CHR_OK;
@@ -3806,9 +3748,6 @@ struct FlatCtx {
     // rays_walk the binned first step's records permuted into walk order
     uint4 *rays = nullptr, *rays_walk = nullptr;
     uint32_t cap = 0;                   // entries of flat_q / flat_best
-    // walk order of the later steps (walk_key): bucket histogram (zero between steps),
-    // bucket cursors, each survivor's bucket per queue position
-    uint32_t *whist = nullptr, *wcursor = nullptr, *wkey = nullptr;
 };
 static int flat_get(uint32_t n, FlatCtx &fc, int ctx = 0) {
     static thread_local Scratch s[NCTX][16];
@@ -3832,7 +3771,6 @@ static int flat_get(uint32_t n, FlatCtx &fc, int ctx = 0) {
 }
 
 static bool trace_steps();
-static bool walk_order_enabled();
 // CHR_SLOT_TIMING: which per-slot timing events a device-driven propagate
 // records.  Each hipEventRecord between two dependent dispatches of a step's
 // chain adds a gap (r03 ab15, 29k bench: all 449.9, trace pair only 452.6,
@@ -3932,13 +3870,8 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
     a.mode = mode;
     a.want = STEP_ONE;
     a.work = nullptr;
-    a.wkey = nullptr;
-    a.whist = nullptr;
     a.prio = 0;
-    FlatEnrol fe{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
-    // the next step's rays in walk-bucket order (walk_key; CHR_WALK_ORDER=0: queue order)
-    const bool worder = fc && fc->whist && fc->rays && fc->enrol_next && walk_order_enabled();
-    uint32_t *whist = worder ? fc->whist : nullptr, *wcursor = worder ? fc->wcursor : nullptr;
+    FlatEnrol fe{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
     const uint32_t threads = std::min(cap, (n + 63u) & ~63u);
     const StepVariant sv = select_step_variant(g);
     // host-driven: the split when this launch is one step; device-driven: the
@@ -4000,9 +3933,7 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
         a.zero_word = count_next;   // cleared by the shade pass, filled by this step's scatter
         if (fc->enrol_next)
             fe = FlatEnrol{ph->d_pos, ph->d_dir, hits, fc->flat_q, count_next, fc->flat_best, fc->rays,
-                           ph->d_last_hit_triangles, worder ? fc->wkey : nullptr, wcursor};
-        a.wkey = worder ? fc->wkey : nullptr;
-        a.whist = whist;
+                           ph->d_last_hit_triangles};
         if (trace_steps() && pre) {   // debugging: per-walk cost histogram (counting variants), printed per step
             ta.walk_hist = next + 16 + 2 * (size_t)(sc ? sc->n_layout : n);
             CHR_HIP_CHECK(hipMemsetAsync(ta.walk_hist, 0, 34 * 4, stream));
@@ -4080,7 +4011,7 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
                            (const DevGeom *)g->d_dev, at, cap);
         if (sc->evt_tail1) CHR_HIP_CHECK(hipEventRecord(sc->evt_tail1, ts));
         launch_mask_scan(masks, nwords, offsets, bsums, out_queue, counters + 1, nullptr, stream, dev_n, mode, STEP_TAIL,
-                         hnp, whist, wcursor);
+                         hnp);
         hipLaunchKernelGGL(scatter_queue_kernel, dim3(std::min<uint32_t>(4096u, grid_for(n))), dim3(BLOCK), 0, stream,
                            masks, offsets, bsums, counters + 1, in_queue, 0, (int32_t)n, out_queue, fe, dev_n, mode,
                            STEP_TAIL);
@@ -4100,8 +4031,7 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
         hipLaunchKernelGGL(sv.fn, dim3(grid_for(threads)), dim3(BLOCK), 0, stream, (const DevGeom *)g->d_dev, a, cap);
     }
     if (ev1) CHR_HIP_CHECK(hipEventRecord(ev1, stream));
-    launch_mask_scan(masks, nwords, offsets, bsums, out_queue, counters + 1, nullptr, stream, dev_n, mode, STEP_IDLE, hnp,
-                     whist, wcursor);
+    launch_mask_scan(masks, nwords, offsets, bsums, out_queue, counters + 1, nullptr, stream, dev_n, mode, STEP_IDLE, hnp);
     hipLaunchKernelGGL(scatter_queue_kernel, dim3(sc ? std::min<uint32_t>(4096u, grid_for(n)) : grid_for(n)), dim3(BLOCK),
                        0, stream, masks, offsets, bsums, counters + 1, in_queue, 0, (int32_t)n, out_queue, fe, dev_n,
                        mode, STEP_IDLE);
@@ -4147,13 +4077,6 @@ static int timing_events(size_t n, std::vector<hipEvent_t> **out, int ctx = 0) {
     }
     *out = &v;
     return CHR_OK;
-}
-
-// CHR_WALK_ORDER=0: the steps after the first walk their rays in queue order instead
-// of by walk bucket (walk_key; A/B, read per launch)
-static bool walk_order_enabled() {
-    const char *e = getenv("CHR_WALK_ORDER");
-    return !(e && e[0] == '0');
 }
 
 static bool trace_steps() {   // CHR_TRACE_STEPS=1: one stderr line per host step (debugging)
@@ -4220,10 +4143,8 @@ static int prop_bufs(uint32_t nphotons, int32_t ntpb, int32_t max_blocks, int ct
     const size_t qbytes = ((size_t)nphotons + 1) * 4;
     // split path: hits, ray counter, binning keys/order/histogram
     const size_t hbytes = b.fused ? (size_t)nphotons * 24 + 128 + 256 + 512 + sort_temp_bytes16(nphotons) : 0;
-    // split path: ray records, queue order + walk order (FlatCtx::rays / rays_walk),
-    // walk buckets (histogram, cursors) and each survivor's bucket
-    const size_t rbytes = b.fused ? (size_t)nphotons * 64 + 512 + 2 * (size_t)WALK_BUCKETS * 4 + (size_t)nphotons * 4 + 512
-                                  : 0;
+    // split path: ray records, queue order + walk order (FlatCtx::rays / rays_walk)
+    const size_t rbytes = b.fused ? (size_t)nphotons * 64 + 512 : 0;
     const size_t base_bytes = 2 * qbytes + swords * 4 + 64 + hbytes + rbytes;
     const size_t mbytes = tail_masks ? ((size_t)nphotons + 63) / 64 * 8 + 512 : 0;
     void *buf = nullptr;
@@ -4242,9 +4163,6 @@ static int prop_bufs(uint32_t nphotons, int32_t ntpb, int32_t max_blocks, int ct
     if (b.fused) {
         b.fc.rays = (uint4 *)(((uintptr_t)buf + 2 * qbytes + swords * 4 + 64 + hbytes + 255) & ~(uintptr_t)255);
         b.fc.rays_walk = b.fc.rays + 2 * (size_t)nphotons;
-        b.fc.whist = (uint32_t *)(((uintptr_t)(b.fc.rays_walk + 2 * (size_t)nphotons) + 255) & ~(uintptr_t)255);
-        b.fc.wcursor = b.fc.whist + WALK_BUCKETS;
-        b.fc.wkey = b.fc.wcursor + WALK_BUCKETS;
     }
     return CHR_OK;
 }
@@ -4256,7 +4174,6 @@ static int prop_start(const PropBufs &b, uint32_t nphotons, uint32_t true_nphoto
     ZeroWords z{{b.fused ? b.fc.ctl : nullptr, b.scratch, done}, {32u, 16u, 1u}};
     hipLaunchKernelGGL(init_queue_kernel, dim3(grid_for(nphotons)), dim3(BLOCK), 0, stream, b.q[0], b.q[1], nphotons,
                        true_nphotons, ncopies, z);
-    if (b.fused && b.fc.whist) CHR_HIP_CHECK(hipMemsetAsync(b.fc.whist, 0, (size_t)WALK_BUCKETS * 4, stream));
     CHR_HIP_CHECK(hipGetLastError());
     return CHR_OK;
 }

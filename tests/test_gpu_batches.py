@@ -225,12 +225,11 @@ def test_batches_slot_timing_modes_identical(cuda, small_detector, monkeypatch):
 #   CHR_HOST_STEPS=1        the host reads the survivor count every step
 #   CHR_STEP_LAUNCH=0       one launch per chunk (the reference's launch structure)
 #   CHR_TRACE_STEPS=1       per-step stderr lines (debugging)
-#   CHR_WALK_ORDER=0        the steps after the first walk in queue order, not by walk bucket
 #   CHR_PROPAGATE_VARIANT   2/4 fused step kernels, 7/8 binning every / no step, 1 the
 #                           exact-order walk of the reference BVH, 5 the counting form
 #   CHR_SLOT_TIMING         test_batches_slot_timing_modes_identical
 #   CHR_WIDE_LEAF_MAX / CHR_EXACT_ORDER_ONLY: test_geometry_build_switches_identical
-SWITCHES = [('CHR_HOST_STEPS', '1'), ('CHR_STEP_LAUNCH', '0'), ('CHR_TRACE_STEPS', '1'), ('CHR_WALK_ORDER', '0'),
+SWITCHES = [('CHR_HOST_STEPS', '1'), ('CHR_STEP_LAUNCH', '0'), ('CHR_TRACE_STEPS', '1'),
             ('CHR_PROPAGATE_VARIANT', '2'), ('CHR_PROPAGATE_VARIANT', '4'), ('CHR_PROPAGATE_VARIANT', '7'),
             ('CHR_PROPAGATE_VARIANT', '8'), ('CHR_PROPAGATE_VARIANT', '1'), ('CHR_PROPAGATE_VARIANT', '5')]
 
