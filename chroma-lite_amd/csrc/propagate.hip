@@ -216,19 +216,8 @@ __device__ __forceinline__ bool intersect_record(V3 o, V3 d, float4 r0, float4 r
     return intersect_triangle(o, d, v0, v1 - v0, v2 - v0, distance);
 }
 // the record index of a wide-BVH triangle record pointer: what the wide walks
-// return for a hit (finish_fill<1> reads the triangle id and normal from it)
+// return for a hit (finish_fill<true> reads the triangle id and normal from it)
 __device__ __forceinline__ int rec_of(const DevGeom &g, const float4 *r) { return (int)((r - g.wtri) >> 2); }
-// cross(v1 - v0, v2 - v1) of a record: the unnormalised normal of fill_state (photon.h:365-367)
-__device__ __forceinline__ V3 record_cross(float4 r0, float4 r1, float4 r2) {
-    const V3 v0 = v3(r0.x, r0.y, r0.z), v1 = v3(r0.w, r1.x, r1.y), v2 = v3(r1.z, r1.w, r2.x);
-    return cross(v1 - v0, v2 - v1);
-}
-// trace_kernel's hit record of the triangle in record r (the shade pass then
-// needs no gather of it): (material code, cross) -- the triangle id goes in hits.x
-__device__ __forceinline__ uint4 hit_extra(float4 r0, float4 r1, float4 r2, uint32_t code) {
-    const V3 c = record_cross(r0, r1, r2);
-    return make_uint4(code, __float_as_uint(c.x), __float_as_uint(c.y), __float_as_uint(c.z));
-}
 
 // mesh.h:45-126 -- nearest triangle != last_hit; reference DFS order.
 // The children of a popped group are fetched BATCH at a time (independent
@@ -891,14 +880,11 @@ __device__ CHR_COLD void wireplanes(const DevGeom &g, const Photon &p, float bes
 // Second half of fill_state (photon.h:272-397): the mesh hit (or an analytic
 // wire plane, FP64) -> material pair, surface, oriented normal and the four
 // interpolated bulk properties; no hit -> NO_HIT.  s.distance holds the mesh
-// hit distance on entry.  SRC 1: mesh_triangle is a wide-BVH triangle record
-// (what the wide walks return: triangle id and vertices read from it); 0: a
-// triangle id of the reference walk (the 48-byte reference records); 2: a
-// triangle id whose material code and e1 x e3 the walk already took from its
-// record (hx = (code, cross), trace_kernel's hit record: no gather here).
-template <int SRC>
-__device__ __forceinline__ void finish_fill(const DevGeom &g, State &s, Photon &p, int mesh_triangle,
-                                            uint4 hx = make_uint4(0u, 0u, 0u, 0u)) {
+// hit distance on entry.  REC: mesh_triangle is a wide-BVH triangle record
+// (what the wide walks return: triangle id and vertices read from it); else a
+// triangle id of the reference walk (the 48-byte reference records).
+template <bool REC>
+__device__ __forceinline__ void finish_fill(const DevGeom &g, State &s, Photon &p, int mesh_triangle) {
     int m1, m2;
     bool use_analytic = false;
     int a_surface = -1, a_inner = -1, a_outer = -1;
@@ -916,23 +902,22 @@ __device__ __forceinline__ void finish_fill(const DevGeom &g, State &s, Photon &
         if (a_dot_raw > 0.0f) { m1 = a_outer; m2 = a_inner; s.normal = a_normal_raw; s.inside_to_outside = false; }
         else { m1 = a_inner; m2 = a_outer; s.normal = -a_normal_raw; s.inside_to_outside = true; }
     } else if (mesh_triangle != -1) {
-        V3 c;   // cross(v1 - v0, v2 - v1) (photon.h:365-367)
+        V3 e1, e3;   // v1 - v0, v2 - v1 (photon.h:365-367)
         int tid;
         uint32_t code;
-        if constexpr (SRC == 2) {
-            c = v3(__uint_as_float(hx.y), __uint_as_float(hx.z), __uint_as_float(hx.w));
-            tid = mesh_triangle;
-            code = hx.x;
-        } else if constexpr (SRC == 1) {   // one record, four independent loads (no dependent material-code gather)
+        if constexpr (REC) {   // one record, four independent loads (no dependent material-code gather)
             const float4 *r = g.wtri + 4 * (size_t)mesh_triangle;
             const float4 r0 = gld(r), r1 = gld(r + 1), r2 = gld(r + 2), r3 = gld(r + 3);
-            c = record_cross(r0, r1, r2);
+            const V3 v0 = v3(r0.x, r0.y, r0.z), v1 = v3(r0.w, r1.x, r1.y), v2 = v3(r1.z, r1.w, r2.x);
+            e1 = v1 - v0;
+            e3 = v2 - v1;
             tid = (int)__float_as_uint(r2.y);
             code = __float_as_uint(r3.z);
         } else {
             const float4 *r = g.tri + 3 * (size_t)mesh_triangle;
             const float4 r0 = gld(r), r1 = gld(r + 1), r2 = gld(r + 2);
-            c = cross(v3(r0.w, r1.x, r1.y), v3(r2.y, r2.z, r2.w));
+            e1 = v3(r0.w, r1.x, r1.y);
+            e3 = v3(r2.y, r2.z, r2.w);
             tid = mesh_triangle;
             code = gld(g.material_codes + tid);
         }
@@ -940,7 +925,7 @@ __device__ __forceinline__ void finish_fill(const DevGeom &g, State &s, Photon &
         const int inner = convert(0xFF & (int)(code >> 24));
         const int outer = convert(0xFF & (int)(code >> 16));
         s.surface_index = convert(0xFF & (int)(code >> 8));
-        s.normal = normalize(c);
+        s.normal = normalize(cross(e1, e3));
         if (dot(s.normal, -p.dir) > 0.0f) { m1 = outer; m2 = inner; s.inside_to_outside = false; }
         else { m1 = inner; m2 = outer; s.normal = -s.normal; s.inside_to_outside = true; }
     } else {
@@ -969,7 +954,7 @@ __device__ __forceinline__ void fill_state(const DevGeom &g, State &s, Photon &p
         mesh_triangle =
             intersect_wide_sched<COUNT, WIDE - 1000>(g, p.pos, p.dir, s.distance, p.last_hit, wst, overflow, cnt);
     else mesh_triangle = intersect_mesh<BATCH>(g, p.pos, p.dir, s.distance, p.last_hit, st, overflow);
-    finish_fill<(WIDE != 0) ? 1 : 0>(g, s, p, mesh_triangle);
+    finish_fill<(WIDE != 0)>(g, s, p, mesh_triangle);
 }
 
 // photon.h:399-427
@@ -1417,7 +1402,6 @@ struct PropagateArgs {
     uint32_t *counters;                // [0]: stack overflows
     const uint32_t *order;             // coherence order: work-item t runs slot order[t] (nullptr: t)
     const int2 *hits;                  // shade_kernel: walk result per queue position (trace_kernel)
-    const uint4 *hitx;                 // shade_kernel: the hit triangle's material code and e1 x e3 (trace_kernel)
     const unsigned long long *flat_best;   // shade_kernel: results of the flat walks (FLAT_HIT entries of hits)
     uint32_t *zero_word;               // shade_kernel: word cleared once (next step's flat-walk count)
     uint32_t *diag;                    // multi-step kernels (nullptr: off): [0] += flat walks walked whole,
@@ -1666,8 +1650,8 @@ struct QueuedPhoton {
     uint32_t pid, history;
     V3 pos, dir, pol;
     float wavelength, time, weight;
+    int last_hit;
     int2 hit;
-    uint4 hx;   // (code, e1 x e3) of the hit triangle when hit.x >= 0 (trace_kernel)
 };
 // the photon at queue position q; pid: its queue entry when already loaded (the
 // shade kernel's two-ahead prefetch), else read here first (a dependent load)
@@ -1683,8 +1667,8 @@ __device__ __forceinline__ void fetch_queued(const PropagateArgs &a, uint32_t q,
     f.wavelength = a.wl[f.pid];
     f.time = a.t[f.pid];
     f.weight = a.weights[f.pid];
+    f.last_hit = a.last_hit[f.pid];
     f.hit = a.hits[q];
-    f.hx = a.hitx[q];
 }
 // The queue entry of the photon two positions ahead is loaded one iteration
 // early, so the next photon's state loads go out without first waiting for its
@@ -1736,26 +1720,23 @@ __global__ __launch_bounds__(BLOCK, MINW) void shade_kernel(const DevGeom *__res
             p.pol = cur.pol / norm(cur.pol);
             p.wavelength = cur.wavelength;
             p.time = cur.time;
-            p.last_hit = -1;   // set by finish_fill; a NaN photon keeps its own (read below)
+            p.last_hit = cur.last_hit;
             p.weight = cur.weight;
             const float prod = ((((p.dir.x * p.dir.y) * p.dir.z) * p.pos.x) * p.pos.y) * p.pos.z;
             if (chr_isnan(prod)) {
                 p.history |= CHR_NO_HIT | CHR_NAN_ABORT;
-                p.last_hit = a.last_hit[cur.pid];
             } else {
                 State s;
                 int tri = cur.hit.x;
                 s.distance = __int_as_float(cur.hit.y);
-                pf.tick(P_FILL);
-                pf.call(P_FILL);
                 if (tri == FLAT_HIT) {            // (distance bits, reference rank) of a decomposed walk
                     const unsigned long long key = a.flat_best[cur.hit.y];
                     tri = key == ~0ull ? -1 : (int)g.wrank_rec[(uint32_t)key];
                     s.distance = key == ~0ull ? -1.0f : __uint_as_float((uint32_t)(key >> 32));
-                    finish_fill<1>(g, s, p, tri);   // a record
-                } else {
-                    finish_fill<2>(g, s, p, tri, cur.hx);   // a triangle id with its code and e1 x e3
                 }
+                pf.tick(P_FILL);
+                pf.call(P_FILL);
+                finish_fill<true>(g, s, p, tri);
                 pf.tick(P_PHYS);
                 if (p.last_hit != -1) {
                     pf.call(P_PHYS);
@@ -1772,9 +1753,8 @@ __global__ __launch_bounds__(BLOCK, MINW) void shade_kernel(const DevGeom *__res
         // before the write-back (see above)
         asm volatile("" ::"v"(nx.pid), "v"(nx.history), "v"(nx.pos.x), "v"(nx.pos.y), "v"(nx.pos.z), "v"(nx.dir.x),
                      "v"(nx.dir.y), "v"(nx.dir.z), "v"(nx.pol.x), "v"(nx.pol.y), "v"(nx.pol.z));
-        asm volatile("" ::"v"(nx.wavelength), "v"(nx.time), "v"(nx.weight), "v"(nx.hit.x),
+        asm volatile("" ::"v"(nx.wavelength), "v"(nx.time), "v"(nx.weight), "v"(nx.last_hit), "v"(nx.hit.x),
                      "v"(nx.hit.y), "v"(pid2));
-        asm volatile("" ::"v"(nx.hx.x), "v"(nx.hx.y), "v"(nx.hx.z), "v"(nx.hx.w));
         if (valid) {
             const uint32_t pid = cur.pid;
             store3(a.pos, pid, p.pos);
@@ -2602,7 +2582,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_tail_kernel(const DevGe
                 if (!(chr_isfinite(inv.x) && chr_isfinite(inv.y) && chr_isfinite(inv.z))) flat++;
             }
             s.distance = dist;
-            finish_fill<1>(g, s, p, tri);
+            finish_fill<true>(g, s, p, tri);
             bool stop = p.last_hit == -1;
             if (!stop) {
                 int command = propagate_to_boundary(g, p, s, rng, a.use_weights, scatter_first);
@@ -2709,8 +2689,7 @@ struct TraceArgs {
     const int32_t *last_hit;
     const uint32_t *queue;       // this step's queue
     uint32_t n;                  // queue length
-    int2 *hits;                  // per queue position: (triangle id or -1, distance bits)
-    uint4 *hitx;                 // per queue position with a hit: (material code, e1 x e3) of the triangle
+    int2 *hits;                  // per queue position: (triangle or -1, distance bits)
     uint32_t *next;              // ray counter (zeroed by the host)
     uint32_t *counters;          // [0] overflows, [2..] u64 walk counters (COUNT)
     const uint32_t *order;       // fetch order: the j-th ray walked is queue position order[j] (nullptr: j)
@@ -2849,8 +2828,6 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
     float best = 0.0f;
     uint32_t best_rank = 0, last = 0, node = 0;
     int best_id = -1, sp = 0;
-    int best_tid = -1;              // the best triangle's id, code and e1 x e3 (hit_extra)
-    uint4 best_x = make_uint4(0u, 0u, 0u, 0u);
     bool walk_done = true, drain = false;
     uint32_t qh = 0, qt = 0, pcur = 0, pleft = 0;
     constexpr uint32_t INVALID = 0xFFFFFFFFu;
@@ -2869,10 +2846,8 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
     while (true) {
         pf.tick(P_REFILL);   // the last step goes to the region each work-item was in
         if (has_ray && walk_done && pleft == 0 && qh == qt) {   // walk over: publish (mesh.h:123-125)
-            if (flat_f < 0) {
-                a.hits[q] = make_int2(best_id == -1 ? -1 : best_tid, __float_as_int(best_id == -1 ? -1.0f : best));
-                if (best_id != -1) a.hitx[q] = best_x;
-            } else if (best_id != -1)   // a sub-walk: its best joins the flat walk's minimum
+            if (flat_f < 0) a.hits[q] = make_int2(best_id, __float_as_int(best_id == -1 ? -1.0f : best));
+            else if (best_id != -1)   // a sub-walk: its best joins the flat walk's minimum
                 atomicMin(a.flat_best + flat_f, ((unsigned long long)__float_as_uint(best) << 32) | best_rank);
             has_ray = false;
             if constexpr (COUNT) {
@@ -3060,8 +3035,6 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
             best = dist;
             best_rank = rank;
             best_id = rec_of(g, r);
-            best_tid = (int)id;
-            best_x = hit_extra(r0, r1, r2, __float_as_uint(r3.z));
         }
     }
     if constexpr (!COUNT) {
@@ -3095,14 +3068,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
             const int rt = __shfl(tri, mine);
             const float rd = __shfl(sdist, mine);
             if (has_ray) {                                        // publish (mesh.h:123-125)
-                int tid = -1;
-                if (rt != -1) {   // the record of the drained walk's hit (hit_extra)
-                    const float4 *r = g.wtri + 4 * (size_t)rt;
-                    const float4 r0 = gld(r), r1 = gld(r + 1), r2 = gld(r + 2), r3 = gld(r + 3);
-                    tid = (int)__float_as_uint(r2.y);
-                    a.hitx[q] = hit_extra(r0, r1, r2, __float_as_uint(r3.z));
-                }
-                a.hits[q] = make_int2(tid, __float_as_int(rt == -1 ? -1.0f : rd));
+                a.hits[q] = make_int2(rt, __float_as_int(rt == -1 ? -1.0f : rd));
                 pf.call(P_DRAIN);
             }
             pf.tick(P_IDLE);
@@ -3733,7 +3699,6 @@ static int launch_chunk(const chr_geometry *g, const chr_photons *ph, uint32_t *
     a.alive_masks = masks; a.counters = counters;
     a.order = nullptr;
     a.hits = nullptr;
-    a.hitx = nullptr;
     a.flat_best = nullptr;
     a.zero_word = nullptr;
     a.diag = nullptr;
@@ -3782,7 +3747,6 @@ struct FlatCtx {
     // step's classification, then every step's scatter for the next step),
     // rays_walk the binned first step's records permuted into walk order
     uint4 *rays = nullptr, *rays_walk = nullptr;
-    uint4 *hitx = nullptr;              // the walk results' (code, e1 x e3) per queue position (TraceArgs::hitx)
     uint32_t cap = 0;                   // entries of flat_q / flat_best
 };
 static int flat_get(uint32_t n, FlatCtx &fc, int ctx = 0) {
@@ -3899,7 +3863,6 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
     a.alive_masks = masks; a.counters = counters;
     a.order = nullptr;
     a.hits = nullptr;
-    a.hitx = nullptr;
     a.flat_best = nullptr;
     a.zero_word = nullptr;
     a.diag = fc ? fc->ctl + 4 : nullptr;
@@ -3961,7 +3924,6 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
         TraceArgs ta;
         ta.pos = ph->d_pos; ta.dir = ph->d_dir; ta.flags = ph->d_flags; ta.last_hit = ph->d_last_hit_triangles;
         ta.queue = in_queue; ta.n = n; ta.hits = hits; ta.next = next; ta.counters = counters; ta.order = nullptr;
-        ta.hitx = fc->hitx;
         ta.rays = use_rays ? fc->rays : nullptr;
         ta.walk_hist = nullptr;
         ta.flat_q = fc->flat_q; ta.flat_count = count_cur; ta.flat_best = fc->flat_best; ta.diag = fc->ctl + 3;
@@ -4011,7 +3973,6 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
             return CHR_OK;
         }
         a.hits = hits;
-        a.hitx = fc->hitx;
         a.max_steps = 1;
         if (sc && sc->rng_ready) CHR_HIP_CHECK(hipStreamWaitEvent(stream, sc->rng_ready, 0));
         hipLaunchKernelGGL(sv.shade, dim3(grid_for(threads)), dim3(BLOCK), 0, stream, (const DevGeom *)g->d_dev, a, cap);
@@ -4183,7 +4144,7 @@ static int prop_bufs(uint32_t nphotons, int32_t ntpb, int32_t max_blocks, int ct
     // split path: hits, ray counter, binning keys/order/histogram
     const size_t hbytes = b.fused ? (size_t)nphotons * 24 + 128 + 256 + 512 + sort_temp_bytes16(nphotons) : 0;
     // split path: ray records, queue order + walk order (FlatCtx::rays / rays_walk)
-    const size_t rbytes = b.fused ? (size_t)nphotons * 80 + 768 : 0;
+    const size_t rbytes = b.fused ? (size_t)nphotons * 64 + 512 : 0;
     const size_t base_bytes = 2 * qbytes + swords * 4 + 64 + hbytes + rbytes;
     const size_t mbytes = tail_masks ? ((size_t)nphotons + 63) / 64 * 8 + 512 : 0;
     void *buf = nullptr;
@@ -4202,7 +4163,6 @@ static int prop_bufs(uint32_t nphotons, int32_t ntpb, int32_t max_blocks, int ct
     if (b.fused) {
         b.fc.rays = (uint4 *)(((uintptr_t)buf + 2 * qbytes + swords * 4 + 64 + hbytes + 255) & ~(uintptr_t)255);
         b.fc.rays_walk = b.fc.rays + 2 * (size_t)nphotons;
-        b.fc.hitx = (uint4 *)(((uintptr_t)(b.fc.rays_walk + 2 * (size_t)nphotons) + 255) & ~(uintptr_t)255);
     }
     return CHR_OK;
 }
