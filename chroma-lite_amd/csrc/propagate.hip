@@ -4916,6 +4916,49 @@ extern "C" int chr_device_profile_fetch(uint64_t *h_calls, uint64_t *h_cycles, i
 #endif
 }
 
+namespace chr {
+// chr_walk_lone_timing: walk_lone on one wave per workgroup, each ray reps times
+__global__ __launch_bounds__(64) void walk_lone_timing_kernel(const DevGeom *__restrict__ gdev, const float *rays,
+                                                              uint32_t n, uint32_t reps, uint32_t *out) {
+    __shared__ uint32_t stacks[8 * TAIL_STACK * 2];
+    __shared__ uint32_t tris[2 * TAIL_TRI];
+    const DevGeom &g = *gdev;
+    uint32_t overflow = 0;
+    for (uint32_t r = blockIdx.x; r < n; r += gridDim.x) {
+        const float *ry = rays + 7 * (size_t)r;
+        const V3 o = v3(ry[0], ry[1], ry[2]), d = v3(ry[3], ry[4], ry[5]);
+        const uint32_t last = __float_as_uint(ry[6]);
+        for (uint32_t k = 0; k < reps; ++k) {
+            float sd;
+            uint32_t it = 0;
+            const unsigned long long t0 = __builtin_amdgcn_s_memrealtime(), c0 = __builtin_amdgcn_s_memtime();
+            const int tri = walk_lone(g, o, d, last, LdsFlat{(CHR_LDS uint32_t *)stacks}, TAIL_STACK * 8,
+                                      LdsFlat{(CHR_LDS uint32_t *)tris}, overflow, sd, it);
+            const unsigned long long t1 = __builtin_amdgcn_s_memrealtime(), c1 = __builtin_amdgcn_s_memtime();
+            if (threadIdx.x == 0) {
+                uint32_t *o4 = out + 4 * ((size_t)r * reps + k);
+                o4[0] = (uint32_t)tri;
+                o4[1] = it;
+                o4[2] = (uint32_t)(t1 - t0);
+                o4[3] = (uint32_t)(c1 - c0);
+            }
+        }
+    }
+}
+}  // namespace chr
+
+extern "C" int chr_walk_lone_timing(const chr_geometry *g, const float *d_rays, uint32_t n, uint32_t reps,
+                                    uint32_t nwaves, uint32_t *d_out, void *stream) {
+    if (!g || !d_rays || !d_out || nwaves == 0 || reps == 0)
+        return chr::fail(CHR_ERR_INVALID, "chr_walk_lone_timing: bad argument");
+    if (g->dev.nwnodes == 0) return chr::fail(CHR_ERR_INVALID, "chr_walk_lone_timing: geometry has no wide BVH");
+    if (n == 0) return CHR_OK;
+    hipLaunchKernelGGL(chr::walk_lone_timing_kernel, dim3(std::min(nwaves, n)), dim3(64), 0, (hipStream_t)stream,
+                       (const chr::DevGeom *)g->d_dev, d_rays, n, reps, d_out);
+    CHR_HIP_CHECK(hipGetLastError());
+    return CHR_OK;
+}
+
 // The renderer (render.cu, hybrid_render.cu, transform.cu): same translation
 // unit, it walks the same BVH and runs the same photon physics.
 #include "render.hip"
