@@ -906,8 +906,8 @@ def run_rank(args):
                   'host_steps_per_propagate': r0['host_steps'] / steps,
                   'stream_draining_host_syncs_per_propagate': r0['host_syncs'] / steps,
                   'stack_overflows': int(sum(r['overflows'] for r in reports)),
-                  'flat_walks_decomposed': int(sum(r['flat'] for r in reports)),
-                  'flat_walks_whole': int(sum(r['flat_whole'] for r in reports)),
+                  'flat_walks_trace': int(sum(r['flat'] for r in reports)),
+                  'flat_walks_tail': int(sum(r['flat_whole'] for r in reports)),
                   'tail_launch': r0['tail'],
                   'first_propagate_trace_launches': [{'rays': r, 'ms': round(float(m), 3)} for r, m in
                                                      zip(r0['launch_rays'], r0['launch_ms'][:len(r0['launch_rays'])])],

@@ -343,40 +343,57 @@ __device__ __forceinline__ F2 pk_fma(F2 a, F2 b, F2 c) { return __builtin_elemen
 // axis with finite 1/d the near/far plane distances are fmaf(x, inv, noid) --
 // the reference's own expression (intersect_box, intersect.h:113-157), and
 // since fmaf is monotone in x, selecting the near/far bound by the sign of
-// inv gives exactly the min/max the reference takes.  An axis with
-// non-finite 1/d is skipped by the reference; here it yields [-inf, +inf]
-// (inv 0, offsets -inf/+inf), which leaves tmin/tmax unchanged the same way.
+// inv gives exactly the min/max the reference takes.
+// A FLAT axis (1/d not finite: d = +-0 or denormal) is skipped by the
+// reference's box test, so its DFS enters every box the ray's projection
+// crosses (one such walk took 19 s in round 1; rounds 2-4 split it into 2^18
+// sub-walks shared by the grid).  The traversal here instead tests that axis
+// as what it is, the ray's constant coordinate o inside [lo, hi]: multiplier
+// 2^100 and offset -o * 2^100 (both exact), so fmaf(x, 2^100, -o * 2^100) is
+// (x - o) * 2^100 rounded once -- negative, zero or positive exactly as x - o.
+// The nearest hit is unchanged: a triangle the ray hits holds a point at the
+// ray's coordinate on that axis (up to Moller-Trumbore's 1e-6 barycentric
+// tolerance, ~1e-5 mm), and its reference leaf box extends at least one
+// quantum (world_scale, ~0.7 mm on the 29k detector) beyond its vertices
+// (bvh.cu make_leaves: lower - 1, upper + 1), so every box on the way to it
+// holds o on that axis; the traversal only skips boxes that hold no hit.  (The
+// one exception: a leaf box at the world minimum (quantised lower bound 0 gets
+// no margin) hit by a ray lying within that tolerance outside the world box.)
+// The leaf-box acceptance of a candidate (intersect_box_slab) keeps the
+// reference's skip of the flat axis (RaySlab::flat).
 struct RaySlab {
-    float inx, iny, inz;        // multipliers (inv or 0)
-    float onx, ony, onz;        // near offsets (noid or -inf)
-    float ofx, ofy, ofz;        // far offsets (noid or +inf)
+    float inx, iny, inz;        // multipliers (inv, or 2^100 on a flat axis)
+    float onx, ony, onz;        // near offsets (noid, or -o * 2^100)
+    float ofx, ofy, ofz;        // far offsets (same)
     bool negx, negy, negz;      // inv < 0: the near plane is the box's hi face
+    uint32_t flat;              // bit k: axis k flat (skipped by intersect_box_slab, as the reference does)
 };
-__device__ __forceinline__ RaySlab make_slab(V3 noid, V3 inv) {
+__device__ __forceinline__ RaySlab make_slab(V3 o, V3 noid, V3 inv) {
     RaySlab r;
-    const float inf = __builtin_inff();
+    constexpr float BIG = 1.2676506e30f;   // 2^100
     const bool fx = chr_isfinite(inv.x), fy = chr_isfinite(inv.y), fz = chr_isfinite(inv.z);
-    r.inx = fx ? inv.x : 0.0f; r.onx = fx ? noid.x : -inf; r.ofx = fx ? noid.x : inf;
-    r.iny = fy ? inv.y : 0.0f; r.ony = fy ? noid.y : -inf; r.ofy = fy ? noid.y : inf;
-    r.inz = fz ? inv.z : 0.0f; r.onz = fz ? noid.z : -inf; r.ofz = fz ? noid.z : inf;
-    r.negx = inv.x < 0.0f; r.negy = inv.y < 0.0f; r.negz = inv.z < 0.0f;
+    r.inx = fx ? inv.x : BIG; r.onx = fx ? noid.x : -(o.x * BIG); r.ofx = r.onx;
+    r.iny = fy ? inv.y : BIG; r.ony = fy ? noid.y : -(o.y * BIG); r.ofy = r.ony;
+    r.inz = fz ? inv.z : BIG; r.onz = fz ? noid.z : -(o.z * BIG); r.ofz = r.onz;
+    r.negx = fx && inv.x < 0.0f; r.negy = fy && inv.y < 0.0f; r.negz = fz && inv.z < 0.0f;
+    r.flat = (fx ? 0u : 1u) | (fy ? 0u : 2u) | (fz ? 0u : 4u);
     return r;
 }
 
-// intersect_box (intersect.h:113-157) from the ray's slab constants: an axis
-// whose 1/d is not finite has multiplier 0 there and is skipped, the others
-// compute fmaf(bound, inv, noid) exactly as intersect_box does.
+// intersect_box (intersect.h:113-157) from the ray's slab constants: a flat
+// axis is skipped (the reference's isfinite test), the others compute
+// fmaf(bound, inv, noid) exactly as intersect_box does.
 __device__ __forceinline__ bool intersect_box_slab(const RaySlab &r, V3 lo, V3 hi, float &dist) {
     float tmin = 0.0f, tmax = __builtin_inff();
-    if (r.inx != 0.0f) {
+    if (!(r.flat & 1u)) {
         const float t0 = __builtin_fmaf(lo.x, r.inx, r.onx), t1 = __builtin_fmaf(hi.x, r.inx, r.onx);
         tmin = fmax_(tmin, fmin_(t0, t1)); tmax = fmin_(tmax, fmax_(t0, t1));
     }
-    if (r.iny != 0.0f) {
+    if (!(r.flat & 2u)) {
         const float t0 = __builtin_fmaf(lo.y, r.iny, r.ony), t1 = __builtin_fmaf(hi.y, r.iny, r.ony);
         tmin = fmax_(tmin, fmin_(t0, t1)); tmax = fmin_(tmax, fmax_(t0, t1));
     }
-    if (r.inz != 0.0f) {
+    if (!(r.flat & 4u)) {
         const float t0 = __builtin_fmaf(lo.z, r.inz, r.onz), t1 = __builtin_fmaf(hi.z, r.inz, r.onz);
         tmin = fmax_(tmin, fmin_(t0, t1)); tmax = fmin_(tmax, fmax_(t0, t1));
     }
@@ -386,19 +403,17 @@ __device__ __forceinline__ bool intersect_box_slab(const RaySlab &r, V3 lo, V3 h
 }
 
 // What a queued photon's walk is: 0 none (NaN state: the step aborts it,
-// propagate.cu:307-310), 1 an ordinary walk, 2 a FLAT walk -- a direction
-// component whose reciprocal is not finite (+-0 or denormal).  The reference's
-// slab test skips such an axis (intersect.h:121-144), so every box is tested
-// in 2D (or 1D) and the walk visits every box the ray's projection crosses
-// before the nearest hit: tens of millions of node and triangle fetches on the
-// 29k-PMT detector (one such ray made one trace launch last 19 s, round 2).
-// Flat walks are split into independent sub-walks (wide_bvh.h cut items) that
-// the whole persistent grid shares.  d must be the normalised direction.
+// propagate.cu:307-310), 1 a walk.  (Rounds 2-4 had a kind 2, FLAT: a
+// direction component with non-finite reciprocal, walked as 2^18 sub-walks;
+// the flat-axis slab test above makes it an ordinary walk.)  d must be the
+// normalised direction.
 __device__ __forceinline__ int walk_kind(V3 o, V3 d) {
     const float prod = ((((d.x * d.y) * d.z) * o.x) * o.y) * o.z;
-    if (chr_isnan(prod)) return 0;
-    const float ix = 1.0f / d.x, iy = 1.0f / d.y, iz = 1.0f / d.z;
-    return (chr_isfinite(ix) && chr_isfinite(iy) && chr_isfinite(iz)) ? 1 : 2;
+    return chr_isnan(prod) ? 0 : 1;
+}
+// a flat ray (diagnostic counts: detail.flat_walks)
+__device__ __forceinline__ bool flat_ray(V3 d) {
+    return !(chr_isfinite(1.0f / d.x) && chr_isfinite(1.0f / d.y) && chr_isfinite(1.0f / d.z));
 }
 
 // Slab-test the up-to-8 children of one wide node.  Returns the leaf children
@@ -583,7 +598,7 @@ __device__ int intersect_wide_sched(const DevGeom &g, V3 o, V3 d, float &min_dis
     if constexpr (COUNT) cnt.walks++;
     const V3 noid = v3(-o.x / d.x, -o.y / d.y, -o.z / d.z);
     const V3 inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
-    const RaySlab slab = make_slab(noid, inv);
+    const RaySlab slab = make_slab(o, noid, inv);
     float best = __builtin_inff();
     uint32_t best_rank = 0xFFFFFFFFu;
     int best_id = -1;
@@ -686,7 +701,7 @@ __device__ int intersect_wide_spec(const DevGeom &g, V3 o, V3 d, float &min_dist
     if constexpr (COUNT) cnt.walks++;
     const V3 noid = v3(-o.x / d.x, -o.y / d.y, -o.z / d.z);
     const V3 inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
-    const RaySlab slab = make_slab(noid, inv);
+    const RaySlab slab = make_slab(o, noid, inv);
     float best = __builtin_inff();
     uint32_t best_rank = 0xFFFFFFFFu;
     int best_id = -1;
@@ -1920,7 +1935,7 @@ __device__ __forceinline__ int walk_segment(const DevGeom &g, bool act, V3 o, V3
     const unsigned long long below = (1ull << lane) - 1ull;
     const V3 noid = v3(-o.x / d.x, -o.y / d.y, -o.z / d.z);
     const V3 inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
-    const RaySlab r = make_slab(noid, inv);
+    const RaySlab r = make_slab(o, noid, inv);
     uint32_t cur = (act && L < 8u) ? 0u : INVALID;   // cursor 0 starts at the root
     float cur_t = 0.0f;
     int sp = 0;
@@ -2200,7 +2215,7 @@ __device__ __forceinline__ int walk_lone(const DevGeom &g, V3 o, V3 d, uint32_t 
     const unsigned long long below = (1ull << lane) - 1ull;
     const V3 noid = v3(-o.x / d.x, -o.y / d.y, -o.z / d.z);
     const V3 inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
-    const RaySlab r = make_slab(noid, inv);
+    const RaySlab r = make_slab(o, noid, inv);
     uint32_t cur = lane < 8u ? 0u : INVALID;          // cursor 0 starts at the root
     float cur_t = 0.0f;
     int sp = 0;
@@ -2822,9 +2837,10 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
     const uint32_t K = (g.nwcut > 1u && nflat <= (1u << 30) / g.nwcut) ? g.nwcut : 1u;
     const uint32_t total = n + nflat * K;
     int flat_f = -1;                // flat walk of the current sub-walk (-1: an ordinary ray)
+    uint32_t nflat_rays = 0;        // flat rays walked by this work-item (flat-axis slab test; diagnostic)
     uint32_t cmask = 0xFFu;         // children of the first node this walk may enter
     V3 o = v3(0.0f, 0.0f, 0.0f), d = v3(0.0f, 0.0f, 1.0f);
-    RaySlab slab = make_slab(o, d);
+    RaySlab slab = make_slab(o, o, d);
     float best = 0.0f;
     uint32_t best_rank = 0, last = 0, node = 0;
     int best_id = -1, sp = 0;
@@ -2926,13 +2942,14 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
                         last = (uint32_t)a.last_hit[pid];
                     }
                     if (start) {
-                        slab = make_slab(v3(-o.x / d.x, -o.y / d.y, -o.z / d.z), v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z));
+                        slab = make_slab(o, v3(-o.x / d.x, -o.y / d.y, -o.z / d.z), v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z));
                         best_id = -1;
                         sp = 0;
                         walk_done = false;
                         has_ray = true;
                         walk_cost = 0;
                         pf.call(P_REFILL);
+                        if (slab.flat && flat_f < 0) nflat_rays++;
                         if constexpr (COUNT) cnt.walks++;
                     }
                 }
@@ -3087,6 +3104,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
 #endif
     if (overflow) atomicAdd(a.counters, overflow);
     if (a.diag && nflat && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(a.diag, nflat);
+    if (a.diag && nflat_rays) atomicAdd(a.diag, nflat_rays);
     if constexpr (COUNT) {
         unsigned long long *c64 = reinterpret_cast<unsigned long long *>(a.counters + 2);
         atomicAdd(c64, (unsigned long long)cnt.nodes);

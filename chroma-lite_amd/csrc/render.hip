@@ -63,7 +63,7 @@ __global__ __launch_bounds__(BLOCK) void render_kernel(const DevGeom *__restrict
     float4 *col = color_all + (size_t)id * alpha_depth;
     uint32_t *rk = rank_all + (size_t)id * alpha_depth;
     for (uint32_t i = 0; i < n; ++i) rk[i] = 0u;              // entries of an earlier render
-    const RaySlab r = make_slab(noid, inv);
+    const RaySlab r = make_slab(o, noid, inv);
     CHR_LDS uint32_t *stk = (CHR_LDS uint32_t *)lds + threadIdx.x;
     uint32_t spill[WIDE_STACK - RENDER_LDS];
     int sp = 0;

@@ -179,8 +179,8 @@ typedef struct chr_propagate_stats {
     uint32_t trace_ms_n;          /* entries of trace_launch_ms filled (first CHR_TRACE_MS_MAX launches) */
     float trace_launch_ms[32];    /* device time of each trace_kernel launch, in order */
     uint32_t flat_walks;          /* walks with a direction component of non-finite reciprocal (the reference's
-                                     slab test then skips that axis): split into sub-walks by trace_kernel */
-    uint32_t flat_walks_whole;    /* such walks done whole by the multi-step (tail) kernel */
+                                     slab test then skips that axis) done by trace_kernel (flat-axis slab test) */
+    uint32_t flat_walks_whole;    /* such walks done by the multi-step (tail) kernel */
     uint32_t tail_photons;        /* photons handed to the multi-step (tail) launch (nsteps policy) */
     double tail_ms;               /* device time of that launch (HIP events; CHR_SLOT_TIMING=1, else 0) */
     uint32_t tail_max_steps;      /* most steps one photon ran in the tail launch */

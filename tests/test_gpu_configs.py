@@ -109,8 +109,9 @@ def _flatten_some(photons, seed, nplane, naxis):
 
 @pytest.mark.parametrize('ntpb,max_blocks,max_steps', [(64, 64, 1000), (256, 1024, 1000)])
 def test_flat_walks_small_detector(cuda, small_detector, ntpb, max_blocks, max_steps):
-    """(64, 64): many one-step host steps -> flat walks decomposed by the trace
-    pass; (256, 1024): one multi-step launch -> walked whole by the tail."""
+    """(64, 64): many one-step host steps -> flat walks in the trace pass;
+    (256, 1024): one multi-step launch -> flat walks in the tail (both with the
+    flat-axis slab test, propagate.hip make_slab)."""
     from chroma import gpu
     from chroma.photon_source import isotropic
     photons = _flatten_some(isotropic(30000, seed=41), 41, 3750, 470)
@@ -143,8 +144,8 @@ def test_c2_tiny_1m_binned_first_step(cuda, tiny_geo):
     assert ((host.flags & 4) != 0).sum() > 1000
 
 
-def test_c2_tiny_flat_walks_decomposed(cuda, tiny_geo):
-    """Flat walks at 1M photons on demo.tiny(): decomposed over the cut items."""
+def test_c2_tiny_flat_walks(cuda, tiny_geo):
+    """Flat walks at 1M photons on demo.tiny() (trace pass, flat-axis slab test)."""
     from chroma import gpu
     from chroma.photon_source import isotropic
     photons = _flatten_some(isotropic(1 << 20, seed=5), 5, 2000, 200)

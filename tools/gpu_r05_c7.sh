@@ -1,0 +1,12 @@
+# flat-axis slab test (flat rays walked as ordinary walks): flat parity tests, GPU suite, library A/B
+set -u
+R=${GRAFT_REPO_ROOT}
+O=$R/gpurun_out/r05_c7
+mkdir -p $O
+cd $R
+timeout -k 10 600 python -u -m pytest tests/test_gpu_configs.py -m gpu -x -v -k "flat or c2" --timeout 600 --timeout-method thread > $O/pytest_flat.log 2>&1 || { tail -30 $O/pytest_flat.log; exit 1; }
+tail -1 $O/pytest_flat.log
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { tail -30 $O/pytest_gpu.log; exit 1; }
+tail -1 $O/pytest_gpu.log
+bash tools/gpu_ab_libs.sh r05_ab_flat 2 "--steps 20 --warmup 5" base=chroma-lite_amd/chroma/_lib/ab/base.so flat=chroma-lite_amd/chroma/_lib/ab/flat.so || exit 1
+bash tools/gpu_ab_libs.sh r05_ab_flat_c5 1 "--steps 20 --warmup 5 --detector scint" base=chroma-lite_amd/chroma/_lib/ab/base.so flat=chroma-lite_amd/chroma/_lib/ab/flat.so || exit 1
