@@ -61,8 +61,8 @@ class GeometryDesc(ctypes.Structure):
 
 class WideBvhDesc(ctypes.Structure):
     """chr_wide_bvh_desc: the traversal BVH in compact (cacheable) form."""
-    _fields_ = [('nnodes', c_u32), ('nrec', c_u32), ('ncut', c_u32), ('max_depth', c_u32), ('usable', c_i32),
-                ('leaf_max', c_u32), ('h_nodes', c_vp), ('h_rec_id', c_vp), ('h_rec_rank', c_vp), ('h_cut', c_vp)]
+    _fields_ = [('nnodes', c_u32), ('nrec', c_u32), ('max_depth', c_u32), ('usable', c_i32),
+                ('leaf_max', c_u32), ('h_nodes', c_vp), ('h_rec_id', c_vp), ('h_rec_rank', c_vp)]
 
 
 class PhotonsDesc(ctypes.Structure):
@@ -128,7 +128,7 @@ _SIGNATURES = {
     'chr_wide_bvh_copy': (c_i32, [c_vp, c_vp, c_vp]),
     'chr_wide_bvh_free': (c_i32, [c_vp]),
     'chr_wide_bvh_describe': (c_i32, [c_vp, ctypes.POINTER(WideBvhDesc)]),
-    'chr_wide_bvh_export': (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp]),
+    'chr_wide_bvh_export': (c_i32, [c_vp, c_vp, c_vp, c_vp]),
     'chr_wide_bvh_key': (c_i32, [ctypes.c_char_p, c_u32]),
     'chr_wide_bvh_records': (c_i32, [ctypes.POINTER(GeometryDesc), ctypes.POINTER(WideBvhDesc), c_u32, c_u32, c_vp]),
     'chr_geometry_create_wide': (c_i32, [ctypes.POINTER(GeometryDesc), ctypes.POINTER(WideBvhDesc),

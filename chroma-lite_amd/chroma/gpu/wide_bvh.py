@@ -7,14 +7,14 @@ libchroma_amd builds over the reference BVH (csrc/wide_bvh.cpp): 33-36 s of
 host work for the 29k-PMT detector, which every process creating a
 GPUGeometry would repeat.  Its compact form (chr_wide_bvh_desc: 96-byte
 nodes, each triangle record's triangle id and reference DFS rank, the
-sub-walk cut) is a function of the mesh and the reference BVH alone; the
+nothing else) is a function of the mesh and the reference BVH alone; the
 upload rebuilds the 64-byte triangle records from the geometry
 (chr_geometry_create_wide), so a cached copy cannot go stale against the
 materials.
 
 Cache layout, next to the reference BVH it was built from:
 ``<cache_dir>/bvh/<mesh md5>/<bvh name>.wide/<builder key>/`` holding
-``nodes.npy rec_id.npy rec_rank.npy cut.npy meta.json`` (plain .npy files,
+``nodes.npy rec_id.npy rec_rank.npy meta.json`` (plain .npy files,
 memory-mapped on load, read with allow_pickle=False).  ``meta.json`` records
 a fingerprint of the reference BVH; a mismatch means rebuild.
 ``$CHROMA_WIDE_CACHE=0`` turns the cache off.
@@ -30,7 +30,7 @@ import numpy as np
 from chroma.gpu import _native
 from chroma.log import logger
 
-_ARRAYS = ('nodes', 'rec_id', 'rec_rank', 'cut')
+_ARRAYS = ('nodes', 'rec_id', 'rec_rank')
 
 
 def builder_key():
@@ -60,20 +60,18 @@ def fingerprint(bvh):
 class WideBVH(object):
     """Compact traversal BVH: arrays + the facts chr_wide_bvh_desc carries."""
 
-    def __init__(self, nodes, rec_id, rec_rank, cut, max_depth, usable, leaf_max, key):
+    def __init__(self, nodes, rec_id, rec_rank, max_depth, usable, leaf_max, key):
         self.nodes = nodes            # uint8 (nnodes, 96)
         self.rec_id = rec_id          # uint32 (nrec,)
         self.rec_rank = rec_rank      # uint32 (nrec,)
-        self.cut = cut                # uint32 (ncut, 2)
         self.max_depth, self.usable, self.leaf_max, self.key = int(max_depth), bool(usable), int(leaf_max), key
 
     def desc(self):
         ptr = lambda a: a.ctypes.data if a.size else None   # noqa: E731
         d = _native.WideBvhDesc()
-        d.nnodes, d.nrec, d.ncut = len(self.nodes), len(self.rec_id), len(self.cut)
+        d.nnodes, d.nrec = len(self.nodes), len(self.rec_id)
         d.max_depth, d.usable, d.leaf_max = self.max_depth, int(self.usable), self.leaf_max
-        d.h_nodes, d.h_rec_id, d.h_rec_rank, d.h_cut = (ptr(self.nodes), ptr(self.rec_id), ptr(self.rec_rank),
-                                                        ptr(self.cut))
+        d.h_nodes, d.h_rec_id, d.h_rec_rank = ptr(self.nodes), ptr(self.rec_id), ptr(self.rec_rank)
         return d
 
     def records(self, packed, first=0, n=None):
@@ -97,12 +95,10 @@ def build(packed):
         nodes = np.empty((d.nnodes, 96), np.uint8)
         rec_id = np.empty(d.nrec, np.uint32)
         rec_rank = np.empty(d.nrec, np.uint32)
-        cut = np.empty((d.ncut, 2), np.uint32)
-        _native.call('chr_wide_bvh_export', h, nodes.ctypes.data, rec_id.ctypes.data, rec_rank.ctypes.data,
-                     cut.ctypes.data if d.ncut else None)
+        _native.call('chr_wide_bvh_export', h, nodes.ctypes.data, rec_id.ctypes.data, rec_rank.ctypes.data)
     finally:
         _native.lib().chr_wide_bvh_free(h)
-    return WideBVH(nodes, rec_id, rec_rank, cut, d.max_depth, d.usable, d.leaf_max, builder_key())
+    return WideBVH(nodes, rec_id, rec_rank, d.max_depth, d.usable, d.leaf_max, builder_key())
 
 
 def cache_enabled():
@@ -162,8 +158,8 @@ def load(cache_dir, mesh_hash, name, key, fp):
     except (OSError, ValueError) as e:
         logger.warning('traversal BVH cache %s unreadable: %s', d, e)
         return None
-    return WideBVH(arrs['nodes'], arrs['rec_id'], arrs['rec_rank'], arrs['cut'], meta['max_depth'],
-                   meta['usable'], meta['leaf_max'], key)
+    return WideBVH(arrs['nodes'], arrs['rec_id'], arrs['rec_rank'], meta['max_depth'], meta['usable'],
+                   meta['leaf_max'], key)
 
 
 def obtain(bvh, packed):

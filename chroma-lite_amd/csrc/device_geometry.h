@@ -66,9 +66,6 @@ struct DevGeom {
     const chr_wireplane_desc *wireplanes;
     const uint4 *wnodes;             // 8-wide SAH BVH, node i at wnodes[wstride * i] (wide_bvh.h)
     const float4 *wtri;              // 3 float4 per leaf triangle record (wide_bvh.h)
-    const uint2 *wcut;               // sub-walk items (node, child mask) of a decomposed walk (wide_bvh.h)
-    const uint32_t *wrank_rec;       // reference DFS rank -> triangle record (wtri index)
-    uint32_t nwcut;
     uint32_t nwnodes, nwtri;
     uint32_t wstride;                // uint4 per node slot: 8 (each 96-byte node padded to one 128-byte line)
     float ox, oy, oz, scale;         // world_origin, world_scale

@@ -219,7 +219,7 @@ struct Stager {
 // the traversal BVH (compact form w) into HBM: 96-byte nodes in 128-byte slots
 // (one line per node: r01 no gain over the packed stride; r03 ab21, where the
 // later steps' walks are line-bound, 463.7 -> 467.1 M/s), the 64-byte triangle
-// records rebuilt from the geometry, the sub-walk cut and the rank -> record map
+// records rebuilt from the geometry
 static int upload_wide(chr_geometry *g, const chr_geometry_desc *d, const chr_wide_bvh_desc *w) {
     chr::WideCheck c;
     CHR_TRY(chr::wide_validate(d, w, c));
@@ -250,11 +250,6 @@ static int upload_wide(chr_geometry *g, const chr_geometry_desc *d, const chr_wi
     CHR_TRY(st.finish());
     dg.nwnodes = w->nnodes;
     dg.nwtri = w->nrec;
-    CHR_TRY(dev_upload(g, w->h_cut, (size_t)w->ncut * 8, &p));
-    dg.wcut = (const uint2 *)p;
-    dg.nwcut = w->ncut;
-    CHR_TRY(dev_upload(g, c.rank_rec.data(), c.rank_rec.size() * 4, &p));
-    dg.wrank_rec = (const uint32_t *)p;
     return CHR_OK;
 }
 
@@ -325,14 +320,12 @@ static int geometry_create(const chr_geometry_desc *d, const chr_wide_bvh_desc *
                 std::vector<chr::WideTri>().swap(wb.tri);
                 built.nnodes = (uint32_t)wb.nodes.size();
                 built.nrec = (uint32_t)rec_id.size();
-                built.ncut = (uint32_t)(wb.cut.size() / 2);
                 built.max_depth = wb.max_depth;
                 built.usable = wb.usable ? 1 : 0;
                 built.leaf_max = wb.leaf_max;
                 built.h_nodes = wb.nodes.data();
                 built.h_rec_id = rec_id.data();
                 built.h_rec_rank = rec_rank.data();
-                built.h_cut = wb.cut.data();
                 if (built.usable && !exact_only) w = &built;
             }
             if (w) {

@@ -1417,8 +1417,6 @@ struct PropagateArgs {
     uint32_t *counters;                // [0]: stack overflows
     const uint32_t *order;             // coherence order: work-item t runs slot order[t] (nullptr: t)
     const int2 *hits;                  // shade_kernel: walk result per queue position (trace_kernel)
-    const unsigned long long *flat_best;   // shade_kernel: results of the flat walks (FLAT_HIT entries of hits)
-    uint32_t *zero_word;               // shade_kernel: word cleared once (next step's flat-walk count)
     uint32_t *diag;                    // multi-step kernels (nullptr: off): [0] += flat walks walked whole,
                                        // [1] max steps of one photon, [2..3] u64 max of (cycles << 16 | steps),
                                        // [4..13] u64 sums over photons of > 64 steps (tail kernel): walk
@@ -1437,9 +1435,6 @@ struct PropagateArgs {
 };
 // modes of a device-driven step slot (step_head_kernel)
 constexpr uint32_t STEP_IDLE = 0, STEP_ONE = 1, STEP_TAIL = 2;
-// hits[q] = (FLAT_HIT, f): queue position q holds flat walk f of this step,
-// its result is flat_best[f] (trace_kernel)
-constexpr int FLAT_HIT = -3;
 
 __device__ __forceinline__ V3 load3(const float *p, uint32_t i) { return v3(p[3 * i], p[3 * i + 1], p[3 * i + 2]); }
 __device__ __forceinline__ void store3(float *p, uint32_t i, V3 v) { p[3 * i] = v.x; p[3 * i + 1] = v.y; p[3 * i + 2] = v.z; }
@@ -1708,7 +1703,6 @@ __global__ __launch_bounds__(BLOCK, MINW) void shade_kernel(const DevGeom *__res
     const DevGeom g = phys_cache(*gdev, phys_lds, SHADE_PHYS_WORDS);
     const uint32_t slot = blockIdx.x * BLOCK + threadIdx.x;
     const uint32_t n = a.dev_n ? *a.dev_n - 1u : (uint32_t)a.nthreads;
-    if (slot == 0 && a.zero_word) *a.zero_word = 0u;
     if (slot >= cap || (slot & ~63u) >= n) return;   // whole waves (cap % 64 == 0)
     chr_xorwow rng;
     bool have_rng = false;
@@ -1742,13 +1736,8 @@ __global__ __launch_bounds__(BLOCK, MINW) void shade_kernel(const DevGeom *__res
                 p.history |= CHR_NO_HIT | CHR_NAN_ABORT;
             } else {
                 State s;
-                int tri = cur.hit.x;
+                const int tri = cur.hit.x;
                 s.distance = __int_as_float(cur.hit.y);
-                if (tri == FLAT_HIT) {            // (distance bits, reference rank) of a decomposed walk
-                    const unsigned long long key = a.flat_best[cur.hit.y];
-                    tri = key == ~0ull ? -1 : (int)g.wrank_rec[(uint32_t)key];
-                    s.distance = key == ~0ull ? -1.0f : __uint_as_float((uint32_t)(key >> 32));
-                }
                 pf.tick(P_FILL);
                 pf.call(P_FILL);
                 finish_fill<true>(g, s, p, tri);
@@ -2712,11 +2701,7 @@ struct TraceArgs {
                                  // queue -> flags / pos / dir / last_hit per refill instead)
     uint32_t *walk_hist;         // COUNT: [0..31] walks by log2(nodes + triangles), [32..33] u64 max (cost << 32 | photon)
     uint2 *spill;                // stack entries >= SL: (WIDE_STACK - SL) x gridDim.x*BLOCK, entry-major (HBM, no scratch)
-    // flat walks of this step (walk_kind 2), enrolled before the launch:
-    const uint32_t *flat_q;      // queue positions
-    const uint32_t *flat_count;  // how many (device word)
-    unsigned long long *flat_best;   // per flat walk: min over its sub-walks of (distance bits << 32 | rank)
-    uint32_t *diag;              // [0] += flat walks of this launch (nullptr: off)
+    uint32_t *diag;              // [0] += flat rays walked by this launch (nullptr: off)
     // device-driven steps (nullptr: host-driven): the queue length is *dev_n - 1
     // (the input queue's count header) and the launch runs only if *mode is STEP_ONE
     const uint32_t *dev_n;
@@ -2724,16 +2709,6 @@ struct TraceArgs {
 };
 constexpr uint32_t CLAIM = 64;       // rays a wave takes from the ray counter per refill (at most)
 constexpr uint32_t DRAIN_MAX = 4;    // a wave drains its last <= DRAIN_MAX walks whole-wave
-
-// Enrol queue position p in the flat list of the next trace launch (its walk
-// is flat, walk_kind 2): f = slot in the flat list, hits[p] = (FLAT_HIT, f).
-__device__ __forceinline__ void enrol_flat_at(uint32_t p, int2 *hits, uint32_t *flat_q, uint32_t *flat_count,
-                                              unsigned long long *flat_best) {
-    const uint32_t f = atomicAdd(flat_count, 1u);
-    flat_q[f] = p;
-    flat_best[f] = ~0ull;
-    hits[p] = make_int2(FLAT_HIT, (int)f);
-}
 
 // Ray record of one queue position, the only thing trace_kernel's refill
 // reads: written in walk order by the kernel that builds the queue (the
@@ -2743,7 +2718,7 @@ __device__ __forceinline__ void enrol_flat_at(uint32_t p, int2 *hits, uint32_t *
 // of the photon arrays (propagate.cu:280-293).  Words: origin, the normalised
 // direction (propagate.cu:280-281, the same float operations as the walk
 // made), the photon's last hit, its queue position; bit 31 of the last word:
-// no ordinary walk here (dead on entry, NaN state, or flat: walked as sub-walks).
+// no walk here (dead on entry, or NaN state).
 constexpr uint32_t RAY_SKIP = 0x80000000u;
 __device__ __forceinline__ void put_ray(uint4 *rays, uint32_t j, V3 o, V3 d, int32_t last_hit, uint32_t q, bool walk) {
     rays[2 * (size_t)j] = make_uint4(__float_as_uint(o.x), __float_as_uint(o.y), __float_as_uint(o.z),
@@ -2752,29 +2727,22 @@ __device__ __forceinline__ void put_ray(uint4 *rays, uint32_t j, V3 o, V3 d, int
                                          q | (walk ? 0u : RAY_SKIP));
 }
 
-// Enrol queue position p for the next trace launch if its walk is flat; with
-// rays, also write its ray record at walk position j.
-__device__ __forceinline__ void enrol_flat(const float *pos, const float *dir, uint32_t pid, uint32_t p, int2 *hits,
-                                           uint32_t *flat_q, uint32_t *flat_count, unsigned long long *flat_best,
-                                           uint4 *rays = nullptr, const int32_t *last_hit = nullptr,
-                                           uint32_t j = 0) {
+// The ray record of photon pid at queue position p, written at walk position j.
+__device__ __forceinline__ void put_photon_ray(const float *pos, const float *dir, uint32_t pid, uint32_t p,
+                                               uint4 *rays, const int32_t *last_hit, uint32_t j) {
     const V3 o = load3(pos, pid);
     V3 d = load3(dir, pid);
     d = d / norm(d);
-    const int kind = walk_kind(o, d);
-    if (kind == 2) enrol_flat_at(p, hits, flat_q, flat_count, flat_best);
-    if (rays) put_ray(rays, j, o, d, last_hit[pid], p, kind == 1);
+    put_ray(rays, j, o, d, last_hit[pid], p, walk_kind(o, d) == 1);
 }
 
-// first host step: enrol the flat walks of the initial queue; with keys, also
-// the direction-binning key of every queue position (bin_key_kernel's, one
-// pass over the photons instead of two), and with rays the ray record of every
-// queue position at its own index (binned: permuted into walk order after the sort)
+// first host step: with keys, the direction-binning key of every queue
+// position (bin_key_kernel's, one pass over the photons instead of two), and
+// with rays the ray record of every queue position at its own index (binned:
+// permuted into walk order after the sort)
 __global__ __launch_bounds__(BLOCK) void classify_kernel(const float *pos, const float *dir, const uint32_t *flags,
                                                          const int32_t *last_hit, const uint32_t *queue, uint32_t n,
-                                                         int2 *hits, uint32_t *flat_q, uint32_t *flat_count,
-                                                         unsigned long long *flat_best, uint32_t *keys, uint32_t *vals,
-                                                         uint4 *rays) {
+                                                         uint32_t *keys, uint32_t *vals, uint4 *rays) {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     if (i >= n) return;
     const uint32_t pid = queue[i];
@@ -2786,7 +2754,7 @@ __global__ __launch_bounds__(BLOCK) void classify_kernel(const float *pos, const
         if (rays) put_ray(rays, i, v3(0.0f, 0.0f, 0.0f), v3(0.0f, 0.0f, 0.0f), -1, i, false);
         return;
     }
-    enrol_flat(pos, dir, pid, i, hits, flat_q, flat_count, flat_best, rays, last_hit, i);
+    if (rays) put_photon_ray(pos, dir, pid, i, rays, last_hit, i);
 }
 
 // rays_out[j] = rays_in[order[j]]: the first step's records in the binned walk order
@@ -2831,14 +2799,8 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
     WalkCounts cnt{0u, 0u, 0u, 0u, 0u, 0ull, 0ull, 0u};
     bool has_ray = false, exhausted = false;
     uint32_t q = 0, pid = 0, walk_cost = 0;
-    // work items: [0, n) the queued rays (flat ones skipped), then K sub-walks
-    // per flat walk (K = the geometry's cut size; 1 = the whole walk)
-    const uint32_t nflat = a.flat_count ? *a.flat_count : 0u;
-    const uint32_t K = (g.nwcut > 1u && nflat <= (1u << 30) / g.nwcut) ? g.nwcut : 1u;
-    const uint32_t total = n + nflat * K;
-    int flat_f = -1;                // flat walk of the current sub-walk (-1: an ordinary ray)
+    const uint32_t total = n;       // work items: the queued rays
     uint32_t nflat_rays = 0;        // flat rays walked by this work-item (flat-axis slab test; diagnostic)
-    uint32_t cmask = 0xFFu;         // children of the first node this walk may enter
     V3 o = v3(0.0f, 0.0f, 0.0f), d = v3(0.0f, 0.0f, 1.0f);
     RaySlab slab = make_slab(o, o, d);
     float best = 0.0f;
@@ -2862,9 +2824,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
     while (true) {
         pf.tick(P_REFILL);   // the last step goes to the region each work-item was in
         if (has_ray && walk_done && pleft == 0 && qh == qt) {   // walk over: publish (mesh.h:123-125)
-            if (flat_f < 0) a.hits[q] = make_int2(best_id, __float_as_int(best_id == -1 ? -1.0f : best));
-            else if (best_id != -1)   // a sub-walk: its best joins the flat walk's minimum
-                atomicMin(a.flat_best + flat_f, ((unsigned long long)__float_as_uint(best) << 32) | best_rank);
+            a.hits[q] = make_int2(best_id, __float_as_int(best_id == -1 ? -1.0f : best));
             has_ray = false;
             if constexpr (COUNT) {
                 if (a.walk_hist) {
@@ -2888,7 +2848,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
                 if (!has_ray && rank < want) {
                     bool start = false;
                     if (j < n && a.rays) {
-                        // the ray record: one 32-B load (put_ray); skip bit: dead / NaN / flat
+                        // the ray record: one 32-B load (put_ray); skip bit: dead / NaN
                         const uint4 r0 = gld(a.rays + 2 * (size_t)j), r1 = gld(a.rays + 2 * (size_t)j + 1);
                         q = r1.w & ~RAY_SKIP;
                         if (!(r1.w & RAY_SKIP)) {
@@ -2897,49 +2857,26 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
                             last = r1.z;
                             if constexpr (COUNT) pid = a.walk_hist ? a.queue[q] : q;
                             start = true;
-                            flat_f = -1;
                             node = 0;
-                            cmask = 0xFFu;
                             best = __builtin_inff();
                             best_rank = 0xFFFFFFFFu;
                         }
                     } else if (j < n) {
                         q = a.order ? a.order[j] : j;
                         pid = a.queue[q];
-                        // dead on entry / NaN: no walk (the step kernel skips / aborts them);
-                        // flat: enrolled before the launch, walked as sub-walks below
+                        // dead on entry / NaN: no walk (the step kernel skips / aborts them)
                         if (!((a.flags[pid] & 0xFFFFu) & DEAD_MASK)) {
                             o = load3(a.pos, pid);
                             d = load3(a.dir, pid);
                             d = d / norm(d);                        // propagate.cu:280-281
                             if (walk_kind(o, d) == 1) {
                                 start = true;
-                                flat_f = -1;
                                 node = 0;
-                                cmask = 0xFFu;
                                 best = __builtin_inff();
                                 best_rank = 0xFFFFFFFFu;
                                 last = (uint32_t)a.last_hit[pid];
                             }
                         }
-                    } else if (j < total) {                       // sub-walk k of flat walk f
-                        const uint32_t it = j - n, f = it / K, k = it - f * K;
-                        q = a.flat_q[f];
-                        pid = a.queue[q];
-                        o = load3(a.pos, pid);
-                        d = load3(a.dir, pid);
-                        d = d / norm(d);
-                        const uint2 item = K == 1u ? make_uint2(0u, 0xFFu) : g.wcut[k];
-                        // start from the best any sub-walk has published (only ever larger
-                        // than the final minimum, so culling with it is conservative)
-                        const unsigned long long key = a.flat_best[f];
-                        start = true;
-                        flat_f = (int)f;
-                        node = item.x;
-                        cmask = item.y;
-                        best = key == ~0ull ? __builtin_inff() : __uint_as_float((uint32_t)(key >> 32));
-                        best_rank = key == ~0ull ? 0xFFFFFFFFu : (uint32_t)key;
-                        last = (uint32_t)a.last_hit[pid];
                     }
                     if (start) {
                         slab = make_slab(o, v3(-o.x / d.x, -o.y / d.y, -o.z / d.z), v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z));
@@ -2949,7 +2886,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
                         has_ray = true;
                         walk_cost = 0;
                         pf.call(P_REFILL);
-                        if (slab.flat && flat_f < 0) nflat_rays++;
+                        if (slab.flat) nflat_rays++;
                         if constexpr (COUNT) cnt.walks++;
                     }
                 }
@@ -2965,8 +2902,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
             // every small launch).  Each restarts from the root seeded with its
             // best so far (conservative culling, the same nearest hit); the
             // lanes' stacks are abandoned and their LDS rows reused.
-            if (exhausted && __ballot(has_ray) != 0 && (uint32_t)__popcll(__ballot(has_ray)) <= DRAIN_MAX &&
-                __ballot(has_ray && flat_f >= 0) == 0) {   // no cut-item sub-walks (they start mid-tree)
+            if (exhausted && __ballot(has_ray) != 0 && (uint32_t)__popcll(__ballot(has_ray)) <= DRAIN_MAX) {
                 drain = true;   // after the loop, where the walk state below is no longer live
                 break;
             }
@@ -3005,13 +2941,12 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
 #ifdef CHR_DEVICE_PROFILE
             pf.call(P_NODE);
             for (int k = 0; k < 8; ++k)
-                pf.call(P_BOX, ((((k < 4 ? a4.z : a4.w) >> (8 * (k & 3))) & 0xFFu) != 0u && ((cmask >> k) & 1u)) ? 1u : 0u);
+                pf.call(P_BOX, (((k < 4 ? a4.z : a4.w) >> (8 * (k & 3))) & 0xFFu) != 0u ? 1u : 0u);
 #endif
             uint32_t near_node;
             float near_t;
             uint32_t leaf_mask =
-                expand_node<SL, TB>(h, a1, a2, a3, a4, a5, slab, best, near_node, near_t, st, sp, overflow, cmask);
-            cmask = 0xFFu;
+                expand_node<SL, TB>(h, a1, a2, a3, a4, a5, slab, best, near_node, near_t, st, sp, overflow, 0xFFu);
             node = near_node;
             while (leaf_mask) {
                 const int k = __builtin_ctz(leaf_mask);
@@ -3103,7 +3038,6 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
     prof_add(CHR_PROF_TRACE_KERNEL, 1ull, pf.total());
 #endif
     if (overflow) atomicAdd(a.counters, overflow);
-    if (a.diag && nflat && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(a.diag, nflat);
     if (a.diag && nflat_rays) atomicAdd(a.diag, nflat_rays);
     if constexpr (COUNT) {
         unsigned long long *c64 = reinterpret_cast<unsigned long long *>(a.counters + 2);
@@ -3225,20 +3159,17 @@ __device__ __forceinline__ uint32_t word_offset(const uint32_t *word_offsets, co
     return word_offsets[w] + block_prefix[w / SCAN_WORDS];
 }
 
-// Survivors of a split step also enrol their next walk if it is flat
-// (FlatEnrol: next step's flat list; pos == nullptr: off).
-struct FlatEnrol {
+// Survivors of a split step also write their next walk's ray record
+// (RayEnrol: the next step's records, in queue order; pos == nullptr: off).
+struct RayEnrol {
     const float *pos, *dir;
-    int2 *hits;
-    uint32_t *flat_q, *flat_count;
-    unsigned long long *flat_best;
-    uint4 *rays;                 // + the next step's ray records, in queue order (nullptr: off)
+    uint4 *rays;
     const int32_t *last_hit;
 };
 __global__ __launch_bounds__(BLOCK) void scatter_queue_kernel(const unsigned long long *masks, const uint32_t *word_offsets,
                                                                const uint32_t *block_prefix, const uint32_t *base,
                                                                const uint32_t *in_queue, int32_t first, int32_t n,
-                                                               uint32_t *out_queue, FlatEnrol fe, const uint32_t *dev_n,
+                                                               uint32_t *out_queue, RayEnrol fe, const uint32_t *dev_n,
                                                                const uint32_t *mode, uint32_t skip) {
     // skip: a second mode that runs nothing here (a tail run on its own stream
     // by chr_propagate_batches leaves no queue behind)
@@ -3254,9 +3185,7 @@ __global__ __launch_bounds__(BLOCK) void scatter_queue_kernel(const unsigned lon
             const uint32_t pid = in_queue[first + id];
             out_queue[o] = pid;
             // out_queue[0] is the count header: position o - 1 of the next step's queue
-            if (fe.pos)
-                enrol_flat(fe.pos, fe.dir, pid, o - 1u, fe.hits, fe.flat_q, fe.flat_count, fe.flat_best, fe.rays,
-                           fe.last_hit, o - 1u);
+            if (fe.pos) put_photon_ray(fe.pos, fe.dir, pid, o - 1u, fe.rays, fe.last_hit, o - 1u);
         }
     }
 }
@@ -3717,8 +3646,6 @@ static int launch_chunk(const chr_geometry *g, const chr_photons *ph, uint32_t *
     a.alive_masks = masks; a.counters = counters;
     a.order = nullptr;
     a.hits = nullptr;
-    a.flat_best = nullptr;
-    a.zero_word = nullptr;
     a.diag = nullptr;
     a.dev_n = nullptr;
     a.mode = nullptr;
@@ -3732,7 +3659,7 @@ static int launch_chunk(const chr_geometry *g, const chr_photons *ph, uint32_t *
     launch_mask_scan(masks, nwords, offsets, bsums, out_queue, counters + 1, nullptr, stream);
     hipLaunchKernelGGL(scatter_queue_kernel, dim3(grid_for(nthreads)), dim3(BLOCK), 0, stream, masks, offsets, bsums,
                        counters + 1, in_queue, first, nthreads, out_queue,
-                       FlatEnrol{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr}, (const uint32_t *)nullptr,
+                       RayEnrol{nullptr, nullptr, nullptr, nullptr}, (const uint32_t *)nullptr,
                        (const uint32_t *)nullptr, STEP_IDLE);
     CHR_HIP_CHECK(hipGetLastError());
     return CHR_OK;
@@ -3749,30 +3676,25 @@ static int device_cus() {
     return cus[dev & 15];
 }
 
-// Flat-walk bookkeeping of one propagate (trace_kernel): one list of queue
-// positions (the step's flat walks; the next step's list is written by the
-// step's scatter after the trace has read this one), their results, and
-// control words: ctl[1 + cur] the list count of the step, ctl[2 - cur] the
-// next step's, ctl[3] flat walks decomposed (diagnostic), ctl[4] flat walks
-// walked whole by the multi-step kernels (diagnostic).
+// Split-step bookkeeping of one propagate (trace_kernel): control words --
+// ctl[3] flat rays walked by the trace kernel, ctl[4] flat rays walked by the
+// multi-step kernels (diagnostics; rounds 2-4 decomposed flat walks into
+// sub-walks, §11.6) -- and the ray records.
 struct FlatCtx {
-    uint32_t *flat_q;
-    unsigned long long *flat_best;
     uint32_t *ctl;
-    int cur;
     bool enrol_next;
     // trace_kernel's ray records (put_ray): rays in queue order (the first
     // step's classification, then every step's scatter for the next step),
     // rays_walk the binned first step's records permuted into walk order
     uint4 *rays = nullptr, *rays_walk = nullptr;
-    uint32_t cap = 0;                   // entries of flat_q / flat_best
 };
 static int flat_get(uint32_t n, FlatCtx &fc, int ctx = 0) {
     static thread_local Scratch s[NCTX][16];
     int dev = 0;
     CHR_HIP_CHECK(hipGetDevice(&dev));
     Scratch &x = s[ctx % NCTX][dev & 15];
-    const size_t bytes = 256 + (size_t)n * 12 + 64;
+    (void)n;
+    const size_t bytes = 256;
     if (x.bytes < bytes) {
         if (x.ptr) CHR_HIP_CHECK(hipFree(x.ptr));
         x.ptr = nullptr;
@@ -3780,11 +3702,7 @@ static int flat_get(uint32_t n, FlatCtx &fc, int ctx = 0) {
         x.bytes = bytes;
     }
     fc.ctl = (uint32_t *)x.ptr;
-    fc.flat_best = (unsigned long long *)((char *)x.ptr + 256);
-    fc.flat_q = (uint32_t *)(fc.flat_best + n);
-    fc.cur = 0;
     fc.enrol_next = false;
-    fc.cap = n;
     return CHR_OK;
 }
 
@@ -3881,15 +3799,13 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
     a.alive_masks = masks; a.counters = counters;
     a.order = nullptr;
     a.hits = nullptr;
-    a.flat_best = nullptr;
-    a.zero_word = nullptr;
     a.diag = fc ? fc->ctl + 4 : nullptr;
     a.dev_n = dev_n;
     a.mode = mode;
     a.want = STEP_ONE;
     a.work = nullptr;
     a.prio = 0;
-    FlatEnrol fe{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+    RayEnrol fe{nullptr, nullptr, nullptr, nullptr};
     const uint32_t threads = std::min(cap, (n + 63u) & ~63u);
     const StepVariant sv = select_step_variant(g);
     // host-driven: the split when this launch is one step; device-driven: the
@@ -3923,7 +3839,6 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
         CHR_HIP_CHECK(hipMemsetAsync(next, 0, 4, stream));
     }
     if (split) {
-        uint32_t *count_cur = fc->ctl + 1 + fc->cur, *count_next = fc->ctl + 1 + (fc->cur ^ 1);
         // direction binning: 16-bit radix sort of (direction cell, queue position); hits region:
         // [hits n x int2][next + pad, 16 words][keys n][values n][walk hist 64 words]
         // (device-driven slots bin only the first step, whose length the host knows)
@@ -3934,24 +3849,19 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
         // ray records: the first step's from its classification, later steps' from
         // the previous step's scatter (enrol_next)
         const bool use_rays = fc->rays && (first_one_step || fc->enrol_next);
-        if (first_one_step && pre)   // flat walks of the initial queue (later steps: enrolled by the previous scatter)
+        if (first_one_step && pre)   // the initial queue's ray records and keys (later steps: the previous scatter)
             hipLaunchKernelGGL(classify_kernel, dim3(grid_for(n)), dim3(BLOCK), 0, stream, ph->d_pos, ph->d_dir,
-                               ph->d_flags, ph->d_last_hit_triangles, in_queue, n, hits, fc->flat_q, count_cur,
-                               fc->flat_best, bin_now ? keys : nullptr, bin_now ? order : nullptr,
-                               use_rays ? fc->rays : nullptr);
+                               ph->d_flags, ph->d_last_hit_triangles, in_queue, n, bin_now ? keys : nullptr,
+                               bin_now ? order : nullptr, use_rays ? fc->rays : nullptr);
         TraceArgs ta;
         ta.pos = ph->d_pos; ta.dir = ph->d_dir; ta.flags = ph->d_flags; ta.last_hit = ph->d_last_hit_triangles;
         ta.queue = in_queue; ta.n = n; ta.hits = hits; ta.next = next; ta.counters = counters; ta.order = nullptr;
         ta.rays = use_rays ? fc->rays : nullptr;
         ta.walk_hist = nullptr;
-        ta.flat_q = fc->flat_q; ta.flat_count = count_cur; ta.flat_best = fc->flat_best; ta.diag = fc->ctl + 3;
+        ta.diag = fc->ctl + 3;
         ta.dev_n = dev_n;
         ta.mode = mode;
-        a.flat_best = fc->flat_best;
-        a.zero_word = count_next;   // cleared by the shade pass, filled by this step's scatter
-        if (fc->enrol_next)
-            fe = FlatEnrol{ph->d_pos, ph->d_dir, hits, fc->flat_q, count_next, fc->flat_best, fc->rays,
-                           ph->d_last_hit_triangles};
+        if (fc->enrol_next) fe = RayEnrol{ph->d_pos, ph->d_dir, fc->rays, ph->d_last_hit_triangles};
         if (trace_steps() && pre) {   // debugging: per-walk cost histogram (counting variants), printed per step
             ta.walk_hist = next + 16 + 2 * (size_t)(sc ? sc->n_layout : n);
             CHR_HIP_CHECK(hipMemsetAsync(ta.walk_hist, 0, 34 * 4, stream));
@@ -4268,7 +4178,6 @@ static int device_slots(const chr_geometry *g, const chr_photons *ph, uint32_t n
                          b.hits, b.sort_space, k == 0, ev[2], timing ? ev[3] : nullptr, &split, &b.fc, &sc);
         if (rc) return rc;
         if (timing == 2) CHR_HIP_CHECK(hipEventRecord(ev[4], stream));
-        b.fc.cur ^= 1;   // the step's scatter enrolled the next step's flat walks in the other list
         cur ^= 1;
         scatter_first = 0;
         if (k >= 1) {   // slot k - 1's head has run (its mode is known): is there a slot k + 1?
@@ -4492,7 +4401,6 @@ extern "C" int chr_propagate(const chr_geometry *g, const chr_photons *ph, uint3
                              nsteps, use_weights, scatter_first, scratch, stream, events[0], events[1], hits,
                              sort_space, step == 0, events[2], events[3], &split_step, &fc);
             if (rc) return rc;
-            fc.cur ^= 1;   // the step's scatter enrolled the next step's flat walks in the other list
             st.launches++;
             nchunks = 1;
             if (split_step) {

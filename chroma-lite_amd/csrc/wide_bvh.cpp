@@ -395,30 +395,6 @@ int build_wide_bvh(const chr_geometry_desc *d, WideBVH &out) {
     }
     out.tri.resize(tri_next);
     if (7 * (out.max_depth + 1) + 1 > (uint32_t)WIDE_STACK) out.usable = false;
-    // rank -> triangle record (the tie-break rank identifies the triangle of a
-    // decomposed walk's (distance, rank) result)
-    out.rank_rec.assign(nreach, 0xFFFFFFFFu);
-    for (size_t i = 0; i < out.tri.size(); ++i)
-        if (out.tri[i].rank < nreach) out.rank_rec[out.tri[i].rank] = (uint32_t)i;
-    // cut: BFS frontier of inner nodes until it holds WIDE_CUT_TARGET nodes;
-    // nodes above it contribute their leaf children as (node, leaf mask) items
-    out.cut.clear();
-    std::vector<uint32_t> frontier{0}, nextf;
-    while (!frontier.empty() && frontier.size() < WIDE_CUT_TARGET) {
-        nextf.clear();
-        for (uint32_t n : frontier) {
-            const WideNode &W = out.nodes[n];
-            uint32_t leaf_mask = 0;
-            for (int k = 0; k < 8; ++k) {
-                if (W.kind[k] == 0) continue;
-                if (W.kind[k] == WIDE_INNER) nextf.push_back(W.child_base + W.off[k]);
-                else leaf_mask |= 1u << k;
-            }
-            if (leaf_mask) { out.cut.push_back(n); out.cut.push_back(leaf_mask); }
-        }
-        frontier.swap(nextf);
-    }
-    for (uint32_t n : frontier) { out.cut.push_back(n); out.cut.push_back(0xFFu); }
     return CHR_OK;
 }
 
@@ -434,7 +410,7 @@ void wide_compact(const WideBVH &b, std::vector<uint32_t> &rec_id, std::vector<u
 }
 
 int wide_validate(const chr_geometry_desc *d, const chr_wide_bvh_desc *w, WideCheck &out) {
-    if (!w->h_nodes || w->nnodes == 0 || (w->nrec && (!w->h_rec_id || !w->h_rec_rank)) || (w->ncut && !w->h_cut))
+    if (!w->h_nodes || w->nnodes == 0 || (w->nrec && (!w->h_rec_id || !w->h_rec_rank)))
         return chr::fail(CHR_ERR_INVALID, "wide BVH: missing arrays");
     if (!w->usable) return chr::fail(CHR_ERR_INVALID, "wide BVH: marked unusable (use chr_geometry_create)");
     if (w->nrec > d->ntriangles) return chr::fail(CHR_ERR_INVALID, "wide BVH: %u records > %u triangles", w->nrec, d->ntriangles);
@@ -466,8 +442,6 @@ int wide_validate(const chr_geometry_desc *d, const chr_wide_bvh_desc *w, WideCh
     }
     if (7 * (maxd + 1) + 1 > (uint32_t)WIDE_STACK)
         return chr::fail(CHR_ERR_INVALID, "wide BVH: depth %u exceeds the walk's stack", maxd);
-    for (uint32_t i = 0; i < w->ncut; ++i)
-        if (w->h_cut[2 * i] >= nn) return chr::fail(CHR_ERR_INVALID, "wide BVH: cut item %u out of range", i);
     // records: triangle ids in range, ranks a permutation of [0, nrec)
     out.rank_rec.assign(nrec, 0xFFFFFFFFu);
     int bad = 0;
@@ -580,15 +554,14 @@ extern "C" int chr_wide_bvh_describe(const chr_wide_result *r, chr_wide_bvh_desc
     std::memset(out, 0, sizeof(*out));
     out->nnodes = (uint32_t)r->b.nodes.size();
     out->nrec = (uint32_t)r->b.tri.size();
-    out->ncut = (uint32_t)(r->b.cut.size() / 2);
     out->max_depth = r->b.max_depth;
     out->usable = r->b.usable ? 1 : 0;
     out->leaf_max = r->b.leaf_max;
     return CHR_OK;
 }
 
-extern "C" int chr_wide_bvh_export(const chr_wide_result *r, void *h_nodes, uint32_t *h_rec_id, uint32_t *h_rec_rank,
-                                   uint32_t *h_cut) {
+extern "C" int chr_wide_bvh_export(const chr_wide_result *r, void *h_nodes, uint32_t *h_rec_id,
+                                   uint32_t *h_rec_rank) {
     if (!r) return chr::fail(CHR_ERR_INVALID, "chr_wide_bvh_export: null handle");
     if (h_nodes) std::memcpy(h_nodes, r->b.nodes.data(), r->b.nodes.size() * sizeof(chr::WideNode));
     if (h_rec_id || h_rec_rank) {
@@ -599,7 +572,6 @@ extern "C" int chr_wide_bvh_export(const chr_wide_result *r, void *h_nodes, uint
             if (h_rec_rank) h_rec_rank[i] = r->b.tri[i].rank;
         }
     }
-    if (h_cut) std::memcpy(h_cut, r->b.cut.data(), r->b.cut.size() * 4);
     return CHR_OK;
 }
 

@@ -33,7 +33,7 @@ constexpr uint8_t WIDE_INNER = 0x80;
 
 // version of the builder's output (the traversal-BVH cache key, chr_wide_bvh_key):
 // bump it whenever the same inputs would build a different tree
-constexpr int WIDE_FORMAT = 1;
+constexpr int WIDE_FORMAT = 2;   // 2: no sub-walk cut (round 5)
 
 struct alignas(16) WideNode {
     float origin[3];
@@ -67,21 +67,7 @@ struct WideBVH {
     uint32_t max_depth = 0;        // levels below the root
     uint32_t leaf_max = 0;         // builder setting used
     bool usable = true;            // false: the exact-order traversal must be used
-    // Decomposition of one walk into independent sub-walks (flat rays, see
-    // propagate.hip trace_kernel): (node, child mask) pairs whose subtrees
-    // partition the triangle records -- the nodes of one BFS frontier (all
-    // children) plus the leaf children of the nodes above it.
-    std::vector<uint32_t> cut;     // 2 words per item
-    std::vector<uint32_t> rank_rec; // reference DFS rank -> triangle record (index into tri)
 };
-
-// target number of sub-walks per decomposed walk (frontier size): the longest
-// sub-walk sets the launch time.  The BFS stops at the first level whose
-// frontier reaches the target, so a cut holds between 2^18 and 8 x 2^18 items
-// (one 8-wide level overshoots by up to 8x).  r02 rocprof: a 32,768-item cut
-// left ~1,200-node subtrees on the 29k detector and one flat walk made a 15 ms
-// launch; 2^18 items make each subtree about 8x smaller.
-constexpr uint32_t WIDE_CUT_TARGET = 1u << 18;
 
 // stack capacity of the wide traversal (entries); the builder marks a tree
 // whose worst-case stack (7 pushes per level) would not fit as unusable
@@ -94,7 +80,7 @@ int build_wide_bvh(const chr_geometry_desc *d, WideBVH &out);
 void wide_compact(const WideBVH &b, std::vector<uint32_t> &rec_id, std::vector<uint32_t> &rec_rank);
 
 // A compact form checked against a geometry, ready to rebuild records from:
-// every node / record / cut index in range, the depth within WIDE_STACK, the
+// every node / record index in range, the depth within WIDE_STACK, the
 // ranks a permutation (rank_rec = its inverse), each record's triangle under a
 // reference leaf (leafq: that leaf's x/y/z words per triangle).
 struct WideCheck {

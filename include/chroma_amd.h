@@ -323,26 +323,23 @@ int chr_wide_bvh_free(chr_wide_result *r);
  * chroma/loader.py:131-160); here the structure the kernel walks is the wide
  * BVH, a function of the mesh and the reference BVH only.  Its compact form
  * keeps what the build decides -- the nodes, each triangle record's triangle
- * id and reference DFS rank, the sub-walk cut -- and drops what the upload
+ * id and reference DFS rank -- and drops what the upload
  * derives from the geometry descriptor (vertices, reference leaf words,
  * material codes), so a cached copy cannot go stale against the materials. */
 typedef struct chr_wide_bvh_desc {
     uint32_t nnodes;                /* 96-byte nodes (wide_bvh.h WideNode) */
     uint32_t nrec;                  /* triangle records = triangles reachable in the reference BVH */
-    uint32_t ncut;                  /* sub-walk items, 2 words each */
     uint32_t max_depth;             /* levels below the root */
     int32_t usable;                 /* 0: the wide walk cannot be used (the exact-order walk is) */
     uint32_t leaf_max;              /* builder setting it was built with */
     const void *h_nodes;            /* [nnodes*96 B] */
     const uint32_t *h_rec_id;       /* [nrec] triangle id of record i */
     const uint32_t *h_rec_rank;     /* [nrec] its reference DFS rank (a permutation of [0, nrec)) */
-    const uint32_t *h_cut;          /* [ncut*2] (node, child mask) */
 } chr_wide_bvh_desc;
 /* sizes and settings of a built result (pointers left NULL) */
 int chr_wide_bvh_describe(const chr_wide_result *r, chr_wide_bvh_desc *out);
 /* copy the compact form into caller arrays sized by chr_wide_bvh_describe */
-int chr_wide_bvh_export(const chr_wide_result *r, void *h_nodes, uint32_t *h_rec_id, uint32_t *h_rec_rank,
-                        uint32_t *h_cut);
+int chr_wide_bvh_export(const chr_wide_result *r, void *h_nodes, uint32_t *h_rec_id, uint32_t *h_rec_rank);
 /* the builder's settings as a short string ("w<format>-l<leaf max>"):
  * part of a cache key -- a compact form is reused only under the same settings */
 int chr_wide_bvh_key(char *out, uint32_t n);

@@ -79,7 +79,7 @@ def test_corrupt_cache_refused_before_upload(cuda, tmp_path, small_detector):
     from chroma.gpu.packing import PackedGeometry
     packed = PackedGeometry(small_detector)
     w = wide_bvh.build(packed)
-    bad = wide_bvh.WideBVH(w.nodes, np.array(w.rec_id), np.array(w.rec_rank), w.cut, w.max_depth, w.usable,
+    bad = wide_bvh.WideBVH(w.nodes, np.array(w.rec_id), np.array(w.rec_rank), w.max_depth, w.usable,
                            w.leaf_max, w.key)
     bad.rec_id[3] = len(packed.triangles) + 5
     g = copy.copy(small_detector)

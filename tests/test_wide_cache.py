@@ -29,7 +29,7 @@ def test_compact_rebuilds_records(small_packed):
     n = len(w.rec_id)
     part = w.records(small_packed, first=n // 3, n=n // 4)
     assert np.array_equal(part, rec[n // 3:n // 3 + n // 4])
-    assert w.leaf_max == 3 and w.key == 'w1-l3'
+    assert w.leaf_max == 3 and w.key == 'w2-l3'
 
 
 def test_compact_physics_scene():
@@ -43,15 +43,14 @@ def test_compact_physics_scene():
 
 def _corrupt(w, **changes):
     from chroma.gpu.wide_bvh import WideBVH
-    arrs = {k: np.array(getattr(w, k), copy=True) for k in ('nodes', 'rec_id', 'rec_rank', 'cut')}
+    arrs = {k: np.array(getattr(w, k), copy=True) for k in ('nodes', 'rec_id', 'rec_rank')}
     for k, f in changes.items():
         f(arrs[k])
-    return WideBVH(arrs['nodes'], arrs['rec_id'], arrs['rec_rank'], arrs['cut'], w.max_depth, w.usable,
-                   w.leaf_max, w.key)
+    return WideBVH(arrs['nodes'], arrs['rec_id'], arrs['rec_rank'], w.max_depth, w.usable, w.leaf_max, w.key)
 
 
 @pytest.mark.parametrize('what', ['rank_dup', 'rank_range', 'id_range', 'inner_child', 'leaf_range', 'kind',
-                                  'backward_child', 'cut'])
+                                  'backward_child'])
 def test_corrupt_compact_form_refused(small_packed, what):
     from chroma.gpu import _native, wide_bvh
     w = wide_bvh.build(small_packed)
@@ -73,7 +72,6 @@ def test_corrupt_compact_form_refused(small_packed, what):
             (len(w.nodes) - 1, slice(68, 72)), np.frombuffer(np.uint32(len(w.rec_id)).tobytes(), np.uint8))),
         'kind': dict(nodes=lambda a: node_field(a, 72, 9)),
         'backward_child': dict(nodes=lambda a: child_base(a, 0)),
-        'cut': dict(cut=lambda a: a.__setitem__((0, 0), len(w.nodes))),
     }[what]
     c = _corrupt(w, **bad)
     with pytest.raises(_native.NativeError, match='wide BVH'):
@@ -97,13 +95,13 @@ def test_cache_round_trip(tmp_path, small_detector):
     w1, src1 = wide_bvh.obtain(geo.bvh, packed)
     assert src1 == 'built'
     d = wide_bvh.directory(str(tmp_path), md5, 'default', wide_bvh.builder_key())
-    assert sorted(os.listdir(d)) == ['cut.npy', 'meta.json', 'nodes.npy', 'rec_id.npy', 'rec_rank.npy']
+    assert sorted(os.listdir(d)) == ['meta.json', 'nodes.npy', 'rec_id.npy', 'rec_rank.npy']
     assert cache.list_bvh(md5) == ['default']          # the .wide directory is not a BVH
     assert wide_bvh.obtain(geo.bvh, packed)[1] == 'memory'
     bvh2 = cache.load_bvh(md5)
     w2, src2 = wide_bvh.obtain(bvh2, packed)
     assert src2 == 'cache'
-    for k in ('nodes', 'rec_id', 'rec_rank', 'cut'):
+    for k in ('nodes', 'rec_id', 'rec_rank'):
         assert np.array_equal(np.asarray(getattr(w1, k)), np.asarray(getattr(w2, k)))
     assert np.array_equal(w2.records(packed), wide_bvh.build(packed).records(packed))
     # another reference BVH under the same name: the fingerprint no longer matches
