@@ -3715,14 +3715,6 @@ static bool trace_steps();
 // "1" every slot's events as well (kernel_ms, tail_ms, the prefix split);
 // "0" only the events the streams and the host synchronise on.  Times not
 // recorded read 0 in chr_propagate_stats.
-// CHR_EARLY_BIN_SLOT=k (chr_propagate_batches): the next batch's binning part
-// is queued on the prefix stream once this batch has queued its slot k (0: with
-// the next batch's walk, at this batch's end).
-static int early_bin_slot() {
-    const char *e = getenv("CHR_EARLY_BIN_SLOT");
-    return e ? atoi(e) : 0;
-}
-
 static int slot_timing() {
     const char *e = getenv("CHR_SLOT_TIMING");
     if (!e || e[0] == 't') return 1;
@@ -3751,11 +3743,9 @@ struct SlotCtl {
     hipEvent_t evt_tail0 = nullptr, evt_tail1 = nullptr;   // around the tail kernel, on tail_stream
     hipEvent_t rng_ready = nullptr;   // the previous batch's tail done: the first RNG use waits for it
     // chr_propagate_batches runs a batch's first slot in two parts: PHASE_PREFIX
-    // (head, ray records, binning, the BVH walk: no random numbers) on the prefix
-    // stream, ending with prefix_done -- or that prefix itself in two, PHASE_BIN
-    // (head, ray records, binning) queued early and PHASE_TRACE (the walk) --;
-    // PHASE_REST (shade pass on) on the batch stream after prefix_done, starting
-    // with ev_rest0
+    // (head, flat-walk classification, binning, the BVH walk: no random numbers)
+    // on the prefix stream, ending with prefix_done; PHASE_REST (shade pass on)
+    // on the batch stream after prefix_done, starting with ev_rest0
     int phase = 0;
     int ctx = 0;                      // buffer context (walk-stack column)
     uint32_t *host_ring = nullptr;    // pinned (mode, length) words the head kernel writes (nullptr: none)
@@ -3766,7 +3756,7 @@ struct SlotCtl {
     HeadNext next_head{nullptr, nullptr, nullptr, nullptr, nullptr, 0u, 0u, 0, 0};
     hipEvent_t prefix_done = nullptr, ev_rest0 = nullptr;
 };
-constexpr int PHASE_ALL = 0, PHASE_PREFIX = 1, PHASE_REST = 2, PHASE_BIN = 3, PHASE_TRACE = 4;
+constexpr int PHASE_ALL = 0, PHASE_PREFIX = 1, PHASE_REST = 2;
 
 // The wave-adaptive tail kernel as one resident grid whose photon groups take
 // queue positions from a counter (PropagateArgs::work; the slot's ray counter,
@@ -3827,10 +3817,9 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
     uint32_t *next = split ? (uint32_t *)(hits + (sc ? sc->n_layout : n)) : nullptr;
     const int phase = sc ? sc->phase : PHASE_ALL;
     const bool pre = phase != PHASE_REST, rest = phase == PHASE_ALL || phase == PHASE_REST;
-    const bool do_bin = pre && phase != PHASE_TRACE, do_trace = pre && phase != PHASE_BIN;
-    if (phase != PHASE_ALL && (!split || (phase != PHASE_BIN && !sc->prefix_done)))
+    if (phase != PHASE_ALL && (!split || !sc->prefix_done))
         return chr::fail(CHR_ERR_INVALID, "launch_step: a split slot needs the split path and its prefix event");
-    if (ev0 && do_bin) CHR_HIP_CHECK(hipEventRecord(ev0, stream));
+    if (ev0 && pre) CHR_HIP_CHECK(hipEventRecord(ev0, stream));
     if (!pre) {
         CHR_HIP_CHECK(hipStreamWaitEvent(stream, sc->prefix_done, 0));
         if (sc->ev_rest0) CHR_HIP_CHECK(hipEventRecord(sc->ev_rest0, stream));
@@ -3842,7 +3831,7 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
         hn.ray_counter = next;
     }
     const HeadNext *hnp = hn.mode ? &hn : nullptr;
-    if (sc && do_bin && !(sc->fold_head && !first_step)) {
+    if (sc && pre && !(sc->fold_head && !first_step)) {
         if (!next) return chr::fail(CHR_ERR_INVALID, "launch_step: device-driven steps need the split path");
         hipLaunchKernelGGL(step_head_kernel, dim3(1), dim3(64), 0, stream, in_queue - 1, out_queue, sc->mode, sc->nk,
                            sc->done, next, sc->tail_below, sc->remaining, use_weights, sc->n_layout, sc->host_ring);
@@ -3855,12 +3844,12 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
         // (device-driven slots bin only the first step, whose length the host knows)
         const bool binned = (sv.binned == 1 || (sv.binned == 2 && first_one_step && n >= kBinFirstMin)) &&
                             (!sc || first_one_step);
-        const bool bin_now = binned && do_bin;
+        const bool bin_now = binned && pre;
         uint32_t *keys = next + 16, *order = keys + n;
         // ray records: the first step's from its classification, later steps' from
         // the previous step's scatter (enrol_next)
         const bool use_rays = fc->rays && (first_one_step || fc->enrol_next);
-        if (first_one_step && do_bin)   // the initial queue's ray records and keys (later steps: the previous scatter)
+        if (first_one_step && pre)   // the initial queue's ray records and keys (later steps: the previous scatter)
             hipLaunchKernelGGL(classify_kernel, dim3(grid_for(n)), dim3(BLOCK), 0, stream, ph->d_pos, ph->d_dir,
                                ph->d_flags, ph->d_last_hit_triangles, in_queue, n, bin_now ? keys : nullptr,
                                bin_now ? order : nullptr, use_rays ? fc->rays : nullptr);
@@ -3873,7 +3862,7 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
         ta.dev_n = dev_n;
         ta.mode = mode;
         if (fc->enrol_next) fe = RayEnrol{ph->d_pos, ph->d_dir, fc->rays, ph->d_last_hit_triangles};
-        if (trace_steps() && do_trace) {   // debugging: per-walk cost histogram (counting variants), printed per step
+        if (trace_steps() && pre) {   // debugging: per-walk cost histogram (counting variants), printed per step
             ta.walk_hist = next + 16 + 2 * (size_t)(sc ? sc->n_layout : n);
             CHR_HIP_CHECK(hipMemsetAsync(ta.walk_hist, 0, 34 * 4, stream));
         }
@@ -3894,11 +3883,7 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
             ta.order = vals_out;
             if (use_rays) ta.rays = fc->rays_walk;
         }
-        if (phase == PHASE_BIN) {
-            CHR_HIP_CHECK(hipGetLastError());
-            return CHR_OK;
-        }
-        if (do_trace) {
+        if (pre) {
             const int cus = device_cus();
             if (cus <= 0) return chr::fail(CHR_ERR_HIP, "launch_step: no compute units");
             const int tb = sv.trace_block;
@@ -4134,7 +4119,6 @@ static int grow_events(std::vector<hipEvent_t> &v, size_t n) {
 // How device_slots runs a propagate besides its buffers.
 struct SlotRun {
     std::vector<hipEvent_t> *events = nullptr;   // SLOT_EVENTS per slot (grown here)
-    std::function<int(int)> on_slot;   // called after slot k is queued (chr_propagate_batches: early binning)
     hipStream_t tstream = nullptr;     // tail kernels go there (chr_propagate_batches; nullptr: on the stream)
     hipEvent_t rng_ready = nullptr;    // the first RNG use waits for it
     hipEvent_t prefix_done = nullptr;  // slot 0's prefix was queued by queue_prefix and ends with this event
@@ -4194,7 +4178,6 @@ static int device_slots(const chr_geometry *g, const chr_photons *ph, uint32_t n
                          b.hits, b.sort_space, k == 0, ev[2], timing ? ev[3] : nullptr, &split, &b.fc, &sc);
         if (rc) return rc;
         if (timing == 2) CHR_HIP_CHECK(hipEventRecord(ev[4], stream));
-        if (run.on_slot) CHR_TRY(run.on_slot(k));
         cur ^= 1;
         scatter_first = 0;
         if (k >= 1) {   // slot k - 1's head has run (its mode is known): is there a slot k + 1?
@@ -4564,15 +4547,15 @@ static bool photons_alias(const chr_photons *a, uint32_t na, const chr_photons *
 static int queue_prefix(const chr_geometry *g, const chr_photons *ph, uint32_t nphotons, uint32_t true_nphotons,
                         uint32_t ncopies, uint32_t *rng, uint32_t nslots, int32_t ntpb, int32_t max_steps,
                         int32_t use_weights, int32_t scatter_first, PropBufs &b, int ctx,
-                        std::vector<hipEvent_t> &events, hipEvent_t prefix_done, hipStream_t ps, int parts = 3) {
+                        std::vector<hipEvent_t> &events, hipEvent_t prefix_done, hipStream_t ps) {
     uint32_t *ctl = nullptr;
     CHR_TRY(slot_ctl_get(2 * (size_t)max_steps + 8, &ctl, ctx));
     uint32_t *done = ctl + 2 * (size_t)max_steps;
-    if (parts & 1) CHR_TRY(prop_start(b, nphotons, true_nphotons, ncopies, ps, done));
+    CHR_TRY(prop_start(b, nphotons, true_nphotons, ncopies, ps, done));
     b.fc.enrol_next = true;
     CHR_TRY(grow_events(events, SLOT_EVENTS));
     SlotCtl sc{ctl, ctl + 1, done, nphotons, max_steps, (uint32_t)ntpb * 16 * 8};
-    sc.phase = parts == 1 ? PHASE_BIN : (parts == 2 ? PHASE_TRACE : PHASE_PREFIX);
+    sc.phase = PHASE_PREFIX;
     sc.ctx = ctx;
     sc.prefix_done = prefix_done;
     sc.host_ring = b.pinned + 64;   // ring entry 0 (device_slots' slot 0): this head is slot 0's
@@ -4645,29 +4628,22 @@ static int propagate_batches(const chr_geometry *g, const chr_photons *phs, cons
     CHR_HIP_CHECK(hipEventRecord((*entry_ev)[0], stream));
     CHR_HIP_CHECK(hipStreamWaitEvent(ps, (*entry_ev)[0], 0));
     // batch j's prefix is queued when batch j starts (after batch j - 1's slots, so
-    // it runs beside that batch's tail); its binning part (queues, head, ray records,
-    // direction sort) earlier, once batch j - 1 has queued its slot early_slot()
-    // (the later, under-occupied launches), unless batch j shares photon arrays with
-    // batch j - 1.  parts: 1 binning, 2 walk, 3 both (queue_prefix)
-    auto prefix = [&](size_t j, int parts) -> int {
+    // it runs beside that batch's tail)
+    auto prefix = [&](size_t j) -> int {
         const uint32_t i = idx[j];
         const int c = (int)(j % NCTX);
-        if (parts & 1) {
-            if (j >= (size_t)NCTX) CHR_HIP_CHECK(hipStreamWaitEvent(ps, bh[j - NCTX].done, 0));   // the context is free
-            for (size_t e = j >= (size_t)NCTX ? j - NCTX + 1 : 0; e < j; ++e)   // shared photon arrays: after that batch
-                if (photons_alias(phs + i, nphotons[i], phs + idx[e], nphotons[idx[e]]))
-                    CHR_HIP_CHECK(hipStreamWaitEvent(ps, bh[e].done, 0));
-            CHR_TRY(prop_bufs(nphotons[i], ntpb, max_blocks, c, true, bufs[c]));
-            bufs[c].pinned = bh[j].pinned;
-        }
+        if (j >= (size_t)NCTX) CHR_HIP_CHECK(hipStreamWaitEvent(ps, bh[j - NCTX].done, 0));   // the context is free
+        for (size_t e = j >= (size_t)NCTX ? j - NCTX + 1 : 0; e < j; ++e)   // shared photon arrays: after that batch
+            if (photons_alias(phs + i, nphotons[i], phs + idx[e], nphotons[idx[e]]))
+                CHR_HIP_CHECK(hipStreamWaitEvent(ps, bh[e].done, 0));
+        CHR_TRY(prop_bufs(nphotons[i], ntpb, max_blocks, c, true, bufs[c]));
+        bufs[c].pinned = bh[j].pinned;
         return queue_prefix(g, phs + i, nphotons[i], true_nphotons[i], ncopies[i], d_rng_states, rng_nslots, ntpb,
-                            max_steps, use_weights, scatter_first, bufs[c], c, bh[j].ev, bh[j].prefix_done, ps, parts);
+                            max_steps, use_weights, scatter_first, bufs[c], c, bh[j].ev, bh[j].prefix_done, ps);
     };
-    const int early = early_bin_slot();
-    std::vector<char> binned(nb, 0);
     std::vector<int> slots(nb, 0);
     for (size_t j = 0; j < nb; ++j) {
-        CHR_TRY(prefix(j, binned[j] ? 2 : 3));
+        CHR_TRY(prefix(j));
         const uint32_t i = idx[j];
         const int c = (int)(j % NCTX);
         PropBufs &b = bufs[c];
@@ -4677,15 +4653,6 @@ static int propagate_batches(const chr_geometry *g, const chr_photons *phs, cons
         run.rng_ready = j > 0 ? bh[j - 1].done : nullptr;   // the previous batch's tail advances the RNG slots
         run.prefix_done = bh[j].prefix_done;
         run.ctx = c;
-        if (early > 0 && j + 1 < nb &&
-            !photons_alias(phs + idx[j + 1], nphotons[idx[j + 1]], phs + i, nphotons[i]))
-            run.on_slot = [&, j](int k) -> int {
-                if (k == early && !binned[j + 1]) {
-                    CHR_TRY(prefix(j + 1, 1));
-                    binned[j + 1] = 1;
-                }
-                return CHR_OK;
-            };
         uint32_t *ctl = nullptr;
         CHR_TRY(device_slots(g, phs + i, nphotons[i], d_rng_states, rng_nslots, ntpb, max_steps, use_weights,
                              scatter_first, b, run, stream, &ctl, &slots[j]));
