@@ -3770,18 +3770,11 @@ static bool tail_work_queue(const StepVariant &sv, const SlotCtl *sc, int32_t us
     return sv.tail_group == 8 && sc && !use_weights && sc->tail_below <= cap;
 }
 // blocks of a tail launch: every slot's group, or (work queue) the resident grid
-// CHR_TAIL_GRID_DIV=k: a tail on the tail stream (chr_propagate_batches) runs on
-// 1/k of the resident grid, leaving CUs to the next batch's prefix (A/B)
-static unsigned tail_grid_div() {
-    const char *e = getenv("CHR_TAIL_GRID_DIV");
-    const int v = e ? atoi(e) : 1;
-    return v > 1 ? (unsigned)v : 1u;
-}
-static unsigned tail_grid(const StepVariant &sv, uint32_t threads, bool work_queue, unsigned div = 1) {
+static unsigned tail_grid(const StepVariant &sv, uint32_t threads, bool work_queue) {
     const unsigned full = grid_for((uint64_t)threads * sv.tail_group);
     if (!work_queue) return full;
     const int cus = device_cus();
-    const unsigned resident = (unsigned)std::max(1, cus) * (unsigned)kTailWaves * 4u * 64u / BLOCK / div;
+    const unsigned resident = (unsigned)std::max(1, cus) * (unsigned)kTailWaves * 4u * 64u / BLOCK;
     return std::max(1u, std::min(full, resident));
 }
 
@@ -3942,7 +3935,7 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
         at.max_steps = sc->remaining;
         at.want = STEP_TAIL;
         at.work = tail_work_queue(sv, sc, use_weights, cap) ? next : nullptr;
-        hipLaunchKernelGGL(sv.tail, dim3(tail_grid(sv, threads, at.work != nullptr, tail_grid_div())), dim3(BLOCK), 0, ts,
+        hipLaunchKernelGGL(sv.tail, dim3(tail_grid(sv, threads, at.work != nullptr)), dim3(BLOCK), 0, ts,
                            (const DevGeom *)g->d_dev, at, cap);
         if (sc->evt_tail1) CHR_HIP_CHECK(hipEventRecord(sc->evt_tail1, ts));
         launch_mask_scan(masks, nwords, offsets, bsums, out_queue, counters + 1, nullptr, stream, dev_n, mode, STEP_TAIL,
