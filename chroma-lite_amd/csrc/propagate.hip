@@ -1413,7 +1413,6 @@ struct PropagateArgs {
     uint32_t nslots;
     const uint32_t *input_queue;
     int32_t first, nthreads, max_steps, use_weights, scatter_first;
-    uint32_t slot0;                    // shade_kernel: first RNG slot of this launch's grid (a split launch)
     unsigned long long *alive_masks;   // one word per 64 slots
     uint32_t *counters;                // [0]: stack overflows
     const uint32_t *order;             // coherence order: work-item t runs slot order[t] (nullptr: t)
@@ -1702,7 +1701,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void shade_kernel(const DevGeom *__res
     if (a.mode && *a.mode != a.want) return;
     __shared__ uint4 phys_lds[SHADE_PHYS_WORDS / 4];
     const DevGeom g = phys_cache(*gdev, phys_lds, SHADE_PHYS_WORDS);
-    const uint32_t slot = a.slot0 + blockIdx.x * BLOCK + threadIdx.x;
+    const uint32_t slot = blockIdx.x * BLOCK + threadIdx.x;
     const uint32_t n = a.dev_n ? *a.dev_n - 1u : (uint32_t)a.nthreads;
     if (slot >= cap || (slot & ~63u) >= n) return;   // whole waves (cap % 64 == 0)
     chr_xorwow rng;
@@ -3645,7 +3644,6 @@ static int launch_chunk(const chr_geometry *g, const chr_photons *ph, uint32_t *
     a.rng = rng; a.nslots = nslots; a.input_queue = in_queue; a.first = first; a.nthreads = nthreads;
     a.max_steps = max_steps; a.use_weights = use_weights; a.scatter_first = scatter_first;
     a.alive_masks = masks; a.counters = counters;
-    a.slot0 = 0;
     a.order = nullptr;
     a.hits = nullptr;
     a.diag = nullptr;
@@ -3706,13 +3704,6 @@ static int flat_get(uint32_t n, FlatCtx &fc, int ctx = 0) {
     fc.ctl = (uint32_t *)x.ptr;
     fc.enrol_next = false;
     return CHR_OK;
-}
-
-// CHR_SHADE_SPLIT=0: a batch's first shade pass waits for the previous batch's
-// tail as a whole (A/B; default 1: only its slots below the tail bound wait)
-static bool shade_split_enabled() {
-    const char *e = getenv("CHR_SHADE_SPLIT");
-    return !(e && e[0] == '0');
 }
 
 static bool trace_steps();
@@ -3806,7 +3797,6 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
     a.rng = rng; a.nslots = nslots; a.input_queue = in_queue; a.first = 0; a.nthreads = (int32_t)n;
     a.max_steps = max_steps; a.use_weights = use_weights; a.scatter_first = scatter_first;
     a.alive_masks = masks; a.counters = counters;
-    a.slot0 = 0;
     a.order = nullptr;
     a.hits = nullptr;
     a.diag = fc ? fc->ctl + 4 : nullptr;
@@ -3912,25 +3902,8 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
         }
         a.hits = hits;
         a.max_steps = 1;
-        unsigned sblocks = grid_for(threads), sfirst = 0;
-        if (sc && sc->rng_ready) {
-            // The previous batch's tail (on the tail stream) uses RNG slots below its queue
-            // length only -- < nthreads_per_block * 128 unless use_weights -- so the slots
-            // above that bound are shaded now, beside it, and only the rest waits for it
-            // (chr_propagate_batches; same states, same order per slot)
-            const uint64_t bound = use_weights ? (uint64_t)cap : std::min<uint64_t>(cap, sc->tail_below);
-            sfirst = (unsigned)std::min<uint64_t>(sblocks, (bound + BLOCK - 1) / BLOCK);
-            if (shade_split_enabled() && sfirst < sblocks) {
-                PropagateArgs ah = a;
-                ah.slot0 = sfirst * BLOCK;
-                hipLaunchKernelGGL(sv.shade, dim3(sblocks - sfirst), dim3(BLOCK), 0, stream, (const DevGeom *)g->d_dev,
-                                   ah, cap);
-                sblocks = sfirst;
-            }
-            CHR_HIP_CHECK(hipStreamWaitEvent(stream, sc->rng_ready, 0));
-        }
-        if (sblocks)
-            hipLaunchKernelGGL(sv.shade, dim3(sblocks), dim3(BLOCK), 0, stream, (const DevGeom *)g->d_dev, a, cap);
+        if (sc && sc->rng_ready) CHR_HIP_CHECK(hipStreamWaitEvent(stream, sc->rng_ready, 0));
+        hipLaunchKernelGGL(sv.shade, dim3(grid_for(threads)), dim3(BLOCK), 0, stream, (const DevGeom *)g->d_dev, a, cap);
     }
     if (split_out) *split_out = split;
     if (tail && sc && sc->tail_stream) {   // the tail on its own stream (chr_propagate_batches)
