@@ -55,8 +55,13 @@ DEVICE_REGION_NAMES = {
     19: 'lone_expand',
     20: 'lone_tris',
     21: 'lone_walk',
+    22: 'long_walk',
+    23: 'long_fill',
+    24: 'long_to_boundary',
+    25: 'long_at_boundary',
+    26: 'long_other',
 }
-NREGIONS = 22        # CHR_PROF_NREGIONS
+NREGIONS = 27        # CHR_PROF_NREGIONS
 COUNTERS = 64        # CHR_PROF_COUNT (profile.h:16)
 
 

@@ -2415,6 +2415,45 @@ __device__ __forceinline__ int walk_lone(const DevGeom &g, V3 o, V3 d, uint32_t 
     return best_id;
 }
 
+// Where a long-lived photon's tail step goes (profile build: CHR_PROF_LONG_*):
+// wave cycles per phase of the steps beyond the 64th of each photon, counted by its
+// group's first lane.  mark(i) closes phase i at the current clock.
+enum { LP_WALK, LP_FILL, LP_TO_BOUNDARY, LP_AT_BOUNDARY, LP_OTHER, LP_N };
+template <bool ON>
+struct LongProf {
+    __device__ __forceinline__ void step(bool) {}
+    __device__ __forceinline__ void mark(int) {}
+    __device__ __forceinline__ void flush() {}
+};
+#ifdef CHR_DEVICE_PROFILE
+template <>
+struct LongProf<true> {
+    unsigned long long cyc[LP_N] = {0ull, 0ull, 0ull, 0ull, 0ull}, steps = 0ull, t = 0ull;
+    bool on = false;
+    // a step begins (on: this lane's photon is long and walks this step); the time
+    // since the last phase closed is OTHER (the loop, the ballots, the walk's set-up)
+    __device__ __forceinline__ void step(bool long_walk) {
+        const unsigned long long now = __builtin_amdgcn_s_memtime();
+        if (on) cyc[LP_OTHER] += now - t;
+        on = long_walk;
+        if (on) steps++;
+        t = now;
+    }
+    __device__ __forceinline__ void mark(int i) {
+        const unsigned long long now = __builtin_amdgcn_s_memtime();
+        if (on) cyc[i] += now - t;
+        t = now;
+    }
+    __device__ __forceinline__ void flush() {
+        prof_add(CHR_PROF_LONG_WALK, steps, cyc[LP_WALK]);
+        prof_add(CHR_PROF_LONG_FILL, 0ull, cyc[LP_FILL]);
+        prof_add(CHR_PROF_LONG_TO_BOUNDARY, 0ull, cyc[LP_TO_BOUNDARY]);
+        prof_add(CHR_PROF_LONG_AT_BOUNDARY, 0ull, cyc[LP_AT_BOUNDARY]);
+        prof_add(CHR_PROF_LONG_OTHER, 0ull, cyc[LP_OTHER]);
+    }
+};
+#endif
+
 template <int MINW>
 __global__ __launch_bounds__(BLOCK, MINW) void propagate_tail_kernel(const DevGeom *__restrict__ gdev, PropagateArgs a,
                                                                      uint32_t cap) {
@@ -2457,6 +2496,11 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_tail_kernel(const DevGe
     enum { P_WALK, P_PHYS, P_OTHER };
     Prof<3> pf;
     pf.start(P_OTHER);
+#ifdef CHR_DEVICE_PROFILE
+    LongProf<true> lpf;
+#else
+    LongProf<false> lpf;
+#endif
     // run_photon's write-back (propagate.cu:343-353) and the alive bit
     auto finish = [&]() {
         store3(a.pos, pid, p.pos);
@@ -2530,6 +2574,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_tail_kernel(const DevGe
         }
         // the walk, spread over the wave
         const unsigned long long wm = __ballot(walk && sub == 0);   // bit 8g: group g walks
+        lpf.step(walk && sub == 0 && steps > 64);
         int tri = -1;
         float dist = -1.0f;
         const int w = __popcll(wm);
@@ -2585,11 +2630,14 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_tail_kernel(const DevGe
                 const V3 inv = v3(1.0f / p.dir.x, 1.0f / p.dir.y, 1.0f / p.dir.z);
                 if (!(chr_isfinite(inv.x) && chr_isfinite(inv.y) && chr_isfinite(inv.z))) flat++;
             }
+            lpf.mark(LP_WALK);
             s.distance = dist;
             finish_fill<true>(g, s, p, tri);
+            lpf.mark(LP_FILL);
             bool stop = p.last_hit == -1;
             if (!stop) {
                 int command = propagate_to_boundary(g, p, s, rng, a.use_weights, scatter_first);
+                lpf.mark(LP_TO_BOUNDARY);
                 scatter_first = 0;
                 if (command == BREAK) {
                     stop = true;
@@ -2600,6 +2648,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_tail_kernel(const DevGe
                     }
                     if (command == PASS) propagate_at_boundary(p, s, rng);
                 }
+                lpf.mark(LP_AT_BOUNDARY);
             }
             pf.tick(P_OTHER);
             if (stop) finish();
@@ -2614,6 +2663,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_tail_kernel(const DevGe
     prof_add(CHR_PROF_TAIL_PHYSICS, pf.calls[P_PHYS], pf.cyc[P_PHYS]);
     prof_add(CHR_PROF_TAIL_OTHER, 0ull, pf.cyc[P_OTHER]);
     prof_add(CHR_PROF_TAIL_KERNEL, 1ull, pf.total());
+    lpf.flush();
 #endif
 }
 

@@ -546,7 +546,13 @@ enum {
     CHR_PROF_LONE_EXPAND = 19,        /* children slab-tested, near child, pushes, triangle list */
     CHR_PROF_LONE_TRIS = 20,          /* triangles tested, nearest hit reduced */
     CHR_PROF_LONE_WALK = 21,          /* all of the above (calls = iterations) */
-    CHR_PROF_NREGIONS = 22,
+    /* a long-lived photon's tail steps (its steps beyond the 64th), wave cycles per phase: */
+    CHR_PROF_LONG_WALK = 22,          /* the walk (calls = such steps) */
+    CHR_PROF_LONG_FILL = 23,          /* finish_fill: the hit's record, normal, material, surface */
+    CHR_PROF_LONG_TO_BOUNDARY = 24,   /* propagate_to_boundary */
+    CHR_PROF_LONG_AT_BOUNDARY = 25,   /* propagate_at_surface / _at_boundary */
+    CHR_PROF_LONG_OTHER = 26,         /* the rest of the step: the kernel's loop, ballots, the walk's set-up */
+    CHR_PROF_NREGIONS = 27,
     CHR_PROF_COUNT = 64               /* counter array length (profile.h:16) */
 };
 /* 1 when this library was built with the device profile, else 0 */

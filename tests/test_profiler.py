@@ -65,5 +65,5 @@ def test_profile_library_exports():
     assert lib.chr_device_profile_enabled() == 1
     assert lib.chr_version() == 1
     names = __import__('chroma.gpu.profiler', fromlist=['x']).DEVICE_REGION_NAMES
-    assert len(names) == 22 and names[0] == 'intersect_mesh' and names[3] == 'intersect_box'
-    assert names[21] == 'lone_walk'
+    assert len(names) == 27 and names[0] == 'intersect_mesh' and names[3] == 'intersect_box'
+    assert names[21] == 'lone_walk' and names[26] == 'long_other'

@@ -27,4 +27,12 @@ if lw.get('calls'):
     for k in ('lone_refill', 'lone_fetch', 'lone_expand', 'lone_tris'):
         print('%-12s %7.0f cycles/iteration (%.0f%%)' % (k, r[k]['cycles'] / it, 100.0 * r[k]['cycles'] / lw['cycles']))
     print('lone walk %.0f cycles/iteration = %.3f us at %d kHz' % (lw['cycles'] / it, lw['cycles'] / it / khz * 1e3, khz))
+lg = r.get('long_walk', {})
+if lg.get('calls'):
+    n = lg['calls']
+    tot = sum(r[k]['cycles'] for k in ('long_walk', 'long_fill', 'long_to_boundary', 'long_at_boundary', 'long_other'))
+    for k in ('long_walk', 'long_fill', 'long_to_boundary', 'long_at_boundary', 'long_other'):
+        print('%-17s %7.0f cycles/step = %6.3f us (%.0f%%)' % (k, r[k]['cycles'] / n, r[k]['cycles'] / n / khz * 1e3,
+                                                          100.0 * r[k]['cycles'] / tot))
+    print('long-lived photon step %.3f us over %d steps' % (tot / n / khz * 1e3, n))
 PY
