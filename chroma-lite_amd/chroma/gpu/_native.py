@@ -93,7 +93,7 @@ _SIGNATURES = {
     'chr_geometry_create': (c_i32, [ctypes.POINTER(GeometryDesc), ctypes.POINTER(c_vp)]),
     'chr_geometry_destroy': (c_i32, [c_vp]),
     'chr_geometry_device_bytes': (c_i32, [c_vp, ctypes.POINTER(c_u64)]),
-    'chr_walk_lone_timing': (c_i32, [c_vp, c_vp, c_u32, c_u32, c_u32, c_vp, c_vp]),
+    'chr_walk_lone_timing': (c_i32, [c_vp, c_vp, c_u32, c_u32, c_u32, c_i32, c_vp, c_vp]),
     'chr_geometry_phys_words': (c_i32, [c_vp, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32)]),
     'chr_init_rng': (c_i32, [c_vp, c_u32, c_u64, c_u64, c_vp]),
     'chr_rng_download': (c_i32, [c_vp, c_u32, c_vp, c_vp]),

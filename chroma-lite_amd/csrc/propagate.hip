@@ -2415,6 +2415,307 @@ __device__ __forceinline__ int walk_lone(const DevGeom &g, V3 o, V3 d, uint32_t 
     return best_id;
 }
 
+// ---------------------------------------------------------------- pair walk
+// The lone walk on two waves of a workgroup (two SIMDs): the WALKER runs the
+// node expansions, the stack and the refills, and lists each iteration's
+// hit-leaf triangles into a ring of two LDS buffers; the TESTER, another wave of
+// the workgroup with no photon of its own, tests the listed triangles and
+// publishes the running (distance, reference rank) minimum, which the walker
+// culls with.  walk_lone does both in one instruction stream (~2,300 shader
+// cycles per iteration, bound by its own issue, §11.7); split, each wave issues
+// about half of it per iteration.  The tester's best lags the walker by about
+// an iteration -- never below the final one, so culling stays conservative -- and
+// the result is the min over every listed triangle with the reference leaf-box
+// check, as in walk_lone / walk_segment.
+// The mailbox (PB_* words, LDS, one per workgroup) carries the ray and the
+// handshake: the walker posts (PS_REQ), a helper takes it (PS_TAKEN), lists
+// count up in PB_WSEQ, the tester's progress in PB_TREAD (lists read: the
+// walker may reuse that buffer) and PB_TSEQ (lists tested), the walker's end in
+// PB_WDONE, the tester's in PS_DONE.  Every wait is bounded (PAIR_SPIN_MAX
+// polls): a lost handshake ends the walk with PB_ABORT set and is counted with
+// the stack overflows, never hangs the wave.
+enum : int {
+    PB_STATE, PB_IDLE, PB_WORKERS, PB_WSEQ, PB_WDONE, PB_TREAD, PB_TSEQ, PB_BEST, PB_RANK, PB_ID,
+    PB_OX, PB_OY, PB_OZ, PB_DX, PB_DY, PB_DZ, PB_LAST, PB_CNT0, PB_CNT1, PB_LISTS, PB_ABORT, PB_WORDS = 24
+};
+enum : uint32_t { PS_IDLE = 0, PS_POSTING = 1, PS_REQ = 2, PS_TAKEN = 3, PS_DONE = 4, PS_EXIT = 5 };
+constexpr uint32_t PAIR_SPIN_MAX = 1u << 21;
+__device__ __forceinline__ uint32_t lds_ld(CHR_LDS uint32_t *p) {
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)*(volatile CHR_LDS uint32_t *)p);
+}
+__device__ __forceinline__ void lds_st(CHR_LDS uint32_t *p, uint32_t v) {   // lane 0 writes
+    if (__lane_id() == 0) *(volatile CHR_LDS uint32_t *)p = v;
+}
+__device__ __forceinline__ void lds_release() { __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup"); }
+__device__ __forceinline__ void lds_acquire() { __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup"); }
+// poll until pred() (wave-uniform), at most PAIR_SPIN_MAX times; false on timeout
+template <class P>
+__device__ __forceinline__ bool pair_wait(CHR_LDS uint32_t *box, P pred) {
+    for (uint32_t i = 0; i < PAIR_SPIN_MAX; ++i) {
+        if (pred()) return true;
+        if (lds_ld(box + PB_ABORT)) return false;
+        __builtin_amdgcn_s_sleep(1);
+    }
+    lds_st(box + PB_ABORT, 1u);
+    return false;
+}
+
+// The walker (whole wave, converged).  lists: this wave's 2 x TAIL_TRI words;
+// stk: cap entries of stack, the last 8 of them used as the refill's scratch.
+// The box must have been posted (ray, seed best, PB_LISTS) by this wave.
+template <class M>
+__device__ __forceinline__ int walk_pair_walker(const DevGeom &g, const TopNodes &top, V3 o, V3 d, M stk, int cap,
+                                                CHR_LDS uint32_t *lists, CHR_LDS uint32_t *box, uint32_t &overflow,
+                                                float &min_distance, uint32_t &iters) {
+    constexpr uint32_t INVALID = 0xFFFFFFFFu;
+    auto ufl = [](float x) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(x))); };
+    auto uu = [](uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); };
+    o = v3(ufl(o.x), ufl(o.y), ufl(o.z));
+    d = v3(ufl(d.x), ufl(d.y), ufl(d.z));
+    const int scap = cap - 8;                         // stack entries; [scap, cap): the refill's scratch
+    const uint32_t lane = __lane_id();
+    const uint32_t k = lane & 7u;
+    const uint32_t lead = lane & ~7u;
+    const unsigned long long below = (1ull << lane) - 1ull;
+    const V3 noid = v3(-o.x / d.x, -o.y / d.y, -o.z / d.z);
+    const V3 inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    const RaySlab r = make_slab(o, noid, inv);
+    uint32_t cur = lane < 8u ? 0u : INVALID;
+    float cur_t = 0.0f;
+    int sp = 0;
+    uint32_t nl = 0;                                  // lists published
+    bool ok = true;
+    iters = 0;
+    uint4 h, a1, a2, a3, a4, a5;
+    load_node(g, top, cur == INVALID ? 0u : cur, h, a1, a2, a3, a4, a5);
+    while (true) {
+        iters++;
+        const float best = __uint_as_float(lds_ld(box + PB_BEST));
+        bool inner = false, leafhit = false;
+        float tk = 0.0f;
+        uint32_t kind = 0, child = 0, first = 0;
+        if (cur != INVALID) {
+            const V3 org = v3(__uint_as_float(h.x), __uint_as_float(h.y), __uint_as_float(h.z));
+            const float sx = exp_scale(h.w), sy = exp_scale(h.w >> 8), sz = exp_scale(h.w >> 16);
+            kind = byte8(a4.z, a4.w, k);
+            auto q = [k](uint32_t lo4, uint32_t hi4) { return (float)byte8(lo4, hi4, k); };
+            const float tnx = __builtin_fmaf(__builtin_fmaf(q(r.negx ? a2.z : a1.x, r.negx ? a2.w : a1.y), sx, org.x), r.inx, r.onx);
+            const float tfx = __builtin_fmaf(__builtin_fmaf(q(r.negx ? a1.x : a2.z, r.negx ? a1.y : a2.w), sx, org.x), r.inx, r.ofx);
+            const float tny = __builtin_fmaf(__builtin_fmaf(q(r.negy ? a3.x : a1.z, r.negy ? a3.y : a1.w), sy, org.y), r.iny, r.ony);
+            const float tfy = __builtin_fmaf(__builtin_fmaf(q(r.negy ? a1.z : a3.x, r.negy ? a1.w : a3.y), sy, org.y), r.iny, r.ofy);
+            const float tnz = __builtin_fmaf(__builtin_fmaf(q(r.negz ? a3.z : a2.x, r.negz ? a3.w : a2.y), sz, org.z), r.inz, r.onz);
+            const float tfz = __builtin_fmaf(__builtin_fmaf(q(r.negz ? a2.x : a3.z, r.negz ? a2.y : a3.w), sz, org.z), r.inz, r.ofz);
+            const float tmin = __builtin_fmaxf(__builtin_fmaxf(__builtin_fmaxf(tnx, tny), tnz), 0.0f);
+            const float tmax = __builtin_fminf(__builtin_fminf(tfx, tfy), tfz);
+            const bool hit = (kind != 0u) & !(tmin > tmax) & !(tmin > best);
+            inner = hit & (kind == WIDE_INNER);
+            leafhit = hit & (kind != WIDE_INNER);
+            tk = tmin;
+            const uint32_t off = byte8(a5.x, a5.y, k);
+            child = a4.x + off;
+            first = a4.y + off;
+        }
+        // near child (walk_lone's 32-bit keys) and pushes
+        uint32_t key = inner ? ((__float_as_uint(tk) & ~7u) | k) : INVALID;
+        auto dmin = [](uint32_t v, auto ctrl) {
+            const uint32_t o2 = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, decltype(ctrl)::value, 0xF, 0xF, true);
+            return o2 < v ? o2 : v;
+        };
+        key = dmin(key, std::integral_constant<int, 0xB1>());
+        key = dmin(key, std::integral_constant<int, 0x4E>());
+        key = dmin(key, std::integral_constant<int, 0x141>());
+        uint32_t near = INVALID;
+        if (key != INVALID) near = a4.x + byte8(a5.x, a5.y, key & 7u);
+        const bool push = inner && (key & 7u) != k;
+        const unsigned long long pm = __ballot(push);
+        const int pos = sp + __popcll(pm & below);
+        if (push && pos < scap) {
+            stk[2 * pos] = child;
+            stk[2 * pos + 1] = __float_as_uint(tk);
+        }
+        const int npush = __popcll(pm);
+        if (sp + npush > scap) {
+            if (lane == 0) overflow += (uint32_t)(sp + npush - scap);
+            sp = scap;
+        } else {
+            sp += npush;
+        }
+        cur = near;
+        cur_t = __uint_as_float(key & ~7u);
+        // this expansion's hit-leaf triangles -> list nl (buffer nl & 1, free once the
+        // tester has read list nl - 2)
+        const uint32_t cnt = leafhit ? kind : 0u;
+        const unsigned long long b0 = __ballot(cnt & 1u), b1 = __ballot(cnt & 2u), b2 = __ballot(cnt & 4u);
+        const uint32_t Tn = uu(__popcll(b0) + 2u * __popcll(b1) + 4u * __popcll(b2));
+        if (Tn) {
+            const uint32_t pre = __popcll(b0 & below) + 2u * __popcll(b1 & below) + 4u * __popcll(b2 & below);
+            if (nl >= 2u && ok) ok = pair_wait(box, [&]() { return lds_ld(box + PB_TREAD) + 1u >= nl; });
+            const int nb = (int)(nl & 1u) * TAIL_TRI;
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                if ((uint32_t)i < cnt) lists[nb + (int)min(pre + (uint32_t)i, (uint32_t)(TAIL_TRI - 1))] = first + (uint32_t)i;
+            lds_st(box + PB_CNT0 + (nl & 1u), Tn);
+            lds_release();
+            lds_st(box + PB_WSEQ, nl + 1u);
+            nl++;
+        }
+        // cursors without a node take the topmost unculled stack entries (walk_lone's refill)
+        unsigned long long em = __ballot(k == 0u && cur == INVALID);
+        while (em != 0 && sp > 0) {
+            const int W = sp < 8 ? sp : 8;
+            uint32_t en = 0, et = 0;
+            bool okk = false;
+            if (lane < (uint32_t)W) {
+                en = stk[2 * (sp - 1 - (int)lane)];
+                et = stk[2 * (sp - 1 - (int)lane) + 1];
+                okk = !(__uint_as_float(et) > best);           // mesh.h:94-96
+            }
+            const unsigned long long okm = __ballot(okk);
+            const int need = __popcll(em), nv = __popcll(okm);
+            const int take = need < nv ? need : nv;
+            const int rho = __popcll(okm & below);
+            const unsigned long long stopm = __ballot(okk && rho == take);
+            const int consumed = stopm ? (__ffsll((long long)stopm) - 1) : W;
+            if (okk && rho < take) {
+                stk[2 * (scap + rho)] = en;
+                stk[2 * (scap + rho) + 1] = et;
+            }
+            __builtin_amdgcn_wave_barrier();
+            const bool empty = ((em >> lead) & 1ull) != 0;
+            const int rnk = __popcll(em & ((1ull << lead) - 1ull));
+            const unsigned long long taken = __ballot(k == 0u && empty && rnk < take);
+            if (empty && rnk < take) {
+                cur = stk[2 * (scap + rnk)];
+                cur_t = __uint_as_float(stk[2 * (scap + rnk) + 1]);
+            }
+            __builtin_amdgcn_wave_barrier();
+            sp = (int)uu((uint32_t)(sp - consumed));
+            em &= ~taken;
+        }
+        sp = (int)uu((uint32_t)sp);
+        if (cur != INVALID && cur_t > best) cur = INVALID;
+        if (__ballot(cur != INVALID) == 0 && sp == 0) break;
+        load_node(g, top, cur == INVALID ? 0u : cur, h, a1, a2, a3, a4, a5);
+    }
+    lds_release();
+    lds_st(box + PB_WDONE, nl);
+    if (ok) ok = pair_wait(box, [&]() { return lds_ld(box + PB_STATE) == PS_DONE; });
+    lds_acquire();
+    const float best = __uint_as_float(lds_ld(box + PB_BEST));
+    const int best_id = (int)lds_ld(box + PB_ID);
+    if (!ok && lane == 0) overflow += 1u << 20;   // a lost handshake: reported as stack overflows
+    min_distance = best_id == -1 ? -1.0f : best;
+    return best_id;
+}
+
+// The tester (whole wave, converged), after taking a posted box: tests every
+// list the walker publishes until the walker's end, then PS_DONE.  lbase: the
+// LDS word base PB_LISTS is relative to.
+__device__ __forceinline__ void walk_pair_tester(const DevGeom &g, CHR_LDS uint32_t *box, CHR_LDS uint32_t *lbase) {
+    const uint32_t lane = __lane_id();
+    const V3 o = v3(__uint_as_float(lds_ld(box + PB_OX)), __uint_as_float(lds_ld(box + PB_OY)),
+                    __uint_as_float(lds_ld(box + PB_OZ)));
+    const V3 d = v3(__uint_as_float(lds_ld(box + PB_DX)), __uint_as_float(lds_ld(box + PB_DY)),
+                    __uint_as_float(lds_ld(box + PB_DZ)));
+    const uint32_t last = lds_ld(box + PB_LAST);
+    CHR_LDS uint32_t *lists = lbase + lds_ld(box + PB_LISTS);
+    float best = __uint_as_float(lds_ld(box + PB_BEST));
+    uint32_t best_rank = lds_ld(box + PB_RANK);
+    int best_id = (int)lds_ld(box + PB_ID);
+    const V3 noid = v3(-o.x / d.x, -o.y / d.y, -o.z / d.z);
+    const V3 inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    for (uint32_t j = 0;; ++j) {
+        uint32_t ws = 0;
+        const bool ok = pair_wait(box, [&]() {
+            const uint32_t wd = lds_ld(box + PB_WDONE);
+            ws = lds_ld(box + PB_WSEQ);
+            return ws > j || wd == j;
+        });
+        if (!ok || ws <= j) break;   // the walker's end: every list tested
+        lds_acquire();
+        const uint32_t n = lds_ld(box + PB_CNT0 + (j & 1u));
+        const int nb = (int)(j & 1u) * TAIL_TRI;
+        const uint32_t trec = lane < n ? lists[nb + (int)lane] : 0u;
+        // the list is in registers: its buffer is free (before the loads, which a
+        // release would wait for)
+        if (n <= 64u) { lds_release(); lds_st(box + PB_TREAD, j + 1u); }
+        const float4 *rr = g.wtri + 4 * (size_t)trec;
+        const float4 r0 = gld(rr), r1 = gld(rr + 1), r2 = gld(rr + 2);
+        const uint2 w3 = gld_lo2(rr + 3);
+        float lbest = best;
+        uint32_t lrank = best_rank;
+        int lid = -1;
+        auto test = [&](const float4 &t0, const float4 &t1, const float4 &t2, uint2 w, const float4 *tr) {
+            const uint32_t id = __float_as_uint(t2.y);
+            float dist;
+            if (id == last || !intersect_record(o, d, t0, t1, t2, dist)) return;
+            const uint32_t rank = __float_as_uint(t2.z);
+            if (!(dist < lbest || (dist == lbest && rank < lrank))) return;
+            V3 lo, hi;
+            node_bounds(g, make_uint4(__float_as_uint(t2.w), w.x, w.y, 0u), lo, hi);
+            float bd;
+            if (!intersect_box(noid, inv, lo, hi, bd) || bd > lbest) return;   // mesh.h:94-96
+            lbest = dist;
+            lrank = rank;
+            lid = rec_of(g, tr);
+        };
+        if (lane < n) test(r0, r1, r2, w3, rr);
+        for (uint32_t i = lane + 64u; i < n; i += 64u) {
+            const float4 *tr = g.wtri + 4 * (size_t)lists[nb + (int)i];
+            test(gld(tr), gld(tr + 1), gld(tr + 2), gld_lo2(tr + 3), tr);
+        }
+        if (n > 64u) { lds_release(); lds_st(box + PB_TREAD, j + 1u); }
+        const unsigned long long hm = __ballot(lid != -1);
+        if (hm != 0) {
+            unsigned long long lkey = lid == -1 ? ~0ull : (((unsigned long long)__float_as_uint(lbest) << 32) | lrank);
+            for (int off = 1; off < 64; off <<= 1) {
+                const unsigned long long ok2 = __shfl_xor(lkey, off);
+                const int oid = __shfl_xor(lid, off);
+                if (ok2 < lkey) { lkey = ok2; lid = oid; }
+            }
+            best = __int_as_float(__builtin_amdgcn_readfirstlane((int)(uint32_t)(lkey >> 32)));
+            best_rank = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)lkey);
+            best_id = __builtin_amdgcn_readfirstlane(lid);
+            lds_st(box + PB_RANK, best_rank);
+            lds_st(box + PB_ID, (uint32_t)best_id);
+            lds_st(box + PB_BEST, __float_as_uint(best));
+        }
+        lds_release();
+        lds_st(box + PB_TSEQ, j + 1u);
+    }
+    lds_release();
+    lds_st(box + PB_STATE, PS_DONE);
+}
+
+// The walker's side of a pair walk: post the ray into the box (the caller has
+// claimed it: PS_POSTING), walk, release the box.
+template <class M>
+__device__ __forceinline__ int walk_pair(const DevGeom &g, const TopNodes &top, V3 o, V3 d, uint32_t last, M stk,
+                                         int cap, CHR_LDS uint32_t *lists, uint32_t lists_off, CHR_LDS uint32_t *box,
+                                         uint32_t &overflow, float &min_distance, uint32_t &iters) {
+    lds_st(box + PB_WSEQ, 0u);
+    lds_st(box + PB_WDONE, 0xFFFFFFFFu);
+    lds_st(box + PB_TREAD, 0u);
+    lds_st(box + PB_TSEQ, 0u);
+    lds_st(box + PB_BEST, __float_as_uint(__builtin_inff()));
+    lds_st(box + PB_RANK, 0xFFFFFFFFu);
+    lds_st(box + PB_ID, 0xFFFFFFFFu);
+    lds_st(box + PB_OX, __float_as_uint(o.x));
+    lds_st(box + PB_OY, __float_as_uint(o.y));
+    lds_st(box + PB_OZ, __float_as_uint(o.z));
+    lds_st(box + PB_DX, __float_as_uint(d.x));
+    lds_st(box + PB_DY, __float_as_uint(d.y));
+    lds_st(box + PB_DZ, __float_as_uint(d.z));
+    lds_st(box + PB_LAST, last);
+    lds_st(box + PB_LISTS, lists_off);
+    lds_release();
+    lds_st(box + PB_STATE, PS_REQ);
+    const int tri = walk_pair_walker(g, top, o, d, stk, cap, lists, box, overflow, min_distance, iters);
+    lds_release();
+    lds_st(box + PB_STATE, PS_IDLE);
+    return tri;
+}
+
 // Where a long-lived photon's tail step goes (profile build: CHR_PROF_LONG_*):
 // wave cycles per phase of the steps beyond the 64th of each photon, counted by its
 // group's first lane.  mark(i) closes phase i at the current clock.
@@ -4893,13 +5194,38 @@ extern "C" int chr_device_profile_fetch(uint64_t *h_calls, uint64_t *h_cycles, i
 }
 
 namespace chr {
-// chr_walk_lone_timing: walk_lone on one wave per workgroup, each ray reps times
-__global__ __launch_bounds__(64) void walk_lone_timing_kernel(const DevGeom *__restrict__ gdev, const float *rays,
-                                                              uint32_t n, uint32_t reps, uint32_t *out) {
+// chr_walk_lone_timing: walk_lone on one wave per workgroup (walker 0), or the
+// pair walk on two (walker 1: wave 0 walks, wave 1 tests), each ray reps times
+__global__ __launch_bounds__(128) void walk_lone_timing_kernel(const DevGeom *__restrict__ gdev, const float *rays,
+                                                               uint32_t n, uint32_t reps, uint32_t *out,
+                                                               int32_t walker) {
     __shared__ uint32_t stacks[8 * TAIL_STACK * 2];
     __shared__ uint32_t tris[2 * TAIL_TRI];
+    __shared__ uint32_t box_s[PB_WORDS];
+    CHR_LDS uint32_t *box = (CHR_LDS uint32_t *)box_s;
     const DevGeom &g = *gdev;
     uint32_t overflow = 0;
+    const TopNodes top{nullptr, 0u};
+    if (threadIdx.x == 0) {
+        box[PB_STATE] = PS_IDLE;
+        box[PB_ABORT] = 0u;
+    }
+    __syncthreads();
+    if (threadIdx.x >= 64) {   // the tester wave (walker 1), else idle
+        if (walker != 1) return;
+        while (true) {
+            uint32_t st = PS_IDLE;
+            for (uint32_t i = 0; i < PAIR_SPIN_MAX * 8u; ++i) {
+                st = lds_ld(box + PB_STATE);
+                if (st == PS_REQ || st == PS_EXIT) break;
+                __builtin_amdgcn_s_sleep(1);
+            }
+            if (st != PS_REQ) return;
+            lds_acquire();
+            lds_st(box + PB_STATE, PS_TAKEN);
+            walk_pair_tester(g, box, (CHR_LDS uint32_t *)tris);
+        }
+    }
     for (uint32_t r = blockIdx.x; r < n; r += gridDim.x) {
         const float *ry = rays + 7 * (size_t)r;
         const V3 o = v3(ry[0], ry[1], ry[2]), d = v3(ry[3], ry[4], ry[5]);
@@ -4908,8 +5234,11 @@ __global__ __launch_bounds__(64) void walk_lone_timing_kernel(const DevGeom *__r
             float sd;
             uint32_t it = 0;
             const unsigned long long t0 = __builtin_amdgcn_s_memrealtime(), c0 = __builtin_amdgcn_s_memtime();
-            const int tri = walk_lone(g, o, d, last, LdsFlat{(CHR_LDS uint32_t *)stacks}, TAIL_STACK * 8,
-                                      LdsFlat{(CHR_LDS uint32_t *)tris}, overflow, sd, it);
+            const int tri = walker == 1
+                                ? walk_pair(g, top, o, d, last, LdsFlat{(CHR_LDS uint32_t *)stacks}, TAIL_STACK * 8,
+                                            (CHR_LDS uint32_t *)tris, 0u, box, overflow, sd, it)
+                                : walk_lone(g, o, d, last, LdsFlat{(CHR_LDS uint32_t *)stacks}, TAIL_STACK * 8,
+                                            LdsFlat{(CHR_LDS uint32_t *)tris}, overflow, sd, it);
             const unsigned long long t1 = __builtin_amdgcn_s_memrealtime(), c1 = __builtin_amdgcn_s_memtime();
             if (threadIdx.x == 0) {
                 uint32_t *o4 = out + 4 * ((size_t)r * reps + k);
@@ -4920,17 +5249,22 @@ __global__ __launch_bounds__(64) void walk_lone_timing_kernel(const DevGeom *__r
             }
         }
     }
+    if (walker == 1) {
+        lds_release();
+        lds_st(box + PB_STATE, PS_EXIT);
+    }
+    if (overflow) atomicAdd(out + 4 * (size_t)n * reps, overflow);
 }
 }  // namespace chr
 
 extern "C" int chr_walk_lone_timing(const chr_geometry *g, const float *d_rays, uint32_t n, uint32_t reps,
-                                    uint32_t nwaves, uint32_t *d_out, void *stream) {
-    if (!g || !d_rays || !d_out || nwaves == 0 || reps == 0)
+                                    uint32_t nwaves, int32_t walker, uint32_t *d_out, void *stream) {
+    if (!g || !d_rays || !d_out || nwaves == 0 || reps == 0 || walker < 0 || walker > 1)
         return chr::fail(CHR_ERR_INVALID, "chr_walk_lone_timing: bad argument");
     if (g->dev.nwnodes == 0) return chr::fail(CHR_ERR_INVALID, "chr_walk_lone_timing: geometry has no wide BVH");
     if (n == 0) return CHR_OK;
-    hipLaunchKernelGGL(chr::walk_lone_timing_kernel, dim3(std::min(nwaves, n)), dim3(64), 0, (hipStream_t)stream,
-                       (const chr::DevGeom *)g->d_dev, d_rays, n, reps, d_out);
+    hipLaunchKernelGGL(chr::walk_lone_timing_kernel, dim3(std::min(nwaves, n)), dim3(128), 0, (hipStream_t)stream,
+                       (const chr::DevGeom *)g->d_dev, d_rays, n, reps, d_out, walker);
     CHR_HIP_CHECK(hipGetLastError());
     return CHR_OK;
 }

@@ -41,22 +41,33 @@ def main():
     dr = ga.to_gpu(rays.reshape(-1))
     reps = 8
     out = {'detector': det_name, 'rays': int(len(alive))}
-    for nw in (1, 256, 2048):
-        n = len(alive) if nw > 1 else 256
-        res = ga.zeros(n * reps * 4, np.uint32)
-        _native.call('chr_walk_lone_timing', gdet._handle, dr.gpudata, n, reps, nw, res.gpudata, current_stream())
-        torch.cuda.synchronize()
-        r = res.get().reshape(n, reps, 4).astype(np.float64)
-        it = np.maximum(r[:, :, 1], 1)
-        row = {}
-        for name, sl in (('first', slice(0, 1)), ('warm', slice(1, reps))):
-            row[name] = {'iterations': float(np.median(r[:, sl, 1])),
-                         'ns_per_walk': float(np.median(r[:, sl, 2] * 10)),
-                         'ns_per_iteration': float(np.median(r[:, sl, 2] * 10 / it[:, sl])),
-                         'cycles_per_iteration': float(np.median(r[:, sl, 3] / it[:, sl]))}
-        same = bool(np.all(r[:, :, 0] == r[:, :1, 0]))
-        out['waves_%d' % nw] = dict(row, results_repeat=same, rays=n)
-        print(json.dumps({'waves': nw, **row}), flush=True)
+    base = None
+    for walker, wname in ((0, 'lone'), (1, 'pair')):
+        for nw in (1, 256, 2048):
+            n = len(alive) if nw > 1 else 256
+            res = ga.zeros(n * reps * 4 + 1, np.uint32)
+            _native.call('chr_walk_lone_timing', gdet._handle, dr.gpudata, n, reps, nw, walker, res.gpudata,
+                         current_stream())
+            torch.cuda.synchronize()
+            raw = res.get()
+            r = raw[:-1].reshape(n, reps, 4).astype(np.float64)
+            it = np.maximum(r[:, :, 1], 1)
+            row = {}
+            for name, sl in (('first', slice(0, 1)), ('warm', slice(1, reps))):
+                row[name] = {'iterations': float(np.median(r[:, sl, 1])),
+                             'ns_per_walk': float(np.median(r[:, sl, 2] * 10)),
+                             'ns_per_iteration': float(np.median(r[:, sl, 2] * 10 / it[:, sl])),
+                             'cycles_per_iteration': float(np.median(r[:, sl, 3] / it[:, sl]))}
+            same = bool(np.all(r[:, :, 0] == r[:, :1, 0]))
+            tris = raw[:-1].reshape(n, reps, 4)[:, 0, 0]
+            if nw == 2048:
+                if walker == 0:
+                    base = tris.copy()
+                else:
+                    row['same_as_lone'] = bool(np.array_equal(tris, base[:len(tris)]))
+            row['overflow'] = int(raw[-1])
+            out['%s_waves_%d' % (wname, nw)] = dict(row, results_repeat=same, rays=n)
+            print(json.dumps({'walker': wname, 'waves': nw, **row}), flush=True)
     print(json.dumps(out))
 
 
