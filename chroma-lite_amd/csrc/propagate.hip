@@ -1427,6 +1427,8 @@ struct PropagateArgs {
     const uint32_t *mode;
     uint32_t prio;                     // tail kernel: raise its waves' issue priority (s_setprio; the
                                        // batches' tail, the critical path beside the next batch's walk)
+    uint32_t pair;                     // tail kernel: a lone walk takes an idle wave of its workgroup as
+                                       // triangle tester (walk_pair; CHR_PAIR_WALK=0: walk_lone alone)
     uint32_t want;
     // tail kernel, work-queue mode (nullptr: group g runs queue positions g, g + cap, ...): a
     // zeroed counter the photon groups take queue positions from, for queues no longer than
@@ -2766,6 +2768,16 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_tail_kernel(const DevGe
     // a tail overlapped by the next batch (chr_propagate_batches) is the critical
     // path: its waves win the SIMD's issue arbitration over that batch's walk
     if (a.prio) __builtin_amdgcn_s_setprio(3);
+    // the workgroup's pair-walk mailbox (walk_pair), ordered before any use by the
+    // barriers of phys_cache / stage_top below
+    __shared__ uint32_t box_s[PB_WORDS];
+    CHR_LDS uint32_t *box = (CHR_LDS uint32_t *)box_s;
+    if (threadIdx.x == 0) {
+        box_s[PB_STATE] = PS_IDLE;
+        box_s[PB_IDLE] = 0u;
+        box_s[PB_WORKERS] = BLOCK / 64;
+        box_s[PB_ABORT] = 0u;
+    }
     __shared__ uint4 phys_lds[TAIL_PHYS_WORDS / 4];
     const DevGeom g = phys_cache(*gdev, phys_lds, TAIL_PHYS_WORDS);
     __shared__ uint4 top_lds[6 * TOP_NODES];   // 7 KB: 2 workgroups per CU hold 2 x 79 KB
@@ -2777,7 +2789,33 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_tail_kernel(const DevGe
     // launch is one resident grid (no waves waiting for dispatch behind the first ones,
     // no wave held by its slowest photon while its other groups idle)
     const bool wq = a.work != nullptr && n <= cap;
-    if (!wq && (tid & ~63u) / 8 >= nslot) return;      // whole waves: the others help walk
+    // A wave without photons (left) serves as its workgroup's pair-walk tester
+    // (walk_pair_tester) until no wave of the workgroup has photons: every wave
+    // calls this once, when it leaves the photon loop (or has no slot at all).
+    auto serve = [&]() {
+        if (lane == 0) atomicSub(&box_s[PB_WORKERS], 1u);
+        if (!a.pair) return;
+        if (lane == 0) atomicAdd(&box_s[PB_IDLE], 1u);
+        while (true) {
+            if (lds_ld(box + PB_STATE) == PS_REQ) {
+                uint32_t old = 0;
+                if (lane == 0) old = atomicCAS(&box_s[PB_STATE], PS_REQ, PS_TAKEN);
+                if ((uint32_t)__builtin_amdgcn_readfirstlane((int)old) == PS_REQ) {
+                    if (lane == 0) atomicSub(&box_s[PB_IDLE], 1u);
+                    lds_acquire();
+                    walk_pair_tester(g, box, (CHR_LDS uint32_t *)tris);
+                    if (lane == 0) atomicAdd(&box_s[PB_IDLE], 1u);
+                    continue;
+                }
+            }
+            if (lds_ld(box + PB_WORKERS) == 0u) break;   // no walker left to serve
+            __builtin_amdgcn_s_sleep(2);
+        }
+    };
+    if (!wq && (tid & ~63u) / 8 >= nslot) {            // whole waves: the others help walk
+        serve();
+        return;
+    }
     auto next_q = [&]() -> uint32_t {   // the group's next queue position (group-uniform)
         uint32_t v = 0;
         if (sub == 0) v = atomicAdd(a.work, 1u);
@@ -2904,7 +2942,17 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_tail_kernel(const DevGe
             const uint32_t seg0 = lane & ~(uint32_t)(Gs - 1);
             float sd;
             uint32_t it;
-            const int st = Gs == 64
+            // one walker: with an idle wave of the workgroup as its triangle tester when
+            // there is one (claimed by the mailbox's PS_IDLE -> PS_POSTING)
+            bool paired = false;
+            if (Gs == 64 && a.pair && lds_ld(box + PB_IDLE) != 0u && lds_ld(box + PB_STATE) == PS_IDLE) {
+                uint32_t old = PS_TAKEN;
+                if (lane == 0) old = atomicCAS(&box_s[PB_STATE], PS_IDLE, PS_POSTING);
+                paired = (uint32_t)__builtin_amdgcn_readfirstlane((int)old) == PS_IDLE;
+            }
+            const int st = paired ? walk_pair(g, top, o, dd, last, LdsFlat{wstack}, TAIL_STACK * 8, wtris,
+                                              (threadIdx.x >> 6) * 2u * TAIL_TRI, box, overflow, sd, it)
+                           : Gs == 64
                                ? walk_lone(g, o, dd, last, LdsFlat{wstack}, TAIL_STACK * 8, LdsFlat{wtris}, overflow, sd, it)
                                : walk_segment<0>(g, act, o, dd, last, Gs, LdsFlat{wstack + seg0 / 8 * TAIL_STACK * 2},
                                                  TAIL_STACK * Gs / 8, LdsFlat{wtris + 4 * seg0}, top, overflow, sd, it);
@@ -2958,6 +3006,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_tail_kernel(const DevGe
     if (!wq && have_rng && sub == 0) store_rng(a, slot, rng);
     if (sub == 0 && overflow) atomicAdd(a.counters, overflow);
     if (sub == 0 && flat && a.diag) atomicAdd(a.diag, flat);
+    serve();
 #ifdef CHR_DEVICE_PROFILE
     pf.tick(P_OTHER);
     prof_add(CHR_PROF_TAIL_WALK, pf.calls[P_WALK], pf.cyc[P_WALK]);
@@ -3980,6 +4029,7 @@ static StepVariant select_step_variant(const chr_geometry *g) {
 }
 
 // scratch layout (u32 words): [0] overflows [1] queue base [2..11] u64 walk counters [12..15] pad; masks (u64, 8-aligned); offsets
+static bool pair_walk_enabled();
 static int launch_chunk(const chr_geometry *g, const chr_photons *ph, uint32_t *rng, uint32_t nslots, int32_t first,
                         int32_t nthreads, const uint32_t *in_queue, uint32_t *out_queue, int32_t max_steps,
                         int32_t use_weights, int32_t scatter_first, uint32_t *scratch, hipStream_t stream,
@@ -4003,6 +4053,7 @@ static int launch_chunk(const chr_geometry *g, const chr_photons *ph, uint32_t *
     a.want = STEP_ONE;
     a.work = nullptr;
     a.prio = 0;
+    a.pair = pair_walk_enabled() ? 1u : 0u;
     if (ev0) CHR_HIP_CHECK(hipEventRecord(ev0, stream));
     hipLaunchKernelGGL(select_variant(g), dim3(grid_for(nthreads)), dim3(BLOCK), 0, stream,
                        (const DevGeom *)g->d_dev, a);
@@ -4066,6 +4117,13 @@ static bool trace_steps();
 // "1" every slot's events as well (kernel_ms, tail_ms, the prefix split);
 // "0" only the events the streams and the host synchronise on.  Times not
 // recorded read 0 in chr_propagate_stats.
+// CHR_PAIR_WALK=0: the tail's lone walks on their own wave only (walk_lone; A/B,
+// default 1: walk_pair with an idle wave of the workgroup as tester)
+static bool pair_walk_enabled() {
+    const char *e = getenv("CHR_PAIR_WALK");
+    return !(e && e[0] == '0');
+}
+
 static int slot_timing() {
     const char *e = getenv("CHR_SLOT_TIMING");
     if (!e || e[0] == 't') return 1;
@@ -4156,6 +4214,7 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
     a.want = STEP_ONE;
     a.work = nullptr;
     a.prio = 0;
+    a.pair = pair_walk_enabled() ? 1u : 0u;
     RayEnrol fe{nullptr, nullptr, nullptr, nullptr};
     const uint32_t threads = std::min(cap, (n + 63u) & ~63u);
     const StepVariant sv = select_step_variant(g);
