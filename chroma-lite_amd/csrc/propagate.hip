@@ -2488,11 +2488,28 @@ __device__ __forceinline__ int walk_pair_walker(const DevGeom &g, const TopNodes
     uint32_t nl = 0;                                  // lists published
     bool ok = true;
     iters = 0;
-    uint4 h, a1, a2, a3, a4, a5;
-    load_node(g, top, cur == INVALID ? 0u : cur, h, a1, a2, a3, a4, a5);
+    // a node's 88 used bytes (the last 16-byte word's first 8: its slot offsets), from
+    // the LDS top of the tree or global memory: every register a load writes is read
+    // by the expansion, so none is reused as a temporary while the load is in flight
+    // (the compiler would wait for every load there)
+    uint4 h, a1, a2, a3, a4;
+    uint2 a5;
+    auto fetch_node = [&](uint32_t node) {
+        if (node < top.n) {
+            const CHR_LDS u32x4 *tp = top.p + 6u * node;
+            h = u4(tp[0]); a1 = u4(tp[1]); a2 = u4(tp[2]); a3 = u4(tp[3]); a4 = u4(tp[4]);
+            const chr_u32x2 t5 = *(const CHR_LDS chr_u32x2 *)(tp + 5);
+            a5 = make_uint2(t5.x, t5.y);
+        } else {
+            const uint4 *np = g.wnodes + (size_t)g.wstride * node;
+            h = gld(np); a1 = gld(np + 1); a2 = gld(np + 2); a3 = gld(np + 3); a4 = gld(np + 4);
+            a5 = gld_lo2(np + 5);
+        }
+    };
+    fetch_node(cur == INVALID ? 0u : cur);
+    float best = __uint_as_float(lds_ld(box + PB_BEST));   // the tester's, read once per iteration
     while (true) {
         iters++;
-        const float best = __uint_as_float(lds_ld(box + PB_BEST));
         bool inner = false, leafhit = false;
         float tk = 0.0f;
         uint32_t kind = 0, child = 0, first = 0;
@@ -2545,22 +2562,10 @@ __device__ __forceinline__ int walk_pair_walker(const DevGeom &g, const TopNodes
         cur = near;
         cur_t = __uint_as_float(key & ~7u);
         // this expansion's hit-leaf triangles -> list nl (buffer nl & 1, free once the
-        // tester has read list nl - 2)
+        // tester has read list nl - 2), published once the next nodes are in flight
         const uint32_t cnt = leafhit ? kind : 0u;
         const unsigned long long b0 = __ballot(cnt & 1u), b1 = __ballot(cnt & 2u), b2 = __ballot(cnt & 4u);
         const uint32_t Tn = uu(__popcll(b0) + 2u * __popcll(b1) + 4u * __popcll(b2));
-        if (Tn) {
-            const uint32_t pre = __popcll(b0 & below) + 2u * __popcll(b1 & below) + 4u * __popcll(b2 & below);
-            if (nl >= 2u && ok) ok = pair_wait(box, [&]() { return lds_ld(box + PB_TREAD) + 1u >= nl; });
-            const int nb = (int)(nl & 1u) * TAIL_TRI;
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-                if ((uint32_t)i < cnt) lists[nb + (int)min(pre + (uint32_t)i, (uint32_t)(TAIL_TRI - 1))] = first + (uint32_t)i;
-            lds_st(box + PB_CNT0 + (nl & 1u), Tn);
-            lds_release();
-            lds_st(box + PB_WSEQ, nl + 1u);
-            nl++;
-        }
         // cursors without a node take the topmost unculled stack entries (walk_lone's refill)
         unsigned long long em = __ballot(k == 0u && cur == INVALID);
         while (em != 0 && sp > 0) {
@@ -2596,17 +2601,31 @@ __device__ __forceinline__ int walk_pair_walker(const DevGeom &g, const TopNodes
         }
         sp = (int)uu((uint32_t)sp);
         if (cur != INVALID && cur_t > best) cur = INVALID;
-        if (__ballot(cur != INVALID) == 0 && sp == 0) break;
-        load_node(g, top, cur == INVALID ? 0u : cur, h, a1, a2, a3, a4, a5);
+        const bool end = __ballot(cur != INVALID) == 0 && sp == 0;
+        if (!end) fetch_node(cur == INVALID ? 0u : cur);
+        if (Tn) {
+            const uint32_t pre = __popcll(b0 & below) + 2u * __popcll(b1 & below) + 4u * __popcll(b2 & below);
+            if (nl >= 2u && ok) ok = pair_wait(box, [&]() { return lds_ld(box + PB_TREAD) + 1u >= nl; });
+            const int nb = (int)(nl & 1u) * TAIL_TRI;
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                if ((uint32_t)i < cnt) lists[nb + (int)min(pre + (uint32_t)i, (uint32_t)(TAIL_TRI - 1))] = first + (uint32_t)i;
+            lds_st(box + PB_CNT0 + (nl & 1u), Tn);
+            lds_release();
+            lds_st(box + PB_WSEQ, nl + 1u);
+            nl++;
+        }
+        best = __uint_as_float(lds_ld(box + PB_BEST));
+        if (end) break;
     }
     lds_release();
     lds_st(box + PB_WDONE, nl);
     if (ok) ok = pair_wait(box, [&]() { return lds_ld(box + PB_STATE) == PS_DONE; });
     lds_acquire();
-    const float best = __uint_as_float(lds_ld(box + PB_BEST));
+    const float fbest = __uint_as_float(lds_ld(box + PB_BEST));
     const int best_id = (int)lds_ld(box + PB_ID);
     if (!ok && lane == 0) overflow += 1u << 20;   // a lost handshake: reported as stack overflows
-    min_distance = best_id == -1 ? -1.0f : best;
+    min_distance = best_id == -1 ? -1.0f : fbest;
     return best_id;
 }
 
