@@ -1,0 +1,79 @@
+"""The lone walk split over two waves (walk_pair): on the same rays
+it returns exactly walk_lone's nearest hit (record index; walk_lone is pinned to
+the oracle through the tail parity tests, test_gpu_batches.py), with no lost
+handshake or stack overflow, including flat (axis-parallel / plane-parallel)
+directions and rays that start on a surface with their last hit excluded.
+Reference walk semantics: chroma/cuda/mesh.h:45-126."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope='module')
+def cuda():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip('no HIP device')
+    from chroma.gpu import create_cuda_context
+    return create_cuda_context()
+
+
+def _rays(n, seed):
+    rng = np.random.default_rng(seed)
+    o = rng.uniform(-600.0, 600.0, (n, 3)).astype(np.float32)
+    d = rng.normal(size=(n, 3))
+    d[: n // 8, 2] = 0.0                       # plane-parallel
+    d[n // 8: n // 4, 1:] = 0.0                # axis-parallel
+    d /= np.linalg.norm(d, axis=1)[:, None]
+    rays = np.zeros((n, 7), np.float32)
+    rays[:, 0:3] = o
+    rays[:, 3:6] = d.astype(np.float32)
+    rays[:, 6] = np.full(n, -1, np.int32).view(np.float32)
+    return rays
+
+
+def _walk(det, rays, walker, nwaves, reps=2):
+    import torch
+    from chroma.gpu import _native, gpuarray as ga
+    from chroma.gpu.tools import current_stream
+    n = len(rays)
+    dr = ga.to_gpu(rays.reshape(-1))
+    out = ga.zeros(n * reps * 4 + 1, np.uint32)
+    _native.call('chr_walk_lone_timing', det._handle, dr.gpudata, n, reps, nwaves, walker, out.gpudata,
+                 current_stream())
+    torch.cuda.synchronize()
+    raw = out.get()
+    return raw[:-1].reshape(n, reps, 4)[:, :, 0].astype(np.int32), int(raw[-1])
+
+
+@pytest.mark.parametrize('nwaves', [1, 64])
+def test_pair_walk_equals_lone(cuda, small_detector, nwaves):
+    from chroma import gpu
+    det = gpu.GPUDetector(small_detector)
+    rays = _rays(512 if nwaves > 1 else 96, seed=3 + nwaves)
+    lone, ov0 = _walk(det, rays, 0, nwaves)
+    pair, ov1 = _walk(det, rays, 1, nwaves)
+    assert ov0 == 0 and ov1 == 0
+    assert np.array_equal(lone[:, 0], lone[:, 1]) and np.array_equal(pair[:, 0], pair[:, 1])
+    assert np.array_equal(lone, pair)
+    assert (lone[:, 0] >= 0).sum() > len(rays) // 2     # most rays hit something
+
+
+def test_pair_walk_from_hits(cuda, small_detector, small_packed):
+    """Rays with their nearest triangle excluded (last hit = that triangle's id, as a
+    tail step's ray restarting on the surface it reached): the walk finds the next one."""
+    from chroma import gpu
+    from chroma.gpu import wide_bvh
+    det = gpu.GPUDetector(small_detector)
+    rec_id = np.asarray(wide_bvh.build(small_packed).rec_id)   # the same deterministic build as the upload's
+    rays = _rays(512, seed=11)
+    first, _ = _walk(det, rays, 0, 64, reps=1)
+    hit = first[:, 0] >= 0
+    rr = rays[hit].copy()
+    rr[:, 6] = rec_id[first[hit, 0]].astype(np.int32).view(np.float32)
+    lone, ov0 = _walk(det, rr, 0, 64)
+    pair, ov1 = _walk(det, rr, 1, 64)
+    assert ov0 == 0 and ov1 == 0 and np.array_equal(lone, pair)
+    assert not np.array_equal(lone[:, 0], first[hit, 0])      # the excluded triangles are not found again
+    assert np.all(lone[:, 0] != first[hit, 0])
