@@ -2474,7 +2474,7 @@ __device__ __forceinline__ int walk_pair_walker(const DevGeom &g, const TopNodes
     auto uu = [](uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); };
     o = v3(ufl(o.x), ufl(o.y), ufl(o.z));
     d = v3(ufl(d.x), ufl(d.y), ufl(d.z));
-    const int scap = cap;                             // stack entries
+    const int scap = cap - 8;                         // stack entries; [scap, cap): the refill's scratch
     const uint32_t lane = __lane_id();
     const uint32_t k = lane & 7u;
     const uint32_t lead = lane & ~7u;
@@ -2583,22 +2583,22 @@ __device__ __forceinline__ int walk_pair_walker(const DevGeom &g, const TopNodes
             const int rho = __popcll(okm & below);
             const unsigned long long stopm = __ballot(okk && rho == take);
             const int consumed = stopm ? (__ffsll((long long)stopm) - 1) : W;
-            // the r-th empty cursor takes the r-th unculled entry: scalar readlanes (take
-            // <= 8, usually 1-2), no LDS round trip through a scratch buffer
-            unsigned long long om = okm, tm = em, taken = 0;
-            for (int r = 0; r < take; ++r) {
-                const int src = __ffsll((long long)om) - 1;
-                const int dst = __ffsll((long long)tm) - 1;
-                om &= om - 1;
-                tm &= tm - 1;
-                taken |= 1ull << dst;
-                const uint32_t e_n = (uint32_t)__builtin_amdgcn_readlane((int)en, src);
-                const uint32_t e_t = (uint32_t)__builtin_amdgcn_readlane((int)et, src);
-                if ((int)lead == dst) {
-                    cur = e_n;
-                    cur_t = __uint_as_float(e_t);
-                }
+            // the r-th empty cursor takes the r-th unculled entry through the scratch
+            // words (an LDS broadcast to its 8 lanes; handing them over by scalar
+            // readlanes instead measured slower)
+            if (okk && rho < take) {
+                stk[2 * (scap + rho)] = en;
+                stk[2 * (scap + rho) + 1] = et;
             }
+            __builtin_amdgcn_wave_barrier();
+            const bool empty = ((em >> lead) & 1ull) != 0;
+            const int rnk = __popcll(em & ((1ull << lead) - 1ull));
+            const unsigned long long taken = __ballot(k == 0u && empty && rnk < take);
+            if (empty && rnk < take) {
+                cur = stk[2 * (scap + rnk)];
+                cur_t = __uint_as_float(stk[2 * (scap + rnk) + 1]);
+            }
+            __builtin_amdgcn_wave_barrier();
             sp = (int)uu((uint32_t)(sp - consumed));
             em &= ~taken;
         }
