@@ -2583,9 +2583,6 @@ __device__ __forceinline__ int walk_pair_walker(const DevGeom &g, const TopNodes
             const int rho = __popcll(okm & below);
             const unsigned long long stopm = __ballot(okk && rho == take);
             const int consumed = stopm ? (__ffsll((long long)stopm) - 1) : W;
-            // the r-th empty cursor takes the r-th unculled entry through the scratch
-            // words (an LDS broadcast to its 8 lanes; handing them over by scalar
-            // readlanes instead measured slower)
             if (okk && rho < take) {
                 stk[2 * (scap + rho)] = en;
                 stk[2 * (scap + rho) + 1] = et;
