@@ -516,7 +516,9 @@ class PropagateWorkload(object):
                           'long_walk_us_per_step': round(s.tail_long_walk_ticks / 100.0 /
                                                          max(1, s.tail_long_steps), 3),
                           'long_walk_iterations_per_step': round(s.tail_long_walk_iterations /
-                                                                 max(1, s.tail_long_steps), 2)} for s in stats]}
+                                                                 max(1, s.tail_long_steps), 2),
+                          'long_paired_step_fraction': round(s.tail_long_paired_steps / max(1, s.tail_long_steps), 3)}
+                         for s in stats]}
 
     def untimed_passes(self):
         """After timing: the counting variant (own-layout bytes, SIMD efficiency)

@@ -81,7 +81,7 @@ class PropagateStats(ctypes.Structure):
                 ('tail_max_steps', c_u32), ('tail_slowest_steps', c_u32), ('tail_max_cycles', c_u64),
                 ('tail_long_photons', c_u32), ('reserved2', c_u32), ('tail_long_steps', c_u64),
                 ('tail_long_ticks', c_u64), ('tail_long_walk_ticks', c_u64), ('tail_long_walk_iterations', c_u64),
-                ('host_syncs', c_u32), ('reserved3', c_u32), ('trace_launch_rays', c_u32 * 32)]
+                ('host_syncs', c_u32), ('tail_long_paired_steps', c_u32), ('trace_launch_rays', c_u32 * 32)]
 
 
 class KernelAttr(ctypes.Structure):

@@ -2848,7 +2848,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_tail_kernel(const DevGe
     Photon p;
     State s;
     int steps = 0, scatter_first = 0;
-    uint32_t q = wq ? next_q() : slot, pid = 0, iters = 0;
+    uint32_t q = wq ? next_q() : slot, pid = 0, iters = 0, paired_steps = 0;
     bool live = false, exhausted = wq ? q >= n : slot >= nslot;
     unsigned long long t0 = 0, walk_ticks = 0;
     enum { P_WALK, P_PHYS, P_OTHER };
@@ -2884,6 +2884,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_tail_kernel(const DevGe
                     atomicAdd(d64 + 2, (unsigned long long)iters);
                     atomicAdd(d64 + 3, (unsigned long long)steps);
                     atomicAdd(d64 + 4, 1ull);
+                    atomicAdd(d64 + 5, (unsigned long long)paired_steps);
                 }
             }
         }
@@ -2910,6 +2911,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_tail_kernel(const DevGe
                 p.weight = a.weights[pid];
                 steps = 0;
                 iters = 0;
+                paired_steps = 0;
                 walk_ticks = 0;
                 scatter_first = a.scatter_first;
                 live = true;
@@ -2986,6 +2988,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_tail_kernel(const DevGe
             }
             if (walk) {
                 iters += it;
+                paired_steps += paired ? 1u : 0u;
                 walk_ticks += __builtin_amdgcn_s_memrealtime() - tw0;
             }
             pf.tick(P_OTHER);
@@ -4685,11 +4688,11 @@ static int slot_stats(chr_propagate_stats &st, const uint32_t *h, int k, const s
 }
 
 // device counters of a propagate -> pinned words [2] overflows, [4..17] walk
-// counters, [20..34] flat-walk and tail diagnostics (fused path)
+// counters, [20..36] flat-walk and tail diagnostics (fused path)
 static int counter_readback(const PropBufs &b, hipStream_t s) {
     CHR_HIP_CHECK(hipMemcpyAsync(b.pinned + 2, b.scratch, 4, hipMemcpyDeviceToHost, s));
     CHR_HIP_CHECK(hipMemcpyAsync(b.pinned + 4, b.scratch + 2, 56, hipMemcpyDeviceToHost, s));
-    if (b.fused) CHR_HIP_CHECK(hipMemcpyAsync(b.pinned + 20, b.fc.ctl + 3, 60, hipMemcpyDeviceToHost, s));
+    if (b.fused) CHR_HIP_CHECK(hipMemcpyAsync(b.pinned + 20, b.fc.ctl + 3, 68, hipMemcpyDeviceToHost, s));
     return CHR_OK;
 }
 
@@ -4704,13 +4707,14 @@ static void counter_stats(chr_propagate_stats &st, const PropBufs &b) {
         st.tail_max_steps = pinned[22];
         st.tail_max_cycles = key >> 16;
         st.tail_slowest_steps = (uint32_t)(key & 0xFFFFu);
-        uint64_t lp[5];
-        std::memcpy(lp, pinned + 25, 40);   // ctl[8..17]
+        uint64_t lp[6];
+        std::memcpy(lp, pinned + 25, 48);   // ctl[8..19]
         st.tail_long_walk_ticks = lp[0];
         st.tail_long_ticks = lp[1];
         st.tail_long_walk_iterations = lp[2];
         st.tail_long_steps = lp[3];
         st.tail_long_photons = (uint32_t)lp[4];
+        st.tail_long_paired_steps = (uint32_t)lp[5];
     }
     uint64_t c[7];
     std::memcpy(c, pinned + 4, 56);

@@ -194,7 +194,7 @@ typedef struct chr_propagate_stats {
     uint64_t tail_long_walk_iterations;   /*   and dependent walk iterations */
     uint32_t host_syncs;          /* waits that drain the stream (the host reads the survivor count): one
                                      per host step when host-driven, 1 when the steps are device-driven */
-    uint32_t reserved3;
+    uint32_t tail_long_paired_steps;  /* the long photons' steps whose walk had a tester wave (walk_pair) */
     uint32_t trace_launch_rays[32];   /* queued photons of each trace_kernel launch, in order */
 } chr_propagate_stats;
 #define CHR_TRACE_MS_MAX 32

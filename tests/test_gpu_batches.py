@@ -299,3 +299,5 @@ def test_mirror_scene_long_tail_parity(cuda):
         assert np.all(np.abs(a - b) <= 1e-5 * np.maximum(np.abs(b), 1.0)), 'mirror scene: %s' % f
     assert np.array_equal(rng, states.reshape(6, nslots))
     assert stats[0].tail_photons > 0
+    if stats[0].tail_long_steps > 0:   # long-lived photons walk with a tester wave (walk_pair)
+        assert stats[0].tail_long_paired_steps > 0
