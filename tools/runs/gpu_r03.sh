@@ -5,7 +5,7 @@
 #   prof:  rocprof kernel trace + PMC passes (tools/rocprof_bench.sh) -> stamped summary, then the bench
 # Every GPU step has its own time limit; the first failure ends the script.
 set -u
-R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
+R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/../.." && pwd)}
 TAG=$1
 MODE=${2:-all}
 SEL=${3:-tests}

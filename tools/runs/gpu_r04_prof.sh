@@ -3,7 +3,7 @@
 # command (29k detector), then the same PMC passes for C5 (scintillator detector)
 # usage: tools/gpu_r04_prof.sh TAG   (GIT_HEAD in the environment)
 set -u
-R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
+R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/../.." && pwd)}
 T=$1
 cd "$R"
 bash tools/rocprof_bench.sh "gpurun_out/$T/prof29k" --steps 20 --warmup 5 || exit $?

@@ -4,7 +4,7 @@
 #  2. bench lines of C2 / C3 / C5 and a kernel trace of C2
 # usage: tools/gpu_r05_prof.sh TAG [prof|configs|both]
 set -u
-R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
+R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/../.." && pwd)}
 T=$1; WHAT=${2:-both}
 cd "$R"
 export CHROMA_BENCH_CACHE=/tmp/chroma_bench_cache
