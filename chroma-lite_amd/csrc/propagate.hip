@@ -3124,7 +3124,6 @@ struct TraceArgs {
     uint32_t *walk_hist;         // COUNT: [0..31] walks by log2(nodes + triangles), [32..33] u64 max (cost << 32 | photon)
     uint2 *spill;                // stack entries >= SL: (WIDE_STACK - SL) x gridDim.x*BLOCK, entry-major (HBM, no scratch)
     uint32_t *diag;              // [0] += flat rays walked by this launch (nullptr: off)
-    uint32_t drain_prio;         // issue priority of a draining wave (s_setprio; 0: unchanged)
     // device-driven steps (nullptr: host-driven): the queue length is *dev_n - 1
     // (the input queue's count header) and the launch runs only if *mode is STEP_ONE
     const uint32_t *dev_n;
@@ -3414,11 +3413,6 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
     }
     if constexpr (!COUNT) {
         if (drain) {
-            // a draining wave holds the launch's last walks: let it win the SIMD's
-            // issue arbitration over waves that still have many
-            if (a.drain_prio == 1) __builtin_amdgcn_s_setprio(1);
-            else if (a.drain_prio == 2) __builtin_amdgcn_s_setprio(2);
-            else if (a.drain_prio == 3) __builtin_amdgcn_s_setprio(3);
             pf.tick(P_DRAIN);
             const unsigned long long rm = __ballot(has_ray);
             const int w = __popcll(rm);
@@ -4152,14 +4146,6 @@ static bool pair_walk_enabled() {
     return !(e && e[0] == '0');
 }
 
-// CHR_DRAIN_PRIO (A/B): issue priority 0-3 of a trace_kernel wave once it drains
-// its last walks (default 0)
-static uint32_t drain_prio() {
-    const char *e = getenv("CHR_DRAIN_PRIO");
-    const int v = e ? atoi(e) : 0;
-    return v < 0 ? 0u : (v > 3 ? 3u : (uint32_t)v);
-}
-
 static int slot_timing() {
     const char *e = getenv("CHR_SLOT_TIMING");
     if (!e || e[0] == 't') return 1;
@@ -4305,7 +4291,6 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
         ta.rays = use_rays ? fc->rays : nullptr;
         ta.walk_hist = nullptr;
         ta.diag = fc->ctl + 3;
-        ta.drain_prio = drain_prio();
         ta.dev_n = dev_n;
         ta.mode = mode;
         if (fc->enrol_next) fe = RayEnrol{ph->d_pos, ph->d_dir, fc->rays, ph->d_last_hit_triangles};
