@@ -3124,7 +3124,6 @@ struct TraceArgs {
     uint32_t *walk_hist;         // COUNT: [0..31] walks by log2(nodes + triangles), [32..33] u64 max (cost << 32 | photon)
     uint2 *spill;                // stack entries >= SL: (WIDE_STACK - SL) x gridDim.x*BLOCK, entry-major (HBM, no scratch)
     uint32_t *diag;              // [0] += flat rays walked by this launch (nullptr: off)
-    uint32_t refill_pipe;        // ray-record refills pipelined over two steps (no stall; rays path only)
     // device-driven steps (nullptr: host-driven): the queue length is *dev_n - 1
     // (the input queue's count header) and the launch runs only if *mode is STEP_ONE
     const uint32_t *dev_n;
@@ -3259,12 +3258,12 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
         if (slab.flat) nflat_rays++;
         if constexpr (COUNT) cnt.walks++;
     };
-    // Pipelined refill (a.refill_pipe, ray records): a claim's counter add is issued in
+    // Pipelined refill (ray records, a.rays): a claim's counter add is issued in
     // one step, its ray records are loaded in the next, the walks begin in the one after
     // -- each wait covered by that step's own node / triangle loads (issued later, waited
     // for anyway) instead of stalling the wave twice per refill.  The lanes of a claim
     // still begin together (a binned launch keeps its coherent walks).
-    const bool pipe = a.refill_pipe != 0u && a.rays != nullptr;
+    const bool pipe = a.rays != nullptr;
     int rstage = 0;                  // 0 idle, 1 counter add in flight, 2 records in flight
     uint32_t rbase = 0, rj = 0, rwant = 0;
     int rleader = 0;
@@ -4210,12 +4209,6 @@ static bool pair_walk_enabled() {
     return !(e && e[0] == '0');
 }
 
-// CHR_REFILL_PIPE=1: trace_kernel's ray refills pipelined over two steps (A/B)
-static bool refill_pipe_enabled() {
-    const char *e = getenv("CHR_REFILL_PIPE");
-    return e && e[0] == '1';
-}
-
 static int slot_timing() {
     const char *e = getenv("CHR_SLOT_TIMING");
     if (!e || e[0] == 't') return 1;
@@ -4361,7 +4354,6 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
         ta.rays = use_rays ? fc->rays : nullptr;
         ta.walk_hist = nullptr;
         ta.diag = fc->ctl + 3;
-        ta.refill_pipe = refill_pipe_enabled() ? 1u : 0u;
         ta.dev_n = dev_n;
         ta.mode = mode;
         if (fc->enrol_next) fe = RayEnrol{ph->d_pos, ph->d_dir, fc->rays, ph->d_last_hit_triangles};
