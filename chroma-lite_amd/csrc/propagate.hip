@@ -3243,32 +3243,6 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
     enum { P_NODE, P_TRI, P_REFILL, P_IDLE, P_DRAIN, P_BOX = 3 };   // regions (calls: P_REFILL = walks, P_BOX = boxes)
     Prof<5> pf;
     pf.start(P_REFILL);
-    // a walk from the ray now in o, d, last (the refill's last step)
-    auto begin_walk = [&]() {
-        node = 0;
-        best = __builtin_inff();
-        best_rank = 0xFFFFFFFFu;
-        slab = make_slab(o, v3(-o.x / d.x, -o.y / d.y, -o.z / d.z), v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z));
-        best_id = -1;
-        sp = 0;
-        walk_done = false;
-        has_ray = true;
-        walk_cost = 0;
-        pf.call(P_REFILL);
-        if (slab.flat) nflat_rays++;
-        if constexpr (COUNT) cnt.walks++;
-    };
-    // Pipelined refill (ray records, a.rays): a claim's counter add is issued in
-    // one step, its ray records are loaded in the next, the walks begin in the one after
-    // -- each wait covered by that step's own node / triangle loads (issued later, waited
-    // for anyway) instead of stalling the wave twice per refill.  The lanes of a claim
-    // still begin together (a binned launch keeps its coherent walks).
-    const bool pipe = a.rays != nullptr;
-    int rstage = 0;                  // 0 idle, 1 counter add in flight, 2 records in flight
-    uint32_t rbase = 0, rj = 0, rwant = 0;
-    int rleader = 0;
-    bool rmine = false;              // this lane takes a ray of the claim in flight
-    uint4 pr0 = make_uint4(0u, 0u, 0u, 0u), pr1 = pr0;
     while (true) {
         pf.tick(P_REFILL);   // the last step goes to the region each work-item was in
         if (has_ray && walk_done && pleft == 0 && qh == qt) {   // walk over: publish (mesh.h:123-125)
@@ -3282,44 +3256,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
                 }
             }
         }
-        if (pipe) {
-            if (rstage == 2) {                          // the records are in: begin the walks
-                if (rmine) {
-                    rmine = false;
-                    q = pr1.w & ~RAY_SKIP;
-                    if (!(pr1.w & RAY_SKIP)) {
-                        o = v3(__uint_as_float(pr0.x), __uint_as_float(pr0.y), __uint_as_float(pr0.z));
-                        d = v3(__uint_as_float(pr0.w), __uint_as_float(pr1.x), __uint_as_float(pr1.y));
-                        last = pr1.z;
-                        if constexpr (COUNT) pid = a.walk_hist ? a.queue[q] : q;
-                        begin_walk();
-                    }
-                }
-                rstage = 0;
-            } else if (rstage == 1) {                   // the claim's base is in: load the records
-                const uint32_t base = (uint32_t)__shfl((int)rbase, rleader);
-                if (base + rwant >= total) exhausted = true;
-                rj += base;
-                if (rmine && rj < n) {
-                    pr0 = gld(a.rays + 2 * (size_t)rj);
-                    pr1 = gld(a.rays + 2 * (size_t)rj + 1);
-                } else {
-                    rmine = false;
-                }
-                rstage = 2;
-            }
-            if (rstage == 0 && !exhausted) {
-                const unsigned long long need = __ballot(!has_ray);
-                if (need != 0 && (__popcll(need) >= R || need == __ballot(1))) {
-                    rwant = (uint32_t)__popcll(need) < claim ? (uint32_t)__popcll(need) : claim;
-                    rj = (uint32_t)__popcll(need & ((1ull << lane) - 1ull));   // + the base, next step
-                    rleader = __ffsll((long long)need) - 1;
-                    if ((int)lane == rleader) rbase = atomicAdd(a.next, rwant);
-                    rmine = !has_ray && rj < rwant;
-                    rstage = 1;
-                }
-            }
-        } else if (!exhausted) {
+        if (!exhausted) {
             const unsigned long long need = __ballot(!has_ray);
             if (need != 0 && (__popcll(need) >= R || need == __ballot(1))) {
                 const uint32_t want = (uint32_t)__popcll(need) < claim ? (uint32_t)__popcll(need) : claim;
@@ -3387,7 +3324,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
             // every small launch).  Each restarts from the root seeded with its
             // best so far (conservative culling, the same nearest hit); the
             // lanes' stacks are abandoned and their LDS rows reused.
-            if (exhausted && rstage == 0 && __ballot(has_ray) != 0 && (uint32_t)__popcll(__ballot(has_ray)) <= DRAIN_MAX) {
+            if (exhausted && __ballot(has_ray) != 0 && (uint32_t)__popcll(__ballot(has_ray)) <= DRAIN_MAX) {
                 drain = true;   // after the loop, where the walk state below is no longer live
                 break;
             }
@@ -3398,7 +3335,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
         const unsigned long long mw = __ballot(can_walk);
         const unsigned long long mt = __ballot(has_work);
         if ((mw | mt) == 0) {
-            if (exhausted && rstage == 0 && __ballot(has_ray) == 0) {
+            if (exhausted && __ballot(has_ray) == 0) {
                 break;
             }
             continue;                                    // walks ended: publish + refill
