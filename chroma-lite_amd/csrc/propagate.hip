@@ -3193,7 +3193,10 @@ __global__ __launch_bounds__(BLOCK) void permute_rays_kernel(const uint4 *rays_i
 // COUNT: walk counters; F: triangle step once F/8 of the walking lanes have
 // parked leaves (intersect_wide_spec); SL: stack entries in LDS; MINW: waves
 // per SIMD; R: refill once R of the 64 lanes are without a ray.
-template <bool COUNT, int F, int SL, int MINW, int R>
+// GATHER: refill from the photon arrays (order -> queue -> flags / pos / dir /
+// last hit) instead of the ray records; a separate instantiation, so the
+// ray-record kernel's walk loop carries no code of the other refill.
+template <bool COUNT, int F, int SL, int MINW, int R, bool GATHER = false>
 __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__restrict__ gdev, TraceArgs a) {
     constexpr int TB = BLOCK;
     __shared__ uint32_t lds[(2 * SL + LEAFQ) * TB];
@@ -3269,7 +3272,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
                 const uint32_t j = base + rank;
                 if (!has_ray && rank < want) {
                     bool start = false;
-                    if (j < n && a.rays) {
+                    if (!GATHER && j < n) {
                         // the ray record: one 32-B load (put_ray); skip bit: dead / NaN
                         const uint4 r0 = gld(a.rays + 2 * (size_t)j), r1 = gld(a.rays + 2 * (size_t)j + 1);
                         q = r1.w & ~RAY_SKIP;
@@ -3283,7 +3286,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
                             best = __builtin_inff();
                             best_rank = 0xFFFFFFFFu;
                         }
-                    } else if (j < n) {
+                    } else if (GATHER && j < n) {
                         q = a.order ? a.order[j] : j;
                         pid = a.queue[q];
                         // dead on entry / NaN: no walk (the step kernel skips / aborts them)
@@ -3994,6 +3997,7 @@ typedef void (*trace_fn)(const DevGeom *, TraceArgs);
 struct StepVariant {
     propagate_step_fn fn;           // fused step kernel (any max_steps)
     trace_fn trace = nullptr;       // one-step launches: trace_kernel + shade (nullptr: fn)
+    trace_fn trace_gather = nullptr;   // its form refilling from the photon arrays (no ray records)
     propagate_step_fn shade = nullptr;
     int trace_waves = 4;            // waves per SIMD of the trace kernel (persistent grid size)
     int trace_block = BLOCK;        // its workgroup size
@@ -4033,6 +4037,7 @@ static StepVariant select_step_variant(const chr_geometry *g) {
         case 5:   // walk counters of the one-step launches' trace kernel; the tail as variant 0
             sv.fn = propagate_step_kernel<8, 4, kWalk, true>;
             sv.trace = trace_kernel<true, 6, 12, 4, 32>;
+            sv.trace_gather = trace_kernel<true, 6, 12, 4, 32, true>;
             sv.shade = shade_kernel<3>;
             sv.tail = propagate_tail_kernel<kTailWaves>;
             sv.tail_group = 8;
@@ -4041,6 +4046,7 @@ static StepVariant select_step_variant(const chr_geometry *g) {
         default:   // 0, 7, 8
             sv.fn = propagate_step_kernel<8, 4, kWalk>;
             sv.trace = trace_kernel<false, 6, 12, 4, 48>;
+            sv.trace_gather = trace_kernel<false, 6, 12, 4, 48, true>;
             sv.shade = shade_kernel<3>;
             sv.tail = propagate_tail_kernel<kTailWaves>;
             sv.tail_group = 8;
@@ -4324,7 +4330,8 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
             if (int rc = walk_stack_get((size_t)WIDE_STACK * blocks * tb * sizeof(uint2), &ta.spill, sc ? sc->ctx : 0))
                 return rc;
             if (evt0) CHR_HIP_CHECK(hipEventRecord(evt0, stream));
-            hipLaunchKernelGGL(sv.trace, dim3(blocks), dim3(tb), 0, stream, (const DevGeom *)g->d_dev, ta);
+            hipLaunchKernelGGL(ta.rays ? sv.trace : sv.trace_gather, dim3(blocks), dim3(tb), 0, stream,
+                               (const DevGeom *)g->d_dev, ta);
             if (evt1) CHR_HIP_CHECK(hipEventRecord(evt1, stream));
         }
         if (!rest) {
