@@ -898,14 +898,16 @@ __device__ CHR_COLD void wireplanes(const DevGeom &g, const Photon &p, float bes
 // hit distance on entry.  REC: mesh_triangle is a wide-BVH triangle record
 // (what the wide walks return: triangle id and vertices read from it); else a
 // triangle id of the reference walk (the 48-byte reference records).
-template <bool REC>
+// WIRES = false: instantiated for geometries without analytic wire planes (the
+// FP64 wire-plane code is then not part of the kernel at all)
+template <bool REC, bool WIRES = true>
 __device__ __forceinline__ void finish_fill(const DevGeom &g, State &s, Photon &p, int mesh_triangle) {
     int m1, m2;
     bool use_analytic = false;
     int a_surface = -1, a_inner = -1, a_outer = -1;
     V3 a_normal_raw = v3(0.0f, 0.0f, 0.0f);
     float a_dot_raw = 0.0f, a_distance = 1e30f;
-    if (g.nwireplanes > 0) {
+    if (WIRES && g.nwireplanes > 0) {
         const float best_distance = (mesh_triangle == -1) ? 1e30f : s.distance;
         wireplanes(g, p, best_distance, a_surface, a_inner, a_outer, a_normal_raw, a_dot_raw, a_distance);
         if (a_surface >= 0) use_analytic = ((double)a_distance + 1e-12 < (double)best_distance);
@@ -1697,7 +1699,7 @@ __device__ __forceinline__ void fetch_queued(const PropagateArgs &a, uint32_t q,
 // peeled, so every path into the loop has the write-back behind the prefetch: the
 // prefetch is waited for at the physics' join, before the stores, and nothing waits
 // for the stores.
-template <int MINW>
+template <int MINW, bool WIRES = true>
 __global__ __launch_bounds__(BLOCK, MINW) void shade_kernel(const DevGeom *__restrict__ gdev, PropagateArgs a,
                                                             uint32_t cap) {
     if (a.mode && *a.mode != a.want) return;
@@ -1742,7 +1744,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void shade_kernel(const DevGeom *__res
                 s.distance = __int_as_float(cur.hit.y);
                 pf.tick(P_FILL);
                 pf.call(P_FILL);
-                finish_fill<true>(g, s, p, tri);
+                finish_fill<true, WIRES>(g, s, p, tri);
                 pf.tick(P_PHYS);
                 if (p.last_hit != -1) {
                     pf.call(P_PHYS);
@@ -2776,7 +2778,7 @@ struct LongProf<true> {
 };
 #endif
 
-template <int MINW>
+template <int MINW, bool WIRES = true>
 __global__ __launch_bounds__(BLOCK, MINW) void propagate_tail_kernel(const DevGeom *__restrict__ gdev, PropagateArgs a,
                                                                      uint32_t cap) {
     __shared__ uint32_t stacks[(BLOCK / 8) * TAIL_STACK * 2];
@@ -3003,7 +3005,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_tail_kernel(const DevGe
             }
             lpf.mark(LP_WALK);
             s.distance = dist;
-            finish_fill<true>(g, s, p, tri);
+            finish_fill<true, WIRES>(g, s, p, tri);
             lpf.mark(LP_FILL);
             bool stop = p.last_hit == -1;
             if (!stop) {
@@ -4021,6 +4023,7 @@ static constexpr uint32_t kBinFirstMin = 1u << 20;
 static StepVariant select_step_variant(const chr_geometry *g) {
     const char *e = getenv("CHR_PROPAGATE_VARIANT");
     int v = e ? atoi(e) : 0;
+    const bool wires = g->dev.nwireplanes > 0;   // shade / tail without the wire-plane code otherwise
     StepVariant sv;
     if (g->dev.nwnodes == 0 || v == kExactVariant) {
         sv.fn = propagate_step_kernel<8, 4, 0>;
@@ -4038,8 +4041,8 @@ static StepVariant select_step_variant(const chr_geometry *g) {
             sv.fn = propagate_step_kernel<8, 4, kWalk, true>;
             sv.trace = trace_kernel<true, 6, 12, 4, 32>;
             sv.trace_gather = trace_kernel<true, 6, 12, 4, 32, true>;
-            sv.shade = shade_kernel<3>;
-            sv.tail = propagate_tail_kernel<kTailWaves>;
+            sv.shade = wires ? shade_kernel<3> : shade_kernel<3, false>;
+            sv.tail = wires ? propagate_tail_kernel<kTailWaves> : propagate_tail_kernel<kTailWaves, false>;
             sv.tail_group = 8;
             sv.binned = 2;
             break;
@@ -4047,8 +4050,8 @@ static StepVariant select_step_variant(const chr_geometry *g) {
             sv.fn = propagate_step_kernel<8, 4, kWalk>;
             sv.trace = trace_kernel<false, 6, 12, 4, 48>;
             sv.trace_gather = trace_kernel<false, 6, 12, 4, 48, true>;
-            sv.shade = shade_kernel<3>;
-            sv.tail = propagate_tail_kernel<kTailWaves>;
+            sv.shade = wires ? shade_kernel<3> : shade_kernel<3, false>;
+            sv.tail = wires ? propagate_tail_kernel<kTailWaves> : propagate_tail_kernel<kTailWaves, false>;
             sv.tail_group = 8;
             sv.binned = v == 7 ? 1 : (v == 8 ? 0 : 2);
             break;

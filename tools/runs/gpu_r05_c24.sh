@@ -1,0 +1,10 @@
+# shade / tail kernels without the wire-plane code for geometries without wire planes: tests, library A/B
+set -u
+R=${GRAFT_REPO_ROOT}
+O=$R/gpurun_out/r05_c24
+mkdir -p $O
+cd $R
+timeout -k 10 900 python -u -m pytest tests/test_gpu_batches.py tests/test_gpu_parity.py tests/test_gpu_configs.py -m gpu -x -q --timeout 600 --timeout-method thread > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
+tail -1 $O/pytest.log
+bash tools/gpu_ab_libs.sh r05_ab_wires_libs 3 "--steps 20 --warmup 5" base=chroma-lite_amd/chroma/_lib/ab/base.so wires=chroma-lite_amd/chroma/_lib/ab/wires.so || exit 1
+bash tools/gpu_ab_libs.sh r05_ab_wires_libs_c5 2 "--steps 20 --warmup 5 --detector scint" base=chroma-lite_amd/chroma/_lib/ab/base.so wires=chroma-lite_amd/chroma/_lib/ab/wires.so || exit 1
