@@ -224,6 +224,57 @@ def _native_host_threads():
     return _native.host_threads()
 
 
+# Host memory one rank holds (GB), measured on MI355X boxes (profiles/r05: 29k rank 0
+# peaks at 63.6 GB with a cold geometry build plus the oracle's parity sample, a rank
+# loading geometry and traversal BVH from the node-local cache holds 24.6-25.1 GB):
+# (rank 0: build + oracle checks, any other rank: cache load + device upload)
+HOST_GB_PER_RANK = {'29k': (64.0, 26.0), 'demo': (28.0, 11.0), 'scint': (28.0, 11.0), 'tiny': (3.0, 2.0),
+                    'small': (2.0, 1.0)}
+
+
+def host_memory_available():
+    """Bytes of host memory this job can still take: MemAvailable, capped by the
+    cgroup limit (memory.max - memory.current) when one is set.
+    CHROMA_BENCH_MEMAVAILABLE_GB overrides (tests)."""
+    o = os.environ.get('CHROMA_BENCH_MEMAVAILABLE_GB')
+    if o:
+        return float(o) * 1e9
+    avail = None
+    try:
+        with open('/proc/meminfo') as f:
+            for line in f:
+                if line.startswith('MemAvailable:'):
+                    avail = int(line.split()[1]) * 1024.0
+    except (OSError, ValueError):
+        pass
+    try:
+        with open('/sys/fs/cgroup/memory.max') as f:
+            lim = f.read().strip()
+        if lim != 'max':
+            with open('/sys/fs/cgroup/memory.current') as f:
+                room = float(int(lim) - int(f.read().strip()))
+            avail = room if avail is None else min(avail, room)
+    except (OSError, ValueError):
+        pass
+    return avail
+
+
+def preflight_host_memory(detector, local_world, avail=None):
+    """Does this node's host memory hold every local rank of the job?  Rank 0
+    builds (or loads) the geometry and runs the oracle checks, every other rank
+    loads the geometry from the node-local cache and keeps its host copy.
+    Returns the record the line carries (detail.preflight); 'fits' False means
+    the run is refused before any rank allocates (an out-of-memory kill of 8
+    ranks mid-setup would say nothing)."""
+    first, other = HOST_GB_PER_RANK.get(detector, (0.0, 0.0))
+    need = (first + other * max(0, local_world - 1)) * 1e9
+    avail = host_memory_available() if avail is None else avail
+    return {'local_ranks': local_world, 'need_gb': round(need / 1e9, 1),
+            'per_rank_gb': {'rank0': first, 'other': other},
+            'available_gb': None if avail is None else round(avail / 1e9, 1),
+            'fits': avail is None or need <= avail}
+
+
 def rng_first_subsequence(rank, nslots):
     """Rank r's RNG slots are curand subsequences [r*nslots, (r+1)*nslots):
     disjoint streams, and rank 0 draws what a single-GPU run draws."""
@@ -282,14 +333,91 @@ def _allreduce(dist, x, op):
     return float(t.item())
 
 
+FLOAT_RTOL = 1e-5
+PARITY_RULE = ('flags, last-hit triangles, channels bit-exact; |gpu - oracle| <= 1e-5 * max(|oracle|, 1) per '
+               'component for pos (mm), dir, pol, 1e-5 * |oracle| for t and wavelengths (BASELINE north_star, '
+               'tests/test_gpu_configs_full.py)')
+
+
+def photon_record(i, batches, gf, hf, gl, hl):
+    """Where photon i of a parity sample sits (batch, index in it) and its
+    discrete outcome on both sides."""
+    b = int(np.searchsorted(np.cumsum(batches), i, side='right'))
+    return {'index': int(i), 'batch': b, 'index_in_batch': int(i - sum(batches[:b])),
+            'flags_gpu': int(gf[i]), 'flags_oracle': int(hf[i]),
+            'last_hit_gpu': int(gl[i]), 'last_hit_oracle': int(hl[i])}
+
+
+def float_contract(a, b, field, batches, gf, hf, gl, hl):
+    """The float parity rule for one photon field (PARITY_RULE): violation count,
+    largest absolute difference, and the worst photon (largest |a-b| / tolerance)
+    with its values, flags and last hit."""
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    floor = 1.0 if field in ('pos', 'dir', 'pol') else 0.0
+    tol = FLOAT_RTOL * np.maximum(np.abs(b), floor)
+    diff = np.abs(a - b)
+    with np.errstate(divide='ignore', invalid='ignore'):
+        ratio = np.where(diff == 0, 0.0, np.where(tol > 0, diff / np.where(tol > 0, tol, 1.0), np.inf))
+    ratio = np.where(np.isnan(a) & np.isnan(b), 0.0, np.where(np.isnan(ratio), np.inf, ratio))
+    if ratio.ndim > 1:
+        per_photon = ratio.max(axis=1)
+        dmax = diff.max(axis=1)
+    else:
+        per_photon, dmax = ratio, diff
+    out = {'violations': int(np.count_nonzero(per_photon > 1.0)), 'differing': int(np.count_nonzero(dmax > 0)),
+           'max_abs': float(np.nanmax(dmax)) if dmax.size else 0.0}
+    if dmax.size and out['differing']:
+        i = int(np.argmax(per_photon))
+        rec = photon_record(i, batches, gf, hf, gl, hl)
+        rec.update({'gpu': np.atleast_1d(a[i]).tolist(), 'oracle': np.atleast_1d(b[i]).tolist(),
+                    'abs_diff': np.atleast_1d(diff[i]).tolist(), 'over_tolerance': float(per_photon[i])})
+        out['worst'] = rec
+        out['differing_sample'] = [int(j) for j in np.flatnonzero(dmax > 0)[:16]]
+    return out
+
+
+REFERENCE_GEOMETRY_KEYS = {'29k': 'detector_29k', 'demo': 'demo_detector'}
+
+
+def geometry_md5_check(name, det, detail):
+    """The bench geometry against the reference generator's own build
+    (tests/golden/reference_hashes.json, written by make_golden_geometry.py in
+    the build container): True / False, or None when no record exists for this
+    detector (or the workload has no host geometry).  The hashes go to
+    detail.geometry_hashes."""
+    key = REFERENCE_GEOMETRY_KEYS.get(name)
+    if key is None or det is None or not hasattr(det, 'mesh'):
+        return None
+    with open(os.path.join(ROOT, 'tests', 'golden', 'reference_hashes.json')) as f:
+        want = json.load(f).get(key)
+    if want is None:
+        return None
+    from chroma.demo import geometry_hashes
+    t0 = time.time()
+    got = geometry_hashes(det)
+    fields = sorted(k for k in got if k in want)
+    detail['geometry_hashes'] = {'reference_record': 'tests/golden/reference_hashes.json[%s]' % key,
+                                 'fields': fields, 'differ': [k for k in fields if got[k] != want[k]],
+                                 'seconds': round(time.time() - t0, 1)}
+    return not detail['geometry_hashes']['differ']
+
+
 def result_line(args, world, elapsed, per_step_s, total_photons, detector_info, detail):
     value = total_photons / elapsed
-    workload = ('GPUPhotons.propagate of %s isotropic photons per step on %s, max_steps=%d, launch shape %dx%d '
-                '(%d RNG slots)' % (
-                    ('%d in total over %d GPUs' % (args.total_photons, world)) if args.total_photons
-                    else ('%d per GPU' % args.photons), DETECTORS[args.detector][0], args.max_steps,
-                    args.nthreads_per_block, args.max_blocks, args.nthreads_per_block * args.max_blocks))
-    cfg = {'workload': workload, 'detector': args.detector, 'max_steps': args.max_steps,
+    group = detail.get('pipelined_steps_per_call', 1)
+    if args.pipeline and group > 1:
+        call = ('chroma.gpu.propagate_batches (the call Simulation.simulate makes) of %d batches per call, '
+                'each batch one GPUPhotons.propagate-equivalent of' % group)
+    else:
+        call = 'one GPUPhotons.propagate call per step of'
+    workload = ('%s %s isotropic photons on %s, max_steps=%d, launch shape %dx%d (%d RNG slots)' % (
+        call, ('%d in total over %d GPUs' % (args.total_photons, world)) if args.total_photons
+        else ('%d per GPU' % args.photons), DETECTORS[args.detector][0], args.max_steps,
+        args.nthreads_per_block, args.max_blocks, args.nthreads_per_block * args.max_blocks))
+    cfg = {'workload': workload, 'timed_call': 'propagate_batches' if (args.pipeline and group > 1) else 'propagate',
+           'batches_per_call': group if args.pipeline else 1,
+           'detector': args.detector, 'max_steps': args.max_steps,
            'parallelism': 'photon-sharded x%d, geometry replicated' % world}
     if args.total_photons:
         cfg['total_photons'] = args.total_photons
@@ -302,6 +430,9 @@ def result_line(args, world, elapsed, per_step_s, total_photons, detector_info, 
         'vs_baseline': (value / PUBLISHED_29K) if args.detector == '29k' else None,
         'dtype': 'f32', 'data': 'synthetic isotropic point source (BASELINE.md section 3), seed %d+rank' % PHOTON_SEED,
         'config': dict(cfg, **detector_info),
+        'value_propagate_per_call': value if not args.pipeline else (detail.get('sequential') or {}).get('photons_per_s'),
+        'value_propagate_per_call_note': 'one GPUPhotons.propagate call per step (the reference caller\'s loop, '
+                                         'its multi-step tail not overlapped): detail.sequential',
         'detail': dict({'step_ms': [round(1e3 * s, 3) for s in per_step_s]}, **detail),
         'roofline': None, 'cpu_baseline': None, 'parity': None,
     }
@@ -603,11 +734,13 @@ class PropagateWorkload(object):
         """Oracle (plain C port of the reference kernel, OpenMP) on a bounded
         sample of the same workload (grown until it takes ~budget/4 .. budget/2
         seconds); also returns the oracle's photons (the parity reference) and
-        its walk counts on the reference BVH (roofline bytes)."""
-        n = 4000
+        its walk counts on the reference BVH (roofline bytes).  --parity-photons
+        fixes the sample instead (reproducible: the line records n either way)."""
+        fixed = getattr(self.args, 'parity_photons', 0)
+        n = min(self.nphotons, fixed) if fixed else 4000
         while True:
             hosts, stats, dt = self._oracle_batches(n, threads)
-            if dt > budget_s / 4 or n * 4 > self.nphotons:
+            if fixed or dt > budget_s / 4 or n * 4 > self.nphotons:
                 break
             n = int(min(self.nphotons, n * max(2.0, min(8.0, (budget_s / 2) / max(dt, 1e-3)))))
         cpu = dict(value=n / dt, unit='photons/s', cores=threads, kind='port',
@@ -680,15 +813,26 @@ class PropagateWorkload(object):
         ch_gpu, ch_ref = channel(gf, gl), channel(hf, hl)
         rel = max(max_rel(got[f], cat(hosts, f)) for f in ('pos', 't', 'wavelengths'))
         dp = max(float(np.max(np.abs(got[f] - cat(hosts, f)))) if n else 0.0 for f in ('dir', 'pol'))
-        return {'rank': rank, 'n': int(n), 'batches': sample['batches'], 'path': sample['path'],
-                'rng_first_subsequence': rng_first_subsequence(rank, self.nslots),
-                'photon_seed': PHOTON_SEED + rank,
-                'flags_equal': bool(np.array_equal(gf, hf)), 'last_hit_equal': bool(np.array_equal(gl, hl)),
-                'channel_equal': bool(np.array_equal(ch_gpu, ch_ref)),
-                'flags_mismatches': int(np.count_nonzero(gf != hf)),
-                'detected': int(np.count_nonzero(ch_ref >= 0)), 'max_rel': rel, 'dir_pol_max_abs': dp,
-                'binned_first_step': bool(n // 2 >= (1 << 20)),
-                'stack_overflows': sample['stack_overflows'], 'oracle_on_rank': self.rank}
+        floats = {f: float_contract(got[f], cat(hosts, f), f, sample['batches'], gf, hf, gl, hl)
+                  for f in ('pos', 'dir', 'pol', 't', 'wavelengths')}
+        out = {'rank': rank, 'n': int(n), 'batches': sample['batches'], 'path': sample['path'],
+               'rng_first_subsequence': rng_first_subsequence(rank, self.nslots),
+               'photon_seed': PHOTON_SEED + rank,
+               'flags_equal': bool(np.array_equal(gf, hf)), 'last_hit_equal': bool(np.array_equal(gl, hl)),
+               'channel_equal': bool(np.array_equal(ch_gpu, ch_ref)),
+               'flags_mismatches': int(np.count_nonzero(gf != hf)),
+               'last_hit_mismatches': int(np.count_nonzero(gl != hl)),
+               'detected': int(np.count_nonzero(ch_ref >= 0)), 'max_rel': rel, 'dir_pol_max_abs': dp,
+               'rule': PARITY_RULE, 'floats': floats,
+               'bit_identical': bool(all(v['max_abs'] == 0.0 for v in floats.values())),
+               'binned_first_step': bool(n // 2 >= (1 << 20)),
+               'stack_overflows': sample['stack_overflows'], 'oracle_on_rank': self.rank}
+        bad = np.flatnonzero((gf != hf) | (gl != hl))
+        if bad.size:
+            out['first_discrete_mismatches'] = [photon_record(i, sample['batches'], gf, hf, gl, hl) for i in bad[:8]]
+        out['ok'] = bool(out['flags_equal'] and out['last_hit_equal'] and out['channel_equal'] and
+                         all(v['violations'] == 0 for v in floats.values()))
+        return out
 
     def check(self, full, budget_s, threads, sample):
         """Rank 0 (full): cpu_baseline + parity on the adaptive sample.  Otherwise
@@ -728,6 +872,13 @@ def parse_args(argv=None):
     ap.add_argument('--max-blocks', type=int, default=1024)
     ap.add_argument('--seed', type=int, default=1)
     ap.add_argument('--cpu-budget', type=float, default=20.0, help='seconds of CPU-baseline work')
+    ap.add_argument('--parity-photons', type=int, default=0,
+                    help='rank 0: a fixed parity / cpu_baseline sample of this many photons (0: grown to '
+                         '~--cpu-budget/4 .. /2 seconds of oracle work; the line records the n used)')
+    ap.add_argument('--no-preflight', action='store_true',
+                    help='run even when the host-memory pre-flight says the local ranks do not fit')
+    ap.add_argument('--allow-parity-failure', action='store_true',
+                    help='exit 0 even when the parity check fails (diagnostic runs)')
     ap.add_argument('--rank-parity-photons', type=int, default=1 << 17,
                     help='photons of its own shard each rank > 0 checks against the oracle')
     ap.add_argument('--no-cpu-baseline', action='store_true', help='also skips the parity check')
@@ -814,6 +965,19 @@ def run_rank(args):
     # libchroma_amd's host-side builds use this rank's share of the job's cores
     # (the box's cgroup quota, not nproc), not a full team per rank
     local_world = int(os.environ.get('LOCAL_WORLD_SIZE', str(world)))
+    preflight = preflight_host_memory(args.detector, local_world)
+    if world > 1:
+        # one decision for the whole job (local rank 0's view of the node), taken before
+        # any rank allocates its geometry
+        box = [preflight]
+        dist.broadcast_object_list(box, src=0)
+        preflight = box[0]
+    if not preflight['fits'] and not args.no_preflight:
+        raise SystemExit('bench.py: host memory pre-flight refused the run: %d local ranks of the %s detector need '
+                         '~%.0f GB of host memory (rank 0 %.0f GB, each other rank %.0f GB) and %.0f GB is available '
+                         '(--no-preflight to run anyway)' % (
+                             local_world, args.detector, preflight['need_gb'], preflight['per_rank_gb']['rank0'],
+                             preflight['per_rank_gb']['other'], preflight['available_gb']))
     from chroma.gpu import _native
     _native.set_host_threads(max(1, usable_cpus() // max(1, local_world)))
     wl = WORKLOAD(args, rank, world, local, dist, nphotons)
@@ -889,10 +1053,11 @@ def run_rank(args):
     else:
         reports = [report]
 
+    rc = 0
     if rank == 0:
         steps = max(1, args.steps)
         r0 = reports[0]
-        detail = {'pipelined_steps_per_call': wl.group, 'warmup_steps_run': warmup,
+        detail = {'pipelined_steps_per_call': wl.group, 'warmup_steps_run': warmup, 'preflight': preflight,
                   # the timed steps' input batches were filled before t0 (timed_loop's prepare;
                   # bench.py since 40b6d98) rather than restored inside the timed region
                   'inputs_prefilled': getattr(wl, 'prepare', None) is not None and wl.group >= args.steps,
@@ -932,14 +1097,20 @@ def run_rank(args):
                 parity['per_rank'] = per_rank
                 parity['all_ranks_equal'] = all(p is not None and p['flags_equal'] and p['last_hit_equal'] and
                                                 p['channel_equal'] for p in parity['per_rank'])
+            parity['ok'] = bool(par['ok'] and all(p is not None and p['ok'] for p in per_rank))
             result['parity'] = parity
             if r0['trace_launches']:
                 result['roofline'] = roofline(args, reports, ostats)
+        result['geometry_md5_match'] = geometry_md5_check(args.detector, getattr(wl, 'det', None), detail)
         print(json.dumps(result), flush=True)
+        if check is not None and not result['parity']['ok']:
+            log('bench.py: PARITY FAILED against the oracle (parity.ok false; parity.floats / '
+                'first_discrete_mismatches name the photons)')
+            rc = 0 if args.allow_parity_failure else 3
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
-    return 0
+    return rc
 
 
 def main(argv=None):

@@ -49,3 +49,22 @@ def detector(pmt_radius=14000.0, sphere_radius=14500.0, spiral_step=350.0):
 
 def tiny():
     return detector(2000.0, 2500.0, 700.0)
+
+
+def geometry_hashes(det):
+    """Counts and MD5s of a flattened detector: vertices (float32 bytes),
+    triangles, solid_id and solid_id_to_channel_index (as int64) -- the record
+    tests/golden/make_golden_geometry.py writes from the reference's own build
+    (reference_hashes.json 'demo_detector' / 'detector_29k'), so a benchmark
+    geometry is checked against the reference's generator."""
+    import hashlib
+
+    def md5(a):
+        return hashlib.md5(np.ascontiguousarray(a).tobytes()).hexdigest()
+    det.flatten()
+    return {'channels': int(det.num_channels()), 'triangles': int(len(det.mesh.triangles)),
+            'vertices': int(len(det.mesh.vertices)),
+            'md5_vertices': md5(np.asarray(det.mesh.vertices, np.float32)),
+            'md5_triangles': md5(np.asarray(det.mesh.triangles).astype(np.int64)),
+            'md5_solid_id': md5(np.asarray(det.solid_id).astype(np.int64)),
+            'md5_solid_id_to_channel_index': md5(np.asarray(det.solid_id_to_channel_index).astype(np.int64))}

@@ -6,7 +6,8 @@ objects of the N>1 line -- runs on CPU with gloo (tests/test_bench_dist.py).
 Test infrastructure only: the stand-in propagates nothing and the line it
 prints is not a measurement.
 
-STUB_FAIL_RANK=r makes rank r exit with status 3 after the process group is up.
+STUB_FAIL_RANK=r makes rank r exit with status 3 after the process group is up;
+STUB_PARITY_FAIL_RANK=r makes rank r's parity check fail.
 """
 import os
 import sys
@@ -87,7 +88,8 @@ class StubWorkload(object):
         return {'triangles': 0, 'bvh_nodes': 0, 'channels': 4}
 
     def _parity(self, rank, n, full, threads):
-        return {'rank': rank, 'n': n, 'flags_equal': True, 'last_hit_equal': True, 'channel_equal': True,
+        ok = os.environ.get('STUB_PARITY_FAIL_RANK') != str(rank)
+        return {'rank': rank, 'n': n, 'flags_equal': ok, 'last_hit_equal': True, 'channel_equal': True, 'ok': ok,
                 'threads': threads, 'full': full, 'oracle_on_rank': self.rank,
                 'rng_first_subsequence': bench.rng_first_subsequence(rank, self.args.nthreads_per_block *
                                                                      self.args.max_blocks)}

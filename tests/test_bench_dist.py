@@ -191,3 +191,71 @@ def test_bench_failed_rank_fails_the_run():
 def test_bench_world_size_mismatch_is_refused():
     rc, line, err = _stub_bench(['--gpus', '4', '--steps', '1', '--detector', 'small'], {'WORLD_SIZE': '1'})
     assert rc != 0 and line is None and 'WORLD_SIZE=1' in err
+
+
+def test_bench_parity_failure_exits_nonzero():
+    """A parity check that fails (here rank 1's sample, checked by rank 0's
+    oracle) still prints the line -- parity.ok false, the failing rank named --
+    and the run exits non-zero (the bench enforces the
+    contract instead of only reporting it)."""
+    rc, line, err = _stub_bench(['--gpus', '2', '--steps', '2', '--warmup', '1', '--photons', '1000',
+                                 '--sequential-steps', '0', '--detector', 'small'], {'STUB_PARITY_FAIL_RANK': '1'})
+    assert rc != 0 and 'PARITY FAILED' in err
+    assert line is not None and line['parity']['ok'] is False
+    assert [p['ok'] for p in line['parity']['per_rank']] == [True, False]
+    rc, line, err = _stub_bench(['--gpus', '2', '--steps', '2', '--warmup', '1', '--photons', '1000',
+                                 '--sequential-steps', '0', '--detector', 'small', '--allow-parity-failure'],
+                                {'STUB_PARITY_FAIL_RANK': '1'})
+    assert rc == 0 and line['parity']['ok'] is False
+
+
+def test_bench_host_memory_preflight():
+    """The first 8-GPU run fails loudly rather than by an out-of-memory kill
+    (VERDICT r05 item 7): 8 ranks of the 29k detector need ~64 GB on rank 0
+    (cold build + oracle) and ~26 GB on each other rank; with 150 GB available
+    the run is refused before any rank builds geometry, with the numbers in the
+    message.  A job that fits carries the pre-flight record in the line."""
+    sys.path.insert(0, ROOT)
+    import bench
+    pf = bench.preflight_host_memory('29k', 8, avail=150e9)
+    assert not pf['fits'] and pf['need_gb'] == 64.0 + 7 * 26.0
+    assert bench.preflight_host_memory('29k', 8, avail=300e9)['fits']
+    assert bench.preflight_host_memory('29k', 1, avail=70e9)['fits']
+    rc, line, err = _stub_bench(['--gpus', '8', '--steps', '1', '--detector', '29k'],
+                                {'CHROMA_BENCH_MEMAVAILABLE_GB': '150'}, timeout=300)
+    assert rc != 0 and line is None
+    assert 'pre-flight refused' in err and '246 GB' in err and '150 GB' in err
+    rc, line, err = _stub_bench(['--gpus', '2', '--steps', '1', '--warmup', '0', '--photons', '1000',
+                                 '--sequential-steps', '0', '--detector', 'small'],
+                                {'CHROMA_BENCH_MEMAVAILABLE_GB': '150'})
+    assert rc == 0, err
+    pf = line['detail']['preflight']
+    assert pf['fits'] and pf['local_ranks'] == 2 and pf['need_gb'] == 3.0 and pf['available_gb'] == 150.0
+
+
+def test_bench_float_parity_rule():
+    """bench.py's float contract (PARITY_RULE): pos within 1e-5 * max(|oracle|, 1 mm),
+    t / wavelengths within 1e-5 * |oracle|; the worst photon is named with its batch,
+    values, flags and last hit."""
+    sys.path.insert(0, ROOT)
+    import bench
+    n = 10
+    gf = hf = np.full(n, 4, np.uint32)
+    gl = hl = np.arange(n, dtype=np.int32)
+    want = np.zeros((n, 3), np.float32)
+    want[:, 0] = 0.3
+    got = want.copy()
+    got[2, 0] += 1e-6                  # 3e-6 relative, but far below 1e-5 * 1 mm
+    r = bench.float_contract(got, want, 'pos', [5, 5], gf, hf, gl, hl)
+    assert r['violations'] == 0 and r['differing'] == 1 and r['worst']['index'] == 2
+    got[7, 1] = 2e-5                   # 2e-5 mm off a coordinate 0: beyond 1e-5 mm
+    r = bench.float_contract(got, want, 'pos', [5, 5], gf, hf, gl, hl)
+    assert r['violations'] == 1 and r['worst']['index'] == 7 and r['worst']['batch'] == 1
+    assert r['worst']['index_in_batch'] == 2 and r['worst']['over_tolerance'] > 1.0
+    t = np.linspace(1.0, 2.0, n)
+    t2 = t.copy()
+    t2[4] *= 1 + 2e-5
+    r = bench.float_contract(t2, t, 't', [5, 5], gf, hf, gl, hl)
+    assert r['violations'] == 1 and r['worst']['index'] == 4 and r['worst']['last_hit_oracle'] == 4
+    r = bench.float_contract(t, t, 't', [5, 5], gf, hf, gl, hl)
+    assert r == {'violations': 0, 'differing': 0, 'max_abs': 0.0}

@@ -5,6 +5,7 @@ import json
 import os
 
 import numpy as np
+import pytest
 
 from conftest import GOLDEN
 
@@ -131,3 +132,18 @@ def test_native_vertex_unique_equals_numpy():
     nan = v.copy()
     nan[5, 1] = np.nan
     assert geometry._native_unique(nan) is None
+
+
+@pytest.mark.parametrize('key,kw', [('demo_detector', {}),
+                                    ('detector_29k', dict(pmt_radius=23780.0, sphere_radius=24280.0))])
+def test_benchmark_geometry_matches_reference_generator(key, kw):
+    """The bench geometries (C3 demo.detector() and the 29k-PMT headline
+    detector) are the reference generator's bit for bit: MD5 of vertices,
+    triangles, solid_id and solid_id_to_channel_index against the record
+    tests/golden/make_golden_geometry.py wrote by building them with the
+    reference's own chroma.demo / Geometry.flatten."""
+    from chroma import demo
+    want = json.load(open(os.path.join(GOLDEN, 'reference_hashes.json')))[key]
+    assert want['params'] == kw
+    got = demo.geometry_hashes(demo.detector(**kw))
+    assert {k: got[k] for k in got} == {k: want[k] for k in got}
