@@ -340,6 +340,12 @@ class Cache(object):
         bvh_dir = self.get_bvh_directory(mesh_hash)
         verify_or_create_dir(bvh_dir, exception_msg='Non-directory already exists where BVH directory should go: '
                                                     + bvh_dir)
+        # the traversal BVHs derived from the BVH this one replaces go with it (their
+        # fingerprint would refuse them anyway)
+        wide_dir = self.get_bvh_filename(mesh_hash, name) + '.wide'
+        if os.path.isdir(wide_dir):
+            import shutil
+            shutil.rmtree(wide_dir, ignore_errors=True)
         _write_npz(self.get_bvh_filename(mesh_hash, name),
                    {'nodes': bvh.nodes, 'layer_offsets': np.asarray(bvh.layer_offsets, dtype=np.int64),
                     'world_origin': np.asarray(bvh.world_coords.world_origin),

@@ -34,8 +34,22 @@ class GPUGeometry(object):
         wide, source = wide_bvh.obtain(geometry.bvh, self.packed)
         t2 = time.time()
         handle = ctypes.c_void_p()
-        _native.call('chr_geometry_create_wide', ctypes.byref(self.packed.desc()), ctypes.byref(wide.desc()),
-                     ctypes.byref(handle))
+        try:
+            _native.call('chr_geometry_create_wide', ctypes.byref(self.packed.desc()), ctypes.byref(wide.desc()),
+                         ctypes.byref(handle))
+        except _native.NativeError as e:
+            if source != 'cache':
+                raise
+            # a cache entry the upload's validation refuses: drop it and build the
+            # traversal BVH again, once, instead of failing every run
+            # until someone deletes the entry
+            logger.warning('traversal BVH from %s refused by the upload (%s): rebuilding', source, e)
+            wide_bvh.discard(geometry.bvh)
+            wide, source = wide_bvh.obtain(geometry.bvh, self.packed, fresh=True)
+            source = 'rebuilt'
+            t2 = time.time()
+            _native.call('chr_geometry_create_wide', ctypes.byref(self.packed.desc()), ctypes.byref(wide.desc()),
+                         ctypes.byref(handle))
         self._handle = handle
         self.geometry = geometry
         self.solid_id_map = ga.to_gpu(np.asarray(geometry.solid_id, dtype=np.uint32))

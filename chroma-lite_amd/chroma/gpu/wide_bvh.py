@@ -16,7 +16,8 @@ Cache layout, next to the reference BVH it was built from:
 ``<cache_dir>/bvh/<mesh md5>/<bvh name>.wide/<builder key>/`` holding
 ``nodes.npy rec_id.npy rec_rank.npy meta.json`` (plain .npy files,
 memory-mapped on load, read with allow_pickle=False).  ``meta.json`` records
-a fingerprint of the reference BVH; a mismatch means rebuild.
+a fingerprint of the reference BVH (a hash of its whole node array); a
+mismatch means rebuild, and so do arrays of the wrong type or shape.
 ``$CHROMA_WIDE_CACHE=0`` turns the cache off.
 """
 import ctypes
@@ -42,19 +43,23 @@ def builder_key():
 
 
 def fingerprint(bvh):
-    """A cheap identity of a reference BVH: node count, world coordinates and a
-    hash of <= 65,536 nodes sampled at a fixed stride (plus the last node)."""
+    """The identity of a reference BVH: node count, world coordinates and a
+    hash of every node (xxh3-128, ~0.3 s for the 29k detector's 3.8 GB of
+    nodes; sha1 when xxhash is not importable).  A BVH rebuilt under the same
+    name that differs in any node never reuses the traversal BVH built from
+    the old one."""
     u = np.ascontiguousarray(bvh.nodes).view(np.uint32).reshape(-1, 4)
-    n = len(u)
-    h = hashlib.sha1()
-    h.update(np.asarray([n], np.int64).tobytes())
+    try:
+        import xxhash
+        h, tag = xxhash.xxh3_128(), 'xxh3:'
+    except ImportError:
+        h, tag = hashlib.sha1(), 'sha1:'
+    h.update(np.asarray([len(u)], np.int64).tobytes())
     h.update(np.asarray(bvh.world_coords.world_origin, np.float32).tobytes())
     h.update(np.asarray([bvh.world_coords.world_scale], np.float32).tobytes())
-    if n:
-        stride = max(1, n // 65536)
-        h.update(np.ascontiguousarray(u[::stride]).tobytes())
-        h.update(np.ascontiguousarray(u[-1]).tobytes())
-    return h.hexdigest()
+    if len(u):
+        h.update(memoryview(u).cast('B'))
+    return tag + h.hexdigest()
 
 
 class WideBVH(object):
@@ -129,12 +134,9 @@ def save(wide, cache_dir, mesh_hash, name, fp):
             return
         except OSError:
             pass
-        try:                   # an entry is there: another process's (keep it) or a stale one (replace it)
-            with open(os.path.join(final, 'meta.json')) as f:
-                if json.load(f).get('fingerprint') == fp:
-                    break
-        except (OSError, ValueError):
-            pass
+        # an entry is there: another process's (keep it) or a stale or corrupt one (replace it)
+        if load(cache_dir, mesh_hash, name, wide.key, fp) is not None:
+            break
         shutil.rmtree(final, ignore_errors=True)
     shutil.rmtree(tmp, ignore_errors=True)
 
@@ -158,23 +160,43 @@ def load(cache_dir, mesh_hash, name, key, fp):
     except (OSError, ValueError) as e:
         logger.warning('traversal BVH cache %s unreadable: %s', d, e)
         return None
+    # the C side reads nnodes * 96 node bytes and nrec ids / ranks: arrays of another
+    # type or shape are a corrupt entry, not something to hand it
+    nodes, rid, rrank = arrs['nodes'], arrs['rec_id'], arrs['rec_rank']
+    if (nodes.dtype != np.uint8 or nodes.ndim != 2 or nodes.shape[1] != 96 or rid.dtype != np.uint32 or
+            rrank.dtype != np.uint32 or rid.ndim != 1 or rrank.shape != rid.shape):
+        logger.warning('traversal BVH cache %s: arrays of the wrong type or shape (nodes %s %s, rec_id %s %s, '
+                       'rec_rank %s %s): rebuilding', d, nodes.dtype, nodes.shape, rid.dtype, rid.shape,
+                       rrank.dtype, rrank.shape)
+        return None
     return WideBVH(arrs['nodes'], arrs['rec_id'], arrs['rec_rank'], meta['max_depth'], meta['usable'],
                    meta['leaf_max'], key)
 
 
-def obtain(bvh, packed):
+def discard(bvh):
+    """Forget a traversal BVH that failed validation on upload: the copy
+    attached to the BVH and its cache entry (the next obtain() rebuilds)."""
+    import shutil
+    w = getattr(bvh, 'wide', None)
+    bvh.wide = None
+    ref = getattr(bvh, 'cache_ref', None)
+    if ref and w is not None:
+        shutil.rmtree(directory(ref[0], ref[1], ref[2], w.key), ignore_errors=True)
+
+
+def obtain(bvh, packed, fresh=False):
     """(WideBVH, source) for a geometry's reference BVH: the copy attached to
     the BVH object ('memory'), its cache entry ('cache'), or a fresh host build
-    ('built', then written to the cache when the BVH came from one).  The BVH
-    object carries ``cache_ref = (cache_dir, mesh_hash, name)`` when it was
-    loaded from or saved to a chroma.cache.Cache."""
+    ('built', then written to the cache when the BVH came from one; fresh=True
+    always builds).  The BVH object carries ``cache_ref = (cache_dir, mesh_hash,
+    name)`` when it was loaded from or saved to a chroma.cache.Cache."""
     key = builder_key()
     w = getattr(bvh, 'wide', None)
-    if w is not None and w.key == key:
+    if w is not None and w.key == key and not fresh:
         return w, 'memory'
     ref = getattr(bvh, 'cache_ref', None) if cache_enabled() else None
     fp = fingerprint(bvh) if ref else None
-    if ref:
+    if ref and not fresh:
         w = load(ref[0], ref[1], ref[2], key, fp)
         if w is not None:
             bvh.wide = w

@@ -2436,8 +2436,11 @@ __device__ __forceinline__ int walk_lone(const DevGeom &g, V3 o, V3 d, uint32_t 
 // count up in PB_WSEQ, the tester's progress in PB_TREAD (lists read: the
 // walker may reuse that buffer) and PB_TSEQ (lists tested), the walker's end in
 // PB_WDONE, the tester's in PS_DONE.  Every wait is bounded (PAIR_SPIN_MAX
-// polls): a lost handshake ends the walk with PB_ABORT set and is counted with
-// the stack overflows, never hangs the wave.
+// polls): a lost handshake -- a timed-out wait, an abort, or a tester that did
+// not test every list (PB_TSEQ != lists published) -- is reported to the caller,
+// which walks the ray again alone (walk_lone), and is counted (1 << 20 in the
+// stack-overflow counter); PB_ABORT then stays set and the workgroup pairs no
+// more walks (an abandoned tester may still be reading the box).
 enum : int {
     PB_STATE, PB_IDLE, PB_WORKERS, PB_WSEQ, PB_WDONE, PB_TREAD, PB_TSEQ, PB_BEST, PB_RANK, PB_ID,
     PB_OX, PB_OY, PB_OZ, PB_DX, PB_DY, PB_DZ, PB_LAST, PB_CNT0, PB_CNT1, PB_LISTS, PB_ABORT, PB_WORDS = 24
@@ -2454,8 +2457,8 @@ __device__ __forceinline__ void lds_release() { __builtin_amdgcn_fence(__ATOMIC_
 __device__ __forceinline__ void lds_acquire() { __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup"); }
 // poll until pred() (wave-uniform), at most PAIR_SPIN_MAX times; false on timeout
 template <class P>
-__device__ __forceinline__ bool pair_wait(CHR_LDS uint32_t *box, P pred) {
-    for (uint32_t i = 0; i < PAIR_SPIN_MAX; ++i) {
+__device__ __forceinline__ bool pair_wait(CHR_LDS uint32_t *box, uint32_t spin, P pred) {
+    for (uint32_t i = 0; i < spin; ++i) {
         if (pred()) return true;
         if (lds_ld(box + PB_ABORT)) return false;
         __builtin_amdgcn_s_sleep(1);
@@ -2469,8 +2472,8 @@ __device__ __forceinline__ bool pair_wait(CHR_LDS uint32_t *box, P pred) {
 // The box must have been posted (ray, seed best, PB_LISTS) by this wave.
 template <class M>
 __device__ __forceinline__ int walk_pair_walker(const DevGeom &g, const TopNodes &top, V3 o, V3 d, M stk, int cap,
-                                                CHR_LDS uint32_t *lists, CHR_LDS uint32_t *box, uint32_t &overflow,
-                                                float &min_distance, uint32_t &iters) {
+                                                CHR_LDS uint32_t *lists, CHR_LDS uint32_t *box, uint32_t spin,
+                                                uint32_t &overflow, float &min_distance, uint32_t &iters, bool &lost) {
     constexpr uint32_t INVALID = 0xFFFFFFFFu;
     auto ufl = [](float x) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(x))); };
     auto uu = [](uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); };
@@ -2607,7 +2610,7 @@ __device__ __forceinline__ int walk_pair_walker(const DevGeom &g, const TopNodes
         if (!end) fetch_node(cur == INVALID ? 0u : cur);
         if (Tn) {
             const uint32_t pre = __popcll(b0 & below) + 2u * __popcll(b1 & below) + 4u * __popcll(b2 & below);
-            if (nl >= 2u && ok) ok = pair_wait(box, [&]() { return lds_ld(box + PB_TREAD) + 1u >= nl; });
+            if (nl >= 2u && ok) ok = pair_wait(box, spin, [&]() { return lds_ld(box + PB_TREAD) + 1u >= nl; });
             const int nb = (int)(nl & 1u) * TAIL_TRI;
 #pragma unroll
             for (int i = 0; i < 4; ++i)
@@ -2622,11 +2625,15 @@ __device__ __forceinline__ int walk_pair_walker(const DevGeom &g, const TopNodes
     }
     lds_release();
     lds_st(box + PB_WDONE, nl);
-    if (ok) ok = pair_wait(box, [&]() { return lds_ld(box + PB_STATE) == PS_DONE; });
+    if (ok) ok = pair_wait(box, spin, [&]() { return lds_ld(box + PB_STATE) == PS_DONE; });
     lds_acquire();
+    // the tester's minimum covers every list only if it tested all nl of them and no
+    // side gave up (a tester whose wait timed out also ends with PS_DONE)
+    if (ok) ok = lds_ld(box + PB_TSEQ) == nl && lds_ld(box + PB_ABORT) == 0u;
     const float fbest = __uint_as_float(lds_ld(box + PB_BEST));
     const int best_id = (int)lds_ld(box + PB_ID);
-    if (!ok && lane == 0) overflow += 1u << 20;   // a lost handshake: reported as stack overflows
+    if (!ok && lane == 0) overflow += 1u << 20;   // a lost handshake: counted with the stack overflows
+    lost = !ok;
     min_distance = best_id == -1 ? -1.0f : fbest;
     return best_id;
 }
@@ -2634,7 +2641,8 @@ __device__ __forceinline__ int walk_pair_walker(const DevGeom &g, const TopNodes
 // The tester (whole wave, converged), after taking a posted box: tests every
 // list the walker publishes until the walker's end, then PS_DONE.  lbase: the
 // LDS word base PB_LISTS is relative to.
-__device__ __forceinline__ void walk_pair_tester(const DevGeom &g, CHR_LDS uint32_t *box, CHR_LDS uint32_t *lbase) {
+__device__ __forceinline__ void walk_pair_tester(const DevGeom &g, CHR_LDS uint32_t *box, CHR_LDS uint32_t *lbase,
+                                                 uint32_t spin) {
     const uint32_t lane = __lane_id();
     const V3 o = v3(__uint_as_float(lds_ld(box + PB_OX)), __uint_as_float(lds_ld(box + PB_OY)),
                     __uint_as_float(lds_ld(box + PB_OZ)));
@@ -2649,16 +2657,19 @@ __device__ __forceinline__ void walk_pair_tester(const DevGeom &g, CHR_LDS uint3
     const V3 inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
     for (uint32_t j = 0;; ++j) {
         uint32_t ws = 0;
-        const bool ok = pair_wait(box, [&]() {
+        const bool ok = pair_wait(box, spin, [&]() {
             const uint32_t wd = lds_ld(box + PB_WDONE);
             ws = lds_ld(box + PB_WSEQ);
             return ws > j || wd == j;
         });
         if (!ok || ws <= j) break;   // the walker's end: every list tested
         lds_acquire();
-        const uint32_t n = lds_ld(box + PB_CNT0 + (j & 1u));
+        // bounded reads whatever the buffers hold: after a lost handshake the walker
+        // reuses them as walk_lone's scratch while this wave may still be reading
+        const uint32_t n = min(lds_ld(box + PB_CNT0 + (j & 1u)), (uint32_t)TAIL_TRI);
         const int nb = (int)(j & 1u) * TAIL_TRI;
-        const uint32_t trec = lane < n ? lists[nb + (int)lane] : 0u;
+        auto rec = [&](uint32_t i) { const uint32_t t = lists[nb + (int)i]; return t < g.nwtri ? t : 0u; };
+        const uint32_t trec = lane < n ? rec(lane) : 0u;
         // the list is in registers: its buffer is free (before the loads, which a
         // release would wait for)
         if (n <= 64u) { lds_release(); lds_st(box + PB_TREAD, j + 1u); }
@@ -2684,7 +2695,7 @@ __device__ __forceinline__ void walk_pair_tester(const DevGeom &g, CHR_LDS uint3
         };
         if (lane < n) test(r0, r1, r2, w3, rr);
         for (uint32_t i = lane + 64u; i < n; i += 64u) {
-            const float4 *tr = g.wtri + 4 * (size_t)lists[nb + (int)i];
+            const float4 *tr = g.wtri + 4 * (size_t)rec(i);
             test(gld(tr), gld(tr + 1), gld(tr + 2), gld_lo2(tr + 3), tr);
         }
         if (n > 64u) { lds_release(); lds_st(box + PB_TREAD, j + 1u); }
@@ -2707,15 +2718,21 @@ __device__ __forceinline__ void walk_pair_tester(const DevGeom &g, CHR_LDS uint3
         lds_st(box + PB_TSEQ, j + 1u);
     }
     lds_release();
-    lds_st(box + PB_STATE, PS_DONE);
+    // TAKEN -> DONE only: after a lost handshake the walker has moved on and the box
+    // may already say something else (PS_EXIT in the timing kernel)
+    if (lane == 0) atomicCAS((uint32_t *)box + PB_STATE, PS_TAKEN, PS_DONE);
 }
 
 // The walker's side of a pair walk: post the ray into the box (the caller has
-// claimed it: PS_POSTING), walk, release the box.
+// claimed it: PS_POSTING), walk, release the box.  lost: the handshake was lost
+// and the result is not the walk's (the caller walks the ray alone); the box
+// then stays aborted (never PS_IDLE again), so no walker of the workgroup claims
+// it while the abandoned tester may still use it.
 template <class M>
 __device__ __forceinline__ int walk_pair(const DevGeom &g, const TopNodes &top, V3 o, V3 d, uint32_t last, M stk,
                                          int cap, CHR_LDS uint32_t *lists, uint32_t lists_off, CHR_LDS uint32_t *box,
-                                         uint32_t &overflow, float &min_distance, uint32_t &iters) {
+                                         uint32_t spin, uint32_t &overflow, float &min_distance, uint32_t &iters,
+                                         bool &lost) {
     lds_st(box + PB_WSEQ, 0u);
     lds_st(box + PB_WDONE, 0xFFFFFFFFu);
     lds_st(box + PB_TREAD, 0u);
@@ -2733,9 +2750,10 @@ __device__ __forceinline__ int walk_pair(const DevGeom &g, const TopNodes &top, 
     lds_st(box + PB_LISTS, lists_off);
     lds_release();
     lds_st(box + PB_STATE, PS_REQ);
-    const int tri = walk_pair_walker(g, top, o, d, stk, cap, lists, box, overflow, min_distance, iters);
+    const int tri = walk_pair_walker(g, top, o, d, stk, cap, lists, box, spin, overflow, min_distance, iters, lost);
     lds_release();
-    lds_st(box + PB_STATE, PS_IDLE);
+    if (lost) lds_st(box + PB_ABORT, 1u);
+    else lds_st(box + PB_STATE, PS_IDLE);
     return tri;
 }
 
@@ -2824,7 +2842,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_tail_kernel(const DevGe
                 if ((uint32_t)__builtin_amdgcn_readfirstlane((int)old) == PS_REQ) {
                     if (lane == 0) atomicSub(&box_s[PB_IDLE], 1u);
                     lds_acquire();
-                    walk_pair_tester(g, box, (CHR_LDS uint32_t *)tris);
+                    walk_pair_tester(g, box, (CHR_LDS uint32_t *)tris, PAIR_SPIN_MAX);
                     if (lane == 0) atomicAdd(&box_s[PB_IDLE], 1u);
                     continue;
                 }
@@ -2967,18 +2985,21 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_tail_kernel(const DevGe
             uint32_t it;
             // one walker: with an idle wave of the workgroup as its triangle tester when
             // there is one (claimed by the mailbox's PS_IDLE -> PS_POSTING)
-            bool paired = false;
-            if (Gs == 64 && a.pair && lds_ld(box + PB_IDLE) != 0u && lds_ld(box + PB_STATE) == PS_IDLE) {
+            bool paired = false, lost = false;
+            if (Gs == 64 && a.pair && lds_ld(box + PB_IDLE) != 0u && lds_ld(box + PB_STATE) == PS_IDLE &&
+                lds_ld(box + PB_ABORT) == 0u) {
                 uint32_t old = PS_TAKEN;
                 if (lane == 0) old = atomicCAS(&box_s[PB_STATE], PS_IDLE, PS_POSTING);
                 paired = (uint32_t)__builtin_amdgcn_readfirstlane((int)old) == PS_IDLE;
             }
-            const int st = paired ? walk_pair(g, top, o, dd, last, LdsFlat{wstack}, TAIL_STACK * 8, wtris,
-                                              (threadIdx.x >> 6) * 2u * TAIL_TRI, box, overflow, sd, it)
-                           : Gs == 64
-                               ? walk_lone(g, o, dd, last, LdsFlat{wstack}, TAIL_STACK * 8, LdsFlat{wtris}, overflow, sd, it)
-                               : walk_segment<0>(g, act, o, dd, last, Gs, LdsFlat{wstack + seg0 / 8 * TAIL_STACK * 2},
-                                                 TAIL_STACK * Gs / 8, LdsFlat{wtris + 4 * seg0}, top, overflow, sd, it);
+            int st = paired ? walk_pair(g, top, o, dd, last, LdsFlat{wstack}, TAIL_STACK * 8, wtris,
+                                        (threadIdx.x >> 6) * 2u * TAIL_TRI, box, PAIR_SPIN_MAX, overflow, sd, it, lost)
+                     : Gs == 64
+                         ? walk_lone(g, o, dd, last, LdsFlat{wstack}, TAIL_STACK * 8, LdsFlat{wtris}, overflow, sd, it)
+                         : walk_segment<0>(g, act, o, dd, last, Gs, LdsFlat{wstack + seg0 / 8 * TAIL_STACK * 2},
+                                           TAIL_STACK * Gs / 8, LdsFlat{wtris + 4 * seg0}, top, overflow, sd, it);
+            // a lost pair handshake: the tester's minimum may be partial -> the walk again, alone
+            if (lost) st = walk_lone(g, o, dd, last, LdsFlat{wstack}, TAIL_STACK * 8, LdsFlat{wtris}, overflow, sd, it);
             if (Gs == 64) {   // one segment: every lane already holds the result
                 tri = st;
                 dist = sd;
@@ -5287,7 +5308,10 @@ extern "C" int chr_device_profile_fetch(uint64_t *h_calls, uint64_t *h_cycles, i
 
 namespace chr {
 // chr_walk_lone_timing: walk_lone on one wave per workgroup (walker 0), or the
-// pair walk on two (walker 1: wave 0 walks, wave 1 tests), each ray reps times
+// pair walk on two (walker 1: wave 0 walks, wave 1 tests), each ray reps times;
+// walker 2: the pair walk with a 2-poll handshake budget, so handshakes are lost
+// (the tail kernel's recovery path: the walk again with walk_lone, no more
+// pairing in the workgroup once aborted)
 __global__ __launch_bounds__(128) void walk_lone_timing_kernel(const DevGeom *__restrict__ gdev, const float *rays,
                                                                uint32_t n, uint32_t reps, uint32_t *out,
                                                                int32_t walker) {
@@ -5304,7 +5328,7 @@ __global__ __launch_bounds__(128) void walk_lone_timing_kernel(const DevGeom *__
     }
     __syncthreads();
     if (threadIdx.x >= 64) {   // the tester wave (walker 1), else idle
-        if (walker != 1) return;
+        if (walker == 0) return;
         while (true) {
             uint32_t st = PS_IDLE;
             for (uint32_t i = 0; i < PAIR_SPIN_MAX * 8u; ++i) {
@@ -5313,9 +5337,11 @@ __global__ __launch_bounds__(128) void walk_lone_timing_kernel(const DevGeom *__
                 __builtin_amdgcn_s_sleep(1);
             }
             if (st != PS_REQ) return;
+            uint32_t old = 0;
+            if (threadIdx.x == 64) old = atomicCAS(&box_s[PB_STATE], PS_REQ, PS_TAKEN);
+            if ((uint32_t)__builtin_amdgcn_readfirstlane((int)old) != PS_REQ) continue;
             lds_acquire();
-            lds_st(box + PB_STATE, PS_TAKEN);
-            walk_pair_tester(g, box, (CHR_LDS uint32_t *)tris);
+            walk_pair_tester(g, box, (CHR_LDS uint32_t *)tris, walker == 2 ? 2u : PAIR_SPIN_MAX);
         }
     }
     for (uint32_t r = blockIdx.x; r < n; r += gridDim.x) {
@@ -5326,11 +5352,16 @@ __global__ __launch_bounds__(128) void walk_lone_timing_kernel(const DevGeom *__
             float sd;
             uint32_t it = 0;
             const unsigned long long t0 = __builtin_amdgcn_s_memrealtime(), c0 = __builtin_amdgcn_s_memtime();
-            const int tri = walker == 1
-                                ? walk_pair(g, top, o, d, last, LdsFlat{(CHR_LDS uint32_t *)stacks}, TAIL_STACK * 8,
-                                            (CHR_LDS uint32_t *)tris, 0u, box, overflow, sd, it)
-                                : walk_lone(g, o, d, last, LdsFlat{(CHR_LDS uint32_t *)stacks}, TAIL_STACK * 8,
-                                            LdsFlat{(CHR_LDS uint32_t *)tris}, overflow, sd, it);
+            bool lost = false;
+            const bool pair = walker != 0 && lds_ld(box + PB_ABORT) == 0u;
+            int tri = pair ? walk_pair(g, top, o, d, last, LdsFlat{(CHR_LDS uint32_t *)stacks}, TAIL_STACK * 8,
+                                       (CHR_LDS uint32_t *)tris, 0u, box, walker == 2 ? 2u : PAIR_SPIN_MAX, overflow,
+                                       sd, it, lost)
+                           : walk_lone(g, o, d, last, LdsFlat{(CHR_LDS uint32_t *)stacks}, TAIL_STACK * 8,
+                                       LdsFlat{(CHR_LDS uint32_t *)tris}, overflow, sd, it);
+            if (lost)
+                tri = walk_lone(g, o, d, last, LdsFlat{(CHR_LDS uint32_t *)stacks}, TAIL_STACK * 8,
+                                LdsFlat{(CHR_LDS uint32_t *)tris}, overflow, sd, it);
             const unsigned long long t1 = __builtin_amdgcn_s_memrealtime(), c1 = __builtin_amdgcn_s_memtime();
             if (threadIdx.x == 0) {
                 uint32_t *o4 = out + 4 * ((size_t)r * reps + k);
@@ -5341,7 +5372,7 @@ __global__ __launch_bounds__(128) void walk_lone_timing_kernel(const DevGeom *__
             }
         }
     }
-    if (walker == 1) {
+    if (walker != 0) {
         lds_release();
         lds_st(box + PB_STATE, PS_EXIT);
     }
@@ -5351,7 +5382,7 @@ __global__ __launch_bounds__(128) void walk_lone_timing_kernel(const DevGeom *__
 
 extern "C" int chr_walk_lone_timing(const chr_geometry *g, const float *d_rays, uint32_t n, uint32_t reps,
                                     uint32_t nwaves, int32_t walker, uint32_t *d_out, void *stream) {
-    if (!g || !d_rays || !d_out || nwaves == 0 || reps == 0 || walker < 0 || walker > 1)
+    if (!g || !d_rays || !d_out || nwaves == 0 || reps == 0 || walker < 0 || walker > 2)
         return chr::fail(CHR_ERR_INVALID, "chr_walk_lone_timing: bad argument");
     if (g->dev.nwnodes == 0) return chr::fail(CHR_ERR_INVALID, "chr_walk_lone_timing: geometry has no wide BVH");
     if (n == 0) return CHR_OK;

@@ -213,11 +213,14 @@ typedef struct chr_kernel_attr {
 int chr_kernel_info(int32_t which, chr_kernel_attr *out);
 /* Diagnostic (no reference counterpart): the tail's lone-photon walk timed in
  * isolation, walker 0 = walk_lone on one wave, 1 = the pair walk (one wave walks,
- * a second wave of the workgroup tests the triangles).  nwaves workgroups; workgroup
+ * a second wave of the workgroup tests the triangles), 2 = the pair walk with a
+ * 2-poll handshake budget, so handshakes are lost and the tail kernel's recovery
+ * (the walk again with walk_lone, no more pairing in that workgroup) runs; each
+ * lost handshake adds 1 << 20 to the last word.  nwaves workgroups; workgroup
  * w walks rays w, w + nwaves, ... each reps times in a row.  d_rays: n x 7 floats
  * (origin, direction, last hit triangle id as int bits); d_out: n x reps x 4 words
  * (record index or -1, iterations, 100 MHz ticks, shader-clock cycles of the walk)
- * + 1 word, the stack overflows / lost handshakes (must read 0). */
+ * + 1 word, the stack overflows (low 20 bits, must read 0) + lost handshakes << 20. */
 int chr_walk_lone_timing(const chr_geometry *g, const float *d_rays, uint32_t n, uint32_t reps,
                          uint32_t nwaves, int32_t walker, uint32_t *d_out, void *stream);
 

@@ -77,3 +77,19 @@ def test_pair_walk_from_hits(cuda, small_detector, small_packed):
     assert ov0 == 0 and ov1 == 0 and np.array_equal(lone, pair)
     assert not np.array_equal(lone[:, 0], first[hit, 0])      # the excluded triangles are not found again
     assert np.all(lone[:, 0] != first[hit, 0])
+
+
+def test_pair_walk_lost_handshake_recovers(cuda, small_detector):
+    """a lost pair handshake must not return the tester's partial
+    minimum.  walker 2 gives every handshake wait 2 polls, so handshakes are
+    lost; the walker then walks the ray again alone and its workgroup pairs no
+    more walks.  Every result equals walk_lone's, and the lost handshakes are
+    counted (1 << 20 each), with no stack overflow."""
+    from chroma import gpu
+    det = gpu.GPUDetector(small_detector)
+    rays = _rays(512, seed=17)
+    lone, ov0 = _walk(det, rays, 0, 64)
+    forced, ov2 = _walk(det, rays, 2, 64)
+    assert ov0 == 0 and (ov2 & 0xFFFFF) == 0
+    assert ov2 >> 20 >= 1                      # the recovery path ran
+    assert np.array_equal(lone, forced)

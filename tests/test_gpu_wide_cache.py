@@ -87,3 +87,30 @@ def test_corrupt_cache_refused_before_upload(cuda, tmp_path, small_detector):
     g.bvh.wide = bad
     with pytest.raises(_native.NativeError, match='wide BVH'):
         gpu.GPUGeometry(g)
+
+
+def test_refused_cache_entry_rebuilt(cuda, tmp_path, small_detector):
+    """a cache entry of the right shape whose contents the upload's
+    validation refuses (a record id out of range) is dropped and the traversal
+    BVH rebuilt once (setup source 'rebuilt'); the next geometry loads the
+    rewritten entry from the cache."""
+    from chroma import gpu
+    from chroma.cache import Cache
+    from chroma.gpu import wide_bvh
+    cache = Cache(str(tmp_path))
+    md5 = small_detector.mesh.md5()
+    g0 = copy.copy(small_detector)
+    g0.bvh = copy.copy(small_detector.bvh)
+    g0.bvh.wide = None
+    cache.save_bvh(g0.bvh, md5)
+    assert gpu.GPUGeometry(g0).setup_times['wide_bvh_source'] == 'built'
+    d = wide_bvh.directory(str(tmp_path), md5, 'default', wide_bvh.builder_key())
+    rid = np.load(d + '/rec_id.npy')
+    rid[3] = len(small_detector.mesh.triangles) + 5
+    np.save(d + '/rec_id.npy', rid, allow_pickle=False)
+    g1 = copy.copy(small_detector)
+    g1.bvh = cache.load_bvh(md5)
+    assert gpu.GPUGeometry(g1).setup_times['wide_bvh_source'] == 'rebuilt'
+    g2 = copy.copy(small_detector)
+    g2.bvh = cache.load_bvh(md5)
+    assert gpu.GPUGeometry(g2).setup_times['wide_bvh_source'] == 'cache'

@@ -139,3 +139,61 @@ def test_host_threads():
     assert _native.host_threads() == default
     with pytest.raises(_native.NativeError):
         _native.set_host_threads(-1)
+
+
+def _saved(tmp_path, small_detector):
+    import copy
+    from chroma.cache import Cache
+    from chroma.gpu import wide_bvh
+    from chroma.gpu.packing import PackedGeometry
+    cache = Cache(str(tmp_path))
+    md5 = small_detector.mesh.md5()
+    geo = copy.copy(small_detector)
+    geo.bvh = copy.copy(small_detector.bvh)
+    cache.save_bvh(geo.bvh, md5)
+    packed = PackedGeometry(geo)
+    assert wide_bvh.obtain(geo.bvh, packed)[1] == 'built'
+    return cache, md5, geo, packed, wide_bvh.directory(str(tmp_path), md5, 'default', wide_bvh.builder_key())
+
+
+@pytest.mark.parametrize('what', ['node_width', 'node_dtype', 'rank_length', 'id_dtype'])
+def test_cache_entry_of_wrong_shape_is_rebuilt(tmp_path, small_detector, what):
+    """load() checks the cached arrays before the C side reads
+    nnodes * 96 node bytes and nrec ids / ranks; an entry of the wrong type or
+    shape is not served (obtain() builds instead)."""
+    from chroma.gpu import wide_bvh
+    cache, md5, geo, packed, d = _saved(tmp_path, small_detector)
+    f = {'node_width': 'nodes', 'node_dtype': 'nodes', 'rank_length': 'rec_rank', 'id_dtype': 'rec_id'}[what]
+    a = np.load(os.path.join(d, f + '.npy'))
+    a = {'node_width': lambda: a[:, :95], 'node_dtype': lambda: a.astype(np.uint16),
+         'rank_length': lambda: a[:-1], 'id_dtype': lambda: a.astype(np.int64)}[what]()
+    np.save(os.path.join(d, f + '.npy'), np.ascontiguousarray(a), allow_pickle=False)
+    key, fp = wide_bvh.builder_key(), wide_bvh.fingerprint(geo.bvh)
+    assert wide_bvh.load(str(tmp_path), md5, 'default', key, fp) is None
+    bvh2 = cache.load_bvh(md5)
+    assert wide_bvh.obtain(bvh2, packed)[1] == 'built'
+    assert wide_bvh.load(str(tmp_path), md5, 'default', key, fp) is not None   # rewritten whole
+
+
+def test_fingerprint_covers_every_node(small_detector):
+    """A reference BVH that differs from the cached one's in a single node
+    (any node, not only a sampled one) has another fingerprint."""
+    import copy
+    from chroma.gpu import wide_bvh
+    bvh = copy.copy(small_detector.bvh)
+    fp = wide_bvh.fingerprint(bvh)
+    n = len(bvh.nodes)
+    for i in (1, n // 2 + 1, n - 2):
+        b = copy.copy(bvh)
+        b.nodes = np.array(bvh.nodes, copy=True)
+        b.nodes.view(np.uint32).reshape(-1, 4)[i, 3] ^= 1
+        assert wide_bvh.fingerprint(b) != fp
+
+
+def test_save_bvh_drops_derived_traversal_bvh(tmp_path, small_detector):
+    """Cache.save_bvh over an existing BVH removes the traversal BVHs derived
+    from the old one (<name>.wide/), as remove_bvh does."""
+    cache, md5, geo, packed, d = _saved(tmp_path, small_detector)
+    assert os.path.isdir(d)
+    cache.save_bvh(geo.bvh, md5)
+    assert not os.path.exists(os.path.dirname(d))
