@@ -581,6 +581,54 @@ struct Prof {
 };
 #endif
 
+// Photon watch (profile build only, chr_watch_set / chr_watch_fetch): every step
+// of one photon (its index in one batch's arrays) recorded by the kernel that ran
+// it, in the layout of the oracle's orc_set_watch, so a parity mismatch can be
+// followed step by step on both sides.  Words: kind (1 shade, 2 tail), queue
+// position, hit triangle (-1: none), walk distance, pos in (3), dir in (3), last
+// hit in, material1, absorption length, scattering length, pos out (3), history
+// out, time out, RNG slot.
+#ifdef CHR_DEVICE_PROFILE
+constexpr uint32_t CHR_WATCH_WORDS = 20, CHR_WATCH_MAX = 4096;
+__device__ uint32_t chr_watch_pid = 0xFFFFFFFFu;
+__device__ unsigned long long chr_watch_array = 0ull;   // the batch's pos array (0: any batch)
+__device__ uint32_t chr_watch_n = 0u;
+__device__ uint32_t chr_watch_buf[CHR_WATCH_MAX * CHR_WATCH_WORDS];
+struct Watch {
+    uint32_t w[CHR_WATCH_WORDS];
+    bool on;
+    __device__ __forceinline__ void begin(uint32_t kind, uint32_t pid, const float *pos_array, uint32_t q,
+                                          uint32_t slot, V3 pos, V3 dir, int last_in) {
+        on = chr_watch_pid != 0xFFFFFFFFu && pid == chr_watch_pid && (chr_watch_array == 0ull || chr_watch_array == (unsigned long long)pos_array);
+        if (!on) return;
+        w[0] = kind; w[1] = q; w[19] = slot;
+        w[4] = __float_as_uint(pos.x); w[5] = __float_as_uint(pos.y); w[6] = __float_as_uint(pos.z);
+        w[7] = __float_as_uint(dir.x); w[8] = __float_as_uint(dir.y); w[9] = __float_as_uint(dir.z);
+        w[10] = (uint32_t)last_in;
+    }
+    __device__ __forceinline__ void filled(int tri, const State &s) {
+        if (!on) return;
+        w[2] = (uint32_t)tri; w[3] = __float_as_uint(s.distance); w[11] = (uint32_t)s.material1;
+        w[12] = __float_as_uint(s.absorption_length); w[13] = __float_as_uint(s.scattering_length);
+    }
+    __device__ __forceinline__ void end(V3 pos, uint32_t history, float time) {
+        if (!on) return;
+        w[14] = __float_as_uint(pos.x); w[15] = __float_as_uint(pos.y); w[16] = __float_as_uint(pos.z);
+        w[17] = history; w[18] = __float_as_uint(time);
+        const uint32_t i = atomicAdd(&chr_watch_n, 1u);
+        if (i < CHR_WATCH_MAX)
+            for (uint32_t k = 0; k < CHR_WATCH_WORDS; ++k) chr_watch_buf[i * CHR_WATCH_WORDS + k] = w[k];
+        on = false;
+    }
+};
+#else
+struct Watch {
+    __device__ __forceinline__ void begin(uint32_t, uint32_t, const float *, uint32_t, uint32_t, V3, V3, int) {}
+    __device__ __forceinline__ void filled(int, const State &) {}
+    __device__ __forceinline__ void end(V3, uint32_t, float) {}
+};
+#endif
+
 // The same query, scheduled for 64-wide SIMT (default).  Leaf triangles are
 // not tested inside the node step of the lane that reached them: a lane that
 // hits leaves parks them (one node's worth) and the WAVE decides each
@@ -1744,7 +1792,10 @@ __global__ __launch_bounds__(BLOCK, MINW) void shade_kernel(const DevGeom *__res
                 s.distance = __int_as_float(cur.hit.y);
                 pf.tick(P_FILL);
                 pf.call(P_FILL);
+                Watch wt;
+                wt.begin(1u, cur.pid, a.pos, pos, slot, p.pos, p.dir, p.last_hit);
                 finish_fill<true, WIRES>(g, s, p, tri);
+                wt.filled(tri, s);
                 pf.tick(P_PHYS);
                 if (p.last_hit != -1) {
                     pf.call(P_PHYS);
@@ -1753,6 +1804,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void shade_kernel(const DevGeom *__res
                         command = propagate_at_surface(g, p, s, rng, a.use_weights);
                     if (command == PASS) propagate_at_boundary(p, s, rng);
                 }
+                wt.end(p.pos, p.history, p.time);
                 pf.tick(P_OTHER);
             }
             alive = (p.history & DEAD_MASK) == 0;
@@ -3026,7 +3078,10 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_tail_kernel(const DevGe
             }
             lpf.mark(LP_WALK);
             s.distance = dist;
+            Watch wt;
+            wt.begin(2u, sub == 0 ? pid : 0xFFFFFFFFu, a.pos, q, slot, p.pos, p.dir, p.last_hit);
             finish_fill<true, WIRES>(g, s, p, tri);
+            wt.filled(tri, s);
             lpf.mark(LP_FILL);
             bool stop = p.last_hit == -1;
             if (!stop) {
@@ -3044,6 +3099,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_tail_kernel(const DevGe
                 }
                 lpf.mark(LP_AT_BOUNDARY);
             }
+            wt.end(p.pos, p.history, p.time);
             pf.tick(P_OTHER);
             if (stop) finish();
         }
@@ -5303,6 +5359,38 @@ extern "C" int chr_device_profile_fetch(uint64_t *h_calls, uint64_t *h_cycles, i
     (void)h_calls; (void)h_cycles; (void)n; (void)clock_khz;
     return chr::fail(CHR_ERR_INVALID, "device profiling symbols not found: load libchroma_amd_prof.so "
                                       "(built with -DCHR_DEVICE_PROFILE=1; CHROMA_DEVICE_PROFILE=1)");
+#endif
+}
+
+extern "C" int chr_watch_set(uint32_t photon, const float *d_pos_array) {
+#ifdef CHR_DEVICE_PROFILE
+    const unsigned long long arr = (unsigned long long)d_pos_array;
+    const uint32_t zero = 0u;
+    CHR_HIP_CHECK(hipDeviceSynchronize());
+    CHR_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(chr::chr_watch_pid), &photon, sizeof(photon)));
+    CHR_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(chr::chr_watch_array), &arr, sizeof(arr)));
+    CHR_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(chr::chr_watch_n), &zero, sizeof(zero)));
+    return CHR_OK;
+#else
+    (void)photon; (void)d_pos_array;
+    return chr::fail(CHR_ERR_INVALID, "photon watch: load libchroma_amd_prof.so (CHROMA_DEVICE_PROFILE=1)");
+#endif
+}
+
+extern "C" int chr_watch_fetch(uint32_t *h_out, uint32_t max_records, uint32_t *nrecords) {
+#ifdef CHR_DEVICE_PROFILE
+    if (!h_out || !nrecords) return chr::fail(CHR_ERR_INVALID, "watch_fetch: bad arguments");
+    CHR_HIP_CHECK(hipDeviceSynchronize());
+    uint32_t n = 0;
+    CHR_HIP_CHECK(hipMemcpyFromSymbol(&n, HIP_SYMBOL(chr::chr_watch_n), sizeof(n)));
+    *nrecords = n;
+    uint32_t k = n < max_records ? n : max_records;
+    if (k > chr::CHR_WATCH_MAX) k = chr::CHR_WATCH_MAX;
+    if (k) CHR_HIP_CHECK(hipMemcpyFromSymbol(h_out, HIP_SYMBOL(chr::chr_watch_buf), sizeof(uint32_t) * k * chr::CHR_WATCH_WORDS));
+    return CHR_OK;
+#else
+    (void)h_out; (void)max_records; (void)nrecords;
+    return chr::fail(CHR_ERR_INVALID, "photon watch: load libchroma_amd_prof.so (CHROMA_DEVICE_PROFILE=1)");
 #endif
 }
 

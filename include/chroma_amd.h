@@ -567,6 +567,16 @@ int chr_device_profile_reset(void *stream);
 /* copy n <= CHR_PROF_COUNT counters to host arrays and the shader clock (kHz) the
  * cycles convert with (hipDeviceAttributeClockRate); synchronises the device */
 int chr_device_profile_fetch(uint64_t *h_calls, uint64_t *h_cycles, int32_t n, uint32_t *clock_khz);
+/* Photon watch (diagnostics, profile build only; no reference counterpart):
+ * every step of photon `photon` (its index in a batch's arrays; d_pos_array =
+ * that batch's pos array, NULL: any batch) run by the shade or tail kernels is
+ * recorded as 20 words -- kind (1 shade, 2 tail), queue position, hit triangle,
+ * walk distance, pos in (3), dir in (3), last hit in, material1, absorption and
+ * scattering lengths, pos out (3), history out, time out, RNG slot (the layout
+ * of the oracle's orc_set_watch).  chr_watch_set clears the record count;
+ * chr_watch_fetch copies min(count, max_records, 4096) records and the count. */
+int chr_watch_set(uint32_t photon, const float *d_pos_array);
+int chr_watch_fetch(uint32_t *h_out, uint32_t max_records, uint32_t *nrecords);
 
 /* ------------------------------------------------------------- misc */
 const char *chr_last_error(void);

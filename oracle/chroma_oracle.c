@@ -868,6 +868,24 @@ typedef struct {
 
 /* propagate.cu:254-366 for one slot; returns 1 if the photon is still alive.
  * *processed is 0 when the photon was dead on entry (no write-back). */
+/* Photon watch (diagnostics, orc_set_watch): every step of one photon as 20
+ * words in the layout of the HIP library's chr_watch_fetch -- kind 0, step,
+ * hit triangle, walk distance, pos in (3), dir in (3), last hit in, material1,
+ * absorption and scattering lengths, pos out (3), history out, time out, slot. */
+static int64_t g_watch_pid = -1;
+static uint32_t *g_watch_buf = NULL, g_watch_cap = 0, g_watch_n = 0, g_watch_slot = 0;
+EXPORT void orc_set_watch(int64_t photon, uint32_t *buf, uint32_t cap) {
+    g_watch_pid = photon; g_watch_buf = buf; g_watch_cap = cap; g_watch_n = 0;
+}
+EXPORT uint32_t orc_watch_count(void) { return g_watch_n; }
+static inline uint32_t fbits(float x) { uint32_t u; memcpy(&u, &x, 4); return u; }
+static void watch_end(uint32_t *w, const Photon *p) {
+    w[14] = fbits(p->pos.x); w[15] = fbits(p->pos.y); w[16] = fbits(p->pos.z);
+    w[17] = p->history; w[18] = fbits(p->time); w[19] = g_watch_slot;
+    if (g_watch_n < g_watch_cap) memcpy(g_watch_buf + 20 * (size_t)g_watch_n, w, 80);
+    g_watch_n++;
+}
+
 static int propagate_one(Geo *g, Photons *ph, uint32_t photon_id, chr_xorwow *rng, int max_steps,
                          int use_weights, int scatter_first, int *processed, int *steps_run) {
     Photon p;
@@ -888,11 +906,27 @@ static int propagate_one(Geo *g, Photons *ph, uint32_t photon_id, chr_xorwow *rn
     *processed = 1;
     State s;
     int steps = 0;
+    const int watch = (int64_t)photon_id == g_watch_pid;
+    uint32_t w[20];
+    int pending = 0;
     while (steps < max_steps) {
+        if (pending) { watch_end(w, &p); pending = 0; }
         steps++;
         float prod = ((((p.dir.x * p.dir.y) * p.dir.z) * p.pos.x) * p.pos.y) * p.pos.z;
         if (chr_isnan(prod)) { p.history |= CHR_NO_HIT | CHR_NAN_ABORT; break; }
+        if (watch) {
+            memset(w, 0, sizeof(w));
+            w[1] = (uint32_t)steps;
+            w[4] = fbits(p.pos.x); w[5] = fbits(p.pos.y); w[6] = fbits(p.pos.z);
+            w[7] = fbits(p.dir.x); w[8] = fbits(p.dir.y); w[9] = fbits(p.dir.z);
+            w[10] = (uint32_t)p.last_hit_triangle;
+        }
         fill_state(g, &s, &p);
+        if (watch) {
+            w[2] = (uint32_t)p.last_hit_triangle; w[3] = fbits(s.distance_to_boundary); w[11] = (uint32_t)s.material1;
+            w[12] = fbits(s.absorption_length); w[13] = fbits(s.scattering_length);
+            pending = 1;
+        }
         if (p.last_hit_triangle == -1) break;
         int command = propagate_to_boundary(g, &p, &s, rng, use_weights, scatter_first);
         scatter_first = 0;
@@ -905,6 +939,7 @@ static int propagate_one(Geo *g, Photons *ph, uint32_t photon_id, chr_xorwow *rn
         }
         propagate_at_boundary(&p, &s, rng);
     }
+    if (pending) watch_end(w, &p);
     *steps_run = steps;
     ph->pos[3 * i] = p.pos.x; ph->pos[3 * i + 1] = p.pos.y; ph->pos[3 * i + 2] = p.pos.z;
     ph->dir[3 * i] = p.dir.x; ph->dir[3 * i + 1] = p.dir.y; ph->dir[3 * i + 2] = p.dir.z;
@@ -950,6 +985,7 @@ static void launch_chunk(const chr_geometry_desc *d, Photons *ph, uint32_t *rng,
         rng_load(rng, nslots, (uint32_t)id, &r);
         uint32_t photon_id = input_queue[first + id];
         int processed, steps_run = 0;
+        if ((int64_t)photon_id == g_watch_pid) g_watch_slot = (uint32_t)id;
         alive[id] = (uint8_t)propagate_one(&g, ph, photon_id, &r, max_steps, use_weights, scatter_first, &processed,
                                            &steps_run);
         if (processed) rng_store(rng, nslots, (uint32_t)id, &r);
@@ -1019,6 +1055,23 @@ EXPORT int orc_distance_to_mesh(const chr_geometry_desc *d, int n, const float *
         nv += g.nodes_visited; nt += g.tris_tested;
     }
     if (nodes_tris) { nodes_tris[0] = nv; nodes_tris[1] = nt; }
+    return 0;
+}
+
+/* intersect_mesh (mesh.h:45-126) of n rays with their last-hit triangles
+ * (diagnostics: a GPU step's ray walked by the reference DFS) */
+EXPORT int orc_intersect_rays(const chr_geometry_desc *d, int n, const float *origin, const float *direction,
+                              const int32_t *last_hit, float *distance, int32_t *triangle) {
+    init_once();
+#pragma omp parallel for
+    for (int i = 0; i < n; ++i) {
+        Geo g = {d, 0, 0, 0, 0, 0};
+        f3 o = mk(origin[3 * i], origin[3 * i + 1], origin[3 * i + 2]);
+        f3 dir = mk(direction[3 * i], direction[3 * i + 1], direction[3 * i + 2]);
+        float dist;
+        triangle[i] = intersect_mesh(&g, o, dir, &dist, last_hit[i]);
+        distance[i] = dist;
+    }
     return 0;
 }
 

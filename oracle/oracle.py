@@ -42,6 +42,9 @@ def lib():
         l.orc_hybrid_update_xyz_lookup.argtypes = [vp, i32, i32, i32, vp, vp, u32, ctypes.c_float, vp, vp, vp, i32]
         l.orc_hybrid_update_xyz_image.argtypes = [vp, i32, vp, u32, vp, vp, ctypes.c_float, vp, vp, vp, vp, i32, i32]
         l.orc_hybrid_process_image.argtypes = [i32, vp, vp, i32]
+        l.orc_set_watch.argtypes = [ctypes.c_int64, vp, u32]
+        l.orc_watch_count.restype = u32
+        l.orc_intersect_rays.argtypes = [vp, i32, vp, vp, vp, vp, vp]
         _lib = l
     return _lib
 
@@ -90,6 +93,19 @@ def distance_to_mesh(packed, origins, directions):
     return dist, tri, counts
 
 
+def intersect_rays(packed, origins, directions, last_hit):
+    """The reference DFS walk of rays exactly as given (no normalisation) with
+    their last-hit triangles: (distance, triangle) per ray."""
+    o = np.ascontiguousarray(origins, dtype=np.float32).reshape(-1, 3)
+    d = np.ascontiguousarray(directions, dtype=np.float32).reshape(-1, 3)
+    last = np.ascontiguousarray(last_hit, dtype=np.int32)
+    dist = np.zeros(len(o), dtype=np.float32)
+    tri = np.zeros(len(o), dtype=np.int32)
+    desc = packed.desc()
+    lib().orc_intersect_rays(ctypes.addressof(desc), len(o), _p(o), _p(d), _p(last), _p(dist), _p(tri))
+    return dist, tri
+
+
 class HostPhotons(object):
     """Writable host copies of the nine photon arrays (float3 as (n,3))."""
     FIELDS = ('pos', 'dir', 'pol', 'wavelengths', 't', 'flags', 'last_hit_triangles', 'weights', 'evidx')
@@ -122,6 +138,24 @@ def propagate(packed, photons, rng_states, nslots, nthreads_per_block=256, max_b
     keys = ('nodes_visited', 'tris_tested', 'max_depth', 'overflows', 'host_steps', 'launches', 'final_alive',
             'traversals')
     return dict(zip(keys, (int(x) for x in stats[:8])))
+
+
+class Watch(object):
+    """Every step of one photon (its index in the batch propagate() is given)
+    recorded by the oracle: 20 words per step (chroma_oracle.c orc_set_watch,
+    the layout of the HIP library's chr_watch_fetch)."""
+
+    def __init__(self, photon, cap=4096):
+        self.buf = np.zeros((cap, 20), dtype=np.uint32)
+        lib().orc_set_watch(int(photon), _p(self.buf), cap)
+
+    def records(self):
+        n = min(int(lib().orc_watch_count()), len(self.buf))
+        return self.buf[:n].copy()
+
+    @staticmethod
+    def off():
+        lib().orc_set_watch(-1, None, 0)
 
 
 def fill_state(packed, pos, dir, last_hit=-1, wavelength=400.0):
