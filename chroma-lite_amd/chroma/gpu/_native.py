@@ -165,6 +165,7 @@ _SIGNATURES = {
     'chr_device_profile_fetch': (c_i32, [c_vp, c_vp, c_i32, ctypes.POINTER(c_u32)]),
     'chr_watch_set': (c_i32, [c_u32, c_vp]),
     'chr_watch_fetch': (c_i32, [c_vp, c_u32, ctypes.POINTER(c_u32)]),
+    'chr_watch_ray': (c_i32, [c_vp, c_vp, c_u32, ctypes.POINTER(c_u32)]),
     'chr_last_error': (ctypes.c_char_p, []),
     'chr_version': (c_i32, []),
     'chr_source_sha': (ctypes.c_char_p, []),

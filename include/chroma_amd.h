@@ -577,6 +577,12 @@ int chr_device_profile_fetch(uint64_t *h_calls, uint64_t *h_cycles, int32_t n, u
  * chr_watch_fetch copies min(count, max_records, 4096) records and the count. */
 int chr_watch_set(uint32_t photon, const float *d_pos_array);
 int chr_watch_fetch(uint32_t *h_out, uint32_t max_records, uint32_t *nrecords);
+/* The walk of one ray by trace_kernel (profile build): h_origin non-NULL arms the
+ * log for the ray with exactly this origin (3 floats); with h_origin NULL,
+ * copies min(count, max_events, 8192) 8-word events (kind 1 start, 2 pop,
+ * 3 node expansion, 4 triangle fetched, 5 triangle hit, 6 leaf-box check,
+ * 7 drain, 8 drain publish, 9 publish) and the count. */
+int chr_watch_ray(const float *h_origin, uint32_t *h_events, uint32_t max_events, uint32_t *nevents);
 
 /* ------------------------------------------------------------- misc */
 const char *chr_last_error(void);

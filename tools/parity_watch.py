@@ -35,6 +35,19 @@ def decode(rec):
             'history': int(r[17]), 'time_out': float(f[18]), 'slot': int(r[19])}
 
 
+EVENT_KINDS = {1: 'start', 2: 'pop', 3: 'node', 4: 'tri_fetch', 5: 'tri_hit', 6: 'leaf_box', 7: 'drain',
+               8: 'drain_publish', 9: 'publish'}
+# which words of each event kind are floats
+EVENT_FLOATS = {1: (5, 6, 7), 2: (2, 3), 3: (3, 6), 4: (3,), 5: (3, 5), 6: (4, 5), 7: (3,), 8: (3,), 9: (3,)}
+
+
+def decode_event(e):
+    e = np.asarray(e, np.uint32)
+    k = int(e[0])
+    f = e.view(np.float32)
+    return [EVENT_KINDS.get(k, k)] + [float(f[i]) if i in EVENT_FLOATS.get(k, ()) else int(e[i]) for i in range(1, 8)]
+
+
 def main():
     import ctypes
     import torch
@@ -64,6 +77,10 @@ def main():
     rng = gpu.get_rng_states(wl.nslots, seed=args.seed, first_subsequence=bench.rng_first_subsequence(0, wl.nslots))
     kw = dict(nthreads_per_block=args.nthreads_per_block, max_blocks=args.max_blocks, max_steps=args.max_steps)
     _native.call('chr_watch_set', local, gps[b].pos.gpudata)
+    wray = os.environ.get('WATCH_RAY')   # "x,y,z": log trace_kernel's walk of the ray with this origin
+    if wray:
+        org = np.array([float(v) for v in wray.split(',')], np.float32)
+        _native.call('chr_watch_ray', org.ctypes.data, None, 0, None)
     t0 = time.time()
     if args.pipeline:
         gpu.propagate_batches(gps, wl.gdet, rng, **kw)
@@ -75,6 +92,12 @@ def main():
     cnt = ctypes.c_uint32(0)
     _native.call('chr_watch_fetch', buf.ctypes.data, 4096, ctypes.byref(cnt))
     gsteps = [decode(r) for r in buf[:min(cnt.value, 4096)]]
+    if wray:
+        ev = np.zeros((8192, 8), np.uint32)
+        ne = ctypes.c_uint32(0)
+        _native.call('chr_watch_ray', None, ev.ctypes.data, 8192, ctypes.byref(ne))
+        out['walk_events_count'] = ne.value
+        out['walk_events'] = [decode_event(e) for e in ev[:min(ne.value, 8192)]]
     got = gps[b].get()
     out['gpu'] = {'seconds': round(time.time() - t0, 1), 'steps': len(gsteps),
                   'final': {'pos': got.pos[local].tolist(), 't': float(got.t[local]),
