@@ -235,7 +235,7 @@ static int upload_wide(chr_geometry *g, const chr_geometry_desc *d, const chr_wi
         const size_t n = std::min<size_t>(per, w->nnodes - i);
         uint8_t *h;
         CHR_TRY(st.acquire(k, &h));
-        chr::wide_fill_node_slots(w, i, n, h);
+        chr::wide_fill_node_slots(w, c, i, n, h);
         CHR_TRY(st.copy(k, static_cast<uint8_t *>(p) + 128 * i, n * 128));
     }
     CHR_TRY(dev_upload(g, nullptr, std::max<size_t>(1, w->nrec) * sizeof(chr::WideTri), &p));

@@ -402,6 +402,61 @@ __device__ __forceinline__ bool intersect_box_slab(const RaySlab &r, V3 lo, V3 h
     return true;
 }
 
+// The reference's nearest-hit decision (mesh.h:45-126) between a candidate X
+// (Moller-Trumbore distance dx, reference DFS rank rx, entry distance bdx of its
+// reference leaf box, which the ray hits) and the best so far B (db, rb, bdb;
+// none: db = bdb = inf, rb = ~0).  The reference meets triangles in rank order,
+// keeps the first, and replaces it only by a later one whose leaf box passes the
+// prune (box entry <= the kept distance, mesh.h:94-96) and whose distance is
+// strictly smaller:
+//   rx > rb (B met first): X replaces B  iff  bdx <= db && dx < db;
+//   rx < rb (X met first): B would not have replaced X unless bdb <= dx && db < dx.
+// When every hit lies beyond its own box's entry (bd <= d) this is the
+// (distance, rank) minimum of the earlier rounds.  It is not when the float
+// Moller-Trumbore reports a hit BEFORE the box entry (a grazing triangle far
+// away: the 29k bench's photon 9,043,377 hits a triangle at 36,510.26 mm whose
+// leaf box the ray enters at 36,511.24; the exact ray misses that triangle
+// triangle's plane 7% (in barycentrics) outside it), which the reference keeps
+// when it meets it first.
+__device__ __forceinline__ bool ref_may_beat(float dx, uint32_t rx, float db, uint32_t rb, float bdb) {
+    return rx < rb ? !(bdb <= dx && db < dx) : dx < db;   // before X's leaf box is tested
+}
+__device__ __forceinline__ bool ref_beats(float dx, uint32_t rx, float bdx, float db, uint32_t rb, float bdb) {
+    return rx < rb ? !(bdb <= dx && db < dx) : (bdx <= db && dx < db);
+}
+// Culling threshold for boxes: a triangle X can replace B only if dx <=
+// max(db, bdb), and the boxes holding X are entered at most `undershoot` after
+// dx.  The float false positives above undershoot by up to 2.5e-4 of the
+// distance (5.8 mm) in 10 M photons of the 29k bench (oracle.undershoot): the
+// traversal keeps every box entered within 2^-11 (4.9e-4) + 1 mm of
+// max(db, bdb).  (inf stays inf: no best yet.)
+#ifndef CHR_CUT_REL   // (build-time A/B of the margin: -DCHR_CUT_REL=0.0f -DCHR_CUT_ABS=0.0f)
+#define CHR_CUT_REL 0x1p-11f
+#endif
+#ifndef CHR_CUT_ABS
+#define CHR_CUT_ABS 1.0f
+#endif
+__device__ __forceinline__ float ref_cut(float db, float bdb) {
+    const float m = __builtin_fmaxf(db, bdb);
+    return __builtin_fmaf(m, CHR_CUT_REL, m + CHR_CUT_ABS);
+}
+// Two lanes' candidates (id -1: none, with d = bd = inf, rank = ~0) merged by the
+// rule above (the one the reference meets first, unless the other replaces it):
+// symmetric, so a butterfly leaves every lane of a segment with the same winner.
+constexpr uint32_t NONE32 = 0xFFFFFFFFu;
+struct RefHit {
+    float d, bd;
+    uint32_t rank;
+    int id;
+};
+__device__ __forceinline__ RefHit ref_merge(const RefHit &a, const RefHit &b) {
+    return ref_beats(b.d, b.rank, b.bd, a.d, a.rank, a.bd) ? b : a;
+}
+__device__ __forceinline__ RefHit shfl_xor_hit(const RefHit &h, int off) {
+    return RefHit{__shfl_xor(h.d, off), __shfl_xor(h.bd, off), (uint32_t)__shfl_xor((int)h.rank, off),
+                  __shfl_xor(h.id, off)};
+}
+
 // What a queued photon's walk is: 0 none (NaN state: the step aborts it,
 // propagate.cu:307-310), 1 a walk.  (Rounds 2-4 had a kind 2, FLAT: a
 // direction component with non-finite reciprocal, walked as 2^18 sub-walks;
@@ -419,14 +474,14 @@ __device__ __forceinline__ bool flat_ray(V3 d) {
 // Slab-test the up-to-8 children of one wide node.  Returns the leaf children
 // hit (bit mask), leaves the nearest hit inner child in near_node/near_t and
 // pushes the other hit inner children in child order.  Boxes entered beyond
-// `best` are culled (strict '>', mesh.h:94-96).  Branch-free over the children
+// `cut` (ref_cut of the best so far) are culled (strict '>', mesh.h:94-96).  Branch-free over the children
 // (the per-child early-outs of a loop cost ~3 scalar exec-mask instructions
 // each and divide the wave anyway): all 8 slab tests, the near child as the
 // first of the smallest entry distance, then one predicated push per child at
 // its prefix position.
 template <int SL = WIDE_LDS, int TB = BLOCK>
 __device__ __forceinline__ uint32_t expand_node(const uint4 h, const uint4 a1, const uint4 a2, const uint4 a3,
-                                                const uint4 a4, const uint4 a5, const RaySlab &r, float best,
+                                                const uint4 a4, const uint4 a5, const RaySlab &r, float cut,
                                                 uint32_t &near_node, float &near_t, WStack &st, int &sp,
                                                 uint32_t &overflow, uint32_t cmask = 0xFFu) {
     const V3 org = v3(__uint_as_float(h.x), __uint_as_float(h.y), __uint_as_float(h.z));
@@ -461,7 +516,7 @@ __device__ __forceinline__ uint32_t expand_node(const uint4 h, const uint4 a1, c
             const uint32_t kind = ((c < 4 ? a4.z : a4.w) >> (8 * (c & 3))) & 0xFFu;
             const float tmin = __builtin_fmaxf(__builtin_fmaxf(__builtin_fmaxf(tnx[h], tny[h]), tnz[h]), 0.0f);
             const float tmax = __builtin_fminf(__builtin_fminf(tfx[h], tfy[h]), tfz[h]);
-            const bool hit = (kind != 0u) & (((cmask >> c) & 1u) != 0u) & !(tmin > tmax) & !(tmin > best);
+            const bool hit = (kind != 0u) & (((cmask >> c) & 1u) != 0u) & !(tmin > tmax) & !(tmin > cut);
             inner |= (uint32_t)(hit & (kind == WIDE_INNER)) << c;
             leaf |= (uint32_t)(hit & (kind != WIDE_INNER)) << c;
             tk[c] = tmin;
@@ -621,7 +676,27 @@ struct Watch {
         on = false;
     }
 };
+// trace_kernel's walk of the watched ray (origin bits chr_wray_o, chr_watch_ray):
+// one 8-word event per step of its lane -- kind, then kind-specific words.
+constexpr uint32_t CHR_WEV_MAX = 8192;
+__device__ uint32_t chr_wray_on = 0u;
+__device__ uint32_t chr_wray_o[3];
+__device__ uint32_t chr_wev_n = 0u;
+__device__ uint32_t chr_wev_buf[CHR_WEV_MAX * 8];
+__device__ __forceinline__ bool wray_match(V3 o) {
+    return chr_wray_on && __float_as_uint(o.x) == chr_wray_o[0] && __float_as_uint(o.y) == chr_wray_o[1] &&
+           __float_as_uint(o.z) == chr_wray_o[2];
+}
+__device__ __forceinline__ void wev(uint32_t k, uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t e,
+                                    uint32_t f, uint32_t h) {
+    const uint32_t i = atomicAdd(&chr_wev_n, 1u);
+    if (i >= CHR_WEV_MAX) return;
+    uint32_t *w = chr_wev_buf + 8 * i;
+    w[0] = k; w[1] = a; w[2] = b; w[3] = c; w[4] = d; w[5] = e; w[6] = f; w[7] = h;
+}
+#define CHR_WEV(on, ...) do { if (on) wev(__VA_ARGS__); } while (0)
 #else
+#define CHR_WEV(on, ...) do { } while (0)
 struct Watch {
     __device__ __forceinline__ void begin(uint32_t, uint32_t, const float *, uint32_t, uint32_t, V3, V3, int) {}
     __device__ __forceinline__ void filled(int, const State &) {}
@@ -647,7 +722,7 @@ __device__ int intersect_wide_sched(const DevGeom &g, V3 o, V3 d, float &min_dis
     const V3 noid = v3(-o.x / d.x, -o.y / d.y, -o.z / d.z);
     const V3 inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
     const RaySlab slab = make_slab(o, noid, inv);
-    float best = __builtin_inff();
+    float best = __builtin_inff(), best_bd = __builtin_inff(), cut = __builtin_inff();
     uint32_t best_rank = 0xFFFFFFFFu;
     int best_id = -1;
     const uint32_t last = (uint32_t)last_hit;
@@ -675,7 +750,7 @@ __device__ int intersect_wide_sched(const DevGeom &g, V3 o, V3 d, float &min_dis
                     sp--;
                     float t;
                     wpop(st, sp, node, t);
-                    if (!(t > best)) { found = true; break; }
+                    if (!(t > cut)) { found = true; break; }
                 }
                 if (!found) { done = true; continue; }
             }
@@ -686,7 +761,7 @@ __device__ int intersect_wide_sched(const DevGeom &g, V3 o, V3 d, float &min_dis
             uint32_t near_node;
             float near_t;
             const uint32_t leaf_mask =
-                expand_node(h, a1, a2, a3, a4, a5, slab, best, near_node, near_t, st, sp, overflow);
+                expand_node(h, a1, a2, a3, a4, a5, slab, cut, near_node, near_t, st, sp, overflow);
             node = near_node;
             if (leaf_mask) {
                 pkinds = ((unsigned long long)a4.w << 32) | a4.z;
@@ -716,14 +791,17 @@ __device__ int intersect_wide_sched(const DevGeom &g, V3 o, V3 d, float &min_dis
                 !intersect_record(o, d, r0, r1, r2, dist))
                 continue;
             const uint32_t rank = __float_as_uint(r2.z);
-            if (!(dist < best || (dist == best && rank < best_rank))) continue;
+            if (!ref_may_beat(dist, rank, best, best_rank, best_bd)) continue;
             const float4 r3 = gld(r + 3);
             V3 lo, hi;
             node_bounds(g, make_uint4(__float_as_uint(r2.w), __float_as_uint(r3.x), __float_as_uint(r3.y), 0u), lo, hi);
             float bd;
-            if (!intersect_box(noid, inv, lo, hi, bd) || bd > best) continue;   // mesh.h:94-96
+            if (!intersect_box(noid, inv, lo, hi, bd) || !ref_beats(dist, rank, bd, best, best_rank, best_bd))
+                continue;   // mesh.h:94-96
             best = dist;
             best_rank = rank;
+            best_bd = bd;
+            cut = ref_cut(best, best_bd);
             best_id = rec_of(g, r);
         }
     }
@@ -750,7 +828,7 @@ __device__ int intersect_wide_spec(const DevGeom &g, V3 o, V3 d, float &min_dist
     const V3 noid = v3(-o.x / d.x, -o.y / d.y, -o.z / d.z);
     const V3 inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
     const RaySlab slab = make_slab(o, noid, inv);
-    float best = __builtin_inff();
+    float best = __builtin_inff(), best_bd = __builtin_inff(), cut = __builtin_inff();
     uint32_t best_rank = 0xFFFFFFFFu;
     int best_id = -1;
     const uint32_t last = (uint32_t)last_hit;
@@ -775,7 +853,7 @@ __device__ int intersect_wide_spec(const DevGeom &g, V3 o, V3 d, float &min_dist
                     sp--;
                     float t;
                     wpop(st, sp, node, t);
-                    if (!(t > best)) { found = true; break; }
+                    if (!(t > cut)) { found = true; break; }
                 }
                 if (!found) { done = true; continue; }
             }
@@ -785,7 +863,7 @@ __device__ int intersect_wide_spec(const DevGeom &g, V3 o, V3 d, float &min_dist
                         a5 = gld(np + 5);
             uint32_t near_node;
             float near_t;
-            uint32_t leaf_mask = expand_node(h, a1, a2, a3, a4, a5, slab, best, near_node, near_t, st, sp, overflow);
+            uint32_t leaf_mask = expand_node(h, a1, a2, a3, a4, a5, slab, cut, near_node, near_t, st, sp, overflow);
             node = near_node;
             while (leaf_mask) {
                 const int k = __builtin_ctz(leaf_mask);
@@ -815,14 +893,17 @@ __device__ int intersect_wide_spec(const DevGeom &g, V3 o, V3 d, float &min_dist
                 !intersect_record(o, d, r0, r1, r2, dist))
                 continue;
             const uint32_t rank = __float_as_uint(r2.z);
-            if (!(dist < best || (dist == best && rank < best_rank))) continue;
+            if (!ref_may_beat(dist, rank, best, best_rank, best_bd)) continue;
             const float4 r3 = gld(r + 3);
             V3 lo, hi;
             node_bounds(g, make_uint4(__float_as_uint(r2.w), __float_as_uint(r3.x), __float_as_uint(r3.y), 0u), lo, hi);
             float bd;
-            if (!intersect_box(noid, inv, lo, hi, bd) || bd > best) continue;   // mesh.h:94-96
+            if (!intersect_box(noid, inv, lo, hi, bd) || !ref_beats(dist, rank, bd, best, best_rank, best_bd))
+                continue;   // mesh.h:94-96
             best = dist;
             best_rank = rank;
+            best_bd = bd;
+            cut = ref_cut(best, best_bd);
             best_id = rec_of(g, r);
         }
     }
@@ -1479,6 +1560,8 @@ struct PropagateArgs {
                                        // batches' tail, the critical path beside the next batch's walk)
     uint32_t pair;                     // tail kernel: a lone walk takes an idle wave of its workgroup as
                                        // triangle tester (walk_pair; CHR_PAIR_WALK=0: walk_lone alone)
+    uint32_t walk_up;                  // tail kernel: a lone walk with a previous hit starts at that hit's
+                                       // leaf and climbs (walk_lone<true>; CHR_WALK_UP=0: from the root)
     uint32_t want;
     // tail kernel, work-queue mode (nullptr: group g runs queue positions g, g + cap, ...): a
     // zeroed counter the photon groups take queue positions from, for queues no longer than
@@ -1693,6 +1776,12 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_step_kernel(const DevGe
 constexpr uint32_t SHADE_PHYS_WORDS = 12288;   // 48 KB: 3 workgroups of shade_kernel<3> per CU
 // (only DevGeom::phys_hot_words are copied: the re-emission time CDFs stay in HBM)
 constexpr uint32_t TAIL_PHYS_WORDS = 8192;     // 32 KB: 2 tail workgroups (+ 40 KB of walk stacks each)
+// The copy is the launch's dynamic LDS, sized to the geometry's hot words (the
+// demo and 29k detectors: a few KB of their 32 / 48 KB caps), so a workgroup holds
+// only the LDS its geometry needs: host and kernel apply the same rule.
+__host__ __device__ __forceinline__ uint32_t phys_lds_bytes(const DevGeom &g, uint32_t cap_words) {
+    return g.phys && g.phys_hot_words <= cap_words ? g.phys_hot_words * 4u : 0u;
+}
 __device__ __forceinline__ DevGeom phys_cache(const DevGeom &g, uint4 *lds, uint32_t cap_words) {
     DevGeom gl = g;
     if (g.phys && g.phys_hot_words <= cap_words) {   // workgroup-uniform
@@ -1751,7 +1840,7 @@ template <int MINW, bool WIRES = true>
 __global__ __launch_bounds__(BLOCK, MINW) void shade_kernel(const DevGeom *__restrict__ gdev, PropagateArgs a,
                                                             uint32_t cap) {
     if (a.mode && *a.mode != a.want) return;
-    __shared__ uint4 phys_lds[SHADE_PHYS_WORDS / 4];
+    extern __shared__ uint4 phys_lds[];   // phys_lds_bytes(SHADE_PHYS_WORDS) of dynamic LDS
     const DevGeom g = phys_cache(*gdev, phys_lds, SHADE_PHYS_WORDS);
     const uint32_t slot = blockIdx.x * BLOCK + threadIdx.x;
     const uint32_t n = a.dev_n ? *a.dev_n - 1u : (uint32_t)a.nthreads;
@@ -1954,7 +2043,8 @@ struct LoneProf<true> {
 template <int GS, class M>
 __device__ __forceinline__ int walk_segment(const DevGeom &g, bool act, V3 o, V3 d, uint32_t last, int Gs_in, M stk, int cap, M tlist,
                             const TopNodes &top, uint32_t &overflow, float &min_distance, uint32_t &iters,
-                            float best = __builtin_inff(), uint32_t best_rank = 0xFFFFFFFFu, int best_id = -1) {
+                            float best = __builtin_inff(), uint32_t best_rank = 0xFFFFFFFFu, int best_id = -1,
+                            float best_bd = __builtin_inff()) {
     const int Gs = GS ? GS : Gs_in;
     constexpr uint32_t INVALID = 0xFFFFFFFFu;
     constexpr unsigned long long NONE = ~0ull;
@@ -1971,7 +2061,9 @@ __device__ __forceinline__ int walk_segment(const DevGeom &g, bool act, V3 o, V3
         best = ufl(best);
         best_rank = uu(best_rank);
         best_id = (int)uu((uint32_t)best_id);
+        best_bd = ufl(best_bd);
     }
+    float cut = ufl(ref_cut(best, best_bd));   // the culling threshold (ref_cut)
     const uint32_t lane = __lane_id();
     const uint32_t seg0 = lane & ~(uint32_t)(Gs - 1);
     const uint32_t L = lane - seg0;                   // lane within the segment
@@ -2014,7 +2106,7 @@ __device__ __forceinline__ int walk_segment(const DevGeom &g, bool act, V3 o, V3
             if (L < (uint32_t)W) {
                 en = stk[2 * (sp - 1 - (int)L)];
                 et = stk[2 * (sp - 1 - (int)L) + 1];
-                ok = !(__uint_as_float(et) > best);           // mesh.h:94-96
+                ok = !(__uint_as_float(et) > cut);            // mesh.h:94-96
             }
             const unsigned long long okm = __ballot(ok) & segmask;
             const int need = __popcll(em), nv = __popcll(okm);
@@ -2101,7 +2193,7 @@ __device__ __forceinline__ int walk_segment(const DevGeom &g, bool act, V3 o, V3
             const float tfz = __builtin_fmaf(__builtin_fmaf(byte_f(r.negz ? a2.x : a3.z, r.negz ? a2.y : a3.w, kk), sz, org.z), r.inz, r.ofz);
             const float tmin = __builtin_fmaxf(__builtin_fmaxf(__builtin_fmaxf(tnx, tny), tnz), 0.0f);
             const float tmax = __builtin_fminf(__builtin_fminf(tfx, tfy), tfz);
-            const bool hit = (kind != 0u) & !(tmin > tmax) & !(tmin > best);
+            const bool hit = (kind != 0u) & !(tmin > tmax) & !(tmin > cut);
             inner = hit & (kind == WIDE_INNER);
             leafhit = hit & (kind != WIDE_INNER);
             tk = tmin;
@@ -2149,7 +2241,7 @@ __device__ __forceinline__ int walk_segment(const DevGeom &g, bool act, V3 o, V3
         lp.tick(2);
         // test the previous iteration's triangles (entries beyond the segment's
         // lanes, rare, are fetched now)
-        float lbest = best;
+        float lbest = best, lbd = best_bd;
         uint32_t lrank = best_rank;
         int lid = -1;
         for (uint32_t i = L; i < Tp; i += (uint32_t)Gs) {
@@ -2163,48 +2255,45 @@ __device__ __forceinline__ int walk_segment(const DevGeom &g, bool act, V3 o, V3
                 !intersect_record(o, d, r0, r1, r2, dist))
                 continue;
             const uint32_t rank = __float_as_uint(r2.z);
-            if (!(dist < lbest || (dist == lbest && rank < lrank))) continue;
+            if (!ref_may_beat(dist, rank, lbest, lrank, lbd)) continue;
             V3 lo, hi;
             node_bounds(g, make_uint4(__float_as_uint(r2.w), __float_as_uint(r3.x), __float_as_uint(r3.y), 0u), lo, hi);
             float bd;
-            if (!intersect_box(noid, inv, lo, hi, bd) || bd > lbest) continue;   // mesh.h:94-96
+            if (!intersect_box(noid, inv, lo, hi, bd) || !ref_beats(dist, rank, bd, lbest, lrank, lbd))
+                continue;   // mesh.h:94-96
             lbest = dist;
+            lbd = bd;
             lrank = rank;
             lid = rec_of(g, rr);
         }
         __builtin_amdgcn_wave_barrier();   // list reads land before the next iteration's writes
-        // segment min over (distance, rank): usually no lane or one lane has a hit
+        // the segment's winner (ref_merge): usually no lane or one lane has a hit
         const unsigned long long hm = __ballot(lid != -1) & segmask;
         if (hm != 0) {
-            unsigned long long lkey = lid == -1 ? NONE : (((unsigned long long)__float_as_uint(lbest) << 32) | lrank);
+            RefHit w = lid == -1 ? RefHit{__builtin_inff(), __builtin_inff(), NONE32, -1} : RefHit{lbest, lbd, lrank, lid};
             if ((hm & (hm - 1)) == 0) {
                 const int src = __ffsll((long long)hm) - 1;
                 if (GS == 64) {   // src is wave-uniform: scalar reads of the winning lane
-                    lkey = ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(lkey >> 32), src)
-                            << 32) |
-                           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)lkey, src);
-                    lid = __builtin_amdgcn_readlane(lid, src);
+                    w = RefHit{__int_as_float(__builtin_amdgcn_readlane(__float_as_int(w.d), src)),
+                               __int_as_float(__builtin_amdgcn_readlane(__float_as_int(w.bd), src)),
+                               (uint32_t)__builtin_amdgcn_readlane((int)w.rank, src), __builtin_amdgcn_readlane(w.id, src)};
                 } else {
-                    lkey = ((unsigned long long)(uint32_t)__shfl((int)(uint32_t)(lkey >> 32), src) << 32) |
-                           (uint32_t)__shfl((int)(uint32_t)lkey, src);
-                    lid = __shfl(lid, src);
+                    w = RefHit{__shfl(w.d, src), __shfl(w.bd, src), (uint32_t)__shfl((int)w.rank, src), __shfl(w.id, src)};
                 }
             } else {
-                for (int off = 1; off < Gs; off <<= 1) {
-                    const unsigned long long ok = __shfl_xor(lkey, off);
-                    const int oid = __shfl_xor(lid, off);
-                    if (ok < lkey) { lkey = ok; lid = oid; }
-                }
+                for (int off = 1; off < Gs; off <<= 1) w = ref_merge(w, shfl_xor_hit(w, off));
             }
-            best = ufl(__uint_as_float((uint32_t)(lkey >> 32)));
-            best_rank = uu((uint32_t)lkey);
-            best_id = (int)uu((uint32_t)lid);
+            best = ufl(w.d);
+            best_bd = ufl(w.bd);
+            best_rank = uu(w.rank);
+            best_id = (int)uu((uint32_t)w.id);
+            cut = ufl(ref_cut(best, best_bd));
         }
         Tp = uu(Tn);
         sp = (int)uu((uint32_t)sp);
         pb ^= 1;
         lp.tick(3);
-        if (cur != INVALID && cur_t > best) cur = INVALID;
+        if (cur != INVALID && cur_t > cut) cur = INVALID;
     }
     lp.flush();
     min_distance = best_id == -1 ? -1.0f : best;
@@ -2240,11 +2329,19 @@ __device__ __forceinline__ uint32_t byte8(uint32_t lo4, uint32_t hi4, uint32_t k
 // allocator as temporaries, and the compiler then waits for the load first.
 // best / best_rank / best_id: a hit already found seeds the walk (trace_kernel's
 // drain of a walk begun lane by lane), as in walk_segment.
-template <class M>
+// UP (walk_up): the walk starts at node `start` (the leaf node of the photon's
+// previous hit: the ray starts on that triangle, and its next hit is usually
+// close) and climbs -- start's ancestors (its slot's chain words, wide_bvh.h) go on
+// the stack with their entry distance 0, each expanded without the child the
+// chain came from, the 8th of a chain continuing it.  Every node of the tree is
+// then reached exactly once (start's subtree, plus each ancestor's other
+// children), with the same culling: the same tested set as from the root, in
+// ~half the dependent iterations for the tail's long-lived photons.
+template <bool UP = false, class M>
 __device__ __forceinline__ int walk_lone(const DevGeom &g, V3 o, V3 d, uint32_t last, M stk, int cap, M tlist,
                                          uint32_t &overflow, float &min_distance, uint32_t &iters,
                                          float best = __builtin_inff(), uint32_t best_rank = 0xFFFFFFFFu,
-                                         int best_id = -1) {
+                                         int best_id = -1, float best_bd = __builtin_inff(), uint32_t start = 0u) {
     constexpr uint32_t INVALID = 0xFFFFFFFFu;
     auto ufl = [](float x) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(x))); };
     auto uu = [](uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); };
@@ -2254,6 +2351,8 @@ __device__ __forceinline__ int walk_lone(const DevGeom &g, V3 o, V3 d, uint32_t 
     best = ufl(best);
     best_rank = uu(best_rank);
     best_id = (int)uu((uint32_t)best_id);
+    best_bd = ufl(best_bd);
+    float cut = ufl(ref_cut(best, best_bd));   // the culling threshold (ref_cut)
     const uint32_t lane = __lane_id();
     const uint32_t k = lane & 7u;                     // child slot of this lane
     const uint32_t lead = lane & ~7u;                 // its sub-group's first lane
@@ -2261,7 +2360,8 @@ __device__ __forceinline__ int walk_lone(const DevGeom &g, V3 o, V3 d, uint32_t 
     const V3 noid = v3(-o.x / d.x, -o.y / d.y, -o.z / d.z);
     const V3 inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
     const RaySlab r = make_slab(o, noid, inv);
-    uint32_t cur = lane < 8u ? 0u : INVALID;          // cursor 0 starts at the root
+    uint32_t cur = lane < 8u ? (UP ? start : 0u) : INVALID;   // cursor 0 starts at the root (UP: at start)
+    uint32_t chainw = INVALID;                        // UP: ancestor word k of the cursor's node (lane k)
     float cur_t = 0.0f;
     int sp = 0;
     uint32_t Tp = 0;                                  // triangles in flight (listed by the last expansion)
@@ -2280,9 +2380,10 @@ __device__ __forceinline__ int walk_lone(const DevGeom &g, V3 o, V3 d, uint32_t 
     // a triangle fetch the next expansion.  (No LDS copy of the tree top here: a
     // lane-divergent LDS / global choice makes that count unknown.)
     auto fetch_node = [&](uint32_t node) {
-        const uint4 *np = g.wnodes + (size_t)g.wstride * (node == INVALID ? 0u : node);
+        const uint4 *np = g.wnodes + (size_t)g.wstride * (node == INVALID ? 0u : (UP ? node & WIDE_NODE_MASK : node));
         h = gld(np); a1 = gld(np + 1); a2 = gld(np + 2); a3 = gld(np + 3); a4 = gld(np + 4);
         a5 = gld_lo2(np + 5);
+        if constexpr (UP) chainw = gld(reinterpret_cast<const uint32_t *>(np) + 24 + k);   // the slot's chain
     };
     auto fetch_tri = [&](uint32_t trec) {
         rr = g.wtri + 4 * (size_t)trec;
@@ -2300,10 +2401,14 @@ __device__ __forceinline__ int walk_lone(const DevGeom &g, V3 o, V3 d, uint32_t 
         bool inner = false, leafhit = false;
         float tk = 0.0f;
         uint32_t kind = 0, child = 0, first = 0;
+        // UP: an ancestor is expanded without the child its chain came from; a chain's
+        // last known node pushes its own chain
+        const bool more = UP && cur != INVALID && (cur & WIDE_CHAIN_MORE) != 0u;
         if (cur != INVALID) {
             const V3 org = v3(__uint_as_float(h.x), __uint_as_float(h.y), __uint_as_float(h.z));
             const float sx = exp_scale(h.w), sy = exp_scale(h.w >> 8), sz = exp_scale(h.w >> 16);
             kind = byte8(a4.z, a4.w, k);
+            if (UP && (cur & WIDE_ANCESTOR) != 0u && ((cur >> 28) & 7u) == k) kind = 0u;
             auto q = [k](uint32_t lo4, uint32_t hi4) { return (float)byte8(lo4, hi4, k); };
             const float tnx = __builtin_fmaf(__builtin_fmaf(q(r.negx ? a2.z : a1.x, r.negx ? a2.w : a1.y), sx, org.x), r.inx, r.onx);
             const float tfx = __builtin_fmaf(__builtin_fmaf(q(r.negx ? a1.x : a2.z, r.negx ? a1.y : a2.w), sx, org.x), r.inx, r.ofx);
@@ -2313,7 +2418,7 @@ __device__ __forceinline__ int walk_lone(const DevGeom &g, V3 o, V3 d, uint32_t 
             const float tfz = __builtin_fmaf(__builtin_fmaf(q(r.negz ? a2.x : a3.z, r.negz ? a2.y : a3.w), sz, org.z), r.inz, r.ofz);
             const float tmin = __builtin_fmaxf(__builtin_fmaxf(__builtin_fmaxf(tnx, tny), tnz), 0.0f);
             const float tmax = __builtin_fminf(__builtin_fminf(tfx, tfy), tfz);
-            const bool hit = (kind != 0u) & !(tmin > tmax) & !(tmin > best);
+            const bool hit = (kind != 0u) & !(tmin > tmax) & !(tmin > cut);
             inner = hit & (kind == WIDE_INNER);
             leafhit = hit & (kind != WIDE_INNER);
             tk = tmin;
@@ -2348,6 +2453,24 @@ __device__ __forceinline__ int walk_lone(const DevGeom &g, V3 o, V3 d, uint32_t 
         } else {
             sp += npush;
         }
+        if constexpr (UP) {   // a chain onto the stack, entry distance 0, its first ancestor on top
+            const bool cpush = more && chainw != WIDE_NO_PARENT;
+            const unsigned long long cm = __ballot(cpush);
+            if (cm) {
+                const int nc = __popcll(cm);
+                const int cpos = sp + nc - 1 - __popcll(cm & below);
+                if (cpush && cpos < cap) {
+                    stk[2 * cpos] = chainw;
+                    stk[2 * cpos + 1] = 0u;
+                }
+                if (sp + nc > cap) {
+                    if (lane == 0) overflow += (uint32_t)(sp + nc - cap);
+                    sp = cap;
+                } else {
+                    sp += nc;
+                }
+            }
+        }
         cur = near;
         cur_t = __uint_as_float(key & ~7u);           // <= the child's entry distance
         // this expansion's hit-leaf triangles, listed in lane order: each lane writes
@@ -2373,7 +2496,7 @@ __device__ __forceinline__ int walk_lone(const DevGeom &g, V3 o, V3 d, uint32_t 
             if (lane < (uint32_t)W) {
                 en = stk[2 * (sp - 1 - (int)lane)];
                 et = stk[2 * (sp - 1 - (int)lane) + 1];
-                ok = !(__uint_as_float(et) > best);           // mesh.h:94-96
+                ok = !(__uint_as_float(et) > cut);            // mesh.h:94-96
             }
             const unsigned long long okm = __ballot(ok);
             const int need = __popcll(em), nv = __popcll(okm);
@@ -2404,7 +2527,7 @@ __device__ __forceinline__ int walk_lone(const DevGeom &g, V3 o, V3 d, uint32_t 
         // test the previous list's triangles: each lane its own (loaded last
         // iteration); entries beyond the 64 lanes (rare) are fetched in a loop of their
         // own, so the common test waits for nothing in flight
-        float lbest = best;
+        float lbest = best, lbd = best_bd;
         uint32_t lrank = best_rank;
         int lid = -1;
         // (t3 = nullptr: the leaf-box words are loaded for a candidate only)
@@ -2413,15 +2536,17 @@ __device__ __forceinline__ int walk_lone(const DevGeom &g, V3 o, V3 d, uint32_t 
             float dist;
             if (id == last || !intersect_record(o, d, t0, t1, t2, dist)) return;
             const uint32_t rank = __float_as_uint(t2.z);
-            if (!(dist < lbest || (dist == lbest && rank < lrank))) return;
+            if (!ref_may_beat(dist, rank, lbest, lrank, lbd)) return;
             uint2 w;
             if (t3) w = make_uint2(__float_as_uint(t3->x), __float_as_uint(t3->y));
             else w = gld_lo2(tr + 3);
             V3 lo, hi;
             node_bounds(g, make_uint4(__float_as_uint(t2.w), w.x, w.y, 0u), lo, hi);
             float bd;
-            if (!intersect_box(noid, inv, lo, hi, bd) || bd > lbest) return;   // mesh.h:94-96
+            if (!intersect_box(noid, inv, lo, hi, bd) || !ref_beats(dist, rank, bd, lbest, lrank, lbd))
+                return;   // mesh.h:94-96
             lbest = dist;
+            lbd = bd;
             lrank = rank;
             lid = rec_of(g, tr);
         };
@@ -2436,25 +2561,23 @@ __device__ __forceinline__ int walk_lone(const DevGeom &g, V3 o, V3 d, uint32_t 
             const float4 *tr = g.wtri + 4 * (size_t)tlist[pb * TAIL_TRI + (int)i];
             test(gld(tr), gld(tr + 1), gld(tr + 2), nullptr, tr);
         }
-        // wave min over (distance, rank): usually no lane or one lane has a hit
+        // the wave's winner (ref_merge): usually no lane or one lane has a hit
         const unsigned long long hm = __ballot(lid != -1);
         if (hm != 0) {
-            unsigned long long lkey = lid == -1 ? ~0ull : (((unsigned long long)__float_as_uint(lbest) << 32) | lrank);
+            RefHit w = lid == -1 ? RefHit{__builtin_inff(), __builtin_inff(), NONE32, -1} : RefHit{lbest, lbd, lrank, lid};
             if ((hm & (hm - 1)) == 0) {
                 const int src = __ffsll((long long)hm) - 1;
-                lkey = ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(lkey >> 32), src) << 32) |
-                       (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)lkey, src);
-                lid = __builtin_amdgcn_readlane(lid, src);
+                w = RefHit{__int_as_float(__builtin_amdgcn_readlane(__float_as_int(w.d), src)),
+                           __int_as_float(__builtin_amdgcn_readlane(__float_as_int(w.bd), src)),
+                           (uint32_t)__builtin_amdgcn_readlane((int)w.rank, src), __builtin_amdgcn_readlane(w.id, src)};
             } else {
-                for (int off = 1; off < 64; off <<= 1) {
-                    const unsigned long long ok = __shfl_xor(lkey, off);
-                    const int oid = __shfl_xor(lid, off);
-                    if (ok < lkey) { lkey = ok; lid = oid; }
-                }
+                for (int off = 1; off < 64; off <<= 1) w = ref_merge(w, shfl_xor_hit(w, off));
             }
-            best = ufl(__uint_as_float((uint32_t)(lkey >> 32)));
-            best_rank = uu((uint32_t)lkey);
-            best_id = (int)uu((uint32_t)lid);
+            best = ufl(w.d);
+            best_bd = ufl(w.bd);
+            best_rank = uu(w.rank);
+            best_id = (int)uu((uint32_t)w.id);
+            cut = ufl(ref_cut(best, best_bd));
         }
         // this expansion's triangles, in flight during the stack refill and the next
         // expansion (the registers of the ones just tested are free)
@@ -2462,7 +2585,7 @@ __device__ __forceinline__ int walk_lone(const DevGeom &g, V3 o, V3 d, uint32_t 
         fetch_tri(lane < Tn ? tlist[nb + (int)lane] : 0u);
         Tp = Tn;
         pb ^= 1;
-        if (cur != INVALID && cur_t > best) cur = INVALID;   // its node load is in flight: ignored
+        if (cur != INVALID && cur_t > cut) cur = INVALID;   // its node load is in flight: ignored
         lp.tick(3);
         if (__ballot(cur != INVALID) == 0 && Tp == 0 && sp == 0) break;
     }
@@ -2495,7 +2618,9 @@ __device__ __forceinline__ int walk_lone(const DevGeom &g, V3 o, V3 d, uint32_t 
 // more walks (an abandoned tester may still be reading the box).
 enum : int {
     PB_STATE, PB_IDLE, PB_WORKERS, PB_WSEQ, PB_WDONE, PB_TREAD, PB_TSEQ, PB_BEST, PB_RANK, PB_ID,
-    PB_OX, PB_OY, PB_OZ, PB_DX, PB_DY, PB_DZ, PB_LAST, PB_CNT0, PB_CNT1, PB_LISTS, PB_ABORT, PB_WORDS = 24
+    PB_OX, PB_OY, PB_OZ, PB_DX, PB_DY, PB_DZ, PB_LAST, PB_CNT0, PB_CNT1, PB_LISTS, PB_ABORT,
+    PB_BD, PB_CUT,   // the best's leaf-box entry and the culling threshold (ref_cut) the walker reads
+    PB_WORDS = 24
 };
 enum : uint32_t { PS_IDLE = 0, PS_POSTING = 1, PS_REQ = 2, PS_TAKEN = 3, PS_DONE = 4, PS_EXIT = 5 };
 constexpr uint32_t PAIR_SPIN_MAX = 1u << 21;
@@ -2564,7 +2689,7 @@ __device__ __forceinline__ int walk_pair_walker(const DevGeom &g, const TopNodes
         }
     };
     fetch_node(cur == INVALID ? 0u : cur);
-    float best = __uint_as_float(lds_ld(box + PB_BEST));   // the tester's, read once per iteration
+    float cut = __uint_as_float(lds_ld(box + PB_CUT));   // the tester's culling threshold, read once per iteration
     while (true) {
         iters++;
         bool inner = false, leafhit = false;
@@ -2583,7 +2708,7 @@ __device__ __forceinline__ int walk_pair_walker(const DevGeom &g, const TopNodes
             const float tfz = __builtin_fmaf(__builtin_fmaf(q(r.negz ? a2.x : a3.z, r.negz ? a2.y : a3.w), sz, org.z), r.inz, r.ofz);
             const float tmin = __builtin_fmaxf(__builtin_fmaxf(__builtin_fmaxf(tnx, tny), tnz), 0.0f);
             const float tmax = __builtin_fminf(__builtin_fminf(tfx, tfy), tfz);
-            const bool hit = (kind != 0u) & !(tmin > tmax) & !(tmin > best);
+            const bool hit = (kind != 0u) & !(tmin > tmax) & !(tmin > cut);
             inner = hit & (kind == WIDE_INNER);
             leafhit = hit & (kind != WIDE_INNER);
             tk = tmin;
@@ -2632,7 +2757,7 @@ __device__ __forceinline__ int walk_pair_walker(const DevGeom &g, const TopNodes
             if (lane < (uint32_t)W) {
                 en = stk[2 * (sp - 1 - (int)lane)];
                 et = stk[2 * (sp - 1 - (int)lane) + 1];
-                okk = !(__uint_as_float(et) > best);           // mesh.h:94-96
+                okk = !(__uint_as_float(et) > cut);            // mesh.h:94-96
             }
             const unsigned long long okm = __ballot(okk);
             const int need = __popcll(em), nv = __popcll(okm);
@@ -2657,7 +2782,7 @@ __device__ __forceinline__ int walk_pair_walker(const DevGeom &g, const TopNodes
             em &= ~taken;
         }
         sp = (int)uu((uint32_t)sp);
-        if (cur != INVALID && cur_t > best) cur = INVALID;
+        if (cur != INVALID && cur_t > cut) cur = INVALID;
         const bool end = __ballot(cur != INVALID) == 0 && sp == 0;
         if (!end) fetch_node(cur == INVALID ? 0u : cur);
         if (Tn) {
@@ -2672,7 +2797,7 @@ __device__ __forceinline__ int walk_pair_walker(const DevGeom &g, const TopNodes
             lds_st(box + PB_WSEQ, nl + 1u);
             nl++;
         }
-        best = __uint_as_float(lds_ld(box + PB_BEST));
+        cut = __uint_as_float(lds_ld(box + PB_CUT));
         if (end) break;
     }
     lds_release();
@@ -2702,7 +2827,7 @@ __device__ __forceinline__ void walk_pair_tester(const DevGeom &g, CHR_LDS uint3
                     __uint_as_float(lds_ld(box + PB_DZ)));
     const uint32_t last = lds_ld(box + PB_LAST);
     CHR_LDS uint32_t *lists = lbase + lds_ld(box + PB_LISTS);
-    float best = __uint_as_float(lds_ld(box + PB_BEST));
+    float best = __uint_as_float(lds_ld(box + PB_BEST)), best_bd = __uint_as_float(lds_ld(box + PB_BD));
     uint32_t best_rank = lds_ld(box + PB_RANK);
     int best_id = (int)lds_ld(box + PB_ID);
     const V3 noid = v3(-o.x / d.x, -o.y / d.y, -o.z / d.z);
@@ -2728,7 +2853,7 @@ __device__ __forceinline__ void walk_pair_tester(const DevGeom &g, CHR_LDS uint3
         const float4 *rr = g.wtri + 4 * (size_t)trec;
         const float4 r0 = gld(rr), r1 = gld(rr + 1), r2 = gld(rr + 2);
         const uint2 w3 = gld_lo2(rr + 3);
-        float lbest = best;
+        float lbest = best, lbd = best_bd;
         uint32_t lrank = best_rank;
         int lid = -1;
         auto test = [&](const float4 &t0, const float4 &t1, const float4 &t2, uint2 w, const float4 *tr) {
@@ -2736,12 +2861,14 @@ __device__ __forceinline__ void walk_pair_tester(const DevGeom &g, CHR_LDS uint3
             float dist;
             if (id == last || !intersect_record(o, d, t0, t1, t2, dist)) return;
             const uint32_t rank = __float_as_uint(t2.z);
-            if (!(dist < lbest || (dist == lbest && rank < lrank))) return;
+            if (!ref_may_beat(dist, rank, lbest, lrank, lbd)) return;
             V3 lo, hi;
             node_bounds(g, make_uint4(__float_as_uint(t2.w), w.x, w.y, 0u), lo, hi);
             float bd;
-            if (!intersect_box(noid, inv, lo, hi, bd) || bd > lbest) return;   // mesh.h:94-96
+            if (!intersect_box(noid, inv, lo, hi, bd) || !ref_beats(dist, rank, bd, lbest, lrank, lbd))
+                return;   // mesh.h:94-96
             lbest = dist;
+            lbd = bd;
             lrank = rank;
             lid = rec_of(g, tr);
         };
@@ -2752,19 +2879,18 @@ __device__ __forceinline__ void walk_pair_tester(const DevGeom &g, CHR_LDS uint3
         }
         if (n > 64u) { lds_release(); lds_st(box + PB_TREAD, j + 1u); }
         const unsigned long long hm = __ballot(lid != -1);
-        if (hm != 0) {
-            unsigned long long lkey = lid == -1 ? ~0ull : (((unsigned long long)__float_as_uint(lbest) << 32) | lrank);
-            for (int off = 1; off < 64; off <<= 1) {
-                const unsigned long long ok2 = __shfl_xor(lkey, off);
-                const int oid = __shfl_xor(lid, off);
-                if (ok2 < lkey) { lkey = ok2; lid = oid; }
-            }
-            best = __int_as_float(__builtin_amdgcn_readfirstlane((int)(uint32_t)(lkey >> 32)));
-            best_rank = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)lkey);
-            best_id = __builtin_amdgcn_readfirstlane(lid);
+        if (hm != 0) {   // the wave's winner (ref_merge)
+            RefHit wv = lid == -1 ? RefHit{__builtin_inff(), __builtin_inff(), NONE32, -1} : RefHit{lbest, lbd, lrank, lid};
+            for (int off = 1; off < 64; off <<= 1) wv = ref_merge(wv, shfl_xor_hit(wv, off));
+            best = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(wv.d)));
+            best_bd = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(wv.bd)));
+            best_rank = (uint32_t)__builtin_amdgcn_readfirstlane((int)wv.rank);
+            best_id = __builtin_amdgcn_readfirstlane(wv.id);
             lds_st(box + PB_RANK, best_rank);
             lds_st(box + PB_ID, (uint32_t)best_id);
+            lds_st(box + PB_BD, __float_as_uint(best_bd));
             lds_st(box + PB_BEST, __float_as_uint(best));
+            lds_st(box + PB_CUT, __float_as_uint(ref_cut(best, best_bd)));
         }
         lds_release();
         lds_st(box + PB_TSEQ, j + 1u);
@@ -2790,6 +2916,8 @@ __device__ __forceinline__ int walk_pair(const DevGeom &g, const TopNodes &top, 
     lds_st(box + PB_TREAD, 0u);
     lds_st(box + PB_TSEQ, 0u);
     lds_st(box + PB_BEST, __float_as_uint(__builtin_inff()));
+    lds_st(box + PB_BD, __float_as_uint(__builtin_inff()));
+    lds_st(box + PB_CUT, __float_as_uint(__builtin_inff()));
     lds_st(box + PB_RANK, 0xFFFFFFFFu);
     lds_st(box + PB_ID, 0xFFFFFFFFu);
     lds_st(box + PB_OX, __float_as_uint(o.x));
@@ -2869,7 +2997,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_tail_kernel(const DevGe
         box_s[PB_WORKERS] = BLOCK / 64;
         box_s[PB_ABORT] = 0u;
     }
-    __shared__ uint4 phys_lds[TAIL_PHYS_WORDS / 4];
+    extern __shared__ uint4 phys_lds[];   // phys_lds_bytes(TAIL_PHYS_WORDS) of dynamic LDS
     const DevGeom g = phys_cache(*gdev, phys_lds, TAIL_PHYS_WORDS);
     __shared__ uint4 top_lds[6 * TOP_NODES];   // 7 KB: 2 workgroups per CU hold 2 x 79 KB
     const TopNodes top = stage_top<BLOCK>(g, (CHR_LDS u32x4 *)top_lds, TOP_NODES);
@@ -2920,6 +3048,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_tail_kernel(const DevGe
     Photon p;
     State s;
     int steps = 0, scatter_first = 0;
+    uint32_t up_node = 0xFFFFFFFFu;   // the leaf node of the photon's last hit record (walk_up's start)
     uint32_t q = wq ? next_q() : slot, pid = 0, iters = 0, paired_steps = 0;
     bool live = false, exhausted = wq ? q >= n : slot >= nslot;
     unsigned long long t0 = 0, walk_ticks = 0;
@@ -2984,6 +3113,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_tail_kernel(const DevGe
                 steps = 0;
                 iters = 0;
                 paired_steps = 0;
+                up_node = 0xFFFFFFFFu;
                 walk_ticks = 0;
                 scatter_first = a.scatter_first;
                 live = true;
@@ -3020,13 +3150,14 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_tail_kernel(const DevGe
             const int src = m != 0 ? __ffsll((long long)m) - 1 : (int)(lane & ~7u);
             const bool act = m != 0;
             V3 o, dd;
-            uint32_t last;
+            uint32_t last, start = 0xFFFFFFFFu;
             if (w == 1) {   // one walker: its lane is wave-uniform, scalar reads instead of LDS shuffles
                 const int s1 = __ffsll((long long)wm) - 1;
                 auto rl = [s1](float x) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), s1)); };
                 o = v3(rl(p.pos.x), rl(p.pos.y), rl(p.pos.z));
                 dd = v3(rl(p.dir.x), rl(p.dir.y), rl(p.dir.z));
                 last = (uint32_t)__builtin_amdgcn_readlane(p.last_hit, s1);
+                start = (uint32_t)__builtin_amdgcn_readlane((int)up_node, s1);
             } else {
                 o = v3(__shfl(p.pos.x, src), __shfl(p.pos.y, src), __shfl(p.pos.z, src));
                 dd = v3(__shfl(p.dir.x, src), __shfl(p.dir.y, src), __shfl(p.dir.z, src));
@@ -3038,13 +3169,18 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_tail_kernel(const DevGe
             // one walker: with an idle wave of the workgroup as its triangle tester when
             // there is one (claimed by the mailbox's PS_IDLE -> PS_POSTING)
             bool paired = false, lost = false;
-            if (Gs == 64 && a.pair && lds_ld(box + PB_IDLE) != 0u && lds_ld(box + PB_STATE) == PS_IDLE &&
+            // one walker with a previous hit: walk_up from that hit's leaf (ahead of pairing)
+            const bool up = Gs == 64 && a.walk_up && start != 0xFFFFFFFFu;
+            if (Gs == 64 && !up && a.pair && lds_ld(box + PB_IDLE) != 0u && lds_ld(box + PB_STATE) == PS_IDLE &&
                 lds_ld(box + PB_ABORT) == 0u) {
                 uint32_t old = PS_TAKEN;
                 if (lane == 0) old = atomicCAS(&box_s[PB_STATE], PS_IDLE, PS_POSTING);
                 paired = (uint32_t)__builtin_amdgcn_readfirstlane((int)old) == PS_IDLE;
             }
-            int st = paired ? walk_pair(g, top, o, dd, last, LdsFlat{wstack}, TAIL_STACK * 8, wtris,
+            int st = up ? walk_lone<true>(g, o, dd, last, LdsFlat{wstack}, TAIL_STACK * 8, LdsFlat{wtris}, overflow, sd,
+                                          it, __builtin_inff(), 0xFFFFFFFFu, -1, __builtin_inff(),
+                                          (start & WIDE_NODE_MASK) | WIDE_CHAIN_MORE)
+                     : paired ? walk_pair(g, top, o, dd, last, LdsFlat{wstack}, TAIL_STACK * 8, wtris,
                                         (threadIdx.x >> 6) * 2u * TAIL_TRI, box, PAIR_SPIN_MAX, overflow, sd, it, lost)
                      : Gs == 64
                          ? walk_lone(g, o, dd, last, LdsFlat{wstack}, TAIL_STACK * 8, LdsFlat{wtris}, overflow, sd, it)
@@ -3065,6 +3201,9 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_tail_kernel(const DevGe
                 iters += it;
                 paired_steps += paired ? 1u : 0u;
                 walk_ticks += __builtin_amdgcn_s_memrealtime() - tw0;
+                // the hit record's leaf node (its last word), for the next step's walk_up:
+                // in flight during this step's physics
+                up_node = tri >= 0 ? gld(reinterpret_cast<const uint32_t *>(g.wtri + 4 * (size_t)tri) + 15) : 0xFFFFFFFFu;
             }
             pf.tick(P_OTHER);
         }
@@ -3307,7 +3446,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
     uint32_t nflat_rays = 0;        // flat rays walked by this work-item (flat-axis slab test; diagnostic)
     V3 o = v3(0.0f, 0.0f, 0.0f), d = v3(0.0f, 0.0f, 1.0f);
     RaySlab slab = make_slab(o, o, d);
-    float best = 0.0f;
+    float best = 0.0f, best_bd = 0.0f, cut = 0.0f;   // best hit, its leaf box's entry, the culling threshold
     uint32_t best_rank = 0, last = 0, node = 0;
     int best_id = -1, sp = 0;
     bool walk_done = true, drain = false;
@@ -3325,9 +3464,13 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
     enum { P_NODE, P_TRI, P_REFILL, P_IDLE, P_DRAIN, P_BOX = 3 };   // regions (calls: P_REFILL = walks, P_BOX = boxes)
     Prof<5> pf;
     pf.start(P_REFILL);
+#ifdef CHR_DEVICE_PROFILE
+    bool wlog = false;   // this lane walks the watched ray
+#endif
     while (true) {
         pf.tick(P_REFILL);   // the last step goes to the region each work-item was in
         if (has_ray && walk_done && pleft == 0 && qh == qt) {   // walk over: publish (mesh.h:123-125)
+            CHR_WEV(wlog, 9u, q, (uint32_t)best_id, __float_as_uint(best), best_rank, 0u, 0u, 0u);
             a.hits[q] = make_int2(best_id, __float_as_int(best_id == -1 ? -1.0f : best));
             has_ray = false;
             if constexpr (COUNT) {
@@ -3363,6 +3506,8 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
                             start = true;
                             node = 0;
                             best = __builtin_inff();
+                            best_bd = __builtin_inff();
+                            cut = __builtin_inff();
                             best_rank = 0xFFFFFFFFu;
                         }
                     } else if (GATHER && j < n) {
@@ -3377,6 +3522,8 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
                                 start = true;
                                 node = 0;
                                 best = __builtin_inff();
+                                best_bd = __builtin_inff();
+                                cut = __builtin_inff();
                                 best_rank = 0xFFFFFFFFu;
                                 last = (uint32_t)a.last_hit[pid];
                             }
@@ -3392,6 +3539,11 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
                         pf.call(P_REFILL);
                         if (slab.flat) nflat_rays++;
                         if constexpr (COUNT) cnt.walks++;
+#ifdef CHR_DEVICE_PROFILE
+                        wlog = wray_match(o);
+                        CHR_WEV(wlog, 1u, q, j, blockIdx.x, threadIdx.x, __float_as_uint(d.x), __float_as_uint(d.y),
+                                __float_as_uint(d.z));
+#endif
                     }
                 }
             }
@@ -3432,7 +3584,8 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
                     sp--;
                     float t;
                     wpop<SL, TB>(st, sp, node, t);
-                    if (!(t > best)) { found = true; break; }
+                    CHR_WEV(wlog, 2u, node, __float_as_uint(t), __float_as_uint(best), (uint32_t)sp, 0u, 0u, 0u);
+                    if (!(t > cut)) { found = true; break; }
                 }
                 if (!found) { walk_done = true; continue; }
             }
@@ -3450,7 +3603,9 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
             uint32_t near_node;
             float near_t;
             uint32_t leaf_mask =
-                expand_node<SL, TB>(h, a1, a2, a3, a4, a5, slab, best, near_node, near_t, st, sp, overflow, 0xFFu);
+                expand_node<SL, TB>(h, a1, a2, a3, a4, a5, slab, cut, near_node, near_t, st, sp, overflow, 0xFFu);
+            CHR_WEV(wlog, 3u, node, near_node, __float_as_uint(near_t), leaf_mask, (uint32_t)sp, __float_as_uint(best),
+                    qt - qh);
             node = near_node;
             while (leaf_mask) {
                 const int k = __builtin_ctz(leaf_mask);
@@ -3478,17 +3633,23 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
             pleft--;
             const uint32_t id = __float_as_uint(r2.y);
             float dist;
+            CHR_WEV(wlog, 4u, (uint32_t)rec_of(g, r), id, __float_as_uint(best), pleft, 0u, 0u, 0u);
             if (id == last ||
                 !intersect_record(o, d, r0, r1, r2, dist))
                 continue;
             const uint32_t rank = __float_as_uint(r2.z);
-            if (!(dist < best || (dist == best && rank < best_rank))) continue;
+            CHR_WEV(wlog, 5u, (uint32_t)rec_of(g, r), id, __float_as_uint(dist), rank, __float_as_uint(best), best_rank, 0u);
+            if (!ref_may_beat(dist, rank, best, best_rank, best_bd)) continue;
             const float4 r3 = gld(r + 3);
             V3 lo, hi;
             node_bounds(g, make_uint4(__float_as_uint(r2.w), __float_as_uint(r3.x), __float_as_uint(r3.y), 0u), lo, hi);
             float bd;
-            if (!intersect_box_slab(slab, lo, hi, bd) || bd > best) continue;   // mesh.h:94-96
+            const bool boxok = intersect_box_slab(slab, lo, hi, bd);
+            CHR_WEV(wlog, 6u, (uint32_t)rec_of(g, r), id, boxok ? 1u : 0u, __float_as_uint(bd), __float_as_uint(best), 0u, 0u);
+            if (!boxok || !ref_beats(dist, rank, bd, best, best_rank, best_bd)) continue;   // mesh.h:94-96
             best = dist;
+            best_bd = bd;
+            cut = ref_cut(best, best_bd);
             best_rank = rank;
             best_id = rec_of(g, r);
         }
@@ -3496,6 +3657,8 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
     if constexpr (!COUNT) {
         if (drain) {
             pf.tick(P_DRAIN);
+            CHR_WEV(wlog && has_ray, 7u, q, (uint32_t)best_id, __float_as_uint(best), best_rank, (uint32_t)__popcll(__ballot(has_ray)),
+                    0u, 0u);
             const unsigned long long rm = __ballot(has_ray);
             const int w = __popcll(rm);
             const int Gs = w == 1 ? 64 : (w == 2 ? 32 : 16);
@@ -3507,7 +3670,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
             const V3 so = v3(__shfl(o.x, src), __shfl(o.y, src), __shfl(o.z, src));
             const V3 sdir = v3(__shfl(d.x, src), __shfl(d.y, src), __shfl(d.z, src));
             const uint32_t slast = (uint32_t)__shfl((int)last, src);
-            const float sbest = __shfl(best, src);
+            const float sbest = __shfl(best, src), sbd = __shfl(best_bd, src);
             const uint32_t srank = (uint32_t)__shfl((int)best_rank, src);
             const int sid = __shfl(best_id, src);
             const int seg0 = (int)lane & ~(Gs - 1);
@@ -3516,14 +3679,15 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
             uint32_t sit;
             const int tri = w == 1
                                 ? walk_lone(g, so, sdir, slast, LdsRowsT<TB>{wbase, 0}, DSTK * 8,
-                                            LdsRowsT<TB>{wbase, 8 * DSTK * 2}, overflow, sdist, sit, sbest, srank, sid)
+                                            LdsRowsT<TB>{wbase, 8 * DSTK * 2}, overflow, sdist, sit, sbest, srank, sid, sbd)
                                 : walk_segment<0>(g, act, so, sdir, slast, Gs, LdsRowsT<TB>{wbase, seg0 / 8 * DSTK * 2},
                                                   DSTK * Gs / 8, LdsRowsT<TB>{wbase, 8 * DSTK * 2 + 4 * seg0}, top,
-                                                  overflow, sdist, sit, sbest, srank, sid);
+                                                  overflow, sdist, sit, sbest, srank, sid, sbd);
             const int mine = (__popcll(rm & ((1ull << lane) - 1ull)) * Gs) & 63;   // my segment's first lane
             const int rt = __shfl(tri, mine);
             const float rd = __shfl(sdist, mine);
             if (has_ray) {                                        // publish (mesh.h:123-125)
+                CHR_WEV(wlog, 8u, q, (uint32_t)rt, __float_as_uint(rd), 0u, 0u, 0u, 0u);
                 a.hits[q] = make_int2(rt, __float_as_int(rt == -1 ? -1.0f : rd));
                 pf.call(P_DRAIN);
             }
@@ -4133,11 +4297,25 @@ static StepVariant select_step_variant(const chr_geometry *g) {
             sv.binned = v == 7 ? 1 : (v == 8 ? 0 : 2);
             break;
     }
+    // the physics tables' LDS copy is dynamic LDS (phys_lds_bytes): allow the caps, once
+    static const bool lds_caps = []() {
+        const int sb = (int)(SHADE_PHYS_WORDS * 4), tb = (int)(TAIL_PHYS_WORDS * 4);
+        (void)hipFuncSetAttribute((const void *)shade_kernel<3>, hipFuncAttributeMaxDynamicSharedMemorySize, sb);
+        (void)hipFuncSetAttribute((const void *)shade_kernel<3, false>, hipFuncAttributeMaxDynamicSharedMemorySize, sb);
+        (void)hipFuncSetAttribute((const void *)propagate_tail_kernel<kTailWaves>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, tb);
+        (void)hipFuncSetAttribute((const void *)propagate_tail_kernel<kTailWaves, false>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, tb);
+        (void)hipGetLastError();
+        return true;
+    }();
+    (void)lds_caps;
     return sv;
 }
 
 // scratch layout (u32 words): [0] overflows [1] queue base [2..11] u64 walk counters [12..15] pad; masks (u64, 8-aligned); offsets
 static bool pair_walk_enabled();
+static bool walk_up_enabled();
 static int launch_chunk(const chr_geometry *g, const chr_photons *ph, uint32_t *rng, uint32_t nslots, int32_t first,
                         int32_t nthreads, const uint32_t *in_queue, uint32_t *out_queue, int32_t max_steps,
                         int32_t use_weights, int32_t scatter_first, uint32_t *scratch, hipStream_t stream,
@@ -4162,6 +4340,7 @@ static int launch_chunk(const chr_geometry *g, const chr_photons *ph, uint32_t *
     a.work = nullptr;
     a.prio = 0;
     a.pair = pair_walk_enabled() ? 1u : 0u;
+    a.walk_up = walk_up_enabled() ? 1u : 0u;
     if (ev0) CHR_HIP_CHECK(hipEventRecord(ev0, stream));
     hipLaunchKernelGGL(select_variant(g), dim3(grid_for(nthreads)), dim3(BLOCK), 0, stream,
                        (const DevGeom *)g->d_dev, a);
@@ -4229,6 +4408,12 @@ static bool trace_steps();
 // default 1: walk_pair with an idle wave of the workgroup as tester)
 static bool pair_walk_enabled() {
     const char *e = getenv("CHR_PAIR_WALK");
+    return !(e && e[0] == '0');
+}
+// CHR_WALK_UP=0: the tail's lone walks from the root (A/B; default 1: a walk with a
+// previous hit climbs from that hit's leaf, walk_lone<true>, ahead of the pair walk)
+static bool walk_up_enabled() {
+    const char *e = getenv("CHR_WALK_UP");
     return !(e && e[0] == '0');
 }
 
@@ -4323,6 +4508,7 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
     a.work = nullptr;
     a.prio = 0;
     a.pair = pair_walk_enabled() ? 1u : 0u;
+    a.walk_up = walk_up_enabled() ? 1u : 0u;
     RayEnrol fe{nullptr, nullptr, nullptr, nullptr};
     const uint32_t threads = std::min(cap, (n + 63u) & ~63u);
     const StepVariant sv = select_step_variant(g);
@@ -4422,7 +4608,8 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
         a.hits = hits;
         a.max_steps = 1;
         if (sc && sc->rng_ready) CHR_HIP_CHECK(hipStreamWaitEvent(stream, sc->rng_ready, 0));
-        hipLaunchKernelGGL(sv.shade, dim3(grid_for(threads)), dim3(BLOCK), 0, stream, (const DevGeom *)g->d_dev, a, cap);
+        hipLaunchKernelGGL(sv.shade, dim3(grid_for(threads)), dim3(BLOCK), phys_lds_bytes(g->dev, SHADE_PHYS_WORDS), stream,
+                           (const DevGeom *)g->d_dev, a, cap);
     }
     if (split_out) *split_out = split;
     if (tail && sc && sc->tail_stream) {   // the tail on its own stream (chr_propagate_batches)
@@ -4454,7 +4641,8 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
         at.max_steps = sc->remaining;
         at.want = STEP_TAIL;
         at.work = tail_work_queue(sv, sc, use_weights, cap) ? next : nullptr;
-        hipLaunchKernelGGL(sv.tail, dim3(tail_grid(sv, threads, at.work != nullptr)), dim3(BLOCK), 0, ts,
+        hipLaunchKernelGGL(sv.tail, dim3(tail_grid(sv, threads, at.work != nullptr)), dim3(BLOCK),
+                           phys_lds_bytes(g->dev, TAIL_PHYS_WORDS), ts,
                            (const DevGeom *)g->d_dev, at, cap);
         if (sc->evt_tail1) CHR_HIP_CHECK(hipEventRecord(sc->evt_tail1, ts));
         launch_mask_scan(masks, nwords, offsets, bsums, out_queue, counters + 1, nullptr, stream, dev_n, mode, STEP_TAIL,
@@ -4472,7 +4660,8 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
         a.max_steps = sc ? sc->remaining : max_steps;
         a.want = STEP_TAIL;
         a.work = (sc && next && tail_work_queue(sv, sc, use_weights, cap)) ? next : nullptr;
-        hipLaunchKernelGGL(sv.tail, dim3(tail_grid(sv, threads, a.work != nullptr)), dim3(BLOCK), 0, stream,
+        hipLaunchKernelGGL(sv.tail, dim3(tail_grid(sv, threads, a.work != nullptr)), dim3(BLOCK),
+                           phys_lds_bytes(g->dev, TAIL_PHYS_WORDS), stream,
                            (const DevGeom *)g->d_dev, a, cap);
     } else if (!split) {
         hipLaunchKernelGGL(sv.fn, dim3(grid_for(threads)), dim3(BLOCK), 0, stream, (const DevGeom *)g->d_dev, a, cap);
@@ -5377,6 +5566,30 @@ extern "C" int chr_watch_set(uint32_t photon, const float *d_pos_array) {
 #endif
 }
 
+extern "C" int chr_watch_ray(const float *h_origin, uint32_t *h_events, uint32_t max_events, uint32_t *nevents) {
+#ifdef CHR_DEVICE_PROFILE
+    CHR_HIP_CHECK(hipDeviceSynchronize());
+    if (h_origin) {   // arm: the walk of the ray with this origin (bit-exact) is logged
+        const uint32_t on = 1u, zero = 0u;
+        CHR_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(chr::chr_wray_o), h_origin, 3 * sizeof(float)));
+        CHR_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(chr::chr_wev_n), &zero, sizeof(zero)));
+        CHR_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(chr::chr_wray_on), &on, sizeof(on)));
+        return CHR_OK;
+    }
+    if (!h_events || !nevents) return chr::fail(CHR_ERR_INVALID, "watch_ray: bad arguments");
+    uint32_t n = 0;
+    CHR_HIP_CHECK(hipMemcpyFromSymbol(&n, HIP_SYMBOL(chr::chr_wev_n), sizeof(n)));
+    *nevents = n;
+    uint32_t k = n < max_events ? n : max_events;
+    if (k > chr::CHR_WEV_MAX) k = chr::CHR_WEV_MAX;
+    if (k) CHR_HIP_CHECK(hipMemcpyFromSymbol(h_events, HIP_SYMBOL(chr::chr_wev_buf), sizeof(uint32_t) * 8 * k));
+    return CHR_OK;
+#else
+    (void)h_origin; (void)h_events; (void)max_events; (void)nevents;
+    return chr::fail(CHR_ERR_INVALID, "photon watch: load libchroma_amd_prof.so (CHROMA_DEVICE_PROFILE=1)");
+#endif
+}
+
 extern "C" int chr_watch_fetch(uint32_t *h_out, uint32_t max_records, uint32_t *nrecords) {
 #ifdef CHR_DEVICE_PROFILE
     if (!h_out || !nrecords) return chr::fail(CHR_ERR_INVALID, "watch_fetch: bad arguments");
@@ -5399,7 +5612,9 @@ namespace chr {
 // pair walk on two (walker 1: wave 0 walks, wave 1 tests), each ray reps times;
 // walker 2: the pair walk with a 2-poll handshake budget, so handshakes are lost
 // (the tail kernel's recovery path: the walk again with walk_lone, no more
-// pairing in the workgroup once aborted)
+// pairing in the workgroup once aborted); walker 3: walk_up from an arbitrary node
+// (ray r: node (r * 2654435761) mod nodes -- any start covers the tree once);
+// walker 4: walk_up from the leaf node of a given record (8-word rays: + record)
 __global__ __launch_bounds__(128) void walk_lone_timing_kernel(const DevGeom *__restrict__ gdev, const float *rays,
                                                                uint32_t n, uint32_t reps, uint32_t *out,
                                                                int32_t walker) {
@@ -5415,8 +5630,8 @@ __global__ __launch_bounds__(128) void walk_lone_timing_kernel(const DevGeom *__
         box[PB_ABORT] = 0u;
     }
     __syncthreads();
-    if (threadIdx.x >= 64) {   // the tester wave (walker 1), else idle
-        if (walker == 0) return;
+    if (threadIdx.x >= 64) {   // the tester wave (walkers 1, 2), else idle
+        if (walker == 0 || walker >= 3) return;
         while (true) {
             uint32_t st = PS_IDLE;
             for (uint32_t i = 0; i < PAIR_SPIN_MAX * 8u; ++i) {
@@ -5433,16 +5648,21 @@ __global__ __launch_bounds__(128) void walk_lone_timing_kernel(const DevGeom *__
         }
     }
     for (uint32_t r = blockIdx.x; r < n; r += gridDim.x) {
-        const float *ry = rays + 7 * (size_t)r;
+        const float *ry = rays + (walker == 4 ? 8 : 7) * (size_t)r;
         const V3 o = v3(ry[0], ry[1], ry[2]), d = v3(ry[3], ry[4], ry[5]);
         const uint32_t last = __float_as_uint(ry[6]);
+        uint32_t start = (uint32_t)(((unsigned long long)r * 2654435761ull) % g.nwnodes);
+        if (walker == 4) start = gld(reinterpret_cast<const uint32_t *>(g.wtri + 4 * (size_t)__float_as_uint(ry[7])) + 15);
         for (uint32_t k = 0; k < reps; ++k) {
             float sd;
             uint32_t it = 0;
             const unsigned long long t0 = __builtin_amdgcn_s_memrealtime(), c0 = __builtin_amdgcn_s_memtime();
             bool lost = false;
-            const bool pair = walker != 0 && lds_ld(box + PB_ABORT) == 0u;
-            int tri = pair ? walk_pair(g, top, o, d, last, LdsFlat{(CHR_LDS uint32_t *)stacks}, TAIL_STACK * 8,
+            const bool pair = (walker == 1 || walker == 2) && lds_ld(box + PB_ABORT) == 0u;
+            int tri = walker >= 3 ? walk_lone<true>(g, o, d, last, LdsFlat{(CHR_LDS uint32_t *)stacks}, TAIL_STACK * 8,
+                                                    LdsFlat{(CHR_LDS uint32_t *)tris}, overflow, sd, it, __builtin_inff(),
+                                                    0xFFFFFFFFu, -1, __builtin_inff(), start | WIDE_CHAIN_MORE)
+                    : pair ? walk_pair(g, top, o, d, last, LdsFlat{(CHR_LDS uint32_t *)stacks}, TAIL_STACK * 8,
                                        (CHR_LDS uint32_t *)tris, 0u, box, walker == 2 ? 2u : PAIR_SPIN_MAX, overflow,
                                        sd, it, lost)
                            : walk_lone(g, o, d, last, LdsFlat{(CHR_LDS uint32_t *)stacks}, TAIL_STACK * 8,
@@ -5460,7 +5680,7 @@ __global__ __launch_bounds__(128) void walk_lone_timing_kernel(const DevGeom *__
             }
         }
     }
-    if (walker != 0) {
+    if (walker == 1 || walker == 2) {
         lds_release();
         lds_st(box + PB_STATE, PS_EXIT);
     }
@@ -5470,7 +5690,7 @@ __global__ __launch_bounds__(128) void walk_lone_timing_kernel(const DevGeom *__
 
 extern "C" int chr_walk_lone_timing(const chr_geometry *g, const float *d_rays, uint32_t n, uint32_t reps,
                                     uint32_t nwaves, int32_t walker, uint32_t *d_out, void *stream) {
-    if (!g || !d_rays || !d_out || nwaves == 0 || reps == 0 || walker < 0 || walker > 2)
+    if (!g || !d_rays || !d_out || nwaves == 0 || reps == 0 || walker < 0 || walker > 4)
         return chr::fail(CHR_ERR_INVALID, "chr_walk_lone_timing: bad argument");
     if (g->dev.nwnodes == 0) return chr::fail(CHR_ERR_INVALID, "chr_walk_lone_timing: geometry has no wide BVH");
     if (n == 0) return CHR_OK;

@@ -442,6 +442,23 @@ int wide_validate(const chr_geometry_desc *d, const chr_wide_bvh_desc *w, WideCh
     }
     if (7 * (maxd + 1) + 1 > (uint32_t)WIDE_STACK)
         return chr::fail(CHR_ERR_INVALID, "wide BVH: depth %u exceeds the walk's stack", maxd);
+    if (nn > WIDE_NODE_MASK) return chr::fail(CHR_ERR_INVALID, "wide BVH: %u nodes (walk_up needs < 2^27)", nn);
+    // the tree upward: parents (each child has exactly one: the builder's children are
+    // disjoint ranges) and every record's leaf node
+    out.parent.assign(nn, WIDE_NO_PARENT);
+    out.rec_node.assign(nrec, 0u);
+    uint32_t *par = out.parent.data(), *rn = out.rec_node.data();
+#pragma omp parallel for num_threads(chr::host_threads()) schedule(static)
+    for (int64_t i = 0; i < (int64_t)nn; ++i) {
+        const WideNode &W = N[i];
+        for (int k = 0; k < 8; ++k) {
+            const uint8_t kind = W.kind[k];
+            if (kind == WIDE_INNER)
+                par[W.child_base + W.off[k]] = (uint32_t)i | ((uint32_t)k << 28) | WIDE_ANCESTOR;
+            else if (kind != 0)
+                for (uint32_t t = 0; t < kind; ++t) rn[W.tri_base + W.off[k] + t] = (uint32_t)i;
+        }
+    }
     // records: triangle ids in range, ranks a permutation of [0, nrec)
     out.rank_rec.assign(nrec, 0xFFFFFFFFu);
     int bad = 0;
@@ -497,16 +514,26 @@ void wide_fill_records(const chr_geometry_desc *d, const chr_wide_bvh_desc *w, c
         R.rank = w->h_rec_rank[i];
         std::memcpy(R.leaf, &c.leafq[3 * (size_t)t], 12);
         R.code = d->h_material_codes ? d->h_material_codes[t] : 0u;
-        R.pad = 0;
+        R.pad = c.rec_node.empty() ? 0u : c.rec_node[i];
     }
 }
 
-void wide_fill_node_slots(const chr_wide_bvh_desc *w, size_t first, size_t n, uint8_t *out) {
+void wide_fill_node_slots(const chr_wide_bvh_desc *w, const WideCheck &c, size_t first, size_t n, uint8_t *out) {
     const WideNode *N = static_cast<const WideNode *>(w->h_nodes);
+    const uint32_t *par = c.parent.data();
 #pragma omp parallel for num_threads(chr::host_threads()) schedule(static)
     for (int64_t j = 0; j < (int64_t)n; ++j) {
-        std::memcpy(out + 128 * (size_t)j, N + first + (size_t)j, sizeof(WideNode));
-        std::memset(out + 128 * (size_t)j + sizeof(WideNode), 0, 128 - sizeof(WideNode));
+        uint8_t *slot = out + 128 * (size_t)j;
+        std::memcpy(slot, N + first + (size_t)j, sizeof(WideNode));
+        uint32_t chain[8];
+        uint32_t a = (uint32_t)(first + (size_t)j);
+        for (int m = 0; m < 8; ++m) {
+            const uint32_t p = a == WIDE_NO_PARENT || c.parent.empty() ? WIDE_NO_PARENT : par[a];
+            chain[m] = p;
+            a = p == WIDE_NO_PARENT ? WIDE_NO_PARENT : (p & WIDE_NODE_MASK);
+        }
+        if (a != WIDE_NO_PARENT && !c.parent.empty() && par[a] != WIDE_NO_PARENT) chain[7] |= WIDE_CHAIN_MORE;
+        std::memcpy(slot + sizeof(WideNode), chain, sizeof(chain));
     }
 }
 

@@ -86,12 +86,28 @@ void wide_compact(const WideBVH &b, std::vector<uint32_t> &rec_id, std::vector<u
 struct WideCheck {
     std::vector<uint32_t> rank_rec;
     std::vector<uint32_t> leafq;
+    // the tree upward (walk_up): each node's parent as an ancestor word (below;
+    // WIDE_NO_PARENT at the root), each record's leaf node
+    std::vector<uint32_t> parent;
+    std::vector<uint32_t> rec_node;
 };
+// A device node slot (128 bytes) holds the 96-byte node and, in words 24..31, its
+// first 8 ancestors, parent first, as ancestor words: the ancestor's index (bits
+// 0-26) | WIDE_CHAIN_MORE (bit 27: set on the 8th when it has ancestors of its own,
+// which its slot continues) | the slot of the previous node of the chain in it
+// (bits 28-30: the child walk_up skips there) | WIDE_ANCESTOR (bit 31);
+// WIDE_NO_PARENT past the root.  A triangle record's last word (pad) is the node
+// whose leaf holds it.  walk_up starts a walk at the leaf of the previous hit and
+// climbs (node indices < 2^27).
+constexpr uint32_t WIDE_NO_PARENT = 0xFFFFFFFFu;
+constexpr uint32_t WIDE_NODE_MASK = 0x07FFFFFFu;
+constexpr uint32_t WIDE_CHAIN_MORE = 1u << 27;
+constexpr uint32_t WIDE_ANCESTOR = 1u << 31;
 int wide_validate(const chr_geometry_desc *d, const chr_wide_bvh_desc *w, WideCheck &out);
 // the 64-byte triangle records [first, first+n) of a validated compact form
 void wide_fill_records(const chr_geometry_desc *d, const chr_wide_bvh_desc *w, const WideCheck &c, size_t first,
                        size_t n, WideTri *out);
 // 96-byte nodes [first, first+n) into 128-byte slots (the device layout)
-void wide_fill_node_slots(const chr_wide_bvh_desc *w, size_t first, size_t n, uint8_t *out);
+void wide_fill_node_slots(const chr_wide_bvh_desc *w, const WideCheck &c, size_t first, size_t n, uint8_t *out);
 
 }  // namespace chr

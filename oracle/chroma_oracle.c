@@ -233,6 +233,17 @@ static int intersect_node(f3 noid, f3 inv, const Node *node, float min_distance)
     return 1;
 }
 
+/* Diagnostic (orc_undershoot): triangles whose Moller-Trumbore hit distance
+ * lies BEFORE the entry distance of their own reference leaf box (a float
+ * false positive on a grazing triangle): count, largest absolute and relative
+ * undershoot (box entry - hit distance) seen by intersect_mesh. */
+static double g_under_abs = 0.0, g_under_rel = 0.0;
+static uint64_t g_under_n = 0;
+EXPORT void orc_undershoot(double *out) {
+    out[0] = (double)g_under_n; out[1] = g_under_abs; out[2] = g_under_rel;
+    g_under_n = 0; g_under_abs = 0.0; g_under_rel = 0.0;
+}
+
 #define STACK_SIZE 1000
 /* mesh.h:45-126: DFS over groups; within a group ascending child index; an
  * internal child's group is pushed, the last pushed group is popped first;
@@ -265,6 +276,15 @@ static int intersect_mesh(Geo *g, f3 origin, f3 direction, float *min_distance, 
                         g->tris_tested++;
                         get_triangle(g, node.child, &v0, &v1, &v2);
                         if (intersect_triangle(origin, direction, v0, v1, v2, &distance)) {
+                            float bd;
+                            if (intersect_box(noid, inv, node.lower, node.upper, &bd) && bd > distance) {
+#pragma omp critical(orc_under)
+                                {
+                                    g_under_n++;
+                                    if (bd - distance > g_under_abs) g_under_abs = bd - distance;
+                                    if ((bd - distance) / distance > g_under_rel) g_under_rel = (bd - distance) / distance;
+                                }
+                            }
                             if (triangle_index == -1 || distance < *min_distance) {
                                 triangle_index = (int)node.child;
                                 *min_distance = distance;

@@ -45,6 +45,7 @@ def lib():
         l.orc_set_watch.argtypes = [ctypes.c_int64, vp, u32]
         l.orc_watch_count.restype = u32
         l.orc_intersect_rays.argtypes = [vp, i32, vp, vp, vp, vp, vp]
+        l.orc_undershoot.argtypes = [vp]
         _lib = l
     return _lib
 
@@ -104,6 +105,14 @@ def intersect_rays(packed, origins, directions, last_hit):
     desc = packed.desc()
     lib().orc_intersect_rays(ctypes.addressof(desc), len(o), _p(o), _p(d), _p(last), _p(dist), _p(tri))
     return dist, tri
+
+
+def undershoot():
+    """(count, max absolute, max relative) of Moller-Trumbore hits before their
+    own reference leaf box's entry distance since the last call (diagnostic)."""
+    out = np.zeros(3, np.float64)
+    lib().orc_undershoot(_p(out))
+    return int(out[0]), float(out[1]), float(out[2])
 
 
 class HostPhotons(object):

@@ -196,3 +196,72 @@ def test_c3_29k_detector_parity(cuda, geo29k):
     _check(got[0], hosts[0], geo, 'C3 29k 1.1M')
     assert np.array_equal(rng.reshape(-1), st.reshape(-1))
     assert ((hosts[0].flags & 4) != 0).sum() > 10000
+
+
+# BENCH_r05's parity failure: photon 9,043,377 of the bench's
+# 9,897,030-photon parity sample, batch 1, second step (tools/parity_watch.py,
+# profiles/r06/parity_watch).  Its ray meets triangle 30,327,113 only through a
+# float32 Moller-Trumbore false positive: the hit is reported at 36,510.26 mm
+# while the exact ray meets that triangle's plane 7% outside it and enters the
+# triangle's reference leaf box only at 36,511.24 mm.  The reference DFS meets it
+# first and keeps it (the neighbour at 36,510.91 mm does not replace it); round 5's
+# walks culled its box against the neighbour and returned the neighbour.
+FP_ORIGIN = (-1942.692138671875, 16390.626953125, -1976.0341796875)
+FP_DIR = (-0.24864476919174194, -0.8455895781517029, 0.47239193320274353)
+FP_TRIANGLE, FP_DISTANCE = 30327113, 36510.26171875
+
+
+@pytest.mark.timeout(1200)
+def test_false_positive_hit_29k(cuda, geo29k):
+    """The false-positive ray on every GPU walker, against the oracle (the
+    reference DFS): the one-step launch's trace_kernel (2^17 copies: binned
+    first step), the tail kernel (4,000 copies: grouped walks, walk_lone and
+    the pair walk), the fused walk of distance_to_mesh, and walk_lone / the
+    pair walk / the pair walk with lost handshakes in isolation."""
+    import ctypes
+    import torch
+    from chroma import gpu
+    from chroma.event import Photons
+    from chroma.gpu import _native, gpuarray as ga, wide_bvh
+    from chroma.gpu.packing import PackedGeometry
+    from chroma.gpu.tools import current_stream
+    packed = PackedGeometry(geo29k)
+    o = np.array([FP_ORIGIN], np.float32)
+    d = np.array([FP_DIR], np.float32)
+    dist, tri = oracle.intersect_rays(packed, o, d, np.array([-1], np.int32))
+    assert (int(tri[0]), float(dist[0])) == (FP_TRIANGLE, FP_DISTANCE)   # the oracle pinned on this ray
+    gdet = gpu.GPUDetector(geo29k)
+    # whole steps: HIP == oracle on copies of the ray (one step, every copy its own RNG slot)
+    for n in (1 << 17, 4000):
+        ph = Photons(np.repeat(o, n, 0), np.repeat(d, n, 0), np.tile(np.float32([[1, 0, 0]]), (n, 1)),
+                     np.full(n, 420.0, np.float32))
+        gp = gpu.GPUPhotons(ph, copy_flags=True, copy_triangles=False, copy_weights=False)
+        rng = gpu.get_rng_states(NSLOTS, seed=1)
+        gp.propagate(gdet, rng, nthreads_per_block=NTPB, max_blocks=MAXB, max_steps=1)
+        got = gp.get()
+        host = oracle.HostPhotons(ph)
+        host.last_hit_triangles[:] = -1
+        host.weights[:] = 1.0
+        oracle.propagate(packed, host, oracle.rng_init(NSLOTS, seed=1), NSLOTS, NTPB, MAXB, 1)
+        _check(got, host, geo29k, 'false-positive ray x %d' % n)
+        assert (host.last_hit_triangles == FP_TRIANGLE).sum() > n // 4   # ~half reach it unscattered
+    # the fused walk (distance_to_mesh)
+    dd = ga.to_gpu(np.full(1, -7.0, np.float32))
+    _native.call('chr_distance_to_mesh', gdet._handle, 1, ga.to_gpu(o.reshape(-1)).gpudata,
+                 ga.to_gpu(d.reshape(-1)).gpudata, dd.gpudata, current_stream())
+    torch.cuda.synchronize()
+    assert float(dd.get()[0]) == FP_DISTANCE
+    # walk_lone, the pair walk, the pair walk losing its handshakes
+    wide, _ = wide_bvh.obtain(geo29k.bvh, gdet.packed)
+    rays = np.zeros((64, 7), np.float32)
+    rays[:, 0:3] = o
+    rays[:, 3:6] = d
+    rays[:, 6] = np.int32(-1).view(np.float32)
+    dr = ga.to_gpu(rays.reshape(-1))
+    for walker in (0, 1, 2):
+        res = ga.zeros(64 * 4 + 1, np.uint32)
+        _native.call('chr_walk_lone_timing', gdet._handle, dr.gpudata, 64, 1, 8, walker, res.gpudata,
+                     current_stream())
+        torch.cuda.synchronize()
+        recs = res.get()[:-1].reshape(64, 4)[:, 0].view(np.int32)
+        assert np.all(np.asarray(wide.rec_id)[recs] == FP_TRIANGLE), 'walker %d' % walker

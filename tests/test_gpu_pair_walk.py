@@ -93,3 +93,31 @@ def test_pair_walk_lost_handshake_recovers(cuda, small_detector):
     assert ov0 == 0 and (ov2 & 0xFFFFF) == 0
     assert ov2 >> 20 >= 1                      # the recovery path ran
     assert np.array_equal(lone, forced)
+
+
+def test_walk_up_equals_lone(cuda, small_detector, small_packed):
+    """walk_up (the tail's lone walk started at the previous hit's leaf, climbing
+    the ancestor chains in the node slots): from ANY start node it reaches every
+    node once, so it returns walk_lone's record on every ray -- walker 3 starts
+    ray r at node (r * 2654435761) mod nodes; walker 4 at the leaf of the ray's
+    previous hit record (the tail's use), rays restarting on that surface."""
+    from chroma import gpu
+    from chroma.gpu import wide_bvh
+    det = gpu.GPUDetector(small_detector)
+    rays = _rays(512, seed=23)
+    lone, ov0 = _walk(det, rays, 0, 64)
+    up, ov3 = _walk(det, rays, 3, 64)
+    assert ov0 == 0 and ov3 == 0
+    assert np.array_equal(lone, up)
+    # from the previous hit's leaf, that hit excluded
+    rec_id = np.asarray(wide_bvh.build(small_packed).rec_id)
+    first, _ = _walk(det, rays, 0, 64, reps=1)
+    hit = first[:, 0] >= 0
+    rr = np.zeros((int(hit.sum()), 8), np.float32)
+    rr[:, :7] = rays[hit]
+    rr[:, 6] = rec_id[first[hit, 0]].astype(np.int32).view(np.float32)
+    rr[:, 7] = first[hit, 0].astype(np.int32).view(np.float32)
+    lone2, _ = _walk(det, np.ascontiguousarray(rr[:, :7]), 0, 64)
+    up2, ov4 = _walk(det, rr, 4, 64)
+    assert ov4 == 0 and np.array_equal(lone2, up2)
+    assert (up2[:, 0] >= 0).sum() > len(rr) // 2
