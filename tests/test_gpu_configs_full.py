@@ -244,7 +244,10 @@ def test_false_positive_hit_29k(cuda, geo29k):
         host.weights[:] = 1.0
         oracle.propagate(packed, host, oracle.rng_init(NSLOTS, seed=1), NSLOTS, NTPB, MAXB, 1)
         _check(got, host, geo29k, 'false-positive ray x %d' % n)
-        assert (host.last_hit_triangles == FP_TRIANGLE).sum() > n // 4   # ~half reach it unscattered
+        # the false-positive hit decides the photon's bulk material (material1 = 1 from that
+        # triangle's side, 1.75 m absorption length): nearly every copy is absorbed on the
+        # way, against ~30% with the neighbour's (water, 104 m)
+        assert ((host.flags & 2) != 0).sum() > 0.9 * n
     # the fused walk (distance_to_mesh)
     dd = ga.to_gpu(np.full(1, -7.0, np.float32))
     _native.call('chr_distance_to_mesh', gdet._handle, 1, ga.to_gpu(o.reshape(-1)).gpudata,
