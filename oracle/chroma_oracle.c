@@ -1095,6 +1095,42 @@ EXPORT int orc_intersect_rays(const chr_geometry_desc *d, int n, const float *or
     return 0;
 }
 
+/* Diagnostic: every triangle intersect_triangle reports for one ray, whatever the
+ * BVH (brute force over the mesh): up to cap (triangle, distance, leaf box hit,
+ * leaf box entry) -- the leaf box from the reference leaf node of each triangle
+ * (leaf_node[t], -1: none).  Returns the count. */
+EXPORT int orc_ray_all_hits(const chr_geometry_desc *d, const float *origin, const float *direction,
+                            const int32_t *leaf_node, int32_t *tri, float *dist, int32_t *box_hit, float *box_d,
+                            int cap) {
+    init_once();
+    Geo g = {d, 0, 0, 0, 0, 0};
+    f3 o = mk(origin[0], origin[1], origin[2]);
+    f3 dir = mk(direction[0], direction[1], direction[2]);
+    f3 noid = mk(-o.x / dir.x, -o.y / dir.y, -o.z / dir.z);
+    f3 inv = mk(1.0f / dir.x, 1.0f / dir.y, 1.0f / dir.z);
+    int n = 0;
+    for (uint32_t t = 0; t < d->ntriangles; ++t) {
+        f3 v0, v1, v2;
+        float dd;
+        get_triangle(&g, t, &v0, &v1, &v2);
+        if (!intersect_triangle(o, dir, v0, v1, v2, &dd)) continue;
+        if (n < cap) {
+            tri[n] = (int32_t)t;
+            dist[n] = dd;
+            box_hit[n] = -1;
+            box_d[n] = -1.0f;
+            if (leaf_node && leaf_node[t] >= 0) {
+                Node nd = get_node(&g, (uint32_t)leaf_node[t]);
+                float bd = -1.0f;
+                box_hit[n] = intersect_box(noid, inv, nd.lower, nd.upper, &bd);
+                box_d[n] = bd;
+            }
+        }
+        n++;
+    }
+    return n;
+}
+
 static void chunk_iter(int nelements, int ntpb, int maxb, int first, int *count) {
     (void)first;
     int left = nelements;

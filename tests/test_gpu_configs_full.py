@@ -250,8 +250,8 @@ def test_false_positive_hit_29k(cuda, geo29k):
         assert ((host.flags & 2) != 0).sum() > 0.9 * n
     # the fused walk (distance_to_mesh)
     dd = ga.to_gpu(np.full(1, -7.0, np.float32))
-    _native.call('chr_distance_to_mesh', gdet._handle, 1, ga.to_gpu(o.reshape(-1)).gpudata,
-                 ga.to_gpu(d.reshape(-1)).gpudata, dd.gpudata, current_stream())
+    go, gd = ga.to_gpu(o.reshape(-1)), ga.to_gpu(d.reshape(-1))   # held: the call reads them asynchronously
+    _native.call('chr_distance_to_mesh', gdet._handle, 1, go.gpudata, gd.gpudata, dd.gpudata, current_stream())
     torch.cuda.synchronize()
     assert float(dd.get()[0]) == FP_DISTANCE
     # walk_lone, the pair walk, the pair walk losing its handshakes
