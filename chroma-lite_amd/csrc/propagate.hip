@@ -1560,8 +1560,8 @@ struct PropagateArgs {
                                        // batches' tail, the critical path beside the next batch's walk)
     uint32_t pair;                     // tail kernel: a lone walk takes an idle wave of its workgroup as
                                        // triangle tester (walk_pair; CHR_PAIR_WALK=0: walk_lone alone)
-    uint32_t walk_up;                  // tail kernel: a lone walk with a previous hit starts at that hit's
-                                       // leaf and climbs (walk_lone<true>; CHR_WALK_UP=0: from the root)
+    uint32_t walk_up;                  // tail kernel: a walk with a previous hit starts at that hit's leaf
+                                       // and climbs (CHR_WALK_UP: 0 none, 1 lone and grouped, 2 lone only)
     uint32_t want;
     // tail kernel, work-queue mode (nullptr: group g runs queue positions g, g + cap, ...): a
     // zeroed counter the photon groups take queue positions from, for queues no longer than
@@ -1779,9 +1779,15 @@ constexpr uint32_t TAIL_PHYS_WORDS = 8192;     // 32 KB: 2 tail workgroups (+ 40
 // The copy is the launch's dynamic LDS, sized to the geometry's hot words (the
 // demo and 29k detectors: a few KB of their 32 / 48 KB caps), so a workgroup holds
 // only the LDS its geometry needs: host and kernel apply the same rule.
+#ifdef CHR_STATIC_PHYS_LDS   // (build-time A/B: the round-5 static arrays at the caps)
+__host__ __device__ __forceinline__ uint32_t phys_lds_bytes(const DevGeom &, uint32_t) { return 0u; }
+#define CHR_PHYS_LDS(name, cap) __shared__ uint4 name[(cap) / 4]
+#else
 __host__ __device__ __forceinline__ uint32_t phys_lds_bytes(const DevGeom &g, uint32_t cap_words) {
     return g.phys && g.phys_hot_words <= cap_words ? g.phys_hot_words * 4u : 0u;
 }
+#define CHR_PHYS_LDS(name, cap) extern __shared__ uint4 name[]
+#endif
 __device__ __forceinline__ DevGeom phys_cache(const DevGeom &g, uint4 *lds, uint32_t cap_words) {
     DevGeom gl = g;
     if (g.phys && g.phys_hot_words <= cap_words) {   // workgroup-uniform
@@ -1840,7 +1846,7 @@ template <int MINW, bool WIRES = true>
 __global__ __launch_bounds__(BLOCK, MINW) void shade_kernel(const DevGeom *__restrict__ gdev, PropagateArgs a,
                                                             uint32_t cap) {
     if (a.mode && *a.mode != a.want) return;
-    extern __shared__ uint4 phys_lds[];   // phys_lds_bytes(SHADE_PHYS_WORDS) of dynamic LDS
+    CHR_PHYS_LDS(phys_lds, SHADE_PHYS_WORDS);   // phys_lds_bytes(SHADE_PHYS_WORDS) of dynamic LDS
     const DevGeom g = phys_cache(*gdev, phys_lds, SHADE_PHYS_WORDS);
     const uint32_t slot = blockIdx.x * BLOCK + threadIdx.x;
     const uint32_t n = a.dev_n ? *a.dev_n - 1u : (uint32_t)a.nthreads;
@@ -2040,11 +2046,11 @@ struct LoneProf<true> {
 // GS > 0: the segment width as a compile-time constant (GS = 64: one walk on
 // the whole wave, the tail's lone long-lived photon -- segment masks and
 // offsets fold away); GS = 0: the width Gs_in at run time.
-template <int GS, class M>
+template <int GS, class M, bool UP = false>
 __device__ __forceinline__ int walk_segment(const DevGeom &g, bool act, V3 o, V3 d, uint32_t last, int Gs_in, M stk, int cap, M tlist,
                             const TopNodes &top, uint32_t &overflow, float &min_distance, uint32_t &iters,
                             float best = __builtin_inff(), uint32_t best_rank = 0xFFFFFFFFu, int best_id = -1,
-                            float best_bd = __builtin_inff()) {
+                            float best_bd = __builtin_inff(), uint32_t start = 0u) {
     const int Gs = GS ? GS : Gs_in;
     constexpr uint32_t INVALID = 0xFFFFFFFFu;
     constexpr unsigned long long NONE = ~0ull;
@@ -2073,7 +2079,9 @@ __device__ __forceinline__ int walk_segment(const DevGeom &g, bool act, V3 o, V3
     const V3 noid = v3(-o.x / d.x, -o.y / d.y, -o.z / d.z);
     const V3 inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
     const RaySlab r = make_slab(o, noid, inv);
-    uint32_t cur = (act && L < 8u) ? 0u : INVALID;   // cursor 0 starts at the root
+    // cursor 0 starts at the root (UP: at start, walk_lone<true>'s climb; per segment)
+    uint32_t cur = (act && L < 8u) ? (UP ? start : 0u) : INVALID;
+    uint32_t chainw = INVALID;                        // UP: ancestor word k of the cursor's node (lane k)
     float cur_t = 0.0f;
     int sp = 0;
     uint32_t Tp = 0;                                  // triangles listed by the previous iteration
@@ -2161,14 +2169,17 @@ __device__ __forceinline__ int walk_segment(const DevGeom &g, bool act, V3 o, V3
         const float4 *rr;
         if constexpr (GS == 64) {
             const uint32_t trec = has_tri ? tlist[pb * TAIL_TRI + L] : 0u;
-            if (cur != INVALID) load_node(g, top, cur, h, a1, a2, a3, a4, a5);
+            if (cur != INVALID) load_node(g, top, UP ? cur & WIDE_NODE_MASK : cur, h, a1, a2, a3, a4, a5);
+            if (UP && cur != INVALID) chainw = gld(reinterpret_cast<const uint32_t *>(g.wnodes + (size_t)g.wstride * (cur & WIDE_NODE_MASK)) + 24 + k);
             rr = g.wtri + 4 * (size_t)trec;
             if (has_tri) { r0 = gld(rr); r1 = gld(rr + 1); r2 = gld(rr + 2); r3 = gld(rr + 3); }
             lp.wait_loads();
             lp.tick(1);
         } else {
             h = make_uint4(0u, 0u, 0u, 0u); a1 = h; a2 = h; a3 = h; a4 = h; a5 = h;
-            if (cur != INVALID) load_node(g, top, cur, h, a1, a2, a3, a4, a5);
+            if (cur != INVALID) load_node(g, top, UP ? cur & WIDE_NODE_MASK : cur, h, a1, a2, a3, a4, a5);
+            if (UP && cur != INVALID)
+                chainw = gld(reinterpret_cast<const uint32_t *>(g.wnodes + (size_t)g.wstride * (cur & WIDE_NODE_MASK)) + 24 + k);
             r0 = make_float4(0.0f, 0.0f, 0.0f, 0.0f); r1 = r0; r2 = r0; r3 = r0;
             rr = nullptr;
             if (has_tri) {
@@ -2180,11 +2191,13 @@ __device__ __forceinline__ int walk_segment(const DevGeom &g, bool act, V3 o, V3
         bool inner = false, leafhit = false;
         float tk = 0.0f;
         uint32_t kind = 0, child = 0, first = 0;
+        const bool more = UP && cur != INVALID && (cur & WIDE_CHAIN_MORE) != 0u;
         if (cur != INVALID) {
             const V3 org = v3(__uint_as_float(h.x), __uint_as_float(h.y), __uint_as_float(h.z));
             const float sx = exp_scale(h.w), sy = exp_scale(h.w >> 8), sz = exp_scale(h.w >> 16);
             const int kk = (int)k;
             kind = byte_of(a4.z, a4.w, kk);
+            if (UP && (cur & WIDE_ANCESTOR) != 0u && ((cur >> 28) & 7u) == k) kind = 0u;   // the chain's child
             const float tnx = __builtin_fmaf(__builtin_fmaf(byte_f(r.negx ? a2.z : a1.x, r.negx ? a2.w : a1.y, kk), sx, org.x), r.inx, r.onx);
             const float tfx = __builtin_fmaf(__builtin_fmaf(byte_f(r.negx ? a1.x : a2.z, r.negx ? a1.y : a2.w, kk), sx, org.x), r.inx, r.ofx);
             const float tny = __builtin_fmaf(__builtin_fmaf(byte_f(r.negy ? a3.x : a1.z, r.negy ? a3.y : a1.w, kk), sy, org.y), r.iny, r.ony);
@@ -2224,6 +2237,24 @@ __device__ __forceinline__ int walk_segment(const DevGeom &g, bool act, V3 o, V3
             sp = cap;
         } else {
             sp += npush;
+        }
+        if constexpr (UP) {   // a chain onto the segment's stack (walk_lone<true>)
+            const bool cpush = more && chainw != WIDE_NO_PARENT;
+            const unsigned long long cm = __ballot(cpush) & segmask;
+            if (cm) {
+                const int nc = __popcll(cm);
+                const int cpos = sp + nc - 1 - __popcll(cm & below);
+                if (cpush && cpos < cap) {
+                    stk[2 * cpos] = chainw;
+                    stk[2 * cpos + 1] = 0u;
+                }
+                if (sp + nc > cap) {
+                    if (L == 0) overflow += (uint32_t)(sp + nc - cap);
+                    sp = cap;
+                } else {
+                    sp += nc;
+                }
+            }
         }
         cur = near;
         cur_t = near_t;
@@ -2997,7 +3028,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_tail_kernel(const DevGe
         box_s[PB_WORKERS] = BLOCK / 64;
         box_s[PB_ABORT] = 0u;
     }
-    extern __shared__ uint4 phys_lds[];   // phys_lds_bytes(TAIL_PHYS_WORDS) of dynamic LDS
+    CHR_PHYS_LDS(phys_lds, TAIL_PHYS_WORDS);   // phys_lds_bytes(TAIL_PHYS_WORDS) of dynamic LDS
     const DevGeom g = phys_cache(*gdev, phys_lds, TAIL_PHYS_WORDS);
     __shared__ uint4 top_lds[6 * TOP_NODES];   // 7 KB: 2 workgroups per CU hold 2 x 79 KB
     const TopNodes top = stage_top<BLOCK>(g, (CHR_LDS u32x4 *)top_lds, TOP_NODES);
@@ -3162,6 +3193,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_tail_kernel(const DevGe
                 o = v3(__shfl(p.pos.x, src), __shfl(p.pos.y, src), __shfl(p.pos.z, src));
                 dd = v3(__shfl(p.dir.x, src), __shfl(p.dir.y, src), __shfl(p.dir.z, src));
                 last = (uint32_t)__shfl(p.last_hit, src);
+                start = (uint32_t)__shfl((int)up_node, src);
             }
             const uint32_t seg0 = lane & ~(uint32_t)(Gs - 1);
             float sd;
@@ -3184,6 +3216,12 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_tail_kernel(const DevGe
                                         (threadIdx.x >> 6) * 2u * TAIL_TRI, box, PAIR_SPIN_MAX, overflow, sd, it, lost)
                      : Gs == 64
                          ? walk_lone(g, o, dd, last, LdsFlat{wstack}, TAIL_STACK * 8, LdsFlat{wtris}, overflow, sd, it)
+                     : a.walk_up == 1u   // grouped walks climb from their previous hit's leaf too
+                         ? walk_segment<0, LdsFlat, true>(g, act, o, dd, last, Gs,
+                                                          LdsFlat{wstack + seg0 / 8 * TAIL_STACK * 2}, TAIL_STACK * Gs / 8,
+                                                          LdsFlat{wtris + 4 * seg0}, top, overflow, sd, it,
+                                                          __builtin_inff(), 0xFFFFFFFFu, -1, __builtin_inff(),
+                                                          start == 0xFFFFFFFFu ? 0u : ((start & WIDE_NODE_MASK) | WIDE_CHAIN_MORE))
                          : walk_segment<0>(g, act, o, dd, last, Gs, LdsFlat{wstack + seg0 / 8 * TAIL_STACK * 2},
                                            TAIL_STACK * Gs / 8, LdsFlat{wtris + 4 * seg0}, top, overflow, sd, it);
             // a lost pair handshake: the tester's minimum may be partial -> the walk again, alone
@@ -4315,7 +4353,7 @@ static StepVariant select_step_variant(const chr_geometry *g) {
 
 // scratch layout (u32 words): [0] overflows [1] queue base [2..11] u64 walk counters [12..15] pad; masks (u64, 8-aligned); offsets
 static bool pair_walk_enabled();
-static bool walk_up_enabled();
+static uint32_t walk_up_mode();
 static int launch_chunk(const chr_geometry *g, const chr_photons *ph, uint32_t *rng, uint32_t nslots, int32_t first,
                         int32_t nthreads, const uint32_t *in_queue, uint32_t *out_queue, int32_t max_steps,
                         int32_t use_weights, int32_t scatter_first, uint32_t *scratch, hipStream_t stream,
@@ -4340,7 +4378,7 @@ static int launch_chunk(const chr_geometry *g, const chr_photons *ph, uint32_t *
     a.work = nullptr;
     a.prio = 0;
     a.pair = pair_walk_enabled() ? 1u : 0u;
-    a.walk_up = walk_up_enabled() ? 1u : 0u;
+    a.walk_up = walk_up_mode();
     if (ev0) CHR_HIP_CHECK(hipEventRecord(ev0, stream));
     hipLaunchKernelGGL(select_variant(g), dim3(grid_for(nthreads)), dim3(BLOCK), 0, stream,
                        (const DevGeom *)g->d_dev, a);
@@ -4410,11 +4448,12 @@ static bool pair_walk_enabled() {
     const char *e = getenv("CHR_PAIR_WALK");
     return !(e && e[0] == '0');
 }
-// CHR_WALK_UP=0: the tail's lone walks from the root (A/B; default 1: a walk with a
-// previous hit climbs from that hit's leaf, walk_lone<true>, ahead of the pair walk)
-static bool walk_up_enabled() {
+// CHR_WALK_UP=0: the tail's walks from the root (A/B; default 1: a walk with a
+// previous hit climbs from that hit's leaf -- walk_lone<true> ahead of the pair walk,
+// and the grouped walks, walk_segment<0, UP>; 2: the lone walks only)
+static uint32_t walk_up_mode() {
     const char *e = getenv("CHR_WALK_UP");
-    return !(e && e[0] == '0');
+    return e && (e[0] == '0' || e[0] == '2') ? (uint32_t)(e[0] - '0') : 1u;
 }
 
 static int slot_timing() {
@@ -4508,7 +4547,7 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
     a.work = nullptr;
     a.prio = 0;
     a.pair = pair_walk_enabled() ? 1u : 0u;
-    a.walk_up = walk_up_enabled() ? 1u : 0u;
+    a.walk_up = walk_up_mode();
     RayEnrol fe{nullptr, nullptr, nullptr, nullptr};
     const uint32_t threads = std::min(cap, (n + 63u) & ~63u);
     const StepVariant sv = select_step_variant(g);
@@ -5614,7 +5653,9 @@ namespace chr {
 // (the tail kernel's recovery path: the walk again with walk_lone, no more
 // pairing in the workgroup once aborted); walker 3: walk_up from an arbitrary node
 // (ray r: node (r * 2654435761) mod nodes -- any start covers the tree once);
-// walker 4: walk_up from the leaf node of a given record (8-word rays: + record)
+// walker 4: walk_up from the leaf node of a given record (8-word rays: + record);
+// walker 5: the grouped walk's climb (walk_segment<0, UP>, one 64-lane segment) from
+// walker 3's start
 __global__ __launch_bounds__(128) void walk_lone_timing_kernel(const DevGeom *__restrict__ gdev, const float *rays,
                                                                uint32_t n, uint32_t reps, uint32_t *out,
                                                                int32_t walker) {
@@ -5659,7 +5700,12 @@ __global__ __launch_bounds__(128) void walk_lone_timing_kernel(const DevGeom *__
             const unsigned long long t0 = __builtin_amdgcn_s_memrealtime(), c0 = __builtin_amdgcn_s_memtime();
             bool lost = false;
             const bool pair = (walker == 1 || walker == 2) && lds_ld(box + PB_ABORT) == 0u;
-            int tri = walker >= 3 ? walk_lone<true>(g, o, d, last, LdsFlat{(CHR_LDS uint32_t *)stacks}, TAIL_STACK * 8,
+            int tri = walker == 5 ? walk_segment<0, LdsFlat, true>(g, true, o, d, last, 64,
+                                                               LdsFlat{(CHR_LDS uint32_t *)stacks}, TAIL_STACK * 8,
+                                                               LdsFlat{(CHR_LDS uint32_t *)tris}, top, overflow, sd, it,
+                                                               __builtin_inff(), 0xFFFFFFFFu, -1, __builtin_inff(),
+                                                               start | WIDE_CHAIN_MORE)
+                    : walker >= 3 ? walk_lone<true>(g, o, d, last, LdsFlat{(CHR_LDS uint32_t *)stacks}, TAIL_STACK * 8,
                                                     LdsFlat{(CHR_LDS uint32_t *)tris}, overflow, sd, it, __builtin_inff(),
                                                     0xFFFFFFFFu, -1, __builtin_inff(), start | WIDE_CHAIN_MORE)
                     : pair ? walk_pair(g, top, o, d, last, LdsFlat{(CHR_LDS uint32_t *)stacks}, TAIL_STACK * 8,
@@ -5690,7 +5736,7 @@ __global__ __launch_bounds__(128) void walk_lone_timing_kernel(const DevGeom *__
 
 extern "C" int chr_walk_lone_timing(const chr_geometry *g, const float *d_rays, uint32_t n, uint32_t reps,
                                     uint32_t nwaves, int32_t walker, uint32_t *d_out, void *stream) {
-    if (!g || !d_rays || !d_out || nwaves == 0 || reps == 0 || walker < 0 || walker > 4)
+    if (!g || !d_rays || !d_out || nwaves == 0 || reps == 0 || walker < 0 || walker > 5)
         return chr::fail(CHR_ERR_INVALID, "chr_walk_lone_timing: bad argument");
     if (g->dev.nwnodes == 0) return chr::fail(CHR_ERR_INVALID, "chr_walk_lone_timing: geometry has no wide BVH");
     if (n == 0) return CHR_OK;
