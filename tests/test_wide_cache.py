@@ -18,13 +18,31 @@ def _full_and_compact(packed):
     return build_wide_bvh(packed), wide_bvh.build(packed)
 
 
+def _check_records(w, full, packed):
+    """The compact form's records (the upload's) against the full build's: every word
+    but the last (pad) equal; the upload's pad word is the record's leaf node
+    (walk_up's start, wide_bvh.h).  Returns the records."""
+    rec = w.records(packed)
+    words = rec.reshape(-1).view(np.uint32).reshape(-1, 16)
+    assert np.array_equal(words[:, :15], full.tris.view(np.uint8).reshape(-1).view(np.uint32).reshape(-1, 16)[:, :15])
+    nodes = w.nodes.view(np.uint8).reshape(-1, 96)
+    kinds, offs = nodes[:, 72:80].astype(np.int64), nodes[:, 80:88].astype(np.int64)
+    tri_base = nodes[:, 68:72].copy().view(np.uint32).reshape(-1).astype(np.int64)
+    leaf_of = np.full(len(words), -1, np.int64)
+    for k in range(8):
+        for t in range(4):
+            m = (kinds[:, k] >= 1) & (kinds[:, k] <= 4) & (t < kinds[:, k])
+            leaf_of[tri_base[m] + offs[m, k] + t] = np.flatnonzero(m)
+    assert np.all(leaf_of >= 0) and np.array_equal(words[:, 15], leaf_of)
+    return rec
+
+
 def test_compact_rebuilds_records(small_packed):
     full, w = _full_and_compact(small_packed)
     assert w.usable and len(w.nodes) == len(full.nodes) and len(w.rec_id) == len(full.tris)
     assert np.array_equal(w.nodes.view(np.uint8).reshape(-1), full.nodes.view(np.uint8).reshape(-1))
     assert np.array_equal(w.rec_id, full.tris['id']) and np.array_equal(w.rec_rank, full.tris['rank'])
-    rec = w.records(small_packed)
-    assert np.array_equal(rec.reshape(-1), full.tris.view(np.uint8).reshape(-1))
+    rec = _check_records(w, full, small_packed)
     # a sub-range, as the upload fills it chunk by chunk
     n = len(w.rec_id)
     part = w.records(small_packed, first=n // 3, n=n // 4)
@@ -38,7 +56,7 @@ def test_compact_physics_scene():
     from chroma.gpu.packing import PackedGeometry
     packed = PackedGeometry(loader.create_geometry_from_obj(scenes.physics_scene()))
     full, w = _full_and_compact(packed)
-    assert np.array_equal(w.records(packed).reshape(-1), full.tris.view(np.uint8).reshape(-1))
+    _check_records(w, full, packed)
 
 
 def _corrupt(w, **changes):
