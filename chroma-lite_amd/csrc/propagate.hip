@@ -1561,8 +1561,7 @@ struct PropagateArgs {
     uint32_t pair;                     // tail kernel: a lone walk takes an idle wave of its workgroup as
                                        // triangle tester (walk_pair; CHR_PAIR_WALK=0: walk_lone alone)
     uint32_t walk_up;                  // tail kernel: a walk with a previous hit starts at that hit's leaf
-                                       // and climbs (CHR_WALK_UP: 0 none, 1 lone and grouped, 2 lone only,
-                                       // 3 as 1 with the lone climb paired)
+                                       // and climbs (CHR_WALK_UP: 0 none, 1 lone and grouped, 2 lone only)
     uint32_t want;
     // tail kernel, work-queue mode (nullptr: group g runs queue positions g, g + cap, ...): a
     // zeroed counter the photon groups take queue positions from, for queues no longer than
@@ -2679,12 +2678,10 @@ __device__ __forceinline__ bool pair_wait(CHR_LDS uint32_t *box, uint32_t spin, 
 // The walker (whole wave, converged).  lists: this wave's 2 x TAIL_TRI words;
 // stk: cap entries of stack, the last 8 of them used as the refill's scratch.
 // The box must have been posted (ray, seed best, PB_LISTS) by this wave.
-// UP: the climb of walk_lone<true> from node `start`.
-template <bool UP, class M>
+template <class M>
 __device__ __forceinline__ int walk_pair_walker(const DevGeom &g, const TopNodes &top, V3 o, V3 d, M stk, int cap,
                                                 CHR_LDS uint32_t *lists, CHR_LDS uint32_t *box, uint32_t spin,
-                                                uint32_t &overflow, float &min_distance, uint32_t &iters, bool &lost,
-                                                uint32_t start) {
+                                                uint32_t &overflow, float &min_distance, uint32_t &iters, bool &lost) {
     constexpr uint32_t INVALID = 0xFFFFFFFFu;
     auto ufl = [](float x) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(x))); };
     auto uu = [](uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); };
@@ -2698,8 +2695,7 @@ __device__ __forceinline__ int walk_pair_walker(const DevGeom &g, const TopNodes
     const V3 noid = v3(-o.x / d.x, -o.y / d.y, -o.z / d.z);
     const V3 inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
     const RaySlab r = make_slab(o, noid, inv);
-    uint32_t cur = lane < 8u ? (UP ? start : 0u) : INVALID;
-    uint32_t chainw = INVALID;                        // UP: ancestor word k of the cursor's node (lane k)
+    uint32_t cur = lane < 8u ? 0u : INVALID;
     float cur_t = 0.0f;
     int sp = 0;
     uint32_t nl = 0;                                  // lists published
@@ -2712,10 +2708,6 @@ __device__ __forceinline__ int walk_pair_walker(const DevGeom &g, const TopNodes
     uint4 h, a1, a2, a3, a4;
     uint2 a5;
     auto fetch_node = [&](uint32_t node) {
-        if constexpr (UP) {
-            node &= WIDE_NODE_MASK;
-            chainw = gld(reinterpret_cast<const uint32_t *>(g.wnodes + (size_t)g.wstride * node) + 24 + k);
-        }
         if (node < top.n) {
             const CHR_LDS u32x4 *tp = top.p + 6u * node;
             h = u4(tp[0]); a1 = u4(tp[1]); a2 = u4(tp[2]); a3 = u4(tp[3]); a4 = u4(tp[4]);
@@ -2734,12 +2726,10 @@ __device__ __forceinline__ int walk_pair_walker(const DevGeom &g, const TopNodes
         bool inner = false, leafhit = false;
         float tk = 0.0f;
         uint32_t kind = 0, child = 0, first = 0;
-        const bool more = UP && cur != INVALID && (cur & WIDE_CHAIN_MORE) != 0u;
         if (cur != INVALID) {
             const V3 org = v3(__uint_as_float(h.x), __uint_as_float(h.y), __uint_as_float(h.z));
             const float sx = exp_scale(h.w), sy = exp_scale(h.w >> 8), sz = exp_scale(h.w >> 16);
             kind = byte8(a4.z, a4.w, k);
-            if (UP && (cur & WIDE_ANCESTOR) != 0u && ((cur >> 28) & 7u) == k) kind = 0u;   // the chain's child
             auto q = [k](uint32_t lo4, uint32_t hi4) { return (float)byte8(lo4, hi4, k); };
             const float tnx = __builtin_fmaf(__builtin_fmaf(q(r.negx ? a2.z : a1.x, r.negx ? a2.w : a1.y), sx, org.x), r.inx, r.onx);
             const float tfx = __builtin_fmaf(__builtin_fmaf(q(r.negx ? a1.x : a2.z, r.negx ? a1.y : a2.w), sx, org.x), r.inx, r.ofx);
@@ -2781,24 +2771,6 @@ __device__ __forceinline__ int walk_pair_walker(const DevGeom &g, const TopNodes
             sp = scap;
         } else {
             sp += npush;
-        }
-        if constexpr (UP) {   // a chain onto the stack (walk_lone<true>)
-            const bool cpush = more && chainw != WIDE_NO_PARENT;
-            const unsigned long long cm = __ballot(cpush);
-            if (cm) {
-                const int nc = __popcll(cm);
-                const int cpos = sp + nc - 1 - __popcll(cm & below);
-                if (cpush && cpos < scap) {
-                    stk[2 * cpos] = chainw;
-                    stk[2 * cpos + 1] = 0u;
-                }
-                if (sp + nc > scap) {
-                    if (lane == 0) overflow += (uint32_t)(sp + nc - scap);
-                    sp = scap;
-                } else {
-                    sp += nc;
-                }
-            }
         }
         cur = near;
         cur_t = __uint_as_float(key & ~7u);
@@ -2965,11 +2937,11 @@ __device__ __forceinline__ void walk_pair_tester(const DevGeom &g, CHR_LDS uint3
 // and the result is not the walk's (the caller walks the ray alone); the box
 // then stays aborted (never PS_IDLE again), so no walker of the workgroup claims
 // it while the abandoned tester may still use it.
-template <bool UP = false, class M>
+template <class M>
 __device__ __forceinline__ int walk_pair(const DevGeom &g, const TopNodes &top, V3 o, V3 d, uint32_t last, M stk,
                                          int cap, CHR_LDS uint32_t *lists, uint32_t lists_off, CHR_LDS uint32_t *box,
                                          uint32_t spin, uint32_t &overflow, float &min_distance, uint32_t &iters,
-                                         bool &lost, uint32_t start = 0u) {
+                                         bool &lost) {
     lds_st(box + PB_WSEQ, 0u);
     lds_st(box + PB_WDONE, 0xFFFFFFFFu);
     lds_st(box + PB_TREAD, 0u);
@@ -2989,8 +2961,7 @@ __device__ __forceinline__ int walk_pair(const DevGeom &g, const TopNodes &top, 
     lds_st(box + PB_LISTS, lists_off);
     lds_release();
     lds_st(box + PB_STATE, PS_REQ);
-    const int tri = walk_pair_walker<UP>(g, top, o, d, stk, cap, lists, box, spin, overflow, min_distance, iters, lost,
-                                         start);
+    const int tri = walk_pair_walker(g, top, o, d, stk, cap, lists, box, spin, overflow, min_distance, iters, lost);
     lds_release();
     if (lost) lds_st(box + PB_ABORT, 1u);
     else lds_st(box + PB_STATE, PS_IDLE);
@@ -3232,23 +3203,20 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_tail_kernel(const DevGe
             bool paired = false, lost = false;
             // one walker with a previous hit: walk_up from that hit's leaf (ahead of pairing)
             const bool up = Gs == 64 && a.walk_up && start != 0xFFFFFFFFu;
-            if (Gs == 64 && (!up || a.walk_up == 3u) && a.pair && lds_ld(box + PB_IDLE) != 0u &&
-                lds_ld(box + PB_STATE) == PS_IDLE && lds_ld(box + PB_ABORT) == 0u) {
+            if (Gs == 64 && !up && a.pair && lds_ld(box + PB_IDLE) != 0u && lds_ld(box + PB_STATE) == PS_IDLE &&
+                lds_ld(box + PB_ABORT) == 0u) {
                 uint32_t old = PS_TAKEN;
                 if (lane == 0) old = atomicCAS(&box_s[PB_STATE], PS_IDLE, PS_POSTING);
                 paired = (uint32_t)__builtin_amdgcn_readfirstlane((int)old) == PS_IDLE;
             }
-            const uint32_t ustart = (start & WIDE_NODE_MASK) | WIDE_CHAIN_MORE;
-            int st = paired && up ? walk_pair<true>(g, top, o, dd, last, LdsFlat{wstack}, TAIL_STACK * 8, wtris,
-                                                    (threadIdx.x >> 6) * 2u * TAIL_TRI, box, PAIR_SPIN_MAX, overflow, sd,
-                                                    it, lost, ustart)
-                     : up ? walk_lone<true>(g, o, dd, last, LdsFlat{wstack}, TAIL_STACK * 8, LdsFlat{wtris}, overflow, sd,
-                                          it, __builtin_inff(), 0xFFFFFFFFu, -1, __builtin_inff(), ustart)
+            int st = up ? walk_lone<true>(g, o, dd, last, LdsFlat{wstack}, TAIL_STACK * 8, LdsFlat{wtris}, overflow, sd,
+                                          it, __builtin_inff(), 0xFFFFFFFFu, -1, __builtin_inff(),
+                                          (start & WIDE_NODE_MASK) | WIDE_CHAIN_MORE)
                      : paired ? walk_pair(g, top, o, dd, last, LdsFlat{wstack}, TAIL_STACK * 8, wtris,
                                         (threadIdx.x >> 6) * 2u * TAIL_TRI, box, PAIR_SPIN_MAX, overflow, sd, it, lost)
                      : Gs == 64
                          ? walk_lone(g, o, dd, last, LdsFlat{wstack}, TAIL_STACK * 8, LdsFlat{wtris}, overflow, sd, it)
-                     : (a.walk_up == 1u || a.walk_up == 3u)   // grouped walks climb from their previous hit's leaf too
+                     : a.walk_up == 1u   // grouped walks climb from their previous hit's leaf too
                          ? walk_segment<0, LdsFlat, true>(g, act, o, dd, last, Gs,
                                                           LdsFlat{wstack + seg0 / 8 * TAIL_STACK * 2}, TAIL_STACK * Gs / 8,
                                                           LdsFlat{wtris + 4 * seg0}, top, overflow, sd, it,
@@ -4482,11 +4450,10 @@ static bool pair_walk_enabled() {
 }
 // CHR_WALK_UP=0: the tail's walks from the root (A/B; default 1: a walk with a
 // previous hit climbs from that hit's leaf -- walk_lone<true> ahead of the pair walk,
-// and the grouped walks, walk_segment<0, UP>; 2: the lone walks only; 3: as 1, the
-// lone climb paired with an idle tester wave when there is one, walk_pair<true>)
+// and the grouped walks, walk_segment<0, UP>; 2: the lone walks only)
 static uint32_t walk_up_mode() {
     const char *e = getenv("CHR_WALK_UP");
-    return e && (e[0] == '0' || e[0] == '2' || e[0] == '3') ? (uint32_t)(e[0] - '0') : 1u;
+    return e && (e[0] == '0' || e[0] == '2') ? (uint32_t)(e[0] - '0') : 1u;
 }
 
 static int slot_timing() {
@@ -5688,7 +5655,7 @@ namespace chr {
 // (ray r: node (r * 2654435761) mod nodes -- any start covers the tree once);
 // walker 4: walk_up from the leaf node of a given record (8-word rays: + record);
 // walker 5: the grouped walk's climb (walk_segment<0, UP>, one 64-lane segment) from
-// walker 3's start; walker 6: the paired climb (walk_pair<true>) from walker 3's start
+// walker 3's start
 __global__ __launch_bounds__(128) void walk_lone_timing_kernel(const DevGeom *__restrict__ gdev, const float *rays,
                                                                uint32_t n, uint32_t reps, uint32_t *out,
                                                                int32_t walker) {
@@ -5705,7 +5672,7 @@ __global__ __launch_bounds__(128) void walk_lone_timing_kernel(const DevGeom *__
     }
     __syncthreads();
     if (threadIdx.x >= 64) {   // the tester wave (walkers 1, 2), else idle
-        if (walker == 0 || (walker >= 3 && walker != 6)) return;
+        if (walker == 0 || walker >= 3) return;
         while (true) {
             uint32_t st = PS_IDLE;
             for (uint32_t i = 0; i < PAIR_SPIN_MAX * 8u; ++i) {
@@ -5732,12 +5699,8 @@ __global__ __launch_bounds__(128) void walk_lone_timing_kernel(const DevGeom *__
             uint32_t it = 0;
             const unsigned long long t0 = __builtin_amdgcn_s_memrealtime(), c0 = __builtin_amdgcn_s_memtime();
             bool lost = false;
-            const bool pair = (walker == 1 || walker == 2 || walker == 6) && lds_ld(box + PB_ABORT) == 0u;
-            int tri = walker == 6 && pair
-                          ? walk_pair<true>(g, top, o, d, last, LdsFlat{(CHR_LDS uint32_t *)stacks}, TAIL_STACK * 8,
-                                            (CHR_LDS uint32_t *)tris, 0u, box, PAIR_SPIN_MAX, overflow, sd, it, lost,
-                                            start | WIDE_CHAIN_MORE)
-                    : walker == 5 ? walk_segment<0, LdsFlat, true>(g, true, o, d, last, 64,
+            const bool pair = (walker == 1 || walker == 2) && lds_ld(box + PB_ABORT) == 0u;
+            int tri = walker == 5 ? walk_segment<0, LdsFlat, true>(g, true, o, d, last, 64,
                                                                LdsFlat{(CHR_LDS uint32_t *)stacks}, TAIL_STACK * 8,
                                                                LdsFlat{(CHR_LDS uint32_t *)tris}, top, overflow, sd, it,
                                                                __builtin_inff(), 0xFFFFFFFFu, -1, __builtin_inff(),
@@ -5763,7 +5726,7 @@ __global__ __launch_bounds__(128) void walk_lone_timing_kernel(const DevGeom *__
             }
         }
     }
-    if (walker == 1 || walker == 2 || walker == 6) {
+    if (walker == 1 || walker == 2) {
         lds_release();
         lds_st(box + PB_STATE, PS_EXIT);
     }
@@ -5773,7 +5736,7 @@ __global__ __launch_bounds__(128) void walk_lone_timing_kernel(const DevGeom *__
 
 extern "C" int chr_walk_lone_timing(const chr_geometry *g, const float *d_rays, uint32_t n, uint32_t reps,
                                     uint32_t nwaves, int32_t walker, uint32_t *d_out, void *stream) {
-    if (!g || !d_rays || !d_out || nwaves == 0 || reps == 0 || walker < 0 || walker > 6)
+    if (!g || !d_rays || !d_out || nwaves == 0 || reps == 0 || walker < 0 || walker > 5)
         return chr::fail(CHR_ERR_INVALID, "chr_walk_lone_timing: bad argument");
     if (g->dev.nwnodes == 0) return chr::fail(CHR_ERR_INVALID, "chr_walk_lone_timing: geometry has no wide BVH");
     if (n == 0) return CHR_OK;
