@@ -3715,19 +3715,12 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(const DevGeom *__res
             CHR_LDS uint32_t *wbase = (CHR_LDS uint32_t *)(lds + (threadIdx.x & ~63u));
             float sdist;
             uint32_t sit;
-            // a walk with a hit so far climbs from that hit's leaf (walk_lone<true>, §13.2):
-            // what is left is to find anything nearer than it, which is close to it
-            const uint32_t sstart = sid >= 0 ? (gld(reinterpret_cast<const uint32_t *>(g.wtri + 4 * (size_t)sid) + 15) &
-                                                WIDE_NODE_MASK) | WIDE_CHAIN_MORE
-                                             : 0u;
             const int tri = w == 1
-                                ? walk_lone<true>(g, so, sdir, slast, LdsRowsT<TB>{wbase, 0}, DSTK * 8,
-                                                  LdsRowsT<TB>{wbase, 8 * DSTK * 2}, overflow, sdist, sit, sbest, srank,
-                                                  sid, sbd, sstart)
-                                : walk_segment<0, LdsRowsT<TB>, true>(g, act, so, sdir, slast, Gs,
-                                                                      LdsRowsT<TB>{wbase, seg0 / 8 * DSTK * 2}, DSTK * Gs / 8,
-                                                                      LdsRowsT<TB>{wbase, 8 * DSTK * 2 + 4 * seg0}, top,
-                                                                      overflow, sdist, sit, sbest, srank, sid, sbd, sstart);
+                                ? walk_lone(g, so, sdir, slast, LdsRowsT<TB>{wbase, 0}, DSTK * 8,
+                                            LdsRowsT<TB>{wbase, 8 * DSTK * 2}, overflow, sdist, sit, sbest, srank, sid, sbd)
+                                : walk_segment<0>(g, act, so, sdir, slast, Gs, LdsRowsT<TB>{wbase, seg0 / 8 * DSTK * 2},
+                                                  DSTK * Gs / 8, LdsRowsT<TB>{wbase, 8 * DSTK * 2 + 4 * seg0}, top,
+                                                  overflow, sdist, sit, sbest, srank, sid, sbd);
             const int mine = (__popcll(rm & ((1ull << lane) - 1ull)) * Gs) & 63;   // my segment's first lane
             const int rt = __shfl(tri, mine);
             const float rd = __shfl(sdist, mine);
