@@ -4210,14 +4210,6 @@ static size_t sort_temp_bytes16(uint32_t n, int bits = 24) {
 // first launch 5.01 ms with r01-r03's 8+8-bit row-major cells, 4.63 with 11+11-bit
 // Morton cells, 4.55 with Hilbert order (490.3 -> 500.3 M/s); photons identical.
 constexpr int BIN_KEY_BITS = 22;
-// CHR_BIN_SORT_LOW=b (A/B): the sort orders by key bits [b, 22) only -- the Hilbert
-// index's top bits are its coarser levels' cells, so b = 6 orders by 8+8-bit cells in
-// two radix passes instead of three (a stable sort keeps input order inside a cell)
-static int bin_sort_low_bit() {
-    const char *e = getenv("CHR_BIN_SORT_LOW");
-    const int b = e ? atoi(e) : 0;
-    return b < 0 ? 0 : (b > 14 ? 14 : b);
-}
 // u32 words: [0..15] counters | masks (2 per 64 slots) | offsets (1 per 64) |
 // block prefixes (1 per 256 words, +2)
 static uint64_t mask_scan_words(uint64_t n) {   // masks + offsets + block prefixes for n positions
@@ -4625,8 +4617,8 @@ static int launch_step(const chr_geometry *g, const chr_photons *ph, uint32_t *r
                                        n, keys, order);
                 void *temp = (void *)(((uintptr_t)(vals_out + n) + 255) & ~(uintptr_t)255);
                 size_t temp_bytes = sort_temp_bytes16(n, BIN_KEY_BITS);
-                CHR_HIP_CHECK(rocprim::radix_sort_pairs(temp, temp_bytes, keys, keys_out, order, vals_out, n,
-                                                        bin_sort_low_bit(), BIN_KEY_BITS, stream));
+                CHR_HIP_CHECK(rocprim::radix_sort_pairs(temp, temp_bytes, keys, keys_out, order, vals_out, n, 0,
+                                                        BIN_KEY_BITS, stream));
                 if (use_rays)   // the records in the binned walk order
                     hipLaunchKernelGGL(permute_rays_kernel, dim3(grid_for(n)), dim3(BLOCK), 0, stream, fc->rays,
                                        vals_out, n, fc->rays_walk);
