@@ -1561,7 +1561,8 @@ struct PropagateArgs {
     uint32_t pair;                     // tail kernel: a lone walk takes an idle wave of its workgroup as
                                        // triangle tester (walk_pair; CHR_PAIR_WALK=0: walk_lone alone)
     uint32_t walk_up;                  // tail kernel: a walk with a previous hit starts at that hit's leaf
-                                       // and climbs (CHR_WALK_UP: 0 none, 1 lone and grouped, 2 lone only)
+                                       // and climbs (CHR_WALK_UP: 0 none, 1 lone and grouped, 2 lone only,
+                                       // 4 as 1 without the chain prefetch)
     uint32_t want;
     // tail kernel, work-queue mode (nullptr: group g runs queue positions g, g + cap, ...): a
     // zeroed counter the photon groups take queue positions from, for queues no longer than
@@ -2372,7 +2373,9 @@ template <bool UP = false, class M>
 __device__ __forceinline__ int walk_lone(const DevGeom &g, V3 o, V3 d, uint32_t last, M stk, int cap, M tlist,
                                          uint32_t &overflow, float &min_distance, uint32_t &iters,
                                          float best = __builtin_inff(), uint32_t best_rank = 0xFFFFFFFFu,
-                                         int best_id = -1, float best_bd = __builtin_inff(), uint32_t start = 0u) {
+                                         int best_id = -1, float best_bd = __builtin_inff(), uint32_t start = 0u,
+                                         bool have_pre = false, uint32_t pre_cur = 0xFFFFFFFFu,
+                                         uint32_t pre_push = 0xFFFFFFFFu) {
     constexpr uint32_t INVALID = 0xFFFFFFFFu;
     auto ufl = [](float x) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(x))); };
     auto uu = [](uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); };
@@ -2392,9 +2395,19 @@ __device__ __forceinline__ int walk_lone(const DevGeom &g, V3 o, V3 d, uint32_t 
     const V3 inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
     const RaySlab r = make_slab(o, noid, inv);
     uint32_t cur = lane < 8u ? (UP ? start : 0u) : INVALID;   // cursor 0 starts at the root (UP: at start)
+    // UP with start's chain already read (have_pre, the tail's prefetch): cursor c > 0
+    // starts at the ancestor word pre_cur (start's c-th ancestor, lane-wise; INVALID:
+    // none), the 8th (pre_push) goes on the stack, and start pushes no chain of its own
+    const bool pre = UP && have_pre;
+    if (pre) cur = lane < 8u ? (start & ~WIDE_CHAIN_MORE) : pre_cur;
     uint32_t chainw = INVALID;                        // UP: ancestor word k of the cursor's node (lane k)
     float cur_t = 0.0f;
     int sp = 0;
+    if (pre && (pre_push & WIDE_ANCESTOR) != 0u) {   // the 8th ancestor (a valid word), entry distance 0
+        if (lane == 0) { stk[0] = pre_push; stk[1] = 0u; }
+        __builtin_amdgcn_wave_barrier();
+        sp = 1;
+    }
     uint32_t Tp = 0;                                  // triangles in flight (listed by the last expansion)
     int pb = 0;                                       // the list buffer they were read from
     iters = 0;
@@ -3080,6 +3093,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_tail_kernel(const DevGe
     State s;
     int steps = 0, scatter_first = 0;
     uint32_t up_node = 0xFFFFFFFFu;   // the leaf node of the photon's last hit record (walk_up's start)
+    uint32_t up_chain = 0xFFFFFFFFu;  // ancestor word `sub` of that node (read during the step's physics)
     uint32_t q = wq ? next_q() : slot, pid = 0, iters = 0, paired_steps = 0;
     bool live = false, exhausted = wq ? q >= n : slot >= nslot;
     unsigned long long t0 = 0, walk_ticks = 0;
@@ -3145,6 +3159,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_tail_kernel(const DevGe
                 iters = 0;
                 paired_steps = 0;
                 up_node = 0xFFFFFFFFu;
+                up_chain = 0xFFFFFFFFu;
                 walk_ticks = 0;
                 scatter_first = a.scatter_first;
                 live = true;
@@ -3181,7 +3196,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_tail_kernel(const DevGe
             const int src = m != 0 ? __ffsll((long long)m) - 1 : (int)(lane & ~7u);
             const bool act = m != 0;
             V3 o, dd;
-            uint32_t last, start = 0xFFFFFFFFu;
+            uint32_t last, start = 0xFFFFFFFFu, pre_cur = 0xFFFFFFFFu, pre_push = 0xFFFFFFFFu;
             if (w == 1) {   // one walker: its lane is wave-uniform, scalar reads instead of LDS shuffles
                 const int s1 = __ffsll((long long)wm) - 1;
                 auto rl = [s1](float x) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), s1)); };
@@ -3189,6 +3204,10 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_tail_kernel(const DevGe
                 dd = v3(rl(p.dir.x), rl(p.dir.y), rl(p.dir.z));
                 last = (uint32_t)__builtin_amdgcn_readlane(p.last_hit, s1);
                 start = (uint32_t)__builtin_amdgcn_readlane((int)up_node, s1);
+                // cursor c > 0 of the climb starts at the start node's c-th ancestor
+                const int g0 = s1 & ~7, c = (int)(lane >> 3);
+                pre_cur = (uint32_t)__shfl((int)up_chain, g0 + (c > 0 ? c - 1 : 0));
+                pre_push = (uint32_t)__builtin_amdgcn_readlane((int)up_chain, g0 + 7);
             } else {
                 o = v3(__shfl(p.pos.x, src), __shfl(p.pos.y, src), __shfl(p.pos.z, src));
                 dd = v3(__shfl(p.dir.x, src), __shfl(p.dir.y, src), __shfl(p.dir.z, src));
@@ -3211,12 +3230,12 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_tail_kernel(const DevGe
             }
             int st = up ? walk_lone<true>(g, o, dd, last, LdsFlat{wstack}, TAIL_STACK * 8, LdsFlat{wtris}, overflow, sd,
                                           it, __builtin_inff(), 0xFFFFFFFFu, -1, __builtin_inff(),
-                                          (start & WIDE_NODE_MASK) | WIDE_CHAIN_MORE)
+                                          (start & WIDE_NODE_MASK) | WIDE_CHAIN_MORE, a.walk_up != 4u, pre_cur, pre_push)
                      : paired ? walk_pair(g, top, o, dd, last, LdsFlat{wstack}, TAIL_STACK * 8, wtris,
                                         (threadIdx.x >> 6) * 2u * TAIL_TRI, box, PAIR_SPIN_MAX, overflow, sd, it, lost)
                      : Gs == 64
                          ? walk_lone(g, o, dd, last, LdsFlat{wstack}, TAIL_STACK * 8, LdsFlat{wtris}, overflow, sd, it)
-                     : a.walk_up == 1u   // grouped walks climb from their previous hit's leaf too
+                     : (a.walk_up == 1u || a.walk_up == 4u)   // grouped walks climb from their previous hit's leaf too
                          ? walk_segment<0, LdsFlat, true>(g, act, o, dd, last, Gs,
                                                           LdsFlat{wstack + seg0 / 8 * TAIL_STACK * 2}, TAIL_STACK * Gs / 8,
                                                           LdsFlat{wtris + 4 * seg0}, top, overflow, sd, it,
@@ -3259,6 +3278,12 @@ __global__ __launch_bounds__(BLOCK, MINW) void propagate_tail_kernel(const DevGe
             wt.begin(2u, sub == 0 ? pid : 0xFFFFFFFFu, a.pos, q, slot, p.pos, p.dir, p.last_hit);
             finish_fill<true, WIRES>(g, s, p, tri);
             wt.filled(tri, s);
+            // the next walk's start node's ancestor chain (walk_lone<true>'s prefetch), in
+            // flight during the rest of the physics: one dependent iteration less
+            up_chain = up_node != 0xFFFFFFFFu
+                           ? gld(reinterpret_cast<const uint32_t *>(g.wnodes + (size_t)g.wstride * (up_node & WIDE_NODE_MASK)) +
+                                 24 + sub)
+                           : 0xFFFFFFFFu;
             lpf.mark(LP_FILL);
             bool stop = p.last_hit == -1;
             if (!stop) {
@@ -4450,10 +4475,12 @@ static bool pair_walk_enabled() {
 }
 // CHR_WALK_UP=0: the tail's walks from the root (A/B; default 1: a walk with a
 // previous hit climbs from that hit's leaf -- walk_lone<true> ahead of the pair walk,
-// and the grouped walks, walk_segment<0, UP>; 2: the lone walks only)
+// and the grouped walks, walk_segment<0, UP>, the lone walk's first iteration taking the
+// start node's ancestors read during the previous step; 2: the lone walks only; 4: as 1
+// without that prefetch -- A/B)
 static uint32_t walk_up_mode() {
     const char *e = getenv("CHR_WALK_UP");
-    return e && (e[0] == '0' || e[0] == '2') ? (uint32_t)(e[0] - '0') : 1u;
+    return e && (e[0] == '0' || e[0] == '2' || e[0] == '4') ? (uint32_t)(e[0] - '0') : 1u;
 }
 
 static int slot_timing() {
@@ -5655,7 +5682,8 @@ namespace chr {
 // (ray r: node (r * 2654435761) mod nodes -- any start covers the tree once);
 // walker 4: walk_up from the leaf node of a given record (8-word rays: + record);
 // walker 5: the grouped walk's climb (walk_segment<0, UP>, one 64-lane segment) from
-// walker 3's start
+// walker 3's start; walker 7: walker 3 with the start node's chain read beforehand (the
+// tail's prefetch)
 __global__ __launch_bounds__(128) void walk_lone_timing_kernel(const DevGeom *__restrict__ gdev, const float *rays,
                                                                uint32_t n, uint32_t reps, uint32_t *out,
                                                                int32_t walker) {
@@ -5700,7 +5728,17 @@ __global__ __launch_bounds__(128) void walk_lone_timing_kernel(const DevGeom *__
             const unsigned long long t0 = __builtin_amdgcn_s_memrealtime(), c0 = __builtin_amdgcn_s_memtime();
             bool lost = false;
             const bool pair = (walker == 1 || walker == 2) && lds_ld(box + PB_ABORT) == 0u;
-            int tri = walker == 5 ? walk_segment<0, LdsFlat, true>(g, true, o, d, last, 64,
+            uint32_t pc = 0xFFFFFFFFu, pp = 0xFFFFFFFFu;
+            if (walker == 7) {
+                const uint32_t *cw = reinterpret_cast<const uint32_t *>(g.wnodes + (size_t)g.wstride * start) + 24;
+                const int c = (int)((threadIdx.x & 63u) >> 3);
+                pc = c > 0 ? gld(cw + (c - 1)) : 0xFFFFFFFFu;
+                pp = gld(cw + 7);
+            }
+            int tri = walker == 7 ? walk_lone<true>(g, o, d, last, LdsFlat{(CHR_LDS uint32_t *)stacks}, TAIL_STACK * 8,
+                                                    LdsFlat{(CHR_LDS uint32_t *)tris}, overflow, sd, it, __builtin_inff(),
+                                                    0xFFFFFFFFu, -1, __builtin_inff(), start | WIDE_CHAIN_MORE, true, pc, pp)
+                    : walker == 5 ? walk_segment<0, LdsFlat, true>(g, true, o, d, last, 64,
                                                                LdsFlat{(CHR_LDS uint32_t *)stacks}, TAIL_STACK * 8,
                                                                LdsFlat{(CHR_LDS uint32_t *)tris}, top, overflow, sd, it,
                                                                __builtin_inff(), 0xFFFFFFFFu, -1, __builtin_inff(),
@@ -5736,7 +5774,7 @@ __global__ __launch_bounds__(128) void walk_lone_timing_kernel(const DevGeom *__
 
 extern "C" int chr_walk_lone_timing(const chr_geometry *g, const float *d_rays, uint32_t n, uint32_t reps,
                                     uint32_t nwaves, int32_t walker, uint32_t *d_out, void *stream) {
-    if (!g || !d_rays || !d_out || nwaves == 0 || reps == 0 || walker < 0 || walker > 5)
+    if (!g || !d_rays || !d_out || nwaves == 0 || reps == 0 || walker < 0 || walker > 7 || walker == 6)
         return chr::fail(CHR_ERR_INVALID, "chr_walk_lone_timing: bad argument");
     if (g->dev.nwnodes == 0) return chr::fail(CHR_ERR_INVALID, "chr_walk_lone_timing: geometry has no wide BVH");
     if (n == 0) return CHR_OK;

@@ -219,7 +219,8 @@ int chr_kernel_info(int32_t which, chr_kernel_attr *out);
  * lost handshake adds 1 << 20 to the last word; 3 = walk_up from an arbitrary
  * node (ray r: (r * 2654435761) mod nodes), 4 = walk_up from the leaf node of a
  * given record (d_rays then n x 8 words: + the record index), 5 = the grouped
- * walk's climb (one 64-lane segment) from walker 3's start.  nwaves workgroups; workgroup
+ * walk's climb (one 64-lane segment) from walker 3's start, 7 = walker 3 with the
+ * start node's ancestors read beforehand (the tail's prefetch).  nwaves workgroups; workgroup
  * w walks rays w, w + nwaves, ... each reps times in a row.  d_rays: n x 7 floats
  * (origin, direction, last hit triangle id as int bits); d_out: n x reps x 4 words
  * (record index or -1, iterations, 100 MHz ticks, shader-clock cycles of the walk)

@@ -228,13 +228,13 @@ def test_batches_slot_timing_modes_identical(cuda, small_detector, monkeypatch):
 #   CHR_PROPAGATE_VARIANT   2/4 fused step kernels, 7/8 binning every / no step, 1 the
 #                           exact-order walk of the reference BVH, 5 the counting form
 #   CHR_PAIR_WALK=0         the tail's lone walks without a tester wave (walk_lone)
-#   CHR_WALK_UP=0 / 2       the tail's walks from the root / only its lone walks climbing
+#   CHR_WALK_UP=0 / 2 / 4   the tail's walks from the root / only its lone walks climbing / no chain prefetch
 #   CHR_SLOT_TIMING         test_batches_slot_timing_modes_identical
 #   CHR_WIDE_LEAF_MAX / CHR_EXACT_ORDER_ONLY: test_geometry_build_switches_identical
 SWITCHES = [('CHR_HOST_STEPS', '1'), ('CHR_STEP_LAUNCH', '0'), ('CHR_TRACE_STEPS', '1'),
             ('CHR_PROPAGATE_VARIANT', '2'), ('CHR_PROPAGATE_VARIANT', '4'), ('CHR_PROPAGATE_VARIANT', '7'),
             ('CHR_PROPAGATE_VARIANT', '8'), ('CHR_PROPAGATE_VARIANT', '1'), ('CHR_PROPAGATE_VARIANT', '5'),
-            ('CHR_PAIR_WALK', '0'), ('CHR_WALK_UP', '0'), ('CHR_WALK_UP', '2')]
+            ('CHR_PAIR_WALK', '0'), ('CHR_WALK_UP', '0'), ('CHR_WALK_UP', '2'), ('CHR_WALK_UP', '4')]
 
 
 @pytest.mark.parametrize('switch,value', SWITCHES)

@@ -108,8 +108,9 @@ def test_walk_up_equals_lone(cuda, small_detector, small_packed):
     lone, ov0 = _walk(det, rays, 0, 64)
     up, ov3 = _walk(det, rays, 3, 64)
     seg, ov5 = _walk(det, rays, 5, 64)
-    assert ov0 == 0 and ov3 == 0 and ov5 == 0
-    assert np.array_equal(lone, up) and np.array_equal(lone, seg)
+    pre, ov7 = _walk(det, rays, 7, 64)
+    assert ov0 == 0 and ov3 == 0 and ov5 == 0 and ov7 == 0
+    assert np.array_equal(lone, up) and np.array_equal(lone, seg) and np.array_equal(lone, pre)
     # from the previous hit's leaf, that hit excluded
     rec_id = np.asarray(wide_bvh.build(small_packed).rec_id)
     first, _ = _walk(det, rays, 0, 64, reps=1)
