@@ -619,9 +619,22 @@ class PropagateWorkload(object):
     def run_sequential(self, m):
         return self.run(m, pipeline=False)
 
+    def at_max_steps(self, nbatches):
+        """Photons of each of the last call's batches that ran out of steps: their
+        history holds none of the terminal bits (NO_HIT, BULK_ABSORB, SURFACE_DETECT,
+        SURFACE_ABSORB, NAN_ABORT; propagate.cu:282-340 stops them alive at max_steps).
+        Counted on the device from the output flags, after the timed region; None when
+        the stats span more batches than the pool holds."""
+        pool = getattr(self, 'pool', [])
+        if nbatches == 0 or nbatches > len(pool):
+            return [None] * nbatches
+        dead = 0x1 | 0x2 | 0x4 | 0x8 | 0x8000
+        return [int(((gp.flags.tensor & dead) == 0).sum().item()) for gp in pool[:nbatches]]
+
     def rank_report(self, stats):
         """This rank's own numbers from the timed steps' stats."""
         launch_ms = [float(s.trace_launch_ms[i]) for s in stats for i in range(s.trace_ms_n)]
+        at_max = self.at_max_steps(len(stats))
         gp = self.reduced.get('gp')
         return {'rank': self.rank, 'photons_per_step': self.nphotons,
                 'device': self.torch.cuda.get_device_properties(self.local).name, 'local_rank': self.local,
@@ -639,7 +652,7 @@ class PropagateWorkload(object):
                 else 0,
                 'setup': dict(self.setup, **host_memory()),
                 'tail': [{'ms': round(s.tail_ms, 3), 'photons': int(s.tail_photons),
-                          'max_steps': int(s.tail_max_steps),
+                          'max_steps': int(s.tail_max_steps), 'photons_at_max_steps': at_max[i],
                           'slowest_photon_ms': round(s.tail_max_cycles / 1e5, 3),
                           'slowest_photon_steps': int(s.tail_slowest_steps),
                           'long_photons': int(s.tail_long_photons),
@@ -649,7 +662,7 @@ class PropagateWorkload(object):
                           'long_walk_iterations_per_step': round(s.tail_long_walk_iterations /
                                                                  max(1, s.tail_long_steps), 2),
                           'long_paired_step_fraction': round(s.tail_long_paired_steps / max(1, s.tail_long_steps), 3)}
-                         for s in stats]}
+                         for i, s in enumerate(stats)]}
 
     def untimed_passes(self):
         """After timing: the counting variant (own-layout bytes, SIMD efficiency)
