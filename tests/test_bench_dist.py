@@ -259,3 +259,23 @@ def test_bench_float_parity_rule():
     assert r['violations'] == 1 and r['worst']['index'] == 4 and r['worst']['last_hit_oracle'] == 4
     r = bench.float_contract(t, t, 't', [5, 5], gf, hf, gl, hl)
     assert r == {'violations': 0, 'differing': 0, 'max_abs': 0.0}
+
+
+def test_bench_photons_at_max_steps():
+    """detail.tail_launch[i].photons_at_max_steps: photons of each
+    batch whose history holds no terminal bit (NO_HIT, BULK_ABSORB, SURFACE_DETECT,
+    SURFACE_ABSORB, NAN_ABORT) -- the ones propagate.cu's loop left alive at max_steps;
+    scattering / reflection bits and the upper 16 bits do not count as terminal."""
+    sys.path.insert(0, ROOT)
+    import types
+    import bench
+    wl = object.__new__(bench.PropagateWorkload)
+
+    def batch(flags):
+        t = torch.tensor(np.asarray(flags, np.uint32).view(np.int32))
+        return types.SimpleNamespace(flags=types.SimpleNamespace(tensor=t))
+    wl.pool = [batch([0x10, 0x2, 0x4 | 0x10, 0x20, 0x10000]), batch([0x1, 0x8, 0x8000, 0x4]), batch([])]
+    assert wl.at_max_steps(2) == [3, 0]
+    assert wl.at_max_steps(3) == [3, 0, 0]
+    assert wl.at_max_steps(4) == [None] * 4       # more batches than the pool holds
+    assert wl.at_max_steps(0) == []
