@@ -52,10 +52,20 @@ def main():
         for k in ('SQ_WAIT_ANY', 'SQ_WAIT_INST_ANY', 'SQ_ACTIVE_INST_ANY', 'SQ_ACTIVE_INST_VALU'):
             if k in c:
                 o[k.lower() + '_frac'] = round(c[k] / wc, 3)
-        for k in ('SQ_INSTS_VALU', 'SQ_INSTS_VMEM_RD', 'SQ_INSTS_SALU'):
+        for k in ('SQ_INSTS_VALU', 'SQ_INSTS_VMEM_RD', 'SQ_INSTS_SALU', 'SQ_INSTS_LDS', 'SQ_INSTS_SMEM'):
             if k in c:
                 o[k.lower() + '_per_dispatch'] = round(c[k] / counts[cls])
                 o[k.lower() + '_per_wave_quadcycle'] = round(c[k] / wc, 4)
+        # the second pass's LDS counters: issue cycles and stalls as fractions of the wave
+        # cycles, bank-conflict cycles against all LDS-array cycles
+        for k in ('SQ_ACTIVE_INST_LDS', 'SQ_WAIT_INST_LDS'):
+            if k in c:
+                o[k.lower() + '_frac'] = round(c[k] / wc, 4)
+        if c.get('SQ_LDS_IDX_ACTIVE'):
+            o['sq_lds_bank_conflict_per_lds_cycle'] = round(c.get('SQ_LDS_BANK_CONFLICT', 0.0) / c['SQ_LDS_IDX_ACTIVE'], 4)
+        for k in ('SQ_THREAD_CYCLES_VALU', 'SQ_LDS_IDX_ACTIVE', 'SQ_LDS_BANK_CONFLICT'):
+            if k in c:
+                o[k.lower() + '_per_dispatch'] = round(c[k] / counts[cls])
         o['wave_quadcycles_per_dispatch'] = round(wc / counts[cls])
         out[cls] = o
     print(json.dumps(out, indent=1))
